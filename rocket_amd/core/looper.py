@@ -1,0 +1,139 @@
+"""Iteration loop over the children of one stage (train or eval).
+
+Parity (reference ``rocket/core/loop.py``):
+
+* ``Looper(capsules, tag, grad_enabled, repeats, run_every, statefull, priority)``
+  (``:70-89``), ``repeats=0`` ≡ ``None``; nested loopers rejected (``:265-292``);
+* ``set/reset/launch`` only run when ``epoch_idx % run_every == 0`` (``:91-113``);
+* ``set`` runs the children first, then infers ``repeats`` = Σ ``_total`` of the
+  direct ``Dataset`` children (``:294-323``) and creates ``attrs.looper``
+  ``{repeats, state, terminate, tag}`` (``:115-158``);
+* each iteration clears ``attrs.batch``, dispatches the children under
+  ``torch.set_grad_enabled(grad_enabled)`` and stops on ``looper.terminate``
+  (``:182-229``); ``reset`` deletes ``attrs.looper`` (``:160-180``);
+* state ``{iter_idx}`` (kept as in the reference, Q3).
+
+Differences: the progress-bar postfix (loss/lr values are device scalars here,
+see :mod:`rocket_amd.utils.lazy`) is refreshed at most every ``postfix_interval``
+seconds so the host never waits on the device once per step; a resumed epoch
+whose datasets are already exhausted is skipped instead of raising (Q4).
+"""
+
+from __future__ import annotations
+
+import time
+
+import torch
+
+from rocket_amd.core.attributes import Attributes
+from rocket_amd.core.capsule import Capsule
+from rocket_amd.core.dispatcher import Dispatcher
+from rocket_amd.utils.lazy import materialize
+
+
+def _green(s: str) -> str:
+    return f"\x1b[32m{s}\x1b[0m"
+
+
+class Looper(Dispatcher):
+    def __init__(
+        self,
+        capsules: list[Capsule],
+        tag: str = "Looper",
+        grad_enabled: bool = True,
+        repeats: int | None = None,
+        run_every: int = 1,
+        statefull: bool = True,
+        priority: int = 1000,
+        progress: bool = True,
+        postfix_interval: float = 0.5,
+    ) -> None:
+        super().__init__(capsules=capsules, priority=priority)
+        self._statefull = statefull
+        self._repeats = None
+        self._user_defined_repeats = repeats or None
+        self._grad_enabled = grad_enabled
+        self._run_every = max(1, int(run_every))
+        self._iter_idx = 0
+        self._tag = tag
+        self._progress = progress
+        self._postfix_interval = postfix_interval
+
+    def _active(self, attrs: Attributes | None) -> bool:
+        epoch = attrs.launcher.epoch_idx if attrs is not None and attrs.launcher is not None else 0
+        return (epoch or 0) % self._run_every == 0
+
+    def set(self, attrs: Attributes | None = None) -> None:
+        if not self._active(attrs):
+            return
+        Dispatcher.set(self, attrs=attrs)
+        self._repeats = self._user_defined_repeats
+        if self._repeats is None:
+            self.infer_repeats()
+        if self._repeats is None:
+            raise RuntimeError(
+                f"{self.__class__.__name__}: infinite loops are not allowed. Please, specify number of repeats."
+            )
+        if attrs.looper is None:
+            attrs.looper = Attributes(repeats=self._repeats, state=Attributes(), terminate=False, tag=self._tag)
+
+    def reset(self, attrs: Attributes | None = None) -> None:
+        if not self._active(attrs):
+            return
+        Dispatcher.reset(self, attrs=attrs)
+        self._repeats = None
+        if "looper" in attrs:
+            del attrs.looper
+
+    def launch(self, attrs: Attributes | None = None) -> None:
+        if not self._active(attrs):
+            return
+        epoch = attrs.launcher.epoch_idx
+        show = bool(self._progress and self._accelerator is not None and self._accelerator.is_local_main_process)
+        bar = None
+        if show:
+            from tqdm import tqdm
+
+            bar = tqdm(total=self._repeats, desc=f"{_green(self._tag)} epoch={epoch}, grad={self._grad_enabled}")
+        last = 0.0
+        for i in range(self._repeats):
+            attrs.batch = None
+            with torch.set_grad_enabled(self._grad_enabled):
+                Dispatcher.launch(self, attrs)
+            if attrs.looper.terminate:
+                break
+            if bar is not None:
+                now = time.monotonic()
+                if now - last >= self._postfix_interval or i == self._repeats - 1:
+                    state = attrs.looper.state
+                    materialize(v for v in state.values())
+                    bar.set_postfix(state, refresh=False)
+                    last = now
+                bar.update(1)
+        if bar is not None:
+            bar.close()
+        self._iter_idx = 0
+        self._repeats = -1
+
+    def state_dict(self) -> dict:
+        return dict(iter_idx=self._iter_idx)
+
+    def load_state_dict(self, state: dict) -> None:
+        self._iter_idx = state.get("iter_idx")
+
+    def guard(self, capsules: list[Capsule]) -> None:
+        super().guard(capsules)
+        for capsule in capsules:
+            if isinstance(capsule, Looper):
+                raise RuntimeError(f"{self.__class__.__name__}: internal loopers are not allowed.")
+
+    def infer_repeats(self) -> None:
+        from rocket_amd.core.dataset import Dataset
+
+        datasets = [c for c in self._capsules if isinstance(c, Dataset)]
+        total = sum(d._total for d in datasets)
+        if total:
+            self._repeats = total
+        elif datasets and any(d._resumed_exhausted for d in datasets):
+            self._repeats = 0  # epoch finished before the checkpoint was taken (Q4)
+        self._logger.info(f"{self.__class__.__name__} infered {self._repeats} repeats.")

@@ -1,0 +1,96 @@
+"""LeNet-5 as in the reference example (``examples/mnist.py:42-74``).
+
+Topology: conv1 1→6 5×5 pad 2 → ReLU → maxpool 2 → conv2 6→16 5×5 → ReLU →
+maxpool 2 → flatten(400) → fc1 120 → ReLU → fc2 84 → ReLU → fc3 10.  The forward
+takes the batch tuple ``(img, label)`` and returns ``(img, label, logits)`` —
+the reference's batch-in/batch-out contract.
+
+``fused=True`` (default on a GPU) routes the layers through the hand-written
+CDNA4 kernels of :mod:`rocket_amd.ops`:
+
+* conv+bias+ReLU+maxpool fused forward, and a fused backward that scatters the
+  pooled gradient through the saved argmax/ReLU mask;
+* MFMA bf16 linear layers with bias/ReLU epilogues and fused bias-gradient
+  column sums (K5, K8).
+
+``fused=False`` is the plain PyTorch module (CPU reference and numerics oracle);
+both share parameter names, so checkpoints are interchangeable.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+class LeNet(nn.Module):
+    def __init__(self, num_classes: int = 10, fused: bool | None = None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 6, 5, padding=2)
+        self.conv2 = nn.Conv2d(6, 16, 5)
+        self.fc1 = nn.Linear(16 * 5 * 5, 120)
+        self.fc2 = nn.Linear(120, 84)
+        self.fc3 = nn.Linear(84, num_classes)
+        self._fused = fused
+
+    def use_fused(self, x: torch.Tensor) -> bool:
+        if self._fused is False:
+            return False
+        if x.device.type != "cuda":
+            if self._fused:
+                raise RuntimeError("fused LeNet kernels need a HIP device")
+            return False
+        return True
+
+    def logits(self, x: torch.Tensor) -> torch.Tensor:
+        if self.use_fused(x):
+            from rocket_amd.ops import conv as fconv
+            from rocket_amd.ops import linear as flin
+
+            h = fconv.conv_bias_relu_pool(x, self.conv1.weight, self.conv1.bias, padding=2)
+            h = fconv.conv_bias_relu_pool(h, self.conv2.weight, self.conv2.bias, padding=0)
+            h = h.reshape(h.shape[0], -1)
+            h = flin.linear(h, self.fc1.weight, self.fc1.bias, activation="relu")
+            h = flin.linear(h, self.fc2.weight, self.fc2.bias, activation="relu")
+            return flin.linear(h, self.fc3.weight, self.fc3.bias, activation=None)
+        x = F.max_pool2d(F.relu(self.conv1(x)), 2)
+        x = F.max_pool2d(F.relu(self.conv2(x)), 2)
+        x = torch.flatten(x, 1)
+        x = F.relu(self.fc1(x))
+        x = F.relu(self.fc2(x))
+        return self.fc3(x)
+
+    def forward(self, batch):
+        if isinstance(batch, torch.Tensor):
+            return self.logits(batch)
+        img, label = batch[0], batch[1]
+        return (img, label, self.logits(img))
+
+
+class CrossEntropy(nn.Module):
+    """``CrossEntropyLoss(batch[2], batch[1])`` (reference ``examples/mnist.py:81-84``).
+
+    On a HIP device it uses the fused softmax-cross-entropy kernel (loss and
+    d(logits) in one pass).
+    """
+
+    def __init__(self, fused: bool | None = None):
+        super().__init__()
+        self._fused = fused
+
+    def forward(self, batch):
+        logits, target = batch[2], batch[1]
+        if self._fused is not False and logits.device.type == "cuda":
+            from rocket_amd.ops.cross_entropy import cross_entropy
+
+            return cross_entropy(logits, target)
+        return F.cross_entropy(logits.float(), target)
+
+
+def synthetic_mnist(n: int = 60000, device="cpu", seed: int = 0, dtype=torch.float32):
+    """Random 1×28×28 images in [0,1) and labels in [0,10) (no network: no real MNIST)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.rand(n, 1, 28, 28, generator=g, dtype=torch.float32).to(dtype)
+    y = torch.randint(0, 10, (n,), generator=g)
+    return x.to(device), y.to(device)

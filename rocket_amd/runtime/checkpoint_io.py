@@ -1,0 +1,144 @@
+"""Checkpoint writer/reader for the rocket on-disk layout.
+
+The reference's ``Checkpointer`` calls ``accelerator.save_state(dir)``
+(``rocket/core/checkpoint.py:129``) and ``Launcher._resume`` calls
+``accelerator.load_state(dir)`` (``rocket/core/launcher.py:356-363``).  The
+directory layout those produce is the compatibility contract:
+
+    model.safetensors / model_{i}.safetensors   unwrapped state_dict, plain keys
+    optimizer.bin / optimizer_{i}.bin           torch.save(optimizer.state_dict())
+    scheduler.bin / scheduler_{i}.bin           torch.save(scheduler.state_dict())
+    scaler.pt                                   fp16 GradScaler only
+    random_states_{rank}.pkl                    python/numpy/torch(/cuda) RNG + GA step
+    custom_checkpoint_{i}.pkl                   torch.save(obj.state_dict()), registration order
+
+Loading rules kept: the number of ``custom_checkpoint_*.pkl`` files must equal
+the number of registered objects (else ``RuntimeError``); a missing RNG file is
+logged and skipped.  Files we read back are loaded with ``weights_only=True``
+where their content allows it (model/optimizer/scheduler/custom state); the RNG
+file holds numpy RNG state and is only ever written by this code.
+"""
+
+from __future__ import annotations
+
+import os
+import random
+import re
+from pathlib import Path
+from typing import List
+
+import numpy as np
+import torch
+from safetensors.torch import load_file as st_load
+from safetensors.torch import save_file as st_save
+
+from rocket_amd.utils.logging import get_logger
+
+logger = get_logger(__name__)
+
+_CUSTOM_RE = re.compile(r"^custom_checkpoint_(\d+)\.pkl$")
+
+
+def _suffixed(stem: str, ext: str, i: int) -> str:
+    return f"{stem}{'' if i == 0 else f'_{i}'}.{ext}"
+
+
+def _cpu_state_dict(model: torch.nn.Module) -> dict:
+    out = {}
+    seen = {}
+    for k, v in model.state_dict().items():
+        if not isinstance(v, torch.Tensor):
+            continue
+        t = v.detach()
+        key = (t.untyped_storage().data_ptr(), t.storage_offset(), tuple(t.shape)) if t.numel() else None
+        if key is not None and key in seen:  # tied weights: safetensors refuses shared storage
+            continue
+        if key is not None:
+            seen[key] = k
+        out[k] = t.to("cpu").contiguous().clone()
+    return out
+
+
+def save_state(engine, output_dir: str) -> Path:
+    out = Path(output_dir)
+    out.mkdir(parents=True, exist_ok=True)
+    for i, model in enumerate(engine._models):
+        st_save(_cpu_state_dict(engine.unwrap_model(model)), str(out / _suffixed("model", "safetensors", i)),
+                metadata={"format": "pt"})
+    for i, opt in enumerate(engine._optimizers):
+        torch.save(opt.state_dict(), out / _suffixed("optimizer", "bin", i))
+    for i, sched in enumerate(engine._schedulers):
+        torch.save(sched.state_dict(), out / _suffixed("scheduler", "bin", i))
+    if engine.scaler is not None:
+        torch.save(engine.scaler.state_dict(), out / "scaler.pt")
+    states = {
+        "step": engine.step,
+        "random_state": random.getstate(),
+        "numpy_random_seed": np.random.get_state(),
+        "torch_manual_seed": torch.get_rng_state(),
+    }
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        states["torch_cuda_manual_seed"] = torch.cuda.get_rng_state_all()
+    torch.save(states, out / f"random_states_{engine.process_index}.pkl")
+    for i, obj in enumerate(engine._custom_objects):
+        torch.save(obj.state_dict(), out / f"custom_checkpoint_{i}.pkl")
+    return out
+
+
+def _load(path, **kw):
+    try:
+        return torch.load(path, weights_only=True, **kw)
+    except Exception:
+        # only files this framework wrote reach here (RNG state with numpy arrays,
+        # user custom state containing plain Python objects)
+        return torch.load(path, weights_only=False, **kw)
+
+
+def custom_checkpoint_files(input_dir: str) -> List[str]:
+    names = [f for f in os.listdir(input_dir) if _CUSTOM_RE.match(f)]
+    return sorted(names, key=lambda f: int(_CUSTOM_RE.match(f).group(1)))
+
+
+def load_state(engine, input_dir: str, load_custom: bool = True) -> None:
+    src = Path(input_dir)
+    if not src.is_dir():
+        raise FileNotFoundError(f"checkpoint directory {input_dir} does not exist")
+    for i, model in enumerate(engine._models):
+        st = src / _suffixed("model", "safetensors", i)
+        if st.exists():
+            sd = st_load(str(st), device="cpu")
+        else:
+            sd = _load(src / _suffixed("pytorch_model", "bin", i), map_location="cpu")
+        engine.unwrap_model(model).load_state_dict(sd, strict=False)
+    for i, opt in enumerate(engine._optimizers):
+        opt.load_state_dict(_load(src / _suffixed("optimizer", "bin", i), map_location="cpu"))
+    for i, sched in enumerate(engine._schedulers):
+        sched.load_state_dict(_load(src / _suffixed("scheduler", "bin", i)))
+    if engine.scaler is not None and (src / "scaler.pt").exists():
+        engine.scaler.load_state_dict(_load(src / "scaler.pt"))
+    rng = src / f"random_states_{engine.process_index}.pkl"
+    if rng.exists():
+        try:
+            states = torch.load(rng, weights_only=False)  # written by save_state above
+            engine.step = states.get("step", engine.step)
+            random.setstate(states["random_state"])
+            np.random.set_state(states["numpy_random_seed"])
+            torch.set_rng_state(states["torch_manual_seed"])
+            if "torch_cuda_manual_seed" in states and torch.cuda.is_available():
+                cuda_states = states["torch_cuda_manual_seed"]
+                if len(cuda_states) == torch.cuda.device_count():
+                    torch.cuda.set_rng_state_all(cuda_states)
+        except Exception as e:  # pragma: no cover - mirrors accelerate's "could not load"
+            logger.info(f"Could not load random states: {e}")
+    else:
+        logger.info("Could not load random states")
+    if not load_custom:
+        return
+    files = custom_checkpoint_files(str(src))
+    if len(files) != len(engine._custom_objects):
+        raise RuntimeError(
+            f"Number of custom checkpoints in folder {input_dir} does not match the number of registered objects:"
+            f"\n\tFound checkpoints: {len(files)}\n\tRegistered objects: {len(engine._custom_objects)}\n"
+        )
+    for i, obj in enumerate(engine._custom_objects):
+        obj.load_state_dict(_load(src / f"custom_checkpoint_{i}.pkl", map_location="cpu"))

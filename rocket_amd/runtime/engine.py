@@ -1,0 +1,493 @@
+"""The runtime engine: everything the reference delegates to ``accelerate.Accelerator``.
+
+Every capsule of the reference reaches the device/precision/distribution layer
+through ``self._accelerator`` (SURVEY §2.3 lists the 25 call sites).  This class
+provides that surface natively on PyTorch-ROCm so the capsule code keeps its
+shape while the hot path is ours:
+
+==========================  ===================================================
+accelerate surface           here
+==========================  ===================================================
+``Accelerator(...)``         ``Engine(mixed_precision, gradient_accumulation_steps,
+                             project_dir, cpu, seed, …)`` — comm initialised first
+``prepare(model)``           device move, :class:`~rocket_amd.parallel.ddp.DataParallel`
+                             when W>1, autocast+fp32-output forward patch
+``prepare(optimizer)``       :class:`EngineOptimizer` (sync-gated step/zero_grad, fp16 scaler)
+``prepare(scheduler)``       :class:`EngineScheduler` (steps ×W on sync steps)
+``prepare(dataloader)``      :class:`~rocket_amd.runtime.data.ShardedLoader` /
+                             :class:`~rocket_amd.runtime.data.DeviceLoader`
+``accumulate``/``no_sync``   GA state machine (``_do_sync``) + replica ``no_sync``
+``backward``                 ``loss / GA`` (+ GradScaler)
+``gather``/``gather_for_metrics``/``reduce``  RCCL collectives, remainder truncation
+``save_state``/``load_state``  :mod:`rocket_amd.runtime.checkpoint_io` (same layout)
+trackers                     :mod:`rocket_amd.runtime.trackers`
+==========================  ===================================================
+"""
+
+from __future__ import annotations
+
+import contextlib
+import math
+import os
+from typing import Any, Callable, List, Optional
+
+import torch
+from torch import nn
+
+from rocket_amd.parallel.ddp import DataParallel, unwrap
+from rocket_amd.runtime import comm as _comm
+from rocket_amd.runtime import checkpoint_io
+from rocket_amd.runtime.data import (
+    DeviceLoader,
+    DeviceTensorDataset,
+    GradientState,
+    ShardedLoader,
+    _LoaderBase,
+)
+from rocket_amd.runtime.trackers import GeneralTracker, make_tracker
+from rocket_amd.utils.collections import apply_to_collection, is_collection
+from rocket_amd.utils.logging import get_logger
+
+logger = get_logger(__name__)
+
+_MP = {None: None, "no": None, "fp32": None, "bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+def _to_fp32(x):
+    if isinstance(x, torch.Tensor):
+        return x.float() if x.dtype in (torch.float16, torch.bfloat16) else x
+    if is_collection(x) and not isinstance(x, (str, bytes)):
+        return apply_to_collection(x, lambda v, key=None: _to_fp32(v))
+    return x
+
+
+class EngineOptimizer:
+    """Optimizer wrapper: steps and zeroes only on gradient-sync micro-steps.
+
+    Parity: ``accelerate.optimizer.AcceleratedOptimizer`` (reached from
+    ``rocket/core/optimizer.py:109,128-130``).
+    """
+
+    def __init__(self, optimizer: torch.optim.Optimizer, engine: "Engine"):
+        self.optimizer = optimizer
+        self.engine = engine
+        self.step_was_skipped = False
+
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    @property
+    def state(self):
+        return self.optimizer.state
+
+    @property
+    def defaults(self):
+        return self.optimizer.defaults
+
+    def state_dict(self):
+        return self.optimizer.state_dict()
+
+    def load_state_dict(self, sd):
+        self.optimizer.load_state_dict(sd)
+
+    def _uses_bucket_views(self) -> bool:
+        ids = self.engine._bucket_param_ids
+        return bool(ids) and any(id(p) in ids for g in self.optimizer.param_groups for p in g["params"])
+
+    def zero_grad(self, set_to_none: Optional[bool] = None) -> None:
+        if not self.engine.sync_gradients:
+            return
+        if self._uses_bucket_views():
+            self.optimizer.zero_grad(set_to_none=False)
+        else:
+            self.optimizer.zero_grad(set_to_none=True if set_to_none is None else set_to_none)
+
+    def step(self, closure: Callable | None = None):
+        if not self.engine.sync_gradients:
+            return None
+        scaler = self.engine.scaler
+        if scaler is not None:
+            scale_before = scaler.get_scale()
+            scaler.step(self.optimizer, closure) if closure else scaler.step(self.optimizer)
+            scaler.update()
+            self.step_was_skipped = scaler.get_scale() < scale_before
+            return None
+        self.step_was_skipped = False
+        return self.optimizer.step(closure) if closure else self.optimizer.step()
+
+    def __getattr__(self, name):
+        return getattr(self.optimizer, name)
+
+
+class EngineScheduler:
+    """Scheduler wrapper (parity: ``accelerate.scheduler.AcceleratedScheduler``).
+
+    On sync steps it steps once per process (the global batch grew ×W); on
+    accumulation micro-steps it only advances ``_step_count``.
+    """
+
+    def __init__(self, scheduler, optimizers: List[EngineOptimizer], engine: "Engine"):
+        self.scheduler = scheduler
+        self.optimizers = optimizers
+        self.engine = engine
+
+    def step(self, *args, **kwargs):
+        if not self.engine.sync_gradients:
+            self.scheduler._step_count += 1
+            return
+        if any(o.step_was_skipped for o in self.optimizers):
+            return
+        for _ in range(self.engine.num_processes):
+            total = getattr(self.scheduler, "total_steps", None)
+            if total is not None and self.scheduler._step_count > total:
+                continue
+            self.scheduler.step(*args, **kwargs)
+
+    def get_last_lr(self):
+        return self.scheduler.get_last_lr()
+
+    def state_dict(self):
+        return self.scheduler.state_dict()
+
+    def load_state_dict(self, sd):
+        self.scheduler.load_state_dict(sd)
+
+    def __getattr__(self, name):
+        return getattr(self.scheduler, name)
+
+
+class Engine:
+    """Native replacement of the accelerate runtime used by the capsules."""
+
+    def __init__(
+        self,
+        device_placement: bool = True,
+        mixed_precision: str | None = None,
+        gradient_accumulation_steps: int = 1,
+        project_dir: str | None = None,
+        cpu: bool | None = None,
+        seed: int | None = None,
+        bucket_cap_mb: float | None = None,
+        even_batches: bool = True,
+        log_with: List[str] | None = None,
+        **unused: Any,
+    ):
+        env_mp = os.environ.get("ROCKET_MIXED_PRECISION", os.environ.get("ACCELERATE_MIXED_PRECISION"))
+        mixed_precision = mixed_precision if mixed_precision is not None else env_mp
+        if mixed_precision not in _MP:
+            raise ValueError(f"unsupported mixed_precision {mixed_precision!r}")
+        self.ctx = _comm.init(cpu=cpu)
+        self.device_placement = device_placement
+        self.mixed_precision = mixed_precision or "no"
+        self._amp_dtype = _MP[mixed_precision]
+        self.gradient_accumulation_steps = max(1, int(gradient_accumulation_steps))
+        self.gradient_state = GradientState(self.gradient_accumulation_steps)
+        self.project_dir = project_dir
+        self.logging_dir = project_dir
+        self.seed = 0 if seed is None else int(seed)
+        self.even_batches = even_batches
+        self.bucket_cap_mb = bucket_cap_mb or float(os.environ.get("ROCKET_BUCKET_MB", 32.0))
+        self.step = 0
+        self.scaler = None
+        if self.mixed_precision == "fp16":
+            self.scaler = torch.amp.GradScaler(self.device.type)
+        self._models: List[nn.Module] = []
+        self._wrapped: dict = {}
+        self._bucket_param_ids: set = set()
+        self._optimizers: List[EngineOptimizer] = []
+        self._schedulers: List[EngineScheduler] = []
+        self._dataloaders: List[_LoaderBase] = []
+        self._custom_objects: List[Any] = []
+        self.trackers: List[GeneralTracker] = []
+        self.log_with: List[str] = list(log_with or [])
+
+    # ------------------------------------------------------------ topology
+    @property
+    def device(self) -> torch.device:
+        return self.ctx.device
+
+    @property
+    def num_processes(self) -> int:
+        return self.ctx.world_size
+
+    @property
+    def process_index(self) -> int:
+        return self.ctx.rank
+
+    @property
+    def local_process_index(self) -> int:
+        return self.ctx.local_rank
+
+    @property
+    def num_nodes(self) -> int:
+        return self.ctx.num_nodes
+
+    @property
+    def is_main_process(self) -> bool:
+        return self.ctx.is_main_process
+
+    @property
+    def is_local_main_process(self) -> bool:
+        return self.ctx.is_local_main_process
+
+    @property
+    def distributed(self) -> bool:
+        return self.ctx.distributed
+
+    def wait_for_everyone(self) -> None:
+        _comm.barrier()
+
+    def print(self, *args, **kwargs) -> None:
+        if self.is_local_main_process:
+            print(*args, **kwargs)
+
+    # ------------------------------------------------------------- prepare
+    def prepare(self, *objs, device_placement: Optional[List[bool]] = None):
+        placement = device_placement or [self.device_placement] * len(objs)
+        out = []
+        for obj, place in zip(objs, placement):
+            if isinstance(obj, nn.Module):
+                out.append(self.prepare_model(obj, device_placement=place))
+            elif isinstance(obj, torch.optim.Optimizer):
+                out.append(self.prepare_optimizer(obj))
+            elif isinstance(obj, torch.optim.lr_scheduler.LRScheduler) or hasattr(obj, "get_last_lr"):
+                out.append(self.prepare_scheduler(obj))
+            elif isinstance(obj, (torch.utils.data.DataLoader, _LoaderBase)):
+                out.append(self.prepare_data_loader(obj, device_placement=place))
+            else:
+                out.append(obj)
+        return out[0] if len(out) == 1 else tuple(out)
+
+    def prepare_model(self, model: nn.Module, device_placement: bool = True) -> nn.Module:
+        if device_placement:
+            model = model.to(self.device)
+        if self._amp_dtype is not None and not getattr(model.forward, "_rocket_amp", False):
+            orig = model.forward
+            dtype, dev = self._amp_dtype, self.device.type
+
+            def forward(*args, **kwargs):
+                with torch.autocast(device_type=dev, dtype=dtype):
+                    out = orig(*args, **kwargs)
+                return _to_fp32(out)
+
+            forward._rocket_amp = True
+            forward.__wrapped__ = orig
+            model.forward = forward
+        self._models.append(model)
+        if self.distributed and any(p.requires_grad for p in model.parameters()):
+            wrapped = DataParallel(model, bucket_cap_mb=self.bucket_cap_mb)
+            self._wrapped[id(model)] = wrapped
+            self._bucket_param_ids.update(id(p) for p in model.parameters())
+            return wrapped
+        return model
+
+    def prepare_optimizer(self, optimizer: torch.optim.Optimizer) -> EngineOptimizer:
+        if self.device_placement:
+            for state in optimizer.state.values():
+                for k, v in state.items():
+                    if isinstance(v, torch.Tensor) and k != "step":
+                        state[k] = v.to(self.device)
+        wrapped = EngineOptimizer(optimizer, self)
+        self._optimizers.append(wrapped)
+        return wrapped
+
+    def prepare_scheduler(self, scheduler) -> EngineScheduler:
+        opts = [o for o in self._optimizers if o.optimizer is getattr(scheduler, "optimizer", None)]
+        wrapped = EngineScheduler(scheduler, opts or list(self._optimizers), self)
+        self._schedulers.append(wrapped)
+        return wrapped
+
+    def make_loader(self, dataset, device_placement: bool = False, **kwargs) -> _LoaderBase:
+        """Build the sharded loader for a dataset (what ``Dataset.setup`` uses)."""
+        common = dict(
+            num_replicas=self.num_processes,
+            rank=self.process_index,
+            even_batches=self.even_batches,
+            seed=kwargs.pop("seed", self.seed),
+            gradient_state=self.gradient_state,
+        )
+        if isinstance(dataset, DeviceTensorDataset):
+            loader = DeviceLoader(dataset, **kwargs, **common)
+        else:
+            kwargs.setdefault("pin_memory", self.device.type == "cuda")
+            loader = ShardedLoader(dataset, device=self.device if device_placement else None, **kwargs, **common)
+        self._dataloaders.append(loader)
+        return loader
+
+    def prepare_data_loader(self, dl, device_placement: bool = False) -> _LoaderBase:
+        if isinstance(dl, _LoaderBase):
+            if dl not in self._dataloaders:
+                self._dataloaders.append(dl)
+            return dl
+        kw = dict(
+            batch_size=dl.batch_size,
+            drop_last=dl.drop_last,
+            num_workers=dl.num_workers,
+            collate_fn=dl.collate_fn,
+            pin_memory=dl.pin_memory,
+        )
+        if dl.batch_size is None:
+            kw = dict(batch_sampler=dl.batch_sampler, num_workers=dl.num_workers, collate_fn=dl.collate_fn)
+        else:
+            kw["sampler"] = dl.sampler
+        return self.make_loader(dl.dataset, device_placement=device_placement, **kw)
+
+    def skip_first_batches(self, dataloader: _LoaderBase, num_batches: int = 0) -> _LoaderBase:
+        return dataloader.with_skip(num_batches)
+
+    def unwrap_model(self, model: nn.Module) -> nn.Module:
+        model = unwrap(model)
+        fwd = model.__dict__.get("forward")
+        if fwd is not None and getattr(fwd, "_rocket_amp", False):
+            pass  # keep the patched forward on the live model; state_dict is unaffected
+        return model
+
+    def replica(self, model: nn.Module) -> nn.Module:
+        """Return the data-parallel wrapper of a prepared model (or the model itself)."""
+        return self._wrapped.get(id(unwrap(model)), model)
+
+    # ---------------------------------------------------- mixed precision / GA
+    def autocast(self):
+        if self._amp_dtype is None:
+            return contextlib.nullcontext()
+        return torch.autocast(device_type=self.device.type, dtype=self._amp_dtype)
+
+    @property
+    def sync_gradients(self) -> bool:
+        return self.gradient_state.sync_gradients
+
+    @sync_gradients.setter
+    def sync_gradients(self, value: bool) -> None:
+        self.gradient_state.sync_gradients = bool(value)
+
+    @property
+    def end_of_dataloader(self) -> bool:
+        return self.gradient_state.end_of_dataloader
+
+    def _do_sync(self) -> None:
+        if self.gradient_state.end_of_dataloader:
+            self.step = 0
+            self.sync_gradients = True
+        else:
+            self.step += 1
+            self.sync_gradients = (self.step % self.gradient_accumulation_steps) == 0
+
+    @contextlib.contextmanager
+    def no_sync(self, model: nn.Module):
+        rep = self.replica(model)
+        ctx = rep.no_sync() if isinstance(rep, DataParallel) else contextlib.nullcontext()
+        with ctx:
+            yield
+
+    @contextlib.contextmanager
+    def accumulate(self, *models: nn.Module):
+        self._do_sync()
+        with contextlib.ExitStack() as stack:
+            if not self.sync_gradients:
+                for m in models:
+                    stack.enter_context(self.no_sync(m))
+            yield
+
+    def backward(self, loss: torch.Tensor, **kwargs) -> None:
+        if self.gradient_accumulation_steps > 1:
+            loss = loss / self.gradient_accumulation_steps
+        if self.scaler is not None:
+            self.scaler.scale(loss).backward(**kwargs)
+        else:
+            loss.backward(**kwargs)
+
+    def clip_grad_norm_(self, parameters, max_norm: float, norm_type: float = 2.0):
+        if self.scaler is not None:
+            for o in self._optimizers:
+                self.scaler.unscale_(o.optimizer)
+        return torch.nn.utils.clip_grad_norm_(parameters, max_norm, norm_type=norm_type)
+
+    # --------------------------------------------------------- collectives
+    def gather(self, tensor):
+        if isinstance(tensor, torch.Tensor):
+            return _comm.all_gather_tensor(tensor)
+        return apply_to_collection(tensor, lambda v, key=None: self.gather(v))
+
+    def gather_for_metrics(self, input_data, use_gather_object: bool = False):
+        def all_tensors(x):
+            if isinstance(x, torch.Tensor):
+                return True
+            if is_collection(x) and not isinstance(x, (str, bytes)):
+                vals = x.values() if isinstance(x, dict) else x
+                return all(all_tensors(v) for v in vals)
+            return False
+
+        as_object = use_gather_object or not all_tensors(input_data)
+        if as_object:
+            parts = _comm.all_gather_object(input_data)
+            data = [v for part in parts for v in (part if isinstance(part, list) else [part])]
+        else:
+            data = self.gather(input_data)
+        gs = self.gradient_state
+        if gs.end_of_dataloader and gs.remainder > 0 and self.num_processes > 1:
+            r = gs.remainder
+            if as_object:
+                return data[:r]
+            return apply_to_collection(data, lambda v, key=None: v[:r]) if not isinstance(data, torch.Tensor) else data[:r]
+        return data
+
+    def reduce(self, tensor, reduction: str = "sum", scale: float = 1.0):
+        if isinstance(tensor, torch.Tensor):
+            out = tensor.clone()
+            _comm.all_reduce_(out, "mean" if reduction == "mean" else "sum")
+            return out * scale if scale != 1.0 else out
+        return apply_to_collection(tensor, lambda v, key=None: self.reduce(v, reduction, scale))
+
+    # ------------------------------------------------------------ checkpoints
+    def register_for_checkpointing(self, *objects) -> None:
+        bad = [o for o in objects if not (hasattr(o, "state_dict") and hasattr(o, "load_state_dict"))]
+        if bad:
+            raise ValueError(f"objects without state_dict/load_state_dict: {bad}")
+        self._custom_objects.extend(objects)
+
+    def save_state(self, output_dir: str | None = None, **kwargs):
+        if output_dir is None:
+            if self.project_dir is None:
+                raise ValueError("save_state needs output_dir or a project_dir")
+            output_dir = os.path.join(self.project_dir, "checkpoints", f"checkpoint_{len(os.listdir(self.project_dir))}")
+        return checkpoint_io.save_state(self, output_dir)
+
+    def load_state(self, input_dir: str, load_custom: bool = True, **kwargs) -> None:
+        checkpoint_io.load_state(self, input_dir, load_custom=load_custom)
+
+    # ---------------------------------------------------------------- trackers
+    def get_tracker(self, name: str, unwrap: bool = False):
+        for t in self.trackers:
+            if t.name == name:
+                return t.tracker if unwrap else t
+        return GeneralTracker(_blank=True)
+
+    def init_trackers(self, project_name: str = "", config: dict | None = None, init_kwargs: dict | None = None):
+        if not self.is_main_process:
+            return
+        have = {t.name for t in self.trackers}
+        for name in self.log_with:
+            if isinstance(name, GeneralTracker):
+                if name not in self.trackers:
+                    self.trackers.append(name)
+                continue
+            if name in have:
+                continue
+            t = make_tracker(name, project_name, self.logging_dir or ".")
+            if config is not None:
+                t.store_init_configuration(config)
+            self.trackers.append(t)
+
+    def log(self, values: dict, step: int | None = None, log_kwargs: dict | None = None) -> None:
+        if self.is_main_process:
+            for t in self.trackers:
+                t.log(values, step=step, **(log_kwargs or {}).get(t.name, {}))
+
+    def end_training(self) -> None:
+        for t in self.trackers:
+            try:
+                t.finish()
+            except Exception as e:  # pragma: no cover
+                logger.warning(f"tracker {t.name} finish failed: {e}")
+        self.trackers = []
