@@ -1,0 +1,166 @@
+"""Headline benchmark: whole-node samples/s of the MNIST ConvNet training step (BASELINE.json).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` — for N>1
+launched under ``torch.distributed.run`` (one rank per GPU, RCCL).  W untimed
+steps, then exactly K steps bracketed by barrier + device sync on both sides;
+the elapsed time is the MAX over ranks; rank 0 prints ONE JSON line.
+
+What runs: the reference ``examples/mnist.py`` topology built from this
+framework's capsules — ``Launcher → Looper → {Dataset, Module(LeNet) →
+{Loss(CrossEntropy), Optimizer(AdamW), Scheduler(StepLR(100))}, StepTimer}`` —
+bf16 mixed precision, per-GPU batch 1024 (weak scaling: global batch 1024·N),
+synthetic MNIST-shaped data (random 1×28×28 images / labels, resident in HBM
+and reshuffled every epoch on-device), random-init weights.  Every timed step
+does the full work: batch gather, forward, loss, backward, gradient all-reduce
+(N>1), AdamW update, LR schedule, loss accounting.
+
+Extra flags (for A/B runs): ``--impl torch`` uses stock PyTorch ops instead of
+the fused HIP kernels; ``--no-graph`` disables HIP-graph capture of the step.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE_METRIC = "samples/sec (whole node) MNIST ConvNet at 1/2/4/8 MI355X; step-time p50"
+
+
+def _baseline_value(n_gpus: int):
+    """Reference number to divide by: 1-GPU MI355X reference × N (ideal weak scaling)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
+    try:
+        with open(path) as fh:
+            b = json.load(fh)
+        per_gpu = b.get("measured", {}).get("reference_mi355x_1gpu_bf16_samples_per_s")
+        if per_gpu:
+            return float(per_gpu) * n_gpus
+    except Exception:
+        pass
+    return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch")
+    ap.add_argument("--impl", choices=["fused", "torch"], default="fused")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--mp", default="bf16")
+    ap.add_argument("--cpu", action="store_true")
+    args = ap.parse_args()
+
+    import rocket_amd as rocket
+    from rocket_amd.models import CrossEntropy, LeNet
+    from rocket_amd.runtime import comm
+    from rocket_amd.runtime.data import DeviceTensorDataset
+    from rocket_amd.runtime.profiling import StepTimer
+
+    ctx = comm.init(cpu=args.cpu)
+    world = ctx.world_size
+    if world != args.gpus and ctx.rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = ctx.device
+    on_gpu = dev.type == "cuda"
+    fused = on_gpu and args.impl == "fused"
+    if fused:
+        from rocket_amd import ops
+
+        ops.require_native()
+
+    total_iters = args.warmup + args.steps
+    n = (total_iters + 1) * args.batch * world  # one epoch covers the whole run on every rank
+    g = torch.Generator(device=dev).manual_seed(1234)
+    x = torch.rand(n, 1, 28, 28, generator=g, device=dev)
+    y = torch.randint(0, 10, (n,), generator=g, device=dev)
+    data = DeviceTensorDataset(x, y)
+
+    torch.manual_seed(0)
+    net = LeNet(fused=fused)
+    if fused:
+        from rocket_amd.ops.optim import FusedAdamW
+
+        opt = FusedAdamW(net.parameters())
+    else:
+        opt = torch.optim.AdamW(net.parameters(), foreach=True)
+    sched = torch.optim.lr_scheduler.StepLR(opt, 100)
+    timer = StepTimer(warmup=args.warmup, steps=args.steps)
+    launcher = rocket.Launcher(
+        [
+            rocket.Looper(
+                [
+                    rocket.Dataset(data, batch_size=args.batch, shuffle=True, drop_last=True),
+                    rocket.Module(
+                        net,
+                        [rocket.Loss(CrossEntropy(fused=fused)), rocket.Optimizer(opt), rocket.Scheduler(sched)],
+                        capture=fused and not args.no_graph,
+                    ),
+                    timer,
+                ],
+                repeats=total_iters,
+                progress=False,
+            )
+        ],
+        mixed_precision=args.mp if on_gpu else None,
+        num_procs=world,
+        num_epochs=1,
+        destroy_process_group_after_launch=False,
+        cpu=args.cpu,
+    )
+    t0 = time.perf_counter()
+    launcher.launch()
+    wall = time.perf_counter() - t0
+
+    elapsed = timer.elapsed
+    summ = timer.summary()
+    stats = torch.tensor([elapsed, summ.get("step_ms_p50", 0.0)], dtype=torch.float64)
+    if world > 1:
+        parts = comm.all_gather_object(stats.tolist())
+        elapsed = max(p[0] for p in parts)
+        p50 = max(p[1] for p in parts)
+    else:
+        p50 = summ.get("step_ms_p50", 0.0)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * args.batch * args.steps / elapsed
+    base = _baseline_value(world)
+    if ctx.rank == 0:
+        rec = {
+            "metric": BASELINE_METRIC,
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "step_ms_p50": round(p50, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / base, 3) if base else None,
+            "dtype": "bf16" if args.mp == "bf16" else "fp32",
+            "data": "synthetic (random 1x28x28 MNIST-shaped images/labels in HBM, random-init weights)",
+            "config": {
+                "model": "LeNet-5 MNIST 2-conv CNN (reference examples/mnist.py)",
+                "global_batch": args.batch * world,
+                "per_gpu_batch": args.batch,
+                "seq_len": None,
+                "input_shape": [1, 28, 28],
+                "optimizer": "AdamW + StepLR(100)",
+                "parallelism": f"dp{world}",
+                "impl": ("fused-hip" + ("" if args.no_graph else "+hipgraph")) if fused else "torch-eager",
+            },
+            "wall_s": round(wall, 2),
+        }
+        print(json.dumps(rec), flush=True)
+    comm.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,162 @@
+// Fused multi-tensor optimizers: AdamW / Adam and SGD(momentum, nesterov).
+//
+// One launch updates every parameter tensor of an optimizer: a device-resident
+// tensor table (param/grad/state pointers, sizes, group id) and a block table
+// (tensor, chunk) are built once on the host and re-uploaded only when a
+// pointer changes, so the launch is graph-capturable.  Hyper-parameters live in
+// a small device array per param group (lr, betas, eps, weight decay) that the
+// host refreshes only when a scheduler changes them, and the step counter lives
+// in device memory: the LAST block to finish (ticket counter, agent-scope
+// release/acquire) advances it, so bias corrections need no host round trip.
+//
+// Optional AMP hooks: `inv_scale` multiplies every gradient (GradScaler unscale
+// folded into the update) and a non-zero `found_inf` makes the launch a no-op.
+//
+// Memory: each block streams a 4096-element chunk (16 fp32/thread, float4
+// vectorised): params/grads/exp_avg/exp_avg_sq read once, written once.
+#include "rk_common.h"
+
+using namespace rk;
+
+namespace {
+
+constexpr int kChunk = 4096;
+constexpr int kThreads = 256;
+
+struct TensorRec {  // 6 x int64 per tensor, uploaded from the host
+  int64_t p, g, s0, s1, n, group;
+};
+
+struct AdamHyper {  // 8 floats per group
+  float lr, beta1, beta2, eps, wd, decoupled, maximize, pad;
+};
+
+template <typename G>
+__device__ __forceinline__ float gload(const G* g, int64_t i);
+template <> __device__ __forceinline__ float gload<float>(const float* g, int64_t i) { return g[i]; }
+template <> __device__ __forceinline__ float gload<uint16_t>(const uint16_t* g, int64_t i) { return bf2f(g[i]); }
+
+template <typename G>
+__global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __restrict__ tensors,
+                                                          const int2* __restrict__ blocks,
+                                                          const AdamHyper* __restrict__ hyper, float* step,
+                                                          const float* inv_scale, const float* found_inf,
+                                                          unsigned* counter) {
+  __shared__ int flag;
+  const bool skip = found_inf != nullptr && found_inf[0] != 0.f;
+  if (!skip) {
+    const int2 bt = blocks[blockIdx.x];
+    const TensorRec tr = tensors[bt.x];
+    const AdamHyper h = hyper[tr.group];
+    float* __restrict__ p = (float*)tr.p;
+    const G* __restrict__ g = (const G*)tr.g;
+    float* __restrict__ m = (float*)tr.s0;
+    float* __restrict__ v = (float*)tr.s1;
+    const float t = step[0] + 1.f;
+    const float bc1 = 1.f - __powf(h.beta1, t);
+    const float bc2 = 1.f - __powf(h.beta2, t);
+    const float step_size = h.lr / bc1;
+    const float rbc2 = rsqrtf(bc2);
+    const float gs = inv_scale ? inv_scale[0] : 1.f;
+    const float decay = h.decoupled != 0.f ? 1.f - h.lr * h.wd : 1.f;
+    const float l2 = h.decoupled != 0.f ? 0.f : h.wd;
+    const float sgn = h.maximize != 0.f ? -1.f : 1.f;
+    const int64_t start = (int64_t)bt.y * kChunk;
+    const int64_t end = min(start + (int64_t)kChunk, tr.n);
+    auto upd = [&](float& pp, float gg, float& mm, float& vv) {
+      gg = sgn * gg * gs + l2 * pp;
+      pp *= decay;
+      mm = h.beta1 * mm + (1.f - h.beta1) * gg;
+      vv = h.beta2 * vv + (1.f - h.beta2) * gg * gg;
+      pp -= step_size * mm / (sqrtf(vv) * rbc2 + h.eps);
+    };
+    const bool vec = sizeof(G) == 4 && ((tr.p | tr.g | tr.s0 | tr.s1) & 15) == 0;
+    if (vec) {
+      for (int64_t i = start + 4 * threadIdx.x; i < end; i += 4 * kThreads) {
+        if (i + 4 <= end) {
+          float4 pp = *(float4*)(p + i), mm = *(float4*)(m + i), vv = *(float4*)(v + i);
+          float4 gg = *(const float4*)((const float*)g + i);
+          upd(pp.x, gg.x, mm.x, vv.x);
+          upd(pp.y, gg.y, mm.y, vv.y);
+          upd(pp.z, gg.z, mm.z, vv.z);
+          upd(pp.w, gg.w, mm.w, vv.w);
+          *(float4*)(p + i) = pp;
+          *(float4*)(m + i) = mm;
+          *(float4*)(v + i) = vv;
+        } else {
+          for (int64_t k = i; k < end; ++k) upd(p[k], gload<G>(g, k), m[k], v[k]);
+        }
+      }
+    } else {
+      for (int64_t i = start + threadIdx.x; i < end; i += kThreads) upd(p[i], gload<G>(g, i), m[i], v[i]);
+    }
+  }
+  if (last_block_arrived(counter, &flag)) {
+    if (threadIdx.x == 0 && !skip) step[0] += 1.f;
+    reset_counter(counter);
+  }
+}
+
+struct SgdHyper {  // 8 floats per group
+  float lr, momentum, dampening, wd, nesterov, maximize, first, pad;
+};
+
+template <typename G>
+__global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __restrict__ tensors,
+                                                         const int2* __restrict__ blocks,
+                                                         const SgdHyper* __restrict__ hyper, float* step,
+                                                         const float* inv_scale, const float* found_inf,
+                                                         unsigned* counter) {
+  __shared__ int flag;
+  const bool skip = found_inf != nullptr && found_inf[0] != 0.f;
+  if (!skip) {
+    const int2 bt = blocks[blockIdx.x];
+    const TensorRec tr = tensors[bt.x];
+    const SgdHyper h = hyper[tr.group];
+    float* p = (float*)tr.p;
+    const G* g = (const G*)tr.g;
+    float* buf = (float*)tr.s0;
+    const bool first = step[0] == 0.f;  // momentum buffer initialised with the first gradient (torch semantics)
+    const float gs = inv_scale ? inv_scale[0] : 1.f;
+    const float sgn = h.maximize != 0.f ? -1.f : 1.f;
+    const int64_t start = (int64_t)bt.y * kChunk;
+    const int64_t end = min(start + (int64_t)kChunk, tr.n);
+    for (int64_t i = start + threadIdx.x; i < end; i += kThreads) {
+      float gg = gload<G>(g, i) * gs + h.wd * p[i];
+      if (h.momentum != 0.f) {
+        float b = first ? gg : h.momentum * buf[i] + (1.f - h.dampening) * gg;
+        buf[i] = b;
+        gg = h.nesterov != 0.f ? gg + h.momentum * b : b;
+      }
+      p[i] -= sgn * h.lr * gg;
+    }
+  }
+  if (last_block_arrived(counter, &flag)) {
+    if (threadIdx.x == 0 && !skip) step[0] += 1.f;
+    reset_counter(counter);
+  }
+}
+
+}  // namespace
+
+RK_API int rk_optim_chunk() { return kChunk; }
+
+// kind: 0 = Adam/AdamW, 1 = SGD.  gdtype: grads dtype (0 f32, 1 bf16).
+RK_API int rk_optim_mt(int kind, int gdtype, const void* tensors, const void* blocks, int nblocks, const void* hyper,
+                       float* step, const float* inv_scale, const float* found_inf, unsigned* counter, hipStream_t s) {
+  if (nblocks <= 0) return 0;
+  const TensorRec* t = (const TensorRec*)tensors;
+  const int2* b = (const int2*)blocks;
+  if (kind == 0) {
+    if (gdtype == BF16)
+      adam_mt_kernel<uint16_t><<<nblocks, kThreads, 0, s>>>(t, b, (const AdamHyper*)hyper, step, inv_scale, found_inf, counter);
+    else
+      adam_mt_kernel<float><<<nblocks, kThreads, 0, s>>>(t, b, (const AdamHyper*)hyper, step, inv_scale, found_inf, counter);
+  } else {
+    if (gdtype == BF16)
+      sgd_mt_kernel<uint16_t><<<nblocks, kThreads, 0, s>>>(t, b, (const SgdHyper*)hyper, step, inv_scale, found_inf, counter);
+    else
+      sgd_mt_kernel<float><<<nblocks, kThreads, 0, s>>>(t, b, (const SgdHyper*)hyper, step, inv_scale, found_inf, counter);
+  }
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,104 @@
+// Common device helpers for the rocket_amd CDNA4 (gfx950) kernels.
+//
+// Conventions
+//  * every entry point is `extern "C"`, takes raw device pointers plus the HIP
+//    stream to launch on (the current PyTorch stream, so calls are captured by
+//    hipGraphs), and returns a hipError_t code;
+//  * wave size is 64 (never 32): all cross-lane reductions cover 64 lanes;
+//  * bf16 is stored as `__bf16` / raw uint16 and widened to f32 for math.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RK_API extern "C" __attribute__((visibility("default")))
+
+namespace rk {
+
+constexpr int kWave = 64;
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+enum DType : int { F32 = 0, BF16 = 1, F16 = 2 };
+
+__device__ __forceinline__ float bf2f(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// round-to-nearest-even; NaN stays NaN (plain cast lowers to v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+template <typename T> struct Ld;
+template <> struct Ld<float> {
+  static __device__ __forceinline__ float get(const float* p, int64_t i) { return p[i]; }
+  static __device__ __forceinline__ void put(float* p, int64_t i, float v) { p[i] = v; }
+};
+template <> struct Ld<uint16_t> {
+  static __device__ __forceinline__ float get(const uint16_t* p, int64_t i) { return bf2f(p[i]); }
+  static __device__ __forceinline__ void put(uint16_t* p, int64_t i, float v) { p[i] = f2bf(v); }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Block-wide sum; `scratch` must hold blockDim.x/64 floats. Result valid in every thread.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += scratch[i];
+  return t;
+}
+
+// Last-arriving-block election for in-launch grid reductions (CDNA4 rule: agent-scope
+// release by the producer, agent-scope acquire by the consumer; placement-independent).
+// Call from ALL threads after this block's partial results were stored by thread 0.
+// Returns true in every thread of the block that arrived last. `counter` must be 0
+// before the launch; the last block resets it to 0 (so graph replays stay valid).
+__device__ __forceinline__ bool last_block_arrived(unsigned* counter, int* smem_flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = (t == gridDim.x * gridDim.y * gridDim.z - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *smem_flag = last;
+  }
+  __syncthreads();
+  return *smem_flag != 0;
+}
+
+__device__ __forceinline__ void reset_counter(unsigned* counter) {
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Bijective XCD-aware remap of a linear block id (8 XCDs, round-robin dispatch):
+// consecutive logical tiles land on the same XCD (shared L2). Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int nx = 8;
+  if (nblocks < nx) return bid;
+  int q = nblocks / nx, r = nblocks % nx, x = bid % nx, k = bid / nx;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+}  // namespace rk

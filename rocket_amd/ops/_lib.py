@@ -1,0 +1,129 @@
+"""ctypes bindings of the in-tree native libraries.
+
+The HIP kernels are plain ``extern "C"`` entry points in
+``rocket_amd/_lib/librocket_kernels.so`` (built by :mod:`rocket_amd.native.build`).
+They receive raw device pointers and the *current* PyTorch HIP stream, so every
+launch is stream-ordered with PyTorch work and is captured by HIP graphs.
+
+``torch`` is imported first so its HIP runtime is the one our library binds to
+(both carry the ``libamdhip64.so.7`` SONAME).  On a machine with a GPU a
+missing or unloadable library is an error (:func:`require_native`), never a
+silent fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede loading the HIP library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(os.path.dirname(_HERE), "_lib")
+_lock = threading.Lock()
+_libs: dict = {}
+
+c_void_p, c_int, c_int64, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+
+# name -> (restype, argtypes)
+KERNEL_SIGS = {
+    "rk_ce_fwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "rk_ce_bwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int64, c_float, c_void_p, c_void_p, c_int, c_void_p]),
+    "rk_ce_partials_needed": (c_int, [c_int, c_int]),
+    "rk_optim_chunk": (c_int, []),
+    "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _load(name: str, sigs: dict, build_if_missing: bool = True):
+    with _lock:
+        if name in _libs:
+            return _libs[name]
+        path = os.path.join(LIBDIR, f"lib{name}.so")
+        if not os.path.exists(path) and build_if_missing:
+            from rocket_amd.native import build as _build
+
+            _build.build(verbose=False)
+        if not os.path.exists(path):
+            raise NativeError(f"{path} is missing; run `python -m rocket_amd.native.build`")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        for fn, (res, args) in sigs.items():
+            f = getattr(lib, fn, None)
+            if f is None:
+                continue
+            f.restype, f.argtypes = res, args
+        _libs[name] = lib
+        return lib
+
+
+def kernels():
+    return _load("rocket_kernels", KERNEL_SIGS)
+
+
+def available() -> bool:
+    try:
+        kernels()
+        return True
+    except Exception:
+        return False
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        raise NativeError(f"{what} failed with hipError {code}")
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float16:
+        return 2
+    raise NativeError(f"unsupported dtype {t.dtype}")
+
+
+class Workspace:
+    """Per-device scratch: zero-initialised ticket counters for in-launch grid reductions.
+
+    Kernels on one stream run in order and every last-arriving block resets its
+    counter to zero, so one counter per kernel family per device suffices.
+    """
+
+    _per_device: dict = {}
+
+    def __init__(self, device: torch.device):
+        self.counters = torch.zeros(256, dtype=torch.int32, device=device)
+        self._next = 0
+        self._named: dict = {}
+
+    @classmethod
+    def get(cls, device) -> "Workspace":
+        device = torch.device(device)
+        key = (device.type, device.index)
+        ws = cls._per_device.get(key)
+        if ws is None:
+            ws = cls._per_device[key] = Workspace(device)
+        return ws
+
+    def counter(self, name: str) -> int:
+        idx = self._named.get(name)
+        if idx is None:
+            idx = self._named[name] = self._next
+            self._next += 1
+            if self._next > self.counters.numel():
+                raise NativeError("workspace counters exhausted")
+        return self.counters.data_ptr() + 4 * idx

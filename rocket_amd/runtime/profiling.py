@@ -1,0 +1,125 @@
+"""Step timing and trace markers (SURVEY §5 "Tracing / profiling": absent in the reference).
+
+* :class:`StepTimer` — a capsule placed last in a Looper (priority 1).  It
+  records a HIP event at every iteration boundary (no host sync inside the
+  loop) and can bracket a measurement window with a barrier + device sync on
+  both sides, which is the protocol ``bench.py`` reports.  After the loop the
+  per-step device times give p50/p90 without perturbing the steady state.
+* :func:`range_push`/:func:`range_pop` — roctx ranges (``libroctx64``) around
+  step phases so ``rocprofv3 --marker-trace`` timelines are readable; no-ops
+  when the library is unavailable.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import statistics
+import time
+from typing import List, Optional
+
+import torch
+
+from rocket_amd.core.attributes import Attributes
+from rocket_amd.core.capsule import Capsule
+from rocket_amd.runtime import comm as _comm
+
+_roctx = None
+
+
+def _load_roctx():
+    global _roctx
+    if _roctx is None:
+        try:
+            _roctx = ctypes.CDLL("libroctx64.so")
+            _roctx.roctxRangePushA.argtypes = [ctypes.c_char_p]
+        except OSError:
+            _roctx = False
+    return _roctx
+
+
+def range_push(name: str) -> None:
+    lib = _load_roctx()
+    if lib:
+        lib.roctxRangePushA(name.encode())
+
+
+def range_pop() -> None:
+    lib = _load_roctx()
+    if lib:
+        lib.roctxRangePop()
+
+
+def sync_all(device: torch.device) -> None:
+    """Barrier over ranks with device idle on both sides."""
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    _comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+class StepTimer(Capsule):
+    """Measure a window of ``steps`` iterations after ``warmup`` iterations."""
+
+    def __init__(self, warmup: int = 0, steps: Optional[int] = None, priority: int = 1):
+        super().__init__(priority=priority)
+        self.warmup = warmup
+        self.steps = steps
+        self._i = 0
+        self._events: List = []
+        self._host: List[float] = []
+        self.t_start: Optional[float] = None
+        self.t_end: Optional[float] = None
+
+    def _mark(self) -> None:
+        dev = self._accelerator.device
+        if dev.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._events.append(ev)
+        self._host.append(time.perf_counter())
+
+    def set(self, attrs: Attributes | None = None) -> None:
+        if self.warmup == 0 and self.t_start is None:
+            self.start_now()
+
+    def launch(self, attrs: Attributes | None = None) -> None:
+        self._i += 1
+        dev = self._accelerator.device
+        if self._i == self.warmup:
+            sync_all(dev)
+            self.t_start = time.perf_counter()
+            self._mark()
+        elif self._i > self.warmup and (self.steps is None or self._i <= self.warmup + self.steps):
+            self._mark()
+            if self.steps is not None and self._i == self.warmup + self.steps:
+                sync_all(dev)
+                self.t_end = time.perf_counter()
+
+    def start_now(self) -> None:
+        """Start the window before the first iteration (warmup == 0)."""
+        sync_all(self._accelerator.device)
+        self.t_start = time.perf_counter()
+        self._mark()
+
+    @property
+    def elapsed(self) -> float:
+        return (self.t_end or time.perf_counter()) - (self.t_start or 0.0)
+
+    def step_times_ms(self) -> List[float]:
+        if self._events:
+            torch.cuda.synchronize()
+            return [a.elapsed_time(b) for a, b in zip(self._events[:-1], self._events[1:])]
+        return [(b - a) * 1e3 for a, b in zip(self._host[:-1], self._host[1:])]
+
+    def summary(self) -> dict:
+        t = self.step_times_ms()
+        if not t:
+            return {}
+        t_sorted = sorted(t)
+        return {
+            "step_ms_p50": statistics.median(t),
+            "step_ms_p90": t_sorted[min(len(t) - 1, int(0.9 * len(t)))],
+            "step_ms_min": t_sorted[0],
+            "step_ms_mean": sum(t) / len(t),
+        }

@@ -1,0 +1,94 @@
+"""Numerics of the fused cross-entropy and multi-tensor optimizer kernels vs PyTorch fp32 references."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("N,C", [(1024, 10), (37, 3), (256, 1000), (5, 64), (9, 65)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_cross_entropy_matches_torch(N, C, dtype, smoothing):
+    from rocket_amd.ops.cross_entropy import cross_entropy
+
+    torch.manual_seed(0)
+    x = (torch.randn(N, C, device="cuda") * 3).to(dtype).requires_grad_()
+    t = torch.randint(0, C, (N,), device="cuda")
+    t[::7] = -100
+    xr = x.detach().float().requires_grad_()
+    ref = F.cross_entropy(xr, t, label_smoothing=smoothing)
+    out = cross_entropy(x, t, label_smoothing=smoothing)
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    assert torch.allclose(out.float(), ref, atol=tol, rtol=tol), (out.item(), ref.item())
+    g = torch.tensor(0.37, device="cuda")
+    (out * g).backward()
+    (ref * g).backward()
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=1e-2)
+
+
+def test_cross_entropy_sum_and_graph_replay():
+    from rocket_amd.ops.cross_entropy import cross_entropy
+
+    x = torch.randn(300, 10, device="cuda")
+    t = torch.randint(0, 10, (300,), device="cuda")
+    assert torch.allclose(cross_entropy(x, t, reduction="sum"), F.cross_entropy(x, t, reduction="sum"), rtol=1e-5)
+    # the in-launch ticket counter must reset itself across repeated launches / replays
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            cross_entropy(x, t)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = cross_entropy(x, t)
+    for k in range(4):
+        x.copy_(torch.randn_like(x))
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.allclose(y, F.cross_entropy(x, t), rtol=1e-5, atol=1e-6)
+
+
+def _clone_params(ps):
+    return [torch.nn.Parameter(p.detach().clone()) for p in ps]
+
+
+@pytest.mark.parametrize("kind", ["adamw", "adam", "sgd", "sgd_nesterov"])
+def test_fused_optimizer_matches_torch(kind):
+    from rocket_amd.ops.optim import FusedAdam, FusedAdamW, FusedSGD
+
+    torch.manual_seed(0)
+    shapes = [(6, 1, 5, 5), (6,), (16, 6, 5, 5), (16,), (120, 400), (120,), (84, 120), (84,), (10, 84), (10,), (5000,)]
+    base = [torch.randn(s, device="cuda") for s in shapes]
+    a, b = _clone_params(base), _clone_params(base)
+    if kind == "adamw":
+        oa = FusedAdamW([{"params": a[:4], "lr": 3e-3}, {"params": a[4:], "weight_decay": 0.1}], lr=1e-3)
+        ob = torch.optim.AdamW([{"params": b[:4], "lr": 3e-3}, {"params": b[4:], "weight_decay": 0.1}], lr=1e-3)
+    elif kind == "adam":
+        oa = FusedAdam(a, lr=1e-3, weight_decay=0.01)
+        ob = torch.optim.Adam(b, lr=1e-3, weight_decay=0.01)
+    elif kind == "sgd":
+        oa = FusedSGD(a, lr=0.1, momentum=0.9, weight_decay=1e-4)
+        ob = torch.optim.SGD(b, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    else:
+        oa = FusedSGD(a, lr=0.1, momentum=0.9, nesterov=True)
+        ob = torch.optim.SGD(b, lr=0.1, momentum=0.9, nesterov=True)
+    for step in range(5):
+        for pa, pb in zip(a, b):
+            g = torch.randn_like(pa)
+            pa.grad = g.clone()
+            pb.grad = g.clone()
+        oa.step()
+        ob.step()
+        if step == 2:
+            for g in oa.param_groups + ob.param_groups:
+                g["lr"] *= 0.5
+    torch.cuda.synchronize()
+    for pa, pb in zip(a, b):
+        assert torch.allclose(pa, pb, atol=1e-5, rtol=1e-5), (pa - pb).abs().max()
+    sd = oa.state_dict()
+    if kind.startswith("adam"):
+        assert float(sd["state"][0]["step"]) == 5.0
+        assert torch.allclose(sd["state"][4]["exp_avg"], ob.state_dict()["state"][4]["exp_avg"], atol=1e-6)
