@@ -33,11 +33,11 @@ BASELINE_METRIC = "samples/sec (whole node) MNIST ConvNet at 1/2/4/8 MI355X; ste
 
 def _baseline_value(n_gpus: int):
     """Reference number to divide by: 1-GPU MI355X reference × N (ideal weak scaling)."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench", "reference_mi355x.json")
     try:
         with open(path) as fh:
             b = json.load(fh)
-        per_gpu = b.get("measured", {}).get("reference_mi355x_1gpu_bf16_samples_per_s")
+        per_gpu = b.get("reference_mi355x_1gpu_bf16_samples_per_s")
         if per_gpu:
             return float(per_gpu) * n_gpus
     except Exception:

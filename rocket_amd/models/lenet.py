@@ -6,12 +6,14 @@ takes the batch tuple ``(img, label)`` and returns ``(img, label, logits)`` —
 the reference's batch-in/batch-out contract.
 
 ``fused=True`` (default on a GPU) routes the layers through the hand-written
-CDNA4 kernels of :mod:`rocket_amd.ops`:
+CDNA4 kernels of :mod:`rocket_amd.ops.lenet`:
 
-* conv+bias+ReLU+maxpool fused forward, and a fused backward that scatters the
-  pooled gradient through the saved argmax/ReLU mask (SURVEY K1-K4, K9-K11);
-* MFMA bf16 linear layers with bias/ReLU epilogues and fused bias-gradient
-  column sums (K5, K8).
+* the whole feature extractor (both conv+bias+ReLU+maxpool stages) is one MFMA
+  implicit-GEMM launch forward and one backward that routes the pooled
+  gradient through saved 1-byte argmax/ReLU codes (SURVEY K1-K4, K9-K11);
+* the classifier (fc1-ReLU-fc2-ReLU-fc3) is one MFMA launch forward, one for
+  the input-gradient chain and three split-K weight-gradient GEMMs with fused
+  bias gradients (K5, K8).
 
 ``fused=False`` is the plain PyTorch module (CPU reference and numerics oracle);
 both share parameter names, so checkpoints are interchangeable.
@@ -45,15 +47,10 @@ class LeNet(nn.Module):
 
     def logits(self, x: torch.Tensor) -> torch.Tensor:
         if self.use_fused(x):
-            from rocket_amd.ops import conv as fconv
-            from rocket_amd.ops import linear as flin
+            from rocket_amd.ops.lenet import lenet_features, mlp_head
 
-            h = fconv.conv_bias_relu_pool(x, self.conv1.weight, self.conv1.bias, padding=2)
-            h = fconv.conv_bias_relu_pool(h, self.conv2.weight, self.conv2.bias, padding=0)
-            h = h.reshape(h.shape[0], -1)
-            h = flin.linear(h, self.fc1.weight, self.fc1.bias, activation="relu")
-            h = flin.linear(h, self.fc2.weight, self.fc2.bias, activation="relu")
-            return flin.linear(h, self.fc3.weight, self.fc3.bias, activation=None)
+            h = lenet_features(x, self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias)
+            return mlp_head(h, [self.fc1, self.fc2, self.fc3])
         x = F.max_pool2d(F.relu(self.conv1(x)), 2)
         x = F.max_pool2d(F.relu(self.conv2(x)), 2)
         x = torch.flatten(x, 1)

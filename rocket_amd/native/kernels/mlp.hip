@@ -1,0 +1,382 @@
+// Fused ReLU MLP head, 3 linear layers (LeNet classifier fc1-ReLU-fc2-ReLU-fc3: SURVEY K4/K5/K8/K9).
+//
+// Three launches per training step, all on v_mfma_f32_16x16x32_bf16 (f32 accumulate):
+//
+//  mlp3_fwd    A block owns 16 batch rows and runs the whole chain
+//              h1 = relu(x W1^T + b1), h2 = relu(h1 W2^T + b2), y = h2 W3^T + b3
+//              with activations resident in LDS (bf16).  Weights come straight from the
+//              fp32 master copy (L2-resident), every k-step's B fragment of a tile is
+//              prefetched before the first MFMA (one L2 latency per tile, not one per k-step).
+//              Side outputs for the backward are written TRANSPOSED (x^T, h1^T, h2^T:
+//              [features][batch]) so the weight-gradient GEMM reads K-contiguous rows.
+//  mlp3_dgrad  Same row blocking: d2 = (dy W3)[h2>0], d1 = (d2 W2)[h1>0], dx = d1 W1; writes
+//              dy^T, d2^T, d1^T for the weight gradients and dx (row-major) for the conv backward.
+//  mlp3_wgrad  All three dW_l += d_l^T-rows . x_l^T-rows (reduction over the batch) and the bias
+//              gradients (row sums of d_l^T) in ONE grouped launch: a block owns a 32x32 tile
+//              of one layer's dW, its 8 waves split the batch, partial tiles are reduced in LDS
+//              and added once — deterministic, no atomics.
+//
+// Everything is branch-free in the load paths (clamped addresses + selects).
+#include "rk_common.h"
+
+using namespace rk;
+
+namespace {
+
+constexpr int ROWS = 16;
+constexpr int MAXK = 512;
+constexpr int LDSW = MAXK + 8;
+constexpr int NW = 8;  // waves per block
+constexpr int NT = 64 * NW;
+
+// B fragment of a [N][K] fp32 row-major weight for output tile nt, k-step ks (forward: y = a W^T).
+// K % 4 == 0 (checked on the host): two 16-byte loads, each all-in or all-out of range.
+__device__ __forceinline__ bf16x8 wfrag_fwd(const float* W, int N, int K, int nt, int ks, int lane) {
+  const int n = nt * 16 + (lane & 15), k0 = ks * 32 + 8 * (lane >> 4);
+  const int nc = n < N ? n : N - 1;
+  const int ka = k0 < K ? k0 : K - 4, kb = k0 + 4 < K ? k0 + 4 : K - 4;
+  const float4 v0 = *(const float4*)(W + (int64_t)nc * K + ka);
+  const float4 v1 = *(const float4*)(W + (int64_t)nc * K + kb);
+  const bool oa = n < N && k0 < K, ob = n < N && k0 + 4 < K;
+  bf16x8 b;
+  b[0] = (__bf16)(oa ? v0.x : 0.f); b[1] = (__bf16)(oa ? v0.y : 0.f);
+  b[2] = (__bf16)(oa ? v0.z : 0.f); b[3] = (__bf16)(oa ? v0.w : 0.f);
+  b[4] = (__bf16)(ob ? v1.x : 0.f); b[5] = (__bf16)(ob ? v1.y : 0.f);
+  b[6] = (__bf16)(ob ? v1.z : 0.f); b[7] = (__bf16)(ob ? v1.w : 0.f);
+  return b;
+}
+
+// B fragment for the input gradient (dx = d W): B[k = n][col = c] = W[n][c].
+__device__ __forceinline__ bf16x8 wfrag_bwd(const float* W, int N, int K, int ct, int ks, int lane) {
+  const int c = ct * 16 + (lane & 15), n0 = ks * 32 + 8 * (lane >> 4);
+  const int cc = c < K ? c : K - 1;
+  bf16x8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = n0 + j;
+    const float v = W[(int64_t)(n < N ? n : N - 1) * K + cc];
+    b[j] = (__bf16)((c < K && n < N) ? v : 0.f);
+  }
+  return b;
+}
+
+__device__ __forceinline__ bf16x8 afrag(const uint16_t* act, int ks, int lane) {
+  return *(const bf16x8*)(act + (lane & 15) * LDSW + ks * 32 + 8 * (lane >> 4));
+}
+
+// out = act(in . W^T + b) for the block's 16 rows; KS = k-steps (compile time: prefetch depth)
+template <int KS>
+__device__ __forceinline__ void layer_fwd(const uint16_t* in, int K, const float* W, const float* b, int N, bool relu,
+                                          uint16_t* out, float* gout_f32, int64_t row0, int M) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ntiles = (N + 15) / 16;
+  for (int nt = wv; nt < ntiles; nt += NW) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (KS > 0) {
+      bf16x8 bf[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) bf[ks] = wfrag_fwd(W, N, K, nt, ks, lane);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(in, ks, lane), bf[ks], acc, 0, 0, 0);
+    } else {  // generic widths: prefetch 4 k-steps at a time
+      for (int k0 = 0; k0 < (K + 31) / 32; k0 += 4) {
+        bf16x8 bf[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bf[q] = wfrag_fwd(W, N, K, nt, k0 + q, lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (k0 + q < (K + 31) / 32)  // uniform; never read LDS columns past the staged width
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(in, k0 + q, lane), bf[q], acc, 0, 0, 0);
+      }
+    }
+    const int col = nt * 16 + (lane & 15);
+    const float bias = b[col < N ? col : 0];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * (lane >> 4) + i;
+      float v = acc[i] + bias;
+      if (relu) v = fmaxf(v, 0.f);
+      if (col < N) {
+        if (out) out[r * LDSW + col] = f2bf(v);
+        if (gout_f32 && row0 + r < M) gout_f32[(row0 + r) * N + col] = v;
+      }
+    }
+  }
+}
+
+// dgrad: out[16][K] = (in[16][N] . W[N][K]) * [maskT > 0]; maskT is [K][M] (transposed activation)
+template <int KS>
+__device__ __forceinline__ void layer_dgrad(const uint16_t* in, int N, const float* W, int K, const uint16_t* maskT,
+                                            uint16_t* out, uint16_t* gout_rows, int64_t row0, int M) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ctiles = (K + 15) / 16;
+  for (int ct = wv; ct < ctiles; ct += NW) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (KS > 0) {
+      bf16x8 bf[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) bf[ks] = wfrag_bwd(W, N, K, ct, ks, lane);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(in, ks, lane), bf[ks], acc, 0, 0, 0);
+    } else {
+      for (int k0 = 0; k0 < (N + 31) / 32; k0 += 4) {
+        bf16x8 bf[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bf[q] = wfrag_bwd(W, N, K, ct, k0 + q, lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (k0 + q < (N + 31) / 32)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(in, k0 + q, lane), bf[q], acc, 0, 0, 0);
+      }
+    }
+    const int col = ct * 16 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * (lane >> 4) + i;
+      const bool rin = row0 + r < M;
+      float v = acc[i];
+      if (maskT) {
+        const float mv = bf2f(maskT[(int64_t)(col < K ? col : 0) * M + (rin ? row0 + r : 0)]);
+        v = mv > 0.f ? v : 0.f;
+      }
+      if (col < K) {
+        if (out) out[r * LDSW + col] = f2bf(v);
+        if (gout_rows && rin) gout_rows[(row0 + r) * K + col] = f2bf(v);
+      }
+    }
+  }
+}
+
+__device__ void zero_pad(uint16_t* buf, int c0, int c1) {
+  for (int i = threadIdx.x; i < ROWS * (c1 - c0); i += blockDim.x) {
+    const int r = i / (c1 - c0), c = c0 + i % (c1 - c0);
+    buf[r * LDSW + c] = 0;
+  }
+}
+
+__device__ void stage_rows(uint16_t* dst, const void* src, int src_f32, int K, int64_t row0, int M) {
+  const int Kp = (K + 31) / 32 * 32;
+  for (int i = threadIdx.x; i < ROWS * Kp; i += blockDim.x) {
+    const int r = i / Kp, c = i % Kp;
+    const bool ok = c < K && row0 + r < M;
+    const int64_t o = ok ? (row0 + r) * K + c : 0;
+    const float v = src_f32 ? ((const float*)src)[o] : bf2f(((const uint16_t*)src)[o]);
+    dst[r * LDSW + c] = f2bf(ok ? v : 0.f);
+  }
+}
+
+// write the block's [16][C] LDS activation as columns of a transposed [C][M] global tensor
+__device__ void store_transposed(uint16_t* __restrict__ gT, const uint16_t* buf, int C, int64_t row0, int M) {
+  const bool full = row0 + ROWS <= M && (M & 7) == 0;
+  for (int i = threadIdx.x; i < C * 2; i += blockDim.x) {
+    const int c = i >> 1, h = i & 1;  // 8-row half h of column c
+    if (full) {
+      uint4 v;
+      uint32_t* w = (uint32_t*)&v;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[k] = (uint32_t)buf[(8 * h + 2 * k) * LDSW + c] | ((uint32_t)buf[(8 * h + 2 * k + 1) * LDSW + c] << 16);
+      *(uint4*)(gT + (int64_t)c * M + row0 + 8 * h) = v;
+    } else {
+      for (int k = 0; k < 8; ++k)
+        if (row0 + 8 * h + k < M) gT[(int64_t)c * M + row0 + 8 * h + k] = buf[(8 * h + k) * LDSW + c];
+    }
+  }
+}
+
+template <int KS1, int KS2, int KS3>
+__global__ void __launch_bounds__(NT) mlp3_fwd_kernel(const uint16_t* __restrict__ x, int K0, const float* w1,
+                                                      const float* b1, int N1, const float* w2, const float* b2, int N2,
+                                                      const float* w3, const float* b3, int N3, uint16_t* xT,
+                                                      uint16_t* h1T, uint16_t* h2T, float* y, int M) {
+  __shared__ __attribute__((aligned(16))) uint16_t buf0[ROWS * LDSW];
+  __shared__ __attribute__((aligned(16))) uint16_t buf1[ROWS * LDSW];
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+  stage_rows(buf0, x, 0, K0, row0, M);
+  zero_pad(buf1, N1, KS2 > 0 ? KS2 * 32 : (N1 + 31) / 32 * 32);
+  __syncthreads();
+  if (xT) store_transposed(xT, buf0, K0, row0, M);
+  layer_fwd<KS1>(buf0, K0, w1, b1, N1, true, buf1, nullptr, row0, M);
+  __syncthreads();
+  store_transposed(h1T, buf1, N1, row0, M);
+  zero_pad(buf0, N2, KS3 > 0 ? KS3 * 32 : (N2 + 31) / 32 * 32);
+  __syncthreads();
+  layer_fwd<KS2>(buf1, N1, w2, b2, N2, true, buf0, nullptr, row0, M);
+  __syncthreads();
+  store_transposed(h2T, buf0, N2, row0, M);
+  layer_fwd<KS3>(buf0, N2, w3, b3, N3, false, nullptr, y, row0, M);
+}
+
+template <int KS3, int KS2, int KS1>
+__global__ void __launch_bounds__(NT) mlp3_dgrad_kernel(const float* __restrict__ dy, int N3, const float* w3, int N2,
+                                                        const uint16_t* h2T, const float* w2, int N1,
+                                                        const uint16_t* h1T, const float* w1, int K0, uint16_t* dyT,
+                                                        uint16_t* d2T, uint16_t* d1T, uint16_t* dx, int M) {
+  __shared__ __attribute__((aligned(16))) uint16_t buf0[ROWS * LDSW];
+  __shared__ __attribute__((aligned(16))) uint16_t buf1[ROWS * LDSW];
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+  stage_rows(buf0, dy, 1, N3, row0, M);
+  zero_pad(buf1, N2, KS2 > 0 ? KS2 * 32 : (N2 + 31) / 32 * 32);
+  __syncthreads();
+  store_transposed(dyT, buf0, N3, row0, M);
+  layer_dgrad<KS3>(buf0, N3, w3, N2, h2T, buf1, nullptr, row0, M);
+  __syncthreads();
+  store_transposed(d2T, buf1, N2, row0, M);
+  zero_pad(buf0, N1, KS1 > 0 ? KS1 * 32 : (N1 + 31) / 32 * 32);
+  __syncthreads();
+  layer_dgrad<KS2>(buf1, N2, w2, N1, h1T, buf0, nullptr, row0, M);
+  __syncthreads();
+  store_transposed(d1T, buf0, N1, row0, M);
+  if (dx) layer_dgrad<KS1>(buf0, N1, w1, K0, nullptr, nullptr, dx, row0, M);
+}
+
+// ------------------------------------------------------------------ grouped weight gradient
+struct WgradProb {
+  const uint16_t* dT;  // [N][M]
+  const uint16_t* xT;  // [K][M]
+  float* dw;           // [N][K], accumulated
+  float* db;           // [N], accumulated (may be null)
+  int N, K, tiles_k, tile_begin;
+};
+struct WgradArgs {
+  WgradProb p[3];
+  int nprob, M;
+};
+
+// 8 consecutive batch elements m0.. of row r of a [R][M] bf16 tensor; zero when out of range
+// (M % 8 == 0, so a group is all-in or all-out).
+__device__ __forceinline__ bf16x8 rowfrag(const uint16_t* T, int R, int M, int r, int m0) {
+  const bool ok = r < R && m0 < M;
+  const uint4 v = *(const uint4*)(T + (int64_t)(r < R ? r : 0) * M + (ok ? m0 : 0));
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  return __builtin_bit_cast(bf16x8, ok ? v : z);
+}
+
+__global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
+  __shared__ float red[NW][32 * 32];
+  __shared__ float rsum[NW][32];
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < 3; ++i)
+    if (i < a.nprob && (int)blockIdx.x >= a.p[i].tile_begin) pi = i;
+  const WgradProb P = a.p[pi];
+  const int t = blockIdx.x - P.tile_begin;
+  const int n0 = (t / P.tiles_k) * 32, k0 = (t % P.tiles_k) * 32;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
+  const int per = ((a.M + NW * 64 - 1) / (NW * 64)) * 64;  // batch range per wave, multiple of 64
+  const int mb = wv * per, me = min(a.M, mb + per);
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rs[2] = {0.f, 0.f};
+  for (int m = mb; m < me; m += 64) {  // two k-steps per iteration, all loads issued first
+    bf16x8 af[2][2], bf[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int mk = m + 32 * s + 8 * hi;
+      const int mm = mk < me ? mk : a.M;  // a.M -> zero fragment
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[s][i] = rowfrag(P.dT, P.N, a.M, n0 + 16 * i + lo, mm);
+        bf[s][i] = rowfrag(P.xT, P.K, a.M, k0 + 16 * i + lo, mm);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rs[i] += (float)af[s][i][j];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bf[s][j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  // reduce the 8 waves' partial tiles in LDS; C element (row 16i + 4hi + r, col 16j + lo)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wv][(16 * i + 4 * hi + r) * 32 + 16 * j + lo] = acc[i][j][r];
+  // row sums of d^T (bias gradient): lanes lo, lo+16, lo+32, lo+48 hold parts of row 16i + lo
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rs[i] += __shfl_xor(rs[i], 16, 64);
+    rs[i] += __shfl_xor(rs[i], 32, 64);
+  }
+  if (hi == 0) {
+    rsum[wv][lo] = rs[0];
+    rsum[wv][16 + lo] = rs[1];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * 32; e += NT) {
+    const int r = e >> 5, c = e & 31;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][e];
+    if (n0 + r < P.N && k0 + c < P.K) P.dw[(int64_t)(n0 + r) * P.K + k0 + c] += v;
+  }
+  if (k0 == 0 && P.db && threadIdx.x < 32 && n0 + (int)threadIdx.x < P.N) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += rsum[w][threadIdx.x];
+    P.db[n0 + threadIdx.x] += v;
+  }
+}
+
+}  // namespace
+
+// K0, N1, N2 must be multiples of 4 (16-byte weight rows); widths <= 512.
+RK_API int rk_mlp3_fwd(const void* x, int K0, const float* w1, const float* b1, int N1, const float* w2,
+                       const float* b2, int N2, const float* w3, const float* b3, int N3, void* xT, void* h1T,
+                       void* h2T, float* y, int M, hipStream_t s) {
+  if (K0 > MAXK || N1 > MAXK || N2 > MAXK || N3 > MAXK) return (int)hipErrorInvalidValue;
+  if ((K0 & 3) || (N1 & 3) || (N2 & 3)) return (int)hipErrorInvalidValue;
+  const int grid = (M + ROWS - 1) / ROWS;
+  const int k1 = (K0 + 31) / 32, k2 = (N1 + 31) / 32, k3 = (N2 + 31) / 32;
+#define RK_F(A, B, C) mlp3_fwd_kernel<A, B, C><<<grid, NT, 0, s>>>((const uint16_t*)x, K0, w1, b1, N1, w2, b2, N2, w3, b3, N3, (uint16_t*)xT, (uint16_t*)h1T, (uint16_t*)h2T, y, M)
+  if (k1 == 13 && k2 == 4 && k3 == 3) RK_F(13, 4, 3);  // LeNet 400-120-84-10
+  else RK_F(0, 0, 0);
+#undef RK_F
+  return (int)hipGetLastError();
+}
+
+RK_API int rk_mlp3_dgrad(const float* dy, int N3, const float* w3, int N2, const void* h2T, const float* w2, int N1,
+                         const void* h1T, const float* w1, int K0, void* dyT, void* d2T, void* d1T, void* dx, int M,
+                         hipStream_t s) {
+  if (K0 > MAXK || N1 > MAXK || N2 > MAXK || N3 > MAXK) return (int)hipErrorInvalidValue;
+  const int grid = (M + ROWS - 1) / ROWS;
+  const int k3 = (N3 + 31) / 32, k2 = (N2 + 31) / 32, k1 = (N1 + 31) / 32;
+#define RK_D(A, B, C) mlp3_dgrad_kernel<A, B, C><<<grid, NT, 0, s>>>(dy, N3, w3, N2, (const uint16_t*)h2T, w2, N1, (const uint16_t*)h1T, w1, K0, (uint16_t*)dyT, (uint16_t*)d2T, (uint16_t*)d1T, (uint16_t*)dx, M)
+  if (k3 == 1 && k2 == 3 && k1 == 4) RK_D(1, 3, 4);
+  else RK_D(0, 0, 0);
+#undef RK_D
+  return (int)hipGetLastError();
+}
+
+// Grouped dW_l += dT_l . xT_l^T, db_l += rowsum(dT_l) for up to 3 layers. M % 8 == 0.
+RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT, float* const* dw, float* const* db,
+                         const int* Ns, const int* Ks, int M, hipStream_t s) {
+  if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
+  WgradArgs a;
+  a.nprob = nprob;
+  a.M = M;
+  int tiles = 0;
+  for (int i = 0; i < 3; ++i) {
+    const int j = i < nprob ? i : nprob - 1;
+    a.p[i].dT = (const uint16_t*)dT[j];
+    a.p[i].xT = (const uint16_t*)xT[j];
+    a.p[i].dw = dw[j];
+    a.p[i].db = db[j];
+    a.p[i].N = Ns[j];
+    a.p[i].K = Ks[j];
+    a.p[i].tiles_k = (Ks[j] + 31) / 32;
+    a.p[i].tile_begin = tiles;
+    if (i < nprob) tiles += ((Ns[j] + 31) / 32) * a.p[i].tiles_k;
+  }
+  mlp3_wgrad_kernel<<<tiles, NT, 0, s>>>(a);
+  return (int)hipGetLastError();
+}

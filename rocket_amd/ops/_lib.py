@@ -32,6 +32,19 @@ KERNEL_SIGS = {
     "rk_ce_bwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int64, c_float, c_void_p, c_void_p, c_int, c_void_p]),
     "rk_ce_partials_needed": (c_int, [c_int, c_int]),
     "rk_optim_chunk": (c_int, []),
+    "rk_gemm": (c_int, [c_void_p, c_int, c_int64, c_int, c_void_p, c_int, c_int64, c_int, c_void_p, c_int, c_int64,
+                        c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int,
+                        c_int, c_int, c_void_p]),
+    "rk_conv_pool_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 7 + [c_void_p]),
+    "rk_conv_pool_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
+    "rk_conv_pool_dgrad": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int] + [c_int] * 7 + [c_void_p]),
+    "rk_lenet_conv_fwd": (c_int, [c_void_p] * 9 + [c_int, c_void_p]),
+    "rk_lenet_conv_bwd": (c_int, [c_void_p] * 10 + [c_int, c_int, c_void_p]),
+    "rk_mlp3_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                            c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "rk_mlp3_dgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "rk_mlp3_wgrad": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 

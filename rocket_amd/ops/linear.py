@@ -1,0 +1,166 @@
+"""Fused linear layer on the MFMA GEMM kernel (``native/kernels/gemm.hip``).
+
+``linear(x, weight, bias, activation)`` = ``act(x @ weight.T + bias)`` with
+bf16 MFMA math and f32 accumulation.  ``weight``/``bias`` are the fp32 master
+parameters (converted while staging, so no per-step cast kernels).
+
+Backward (one launch each):
+
+* dgrad  ``dx = (dy ⊙ act'(·)) @ W``        — the activation mask is applied
+  while staging ``dy`` (no threshold_backward kernel);
+* wgrad  ``dW = (dy ⊙ act'(·))ᵀ @ x``       — split-K over the batch with f32
+  atomics when the tile grid is small, bias gradient fused as the row sums of
+  the staged ``dyᵀ`` tile.
+
+When a parameter owns a persistent gradient buffer (``param._rocket_direct_grad``,
+set by the engine for flat gradient buckets / graph capture) the kernels
+accumulate straight into ``param.grad`` and notify the data-parallel reducer;
+otherwise they return fresh gradient tensors to autograd.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from rocket_amd.ops import _lib
+
+_ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+
+
+def _direct(p: torch.Tensor | None) -> bool:
+    return p is not None and getattr(p, "_rocket_direct_grad", False) and p.grad is not None
+
+
+def _autocast_on() -> bool:
+    try:
+        return torch.is_autocast_enabled("cuda")
+    except TypeError:  # older signature
+        return torch.is_autocast_enabled()
+
+
+def grad_ready(p: torch.Tensor) -> None:
+    hook = getattr(p, "_rocket_grad_hook", None)
+    if hook is not None:
+        hook(p)
+
+
+def gemm(a, b, c, *, a_trans=False, b_trans=False, M, N, K, lda, ldb, ldc, mask=None, mask_mode=0, ld_mask=0,
+         bias=None, act=0, accumulate=False, c_pre=None, rowsum=None, splitk=1, cfg=0):
+    lib = _lib.kernels()
+    _lib.check(
+        lib.rk_gemm(a.data_ptr(), _lib.dtype_code(a), lda, int(a_trans), _lib.ptr(mask),
+                    _lib.dtype_code(mask) if mask is not None else 0, ld_mask, mask_mode, b.data_ptr(),
+                    _lib.dtype_code(b), ldb, int(b_trans), c.data_ptr(), _lib.dtype_code(c), ldc, _lib.ptr(c_pre),
+                    _lib.ptr(bias), act, int(accumulate), _lib.ptr(rowsum), M, N, K, splitk, cfg,
+                    _lib.stream_ptr(c.device)),
+        "rk_gemm",
+    )
+
+
+def _tiles(M, N, t):
+    return ((M + t - 1) // t) * ((N + t - 1) // t)
+
+
+def _cfg(M, N):
+    return 0 if _tiles(M, N, 64) >= 128 else 1
+
+
+def _splitk(M, N, K):
+    tiles = _tiles(M, N, 64)
+    if tiles >= 128 or K < 256:
+        return 1
+    return int(max(1, min(K // 128, (256 + tiles - 1) // tiles)))
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, act: int, out_dtype):
+        shape = x.shape
+        K = shape[-1]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        if x2.dtype not in (torch.float32, torch.bfloat16):
+            x2 = x2.float()
+        M, N = x2.shape[0], weight.shape[0]
+        w = weight if weight.is_contiguous() else weight.contiguous()
+        y = torch.empty(M, N, dtype=out_dtype, device=x.device)
+        pre = torch.empty_like(y) if act == 2 else None
+        gemm(x2, w, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, act=act, c_pre=pre, cfg=_cfg(M, N))
+        ctx.act = act
+        ctx.params = (weight, bias)
+        ctx.shape = shape
+        ctx.x_dtype = x2.dtype
+        mask = y if act == 1 else pre
+        ctx.save_for_backward(x2, w, bias if bias is not None else None, mask)
+        return y.reshape(*shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, bias, mask = ctx.saved_tensors
+        act = ctx.act
+        M, K = x2.shape
+        N = w.shape[0]
+        dy2 = dy.reshape(M, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        if dy2.dtype not in (torch.float32, torch.bfloat16):
+            dy2 = dy2.float()
+        mmode = act if mask is not None else 0
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, dtype=ctx.x_dtype, device=dy.device)
+            gemm(dy2, w, dx, b_trans=True, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, mask=mask, mask_mode=mmode, ld_mask=N,
+                 cfg=_cfg(M, K))
+            dx = dx.reshape(ctx.shape)
+        need_w = ctx.needs_input_grad[1]
+        need_b = bias is not None and ctx.needs_input_grad[2]
+        if need_w or need_b:
+            wparam = ctx.params
+            direct = _direct(wparam[0]) and (not need_b or _direct(wparam[1]))
+            sk = _splitk(N, K, M)
+            if direct:
+                wp, bp = wparam
+                gemm(dy2, x2, wp.grad, a_trans=True, b_trans=True, M=N, N=K, K=M, lda=N, ldb=K, ldc=K, mask=mask,
+                     mask_mode=mmode, ld_mask=N, accumulate=True, rowsum=bp.grad if need_b else None,
+                     splitk=sk, cfg=0)
+                grad_ready(wp)
+                if need_b:
+                    grad_ready(bp)
+            else:
+                dw = torch.zeros(N, K, dtype=torch.float32, device=dy.device) if sk > 1 else \
+                    torch.empty(N, K, dtype=torch.float32, device=dy.device)
+                db = torch.zeros(N, dtype=torch.float32, device=dy.device) if need_b else None
+                gemm(dy2, x2, dw, a_trans=True, b_trans=True, M=N, N=K, K=M, lda=N, ldb=K, ldc=K, mask=mask,
+                     mask_mode=mmode, ld_mask=N, accumulate=False, rowsum=db, splitk=sk, cfg=0)
+                dw = dw if need_w else None
+        return dx, dw, db, None, None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, activation: str | None = None,
+           out_dtype: torch.dtype | None = None) -> torch.Tensor:
+    act = _ACT[activation]
+    if x.device.type != "cuda":
+        y = F.linear(x, weight, bias)
+        if act == 1:
+            y = F.relu(y)
+        elif act == 2:
+            y = F.gelu(y)
+        return y
+    if out_dtype is None:
+        out_dtype = torch.bfloat16 if (_autocast_on() or x.dtype == torch.bfloat16) else torch.float32
+    if weight.dtype != torch.float32 and weight.dtype != torch.bfloat16:
+        weight = weight.float()
+    return _Linear.apply(x, weight, bias, act, out_dtype)
+
+
+class FusedLinear(torch.nn.Linear):
+    """``nn.Linear`` (same parameters / state_dict keys) with an optional fused activation."""
+
+    def __init__(self, in_features, out_features, bias=True, activation: str | None = None, device=None, dtype=None):
+        super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
+        self.activation = activation
+
+    def forward(self, x):
+        return linear(x, self.weight, self.bias, self.activation)

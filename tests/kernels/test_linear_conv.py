@@ -1,0 +1,121 @@
+"""Numerics of the MFMA linear and fused conv/ReLU/pool kernels vs PyTorch fp32 references."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("M,K,N", [(1024, 400, 120), (1024, 120, 84), (1024, 84, 10), (37, 19, 5), (300, 768, 512)])
+@pytest.mark.parametrize("act", [None, "relu", "gelu"])
+@pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16])
+def test_linear_fwd_bwd(M, K, N, act, xdtype):
+    from rocket_amd.ops.linear import linear
+
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda").to(xdtype).requires_grad_()
+    w = (torch.randn(N, K, device="cuda") / K**0.5).requires_grad_()
+    b = torch.randn(N, device="cuda").requires_grad_()
+    y = linear(x, w, b, activation=act, out_dtype=torch.float32)
+    # reference: same bf16-rounded operands, fp32 math
+    xr = _bf(x.detach()).requires_grad_()
+    wr = _bf(w.detach()).requires_grad_()
+    br = b.detach().clone().requires_grad_()
+    yr = F.linear(xr, wr, br)
+    if act == "relu":
+        yr = F.relu(yr)
+    elif act == "gelu":
+        yr = F.gelu(yr)
+    assert torch.allclose(y, yr, atol=2e-2, rtol=2e-2), (y - yr).abs().max()
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(_bf(g))
+    for a, r in ((x.grad.float(), xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert _rel(a, r) < 2e-2, _rel(a, r)
+
+
+@pytest.mark.parametrize("cfg", [(1, 6, 28, 5, 2), (6, 16, 14, 5, 0), (3, 8, 17, 3, 1)])
+@pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16])
+def test_conv_relu_pool(cfg, xdtype):
+    from rocket_amd.ops.conv import conv_bias_relu_pool
+
+    Ci, Co, H, K, P = cfg
+    torch.manual_seed(0)
+    N = 64
+    x = torch.randn(N, Ci, H, H, device="cuda").to(xdtype).requires_grad_()
+    w = (torch.randn(Co, Ci, K, K, device="cuda") / (Ci * K * K) ** 0.5).requires_grad_()
+    b = (torch.randn(Co, device="cuda") * 0.1).requires_grad_()
+    y = conv_bias_relu_pool(x, w, b, padding=P, out_dtype=torch.float32)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    br = b.detach().clone().requires_grad_()
+    yr = F.max_pool2d(F.relu(F.conv2d(xr, wr, br, padding=P)), 2)
+    assert torch.allclose(y, yr, atol=1e-4, rtol=1e-4), (y - yr).abs().max()
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    assert _rel(x.grad, xr.grad) < (5e-3 if xdtype == torch.bfloat16 else 1e-5)
+    assert _rel(w.grad, wr.grad) < 1e-5
+    assert _rel(b.grad, br.grad) < 1e-5
+
+
+def test_lenet_fused_matches_torch():
+    from rocket_amd.models import CrossEntropy, LeNet
+
+    torch.manual_seed(0)
+    ref = LeNet(fused=False).cuda()
+    fus = LeNet(fused=True).cuda()
+    fus.load_state_dict(ref.state_dict())
+    x = torch.rand(256, 1, 28, 28, device="cuda")
+    y = torch.randint(0, 10, (256,), device="cuda")
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lr = CrossEntropy(fused=False)(ref((x, y)))
+        lf = CrossEntropy(fused=True)(fus((x, y)))
+    assert abs(lr.item() - lf.item()) < 2e-2
+    lr.backward()
+    lf.backward()
+    for (n, a), b in zip(ref.named_parameters(), fus.parameters()):
+        rel = (a.grad - b.grad).norm() / (a.grad.norm() + 1e-12)
+        assert rel < 5e-2, (n, rel.item())
+
+
+def _ref_lenet(x, w1, b1, w2, b2, l1, l2, l3):
+    """fp32 math on bf16-rounded operands, activations rounded to bf16 between layers (the AMP contract)."""
+    h = F.max_pool2d(F.relu(F.conv2d(_bf(x), _bf(w1), b1, padding=2)), 2)
+    h = _bf(h)
+    h = F.max_pool2d(F.relu(F.conv2d(h, _bf(w2), b2)), 2)
+    a2 = _bf(h.flatten(1))
+    h1 = _bf(F.relu(F.linear(a2, _bf(l1.weight), l1.bias)))
+    h2 = _bf(F.relu(F.linear(h1, _bf(l2.weight), l2.bias)))
+    return a2, F.linear(h2, _bf(l3.weight), l3.bias)
+
+
+@pytest.mark.parametrize("N", [1024, 37])
+def test_lenet_fused_blocks(N):
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.lenet import lenet_features, mlp_head
+
+    torch.manual_seed(1)
+    net = LeNet(fused=False).cuda()
+    ref = LeNet(fused=False).cuda()
+    ref.load_state_dict(net.state_dict())
+    x = torch.rand(N, 1, 28, 28, device="cuda")
+    a2 = lenet_features(x, net.conv1.weight, net.conv1.bias, net.conv2.weight, net.conv2.bias)
+    y = mlp_head(a2, [net.fc1, net.fc2, net.fc3])
+    a2r, yr = _ref_lenet(x, ref.conv1.weight, ref.conv1.bias, ref.conv2.weight, ref.conv2.bias, ref.fc1, ref.fc2, ref.fc3)
+    assert _rel(a2, a2r) < 1e-2
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    for (name, p), pr in zip(net.named_parameters(), ref.parameters()):
+        assert _rel(p.grad, pr.grad) < 3e-2, (name, _rel(p.grad, pr.grad))
