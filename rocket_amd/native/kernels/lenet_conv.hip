@@ -48,12 +48,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 constexpr int SPB = 4;               // samples per block
 constexpr int WPS = 4;               // waves per sample
 constexpr int NTHR = 64 * SPB * WPS; // 1024
-constexpr int IMGZ = PADI * PADI;    // zero slot index in img
+constexpr int IMGS = PADI + 1;       // LDS row stride of the padded image (33: breaks bank aliasing)
+constexpr int IMGN = PADI * IMGS;    // 1056
+constexpr int IMGZ = IMGN;           // zero slot index in img
 
 // padded-image offset of conv1 output position (window w of the 14x14 pool grid, quadrant q)
 __device__ __forceinline__ int pos1(int w, int q) {
   const int wr = w / Q1, wc = w - wr * Q1;
-  return (2 * wr + (q >> 1)) * PADI + 2 * wc + (q & 1);
+  return (2 * wr + (q >> 1)) * IMGS + 2 * wc + (q & 1);
 }
 // a1 offset of conv2 output position (window w of the 5x5 pool grid, quadrant q)
 __device__ __forceinline__ int pos2(int w, int q) {
@@ -62,8 +64,11 @@ __device__ __forceinline__ int pos2(int w, int q) {
 }
 
 // ------------------------------------------------------------------------------ forward
+constexpr int A1CL = Q1 * Q1 * 8;  // channel-last conv1 output: [pixel][8 channels], 6 used
+
 struct FwdSmem {
-  float img[SPB][PADI * PADI + 4];
+  float img[SPB][IMGN + 4];
+  uint16_t a1cl[SPB][A1CL + 16];  // zero pixel at A1CL (8 zeros), trash lanes at A1CL+8
   uint16_t a1[SPB][A1N + 8];  // zero slot at A1N, trash at A1N+4
   uint8_t c1[SPB][A1N + 8];
   uint16_t a2[SPB][A2N + 8];  // trash at A2N
@@ -85,13 +90,14 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
   uint16_t* a1 = sm.a1[slot];
   uint8_t* c1 = sm.c1[slot];
 
-  for (int i = st; i < PADI * PADI + 4; i += 64 * WPS) {
-    const int r = (i >> 5) - 2, c = (i & 31) - 2;
-    const bool in = i < PADI * PADI && r >= 0 && r < IMG && c >= 0 && c < IMG;
+  for (int i = st; i < IMGN + 4; i += 64 * WPS) {
+    const int r = i / IMGS - 2, c = i % IMGS - 2;
+    const bool in = i < IMGN && r >= 0 && r < IMG && c >= 0 && c < IMG;
     const float v = x[(int64_t)nc * IMG * IMG + (in ? r * IMG + c : 0)];
     img[i] = in ? v : 0.f;
   }
   if (st < 8) a1[A1N + st] = 0;
+  if (st < 16) sm.a1cl[slot][A1CL + st] = 0;
   const int hi = lane >> 4, lo = lane & 15;
   bf16x8 bw1;
   int koff1[8];
@@ -101,7 +107,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     const bool ok = lo < C1 && r < R1;
     const float v = w1[ok ? lo * R1 + r : 0];
     bw1[j] = tobf(ok ? v : 0.f);
-    koff1[j] = r < R1 ? (r / KS) * PADI + (r % KS) : -100000;
+    koff1[j] = r < R1 ? (r / KS) * IMGS + (r % KS) : -100000;
   }
   const float bias1 = b1[lo < C1 ? lo : 0];
   __syncthreads();
@@ -125,20 +131,23 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     m += bias1;
     const bool on = m > 0.f;
     const int o = lo < C1 ? lo * (Q1 * Q1) + 4 * t + hi : A1N + 4;
-    a1[o] = f2bf(on ? m : 0.f);
+    const uint16_t v = f2bf(on ? m : 0.f);
+    a1[o] = v;
     c1[o] = on ? (uint8_t)arg : 0xFF;
+    sm.a1cl[slot][lo < 8 ? (4 * t + hi) * 8 + lo : A1CL + 8] = lo < C1 ? v : (uint16_t)0;
   }
-  // conv2 operands (loaded here so their latency overlaps the barrier)
-  bf16x8 bw2[5];
-  int koff2[5][8];
+  // conv2 operands, reduction ordered k = (kh*5 + kw)*8 + ci (ci padded 6 -> 8): a lane's 8
+  // consecutive k are the 8 channels of one pixel of the channel-last image = ONE 16-byte read.
+  // 200 -> 7 k-steps; lane (hi) covers (kh,kw) pair kk = 4s + hi.
+  bf16x8 bw2[7];
 #pragma unroll
-  for (int s = 0; s < 5; ++s)
+  for (int s = 0; s < 7; ++s)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int r = 32 * s + 8 * hi + j;
-      const float v = w2[lo * R2 + (r < R2 ? r : 0)];
-      bw2[s][j] = tobf(r < R2 ? v : 0.f);
-      koff2[s][j] = r < R2 ? (r / R1) * (Q1 * Q1) + ((r / KS) % KS) * Q1 + (r % KS) : -100000;
+      const int kk = 4 * s + hi;
+      const bool ok = kk < R1 && j < C1;
+      const float v = w2[ok ? (lo * C1 + j) * R1 + kk : 0];
+      bw2[s][j] = tobf(ok ? v : 0.f);
     }
   const float bias2 = b2[lo];
   __syncthreads();
@@ -153,16 +162,14 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
   for (int t = sw; t < 7; t += WPS) {
     const int w = 4 * t + (lo >> 2);
     const bool wvalid = w < Q2 * Q2;
-    const int pos = pos2(wvalid ? w : 0, lo & 3);
+    const int pos = pos2(wvalid ? w : 0, lo & 3);  // conv2 output position = pixel of a1
+    const uint16_t* acl = sm.a1cl[slot];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 5; ++s) {
-      bf16x8 a;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int ko = koff2[s][j];
-        a[j] = __builtin_bit_cast(__bf16, a1[(wvalid && ko >= 0) ? pos + ko : A1N]);
-      }
+    for (int s = 0; s < 7; ++s) {
+      const int kk = 4 * s + hi;
+      const int px = (wvalid && kk < R1) ? pos + (kk / KS) * Q1 + (kk % KS) : Q1 * Q1;  // Q1*Q1 -> zero pixel
+      const bf16x8 a = *(const bf16x8*)(acl + px * 8);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[s], acc, 0, 0, 0);
     }
     const int wq = 4 * t + hi;
@@ -190,18 +197,30 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
 }
 
 // ------------------------------------------------------------------------------ backward
+// Output-owned decomposition (no LDS float atomics on shared addresses):
+//  phase A  stage 4 samples; expand the pooled conv2 gradient into a dense, zero-ringed
+//           dConv2 image [16][18][18] (bf16) through the argmax/ReLU codes
+//  phase B  conv2 dgrad as a GATHER implicit GEMM: dX2[pixel][ci] = sum_{co,kh,kw}
+//           dConv2[co][ih+4-kh][iw+4-kw] . W2[co][ci][kh][kw]  (13 pixel tiles x 13 k-steps per
+//           sample, all 16 waves); every output element is written by exactly one lane
+//  phase C  waves 0..9: one 16-column tile of dW2 each, reducing over the 4 samples' positions
+//           in registers; waves 10..15: dW1 (2 column tiles) over a share of the 4 x 784 positions
+//  phase D  block totals -> global f32 atomics (one per element per block)
+constexpr int DC = 18;             // dConv2 image side: 10 + 2*4 zero ring
+constexpr int DCN = DC * DC * C2;  // 5184, channel-last [y][x][co]; zero pixel at DCN
+constexpr int DTS = 128;           // row stride of dConv2^T [co][position] (100 used, zero padded)
+constexpr int K2P = 13;            // conv2-dgrad k-steps: (kh,kw,co) = 400 -> 416
+
 struct BwdSmem {
-  float img[SPB][PADI * PADI + 4];  // + zero slot
-  float dx2[SPB][A1N + 4];          // dL/d a1 (conv2 input gradient) + trash slot at A1N
+  float img[SPB][IMGN + 4];  // + zero slot
+  float dx2[SPB][A1N + 4];          // dL/d a1 (conv2 input gradient)
   uint16_t a1[SPB][A1N + 8];        // + zero slot at A1N
   uint8_t c1[SPB][A1N + 8];         // + never-matching slot at A1N
-  uint16_t da2[SPB][A2N + 8];
-  uint8_t c2[SPB][A2N + 8];
-  float gw2[C2 * R2 + 4];           // block-level weight-gradient accumulators (LDS atomics) + trash
-  float gw1[C1 * R1 + 4];
-  float gb2[C2];
-  float gb1[C1 + 2];
-  bf16x4 wfr[10 * 64];
+  uint16_t dc2[SPB][DCN + 16];      // dense channel-last dConv2 with zero ring; zero pixel at DCN
+  uint16_t dcT[SPB][C2 * DTS];      // dConv2^T [co][p = 4*window + quadrant] (wgrad2 A operand)
+  float red1[6][2][256];            // dW1 partials of waves 10..15
+  float rb1[6][16];
+  bf16x8 wfr[K2P * 64];             // conv2-dgrad B fragments
 };
 
 __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__ x, const uint16_t* __restrict__ a1g,
@@ -213,186 +232,204 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
                                                        float* __restrict__ db2, int N, int rounds) {
   __shared__ __attribute__((aligned(16))) BwdSmem sm;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int slot = wave / WPS, sw = wave % WPS, st = threadIdx.x % (64 * WPS);
   const int hi = lane >> 4, lo = lane & 15;
-  float* img = sm.img[slot];
-  float* dx2 = sm.dx2[slot];
-  uint16_t* a1 = sm.a1[slot];
-  uint8_t* c1 = sm.c1[slot];
-  uint16_t* da2 = sm.da2[slot];
-  uint8_t* c2 = sm.c2[slot];
 
-  for (int i = threadIdx.x; i < C2 * R2; i += NTHR) sm.gw2[i] = 0.f;
-  for (int i = threadIdx.x; i < C1 * R1; i += NTHR) sm.gw1[i] = 0.f;
-  if (threadIdx.x < C2) sm.gb2[threadIdx.x] = 0.f;
-  if (threadIdx.x < C1) sm.gb1[threadIdx.x] = 0.f;
-  if (st < 4) {
-    img[PADI * PADI + st] = 0.f;
-    a1[A1N + st] = 0;
-    c1[A1N + st] = 0xFE;
-    da2[A2N + st] = 0;
-    c2[A2N + st] = 0xFE;
-  }
-
-  // conv2 dgrad operand B[k=co][col=r] = w2[co][r] (10 column tiles of 16, K = co = 16) kept in
-  // LDS as bf16 in MFMA-fragment order: wfr[u][lane] = 4 consecutive co for column 16u + (lane&15)
-  for (int i = threadIdx.x; i < 10 * 64; i += NTHR) {
-    const int u = i >> 6, l = i & 63, r = 16 * u + (l & 15);
-    bf16x4 v;
+  // conv2-dgrad reduction index ordered k = (kh*5 + kw)*16 + co (co fastest), so a lane's 8
+  // consecutive k share (kh, kw) and step co by 1: gather offsets are base + j*DC*DC.
+  // B operand B[k][col = ci] = w2[co][ci][kh][kw]: 13 k-steps, lanes lo < 6.
+  // kept in LDS in fragment order (wfr[s*64 + lane]), one ds_read_b128 per k-step
+  for (int i = threadIdx.x; i < K2P * 64; i += NTHR) {
+    const int s = i >> 6, l = i & 63, h = l >> 4, c = l & 15;
+    bf16x8 v;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float f = w2[(4 * (l >> 4) + j) * R2 + (r < R2 ? r : 0)];
-      v[j] = tobf(r < R2 ? f : 0.f);
+    for (int j = 0; j < 8; ++j) {
+      const int kk = 2 * s + (h >> 1), co = 8 * (h & 1) + j;
+      const bool ok = kk < R1 && c < C1;
+      const float f = w2[ok ? (co * C1 + c) * R1 + kk : 0];
+      v[j] = tobf(ok ? f : 0.f);
     }
     sm.wfr[i] = v;
   }
-  auto cofs_of = [&](int u) {
-    const int r = 16 * u + lo;
-    return r < R2 ? (r / R1) * (Q1 * Q1) + ((r / KS) % KS) * Q1 + (r % KS) : -100000;
-  };
-  int cw1[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int r = 16 * u + lo;
-    cw1[u] = r < R1 ? (r / KS) * PADI + (r % KS) : -100000;
-  }
-  float sb2 = 0.f, sb1 = 0.f;
+
+  float accb2 = 0.f;                       // waves 0..9: db2 partial (lane lo = co)
+  f32x4 g2 = {0.f, 0.f, 0.f, 0.f};         // waves 0..9: dW2 tile u = wave
+  f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float sb1 = 0.f;
 
   for (int rd = 0; rd < rounds; ++rd) {
-    const int n = (blockIdx.x * rounds + rd) * SPB + slot;
-    const bool live = n < N;
-    const int nc = live ? n : 0;
-    __syncthreads();  // previous round's readers are done with the staging buffers
-    // ---- stage (dead samples stage zero gradients: every wave runs the same barriers)
-    for (int i = st; i < PADI * PADI; i += 64 * WPS) {
-      const int r = (i >> 5) - 2, c = (i & 31) - 2;
-      const bool in = r >= 0 && r < IMG && c >= 0 && c < IMG;
-      const float v = x[(int64_t)nc * IMG * IMG + (in ? r * IMG + c : 0)];
-      img[i] = in ? v : 0.f;
+    const int nbase = (blockIdx.x * rounds + rd) * SPB;
+    __syncthreads();
+    // ---- phase A: stage
+    for (int i = threadIdx.x; i < SPB * IMGN; i += NTHR) {
+      const int sl = i / IMGN, e = i % IMGN;
+      const int n = nbase + sl;
+      const int r = e / IMGS - 2, c = e % IMGS - 2;
+      const bool in = n < N && r >= 0 && r < IMG && c >= 0 && c < IMG;
+      const float v = x[(int64_t)(n < N ? n : 0) * IMG * IMG + (in ? r * IMG + c : 0)];
+      sm.img[sl][e] = in ? v : 0.f;
     }
-    for (int i = st * 8; i < A1N; i += 64 * WPS * 8) {
-      *(uint4*)(a1 + i) = *(const uint4*)(a1g + (int64_t)nc * A1N + i);
-      *(uint2*)(c1 + i) = *(const uint2*)(code1g + (int64_t)nc * A1N + i);
+    for (int i = threadIdx.x; i < SPB * (A1N / 8); i += NTHR) {
+      const int sl = i / (A1N / 8), e = (i % (A1N / 8)) * 8;
+      const int n = nbase + sl, nc = n < N ? n : 0;
+      *(uint4*)(sm.a1[sl] + e) = *(const uint4*)(a1g + (int64_t)nc * A1N + e);
+      *(uint2*)(sm.c1[sl] + e) = *(const uint2*)(code1g + (int64_t)nc * A1N + e);
     }
-    for (int i = st; i < A1N + 4; i += 64 * WPS) dx2[i] = 0.f;
-    for (int i = st * 8; i < A2N; i += 64 * WPS * 8) {
-      uint4 d = *(const uint4*)(da2g + (int64_t)nc * A2N + i);
-      if (!live) d = make_uint4(0, 0, 0, 0);
-      *(uint4*)(da2 + i) = d;
-      *(uint2*)(c2 + i) = *(const uint2*)(code2g + (int64_t)nc * A2N + i);
+    for (int i = threadIdx.x; i < SPB * (DCN + 16) / 8; i += NTHR) {  // zero dc2 (16-byte stores)
+      const int sl = i / ((DCN + 16) / 8), e = (i % ((DCN + 16) / 8)) * 8;
+      *(uint4*)(sm.dc2[sl] + e) = make_uint4(0, 0, 0, 0);
+    }
+    for (int i = threadIdx.x; i < SPB * C2 * DTS / 8; i += NTHR) {
+      const int sl = i / (C2 * DTS / 8), e = (i % (C2 * DTS / 8)) * 8;
+      *(uint4*)(sm.dcT[sl] + e) = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SPB * A2N; i += NTHR) {  // scatter the pooled gradients
+      const int sl = i / A2N, e = i % A2N, co = e / 25, w = e % 25;
+      const int n = nbase + sl, nc = n < N ? n : 0;
+      const uint16_t g = da2g[(int64_t)nc * A2N + e];
+      const uint8_t cd = code2g[(int64_t)nc * A2N + e];
+      if (n < N && cd < 4) {
+        const int rr = 2 * (w / Q2) + (cd >> 1), cc = 2 * (w % Q2) + (cd & 1);
+        sm.dc2[sl][((rr + 4) * DC + cc + 4) * C2 + co] = g;
+        sm.dcT[sl][co * DTS + 4 * w + cd] = g;
+      }
+    }
+    if (threadIdx.x < SPB * 8) {
+      const int sl = threadIdx.x >> 3, k = threadIdx.x & 7;
+      sm.a1[sl][A1N + k] = 0;
+      sm.c1[sl][A1N + k] = 0xFE;
+      if (k < 4) sm.img[sl][IMGN + k] = 0.f;
     }
     __syncthreads();
 
-    // ---- conv2 dgrad: tiles t of 16 positions (4 windows); A[pos][co] = dConv2 (K = co = 16)
-    for (int t = sw; t < 7; t += WPS) {
-      const int w = 4 * t + (lo >> 2), q = lo & 3;
-      const int wcl = w < Q2 * Q2 ? w : -1;
-      bf16x4 a;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int idx = wcl >= 0 ? (4 * hi + j) * 25 + wcl : A2N;
-        const float v = bf2f(da2[idx]);
-        a[j] = tobf(c2[idx] == q ? v : 0.f);
+    // ---- phase B: conv2 dgrad, 4 samples x 13 pixel tiles, round-robin over the 16 waves
+    for (int tt = wave; tt < SPB * 13; tt += 16) {
+      const int sl = tt / 13, t = tt % 13;
+      const int pix = 16 * t + lo;  // A row of this lane
+      const bool pv = pix < Q1 * Q1;
+      const int ih = pv ? pix / Q1 : 0, iw = pv ? pix % Q1 : 0;
+      const int base = ih * DC + iw;  // pixel (ih, iw) reads dConv2 pixel (ih + 4 - kh, iw + 4 - kw)
+      const uint16_t* dc = sm.dc2[sl];
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int s = 0; s < K2P; ++s) {
+        const int kk = 2 * s + (hi >> 1);  // (kh, kw) pair of this lane's 8 k values (8 channels)
+        const bool ok = pv && kk < R1;
+        const int px = ok ? base + (4 - kk / KS) * DC + (4 - kk % KS) : DC * DC;  // DC*DC -> zero pixel
+        const bf16x8 a = *(const bf16x8*)(dc + px * C2 + 8 * (hi & 1));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, sm.wfr[s * 64 + lane], acc, 0, 0, 0);
       }
-      const int wq = 4 * t + hi;
-      const bool qvalid = wq < Q2 * Q2;
-      const int base = pos2(qvalid ? wq : 0, 0);
-#pragma unroll 2
-      for (int u = 0; u < 10; ++u) {
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
-        c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, sm.wfr[u * 64 + lane], c, 0, 0, 0);
-        const int co = cofs_of(u);
-        const bool ok = qvalid && co >= 0;
+      // C[row = pixel 16t + 4hi + i][col = ci = lo]
+      if (lo < C1) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          atomicAdd(&dx2[ok ? base + (i >> 1) * Q1 + (i & 1) + co : A1N], c[i]);
-      }
-    }
-    // ---- conv2 wgrad, k-step ks = sw (positions 32ks..32ks+31 = windows 8ks..8ks+7)
-    {
-      const int ks = sw;
-      // this lane's 8 positions are windows wa = 8ks+2hi (j<4) and wa+1 (j>=4), quadrant j&3
-      const int wa = 8 * ks + 2 * hi, wb = wa + 1;
-      const bool va = wa < Q2 * Q2, vb = wb < Q2 * Q2;
-      const int ia = va ? lo * 25 + wa : A2N, ib = vb ? lo * 25 + wb : A2N;
-      const float da = bf2f(da2[ia]), db = bf2f(da2[ib]);
-      const uint8_t ca = c2[ia], cb = c2[ib];
-      const int pa = va ? pos2(wa, 0) : -100000, pb = vb ? pos2(wb, 0) : -100000;
-      bf16x8 a;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float v = j < 4 ? (ca == (j & 3) ? da : 0.f) : (cb == (j & 3) ? db : 0.f);
-        a[j] = tobf(v);
-        sb2 += v;
-      }
-#pragma unroll 2
-      for (int u = 0; u < 10; ++u) {
-        bf16x8 b;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int ofs = (j < 4 ? pa : pb) + ((j & 3) >> 1) * Q1 + (j & 1) + cofs_of(u);
-          b[j] = __builtin_bit_cast(__bf16, a1[ofs >= 0 ? ofs : A1N]);
+        for (int i = 0; i < 4; ++i) {
+          const int p = 16 * t + 4 * hi + i;
+          if (p < Q1 * Q1) sm.dx2[sl][lo * (Q1 * Q1) + p] = acc[i];
         }
-        f32x4 g = {0.f, 0.f, 0.f, 0.f};
-        g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, g, 0, 0, 0);
-        const int col = 16 * u + lo;  // C rows = co (4hi+i), cols r = 16u + lo
-#pragma unroll
-        for (int i = 0; i < 4; ++i) atomicAdd(&sm.gw2[col < R2 ? (4 * hi + i) * R2 + col : C2 * R2], g[i]);
       }
     }
-    __syncthreads();  // all dX2 atomics of this sample are complete
-    // ---- conv1 wgrad: k-steps ks = sw, sw+4, ... (windows 8ks..8ks+7 of 196)
-    f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    for (int ks = sw; ks < 25; ks += WPS) {
-      const int wa = 8 * ks + 2 * hi, wb = wa + 1;
-      const bool va = lo < C1 && wa < Q1 * Q1, vb = lo < C1 && wb < Q1 * Q1;
-      const int ia = va ? lo * 196 + wa : A1N, ib = vb ? lo * 196 + wb : A1N;
-      const float da = dx2[ia], db = dx2[ib];
-      const uint8_t ca = c1[ia], cb = c1[ib];
-      const int pa = wa < Q1 * Q1 ? pos1(wa, 0) : -100000, pb = wb < Q1 * Q1 ? pos1(wb, 0) : -100000;
-      bf16x8 a;
+    __syncthreads();
+
+    // ---- phase C
+    if (wave < 10) {
+      // dW2 tile u = wave: rows co (16), cols r = 16u + lo; K = positions of 4 samples (4 x 4 k-steps)
+      const int u = wave;
+      const int r = 16 * u + lo;
+      const int cof = r < R2 ? (r / R1) * (Q1 * Q1) + ((r / KS) % KS) * Q1 + (r % KS) : -100000;
+      for (int sl = 0; sl < SPB; ++sl) {
+        const uint16_t* a1s = sm.a1[sl];
+#pragma unroll 2
+        for (int ks = 0; ks < 4; ++ks) {
+          // positions p = 32ks + 8hi + j, window-major: windows wa = 8ks+2hi (j<4), wa+1 (j>=4)
+          const bf16x8 a = *(const bf16x8*)(sm.dcT[sl] + lo * DTS + 32 * ks + 8 * hi);  // A[co=lo][p]
+          const int wa = 8 * ks + 2 * hi, wb = wa + 1;
+          const int pa = wa < Q2 * Q2 && cof >= 0 ? pos2(wa, 0) + cof : -100000;
+          const int pb = wb < Q2 * Q2 && cof >= 0 ? pos2(wb, 0) + cof : -100000;
+          bf16x8 b;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float v = j < 4 ? (ca == (j & 3) ? da : 0.f) : (cb == (j & 3) ? db : 0.f);
-        a[j] = tobf(v);
-        sb1 += v;
+          for (int j = 0; j < 8; ++j) {
+            accb2 += (float)a[j];
+            const int ofs = (j < 4 ? pa : pb) + ((j & 3) >> 1) * Q1 + (j & 1);
+            b[j] = __builtin_bit_cast(__bf16, a1s[ofs >= 0 ? ofs : A1N]);  // B[k = p][col = r]
+          }
+          g2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, g2, 0, 0, 0);
+        }
       }
+    } else {
+      // dW1: 6 waves split the 4 x 25 k-steps (positions of the 14x14 pool grid)
+      const int wi = wave - 10;
+      int cw[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        bf16x8 b;
+        const int r = 16 * u + lo;
+        cw[u] = r < R1 ? (r / KS) * IMGS + (r % KS) : -100000;
+      }
+      for (int it = wi; it < SPB * 25; it += 6) {
+        const int sl = it / 25, ks = it % 25;
+        const int wa = 8 * ks + 2 * hi, wb = wa + 1;  // this lane's 2 windows (j<4 / j>=4)
+        const bool va = lo < C1 && wa < Q1 * Q1, vb = lo < C1 && wb < Q1 * Q1;
+        const int ia = va ? lo * 196 + wa : A1N, ib = vb ? lo * 196 + wb : A1N;
+        const float da = sm.dx2[sl][va ? ia : 0], dbv = sm.dx2[sl][vb ? ib : 0];
+        const uint8_t ca = sm.c1[sl][ia], cb = sm.c1[sl][ib];
+        const int pa = wa < Q1 * Q1 ? pos1(wa, 0) : -100000, pb = wb < Q1 * Q1 ? pos1(wb, 0) : -100000;
+        bf16x8 a;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int ofs = (j < 4 ? pa : pb) + ((j & 3) >> 1) * PADI + (j & 1) + cw1[u];
-          b[j] = tobf(img[ofs >= 0 ? ofs : IMGZ]);
+          const float v = j < 4 ? (ca == (j & 3) ? da : 0.f) : (cb == (j & 3) ? dbv : 0.f);
+          a[j] = tobf(v);
+          sb1 += v;
         }
-        g1[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, g1[u], 0, 0, 0);
-      }
-    }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int col = 16 * u + lo;
+        for (int u = 0; u < 2; ++u) {
+          bf16x8 b;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool ok = col < R1 && 4 * hi + i < C1;
-        atomicAdd(&sm.gw1[ok ? (4 * hi + i) * R1 + col : C1 * R1], g1[u][i]);
+          for (int j = 0; j < 8; ++j) {
+            const int ofs = (j < 4 ? pa : pb) + ((j & 3) >> 1) * IMGS + (j & 1) + cw[u];
+            b[j] = tobf(sm.img[sl][ofs >= 0 ? ofs : IMGZ]);
+          }
+          g1[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, g1[u], 0, 0, 0);
+        }
       }
     }
   }
 
-  // ---- block reduction in LDS (f32 atomics), then one global atomic per element
-  sb2 += __shfl_xor(sb2, 16, 64);
-  sb2 += __shfl_xor(sb2, 32, 64);
-  sb1 += __shfl_xor(sb1, 16, 64);
-  sb1 += __shfl_xor(sb1, 32, 64);
-  if (hi == 0) {
-    atomicAdd(&sm.gb2[lo], sb2);
-    if (lo < C1) atomicAdd(&sm.gb1[lo], sb1);
+  // ---- phase D: block totals -> global atomics
+  if (wave < 10) {
+    const int u = wave, col = 16 * u + lo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (col < R2) atomicAdd(dw2 + (4 * hi + i) * R2 + col, g2[i]);
+    if (u == 0) {  // db2[co]: lanes lo, lo+16, lo+32, lo+48 hold parts of channel lo
+      accb2 += __shfl_xor(accb2, 16, 64);
+      accb2 += __shfl_xor(accb2, 32, 64);
+      if (hi == 0 && db2) atomicAdd(db2 + lo, accb2);
+    }
+  } else {
+    const int wi = wave - 10;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sm.red1[wi][u][(4 * hi + i) * 16 + lo] = g1[u][i];
+    sb1 += __shfl_xor(sb1, 16, 64);
+    sb1 += __shfl_xor(sb1, 32, 64);
+    if (hi == 0) sm.rb1[wi][lo] = sb1;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < C2 * R2; i += NTHR) atomicAdd(dw2 + i, sm.gw2[i]);
-  for (int i = threadIdx.x; i < C1 * R1; i += NTHR) atomicAdd(dw1 + i, sm.gw1[i]);
-  if (threadIdx.x < C2 && db2) atomicAdd(db2 + threadIdx.x, sm.gb2[threadIdx.x]);
-  if (threadIdx.x < C1 && db1) atomicAdd(db1 + threadIdx.x, sm.gb1[threadIdx.x]);
+  for (int e = threadIdx.x; e < 2 * 256; e += NTHR) {
+    const int u = e >> 8, row = (e & 255) >> 4, col = 16 * u + (e & 15);
+    if (row < C1 && col < R1) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 6; ++w) v += sm.red1[w][u][e & 255];
+      atomicAdd(dw1 + row * R1 + col, v);
+    }
+  }
+  if (threadIdx.x < C1 && db1) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 6; ++w) v += sm.rb1[w][threadIdx.x];
+    atomicAdd(db1 + threadIdx.x, v);
+  }
 }
 
 }  // namespace

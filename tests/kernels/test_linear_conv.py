@@ -69,23 +69,27 @@ def test_conv_relu_pool(cfg, xdtype):
 
 
 def test_lenet_fused_matches_torch():
+    """Fused bf16 LeNet vs the fp32 model: its gradient error must be no worse than torch autocast's."""
     from rocket_amd.models import CrossEntropy, LeNet
 
     torch.manual_seed(0)
     ref = LeNet(fused=False).cuda()
+    amp = LeNet(fused=False).cuda()
     fus = LeNet(fused=True).cuda()
+    amp.load_state_dict(ref.state_dict())
     fus.load_state_dict(ref.state_dict())
     x = torch.rand(256, 1, 28, 28, device="cuda")
     y = torch.randint(0, 10, (256,), device="cuda")
+    lr = CrossEntropy(fused=False)(ref((x, y)))
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        lr = CrossEntropy(fused=False)(ref((x, y)))
+        la = CrossEntropy(fused=False)(amp((x, y)))
         lf = CrossEntropy(fused=True)(fus((x, y)))
     assert abs(lr.item() - lf.item()) < 2e-2
-    lr.backward()
-    lf.backward()
-    for (n, a), b in zip(ref.named_parameters(), fus.parameters()):
-        rel = (a.grad - b.grad).norm() / (a.grad.norm() + 1e-12)
-        assert rel < 5e-2, (n, rel.item())
+    for l in (lr, la, lf):
+        l.backward()
+    for (n, r), a, f in zip(ref.named_parameters(), amp.parameters(), fus.parameters()):
+        err_f, err_a = _rel(f.grad, r.grad), _rel(a.grad, r.grad)
+        assert err_f < max(2 * err_a, 2e-2), (n, err_f, err_a)
 
 
 def _ref_lenet(x, w1, b1, w2, b2, l1, l2, l3):
