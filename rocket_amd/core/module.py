@@ -77,8 +77,7 @@ class Module(Dispatcher):
             self._module.train()
         else:
             self._module.eval()
-        if self._graphs is not None and torch.is_grad_enabled():
-            self._graphs.launch(attrs)
+        if self._graphs is not None and torch.is_grad_enabled() and self._graphs.launch(attrs):
             return
         with self.runner():
             attrs.batch = self._module(attrs.batch)
@@ -91,7 +90,8 @@ class Module(Dispatcher):
             if m is base:
                 engine._models.pop(i)
                 break
-        self._graphs = None
+        if self._graphs is not None:
+            self._graphs.release()  # drop graphs + memory pool, keep counters for inspection
         Dispatcher.destroy(self, attrs=attrs)
 
     @contextlib.contextmanager

@@ -23,17 +23,25 @@ import torch
 
 from rocket_amd.core.attributes import Attributes
 from rocket_amd.core.capsule import Capsule
+from rocket_amd.ops import data as _data_ops
 from rocket_amd.runtime import comm as _comm
 from rocket_amd.utils.lazy import LazyScalar
 
 
 class Loss(Capsule):
+    RING = 1024  # device slots for reported losses under graph replay (tracker flushes far sooner)
+
     def __init__(self, objective: torch.nn.Module, tag: str = "train_loss", priority: int = 1100) -> None:
         super().__init__(statefull=True, priority=priority)
         self._objective = objective
         self._value = 0.0
         self._tag = tag
         self._step = 0
+        self._acc = None        # graph mode: device accumulator of the current GA window
+        self._ring = None       # graph mode: reported values, one slot per sync step
+        self._slot = None       # graph mode: device write cursor into the ring
+        self._slot_host = 0
+        self._acc_pending = False
 
     def _mean_over_ranks(self, loss: torch.Tensor) -> torch.Tensor:
         value = loss.detach().float().reshape(())
@@ -65,13 +73,68 @@ class Loss(Capsule):
             return
         if not torch.is_grad_enabled():
             return
+        if self._acc_pending:  # a graph-accumulated GA window continues eagerly
+            self._value = self._value + self._acc.clone()
+            self._acc.zero_()
+            self._acc_pending = False
         loss = self.compute(attrs)
         self.post(attrs)
         self._accelerator.backward(loss)
 
+    # ---------------------------------------------------- HIP-graph protocol
+    def graph_bind(self, graphs) -> None:
+        """Allocate the static device state used by captured steps."""
+        if self._acc is not None:
+            return
+        dev = self._accelerator.device
+        # W>1: the accumulator lives in the reducer's side channel and is averaged across
+        # ranks by the gradient all-reduce itself
+        self._acc = graphs.side_slot(1)
+        self._ring = torch.zeros(self.RING, device=dev)
+        self._slot = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._zero = torch.zeros(1, device=dev)
+        self._one = torch.ones((), device=dev)
+
+    def graph_prepare(self, attrs: Attributes | None = None) -> None:
+        v = self._value
+        if isinstance(v, torch.Tensor) or v != 0.0:  # fold an eager partial GA window
+            self._acc.add_(v if isinstance(v, torch.Tensor) else float(v))
+            self._value = 0.0
+
+    def graph_device(self, attrs: Attributes) -> None:
+        engine = self._accelerator
+        loss = self._objective(attrs.batch)
+        sync_here = engine.sync_gradients and not attrs.graph_split
+        _data_ops.loss_accum(loss.detach().reshape(1), self._acc, self._ring, self._slot,
+                             1.0 / engine.gradient_accumulation_steps, sync_here)
+        if loss.dtype == self._one.dtype and loss.dim() == 0:
+            engine.backward(loss, gradient=self._one)  # static seed: no fill kernel per step
+        else:
+            engine.backward(loss)
+
+    def graph_device_synced(self, attrs: Attributes) -> None:
+        if self._accelerator.sync_gradients and attrs.graph_split:
+            _data_ops.loss_accum(self._zero, self._acc, self._ring, self._slot, 0.0, True)
+
+    def graph_host(self, attrs: Attributes) -> None:
+        if not self._accelerator.sync_gradients:
+            self._acc_pending = True
+            return
+        self._acc_pending = False
+        value = LazyScalar(self._ring[self._slot_host])
+        self._slot_host = (self._slot_host + 1) % self.RING
+        if attrs.tracker is not None:
+            attrs.tracker.scalars.append(Attributes(step=self._step, data={self._tag: value}))
+        if attrs.looper is not None:
+            attrs.looper.state.loss = value
+        self._step += 1
+
     def state_dict(self) -> dict:
         v = self._value
-        return dict(value=float(v.item()) if isinstance(v, torch.Tensor) else float(v), step=self._step)
+        v = float(v.item()) if isinstance(v, torch.Tensor) else float(v)
+        if self._acc_pending and self._acc is not None:
+            v += float(self._acc.item())
+        return dict(value=v, step=self._step)
 
     def load_state_dict(self, state: dict) -> None:
         self._value = state["value"]
@@ -94,8 +157,11 @@ class Optimizer(Capsule):
         self._optimizer = found[0] if found else engine.prepare_optimizer(self._optimizer)
 
     def step(self) -> None:
-        self._optimizer.step()
-        self._optimizer.zero_grad()
+        if hasattr(self._optimizer, "step_and_zero_grad"):
+            self._optimizer.step_and_zero_grad()
+        else:
+            self._optimizer.step()
+            self._optimizer.zero_grad()
 
     def post(self, attrs: Attributes | None) -> None:
         if not self._accelerator.sync_gradients:
@@ -111,6 +177,27 @@ class Optimizer(Capsule):
     def launch(self, attrs: Attributes | None = None) -> None:
         if torch.is_grad_enabled():
             self.step()
+        self.post(attrs)
+
+    # ---------------------------------------------------- HIP-graph protocol
+    def graph_supported(self) -> bool:
+        return hasattr(self._optimizer, "fused_zero_ok") and self._optimizer.fused_zero_ok()
+
+    def graph_token(self):
+        return self._optimizer.optimizer.version
+
+    def graph_prepare(self, attrs: Attributes | None = None) -> None:
+        inner = self._optimizer.optimizer
+        if inner._key is None:
+            inner.prepare()
+        else:
+            inner.refresh_hyper()  # pointers are frozen into the graph; only lr & co. can change
+
+    def graph_device(self, attrs: Attributes) -> None:
+        if self._accelerator.sync_gradients:
+            self._optimizer.optimizer.launch(zero_grads=True)
+
+    def graph_host(self, attrs: Attributes) -> None:
         self.post(attrs)
 
     def destroy(self, attrs: Attributes | None = None) -> None:
@@ -144,6 +231,13 @@ class Scheduler(Capsule):
     def launch(self, attrs: Attributes | None = None) -> None:
         if torch.is_grad_enabled():
             self._scheduler.step()
+
+    # ---------------------------------------------------- HIP-graph protocol (host-only)
+    def graph_device(self, attrs: Attributes) -> None:
+        return None
+
+    def graph_host(self, attrs: Attributes) -> None:
+        self.launch(attrs)
 
     def destroy(self, attrs: Attributes | None = None) -> None:
         registry = self._accelerator._schedulers

@@ -1,0 +1,87 @@
+// Small data-path kernels that replace chains of PyTorch launches.
+//
+// rk_gather_rows  – batch assembly for HBM-resident datasets: out_t[r] = src_t[idx[r]] for up
+//                   to 4 aligned tensors in ONE launch (a LeNet batch is a 3 KB image row and
+//                   an 8 B label row per sample; torch needs one index_select per tensor).
+//                   Rows are copied with 16 B vectors when size/alignment allow.
+// rk_loss_accum   – the Loss capsule's per-micro-step bookkeeping on the device:
+//                   acc += loss * scale; on a gradient-sync step ring[slot] = acc, slot advances,
+//                   acc = 0.  One single-thread launch instead of five elementwise kernels,
+//                   and graph-capturable (the ring slot lives in device memory).
+#include "rk_common.h"
+
+namespace {
+
+constexpr int kMaxGather = 4;
+
+struct GatherArgs {
+  const char* src[kMaxGather];
+  char* dst[kMaxGather];
+  int64_t row_bytes[kMaxGather];
+  int64_t src_rows[kMaxGather];
+  int ntensors;
+};
+
+// grid: x = row blocks (kRowsPerBlock rows each), y = tensor.  One wave copies one row.
+constexpr int kThreads = 256;
+constexpr int kRowsPerBlock = kThreads / 64;
+
+__global__ void __launch_bounds__(kThreads) gather_rows_kernel(GatherArgs a, const int64_t* __restrict__ idx,
+                                                               int64_t nrows) {
+  const int t = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (r >= nrows) return;
+  int64_t s = idx[r];
+  s = s < 0 ? s + a.src_rows[t] : s;
+  const int64_t rb = a.row_bytes[t];
+  const char* __restrict__ src = a.src[t] + s * rb;
+  char* __restrict__ dst = a.dst[t] + r * rb;
+  if (((rb | (int64_t)a.src[t] | (int64_t)a.dst[t]) & 15) == 0) {
+    const int64_t n = rb >> 4;
+    for (int64_t i = lane; i < n; i += 64) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+  } else if (((rb | (int64_t)a.src[t] | (int64_t)a.dst[t]) & 7) == 0) {
+    const int64_t n = rb >> 3;
+    for (int64_t i = lane; i < n; i += 64) ((uint64_t*)dst)[i] = ((const uint64_t*)src)[i];
+  } else {
+    for (int64_t i = lane; i < rb; i += 64) dst[i] = src[i];
+  }
+}
+
+__global__ void loss_accum_kernel(const float* __restrict__ loss, float* acc, float* ring, int64_t* slot,
+                                  int ring_size, float scale, int sync) {
+  float v = acc[0] + loss[0] * scale;
+  if (sync) {
+    int64_t k = slot[0];
+    ring[k] = v;
+    slot[0] = (k + 1) % ring_size;
+    v = 0.f;
+  }
+  acc[0] = v;
+}
+
+}  // namespace
+
+// srcs/dsts: arrays of device pointers (host memory), row_bytes/src_rows per tensor.
+RK_API int rk_gather_rows(int ntensors, const void* const* srcs, void* const* dsts, const int64_t* row_bytes,
+                          const int64_t* src_rows, const int64_t* idx, int64_t nrows, hipStream_t s) {
+  if (ntensors <= 0 || nrows <= 0) return 0;
+  if (ntensors > kMaxGather) return (int)hipErrorInvalidValue;
+  GatherArgs a{};
+  for (int i = 0; i < ntensors; ++i) {
+    a.src[i] = (const char*)srcs[i];
+    a.dst[i] = (char*)dsts[i];
+    a.row_bytes[i] = row_bytes[i];
+    a.src_rows[i] = src_rows[i];
+  }
+  a.ntensors = ntensors;
+  dim3 grid((unsigned)((nrows + kRowsPerBlock - 1) / kRowsPerBlock), (unsigned)ntensors);
+  gather_rows_kernel<<<grid, kThreads, 0, s>>>(a, idx, nrows);
+  return (int)hipGetLastError();
+}
+
+RK_API int rk_loss_accum(const float* loss, float* acc, float* ring, int64_t* slot, int ring_size, float scale,
+                         int sync, hipStream_t s) {
+  loss_accum_kernel<<<1, 1, 0, s>>>(loss, acc, ring, slot, ring_size, scale, sync);
+  return (int)hipGetLastError();
+}

@@ -11,6 +11,8 @@
 //
 // Optional AMP hooks: `inv_scale` multiplies every gradient (GradScaler unscale
 // folded into the update) and a non-zero `found_inf` makes the launch a no-op.
+// `zero_grads` clears each gradient chunk after it is consumed (the
+// optimizer.step(); optimizer.zero_grad() pair in one pass over the gradient).
 //
 // Memory: each block streams a 4096-element chunk (16 fp32/thread, float4
 // vectorised): params/grads/exp_avg/exp_avg_sq read once, written once.
@@ -37,6 +39,11 @@ template <> __device__ __forceinline__ float gload<float>(const float* g, int64_
 template <> __device__ __forceinline__ float gload<uint16_t>(const uint16_t* g, int64_t i) { return bf2f(g[i]); }
 
 template <typename G>
+__device__ __forceinline__ void zero_chunk(G* g, int64_t start, int64_t end) {
+  for (int64_t i = start + threadIdx.x; i < end; i += kThreads) g[i] = G(0);
+}
+
+template <typename G, bool ZG>
 __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __restrict__ tensors,
                                                           const int2* __restrict__ blocks,
                                                           const AdamHyper* __restrict__ hyper, float* step,
@@ -49,7 +56,7 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
     const TensorRec tr = tensors[bt.x];
     const AdamHyper h = hyper[tr.group];
     float* __restrict__ p = (float*)tr.p;
-    const G* __restrict__ g = (const G*)tr.g;
+    G* __restrict__ g = (G*)tr.g;
     float* __restrict__ m = (float*)tr.s0;
     float* __restrict__ v = (float*)tr.s1;
     const float t = step[0] + 1.f;
@@ -83,13 +90,25 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
           *(float4*)(p + i) = pp;
           *(float4*)(m + i) = mm;
           *(float4*)(v + i) = vv;
+          if (ZG) *(float4*)((float*)g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
-          for (int64_t k = i; k < end; ++k) upd(p[k], gload<G>(g, k), m[k], v[k]);
+          for (int64_t k = i; k < end; ++k) {
+            upd(p[k], gload<G>(g, k), m[k], v[k]);
+            if (ZG) g[k] = G(0);
+          }
         }
       }
     } else {
-      for (int64_t i = start + threadIdx.x; i < end; i += kThreads) upd(p[i], gload<G>(g, i), m[i], v[i]);
+      for (int64_t i = start + threadIdx.x; i < end; i += kThreads) {
+        upd(p[i], gload<G>(g, i), m[i], v[i]);
+        if (ZG) g[i] = G(0);
+      }
     }
+  } else if (ZG) {
+    const int2 bt = blocks[blockIdx.x];
+    const TensorRec tr = tensors[bt.x];
+    const int64_t start = (int64_t)bt.y * kChunk;
+    zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)kChunk, tr.n));
   }
   if (last_block_arrived(counter, &flag)) {
     if (threadIdx.x == 0 && !skip) step[0] += 1.f;
@@ -101,7 +120,7 @@ struct SgdHyper {  // 8 floats per group
   float lr, momentum, dampening, wd, nesterov, maximize, first, pad;
 };
 
-template <typename G>
+template <typename G, bool ZG>
 __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __restrict__ tensors,
                                                          const int2* __restrict__ blocks,
                                                          const SgdHyper* __restrict__ hyper, float* step,
@@ -114,7 +133,7 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
     const TensorRec tr = tensors[bt.x];
     const SgdHyper h = hyper[tr.group];
     float* p = (float*)tr.p;
-    const G* g = (const G*)tr.g;
+    G* g = (G*)tr.g;
     float* buf = (float*)tr.s0;
     const bool first = step[0] == 0.f;  // momentum buffer initialised with the first gradient (torch semantics)
     const float gs = inv_scale ? inv_scale[0] : 1.f;
@@ -129,7 +148,13 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
         gg = h.nesterov != 0.f ? gg + h.momentum * b : b;
       }
       p[i] -= sgn * h.lr * gg;
+      if (ZG) g[i] = G(0);
     }
+  } else if (ZG) {
+    const int2 bt = blocks[blockIdx.x];
+    const TensorRec tr = tensors[bt.x];
+    const int64_t start = (int64_t)bt.y * kChunk;
+    zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)kChunk, tr.n));
   }
   if (last_block_arrived(counter, &flag)) {
     if (threadIdx.x == 0 && !skip) step[0] += 1.f;
@@ -143,20 +168,25 @@ RK_API int rk_optim_chunk() { return kChunk; }
 
 // kind: 0 = Adam/AdamW, 1 = SGD.  gdtype: grads dtype (0 f32, 1 bf16).
 RK_API int rk_optim_mt(int kind, int gdtype, const void* tensors, const void* blocks, int nblocks, const void* hyper,
-                       float* step, const float* inv_scale, const float* found_inf, unsigned* counter, hipStream_t s) {
+                       float* step, const float* inv_scale, const float* found_inf, unsigned* counter, int zero_grads,
+                       hipStream_t s) {
   if (nblocks <= 0) return 0;
   const TensorRec* t = (const TensorRec*)tensors;
   const int2* b = (const int2*)blocks;
+#define RK_OPT_LAUNCH(KERNEL, G, H)                                                                        \
+  (zero_grads ? KERNEL<G, true><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, inv_scale, found_inf, counter) \
+              : KERNEL<G, false><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, inv_scale, found_inf, counter))
   if (kind == 0) {
     if (gdtype == BF16)
-      adam_mt_kernel<uint16_t><<<nblocks, kThreads, 0, s>>>(t, b, (const AdamHyper*)hyper, step, inv_scale, found_inf, counter);
+      RK_OPT_LAUNCH(adam_mt_kernel, uint16_t, AdamHyper);
     else
-      adam_mt_kernel<float><<<nblocks, kThreads, 0, s>>>(t, b, (const AdamHyper*)hyper, step, inv_scale, found_inf, counter);
+      RK_OPT_LAUNCH(adam_mt_kernel, float, AdamHyper);
   } else {
     if (gdtype == BF16)
-      sgd_mt_kernel<uint16_t><<<nblocks, kThreads, 0, s>>>(t, b, (const SgdHyper*)hyper, step, inv_scale, found_inf, counter);
+      RK_OPT_LAUNCH(sgd_mt_kernel, uint16_t, SgdHyper);
     else
-      sgd_mt_kernel<float><<<nblocks, kThreads, 0, s>>>(t, b, (const SgdHyper*)hyper, step, inv_scale, found_inf, counter);
+      RK_OPT_LAUNCH(sgd_mt_kernel, float, SgdHyper);
   }
+#undef RK_OPT_LAUNCH
   return (int)hipGetLastError();
 }

@@ -32,11 +32,13 @@ class _FusedBase(torch.optim.Optimizer):
         self._key = None
         self._tables = None
         self._hyper_host = None
+        self._hyper_list = None
         self._hyper_dev = None
         self._step_dev = None
         self._device = None
         self._gdtype = 0
         self._nblocks = 0
+        self.version = 0  # bumped whenever a device table/state pointer changes (captured graphs go stale)
         self.grad_scale: Optional[torch.Tensor] = None  # 1/scale (AMP); device scalar
         self.found_inf: Optional[torch.Tensor] = None
 
@@ -65,6 +67,7 @@ class _FusedBase(torch.optim.Optimizer):
             self._device = device
             steps = [float(st["step"]) for st in self.state.values() if "step" in st]
             self._step_dev = torch.tensor([max(steps) if steps else 0.0], dtype=torch.float32, device=device)
+            self.version += 1
 
     def prepare(self) -> bool:
         """Host-side bookkeeping; returns False when there is nothing to update."""
@@ -87,14 +90,21 @@ class _FusedBase(torch.optim.Optimizer):
         if key != self._key:
             self._build_tables(active, device)
             self._key = key
-        rows = [self._hyper_row(g) for g in self.param_groups]
-        flat = [x for r in rows for x in r]
-        if self._hyper_host is None or self._hyper_host.tolist() != flat:
-            self._hyper_host = torch.tensor(flat, dtype=torch.float32)
-            if self._hyper_dev is None or self._hyper_dev.numel() != len(flat):
-                self._hyper_dev = torch.empty(len(flat), dtype=torch.float32, device=device)
-            self._hyper_dev.copy_(self._hyper_host.pin_memory(), non_blocking=True)
+        self.refresh_hyper()
         return True
+
+    def refresh_hyper(self) -> None:
+        """Upload the per-group hyper-parameters if a scheduler/user changed them (cheap when unchanged)."""
+        flat = [x for g in self.param_groups for x in self._hyper_row(g)]
+        if flat != self._hyper_list:
+            self._hyper_list = flat
+            if self._hyper_dev is None or self._hyper_dev.numel() != len(flat):
+                self.version += 1
+            host = torch.tensor(flat, dtype=torch.float32).pin_memory()
+            if self._hyper_dev is None or self._hyper_dev.numel() != len(flat):
+                self._hyper_dev = torch.empty(len(flat), dtype=torch.float32, device=self._device)
+            self._hyper_dev.copy_(host, non_blocking=True)
+            self._hyper_host = host  # keep the pinned source alive until the copy has run
 
     def _build_tables(self, active, device) -> None:
         chunk = _lib.kernels().rk_optim_chunk()
@@ -109,17 +119,19 @@ class _FusedBase(torch.optim.Optimizer):
         b_host = torch.tensor(blocks, dtype=torch.int32).pin_memory()
         self._tables = (t_host.to(device, non_blocking=True), b_host.to(device, non_blocking=True))
         self._nblocks = len(blocks) // 2
+        self.version += 1
 
     # --------------------------------------------------------- device side
-    def launch(self) -> None:
-        """Enqueue the fused update (graph-capturable)."""
+    def launch(self, zero_grads: bool = False) -> None:
+        """Enqueue the fused update (graph-capturable); ``zero_grads`` also clears the consumed gradients."""
         lib = _lib.kernels()
         dev = self._device
         _lib.check(
             lib.rk_optim_mt(self.KIND, self._gdtype, self._tables[0].data_ptr(), self._tables[1].data_ptr(),
                             self._nblocks, self._hyper_dev.data_ptr(), self._step_dev.data_ptr(),
                             _lib.ptr(self.grad_scale), _lib.ptr(self.found_inf),
-                            _lib.Workspace.get(dev).counter(f"optim_{id(self)}"), _lib.stream_ptr(dev)),
+                            _lib.Workspace.get(dev).counter(f"optim_{id(self)}"), int(zero_grads),
+                            _lib.stream_ptr(dev)),
             "rk_optim_mt",
         )
 

@@ -43,12 +43,13 @@ from torch import nn
 
 DEFAULT_BUCKET_MB = 32.0
 DEFAULT_FIRST_BUCKET_MB = 1.0
+SIDE_SLOTS = 16
 
 
 class _Bucket:
-    __slots__ = ("index", "params", "offsets", "flat", "pending", "work", "ready")
+    __slots__ = ("index", "params", "offsets", "flat", "pending", "work", "ready", "numel_params")
 
-    def __init__(self, index: int, params: List[nn.Parameter], dtype, device):
+    def __init__(self, index: int, params: List[nn.Parameter], dtype, device, extra: int = 0):
         self.index = index
         self.params = params
         self.offsets = []
@@ -56,7 +57,8 @@ class _Bucket:
         for p in params:
             self.offsets.append(n)
             n += p.numel()
-        self.flat = torch.zeros(n, dtype=dtype, device=device)
+        self.numel_params = n
+        self.flat = torch.zeros(n + extra, dtype=dtype, device=device)
         self.pending = len(params)
         self.work = None
         self.ready: set = set()
@@ -112,6 +114,7 @@ class DataParallel(nn.Module):
         self._sync_module_states()
         self._build_buckets(bucket_cap_mb, first_bucket_mb)
         self._armed = False
+        self._deferred = False
 
     # ----------------------------------------------------------------- setup
     def _flat_broadcast(self, tensors: List[torch.Tensor]) -> None:
@@ -159,6 +162,17 @@ class DataParallel(nn.Module):
             if cur_bytes >= limit:
                 close()
         close()
+        # side channel: a few fp32 slots behind the last fp32 bucket's gradients, averaged by the
+        # same collective (captured steps reduce their loss scalar with the gradients, no extra call)
+        self._side = None
+        self._side_used = 0
+        for bi in range(len(self.buckets) - 1, -1, -1):
+            b = self.buckets[bi]
+            if b.flat.dtype == torch.float32:
+                nb = _Bucket(b.index, b.params, b.flat.dtype, b.flat.device, extra=SIDE_SLOTS)
+                self.buckets[bi] = nb
+                self._side = nb.flat[nb.numel_params :]
+                break
         for b in self.buckets:
             for i, p in enumerate(b.params):
                 self._slot[id(p)] = (b, i)
@@ -166,7 +180,11 @@ class DataParallel(nn.Module):
                     if p.grad is not None:
                         b.view(i).copy_(p.grad)
                 p.grad = b.view(i)
+                p._rocket_direct_grad = True  # fused kernels may accumulate into the view directly
+                p._rocket_grad_hook = self._on_grad
                 p.register_post_accumulate_grad_hook(self._on_grad)
+        self.params = [p for b in self.buckets for p in b.params]
+        self._ids = {id(p) for p in self.params}
 
     # --------------------------------------------------------------- runtime
     @contextlib.contextmanager
@@ -179,13 +197,48 @@ class DataParallel(nn.Module):
             self.require_backward_grad_sync = old
 
     def forward(self, *args, **kwargs):
-        if torch.is_grad_enabled():
+        if torch.is_grad_enabled() and not self._deferred:
             self._arm()
-        if self.broadcast_buffers and self.require_backward_grad_sync:
-            bufs = list(self.module.buffers())
-            if bufs:
-                self._flat_broadcast(bufs)
+        if self.broadcast_buffers and self.require_backward_grad_sync and not self._deferred:
+            self.sync_buffers()
         return self.module(*args, **kwargs)
+
+    def sync_buffers(self) -> None:
+        """Broadcast rank-0 module buffers (BatchNorm statistics) to every rank."""
+        bufs = list(self.module.buffers())
+        if bufs:
+            self._flat_broadcast(bufs)
+
+    # ----------------------------------------------------- captured (graph) steps
+    @contextlib.contextmanager
+    def deferred(self):
+        """Record gradients into the buckets without communicating (HIP-graph capture).
+
+        The captured region contains no collective; the step executor calls
+        :meth:`reduce_now` on the host between the backward graph and the
+        optimizer graph, so RCCL never runs inside a graph.
+        """
+        old = self._deferred
+        self._deferred = True
+        self._armed = False
+        try:
+            yield
+        finally:
+            self._deferred = old
+
+    def reduce_now(self) -> None:
+        """Average every bucket (incl. the side channel) across ranks; stream-ordered, no host wait."""
+        works = [self.comm.all_reduce_avg(b.flat) for b in self.buckets]
+        for w in works:
+            w.wait()
+
+    def side_slot(self, n: int = 1) -> torch.Tensor:
+        """``n`` fp32 slots that are averaged together with the gradients on every sync step."""
+        if self._side is None or self._side_used + n > self._side.numel():
+            return None
+        v = self._side[self._side_used : self._side_used + n]
+        self._side_used += n
+        return v
 
     def _arm(self) -> None:
         for b in self.buckets:
@@ -202,7 +255,7 @@ class DataParallel(nn.Module):
             with torch.no_grad():
                 view.copy_(p.grad)
             p.grad = view
-        if not self._armed or i in b.ready:
+        if self._deferred or not self._armed or i in b.ready:
             return
         if not self._finalize_queued:
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
@@ -232,11 +285,18 @@ class DataParallel(nn.Module):
                 b.work.wait()
                 b.work = None
 
-    def zero_grad(self, set_to_none: bool = False) -> None:
+    def owns(self, p) -> bool:
+        return id(p) in self._ids
+
+    def zero_(self) -> None:
         for b in self.buckets:
             b.flat.zero_()
             for i, p in enumerate(b.params):
-                p.grad = b.view(i)
+                if p.grad is None or p.grad.data_ptr() != b.view(i).data_ptr():
+                    p.grad = b.view(i)
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        self.zero_()
 
     # ---------------------------------------------------------------- access
     def state_dict(self, *args, **kwargs):

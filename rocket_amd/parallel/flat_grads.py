@@ -1,0 +1,74 @@
+"""Persistent flat gradient storage.
+
+Every parameter's ``.grad`` becomes a view into one contiguous fp32 buffer per
+(device, dtype).  What this buys on MI355X:
+
+* gradients have **static addresses**, so a training step that produces and
+  consumes them can be captured once into a HIP graph and replayed;
+* ``zero_grad`` is one ``memset`` of the buffer instead of one kernel per tensor
+  (or an allocation per tensor per step with ``set_to_none``);
+* the fused kernels (:mod:`rocket_amd.ops`) accumulate weight gradients
+  straight into ``param.grad`` (``param._rocket_direct_grad``), skipping
+  autograd's AccumulateGrad copies;
+* the data-parallel reducer can all-reduce the buffer (or contiguous slices of
+  it) in place.
+
+``DataParallel`` builds its bucket views with the same conventions, so a model
+gets exactly one of the two.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import torch
+from torch import nn
+
+
+class FlatGrads:
+    def __init__(self, params: List[nn.Parameter]):
+        groups: Dict[Tuple[torch.device, torch.dtype], List[nn.Parameter]] = {}
+        for p in params:
+            if p.requires_grad:
+                groups.setdefault((p.device, p.dtype), []).append(p)
+        self.buffers: List[torch.Tensor] = []
+        self.params: List[nn.Parameter] = []
+        self.views: List[torch.Tensor] = []
+        for (dev, dtype), ps in groups.items():
+            n = sum(p.numel() for p in ps)
+            flat = torch.zeros(n, dtype=dtype, device=dev)
+            off = 0
+            for p in ps:
+                view = flat[off : off + p.numel()].view_as(p)
+                if p.grad is not None:
+                    with torch.no_grad():
+                        view.copy_(p.grad)
+                p.grad = view
+                p._rocket_direct_grad = True
+                off += p.numel()
+                self.params.append(p)
+                self.views.append(view)
+            self.buffers.append(flat)
+        self._ids = {id(p) for p in self.params}
+
+    def owns(self, p: torch.Tensor) -> bool:
+        return id(p) in self._ids
+
+    def restore_views(self) -> None:
+        """Re-point ``.grad`` at the buffer views (e.g. after ``zero_grad(set_to_none=True)``)."""
+        for p, v in zip(self.params, self.views):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                if p.grad is not None:
+                    with torch.no_grad():
+                        v.copy_(p.grad)
+                else:
+                    v.zero_()
+                p.grad = v
+
+    def zero_(self) -> None:
+        for flat in self.buffers:
+            flat.zero_()
+
+    @property
+    def numel(self) -> int:
+        return sum(b.numel() for b in self.buffers)

@@ -16,7 +16,9 @@ Loading rules kept: the number of ``custom_checkpoint_*.pkl`` files must equal
 the number of registered objects (else ``RuntimeError``); a missing RNG file is
 logged and skipped.  Files we read back are loaded with ``weights_only=True``
 where their content allows it (model/optimizer/scheduler/custom state); the RNG
-file holds numpy RNG state and is only ever written by this code.
+file stores numpy's RNG key as a tensor; reading an accelerate-written RNG file
+allow-lists only numpy's array reconstruction.  Nothing is ever unpickled with
+``weights_only=False``.
 """
 
 from __future__ import annotations
@@ -59,6 +61,19 @@ def _cpu_state_dict(model: torch.nn.Module) -> dict:
     return out
 
 
+def _np_state_plain(st):
+    # ('MT19937', uint32[624], pos, has_gauss, cached) with the key array as a tensor: weights_only-loadable
+    return (st[0], torch.from_numpy(np.asarray(st[1], dtype=np.uint32).astype(np.int64)), int(st[2]), int(st[3]),
+            float(st[4]))
+
+
+def _np_state_restore(st):
+    key = st[1]
+    if isinstance(key, torch.Tensor):
+        key = key.numpy().astype(np.uint32)
+    return (st[0], np.asarray(key, dtype=np.uint32), int(st[2]), int(st[3]), float(st[4]))
+
+
 def save_state(engine, output_dir: str) -> Path:
     out = Path(output_dir)
     out.mkdir(parents=True, exist_ok=True)
@@ -74,7 +89,7 @@ def save_state(engine, output_dir: str) -> Path:
     states = {
         "step": engine.step,
         "random_state": random.getstate(),
-        "numpy_random_seed": np.random.get_state(),
+        "numpy_random_seed": _np_state_plain(np.random.get_state()),
         "torch_manual_seed": torch.get_rng_state(),
     }
     if torch.cuda.is_available() and torch.cuda.is_initialized():
@@ -86,12 +101,30 @@ def save_state(engine, output_dir: str) -> Path:
 
 
 def _load(path, **kw):
+    """Load with the restricted unpickler only — a checkpoint never executes code on resume."""
     try:
         return torch.load(path, weights_only=True, **kw)
+    except Exception as e:
+        raise RuntimeError(
+            f"{path}: not loadable with torch.load(weights_only=True) ({e}). Checkpoint state must consist of "
+            "tensors and plain Python containers/scalars."
+        ) from e
+
+
+def _numpy_safe_globals():
+    """The numpy reconstruction entry points needed to read an RNG state array (no arbitrary code)."""
+    out = [np.ndarray, np.dtype]
+    for mod, name in (("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct")):
+        try:
+            m = __import__(mod, fromlist=[name])
+            out.append(getattr(m, name))
+        except Exception:
+            pass
+    try:
+        out.append(type(np.dtype(np.uint32)))
     except Exception:
-        # only files this framework wrote reach here (RNG state with numpy arrays,
-        # user custom state containing plain Python objects)
-        return torch.load(path, weights_only=False, **kw)
+        pass
+    return out
 
 
 def custom_checkpoint_files(input_dir: str) -> List[str]:
@@ -119,10 +152,11 @@ def load_state(engine, input_dir: str, load_custom: bool = True) -> None:
     rng = src / f"random_states_{engine.process_index}.pkl"
     if rng.exists():
         try:
-            states = torch.load(rng, weights_only=False)  # written by save_state above
+            with torch.serialization.safe_globals(_numpy_safe_globals()):
+                states = torch.load(rng, weights_only=True)
             engine.step = states.get("step", engine.step)
             random.setstate(states["random_state"])
-            np.random.set_state(states["numpy_random_seed"])
+            np.random.set_state(_np_state_restore(states["numpy_random_seed"]))
             torch.set_rng_state(states["torch_manual_seed"])
             if "torch_cuda_manual_seed" in states and torch.cuda.is_available():
                 cuda_states = states["torch_cuda_manual_seed"]

@@ -96,9 +96,10 @@ def init(cpu: bool | None = None, timeout_s: float | None = None) -> ProcessCont
     if world > 1:
         timeout = datetime.timedelta(seconds=timeout_s or float(os.environ.get("ROCKET_PG_TIMEOUT", "1800")))
         if not dist.is_initialized():
-            backend = "nccl" if gpu else "gloo"
+            # ROCKET_DIST_BACKEND=gloo: rehearse multi-rank GPU paths with several ranks on one device
+            backend = os.environ.get("ROCKET_DIST_BACKEND") or ("nccl" if gpu else "gloo")
             kwargs = dict(backend=backend, timeout=timeout)
-            if gpu:
+            if gpu and backend == "nccl":
                 kwargs["device_id"] = device
             dist.init_process_group(**kwargs)
             owns = True

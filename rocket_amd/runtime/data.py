@@ -353,7 +353,17 @@ class DeviceTensorDataset(torch.utils.data.Dataset):
 
 
 class DeviceLoader(_LoaderBase):
-    """Loader over a :class:`DeviceTensorDataset`: per-epoch index table, on-device gathers."""
+    """Loader over a :class:`DeviceTensorDataset`: per-epoch index table, on-device gathers.
+
+    On a HIP device every batch is assembled by ONE native gather launch
+    (all dataset tensors at once) into a small ring of persistent batch
+    buffers (``RING`` deep, per batch size).  The buffers carry
+    ``_rocket_persistent`` so a captured training step reads them in place —
+    no per-step copy into static graph inputs.  Consequently a yielded batch
+    stays valid for ``RING - 1`` further batches; clone it to keep it longer.
+    """
+
+    RING = 4
 
     def __init__(
         self,
@@ -383,6 +393,8 @@ class DeviceLoader(_LoaderBase):
             gradient_state=gradient_state,
         )
         self.device = dataset.device
+        self._rings: dict = {}
+        self._ring_pos: dict = {}
 
     def index_table(self) -> List[torch.Tensor]:
         batches = self.batch_sampler.local_batches()
@@ -394,13 +406,36 @@ class DeviceLoader(_LoaderBase):
             flat = flat.pin_memory().to(self.device, non_blocking=True)
         return list(torch.split(flat, lens))
 
+    def _gather(self, idx: torch.Tensor):
+        tensors = self.dataset.tensors
+        if self.device.type != "cuda":
+            return tuple(t.index_select(0, idx) for t in tensors)
+        from rocket_amd.ops.data import gather_rows
+
+        n = idx.numel()
+        ring = self._rings.get(n)
+        if ring is None:
+            ring = []
+            for _ in range(self.RING):
+                bufs = tuple(torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device) for t in tensors)
+                for b in bufs:
+                    b._rocket_persistent = True
+                ring.append(bufs)
+            self._rings[n] = ring
+        k = self._ring_pos.get(n, 0)
+        self._ring_pos[n] = (k + 1) % self.RING
+        out = ring[k]
+        gather_rows([t.contiguous() for t in tensors], idx, out)
+        return out
+
     def _batches(self):
         for idx in self.index_table():
-            yield tuple(t.index_select(0, idx) for t in self.dataset.tensors)
+            yield self._gather(idx)
 
     def with_skip(self, num_batches: int) -> "DeviceLoader":
         out = DeviceLoader(self.dataset, skip=num_batches, **self._ctor)
         out.set_epoch(self.iteration)
+        out._rings, out._ring_pos = self._rings, self._ring_pos  # same buffers -> same captured graphs
         return out
 
 

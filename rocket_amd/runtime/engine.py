@@ -91,17 +91,13 @@ class EngineOptimizer:
     def load_state_dict(self, sd):
         self.optimizer.load_state_dict(sd)
 
-    def _uses_bucket_views(self) -> bool:
-        ids = self.engine._bucket_param_ids
-        return bool(ids) and any(id(p) in ids for g in self.optimizer.param_groups for p in g["params"])
+    def _params(self):
+        return [p for g in self.optimizer.param_groups for p in g["params"]]
 
     def zero_grad(self, set_to_none: Optional[bool] = None) -> None:
         if not self.engine.sync_gradients:
             return
-        if self._uses_bucket_views():
-            self.optimizer.zero_grad(set_to_none=False)
-        else:
-            self.optimizer.zero_grad(set_to_none=True if set_to_none is None else set_to_none)
+        self.engine.zero_grads(self._params(), set_to_none)
 
     def step(self, closure: Callable | None = None):
         if not self.engine.sync_gradients:
@@ -115,6 +111,27 @@ class EngineOptimizer:
             return None
         self.step_was_skipped = False
         return self.optimizer.step(closure) if closure else self.optimizer.step()
+
+    def fused_zero_ok(self) -> bool:
+        """True when the fused update kernel may clear the gradients itself (same result as zero_grad)."""
+        opt = self.optimizer
+        return (
+            self.engine.scaler is None
+            and hasattr(opt, "launch")
+            and all(getattr(p, "_rocket_direct_grad", False) for p in self._params() if p.requires_grad)
+        )
+
+    def step_and_zero_grad(self, set_to_none: Optional[bool] = None) -> None:
+        """``step(); zero_grad()`` — one kernel for the fused optimizers over persistent gradients."""
+        if not self.engine.sync_gradients:
+            return
+        if self.fused_zero_ok():
+            self.step_was_skipped = False
+            if self.optimizer.prepare():
+                self.optimizer.launch(zero_grads=True)
+            return
+        self.step()
+        self.zero_grad(set_to_none)
 
     def __getattr__(self, name):
         return getattr(self.optimizer, name)
@@ -171,6 +188,7 @@ class Engine:
         bucket_cap_mb: float | None = None,
         even_batches: bool = True,
         log_with: List[str] | None = None,
+        flat_grads: bool | None = None,
         **unused: Any,
     ):
         env_mp = os.environ.get("ROCKET_MIXED_PRECISION", os.environ.get("ACCELERATE_MIXED_PRECISION"))
@@ -194,7 +212,8 @@ class Engine:
             self.scaler = torch.amp.GradScaler(self.device.type)
         self._models: List[nn.Module] = []
         self._wrapped: dict = {}
-        self._bucket_param_ids: set = set()
+        self._grad_owners: list = []  # FlatGrads / DataParallel owning persistent .grad storage
+        self.flat_grads = self.device.type == "cuda" if flat_grads is None else bool(flat_grads)
         self._optimizers: List[EngineOptimizer] = []
         self._schedulers: List[EngineScheduler] = []
         self._dataloaders: List[_LoaderBase] = []
@@ -278,9 +297,48 @@ class Engine:
         if self.distributed and any(p.requires_grad for p in model.parameters()):
             wrapped = DataParallel(model, bucket_cap_mb=self.bucket_cap_mb)
             self._wrapped[id(model)] = wrapped
-            self._bucket_param_ids.update(id(p) for p in model.parameters())
+            self._grad_owners.append(wrapped)
             return wrapped
+        if self.flat_grads and any(p.requires_grad for p in model.parameters()):
+            from rocket_amd.parallel.flat_grads import FlatGrads
+
+            self._grad_owners.append(FlatGrads([p for p in model.parameters()]))
         return model
+
+    def grad_owner(self, p):
+        for o in self._grad_owners:
+            if o.owns(p):
+                return o
+        return None
+
+    def zero_grads(self, params, set_to_none: Optional[bool] = None) -> None:
+        """Zero gradients: one memset per persistent buffer fully covered, views otherwise."""
+        params = list(params)
+        ids = {id(p) for p in params}
+        loose = []
+        done = set()
+        for o in self._grad_owners:
+            mine = [p for p in o.params if id(p) in ids]
+            if not mine:
+                continue
+            if len(mine) == len(o.params):
+                o.zero_()
+            else:
+                with torch.no_grad():
+                    for p in mine:
+                        p.grad.zero_()
+            done.update(id(p) for p in mine)
+        for p in params:
+            if id(p) not in done:
+                loose.append(p)
+        for p in loose:
+            if p.grad is None:
+                continue
+            if set_to_none is False:
+                with torch.no_grad():
+                    p.grad.zero_()
+            else:
+                p.grad = None
 
     def prepare_optimizer(self, optimizer: torch.optim.Optimizer) -> EngineOptimizer:
         if self.device_placement:

@@ -1,0 +1,309 @@
+"""HIP-graph capture of the training micro-step (MI355X: graphs instead of a tracing compiler).
+
+A LeNet-sized step is launch-bound: ~10 kernels of a few µs each, separated by
+host launch latency (~5-10 µs per eager launch).  :class:`StepGraphs` captures
+the complete device side of a ``Module`` capsule's micro-step —
+
+    forward → objective → backward (incl. the fused kernels' direct gradient
+    accumulation) → [gradient all-reduce] → optimizer update + gradient clear
+
+— into HIP graphs per variant (gradient-sync step vs. accumulation step, keyed
+by input signature) and replays them every iteration, while every host-side
+duty of the capsules still runs each iteration: loss/lr reporting to the
+tracker and progress bar, scheduler stepping, GA bookkeeping.
+
+Data parallel (W>1): collectives never run inside a graph.  A sync step is two
+graphs — ``A`` (forward/backward, gradients land in the reducer's flat
+buckets) and ``B`` (post-reduction work: optimizer) — with the RCCL bucket
+all-reduce issued from the host between them (stream-ordered, no host wait).
+The loss scalar rides in the reducer's side channel, so it is averaged by the
+same collective.
+
+Protocol for children of a captured ``Module`` (built-ins implement it):
+
+* ``graph_prepare(attrs)``  – host work before each replay (e.g. the fused
+  optimizer uploads changed hyper-parameters);
+* ``graph_device(attrs)``   – device work of phase A (captured);
+* ``graph_device_synced(attrs)`` – optional device work of phase B, after the
+  gradient reduction (captured);
+* ``graph_host(attrs)``     – host bookkeeping after every replay;
+* ``graph_supported()``     – optional veto; ``graph_token()`` – optional value
+  whose change invalidates captured graphs (e.g. re-allocated optimizer tables).
+
+A child without ``graph_device`` makes the module fall back to eager
+execution, as do unseen input signatures until warmed up, and CPU tensors.
+The first ``warmup`` iterations of each (sync, signature) variant run eagerly,
+which also primes lazily created state (optimizer moments, workspaces).
+
+Inputs: tensors flagged ``_rocket_persistent`` (the device loader's ring
+buffers) are captured in place and get one graph per buffer set — no copy per
+step; any other input is copied into a static buffer before replay.
+"""
+
+from __future__ import annotations
+
+import collections
+from typing import Any, Dict, List, Tuple
+
+import torch
+
+from rocket_amd.core.attributes import Attributes
+from rocket_amd.utils.logging import get_logger
+
+logger = get_logger(__name__)
+
+MAX_VARIANTS = 32
+
+
+def _signature(batch) -> Tuple:
+    if isinstance(batch, torch.Tensor):
+        return (tuple(batch.shape), batch.dtype, batch.device.type)
+    if isinstance(batch, (list, tuple)):
+        return (type(batch).__name__,) + tuple(_signature(b) for b in batch)
+    if isinstance(batch, dict):
+        return ("dict",) + tuple((k, _signature(v)) for k, v in sorted(batch.items(), key=lambda kv: str(kv[0])))
+    return (type(batch).__name__, batch if isinstance(batch, (int, float, str, bool, type(None))) else id(batch))
+
+
+def _tensors(batch) -> List[torch.Tensor]:
+    if isinstance(batch, torch.Tensor):
+        return [batch]
+    if isinstance(batch, (list, tuple)):
+        return [t for b in batch for t in _tensors(b)]
+    if isinstance(batch, dict):
+        return [t for k in sorted(batch, key=str) for t in _tensors(batch[k])]
+    return []
+
+
+def _rebuild(batch, it):
+    if isinstance(batch, torch.Tensor):
+        return next(it)
+    if isinstance(batch, tuple) and hasattr(batch, "_fields"):
+        return type(batch)(*[_rebuild(b, it) for b in batch])
+    if isinstance(batch, (list, tuple)):
+        return type(batch)(_rebuild(b, it) for b in batch)
+    if isinstance(batch, dict):
+        keys = sorted(batch, key=str)
+        vals = {k: _rebuild(batch[k], it) for k in keys}
+        return type(batch)((k, vals[k]) for k in batch)
+    return batch
+
+
+class _Captured:
+    __slots__ = ("graphs", "static_in", "persistent", "out", "sync")
+
+    def __init__(self):
+        self.graphs: list = []   # [A] or [A, B] (B after the host-side gradient reduction)
+        self.static_in = None
+        self.persistent = None   # per input tensor: captured in place (no copy at replay)
+        self.out = None
+        self.sync = False
+
+
+class StepGraphs:
+    def __init__(self, module_capsule, warmup: int = 3):
+        self.mod = module_capsule
+        self.warmup = max(1, int(warmup))
+        self.variants: Dict[Any, _Captured] = {}
+        self.seen = collections.Counter()
+        self.pool = None
+        self.disabled_reason = None
+        self.replays = 0
+        self.captures = 0
+        self._token = None
+        self._checked = False
+
+    def release(self) -> None:
+        self.variants.clear()
+        self.pool = None
+        self.disabled_reason = self.disabled_reason or "released"
+
+    # ------------------------------------------------------------------ checks
+    def _replica(self):
+        from rocket_amd.parallel.ddp import DataParallel
+
+        rep = self.mod._module
+        return rep if isinstance(rep, DataParallel) else None
+
+    def _children_ok(self) -> bool:
+        for c in self.mod._capsules:
+            if not hasattr(c, "graph_device"):
+                self.disabled_reason = f"child {type(c).__name__} has no graph protocol"
+                return False
+            ok = getattr(c, "graph_supported", None)
+            if ok is not None and not ok():
+                self.disabled_reason = f"child {type(c).__name__} is not graph-safe"
+                return False
+        for p in self.mod._module.parameters():
+            if p.requires_grad and not getattr(p, "_rocket_direct_grad", False):
+                self.disabled_reason = "parameters lack persistent gradient buffers"
+                return False
+        if self.mod._accelerator.num_processes > 1 and self._replica() is None:
+            self.disabled_reason = "multi-process run without the rocket data-parallel reducer"
+            return False
+        return True
+
+    def side_slot(self, n: int = 1) -> torch.Tensor:
+        """``n`` static fp32 device slots; under data parallelism they are averaged across ranks
+        by the same collective as the gradients on every sync step."""
+        rep = self._replica()
+        v = rep.side_slot(n) if rep is not None else None
+        if v is None:
+            if rep is not None:
+                raise RuntimeError("data-parallel side channel exhausted")
+            v = torch.zeros(n, device=self.mod._accelerator.device)
+        return v
+
+    def _tokens(self):
+        return tuple(c.graph_token() for c in self.mod._capsules if hasattr(c, "graph_token"))
+
+    def _predict_sync(self) -> bool:
+        engine = self.mod._accelerator
+        if engine.gradient_state.end_of_dataloader:
+            return True
+        return (engine.step + 1) % engine.gradient_accumulation_steps == 0
+
+    # ------------------------------------------------------------------ launch
+    def launch(self, attrs: Attributes) -> bool:
+        """Run the micro-step through a graph; False -> the caller runs it eagerly."""
+        if self.disabled_reason is not None:
+            return False
+        batch = attrs.batch
+        tens = _tensors(batch)
+        if not tens or any(t.device.type != "cuda" for t in tens):
+            return False
+        sync = self._predict_sync()
+        sig = (sync, _signature(batch))
+        pkey = tuple(t.data_ptr() if getattr(t, "_rocket_persistent", False) else 0 for t in tens)
+        key = (sig, pkey)
+        v = self.variants.get(key)
+        if v is None:
+            self.seen[sig] += 1
+            if self.seen[sig] <= self.warmup:
+                return False  # eager warm-up (primes optimizer state / workspaces)
+            if not self._checked:
+                self._checked = True
+                if not self._children_ok():
+                    logger.info(f"graph capture disabled: {self.disabled_reason}")
+                    return False
+                for c in self.mod._capsules:
+                    bind = getattr(c, "graph_bind", None)
+                    if bind is not None:
+                        bind(self)
+            if len(self.variants) >= MAX_VARIANTS:
+                return False
+            self.mod._accelerator._do_sync()
+            self._prepare(attrs)
+            self._check_tokens()
+            self.variants[key] = self._capture(attrs, tens)
+            return True
+        self.mod._accelerator._do_sync()
+        self._prepare(attrs)
+        if self._check_tokens():  # tables re-allocated: every graph is stale, capture again
+            self.variants[key] = self._capture(attrs, tens)
+            return True
+        self._replay(v, attrs, tens)
+        return True
+
+    def _prepare(self, attrs: Attributes) -> None:
+        for c in self.mod._capsules:
+            prep = getattr(c, "graph_prepare", None)
+            if prep is not None:
+                prep(attrs)
+
+    def _check_tokens(self) -> bool:
+        tok = self._tokens()
+        if self._token is None:
+            self._token = tok
+            return False
+        if tok != self._token:
+            self._token = tok
+            self.variants.clear()
+            return True
+        return False
+
+    # ----------------------------------------------------------------- capture
+    def _phase_a(self, attrs: Attributes) -> None:
+        mod = self.mod
+        engine = mod._accelerator
+        rep = self._replica()
+        with engine.autocast():
+            with engine.no_sync(mod._module) if not engine.sync_gradients else _null():
+                with rep.deferred() if rep is not None else _null():
+                    attrs.batch = mod._module(attrs.batch)
+                    for c in mod._capsules:
+                        c.graph_device(attrs)
+
+    def _phase_b(self, attrs: Attributes) -> None:
+        for c in self.mod._capsules:
+            fn = getattr(c, "graph_device_synced", None)
+            if fn is not None:
+                fn(attrs)
+
+    def _capture(self, attrs: Attributes, tens: List[torch.Tensor]) -> _Captured:
+        engine = self.mod._accelerator
+        v = _Captured()
+        v.sync = engine.sync_gradients
+        v.persistent = [bool(getattr(t, "_rocket_persistent", False)) for t in tens]
+        v.static_in = [t if keep else t.detach().clone() for t, keep in zip(tens, v.persistent)]
+        rep = self._replica()
+        split = v.sync and rep is not None
+        if split and rep.broadcast_buffers:
+            rep.sync_buffers()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        cap = Attributes(attrs)
+        cap.batch = _rebuild(attrs.batch, iter(v.static_in))
+        cap.capturing = True
+        cap.graph_split = split
+        torch.cuda.synchronize()
+        ga = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga, pool=self.pool):
+            self._phase_a(cap)
+            if not split:
+                self._phase_b(cap)
+        v.graphs.append(ga)
+        if split:
+            gb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gb, pool=self.pool):
+                self._phase_b(cap)
+            v.graphs.append(gb)
+        v.out = cap.batch
+        self.captures += 1
+        logger.info(f"captured HIP graph(s) for sync={v.sync} ({len(v.graphs)} part(s))")
+        # the captured work has not run yet: replay it for this iteration
+        self._run(v, rep if split else None)
+        attrs.batch = v.out
+        self._host(attrs)
+        return v
+
+    # ------------------------------------------------------------------ replay
+    def _run(self, v: _Captured, rep) -> None:
+        v.graphs[0].replay()
+        if len(v.graphs) > 1:
+            rep.reduce_now()  # host-issued RCCL between the two graphs
+            v.graphs[1].replay()
+        self.replays += 1
+
+    def _host(self, attrs: Attributes) -> None:
+        for c in self.mod._capsules:
+            c.graph_host(attrs)
+
+    def _replay(self, v: _Captured, attrs: Attributes, tens: List[torch.Tensor]) -> None:
+        for dst, src, keep in zip(v.static_in, tens, v.persistent):
+            if not keep:
+                dst.copy_(src, non_blocking=True)
+        rep = self._replica() if len(v.graphs) > 1 else None
+        if rep is not None and rep.broadcast_buffers:
+            rep.sync_buffers()
+        self._run(v, rep)
+        attrs.batch = v.out
+        self._host(attrs)
+
+
+class _null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False

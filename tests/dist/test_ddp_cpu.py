@@ -1,0 +1,164 @@
+"""Multi-process (gloo, W=2) checks of the data-parallel path on CPU.
+
+* the bucketed reducer yields the full-batch mean gradient on every rank;
+* a W=2 Launcher run equals a W=1 run over the same global batches;
+* ``gather_for_metrics`` drops the wrap-around padding of the last batch.
+"""
+
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env(rank, world, port):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+
+
+def _run(fn, world, *args):
+    port = _port()
+    mp.start_processes(fn, args=(world, port) + args, nprocs=world, start_method="spawn", join=True)
+
+
+# ---------------------------------------------------------------- reducer
+def _reducer_worker(rank, world, port, out):
+    _env(rank, world, port)
+    from rocket_amd.runtime import comm
+    from rocket_amd.parallel.ddp import DataParallel
+
+    comm.init(cpu=True)
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    if rank == 1:  # different init on rank 1: construction must broadcast rank 0's weights
+        with torch.no_grad():
+            for p in net.parameters():
+                p.add_(1.0)
+    dp = DataParallel(net, first_bucket_mb=1e-4, bucket_cap_mb=1e-3)  # several buckets
+    x = torch.randn(2 * world, 8, generator=torch.Generator().manual_seed(1))
+    mine = x[rank * 2 : rank * 2 + 2]
+    for _ in range(2):  # second pass checks re-arming and no_sync accumulation
+        dp.zero_grad()
+        with dp.no_sync():
+            dp(mine).pow(2).mean().backward()
+        dp(mine).pow(2).mean().backward()
+    grads = [p.grad.tolist() for p in net.parameters()]
+    with open(os.path.join(out, f"g{rank}.json"), "w") as fh:
+        json.dump(dict(grads=grads, nb=len(dp.buckets)), fh)
+    comm.shutdown()
+
+
+def test_reducer_matches_full_batch(tmp_path):
+    _run(_reducer_worker, 2, str(tmp_path))
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    x = torch.randn(4, 8, generator=torch.Generator().manual_seed(1))
+    # per-rank loss is a mean over 2 rows, gradients averaged over ranks, 2 accumulated backward passes
+    loss = 2 * sum(net(x[r * 2 : r * 2 + 2]).pow(2).mean() for r in range(2)) / 2
+    loss.backward()
+    ref = [p.grad for p in net.parameters()]
+    for r in range(2):
+        got = json.load(open(tmp_path / f"g{r}.json"))
+        assert got["nb"] > 1
+        for g, e in zip(got["grads"], ref):
+            torch.testing.assert_close(torch.tensor(g), e, rtol=1e-5, atol=1e-6)
+
+
+# --------------------------------------------------------- launcher W=2 == W=1
+def _train(world, out_file, bs):
+    import rocket_amd as rocket
+
+    torch.manual_seed(0)
+    n = 24
+    x = torch.randn(n, 6, generator=torch.Generator().manual_seed(5))
+    y = torch.randint(0, 3, (n,), generator=torch.Generator().manual_seed(6))
+    data = [(x[i], y[i]) for i in range(n)]
+    net = torch.nn.Linear(6, 3)
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = net
+
+        def forward(self, b):
+            return (self.lin(b[0]), b[1])
+
+    class Obj(torch.nn.Module):
+        def forward(self, b):
+            return torch.nn.functional.cross_entropy(b[0], b[1])
+
+    losses = []
+
+    class Rec(rocket.Capsule):
+        def __init__(self):
+            super().__init__(priority=10)
+
+        def launch(self, attrs=None):
+            losses.append(float(attrs.looper.state.loss))
+
+    opt = torch.optim.SGD(net.parameters(), lr=0.5)
+    rocket.Launcher(
+        [rocket.Looper([rocket.Dataset(data, batch_size=bs), rocket.Module(Net(), [rocket.Loss(Obj()), rocket.Optimizer(opt)]),
+                        Rec()], progress=False)],
+        num_procs=world, cpu=True, destroy_process_group_after_launch=(world > 1),
+    ).launch()
+    if out_file:
+        with open(out_file, "w") as fh:
+            json.dump(dict(w=[p.tolist() for p in net.parameters()], losses=losses), fh)
+    return net, losses
+
+
+def _launcher_worker(rank, world, port, out):
+    _env(rank, world, port)
+    _train(world, os.path.join(out, f"r{rank}.json"), bs=4)
+
+
+def test_launcher_two_ranks_equals_global_batch(tmp_path):
+    _run(_launcher_worker, 2, str(tmp_path))
+    net, losses = _train(1, None, bs=8)  # same global batches: rank0 gets batches 0,2,.. rank1 1,3,..
+    for r in range(2):
+        got = json.load(open(tmp_path / f"r{r}.json"))
+        for g, p in zip(got["w"], net.parameters()):
+            torch.testing.assert_close(torch.tensor(g), p.detach(), rtol=1e-5, atol=1e-6)
+        # reported loss = mean over ranks of per-rank mean == global-batch mean
+        assert got["losses"] == pytest.approx(losses, rel=1e-5)
+
+
+# ------------------------------------------------------- gather_for_metrics
+def _meter_worker(rank, world, port, out):
+    _env(rank, world, port)
+    import rocket_amd as rocket
+
+    seen = []
+
+    class Collect(rocket.Metric):
+        def launch(self, attrs=None):
+            seen.extend(attrs.batch["idx"].tolist())
+
+        def reset(self, attrs=None):
+            pass
+
+    data = [{"idx": torch.tensor(i)} for i in range(10)]  # 10 samples, bs 3, W 2 -> padded to 12
+    rocket.Launcher(
+        [rocket.Looper([rocket.Dataset(data, batch_size=3), rocket.Meter([Collect()], keys=["idx"])],
+                       grad_enabled=False, progress=False)],
+        num_procs=world, cpu=True,
+    ).launch()
+    with open(os.path.join(out, f"m{rank}.json"), "w") as fh:
+        json.dump(seen, fh)
+
+
+def test_gather_for_metrics_truncates_padding(tmp_path):
+    _run(_meter_worker, 2, str(tmp_path))
+    for r in range(2):
+        seen = json.load(open(tmp_path / f"m{r}.json"))
+        assert sorted(seen) == list(range(10))

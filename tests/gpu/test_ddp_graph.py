@@ -1,0 +1,91 @@
+"""Data-parallel captured steps (graph A -> host all-reduce -> graph B) vs eager, 2 ranks on one GPU.
+
+The ranks share ``cuda:0`` and talk over gloo (``ROCKET_DIST_BACKEND=gloo``):
+this rehearses the multi-GPU code path — deferred bucket reduction, side-channel
+loss averaging, two-part graphs — on the single-GPU box.
+"""
+
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROCKET_DIST_BACKEND="gloo")
+    import rocket_amd as rocket
+    from rocket_amd.core.capsule import Capsule
+    from rocket_amd.models import CrossEntropy, LeNet
+    from rocket_amd.ops.optim import FusedAdamW
+
+    class Rec(Capsule):
+        def __init__(self):
+            super().__init__(priority=10)
+            self.losses = []
+
+        def launch(self, attrs=None):
+            if attrs.looper.state.loss is not None:
+                self.losses.append(attrs.looper.state.loss)
+
+    res = {}
+    for capture in (False, True):
+        dev = torch.device("cuda", 0)
+        g = torch.Generator(device=dev).manual_seed(3)
+        x = torch.rand(256 * 24, 1, 28, 28, generator=g, device=dev)
+        y = torch.randint(0, 10, (256 * 24,), generator=g, device=dev)
+        torch.manual_seed(0)
+        net = LeNet(fused=True)
+        opt = FusedAdamW(net.parameters(), lr=2e-3)
+        rec = Rec()
+        mod = rocket.Module(net, [rocket.Loss(CrossEntropy(fused=True)), rocket.Optimizer(opt)], capture=capture,
+                            warmup=2)
+        rocket.Launcher(
+            [rocket.Looper([rocket.Dataset(rocket.DeviceTensorDataset(x, y), batch_size=128), mod, rec],
+                           repeats=12, progress=False)],
+            logging_dir=os.path.join(out_dir, f"logs{int(capture)}"),
+            mixed_precision="bf16",
+            gradient_accumulation_steps=2,
+            num_procs=world,
+            destroy_process_group_after_launch=False,
+        ).launch()
+        torch.cuda.synchronize()
+        res[str(capture)] = dict(
+            losses=[float(v) for v in rec.losses],
+            w=float(sum(p.detach().double().sum() for p in net.parameters())),
+            replays=(mod._graphs.replays if mod._graphs is not None else 0),
+            reason=(mod._graphs.disabled_reason if mod._graphs is not None else None),
+        )
+    with open(os.path.join(out_dir, f"r{rank}.json"), "w") as fh:
+        json.dump(res, fh)
+    import torch.distributed as dist
+
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_graph_two_ranks(tmp_path):
+    port = _free_port()
+    mp.start_processes(_worker, args=(2, port, str(tmp_path)), nprocs=2, start_method="spawn", join=True)
+    r = [json.load(open(tmp_path / f"r{i}.json")) for i in range(2)]
+    for rank in range(2):
+        e, g = r[rank]["False"], r[rank]["True"]
+        assert g["replays"] > 0 and g["reason"] == "released", g
+        assert len(e["losses"]) == len(g["losses"]) > 0
+        for a, b in zip(e["losses"], g["losses"]):
+            assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (e["losses"], g["losses"])
+        assert abs(e["w"] - g["w"]) <= 1e-3 * max(1.0, abs(e["w"])), (e["w"], g["w"])
+    # replicas stay identical across ranks, and the reported loss is the cross-rank mean
+    assert abs(r[0]["True"]["w"] - r[1]["True"]["w"]) < 1e-6 * max(1.0, abs(r[0]["True"]["w"]))
+    assert r[0]["True"]["losses"] == pytest.approx(r[1]["True"]["losses"], rel=1e-6)
