@@ -194,6 +194,9 @@ class Optimizer(Capsule):
             inner.refresh_hyper()  # pointers are frozen into the graph; only lr & co. can change
 
     def graph_device(self, attrs: Attributes) -> None:
+        return None  # the update needs reduced gradients: phase B
+
+    def graph_device_synced(self, attrs: Attributes) -> None:
         if self._accelerator.sync_gradients:
             self._optimizer.optimizer.launch(zero_grads=True)
 

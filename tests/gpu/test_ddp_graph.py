@@ -47,7 +47,7 @@ def _worker(rank, world, port, out_dir):
         y = torch.randint(0, 10, (256 * 24,), generator=g, device=dev)
         torch.manual_seed(0)
         net = LeNet(fused=True)
-        opt = FusedAdamW(net.parameters(), lr=2e-3)
+        opt = FusedAdamW(net.parameters(), lr=1e-2)
         rec = Rec()
         mod = rocket.Module(net, [rocket.Loss(CrossEntropy(fused=True)), rocket.Optimizer(opt)], capture=capture,
                             warmup=2)
