@@ -16,6 +16,12 @@ does the full work: batch gather, forward, loss, backward, gradient all-reduce
 
 Extra flags (for A/B runs): ``--impl torch`` uses stock PyTorch ops instead of
 the fused HIP kernels; ``--no-graph`` disables HIP-graph capture of the step.
+
+``--model`` selects the other BASELINE configs with the same harness:
+``resnet18`` (CIFAR-10 shape 3×32×32, 10 classes, per-GPU batch 256), ``resnet50``
+(ImageNet shape 3×224×224, 1000 classes, batch 256) and ``vit_b16`` (3×224×224,
+1000 classes, batch 128) — all bf16 autocast, DDP over RCCL for N>1, SGD(momentum)
+for the ResNets and AdamW for ViT, synthetic HBM-resident data (stored bf16).
 """
 
 from __future__ import annotations
@@ -28,7 +34,19 @@ import time
 
 import torch
 
+# MIOpen: benchmark-based solution search at first use (done in the untimed warm-up).  The
+# heuristic-only FAST mode picks ~50x slower NHWC bf16 kernels (bench/conv_probe.py).
+os.environ.setdefault("MIOPEN_FIND_MODE", "NORMAL")
+
 BASELINE_METRIC = "samples/sec (whole node) MNIST ConvNet at 1/2/4/8 MI355X; step-time p50"
+
+MODELS = {
+    # name: (per-GPU batch, input shape, classes, description)
+    "lenet": (1024, (1, 28, 28), 10, "LeNet-5 MNIST 2-conv CNN (reference examples/mnist.py)"),
+    "resnet18": (256, (3, 32, 32), 10, "ResNet-18 CIFAR-10 shape"),
+    "resnet50": (256, (3, 224, 224), 1000, "ResNet-50 ImageNet shape"),
+    "vit_b16": (128, (3, 224, 224), 1000, "ViT-Base/16 ImageNet shape"),
+}
 
 
 def _baseline_value(n_gpus: int):
@@ -50,9 +68,11 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch")
+    ap.add_argument("--model", choices=sorted(MODELS), default="lenet")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default per model)")
     ap.add_argument("--impl", choices=["fused", "torch"], default="fused")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="force HIP-graph capture for the non-LeNet models")
     ap.add_argument("--mp", default="bf16")
     ap.add_argument("--cpu", action="store_true")
     args = ap.parse_args()
@@ -75,19 +95,35 @@ def main() -> int:
 
         ops.require_native()
 
+    bs_default, in_shape, classes, desc = MODELS[args.model]
+    args.batch = args.batch or bs_default
     total_iters = args.warmup + args.steps
     n = (total_iters + 1) * args.batch * world  # one epoch covers the whole run on every rank
     g = torch.Generator(device=dev).manual_seed(1234)
-    x = torch.rand(n, 1, 28, 28, generator=g, device=dev)
-    y = torch.randint(0, 10, (n,), generator=g, device=dev)
+    img_dtype = torch.float32 if args.model == "lenet" else torch.bfloat16
+    x = torch.rand((n,) + in_shape, generator=g, device=dev, dtype=img_dtype)
+    y = torch.randint(0, classes, (n,), generator=g, device=dev)
     data = DeviceTensorDataset(x, y)
 
     torch.manual_seed(0)
-    net = LeNet(fused=fused)
-    if fused:
-        from rocket_amd.ops.optim import FusedAdamW
+    if args.model == "lenet":
+        net = LeNet(fused=fused)
+    else:
+        from rocket_amd import models
 
-        opt = FusedAdamW(net.parameters())
+        net = {"resnet18": lambda: models.resnet18(classes), "resnet50": lambda: models.resnet50(classes),
+               "vit_b16": lambda: models.vit_b16(classes)}[args.model]()
+        if on_gpu:
+            net = net.to(memory_format=torch.channels_last)
+    if fused:
+        from rocket_amd.ops.optim import FusedAdamW, FusedSGD
+
+        if args.model.startswith("resnet"):
+            opt = FusedSGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+        else:
+            opt = FusedAdamW(net.parameters())
+    elif args.model.startswith("resnet"):
+        opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5, foreach=True)
     else:
         opt = torch.optim.AdamW(net.parameters(), foreach=True)
     sched = torch.optim.lr_scheduler.StepLR(opt, 100)
@@ -100,7 +136,9 @@ def main() -> int:
                     rocket.Module(
                         net,
                         [rocket.Loss(CrossEntropy(fused=fused)), rocket.Optimizer(opt), rocket.Scheduler(sched)],
-                        capture=fused and not args.no_graph,
+                        # graph capture pays off for launch-bound steps (LeNet); the big models are
+                        # compute-bound and MIOpen/hipBLASLt run slightly faster eagerly
+                        capture=fused and not args.no_graph and (args.model == "lenet" or args.graph),
                     ),
                     timer,
                 ],
@@ -129,10 +167,10 @@ def main() -> int:
         p50 = summ.get("step_ms_p50", 0.0)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
-    base = _baseline_value(world)
+    base = _baseline_value(world) if args.model == "lenet" else None
     if ctx.rank == 0:
         rec = {
-            "metric": BASELINE_METRIC,
+            "metric": BASELINE_METRIC if args.model == "lenet" else f"samples/sec (whole node) {desc}; step-time p50",
             "value": round(value, 1),
             "unit": "samples/s",
             "n_gpus": world,
@@ -146,14 +184,15 @@ def main() -> int:
             "dtype": "bf16" if args.mp == "bf16" else "fp32",
             "data": "synthetic (random 1x28x28 MNIST-shaped images/labels in HBM, random-init weights)",
             "config": {
-                "model": "LeNet-5 MNIST 2-conv CNN (reference examples/mnist.py)",
+                "model": desc,
                 "global_batch": args.batch * world,
                 "per_gpu_batch": args.batch,
                 "seq_len": None,
-                "input_shape": [1, 28, 28],
-                "optimizer": "AdamW + StepLR(100)",
+                "input_shape": list(in_shape),
+                "optimizer": ("SGD(momentum)" if args.model.startswith("resnet") else "AdamW") + " + StepLR(100)",
                 "parallelism": f"dp{world}",
-                "impl": ("fused-hip" + ("" if args.no_graph else "+hipgraph")) if fused else "torch-eager",
+                "impl": ("fused-hip" + ("+hipgraph" if (not args.no_graph and (args.model == "lenet" or args.graph)) else ""))
+                if fused else "torch-eager",
             },
             "wall_s": round(wall, 2),
         }

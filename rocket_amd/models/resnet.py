@@ -1,0 +1,127 @@
+"""ResNet-18 (CIFAR-10 variant) and ResNet-50 (ImageNet shape) for the BASELINE DDP configs.
+
+MI355X layout: activations are channels-last (NHWC) end to end — MIOpen's bf16
+convolutions prefer it and the fused BatchNorm kernels (:mod:`rocket_amd.ops.norm`)
+reduce over contiguous channels.  Every ``conv → BN (→ +identity) → ReLU`` tail is
+one BN-statistics launch plus one fused apply launch (``BatchNormAct2d``), so the
+residual add and the ReLU never make their own pass over HBM.
+
+The forward follows the reference batch contract: ``(img, label) -> (img, label, logits)``.
+Architecture per He et al. (basic/bottleneck blocks, stride on the 3×3 conv as in
+"ResNet v1.5"); the CIFAR variant uses a 3×3 stride-1 stem without max-pool.
+"""
+
+from __future__ import annotations
+
+from typing import List, Type
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from rocket_amd.ops.norm import BatchNormAct2d
+
+
+def _conv(cin, cout, k, stride=1):
+    return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin: int, width: int, stride: int = 1):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = _conv(cin, width, 3, stride)
+        self.bn1 = BatchNormAct2d(width, relu=True)
+        self.conv2 = _conv(width, cout, 3)
+        self.bn2 = BatchNormAct2d(cout, relu=True)  # relu(bn2(.) + identity), fused
+        self.down = None
+        if stride != 1 or cin != cout:
+            self.down = nn.Sequential(_conv(cin, cout, 1, stride), BatchNormAct2d(cout))
+
+    def forward(self, x):
+        identity = x if self.down is None else self.down(x)
+        out = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(out), residual=identity)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, width: int, stride: int = 1):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = _conv(cin, width, 1)
+        self.bn1 = BatchNormAct2d(width, relu=True)
+        self.conv2 = _conv(width, width, 3, stride)
+        self.bn2 = BatchNormAct2d(width, relu=True)
+        self.conv3 = _conv(width, cout, 1)
+        self.bn3 = BatchNormAct2d(cout, relu=True)
+        self.down = None
+        if stride != 1 or cin != cout:
+            self.down = nn.Sequential(_conv(cin, cout, 1, stride), BatchNormAct2d(cout))
+
+    def forward(self, x):
+        identity = x if self.down is None else self.down(x)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), residual=identity)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block: Type[nn.Module], layers: List[int], num_classes: int = 1000, cifar_stem: bool = False,
+                 zero_init_residual: bool = True):
+        super().__init__()
+        self.cifar_stem = cifar_stem
+        if cifar_stem:
+            self.stem = nn.Sequential(_conv(3, 64, 3), BatchNormAct2d(64, relu=True))
+        else:
+            self.stem = nn.Sequential(_conv(3, 64, 7, 2), BatchNormAct2d(64, relu=True))
+        cin = 64
+        stages = []
+        for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
+            blocks = []
+            for j in range(n):
+                stride = 2 if (i > 0 and j == 0) else 1
+                blocks.append(block(cin, width, stride))
+                cin = width * block.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.fc = nn.Linear(cin, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                last = getattr(m, "bn3", None) if isinstance(m, Bottleneck) else getattr(m, "bn2", None)
+                if isinstance(m, (Bottleneck, BasicBlock)) and last is not None:
+                    nn.init.zeros_(last.weight)
+
+    def logits(self, x: torch.Tensor) -> torch.Tensor:
+        if not torch.is_autocast_enabled(x.device.type):
+            x = x.to(self.fc.weight.dtype if hasattr(self, "fc") else self.head.weight.dtype)  # bf16-stored images
+        x = x.contiguous(memory_format=torch.channels_last)
+        x = self.stem(x)
+        if not self.cifar_stem:
+            x = F.max_pool2d(x, 3, 2, 1)
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+    def forward(self, batch):
+        if isinstance(batch, torch.Tensor):
+            return self.logits(batch)
+        img, label = batch[0], batch[1]
+        return (img, label, self.logits(img))
+
+
+def resnet18(num_classes: int = 10, cifar: bool = True) -> ResNet:
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes=num_classes, cifar_stem=cifar)
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes=num_classes)

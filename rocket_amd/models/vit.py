@@ -1,0 +1,99 @@
+"""ViT-Base/16 (Dosovitskiy et al.) for the BASELINE "ViT-B/16 bf16 DDP" config.
+
+Pre-norm encoder, 12 layers × (MHSA 12 heads + MLP 3072), 224×224 input → 196
+patches + [CLS] = 197 tokens, width 768.
+
+MI355X path: LayerNorm is the one-wave-per-row HIP kernel emitting bf16 straight
+into the next GEMM (:class:`~rocket_amd.ops.norm.FusedLayerNorm`); the GEMMs run
+on the library path (hipBLASLt, bias fused into the epilogue via ``addmm``); GELU
+and the scaled attention softmax are HIP kernels (:mod:`rocket_amd.ops.activation`)
+whose backward recompute from saved inputs/outputs.  The residual stream stays
+fp32 (standard AMP numerics); everything feeding a GEMM is bf16.
+
+Forward contract: ``(img, label) -> (img, label, logits)``.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from rocket_amd.ops.activation import attention, gelu
+from rocket_amd.ops.norm import FusedLayerNorm
+
+
+class Attention(nn.Module):
+    def __init__(self, dim: int, heads: int):
+        super().__init__()
+        self.heads = heads
+        self.qkv = nn.Linear(dim, 3 * dim)
+        self.proj = nn.Linear(dim, dim)
+
+    def forward(self, x):
+        B, L, D = x.shape
+        qkv = self.qkv(x).view(B, L, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
+        o = attention(qkv[0], qkv[1], qkv[2])
+        return self.proj(o.transpose(1, 2).reshape(B, L, D))
+
+
+class Mlp(nn.Module):
+    def __init__(self, dim: int, hidden: int):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+    def forward(self, x):
+        return self.fc2(gelu(self.fc1(x)))
+
+
+class Block(nn.Module):
+    def __init__(self, dim: int, heads: int, mlp_ratio: float = 4.0):
+        super().__init__()
+        self.norm1 = FusedLayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, heads)
+        self.norm2 = FusedLayerNorm(dim, eps=1e-6)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+
+    def forward(self, x):
+        x = x + self.attn(self.norm1(x))
+        return x + self.mlp(self.norm2(x))
+
+
+class VisionTransformer(nn.Module):
+    def __init__(self, img_size=224, patch=16, in_chans=3, num_classes=1000, dim=768, depth=12, heads=12,
+                 mlp_ratio=4.0):
+        super().__init__()
+        self.patch = patch
+        self.patch_embed = nn.Conv2d(in_chans, dim, patch, stride=patch)
+        n = (img_size // patch) ** 2
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, n + 1, dim))
+        self.blocks = nn.Sequential(*[Block(dim, heads, mlp_ratio) for _ in range(depth)])
+        self.norm = FusedLayerNorm(dim, eps=1e-6)
+        self.head = nn.Linear(dim, num_classes)
+        nn.init.trunc_normal_(self.pos_embed, std=0.02)
+        nn.init.trunc_normal_(self.cls_token, std=0.02)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                nn.init.zeros_(m.bias)
+
+    def logits(self, x):
+        if not torch.is_autocast_enabled(x.device.type):
+            x = x.to(self.fc.weight.dtype if hasattr(self, "fc") else self.head.weight.dtype)  # bf16-stored images
+        x = self.patch_embed(x).flatten(2).transpose(1, 2)  # [B, 196, D]
+        x = torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1)
+        x = x.float() + self.pos_embed  # fp32 residual stream
+        x = self.blocks(x)
+        return self.head(self.norm(x)[:, 0])
+
+    def forward(self, batch):
+        if isinstance(batch, torch.Tensor):
+            return self.logits(batch)
+        img, label = batch[0], batch[1]
+        return (img, label, self.logits(img))
+
+
+def vit_b16(num_classes: int = 1000, img_size: int = 224) -> VisionTransformer:
+    return VisionTransformer(img_size=img_size, num_classes=num_classes)

@@ -1,0 +1,155 @@
+// Elementwise / row-wise activation kernels for the transformer path (ViT-B/16):
+//
+//   gelu_fwd     y = gelu(x) (exact erf form), bf16/f32 in, bf16/f32 out, grid-stride.
+//   gelu_bwd     dx = dy * gelu'(x), recomputed from the saved pre-activation (no extra tensor).
+//   softmax_fwd  y = softmax(x * scale) over rows of length L (attention scores), one wave per
+//                row, values held in registers (L <= 1024): one read, one write.
+//   softmax_bwd  dx = scale * y * (dy - sum(dy * y)), one wave per row.
+#include "rk_common.h"
+
+using namespace rk;
+
+namespace {
+
+constexpr int T = 256;
+
+__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(T) gelu_fwd_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * T + threadIdx.x; i < n; i += (int64_t)gridDim.x * T)
+    Ld<TO>::put(y, i, gelu(Ld<TI>::get(x, i)));
+}
+
+template <typename TI, typename TG>
+__global__ void __launch_bounds__(T) gelu_bwd_kernel(const TG* __restrict__ dy, const TI* __restrict__ x,
+                                                     TI* __restrict__ dx, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * T + threadIdx.x; i < n; i += (int64_t)gridDim.x * T)
+    Ld<TI>::put(dx, i, Ld<TG>::get(dy, i) * gelu_grad(Ld<TI>::get(x, i)));
+}
+
+constexpr int SM_MAXJ = 16;  // 16 x 64 lanes = L <= 1024
+
+template <typename TI, typename TO, int NJ>
+__global__ void __launch_bounds__(T) softmax_fwd_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t rows,
+                                                        int L, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (T / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const TI* xr = x + row * L;
+  float v[NJ];
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 64 + lane;
+    v[j] = c < L ? Ld<TI>::get(xr, c) * scale : -INFINITY;
+    m = fmaxf(m, v[j]);
+  }
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    v[j] = (j * 64 + lane) < L ? __expf(v[j] - m) : 0.f;
+    s += v[j];
+  }
+  const float inv = 1.f / wave_sum(s);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 64 + lane;
+    if (c < L) Ld<TO>::put(y + row * L, c, v[j] * inv);
+  }
+}
+
+template <typename TY, typename TG, int NJ>
+__global__ void __launch_bounds__(T) softmax_bwd_kernel(const TG* __restrict__ dy, const TY* __restrict__ y,
+                                                        TG* __restrict__ dx, int64_t rows, int L, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (T / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float yv[NJ], gv[NJ];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 64 + lane;
+    yv[j] = c < L ? Ld<TY>::get(y + row * L, c) : 0.f;
+    gv[j] = c < L ? Ld<TG>::get(dy + row * L, c) : 0.f;
+    s += yv[j] * gv[j];
+  }
+  s = wave_sum(s);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 64 + lane;
+    if (c < L) Ld<TG>::put(dx + row * L, c, scale * yv[j] * (gv[j] - s));
+  }
+}
+
+int egrid(int64_t n) {
+  int64_t g = (n + T - 1) / T;
+  return (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+RK_API int rk_gelu_fwd(int dti, int dto, const void* x, void* y, int64_t n, hipStream_t s) {
+  const int g = egrid(n);
+  if (dti == BF16 && dto == BF16) gelu_fwd_kernel<uint16_t, uint16_t><<<g, T, 0, s>>>((const uint16_t*)x, (uint16_t*)y, n);
+  else if (dti == BF16) gelu_fwd_kernel<uint16_t, float><<<g, T, 0, s>>>((const uint16_t*)x, (float*)y, n);
+  else if (dto == BF16) gelu_fwd_kernel<float, uint16_t><<<g, T, 0, s>>>((const float*)x, (uint16_t*)y, n);
+  else gelu_fwd_kernel<float, float><<<g, T, 0, s>>>((const float*)x, (float*)y, n);
+  return (int)hipGetLastError();
+}
+
+// dti: dtype of x / dx; dtg: dtype of dy
+RK_API int rk_gelu_bwd(int dti, int dtg, const void* dy, const void* x, void* dx, int64_t n, hipStream_t s) {
+  const int g = egrid(n);
+  if (dti == BF16 && dtg == BF16) gelu_bwd_kernel<uint16_t, uint16_t><<<g, T, 0, s>>>((const uint16_t*)dy, (const uint16_t*)x, (uint16_t*)dx, n);
+  else if (dti == BF16) gelu_bwd_kernel<uint16_t, float><<<g, T, 0, s>>>((const float*)dy, (const uint16_t*)x, (uint16_t*)dx, n);
+  else if (dtg == BF16) gelu_bwd_kernel<float, uint16_t><<<g, T, 0, s>>>((const uint16_t*)dy, (const float*)x, (float*)dx, n);
+  else gelu_bwd_kernel<float, float><<<g, T, 0, s>>>((const float*)dy, (const float*)x, (float*)dx, n);
+  return (int)hipGetLastError();
+}
+
+RK_API int rk_softmax_fwd(int dti, int dto, const void* x, void* y, int64_t rows, int L, float scale, hipStream_t s) {
+  if (L <= 0 || L > 64 * SM_MAXJ) return (int)hipErrorInvalidValue;
+  const int grid = (int)((rows + T / 64 - 1) / (T / 64));
+  const int nj = (L + 63) / 64;
+#define RK_SF(TI, TO, NJ) softmax_fwd_kernel<TI, TO, NJ><<<grid, T, 0, s>>>((const TI*)x, (TO*)y, rows, L, scale)
+#define RK_SFN(TI, TO)                 \
+  if (nj <= 2) RK_SF(TI, TO, 2);       \
+  else if (nj <= 4) RK_SF(TI, TO, 4);  \
+  else if (nj <= 8) RK_SF(TI, TO, 8);  \
+  else RK_SF(TI, TO, 16);
+  if (dti == BF16 && dto == BF16) { RK_SFN(uint16_t, uint16_t) }
+  else if (dti == BF16) { RK_SFN(uint16_t, float) }
+  else if (dto == BF16) { RK_SFN(float, uint16_t) }
+  else { RK_SFN(float, float) }
+#undef RK_SFN
+#undef RK_SF
+  return (int)hipGetLastError();
+}
+
+// dty: dtype of y; dtg: dtype of dy and dx
+RK_API int rk_softmax_bwd(int dty, int dtg, const void* dy, const void* y, void* dx, int64_t rows, int L, float scale,
+                          hipStream_t s) {
+  if (L <= 0 || L > 64 * SM_MAXJ) return (int)hipErrorInvalidValue;
+  const int grid = (int)((rows + T / 64 - 1) / (T / 64));
+  const int nj = (L + 63) / 64;
+#define RK_SB(TY, TG, NJ) softmax_bwd_kernel<TY, TG, NJ><<<grid, T, 0, s>>>((const TG*)dy, (const TY*)y, (TG*)dx, rows, L, scale)
+#define RK_SBN(TY, TG)                 \
+  if (nj <= 2) RK_SB(TY, TG, 2);       \
+  else if (nj <= 4) RK_SB(TY, TG, 4);  \
+  else if (nj <= 8) RK_SB(TY, TG, 8);  \
+  else RK_SB(TY, TG, 16);
+  if (dty == BF16 && dtg == BF16) { RK_SBN(uint16_t, uint16_t) }
+  else if (dty == BF16) { RK_SBN(uint16_t, float) }
+  else if (dtg == BF16) { RK_SBN(float, uint16_t) }
+  else { RK_SBN(float, float) }
+#undef RK_SBN
+#undef RK_SB
+  return (int)hipGetLastError();
+}

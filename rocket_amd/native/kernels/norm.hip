@@ -1,0 +1,679 @@
+// Normalisation kernels: BatchNorm over channels-last activations and LayerNorm over rows
+// (the BatchNorm of ResNet-18/50 and the LayerNorm of ViT-B/16).
+//
+// BatchNorm (training), x viewed as [R = N*H*W][C] (channels-last, C contiguous):
+//   bn_stats      grid (C/64, RB): a block reduces rows [rb*rpb, ...) x 64 channels; each thread
+//                 owns 8 consecutive channels (one 16-byte load per row) and accumulates
+//                 shifted sums (pivot = row 0, kills E[x^2]-E[x]^2 cancellation).  Per-block
+//                 partials go to a workspace; the LAST block of each channel column (ticket)
+//                 merges them, writes mean / invstd, the fused scale/shift (a = g*invstd,
+//                 b = beta - mean*a) and updates the running statistics (unbiased var).
+//   bn_apply      y = relu?(x*a + b + residual?), 8 channels per thread, coefficients in registers.
+//   bn_bwd_reduce per channel sum(dy') and sum(dy'*xhat), dy' = dy*[y>0] when ReLU was fused;
+//                 the last block writes dgamma/dbeta (accumulated into the grads) and the two
+//                 per-channel coefficients of the input gradient.
+//   bn_bwd_apply  dx = a*(dy' - k1 - xhat*k2) (folded to P*dy' + Q*x + S) and d(residual) = dy'.
+// LayerNorm over the last dim (C <= 4096), one wave per row:
+//   ln_fwd        two-pass mean/var in registers, y = xhat*g + b (bf16 or f32 out),
+//                 saves mean/rstd.
+//   ln_bwd        dx per row; dgamma/dbeta column partials per block + last-block reduction,
+//                 accumulated into the parameter gradients.
+#include "rk_common.h"
+
+using namespace rk;
+
+namespace {
+
+constexpr int BN_T = 256;        // threads per block
+constexpr int BN_CT = 64;        // channels per block column
+constexpr int BN_RG = BN_T / 8;  // row groups per block pass (each thread: 8 channels)
+constexpr int BN_U = 4;          // rows in flight per thread per loop iteration
+
+template <typename T> struct V8;
+template <> struct V8<uint16_t> {
+  static __device__ __forceinline__ void load(const uint16_t* p, float* v) {
+    const uint4 u = *(const uint4*)p;
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = __uint_as_float(w[k] << 16);
+      v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store(uint16_t* p, const float* v) {
+    uint4 u;
+    uint32_t* w = (uint32_t*)&u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
+    *(uint4*)p = u;
+  }
+};
+template <> struct V8<float> {
+  static __device__ __forceinline__ void load(const float* p, float* v) {
+    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float* v) {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+// reduce per-thread [8] accumulators over the BN_RG row groups of the block into red[64]
+__device__ __forceinline__ void reduce_rowgroups(const float* v, float (*lds)[BN_CT + 1], float* out) {
+  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) lds[rg][cg * 8 + k] = v[k];
+  __syncthreads();
+  if (threadIdx.x < BN_CT) {
+    float s = 0.f;
+    for (int g = 0; g < BN_RG; ++g) s += lds[g][threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+struct BnStatsArgs {
+  const void* x;
+  int64_t R;
+  int C, rpb;
+  float* part;  // [RB][2][C]
+  unsigned* counters;  // [C/64]
+  const float* gamma;
+  const float* beta;
+  float* mean;
+  float* invstd;
+  float* scale;  // a
+  float* shift;  // b
+  float* run_mean;
+  float* run_var;
+  int64_t* nbt;  // num_batches_tracked, may be null
+  float momentum, eps;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
+  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ float s1[BN_CT], s2[BN_CT];
+  __shared__ int flag;
+  const T* x = (const T*)a.x;
+  const int c0 = blockIdx.x * BN_CT;
+  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int c = c0 + cg * 8;
+  const bool cok = c < a.C;  // C % 8 == 0 (host check)
+  const int64_t r0 = (int64_t)blockIdx.y * a.rpb;
+  const int64_t r1 = min(a.R, r0 + a.rpb);
+  float piv[8], acc1[8], acc2[8];
+  V8<T>::load(x + (cok ? c : 0), piv);  // pivot: row 0 (same for every block)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc1[k] = acc2[k] = 0.f;
+  for (int64_t r = r0 + rg; r < r1; r += BN_U * BN_RG) {
+    float v[BN_U][8];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) V8<T>::load(x + min(r + u * BN_RG, r1 - 1) * a.C + (cok ? c : 0), v[u]);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const bool ok = r + u * BN_RG < r1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = ok ? v[u][k] - piv[k] : 0.f;
+        acc1[k] += d;
+        acc2[k] += d * d;
+      }
+    }
+  }
+  if (!cok) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc1[k] = acc2[k] = 0.f;
+  }
+  reduce_rowgroups(acc1, lds, s1);
+  reduce_rowgroups(acc2, lds, s2);
+  float* part = a.part + (int64_t)blockIdx.y * 2 * a.C;
+  if (threadIdx.x < BN_CT && c0 + threadIdx.x < a.C) {
+    part[c0 + threadIdx.x] = s1[threadIdx.x];
+    part[a.C + c0 + threadIdx.x] = s2[threadIdx.x];
+  }
+  // last block of this channel column finalises
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned t = __hip_atomic_fetch_add(a.counters + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = (t == gridDim.y - 1);
+    if (flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!flag) return;
+  // 4 threads per channel split the RB partials
+  const int ch = threadIdx.x >> 2, sub = threadIdx.x & 3;
+  const int cc = c0 + ch;
+  float t1 = 0.f, t2 = 0.f;
+  if (cc < a.C) {
+    for (int b = sub; b < (int)gridDim.y; b += 4) {
+      const float* p = a.part + (int64_t)b * 2 * a.C;
+      t1 += __builtin_nontemporal_load(p + cc);
+      t2 += __builtin_nontemporal_load(p + a.C + cc);
+    }
+  }
+  t1 += __shfl_xor(t1, 1, 64);
+  t1 += __shfl_xor(t1, 2, 64);
+  t2 += __shfl_xor(t2, 1, 64);
+  t2 += __shfl_xor(t2, 2, 64);
+  if (sub == 0 && cc < a.C) {
+    const double n = (double)a.R;
+    const float p0 = Ld<T>::get(x, cc);  // the pivot the partial sums were shifted by
+    const float dm = (float)(t1 / n);
+    const float mean = p0 + dm;
+    float var = (float)(t2 / n) - dm * dm;
+    var = fmaxf(var, 0.f);
+    const float inv = rsqrtf(var + a.eps);
+    a.mean[cc] = mean;
+    a.invstd[cc] = inv;
+    const float g = a.gamma ? a.gamma[cc] : 1.f;
+    const float bb = a.beta ? a.beta[cc] : 0.f;
+    a.scale[cc] = g * inv;
+    a.shift[cc] = bb - mean * g * inv;
+    if (a.run_mean) {
+      const float unb = a.R > 1 ? var * (float)(n / (n - 1.0)) : var;
+      a.run_mean[cc] = (1.f - a.momentum) * a.run_mean[cc] + a.momentum * mean;
+      a.run_var[cc] = (1.f - a.momentum) * a.run_var[cc] + a.momentum * unb;
+    }
+  }
+  if (threadIdx.x == 0 && blockIdx.x == 0 && a.nbt) a.nbt[0] += 1;
+  if (threadIdx.x == 0) __hip_atomic_store(a.counters + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Elementwise passes: thread t owns channel vector cv = t % CV (CV = C/8 <= 256) for the whole
+// launch, so its per-channel coefficients live in registers (loaded once), and walks rows
+// r = r0 + t / CV, stepping by RPP = BN_T / CV rows; 4 rows per iteration with clamped
+// (always valid) addresses keep 4 independent 16-byte loads in flight per tensor.
+// y = relu?(x*a + b + res?)
+template <typename T, typename TO>
+__global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x, const TO* __restrict__ res,
+                                                        const float* __restrict__ scale, const float* __restrict__ shift,
+                                                        TO* __restrict__ y, int64_t R, int C, int relu, int rpb) {
+  const int CV = C >> 3, RPP = BN_T / CV;
+  if ((int)threadIdx.x >= RPP * CV) return;
+  const int cv = threadIdx.x % CV, c = cv * 8;
+  float A[8], B[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    A[k] = scale[c + k];
+    B[k] = shift[c + k];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = min(R, r0 + rpb);
+  for (int64_t r = r0 + threadIdx.x / CV; r < r1; r += BN_U * RPP) {
+    float v[BN_U][8], q[BN_U][8];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const int64_t ru = min(r + u * RPP, r1 - 1);
+      V8<T>::load(x + ru * C + c, v[u]);
+      if (res) V8<TO>::load(res + ru * C + c, q[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float o = v[u][k] * A[k] + B[k];
+        if (res) o += q[u][k];
+        if (relu) o = fmaxf(o, 0.f);
+        v[u][k] = o;
+      }
+      if (r + u * RPP < r1) V8<TO>::store(y + (r + u * RPP) * C + c, v[u]);
+    }
+  }
+}
+
+struct BnBwdArgs {
+  const void* dy;
+  const void* x;
+  const void* y;  // fused-ReLU output (mask), may be null
+  int64_t R;
+  int C, rpb;
+  const float* mean;
+  const float* invstd;
+  float* part;
+  unsigned* counters;
+  float* dgamma;  // accumulated (+=), may be null
+  float* dbeta;
+  const float* scale;  // a = gamma * invstd
+  float* coef;         // [3][C]: dx = P*dy' + Q*x + S
+};
+
+template <typename T, typename TO>
+__global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
+  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ float s1[BN_CT], s2[BN_CT];
+  __shared__ int flag;
+  const TO* dy = (const TO*)a.dy;
+  const T* x = (const T*)a.x;
+  const TO* y = (const TO*)a.y;
+  const int c0 = blockIdx.x * BN_CT;
+  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int c = c0 + cg * 8;
+  const bool cok = c < a.C;
+  const int cs = cok ? c : 0;
+  float mu[8], is[8], acc1[8], acc2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = a.mean[cs + k];
+    is[k] = a.invstd[cs + k];
+    acc1[k] = acc2[k] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * a.rpb;
+  const int64_t r1 = min(a.R, r0 + a.rpb);
+  for (int64_t r = r0 + rg; r < r1; r += BN_U * BN_RG) {
+    float g[BN_U][8], xv[BN_U][8], yv[BN_U][8];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const int64_t ru = min(r + u * BN_RG, r1 - 1);
+      V8<TO>::load(dy + ru * a.C + cs, g[u]);
+      V8<T>::load(x + ru * a.C + cs, xv[u]);
+      if (y) V8<TO>::load(y + ru * a.C + cs, yv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const bool ok = r + u * BN_RG < r1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gg = (ok && (!y || yv[u][k] > 0.f)) ? g[u][k] : 0.f;
+        acc1[k] += gg;
+        acc2[k] += gg * (xv[u][k] - mu[k]) * is[k];
+      }
+    }
+  }
+  if (!cok) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc1[k] = acc2[k] = 0.f;
+  }
+  reduce_rowgroups(acc1, lds, s1);
+  reduce_rowgroups(acc2, lds, s2);
+  float* part = a.part + (int64_t)blockIdx.y * 2 * a.C;
+  if (threadIdx.x < BN_CT && c0 + threadIdx.x < a.C) {
+    part[c0 + threadIdx.x] = s1[threadIdx.x];
+    part[a.C + c0 + threadIdx.x] = s2[threadIdx.x];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned t = __hip_atomic_fetch_add(a.counters + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = (t == gridDim.y - 1);
+    if (flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!flag) return;
+  const int ch = threadIdx.x >> 2, sub = threadIdx.x & 3;
+  const int cc = c0 + ch;
+  float t1 = 0.f, t2 = 0.f;
+  if (cc < a.C) {
+    for (int b = sub; b < (int)gridDim.y; b += 4) {
+      const float* p = a.part + (int64_t)b * 2 * a.C;
+      t1 += __builtin_nontemporal_load(p + cc);
+      t2 += __builtin_nontemporal_load(p + a.C + cc);
+    }
+  }
+  t1 += __shfl_xor(t1, 1, 64);
+  t1 += __shfl_xor(t1, 2, 64);
+  t2 += __shfl_xor(t2, 1, 64);
+  t2 += __shfl_xor(t2, 2, 64);
+  if (sub == 0 && cc < a.C) {
+    if (a.dbeta) a.dbeta[cc] += t1;
+    if (a.dgamma) a.dgamma[cc] += t2;
+    // dx = a*(dy' - k1 - xhat*k2), xhat = (x - mean)*invstd  ->  P*dy' + Q*x + S
+    const float k1 = t1 / (float)a.R, k2 = t2 / (float)a.R;
+    const float sa = a.scale[cc], is = a.invstd[cc], mu = a.mean[cc];
+    a.coef[cc] = sa;
+    a.coef[a.C + cc] = -sa * k2 * is;
+    a.coef[2 * a.C + cc] = sa * (k2 * is * mu - k1);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(a.counters + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// dx = P*dy' + Q*x + S (per-channel coefficients in registers); dres = dy'
+template <typename T, typename TO>
+__global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
+                                                            const TO* __restrict__ y, const float* __restrict__ coef,
+                                                            T* __restrict__ dx, TO* __restrict__ dres, int64_t R, int C,
+                                                            int rpb) {
+  const int CV = C >> 3, RPP = BN_T / CV;
+  if ((int)threadIdx.x >= RPP * CV) return;
+  const int cv = threadIdx.x % CV, c = cv * 8;
+  float P[8], Q[8], S[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    P[k] = coef[c + k];
+    Q[k] = coef[C + c + k];
+    S[k] = coef[2 * C + c + k];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = min(R, r0 + rpb);
+  for (int64_t r = r0 + threadIdx.x / CV; r < r1; r += BN_U * RPP) {
+    float g[BN_U][8], xv[BN_U][8], yv[BN_U][8];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const int64_t ru = min(r + u * RPP, r1 - 1);
+      V8<TO>::load(dy + ru * C + c, g[u]);
+      V8<T>::load(x + ru * C + c, xv[u]);
+      if (y) V8<TO>::load(y + ru * C + c, yv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      if (y) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[u][k] = yv[u][k] > 0.f ? g[u][k] : 0.f;
+      }
+      const bool ok = r + u * RPP < r1;
+      if (ok && dres) V8<TO>::store(dres + (r + u * RPP) * C + c, g[u]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) xv[u][k] = P[k] * g[u][k] + Q[k] * xv[u][k] + S[k];
+      if (ok) V8<T>::store(dx + (r + u * RPP) * C + c, xv[u]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ LayerNorm
+constexpr int LN_T = 256;
+constexpr int LN_W = LN_T / 64;
+constexpr int LN_MAXV = 16;  // up to 16 x 4 elements per lane -> C <= 4096
+
+template <typename T>
+__device__ __forceinline__ void ld4(const T* p, float* v);
+template <>
+__device__ __forceinline__ void ld4<float>(const float* p, float* v) {
+  const float4 a = *(const float4*)p;
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+template <>
+__device__ __forceinline__ void ld4<uint16_t>(const uint16_t* p, float* v) {
+  const uint2 u = *(const uint2*)p;
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+template <typename T>
+__device__ __forceinline__ void st4(T* p, const float* v);
+template <>
+__device__ __forceinline__ void st4<float>(float* p, const float* v) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <>
+__device__ __forceinline__ void st4<uint16_t>(uint16_t* p, const float* v) {
+  uint2 u;
+  u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  *(uint2*)p = u;
+}
+
+template <typename T, typename TO, int NV>
+__global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ g,
+                                                      const float* __restrict__ b, TO* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int64_t rows, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * LN_W + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + row * C;
+  float v[NV][4];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * 64 + lane) * 4;
+    if (c < C) {
+      ld4<T>(xr + c, v[j]);
+    } else {
+      v[j][0] = v[j][1] = v[j][2] = v[j][3] = 0.f;
+    }
+    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+  }
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * 64 + lane) * 4;
+    if (c < C) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d = v[j][k] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / C + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * 64 + lane) * 4;
+    if (c < C) {
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = (v[j][k] - mean) * rstd * (g ? g[c + k] : 1.f) + (b ? b[c + k] : 0.f);
+      st4<TO>(y + row * C + c, o);
+    }
+  }
+}
+
+template <typename T, typename TO, int NV>
+__global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
+                                                      const float* __restrict__ g, const float* __restrict__ mean_in,
+                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                      float* part, unsigned* counter, float* dgamma, float* dbeta,
+                                                      int64_t rows, int C, int rows_per_block) {
+  extern __shared__ float sm[];  // [LN_W][2][C]
+  __shared__ int flag;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float ag[NV][4], ab[NV][4];
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ag[j][k] = ab[j][k] = 0.f;
+  const int64_t rb = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t re = min(rows, rb + rows_per_block);
+  for (int64_t row = rb + w; row < re; row += LN_W) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NV][4], gy[NV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (j * 64 + lane) * 4;
+      if (c < C) {
+        float xv[4], dv[4];
+        ld4<T>(x + row * C + c, xv);
+        ld4<TO>(dy + row * C + c, dv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xh[j][k] = (xv[k] - mean) * rstd;
+          gy[j][k] = dv[k] * (g ? g[c + k] : 1.f);
+          s1 += gy[j][k];
+          s2 += gy[j][k] * xh[j][k];
+          ag[j][k] += dv[k] * xh[j][k];
+          ab[j][k] += dv[k];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (j * 64 + lane) * 4;
+      if (c < C) {
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = rstd * (gy[j][k] - s1 - xh[j][k] * s2);
+        st4<T>(dx + row * C + c, o);
+      }
+    }
+  }
+  // block partial of dgamma/dbeta
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * 64 + lane) * 4;
+    if (c < C) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sm[(w * 2) * C + c + k] = ag[j][k];
+        sm[(w * 2 + 1) * C + c + k] = ab[j][k];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += LN_T) {
+    float t = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < LN_W; ++ww) t += sm[ww * 2 * C + i];
+    part[(int64_t)blockIdx.x * 2 * C + i] = t;
+  }
+  if (last_block_arrived(counter, &flag)) {
+    for (int i = threadIdx.x; i < 2 * C; i += LN_T) {
+      float t = 0.f;
+      for (int bb = 0; bb < (int)gridDim.x; ++bb) t += __builtin_nontemporal_load(part + (int64_t)bb * 2 * C + i);
+      if (i < C) {
+        if (dgamma) dgamma[i] += t;
+      } else {
+        if (dbeta) dbeta[i - C] += t;
+      }
+    }
+    reset_counter(counter);
+  }
+}
+
+int bn_grid_rows(int64_t R, int* rpb) {
+  // at most ~256 row blocks per channel column, >= 32 rows each, multiple of BN_RG
+  int64_t per = (R + 255) / 256;
+  per = (per + BN_RG - 1) / BN_RG * BN_RG;
+  if (per < BN_RG) per = BN_RG;
+  *rpb = (int)per;
+  return (int)((R + per - 1) / per);
+}
+
+}  // namespace
+
+// workspace needed by the BN reductions (floats): 2*C*RB
+RK_API int64_t rk_bn_workspace(int64_t R, int C) {
+  int rpb;
+  const int rb = bn_grid_rows(R, &rpb);
+  return (int64_t)rb * 2 * C;
+}
+
+// x: [R][C] (dt 0 f32 / 1 bf16). Training statistics + fused scale/shift + running stats.
+RK_API int rk_bn_stats(int dt, const void* x, int64_t R, int C, const float* gamma, const float* beta, float* mean,
+                       float* invstd, float* scale, float* shift, float* run_mean, float* run_var, int64_t* nbt,
+                       float momentum, float eps, float* ws, unsigned* counters, hipStream_t s) {
+  if (C % 8 || R <= 0) return (int)hipErrorInvalidValue;
+  BnStatsArgs a{x, R, C, 0, ws, counters, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, nbt, momentum, eps};
+  const int rb = bn_grid_rows(R, &a.rpb);
+  dim3 grid((C + BN_CT - 1) / BN_CT, rb);
+  if (dt == BF16)
+    bn_stats_kernel<uint16_t><<<grid, BN_T, 0, s>>>(a);
+  else
+    bn_stats_kernel<float><<<grid, BN_T, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
+
+// rows per block for the elementwise passes: ~2048 blocks, whole passes of RPP rows
+static int bn_elem_rows(int64_t R, int C, int* grid) {
+  const int rpp = BN_T / (C / 8);
+  int64_t per = (R + 2047) / 2048;
+  per = (per + rpp - 1) / rpp * rpp;
+  if (per < rpp) per = rpp;
+  *grid = (int)((R + per - 1) / per);
+  return (int)per;
+}
+
+// y = relu?(x*scale + shift + res?); dt: x dtype, dto: y/res dtype
+RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const float* scale, const float* shift, void* y,
+                       int64_t R, int C, int relu, hipStream_t s) {
+  if (C % 8 || C > 8 * BN_T || R <= 0) return (int)hipErrorInvalidValue;
+  int grid;
+  const int rpb = bn_elem_rows(R, C, &grid);
+#define RK_BA(T, TO) bn_apply_kernel<T, TO><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y, R, C, relu, rpb)
+  if (dt == BF16 && dto == BF16) RK_BA(uint16_t, uint16_t);
+  else if (dt == BF16) RK_BA(uint16_t, float);
+  else if (dto == BF16) RK_BA(float, uint16_t);
+  else RK_BA(float, float);
+#undef RK_BA
+  return (int)hipGetLastError();
+}
+
+// backward. dt: x/dx dtype; dto: dy/y/dres dtype. y (mask) may be null, dres may be null.
+RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void* y, int64_t R, int C,
+                     const float* mean, const float* invstd, const float* scale, float* dgamma, float* dbeta, void* dx,
+                     void* dres, float* ws, float* coef /*[3C]*/, unsigned* counters, hipStream_t s) {
+  if (C % 8 || C > 8 * BN_T || R <= 0) return (int)hipErrorInvalidValue;
+  BnBwdArgs a{dy, x, y, R, C, 0, mean, invstd, ws, counters, dgamma, dbeta, scale, coef};
+  const int rb = bn_grid_rows(R, &a.rpb);
+  dim3 grid((C + BN_CT - 1) / BN_CT, rb);
+  int eg;
+  const int erpb = bn_elem_rows(R, C, &eg);
+#define RK_BB(T, TO)                                                                                               \
+  do {                                                                                                             \
+    bn_bwd_reduce_kernel<T, TO><<<grid, BN_T, 0, s>>>(a);                                                          \
+    bn_bwd_apply_kernel<T, TO><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x, (const TO*)y, coef, (T*)dx,         \
+                                                   (TO*)dres, R, C, erpb);                                         \
+  } while (0)
+  if (dt == BF16 && dto == BF16) RK_BB(uint16_t, uint16_t);
+  else if (dt == BF16) RK_BB(uint16_t, float);
+  else if (dto == BF16) RK_BB(float, uint16_t);
+  else RK_BB(float, float);
+#undef RK_BB
+  return (int)hipGetLastError();
+}
+
+// LayerNorm forward over rows of C (C % 4 == 0, C <= 4096).  dt: x dtype, dto: y dtype.
+RK_API int rk_ln_fwd(int dt, int dto, const void* x, const float* g, const float* b, void* y, float* mean, float* rstd,
+                     int64_t rows, int C, float eps, hipStream_t s) {
+  if (C % 4 || C > 64 * 4 * LN_MAXV) return (int)hipErrorInvalidValue;
+  const int grid = (int)((rows + LN_W - 1) / LN_W);
+  const int nv = (C + 255) / 256;
+#define RK_LF(T, TO, NV) ln_fwd_kernel<T, TO, NV><<<grid, LN_T, 0, s>>>((const T*)x, g, b, (TO*)y, mean, rstd, rows, C, eps)
+#define RK_LFN(T, TO)                 \
+  if (nv <= 1) RK_LF(T, TO, 1);       \
+  else if (nv <= 2) RK_LF(T, TO, 2);  \
+  else if (nv <= 3) RK_LF(T, TO, 3);  \
+  else if (nv <= 4) RK_LF(T, TO, 4);  \
+  else if (nv <= 8) RK_LF(T, TO, 8);  \
+  else RK_LF(T, TO, 16);
+  if (dt == BF16 && dto == BF16) { RK_LFN(uint16_t, uint16_t) }
+  else if (dt == BF16) { RK_LFN(uint16_t, float) }
+  else if (dto == BF16) { RK_LFN(float, uint16_t) }
+  else { RK_LFN(float, float) }
+#undef RK_LFN
+#undef RK_LF
+  return (int)hipGetLastError();
+}
+
+RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
+  const int64_t rpb = 64;
+  return ((rows + rpb - 1) / rpb) * 2 * C;
+}
+
+// LayerNorm backward; dgamma/dbeta accumulated (+=). dt: x/dx dtype, dto: dy dtype.
+RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float* g, const float* mean,
+                     const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int C, float* ws,
+                     unsigned* counter, hipStream_t s) {
+  if (C % 4 || C > 64 * 4 * LN_MAXV) return (int)hipErrorInvalidValue;
+  const int rpb = 64;
+  const int grid = (int)((rows + rpb - 1) / rpb);
+  const int nv = (C + 255) / 256;
+  const size_t smem = (size_t)LN_W * 2 * C * sizeof(float);
+#define RK_LB(T, TO, NV)                                                                                          \
+  ln_bwd_kernel<T, TO, NV><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx, ws, counter, \
+                                                    dgamma, dbeta, rows, C, rpb)
+#define RK_LBN(T, TO)                 \
+  if (nv <= 1) RK_LB(T, TO, 1);       \
+  else if (nv <= 2) RK_LB(T, TO, 2);  \
+  else if (nv <= 3) RK_LB(T, TO, 3);  \
+  else if (nv <= 4) RK_LB(T, TO, 4);  \
+  else if (nv <= 8) RK_LB(T, TO, 8);  \
+  else RK_LB(T, TO, 16);
+  if (dt == BF16 && dto == BF16) { RK_LBN(uint16_t, uint16_t) }
+  else if (dt == BF16) { RK_LBN(uint16_t, float) }
+  else if (dto == BF16) { RK_LBN(float, uint16_t) }
+  else { RK_LBN(float, float) }
+#undef RK_LBN
+#undef RK_LB
+  return (int)hipGetLastError();
+}

@@ -49,6 +49,19 @@ KERNEL_SIGS = {
                             c_int, c_void_p]),
     "rk_gather_rows": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_loss_accum": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_int, c_void_p]),
+    "rk_bn_workspace": (c_int64, [c_int64, c_int]),
+    "rk_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int] + [c_void_p] * 9 + [c_float, c_float, c_void_p, c_void_p,
+                                                                                  c_void_p]),
+    "rk_bn_apply": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
+                            c_void_p]),
+    "rk_bn_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int] + [c_void_p] * 11),
+    "rk_ln_fwd": (c_int, [c_int, c_int] + [c_void_p] * 6 + [c_int64, c_int, c_float, c_void_p]),
+    "rk_ln_workspace": (c_int64, [c_int64, c_int]),
+    "rk_gelu_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p]),
+    "rk_gelu_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "rk_softmax_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p]),
+    "rk_softmax_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p]),
+    "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 8 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
 }
 
 
@@ -120,9 +133,10 @@ class Workspace:
     """
 
     _per_device: dict = {}
+    SIZE = 16384  # counters are reset by their last block, so one slot per (op, call-site) suffices
 
     def __init__(self, device: torch.device):
-        self.counters = torch.zeros(256, dtype=torch.int32, device=device)
+        self.counters = torch.zeros(self.SIZE, dtype=torch.int32, device=device)
         self._next = 0
         self._named: dict = {}
 
@@ -134,6 +148,21 @@ class Workspace:
         if ws is None:
             ws = cls._per_device[key] = Workspace(device)
         return ws
+
+    def counter_array(self, name: str, n: int) -> int:
+        """Pointer to ``n`` consecutive zeroed counters reserved under ``name``."""
+        key = (name, n)
+        idx = self._named.get(key)
+        if idx is None:
+            idx = self._named[key] = self._next
+            self._next += n
+            if self._next > self.counters.numel():
+                self._grow(self._next)
+        return self.counters.data_ptr() + 4 * idx
+
+    def _grow(self, need: int) -> None:
+        raise NativeError(f"workspace counters exhausted ({need} > {self.counters.numel()}); "
+                          "raise Workspace.SIZE before the first launch")
 
     def counter(self, name: str) -> int:
         idx = self._named.get(name)

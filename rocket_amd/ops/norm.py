@@ -1,0 +1,203 @@
+"""Fused normalisation ops (``native/kernels/norm.hip``).
+
+* :class:`BatchNormAct2d` — ``nn.BatchNorm2d`` whose training forward is two HIP
+  launches over channels-last activations (statistics with an in-launch grid
+  reduction + running-stat update, then one fused ``x*a + b (+ residual) (ReLU)``
+  pass) and whose backward is two launches (per-channel reductions, then the
+  input gradient and the residual gradient).  ResNet blocks call
+  ``bn(x, residual=identity, relu=True)`` so the block epilogue
+  ``relu(bn(conv(x)) + identity)`` is one pass over HBM.
+* :class:`FusedLayerNorm` — ``nn.LayerNorm`` with a one-wave-per-row forward that
+  can emit bf16 directly for the following GEMM, and a backward that fuses the
+  dgamma/dbeta column reduction (block partials + last block).
+
+Parameter gradients accumulate straight into persistent ``.grad`` buffers when the
+engine provides them (graph capture), otherwise they are returned to autograd.
+On CPU (or for layouts the kernels do not cover) the modules run the PyTorch
+reference implementation; on a HIP device the kernels are mandatory.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from rocket_amd.ops import _lib
+from rocket_amd.ops.lenet import _finish, _grad_targets
+
+
+def _dt(t: torch.Tensor) -> int:
+    return _lib.dtype_code(t)
+
+
+def _rows_view(x: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels-last (or [N, C]) -> [R, C] view, no copy."""
+    if x.dim() == 4:
+        return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
+    return x.reshape(-1, x.shape[-1])
+
+
+def _channels_last(x: torch.Tensor) -> torch.Tensor:
+    if x.dim() == 4:
+        return x.contiguous(memory_format=torch.channels_last)
+    return x.contiguous()
+
+
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+        lib = _lib.kernels()
+        x = _channels_last(x)
+        C = x.shape[1]
+        xr = _rows_view(x)
+        R = xr.shape[0]
+        dev = x.device
+        out_dtype = residual.dtype if residual is not None else x.dtype
+        y = torch.empty_like(x, dtype=out_dtype, memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
+        stats = torch.empty(4, C, dtype=torch.float32, device=dev)  # mean, invstd, scale, shift
+        ws = torch.empty(int(lib.rk_bn_workspace(R, C)), dtype=torch.float32, device=dev)
+        ncol = (C + 63) // 64
+        counters = _lib.Workspace.get(dev).counter_array(f"bn{ncol}", ncol)
+        w = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        s = _lib.stream_ptr(dev)
+        _lib.check(lib.rk_bn_stats(_dt(x), xr.data_ptr(), R, C, _lib.ptr(w), _lib.ptr(b), stats[0].data_ptr(),
+                                   stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
+                                   _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(nbt), float(momentum), float(eps),
+                                   ws.data_ptr(), counters, s), "rk_bn_stats")
+        res = None
+        if residual is not None:
+            res = _channels_last(residual)
+        _lib.check(lib.rk_bn_apply(_dt(x), _dt(y), xr.data_ptr(), _lib.ptr(_rows_view(res)) if res is not None else None,
+                                   stats[2].data_ptr(), stats[3].data_ptr(), _rows_view(y).data_ptr(), R, C, int(relu), s),
+                   "rk_bn_apply")
+        ctx.params = (weight, bias)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.out_dtype = out_dtype
+        ctx.save_for_backward(x, y if relu else None, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib.kernels()
+        x, y, stats = ctx.saved_tensors
+        weight, bias = ctx.params
+        C = x.shape[1]
+        dev = x.device
+        dy = _channels_last(dy if dy.dtype == ctx.out_dtype else dy.to(ctx.out_dtype))
+        xr, dyr = _rows_view(x), _rows_view(dy)
+        R = xr.shape[0]
+        params = [p for p in (weight, bias) if p is not None]
+        bufs, direct = _grad_targets(params, dev) if params else ([], False)
+        dgamma = bufs[0] if weight is not None else None
+        dbeta = bufs[-1] if bias is not None else None
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(dy) if ctx.has_res else None
+        ws = torch.empty(int(lib.rk_bn_workspace(R, C)), dtype=torch.float32, device=dev)
+        coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
+        ncol = (C + 63) // 64
+        counters = _lib.Workspace.get(dev).counter_array(f"bn{ncol}", ncol)
+        _lib.check(lib.rk_bn_bwd(_dt(x), _dt(dy), dyr.data_ptr(), xr.data_ptr(),
+                                 _rows_view(y).data_ptr() if y is not None else None, R, C, stats[0].data_ptr(),
+                                 stats[1].data_ptr(), stats[2].data_ptr(), _lib.ptr(dgamma), _lib.ptr(dbeta),
+                                 _rows_view(dx).data_ptr(), _rows_view(dres).data_ptr() if dres is not None else None,
+                                 ws.data_ptr(), coef.data_ptr(), counters, _lib.stream_ptr(dev)), "rk_bn_bwd")
+        g = _finish(params, bufs, direct) if params else []
+        gw = g[0] if weight is not None else None
+        gb = g[-1] if bias is not None else None
+        return dx, gw, gb, dres, None, None, None, None, None, None
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``BatchNorm2d`` with optional fused residual add and ReLU: ``relu?(bn(x) + residual?)``."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True, relu=False,
+                 **kw):
+        super().__init__(num_features, eps=eps, momentum=momentum, affine=affine,
+                         track_running_stats=track_running_stats, **kw)
+        self.relu = relu
+
+    def _fused_ok(self, x, residual) -> bool:
+        return (
+            x.is_cuda and self.training and x.dim() in (2, 4) and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
+            and x.dtype in (torch.float32, torch.bfloat16) and self.momentum is not None
+            and (residual is None or residual.shape == x.shape)
+        )
+
+    def forward(self, x, residual=None):
+        if self._fused_ok(x, residual):
+            if residual is not None and residual.dtype != x.dtype:
+                residual = residual.to(x.dtype)
+            return _BNAct.apply(x, self.weight, self.bias, residual,
+                                self.running_mean if self.track_running_stats else None,
+                                self.running_var if self.track_running_stats else None,
+                                self.num_batches_tracked if self.track_running_stats else None,
+                                self.momentum, self.eps, self.relu)
+        if x.is_cuda and self.training:
+            _lib.kernels()  # a HIP device without the native library is an error, not a fallback
+        y = super().forward(x)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if self.relu else y
+
+
+class _LN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, out_dtype):
+        lib = _lib.kernels()
+        x = x.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dev = x.device
+        y = torch.empty(x.shape, dtype=out_dtype, device=dev)
+        mean = torch.empty(rows, dtype=torch.float32, device=dev)
+        rstd = torch.empty(rows, dtype=torch.float32, device=dev)
+        w = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        _lib.check(lib.rk_ln_fwd(_dt(x), _dt(y), x.data_ptr(), _lib.ptr(w), _lib.ptr(b), y.data_ptr(),
+                                 mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps), _lib.stream_ptr(dev)),
+                   "rk_ln_fwd")
+        ctx.params = (weight, bias)
+        ctx.save_for_backward(x, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib.kernels()
+        x, mean, rstd = ctx.saved_tensors
+        weight, bias = ctx.params
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dev = x.device
+        params = [p for p in (weight, bias) if p is not None]
+        bufs, direct = _grad_targets(params, dev) if params else ([], False)
+        dgamma = bufs[0] if weight is not None else None
+        dbeta = bufs[-1] if bias is not None else None
+        dx = torch.empty_like(x)
+        ws = torch.empty(int(lib.rk_ln_workspace(rows, C)), dtype=torch.float32, device=dev)
+        counter = _lib.Workspace.get(dev).counter("ln_bwd")
+        w = weight.detach() if weight is not None else None
+        _lib.check(lib.rk_ln_bwd(_dt(x), _dt(dy), dy.data_ptr(), x.data_ptr(), _lib.ptr(w), mean.data_ptr(),
+                                 rstd.data_ptr(), dx.data_ptr(), _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C,
+                                 ws.data_ptr(), counter, _lib.stream_ptr(dev)), "rk_ln_bwd")
+        g = _finish(params, bufs, direct) if params else []
+        gw = g[0] if weight is not None else None
+        gb = g[-1] if bias is not None else None
+        return dx, gw, gb, None, None
+
+
+class FusedLayerNorm(nn.LayerNorm):
+    """``LayerNorm`` over the last dim; under autocast the output is bf16 (it feeds a GEMM)."""
+
+    def forward(self, x):
+        C = x.shape[-1]
+        if (x.is_cuda and len(self.normalized_shape) == 1 and C % 4 == 0 and C <= 4096
+                and x.dtype in (torch.float32, torch.bfloat16)):
+            out_dtype = torch.bfloat16 if (torch.is_autocast_enabled("cuda") or x.dtype == torch.bfloat16) else x.dtype
+            return _LN.apply(x, self.weight, self.bias, self.eps, out_dtype)
+        if x.is_cuda:
+            _lib.kernels()
+        return super().forward(x)

@@ -23,6 +23,11 @@ import torch
 from rocket_amd.ops import _lib
 
 
+def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same memory walk: strides agree on every dim of size > 1."""
+    return a.shape == b.shape and all(sa == sb for sa, sb, n in zip(a.stride(), b.stride(), a.shape) if n > 1)
+
+
 class _FusedBase(torch.optim.Optimizer):
     KIND = 0
     STATE_KEYS: tuple = ()
@@ -81,6 +86,10 @@ class _FusedBase(torch.optim.Optimizer):
         for _, p in active:
             if p.dtype != torch.float32:
                 raise RuntimeError(f"{type(self).__name__}: parameters must be fp32 master weights, got {p.dtype}")
+            if not _same_layout(p.grad, p):
+                # the kernel walks param/grad/state memory linearly: layouts must agree
+                raise RuntimeError(f"{type(self).__name__}: gradient layout {p.grad.stride()} differs from the "
+                                   f"parameter layout {p.stride()}")
             self._init_state(p)
         gd = {p.grad.dtype for _, p in active}
         if len(gd) != 1 or next(iter(gd)) not in (torch.float32, torch.bfloat16):
@@ -159,10 +168,13 @@ class _FusedBase(torch.optim.Optimizer):
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
-        for st in self.state.values():
+        for p, st in self.state.items():
             for k in self.STATE_KEYS:
                 if k in st:
-                    st[k] = st[k].float().contiguous()
+                    v = st[k].float()
+                    if v.shape == p.shape and not _same_layout(v, p):  # same memory walk as the param
+                        v = torch.empty_like(p, dtype=torch.float32).copy_(v)
+                    st[k] = v
             if "step" in st and isinstance(st["step"], torch.Tensor):
                 st["step"] = st["step"].detach().to("cpu", torch.float32)
         self._key = None

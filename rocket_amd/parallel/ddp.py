@@ -64,8 +64,9 @@ class _Bucket:
         self.ready: set = set()
 
     def view(self, i: int) -> torch.Tensor:
-        p = self.params[i]
-        return self.flat[self.offsets[i] : self.offsets[i] + p.numel()].view_as(p)
+        from rocket_amd.parallel.flat_grads import _param_view
+
+        return _param_view(self.flat, self.offsets[i], self.params[i])
 
 
 class _TorchDistComm:

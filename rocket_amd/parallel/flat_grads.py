@@ -25,6 +25,26 @@ import torch
 from torch import nn
 
 
+def _param_view(flat: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
+    """A slice of ``flat`` shaped AND strided like ``p`` (channels-last weights get channels-last
+    grads, so autograd accumulates in place instead of copying through a layout change)."""
+    n = p.numel()
+    if p.is_contiguous() or not _dense(p):
+        return flat[off : off + n].view_as(p)
+    return flat.as_strided(p.shape, p.stride(), flat.storage_offset() + off)
+
+
+def _dense(p: torch.Tensor) -> bool:
+    # non-overlapping and dense: the strides are a permutation of a contiguous layout
+    dims = sorted(range(p.dim()), key=lambda d: p.stride(d))
+    expect = 1
+    for d in dims:
+        if p.shape[d] != 1 and p.stride(d) != expect:
+            return False
+        expect *= p.shape[d]
+    return True
+
+
 class FlatGrads:
     def __init__(self, params: List[nn.Parameter]):
         groups: Dict[Tuple[torch.device, torch.dtype], List[nn.Parameter]] = {}
@@ -39,7 +59,7 @@ class FlatGrads:
             flat = torch.zeros(n, dtype=dtype, device=dev)
             off = 0
             for p in ps:
-                view = flat[off : off + p.numel()].view_as(p)
+                view = _param_view(flat, off, p)
                 if p.grad is not None:
                     with torch.no_grad():
                         view.copy_(p.grad)

@@ -58,3 +58,29 @@ def test_fused_step_clears_grads(kind):
         for p, r in zip(ps, ref):
             assert torch.count_nonzero(p.grad) == 0
             torch.testing.assert_close(p.detach(), r.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_fused_optimizer_channels_last_flat_grads():
+    """channels-last weights: flat-gradient views must share the param layout the kernel walks."""
+    from rocket_amd.ops.optim import FusedSGD
+    from rocket_amd.parallel.flat_grads import FlatGrads
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = torch.nn.Conv2d(8, 16, 3, bias=False).to(dev).to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(8, 16, 3, bias=False).to(dev)
+    with torch.no_grad():
+        ref.weight.copy_(m.weight)
+    FlatGrads(list(m.parameters()))
+    opt = FusedSGD(m.parameters(), lr=0.1, momentum=0.9)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    x = torch.randn(4, 8, 10, 10, device=dev)
+    for _ in range(3):
+        m(x.to(memory_format=torch.channels_last)).square().mean().backward()
+        ref(x).square().mean().backward()
+        assert m.weight.grad.stride() == m.weight.stride()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+        ropt.step()
+        ropt.zero_grad()
+    torch.testing.assert_close(m.weight.detach(), ref.weight.detach(), rtol=1e-5, atol=1e-6)

@@ -1,0 +1,88 @@
+"""BatchNorm (+residual +ReLU) and LayerNorm HIP kernels vs a PyTorch fp32 reference."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu,residual", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 200, 7, 7), (64, 24, 32, 32)])
+def test_batchnorm_act(dtype, relu, residual, shape):
+    from rocket_amd.ops.norm import BatchNormAct2d
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    C = shape[1]
+    bn = BatchNormAct2d(C, relu=relu).to(dev)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    x32 = (torch.randn(shape, device=dev) * 3 + 1).to(memory_format=torch.channels_last)
+    r32 = torch.randn(shape, device=dev).to(memory_format=torch.channels_last) if residual else None
+    x = x32.to(dtype).requires_grad_(True)
+    r = r32.to(dtype).requires_grad_(True) if residual else None
+    y = bn(x, residual=r)
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+
+    # fp32 reference on the same (rounded) inputs
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if residual else None
+    w = bn.weight.detach().clone().requires_grad_(True)
+    b = bn.bias.detach().clone().requires_grad_(True)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    ref = F.batch_norm(xr, rm, rv, w, b, training=True, momentum=0.1, eps=1e-5)
+    if residual:
+        ref = ref + rr
+    if relu:
+        ref = F.relu(ref)
+    ref.backward(gy.float())
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(y, ref) < tol
+    assert _rel(bn.running_mean, rm) < 1e-5 and _rel(bn.running_var, rv) < 1e-4
+    assert int(bn.num_batches_tracked) == 1
+    gtol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert _rel(x.grad, xr.grad) < gtol
+    assert _rel(bn.weight.grad, w.grad) < gtol
+    assert _rel(bn.bias.grad, b.grad) < gtol
+    if residual:
+        assert _rel(r.grad, rr.grad) < gtol
+
+
+@pytest.mark.parametrize("in_dtype,autocast", [(torch.float32, False), (torch.float32, True), (torch.bfloat16, False)])
+@pytest.mark.parametrize("C", [768, 256, 100])
+def test_layernorm(in_dtype, autocast, C):
+    from rocket_amd.ops.norm import FusedLayerNorm
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    ln = FusedLayerNorm(C).to(dev)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.5, 0.5)
+    x = (torch.randn(3, 197, C, device=dev) * 2 + 0.5).to(in_dtype).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        y = ln(x)
+    expect = torch.bfloat16 if (autocast or in_dtype == torch.bfloat16) else torch.float32
+    assert y.dtype == expect
+    gy = torch.randn(y.shape, device=dev)
+    y.backward(gy.to(y.dtype))
+    xr = x.detach().float().requires_grad_(True)
+    w = ln.weight.detach().clone().requires_grad_(True)
+    b = ln.bias.detach().clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (C,), w, b, 1e-5)
+    ref.backward(gy.to(y.dtype).float())
+    tol = 1e-5 if expect == torch.float32 else 1e-2
+    assert _rel(y, ref) < tol
+    gtol = 1e-4 if in_dtype == torch.float32 and expect == torch.float32 else 3e-2
+    assert _rel(x.grad, xr.grad) < gtol
+    assert _rel(ln.weight.grad, w.grad) < gtol
+    assert _rel(ln.bias.grad, b.grad) < gtol
