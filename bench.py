@@ -90,9 +90,10 @@ def main() -> int:
     dev = ctx.device
     on_gpu = dev.type == "cuda"
     fused = on_gpu and args.impl == "fused"
-    if fused:
-        from rocket_amd import ops
+    from rocket_amd import ops
 
+    ops.set_fused(fused)
+    if fused:
         ops.require_native()
 
     bs_default, in_shape, classes, desc = MODELS[args.model]

@@ -16,8 +16,8 @@
 // LayerNorm over the last dim (C <= 4096), one wave per row:
 //   ln_fwd        two-pass mean/var in registers, y = xhat*g + b (bf16 or f32 out),
 //                 saves mean/rstd.
-//   ln_bwd        dx per row; dgamma/dbeta column partials per block + last-block reduction,
-//                 accumulated into the parameter gradients.
+//   ln_bwd        dx per row; dgamma/dbeta column partials per block, then a parallel column-sum
+//                 launch accumulates them into the parameter gradients.
 #include "rk_common.h"
 
 using namespace rk;
@@ -460,10 +460,8 @@ template <typename T, typename TO, int NV>
 __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
                                                       const float* __restrict__ g, const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in, T* __restrict__ dx,
-                                                      float* part, unsigned* counter, float* dgamma, float* dbeta,
-                                                      int64_t rows, int C, int rows_per_block) {
+                                                      float* part, int64_t rows, int C, int rows_per_block) {
   extern __shared__ float sm[];  // [LN_W][2][C]
-  __shared__ int flag;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float ag[NV][4], ab[NV][4];
 #pragma unroll
@@ -526,17 +524,36 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
     for (int ww = 0; ww < LN_W; ++ww) t += sm[ww * 2 * C + i];
     part[(int64_t)blockIdx.x * 2 * C + i] = t;
   }
-  if (last_block_arrived(counter, &flag)) {
-    for (int i = threadIdx.x; i < 2 * C; i += LN_T) {
-      float t = 0.f;
-      for (int bb = 0; bb < (int)gridDim.x; ++bb) t += __builtin_nontemporal_load(part + (int64_t)bb * 2 * C + i);
-      if (i < C) {
-        if (dgamma) dgamma[i] += t;
-      } else {
-        if (dbeta) dbeta[i - C] += t;
-      }
+}
+
+// column sums of the [nrows][2C] block partials -> dgamma (first C) / dbeta (last C), accumulated.
+// Block: 64 columns x 16 row-slices; each thread strides its slice with 4 loads in flight.
+constexpr int CS_T = 1024;
+__global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ part, int nrows, int C2,
+                                                      float* dgamma, float* dbeta, int C) {
+  __shared__ float red[CS_T / 64][65];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sl = threadIdx.x >> 6, nsl = CS_T / 64;
+  const int cc = col < C2 ? col : C2 - 1;
+  float t = 0.f;
+  int r = sl;
+  for (; r + 3 * nsl < nrows; r += 4 * nsl) {
+    const float a0 = part[(int64_t)r * C2 + cc], a1 = part[(int64_t)(r + nsl) * C2 + cc];
+    const float a2 = part[(int64_t)(r + 2 * nsl) * C2 + cc], a3 = part[(int64_t)(r + 3 * nsl) * C2 + cc];
+    t += (a0 + a1) + (a2 + a3);
+  }
+  for (; r < nrows; r += nsl) t += part[(int64_t)r * C2 + cc];
+  red[sl][threadIdx.x & 63] = t;
+  __syncthreads();
+  if (threadIdx.x < 64 && col < C2) {
+    float u = 0.f;
+#pragma unroll
+    for (int k = 0; k < CS_T / 64; ++k) u += red[k][threadIdx.x];
+    if (col < C) {
+      if (dgamma) dgamma[col] += u;
+    } else if (dbeta) {
+      dbeta[col - C] += u;
     }
-    reset_counter(counter);
   }
 }
 
@@ -645,8 +662,10 @@ RK_API int rk_ln_fwd(int dt, int dto, const void* x, const float* g, const float
   return (int)hipGetLastError();
 }
 
+constexpr int LN_BWD_RPB = 32;
+
 RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
-  const int64_t rpb = 64;
+  const int64_t rpb = LN_BWD_RPB;
   return ((rows + rpb - 1) / rpb) * 2 * C;
 }
 
@@ -655,13 +674,12 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
                      const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int C, float* ws,
                      unsigned* counter, hipStream_t s) {
   if (C % 4 || C > 64 * 4 * LN_MAXV) return (int)hipErrorInvalidValue;
-  const int rpb = 64;
+  const int rpb = LN_BWD_RPB;
   const int grid = (int)((rows + rpb - 1) / rpb);
   const int nv = (C + 255) / 256;
   const size_t smem = (size_t)LN_W * 2 * C * sizeof(float);
-#define RK_LB(T, TO, NV)                                                                                          \
-  ln_bwd_kernel<T, TO, NV><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx, ws, counter, \
-                                                    dgamma, dbeta, rows, C, rpb)
+#define RK_LB(T, TO, NV) \
+  ln_bwd_kernel<T, TO, NV><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx, ws, rows, C, rpb)
 #define RK_LBN(T, TO)                 \
   if (nv <= 1) RK_LB(T, TO, 1);       \
   else if (nv <= 2) RK_LB(T, TO, 2);  \
@@ -675,5 +693,7 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
   else { RK_LBN(float, float) }
 #undef RK_LBN
 #undef RK_LB
+  if (dgamma || dbeta) colsum_kernel<<<(2 * C + 63) / 64, CS_T, 0, s>>>(ws, grid, 2 * C, dgamma, dbeta, C);
+  (void)counter;
   return (int)hipGetLastError();
 }

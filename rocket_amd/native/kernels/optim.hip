@@ -6,8 +6,8 @@
 // pointer changes, so the launch is graph-capturable.  Hyper-parameters live in
 // a small device array per param group (lr, betas, eps, weight decay) that the
 // host refreshes only when a scheduler changes them, and the step counter lives
-// in device memory: the LAST block to finish (ticket counter, agent-scope
-// release/acquire) advances it, so bias corrections need no host round trip.
+// in device memory: every block reads it first, and the last block to take a ticket
+// advances it, so bias corrections need no host round trip.
 //
 // Optional AMP hooks: `inv_scale` multiplies every gradient (GradScaler unscale
 // folded into the update) and a non-zero `found_inf` makes the launch a no-op.
@@ -38,6 +38,24 @@ __device__ __forceinline__ float gload(const G* g, int64_t i);
 template <> __device__ __forceinline__ float gload<float>(const float* g, int64_t i) { return g[i]; }
 template <> __device__ __forceinline__ float gload<uint16_t>(const uint16_t* g, int64_t i) { return bf2f(g[i]); }
 
+// Every block reads the device step counter once (broadcast through LDS), then thread 0 takes a
+// ticket; the last block to take one advances the counter.  All blocks have already read the old
+// value when the last ticket is taken, so no block waits for its stores or fences at the end.
+__device__ __forceinline__ float read_step_and_ticket(float* step, unsigned* counter, bool skip) {
+  __shared__ float s_step;
+  if (threadIdx.x == 0) s_step = step[0];
+  __syncthreads();
+  const float cur = s_step;
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      if (!skip) step[0] = cur + 1.f;
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  return cur;
+}
+
 template <typename G>
 __device__ __forceinline__ void zero_chunk(G* g, int64_t start, int64_t end) {
   for (int64_t i = start + threadIdx.x; i < end; i += kThreads) g[i] = G(0);
@@ -49,8 +67,8 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
                                                           const AdamHyper* __restrict__ hyper, float* step,
                                                           const float* inv_scale, const float* found_inf,
                                                           unsigned* counter) {
-  __shared__ int flag;
   const bool skip = found_inf != nullptr && found_inf[0] != 0.f;
+  const float t = read_step_and_ticket(step, counter, skip) + 1.f;
   if (!skip) {
     const int2 bt = blocks[blockIdx.x];
     const TensorRec tr = tensors[bt.x];
@@ -59,7 +77,6 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
     G* __restrict__ g = (G*)tr.g;
     float* __restrict__ m = (float*)tr.s0;
     float* __restrict__ v = (float*)tr.s1;
-    const float t = step[0] + 1.f;
     const float bc1 = 1.f - __powf(h.beta1, t);
     const float bc2 = 1.f - __powf(h.beta2, t);
     const float step_size = h.lr / bc1;
@@ -78,7 +95,31 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
       pp -= step_size * mm / (sqrtf(vv) * rbc2 + h.eps);
     };
     const bool vec = sizeof(G) == 4 && ((tr.p | tr.g | tr.s0 | tr.s1) & 15) == 0;
-    if (vec) {
+    if (vec && end - start == kChunk) {
+      // full chunk: all 16 float4 loads of the thread in flight before the first update
+      constexpr int J = kChunk / (4 * kThreads);
+      float4 pp[J], mm[J], vv[J], gg[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int64_t i = start + 4 * (threadIdx.x + j * kThreads);
+        pp[j] = *(const float4*)(p + i);
+        mm[j] = *(const float4*)(m + i);
+        vv[j] = *(const float4*)(v + i);
+        gg[j] = *(const float4*)((const float*)g + i);
+      }
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int64_t i = start + 4 * (threadIdx.x + j * kThreads);
+        upd(pp[j].x, gg[j].x, mm[j].x, vv[j].x);
+        upd(pp[j].y, gg[j].y, mm[j].y, vv[j].y);
+        upd(pp[j].z, gg[j].z, mm[j].z, vv[j].z);
+        upd(pp[j].w, gg[j].w, mm[j].w, vv[j].w);
+        *(float4*)(p + i) = pp[j];
+        *(float4*)(m + i) = mm[j];
+        *(float4*)(v + i) = vv[j];
+        if (ZG) *(float4*)((float*)g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else if (vec) {
       for (int64_t i = start + 4 * threadIdx.x; i < end; i += 4 * kThreads) {
         if (i + 4 <= end) {
           float4 pp = *(float4*)(p + i), mm = *(float4*)(m + i), vv = *(float4*)(v + i);
@@ -110,10 +151,6 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
     const int64_t start = (int64_t)bt.y * kChunk;
     zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)kChunk, tr.n));
   }
-  if (last_block_arrived(counter, &flag)) {
-    if (threadIdx.x == 0 && !skip) step[0] += 1.f;
-    reset_counter(counter);
-  }
 }
 
 struct SgdHyper {  // 8 floats per group
@@ -126,8 +163,8 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
                                                          const SgdHyper* __restrict__ hyper, float* step,
                                                          const float* inv_scale, const float* found_inf,
                                                          unsigned* counter) {
-  __shared__ int flag;
   const bool skip = found_inf != nullptr && found_inf[0] != 0.f;
+  const float cur = read_step_and_ticket(step, counter, skip);
   if (!skip) {
     const int2 bt = blocks[blockIdx.x];
     const TensorRec tr = tensors[bt.x];
@@ -135,7 +172,7 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
     float* p = (float*)tr.p;
     G* g = (G*)tr.g;
     float* buf = (float*)tr.s0;
-    const bool first = step[0] == 0.f;  // momentum buffer initialised with the first gradient (torch semantics)
+    const bool first = cur == 0.f;  // momentum buffer initialised with the first gradient (torch semantics)
     const float gs = inv_scale ? inv_scale[0] : 1.f;
     const float sgn = h.maximize != 0.f ? -1.f : 1.f;
     const int64_t start = (int64_t)bt.y * kChunk;
@@ -155,10 +192,6 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
     const TensorRec tr = tensors[bt.x];
     const int64_t start = (int64_t)bt.y * kChunk;
     zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)kChunk, tr.n));
-  }
-  if (last_block_arrived(counter, &flag)) {
-    if (threadIdx.x == 0 && !skip) step[0] += 1.f;
-    reset_counter(counter);
   }
 }
 

@@ -9,15 +9,37 @@ linear                  MFMA bf16 GEMM + bias/ReLU/GELU epilogue,         K5, K8
                         dgrad/wgrad with fused bias-grad
 conv_bias_relu_pool     direct conv + bias + ReLU + 2x2 maxpool (fwd),    K1-K4, K9-K11
                         unpool+ReLU-bwd fused into dgrad/wgrad
-layer_norm / batch_norm fused fwd/bwd                                      BASELINE configs
+lenet_features/mlp_head MFMA LeNet conv stack / classifier, fwd+bwd        K1-K11 (flagship)
+BatchNormAct2d          stats+apply(+residual+ReLU) fwd, reduce+apply bwd  ResNet configs
+FusedLayerNorm          one wave per row, fused dgamma/dbeta reduction      ViT config
+gelu / softmax          erf-GELU, scaled row softmax (attention)           ViT config
+gather_rows/loss_accum  batch assembly, on-device loss bookkeeping         data path / Loss capsule
 =====================  ================================================  ==========================
+
+``set_fused(False)`` (or ``ROCKET_FUSED=0``) switches the model-level modules
+(BatchNormAct2d, FusedLayerNorm, gelu, softmax) to their stock PyTorch
+implementations for A/B runs; the default on a HIP device is the kernels.
 """
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from rocket_amd.ops import _lib
+
+
+_FUSED = os.environ.get("ROCKET_FUSED", "1") != "0"
+
+
+def set_fused(enabled: bool) -> None:
+    global _FUSED
+    _FUSED = bool(enabled)
+
+
+def fused_enabled() -> bool:
+    return _FUSED
 
 
 def native_available() -> bool:

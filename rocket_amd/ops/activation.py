@@ -15,6 +15,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+import rocket_amd.ops as _ops
 from rocket_amd.ops import _lib
 
 
@@ -39,7 +40,7 @@ class _Gelu(torch.autograd.Function):
 
 
 def gelu(x: torch.Tensor) -> torch.Tensor:
-    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16):
+    if _ops.fused_enabled() and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.numel() % 4 == 0:
         return _Gelu.apply(x)
     return F.gelu(x)
 
@@ -71,7 +72,7 @@ class _Softmax(torch.autograd.Function):
 
 
 def softmax(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
-    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.shape[-1] <= 1024:
+    if _ops.fused_enabled() and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.shape[-1] <= 1024:
         return _Softmax.apply(x, scale)
     return torch.softmax(x.float() * scale, dim=-1).to(x.dtype)
 

@@ -23,6 +23,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+import rocket_amd.ops as _ops
 from rocket_amd.ops import _lib
 from rocket_amd.ops.lenet import _finish, _grad_targets
 
@@ -121,7 +122,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
     def _fused_ok(self, x, residual) -> bool:
         return (
-            x.is_cuda and self.training and x.dim() in (2, 4) and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
+            _ops.fused_enabled() and x.is_cuda and self.training and x.dim() in (2, 4) and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
             and x.dtype in (torch.float32, torch.bfloat16) and self.momentum is not None
             and (residual is None or residual.shape == x.shape)
         )
@@ -135,7 +136,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
                                 self.running_var if self.track_running_stats else None,
                                 self.num_batches_tracked if self.track_running_stats else None,
                                 self.momentum, self.eps, self.relu)
-        if x.is_cuda and self.training:
+        if x.is_cuda and self.training and _ops.fused_enabled():
             _lib.kernels()  # a HIP device without the native library is an error, not a fallback
         y = super().forward(x)
         if residual is not None:
@@ -194,10 +195,10 @@ class FusedLayerNorm(nn.LayerNorm):
 
     def forward(self, x):
         C = x.shape[-1]
-        if (x.is_cuda and len(self.normalized_shape) == 1 and C % 4 == 0 and C <= 4096
+        if (_ops.fused_enabled() and x.is_cuda and len(self.normalized_shape) == 1 and C % 4 == 0 and C <= 4096
                 and x.dtype in (torch.float32, torch.bfloat16)):
             out_dtype = torch.bfloat16 if (torch.is_autocast_enabled("cuda") or x.dtype == torch.bfloat16) else x.dtype
             return _LN.apply(x, self.weight, self.bias, self.eps, out_dtype)
-        if x.is_cuda:
+        if x.is_cuda and _ops.fused_enabled():
             _lib.kernels()
         return super().forward(x)

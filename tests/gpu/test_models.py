@@ -49,10 +49,12 @@ def _compare(tmp_path, make, shape, classes, opt):
     assert mod._graphs.replays > 0, mod._graphs.disabled_reason
     for a, b in zip(le, lg):
         assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (le, lg)
+    # MIOpen weight-gradient kernels accumulate with atomics, so runs are not bitwise identical;
+    # small-norm tensors (BN shifts start at 0) get an absolute floor
     for (k, a), b in zip(ne.state_dict().items(), ng.state_dict().values()):
         if a.dtype.is_floating_point:
-            d = float((a.float() - b.float()).norm() / a.float().norm().clamp_min(1e-6))
-            assert d < 5e-2, (k, d)
+            diff = float((a.float() - b.float()).norm())
+            assert diff <= 5e-2 * float(a.float().norm()) + 2e-3 * a.numel() ** 0.5, (k, diff, float(a.float().norm()))
 
 
 def test_resnet18_graph_matches_eager(tmp_path):
