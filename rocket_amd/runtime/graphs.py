@@ -258,14 +258,15 @@ class StepGraphs:
         cap.graph_split = split
         torch.cuda.synchronize()
         ga = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(ga, pool=self.pool):
+        # thread_local: the RCCL watchdog thread keeps polling its events while we capture
+        with torch.cuda.graph(ga, pool=self.pool, capture_error_mode="thread_local"):
             self._phase_a(cap)
             if not split:
                 self._phase_b(cap)
         v.graphs.append(ga)
         if split:
             gb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gb, pool=self.pool):
+            with torch.cuda.graph(gb, pool=self.pool, capture_error_mode="thread_local"):
                 self._phase_b(cap)
             v.graphs.append(gb)
         v.out = cap.batch
