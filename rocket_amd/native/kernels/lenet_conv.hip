@@ -63,6 +63,68 @@ __device__ __forceinline__ int pos2(int w, int q) {
   return (2 * wr + (q >> 1)) * Q1 + 2 * wc + (q & 1);
 }
 
+// ------------------------------------------------------------------------------ classifier
+// fc1 400->120, fc2 120->84, fc3 84->10 fused into the conv kernels (one block = 4 samples, so an
+// MFMA tile uses rows 0..3; the FLOPs are negligible, the point is one launch and no HBM round
+// trip of the features).  Weights come from a fragment table built once per step by lenet_prep
+// from the fp32 master weights: one 16-byte load per lane per MFMA, no per-block conversion.
+//   forward  fragment (nt, ks)[lane] = W[16nt + lo][32ks + 8hi + j]     (B[k][n] = W[n][k])
+//   dgrad    fragment (it, ks)[lane] = W[32ks + 8hi + j][16it + lo]     (B[k][n] = W[k][n])
+constexpr int F0 = 400, F1 = 120, F2 = 84, F3 = 10;
+constexpr int OFF_F1 = 0;                  // fc1 fwd: 8 n-tiles x 13 k-steps
+constexpr int OFF_F2 = OFF_F1 + 8 * 13;    // fc2 fwd: 6 x 4
+constexpr int OFF_F3 = OFF_F2 + 6 * 4;     // fc3 fwd: 1 x 3
+constexpr int OFF_B3 = OFF_F3 + 1 * 3;     // fc3 dgrad: 6 n-tiles (84) x 1 k-step (10)
+constexpr int OFF_B2 = OFF_B3 + 6 * 1;     // fc2 dgrad: 8 (120) x 3 (84)
+constexpr int OFF_B1 = OFF_B2 + 8 * 3;     // fc1 dgrad: 25 (400) x 4 (120)
+constexpr int NFRAG = OFF_B1 + 25 * 4;     // 261 fragments x 64 lanes x 16 B
+constexpr int A2P = 432;                   // LDS row of pooled conv2 output: data 0..399, zero 400..415, trash 424
+constexpr int A2TRASH = 424;
+constexpr int H1P = 136, H2P = 104, DYP = 40;
+
+__global__ void __launch_bounds__(64) lenet_prep_kernel(const float* __restrict__ w1, const float* __restrict__ w2,
+                                                        const float* __restrict__ w3, bf16x8* __restrict__ frag) {
+  const int f = blockIdx.x, lane = threadIdx.x, lo = lane & 15, hi = lane >> 4;
+  const float* W;
+  int nout, nin, tile, ks, bwd;
+  if (f < OFF_F2) { W = w1; nout = F1; nin = F0; tile = (f - OFF_F1) / 13; ks = (f - OFF_F1) % 13; bwd = 0; }
+  else if (f < OFF_F3) { W = w2; nout = F2; nin = F1; tile = (f - OFF_F2) / 4; ks = (f - OFF_F2) % 4; bwd = 0; }
+  else if (f < OFF_B3) { W = w3; nout = F3; nin = F2; tile = 0; ks = f - OFF_F3; bwd = 0; }
+  else if (f < OFF_B2) { W = w3; nout = F3; nin = F2; tile = f - OFF_B3; ks = 0; bwd = 1; }
+  else if (f < OFF_B1) { W = w2; nout = F2; nin = F1; tile = (f - OFF_B2) / 3; ks = (f - OFF_B2) % 3; bwd = 1; }
+  else { W = w1; nout = F1; nin = F0; tile = (f - OFF_B1) / 4; ks = (f - OFF_B1) % 4; bwd = 1; }
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int a = bwd ? 32 * ks + 8 * hi + j : 16 * tile + lo;  // output-feature row of W
+    const int b = bwd ? 16 * tile + lo : 32 * ks + 8 * hi + j;  // input-feature column of W
+    const bool ok = a < nout && b < nin;
+    v[j] = (__bf16)(ok ? W[a * nin + b] : 0.f);
+  }
+  frag[f * 64 + lane] = v;
+}
+
+// one MFMA tile of a 4-row classifier layer: rows = the block's samples (lanes lo < 4 read `act`,
+// the rest a zero row), K-steps KS from LDS, B fragments from the table (all loads issued first)
+template <int KS>
+__device__ __forceinline__ f32x4 cls_tile(const uint16_t* act, int stride, const uint16_t* zrow,
+                                          const bf16x8* __restrict__ frag, int fbase, int lane) {
+  const int lo = lane & 15, hi = lane >> 4;
+  const uint16_t* row = lo < SPB ? act + lo * stride : zrow;
+  bf16x8 b[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) b[ks] = frag[(fbase + ks) * 64 + lane];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(row + 32 * ks + 8 * hi), b[ks], acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
+  return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
+}
+
 // ------------------------------------------------------------------------------ forward
 constexpr int A1CL = Q1 * Q1 * 8;  // channel-last conv1 output: [pixel][8 channels], 6 used
 
@@ -71,15 +133,26 @@ struct FwdSmem {
   uint16_t a1cl[SPB][A1CL + 16];  // zero pixel at A1CL (8 zeros), trash lanes at A1CL+8
   uint16_t a1[SPB][A1N + 8];  // zero slot at A1N, trash at A1N+4
   uint8_t c1[SPB][A1N + 8];
-  uint16_t a2[SPB][A2N + 8];  // trash at A2N
+  uint16_t a2[SPB][A2P];  // data 0..399, zero pad 400..415, trash at A2TRASH
   uint8_t c2[SPB][A2N + 8];
+  uint16_t h1[SPB][H1P];  // classifier activations (bf16), zero pads for the next layer's K
+  uint16_t h2[SPB][H2P];
+  uint16_t zrow[A2P];
 };
 
+struct ClsFwd {  // classifier operands of the fused forward
+  const bf16x8* frag;
+  const float *fb1, *fb2, *fb3;
+  uint16_t *a2T, *h1T, *h2T;  // transposed activations [features][N] for the weight gradients
+  float* logits;              // [N][10]
+};
+
+template <bool MLP>
 __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__ x, const float* __restrict__ w1,
                                                        const float* __restrict__ b1, const float* __restrict__ w2,
                                                        const float* __restrict__ b2, uint16_t* __restrict__ a1g,
                                                        uint8_t* __restrict__ code1, uint16_t* __restrict__ a2g,
-                                                       uint8_t* __restrict__ code2, int N) {
+                                                       uint8_t* __restrict__ code2, int N, ClsFwd cf) {
   __shared__ __attribute__((aligned(16))) FwdSmem sm;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int slot = wave / WPS, sw = wave % WPS, st = threadIdx.x % (64 * WPS);  // st: thread in sample group
@@ -98,6 +171,10 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
   }
   if (st < 8) a1[A1N + st] = 0;
   if (st < 16) sm.a1cl[slot][A1CL + st] = 0;
+  if (MLP) {
+    if (st < 32) sm.a2[slot][400 + st] = 0;  // K pad of fc1 (400..431; trash at 424 rewritten by conv2)
+    for (int i = threadIdx.x; i < A2P; i += NTHR) sm.zrow[i] = 0;
+  }
   const int hi = lane >> 4, lo = lane & 15;
   bf16x8 bw1;
   int koff1[8];
@@ -183,15 +260,62 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     }
     m += bias2;
     const bool on = m > 0.f;
-    const int o = wq < Q2 * Q2 ? lo * (Q2 * Q2) + wq : A2N;  // flatten order (C, H, W)
+    const int o = wq < Q2 * Q2 ? lo * (Q2 * Q2) + wq : (MLP ? A2TRASH : A2N);  // flatten order (C, H, W)
     sm.a2[slot][o] = f2bf(on ? m : 0.f);
     sm.c2[slot][o] = on ? (uint8_t)arg : 0xFF;
   }
   __syncthreads();
   if (live) {
     for (int i = st * 8; i < A2N; i += 64 * WPS * 8) {
-      *(uint4*)(a2g + (int64_t)n * A2N + i) = *(const uint4*)(sm.a2[slot] + i);
+      if (!MLP) *(uint4*)(a2g + (int64_t)n * A2N + i) = *(const uint4*)(sm.a2[slot] + i);
       *(uint2*)(code2 + (int64_t)n * A2N + i) = *(const uint2*)(sm.c2[slot] + i);
+    }
+  }
+  if constexpr (MLP) {
+    // the host guarantees N % 8 == 0, so every block holds 4 live samples
+    const int n0 = blockIdx.x * SPB;
+    if (wave < 8) {  // fc1: n-tile = wave, 13 k-steps
+      const f32x4 acc = cls_tile<13>(&sm.a2[0][0], A2P, sm.zrow, cf.frag, OFF_F1 + wave * 13, lane);
+      if (hi == 0) {
+        const int col = 16 * wave + lo;
+        const float bb = cf.fb1[col < F1 ? col : 0];
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = col < F1 ? fmaxf(acc[i] + bb, 0.f) : 0.f;
+          sm.h1[i][col] = f2bf(v[i]);
+        }
+        if (col < F1) *(uint2*)(cf.h1T + (int64_t)col * N + n0) = pack4(v[0], v[1], v[2], v[3]);
+      }
+    } else {  // meanwhile: a2^T for the fc1 weight gradient
+      for (int f = threadIdx.x - 512; f < F0; f += 512)
+        *(uint2*)(cf.a2T + (int64_t)f * N + n0) = make_uint2(
+            (uint32_t)sm.a2[0][f] | ((uint32_t)sm.a2[1][f] << 16), (uint32_t)sm.a2[2][f] | ((uint32_t)sm.a2[3][f] << 16));
+      if (threadIdx.x - 512 < SPB * 8) sm.h1[(threadIdx.x - 512) >> 3][128 + ((threadIdx.x - 512) & 7)] = 0;
+    }
+    __syncthreads();
+    if (wave < 6) {  // fc2: 6 n-tiles x 4 k-steps
+      const f32x4 acc = cls_tile<4>(&sm.h1[0][0], H1P, sm.zrow, cf.frag, OFF_F2 + wave * 4, lane);
+      if (hi == 0) {
+        const int col = 16 * wave + lo;
+        const float bb = cf.fb2[col < F2 ? col : 0];
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = col < F2 ? fmaxf(acc[i] + bb, 0.f) : 0.f;
+          sm.h2[i][col] = f2bf(v[i]);
+        }
+        if (col < F2) *(uint2*)(cf.h2T + (int64_t)col * N + n0) = pack4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {  // fc3: 1 n-tile x 3 k-steps -> fp32 logits
+      const f32x4 acc = cls_tile<3>(&sm.h2[0][0], H2P, sm.zrow, cf.frag, OFF_F3, lane);
+      if (hi == 0 && lo < F3) {
+        const float bb = cf.fb3[lo];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cf.logits[(int64_t)(n0 + i) * F3 + lo] = acc[i] + bb;
+      }
     }
   }
 }
@@ -221,15 +345,29 @@ struct BwdSmem {
   float red1[6][2][256];            // dW1 partials of waves 10..15
   float rb1[6][16];
   bf16x8 wfr[K2P * 64];             // conv2-dgrad B fragments
+  // fused classifier backward (MLP=true): gradients of the 4 samples as MFMA A rows
+  uint16_t dyl[SPB][DYP];           // dlogits, K pad 10..39 zero
+  uint16_t d2l[SPB][H2P];           // d(fc2 out) masked, pad 84..
+  uint16_t d1l[SPB][H1P];           // d(fc1 out) masked, pad 120..
+  uint16_t da2[SPB][A2N];           // d(pooled conv2 output)
+  uint16_t zrow[H1P];
 };
 
+struct ClsBwd {
+  const bf16x8* frag;
+  const float* dy;                  // dlogits [N][10] (already scaled by the upstream gradient)
+  const uint16_t *h1T, *h2T;        // forward activations (ReLU masks)
+  uint16_t *dyT, *d2T, *d1T;        // transposed gradients for the weight-gradient launch
+};
+
+template <bool MLP>
 __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__ x, const uint16_t* __restrict__ a1g,
                                                        const uint8_t* __restrict__ code1g,
                                                        const uint16_t* __restrict__ da2g,
                                                        const uint8_t* __restrict__ code2g,
                                                        const float* __restrict__ w2, float* __restrict__ dw1,
                                                        float* __restrict__ db1, float* __restrict__ dw2,
-                                                       float* __restrict__ db2, int N, int rounds) {
+                                                       float* __restrict__ db2, int N, int rounds, ClsBwd cb) {
   __shared__ __attribute__((aligned(16))) BwdSmem sm;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int hi = lane >> 4, lo = lane & 15;
@@ -256,9 +394,63 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
   f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   float sb1 = 0.f;
 
+  if (MLP)
+    for (int i = threadIdx.x; i < H1P; i += NTHR) sm.zrow[i] = 0;
+
   for (int rd = 0; rd < rounds; ++rd) {
     const int nbase = (blockIdx.x * rounds + rd) * SPB;
     __syncthreads();
+    if constexpr (MLP) {
+      // ---- classifier input-gradient chain (host guarantees N % 8 == 0: 4 live samples)
+      if (threadIdx.x < SPB * DYP) {
+        const int sl = threadIdx.x / DYP, o = threadIdx.x % DYP;
+        sm.dyl[sl][o] = f2bf(o < F3 ? cb.dy[(int64_t)(nbase + sl) * F3 + o] : 0.f);
+      } else if (threadIdx.x >= 256 && threadIdx.x < 256 + F3) {
+        const int o = threadIdx.x - 256;
+        const float* d = cb.dy + (int64_t)nbase * F3 + o;
+        *(uint2*)(cb.dyT + (int64_t)o * N + nbase) = pack4(d[0], d[F3], d[2 * F3], d[3 * F3]);
+      }
+      __syncthreads();
+      if (wave < 6) {  // fc3 dgrad: d2 = (dy W3) * [h2 > 0]
+        const f32x4 acc = cls_tile<1>(&sm.dyl[0][0], DYP, sm.zrow, cb.frag, OFF_B3 + wave, lane);
+        if (hi == 0) {
+          const int col = 16 * wave + lo;
+          const uint2 m = *(const uint2*)(cb.h2T + (int64_t)(col < F2 ? col : 0) * N + nbase);
+          const float mk[4] = {bf2f(m.x & 0xffff), bf2f(m.x >> 16), bf2f(m.y & 0xffff), bf2f(m.y >> 16)};
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = (col < F2 && mk[i] > 0.f) ? acc[i] : 0.f;
+            sm.d2l[i][col] = f2bf(v[i]);
+          }
+          if (col < F2) *(uint2*)(cb.d2T + (int64_t)col * N + nbase) = pack4(v[0], v[1], v[2], v[3]);
+        }
+      }
+      __syncthreads();
+      if (wave < 8) {  // fc2 dgrad: d1 = (d2 W2) * [h1 > 0]
+        const f32x4 acc = cls_tile<3>(&sm.d2l[0][0], H2P, sm.zrow, cb.frag, OFF_B2 + wave * 3, lane);
+        if (hi == 0) {
+          const int col = 16 * wave + lo;
+          const uint2 m = *(const uint2*)(cb.h1T + (int64_t)(col < F1 ? col : 0) * N + nbase);
+          const float mk[4] = {bf2f(m.x & 0xffff), bf2f(m.x >> 16), bf2f(m.y & 0xffff), bf2f(m.y >> 16)};
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = (col < F1 && mk[i] > 0.f) ? acc[i] : 0.f;
+            sm.d1l[i][col] = f2bf(v[i]);
+          }
+          if (col < F1) *(uint2*)(cb.d1T + (int64_t)col * N + nbase) = pack4(v[0], v[1], v[2], v[3]);
+        }
+      }
+      __syncthreads();
+      for (int t = wave; t < 25; t += 16) {  // fc1 dgrad: da2 = d1 W1 (400 outputs = 25 tiles)
+        const f32x4 acc = cls_tile<4>(&sm.d1l[0][0], H1P, sm.zrow, cb.frag, OFF_B1 + t * 4, lane);
+        if (hi == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sm.da2[i][16 * t + lo] = f2bf(acc[i]);
+        }
+      }
+    }
     // ---- phase A: stage
     for (int i = threadIdx.x; i < SPB * IMGN; i += NTHR) {
       const int sl = i / IMGN, e = i % IMGN;
@@ -286,7 +478,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
     for (int i = threadIdx.x; i < SPB * A2N; i += NTHR) {  // scatter the pooled gradients
       const int sl = i / A2N, e = i % A2N, co = e / 25, w = e % 25;
       const int n = nbase + sl, nc = n < N ? n : 0;
-      const uint16_t g = da2g[(int64_t)nc * A2N + e];
+      const uint16_t g = MLP ? sm.da2[sl][e] : da2g[(int64_t)nc * A2N + e];
       const uint8_t cd = code2g[(int64_t)nc * A2N + e];
       if (n < N && cd < 4) {
         const int rr = 2 * (w / Q2) + (cd >> 1), cc = 2 * (w % Q2) + (cd & 1);
@@ -437,8 +629,29 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
 RK_API int rk_lenet_conv_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                              void* a1, void* code1, void* a2, void* code2, int N, hipStream_t s) {
   const int grid = (N + SPB - 1) / SPB;
-  lenet_conv_fwd<<<grid, NTHR, 0, s>>>(x, w1, b1, w2, b2, (uint16_t*)a1, (uint8_t*)code1, (uint16_t*)a2,
-                                       (uint8_t*)code2, N);
+  lenet_conv_fwd<false><<<grid, NTHR, 0, s>>>(x, w1, b1, w2, b2, (uint16_t*)a1, (uint8_t*)code1, (uint16_t*)a2,
+                                              (uint8_t*)code2, N, ClsFwd{});
+  return (int)hipGetLastError();
+}
+
+// fc weights (fp32 master) -> bf16 MFMA fragment table (NFRAG x 64 x 16 B)
+RK_API int rk_lenet_prep(const float* fc1w, const float* fc2w, const float* fc3w, void* frag, hipStream_t s) {
+  lenet_prep_kernel<<<NFRAG, 64, 0, s>>>(fc1w, fc2w, fc3w, (bf16x8*)frag);
+  return (int)hipGetLastError();
+}
+
+RK_API int rk_lenet_frag_bytes() { return NFRAG * 64 * 16; }
+
+// Whole LeNet forward (conv stack + classifier) for N % 8 == 0: logits [N][10] fp32, plus the
+// saved state of the fused backward (a1, codes) and the transposed activations of the wgrads.
+RK_API int rk_lenet_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+                        const void* frag, const float* fb1, const float* fb2, const float* fb3, void* a1,
+                        void* code1, void* code2, void* a2T, void* h1T, void* h2T, float* logits, int N,
+                        hipStream_t s) {
+  if (N % 8) return (int)hipErrorInvalidValue;
+  ClsFwd cf{(const bf16x8*)frag, fb1, fb2, fb3, (uint16_t*)a2T, (uint16_t*)h1T, (uint16_t*)h2T, logits};
+  lenet_conv_fwd<true><<<N / SPB, NTHR, 0, s>>>(x, w1, b1, w2, b2, (uint16_t*)a1, (uint8_t*)code1, nullptr,
+                                                (uint8_t*)code2, N, cf);
   return (int)hipGetLastError();
 }
 
@@ -450,7 +663,22 @@ RK_API int rk_lenet_conv_bwd(const float* x, const void* a1, const void* code1, 
   if (rounds < 1) rounds = 1;
   const int per_block = SPB * rounds;
   const int grid = (N + per_block - 1) / per_block;
-  lenet_conv_bwd<<<grid, NTHR, 0, s>>>(x, (const uint16_t*)a1, (const uint8_t*)code1, (const uint16_t*)da2,
-                                       (const uint8_t*)code2, w2, dw1, db1, dw2, db2, N, rounds);
+  lenet_conv_bwd<false><<<grid, NTHR, 0, s>>>(x, (const uint16_t*)a1, (const uint8_t*)code1, (const uint16_t*)da2,
+                                              (const uint8_t*)code2, w2, dw1, db1, dw2, db2, N, rounds, ClsBwd{});
+  return (int)hipGetLastError();
+}
+
+// Fused backward for N % 8 == 0 and N % (4*rounds) == 0: classifier input-gradient chain from
+// dlogits, then the conv stack; writes dy^T, d2^T, d1^T for rk_mlp3_wgrad and ACCUMULATES the
+// conv weight/bias gradients.
+RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const void* code2, const float* w2,
+                        const void* frag, const float* dy, const void* h1T, const void* h2T, void* dyT, void* d2T,
+                        void* d1T, float* dw1, float* db1, float* dw2, float* db2, int N, int rounds, hipStream_t s) {
+  if (rounds < 1) rounds = 1;
+  if (N % 8 || N % (SPB * rounds)) return (int)hipErrorInvalidValue;
+  ClsBwd cb{(const bf16x8*)frag, dy, (const uint16_t*)h1T, (const uint16_t*)h2T, (uint16_t*)dyT, (uint16_t*)d2T,
+            (uint16_t*)d1T};
+  lenet_conv_bwd<true><<<N / (SPB * rounds), NTHR, 0, s>>>(x, (const uint16_t*)a1, (const uint8_t*)code1, nullptr,
+                                                           (const uint8_t*)code2, w2, dw1, db1, dw2, db2, N, rounds, cb);
   return (int)hipGetLastError();
 }

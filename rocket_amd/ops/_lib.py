@@ -40,6 +40,10 @@ KERNEL_SIGS = {
     "rk_conv_pool_dgrad": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int] + [c_int] * 7 + [c_void_p]),
     "rk_lenet_conv_fwd": (c_int, [c_void_p] * 9 + [c_int, c_void_p]),
     "rk_lenet_conv_bwd": (c_int, [c_void_p] * 10 + [c_int, c_int, c_void_p]),
+    "rk_lenet_prep": (c_int, [c_void_p] * 5),
+    "rk_lenet_frag_bytes": (c_int, []),
+    "rk_lenet_fwd": (c_int, [c_void_p] * 16 + [c_int, c_void_p]),
+    "rk_lenet_bwd": (c_int, [c_void_p] * 16 + [c_int, c_int, c_void_p]),
     "rk_mlp3_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                             c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "rk_mlp3_dgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,

@@ -145,6 +145,75 @@ class _MLPHead(torch.autograd.Function):
         return (dx, *_finish(params, bufs, direct))
 
 
+class _LeNetFused(torch.autograd.Function):
+    """The whole LeNet: conv stack + classifier forward in ONE launch (after a tiny weight-fragment
+    prep launch), classifier input-gradient chain + conv backward in ONE launch, the three
+    classifier weight gradients in one grouped launch.  Needs N % 8 == 0."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, f1w, f1b, f2w, f2b, f3w, f3b):
+        lib = _lib.kernels()
+        x = x.contiguous().float()
+        N = x.shape[0]
+        assert tuple(x.shape[1:]) == (1, 28, 28) and N % 8 == 0, "fused LeNet expects [N,1,28,28], N % 8 == 0"
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        cw = [t.detach().float().contiguous() for t in (w1, b1, w2, b2, f1w, f1b, f2w, f2b, f3w, f3b)]
+        frag = torch.empty(int(lib.rk_lenet_frag_bytes()), dtype=torch.uint8, device=dev)
+        _lib.check(lib.rk_lenet_prep(cw[4].data_ptr(), cw[6].data_ptr(), cw[8].data_ptr(), frag.data_ptr(), stream),
+                   "rk_lenet_prep")
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        a1 = torch.empty(N, 1176, **bf)
+        c1 = torch.empty(N, 1176, dtype=torch.uint8, device=dev)
+        c2 = torch.empty(N, 400, dtype=torch.uint8, device=dev)
+        a2T = torch.empty(400, N, **bf)
+        h1T = torch.empty(120, N, **bf)
+        h2T = torch.empty(84, N, **bf)
+        logits = torch.empty(N, 10, dtype=torch.float32, device=dev)
+        _lib.check(lib.rk_lenet_fwd(x.data_ptr(), cw[0].data_ptr(), cw[1].data_ptr(), cw[2].data_ptr(),
+                                    cw[3].data_ptr(), frag.data_ptr(), cw[5].data_ptr(), cw[7].data_ptr(),
+                                    cw[9].data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(), a2T.data_ptr(),
+                                    h1T.data_ptr(), h2T.data_ptr(), logits.data_ptr(), N, stream), "rk_lenet_fwd")
+        ctx.params = (w1, b1, w2, b2, f1w, f1b, f2w, f2b, f3w, f3b)
+        ctx.save_for_backward(x, a1, c1, c2, a2T, h1T, h2T, frag, cw[2])
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        lib = _lib.kernels()
+        x, a1, c1, c2, a2T, h1T, h2T, frag, w2c = ctx.saved_tensors
+        N = x.shape[0]
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        dy = dlogits.contiguous().float()
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        dyT = torch.empty(10, N, **bf)
+        d2T = torch.empty(84, N, **bf)
+        d1T = torch.empty(120, N, **bf)
+        params = ctx.params
+        bufs, direct = _grad_targets(params, dev)
+        rounds = 2 if N % 16 == 0 and N >= 4096 else 1
+        _lib.check(lib.rk_lenet_bwd(x.data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(), w2c.data_ptr(),
+                                    frag.data_ptr(), dy.data_ptr(), h1T.data_ptr(), h2T.data_ptr(), dyT.data_ptr(),
+                                    d2T.data_ptr(), d1T.data_ptr(), bufs[0].data_ptr(), bufs[1].data_ptr(),
+                                    bufs[2].data_ptr(), bufs[3].data_ptr(), N, rounds, stream), "rk_lenet_bwd")
+        probs = ((dyT, h2T, bufs[8], bufs[9], 10, 84), (d2T, h1T, bufs[6], bufs[7], 84, 120),
+                 (d1T, a2T, bufs[4], bufs[5], 120, 400))
+        P = ctypes.c_void_p * 3
+        I = ctypes.c_int * 3
+        _lib.check(lib.rk_mlp3_wgrad(3, P(*[q[0].data_ptr() for q in probs]), P(*[q[1].data_ptr() for q in probs]),
+                                     P(*[q[2].data_ptr() for q in probs]), P(*[q[3].data_ptr() for q in probs]),
+                                     I(*[q[4] for q in probs]), I(*[q[5] for q in probs]), N, stream),
+                   "rk_mlp3_wgrad")
+        return (None, *_finish(params, bufs, direct))
+
+
+def lenet_forward(x, conv1, conv2, fc1, fc2, fc3):
+    """Fused LeNet logits (N % 8 == 0)."""
+    return _LeNetFused.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, fc1.weight, fc1.bias,
+                             fc2.weight, fc2.bias, fc3.weight, fc3.bias)
+
+
 def mlp_head(x, layers: List[torch.nn.Linear]):
     (l1, l2, l3) = layers
     return _MLPHead.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias)

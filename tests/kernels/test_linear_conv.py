@@ -123,3 +123,25 @@ def test_lenet_fused_blocks(N):
     yr.backward(g)
     for (name, p), pr in zip(net.named_parameters(), ref.parameters()):
         assert _rel(p.grad, pr.grad) < 3e-2, (name, _rel(p.grad, pr.grad))
+
+
+@pytest.mark.parametrize("N", [1024, 64, 4096])
+def test_lenet_whole_fused(N):
+    """One-launch forward / one-launch backward LeNet vs the fp32 reference (bf16 activation contract)."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.lenet import lenet_forward
+
+    torch.manual_seed(2)
+    net = LeNet(fused=False).cuda()
+    ref = LeNet(fused=False).cuda()
+    ref.load_state_dict(net.state_dict())
+    x = torch.rand(N, 1, 28, 28, device="cuda")
+    y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
+    _, yr = _ref_lenet(x, ref.conv1.weight, ref.conv1.bias, ref.conv2.weight, ref.conv2.bias, ref.fc1, ref.fc2, ref.fc3)
+    assert y.shape == (N, 10) and y.dtype == torch.float32
+    assert _rel(y, yr) < 1e-2, _rel(y, yr)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    for (name, p), pr in zip(net.named_parameters(), ref.parameters()):
+        assert _rel(p.grad, pr.grad) < 3e-2, (name, _rel(p.grad, pr.grad))
