@@ -27,6 +27,7 @@ from rocket_amd.core import (  # noqa: F401
     Tracker,
 )
 from rocket_amd.runtime.data import DeviceTensorDataset  # noqa: F401
+from rocket_amd.runtime.host_data import HostTensorDataset  # noqa: F401
 from rocket_amd.runtime.engine import Engine  # noqa: F401
 
 __version__ = "0.1.0"

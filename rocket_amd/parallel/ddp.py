@@ -116,6 +116,8 @@ class DataParallel(nn.Module):
         self._build_buckets(bucket_cap_mb, first_bucket_mb)
         self._armed = False
         self._deferred = False
+        # native transport: per-bucket all-reduce on a side stream, one join before the optimizer
+        self._native = self.comm.make_reducer([b.flat for b in self.buckets]) if hasattr(self.comm, "make_reducer") else None
 
     # ----------------------------------------------------------------- setup
     def _flat_broadcast(self, tensors: List[torch.Tensor]) -> None:
@@ -229,9 +231,12 @@ class DataParallel(nn.Module):
 
     def reduce_now(self) -> None:
         """Average every bucket (incl. the side channel) across ranks; stream-ordered, no host wait."""
-        works = [self.comm.all_reduce_avg(b.flat) for b in self.buckets]
+        works = [self._launch(b) for b in self.buckets]
+        if self._native is not None:
+            self._native.join()
         for w in works:
-            w.wait()
+            if w is not None:
+                w.wait()
 
     def side_slot(self, n: int = 1) -> torch.Tensor:
         """``n`` fp32 slots that are averaged together with the gradients on every sync step."""
@@ -264,7 +269,7 @@ class DataParallel(nn.Module):
         b.ready.add(i)
         b.pending -= 1
         if b.pending == 0 and self.require_backward_grad_sync:
-            b.work = self.comm.all_reduce_avg(b.flat)
+            b.work = self._launch(b)
 
     def _finalize(self) -> None:
         """Runs at the end of backward: reduce buckets with params that got no grad."""
@@ -280,11 +285,19 @@ class DataParallel(nn.Module):
                         if i not in b.ready:
                             b.view(i).zero_()
                             b.params[i].grad = b.view(i)
-                b.work = self.comm.all_reduce_avg(b.flat)
+                b.work = self._launch(b)
+        if self._native is not None:
+            self._native.join()
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
                 b.work = None
+
+    def _launch(self, b: _Bucket):
+        if self._native is not None:
+            self._native.launch(b.index)
+            return None
+        return self.comm.all_reduce_avg(b.flat)
 
     def owns(self, p) -> bool:
         return id(p) in self._ids

@@ -37,6 +37,7 @@ from torch import nn
 from rocket_amd.parallel.ddp import DataParallel, unwrap
 from rocket_amd.runtime import comm as _comm
 from rocket_amd.runtime import checkpoint_io
+from rocket_amd.runtime.host_data import HostLoader, HostTensorDataset
 from rocket_amd.runtime.data import (
     DeviceLoader,
     DeviceTensorDataset,
@@ -189,6 +190,7 @@ class Engine:
         even_batches: bool = True,
         log_with: List[str] | None = None,
         flat_grads: bool | None = None,
+        comm: str | None = None,
         **unused: Any,
     ):
         env_mp = os.environ.get("ROCKET_MIXED_PRECISION", os.environ.get("ACCELERATE_MIXED_PRECISION"))
@@ -214,6 +216,9 @@ class Engine:
         self._wrapped: dict = {}
         self._grad_owners: list = []  # FlatGrads / DataParallel owning persistent .grad storage
         self.flat_grads = self.device.type == "cuda" if flat_grads is None else bool(flat_grads)
+        # data-parallel transport: "torch" (ProcessGroupNCCL = RCCL) or "native" (own RCCL communicator)
+        self.comm_backend = comm or ("native" if os.environ.get("ROCKET_NATIVE_COMM") == "1" else "torch")
+        self._native_comm = None
         self._optimizers: List[EngineOptimizer] = []
         self._schedulers: List[EngineScheduler] = []
         self._dataloaders: List[_LoaderBase] = []
@@ -295,7 +300,7 @@ class Engine:
             model.forward = forward
         self._models.append(model)
         if self.distributed and any(p.requires_grad for p in model.parameters()):
-            wrapped = DataParallel(model, bucket_cap_mb=self.bucket_cap_mb)
+            wrapped = DataParallel(model, bucket_cap_mb=self.bucket_cap_mb, comm=self._dp_comm())
             self._wrapped[id(model)] = wrapped
             self._grad_owners.append(wrapped)
             return wrapped
@@ -304,6 +309,15 @@ class Engine:
 
             self._grad_owners.append(FlatGrads([p for p in model.parameters()]))
         return model
+
+    def _dp_comm(self):
+        if self.comm_backend != "native" or self.device.type != "cuda":
+            return None  # DataParallel's default: the torch.distributed RCCL/gloo group
+        if self._native_comm is None:
+            from rocket_amd.parallel.rccl import RcclComm
+
+            self._native_comm = RcclComm(self.device)
+        return self._native_comm
 
     def grad_owner(self, p):
         for o in self._grad_owners:
@@ -367,6 +381,8 @@ class Engine:
         )
         if isinstance(dataset, DeviceTensorDataset):
             loader = DeviceLoader(dataset, **kwargs, **common)
+        elif isinstance(dataset, HostTensorDataset):
+            loader = HostLoader(dataset, device=self.device if device_placement else None, **kwargs, **common)
         else:
             kwargs.setdefault("pin_memory", self.device.type == "cuda")
             loader = ShardedLoader(dataset, device=self.device if device_placement else None, **kwargs, **common)
