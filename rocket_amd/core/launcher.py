@@ -71,6 +71,20 @@ def notebook_launch(fn: Callable, args=(), num_processes: int = 1) -> None:
                        start_method="spawn", join=True)
 
 
+def latest_checkpoint(root: str) -> str | None:
+    """Newest directory under ``root`` holding a complete checkpoint (``random_states_0.pkl`` is
+    written last by the checkpoint writer), or None."""
+    best, best_t = None, -1.0
+    if not root or not os.path.isdir(root):
+        return None
+    for dirpath, _dirs, files in os.walk(root):
+        if "random_states_0.pkl" in files:
+            t = os.path.getmtime(os.path.join(dirpath, "random_states_0.pkl"))
+            if t > best_t:
+                best, best_t = dirpath, t
+    return best
+
+
 class Launcher(Dispatcher):
     def __init__(
         self,
@@ -224,6 +238,13 @@ class Launcher(Dispatcher):
             raise RuntimeError("You need to resume your training in the exact same distributed setup.")
 
     def resume(self, path: str, load_capsules: bool = True) -> "Launcher":
+        """Resume from a checkpoint directory; ``path="latest"`` picks the newest checkpoint written
+        under ``logging_dir/tag`` by any previous version of this experiment (auto-resume)."""
+        if path == "latest":
+            path = latest_checkpoint(os.path.join(self._logging_dir, self._tag or ""))
+            if path is None:
+                self._logger.info("resume('latest'): no checkpoint found, starting fresh")
+                return self
         self._resume_from = path
         self._load_capsules = load_capsules
         return self

@@ -94,9 +94,10 @@ def save_state(engine, output_dir: str) -> Path:
     }
     if torch.cuda.is_available() and torch.cuda.is_initialized():
         states["torch_cuda_manual_seed"] = torch.cuda.get_rng_state_all()
-    torch.save(states, out / f"random_states_{engine.process_index}.pkl")
     for i, obj in enumerate(engine._custom_objects):
         torch.save(obj.state_dict(), out / f"custom_checkpoint_{i}.pkl")
+    # written last: its presence marks a complete checkpoint (Launcher.resume("latest"))
+    torch.save(states, out / f"random_states_{engine.process_index}.pkl")
     return out
 
 

@@ -216,3 +216,18 @@ def test_looper_run_every(tmp_path):
 
 def test_events_enum_values():
     assert [e.value for e in Events] == ["setup", "destroy", "set", "reset", "launch"]
+
+
+def test_resume_latest(tmp_path):
+    part, *_ = _tree(tmp_path, n=10, bs=2, ckpt_every=2, repeats=4, num_epochs=1)
+    part.launch()
+    from rocket_amd.core.launcher import latest_checkpoint
+
+    latest = latest_checkpoint(str(tmp_path / "exp"))
+    assert latest is not None and latest.endswith("003")
+    res, *_ = _tree(tmp_path, n=10, bs=2, ckpt_every=0, num_epochs=1)
+    res.resume("latest")
+    assert res._resume_from == latest
+    res.launch()
+    fresh, *_ = _tree(tmp_path / "none", n=10, bs=2, ckpt_every=0)
+    assert fresh.resume("latest")._resume_from is None

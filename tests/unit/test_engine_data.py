@@ -195,3 +195,11 @@ def test_collate_keeps_builtin_leaves():
 def test_move_nested():
     out = torch_move({"a": [torch.ones(1), "s"], "b": (torch.zeros(1),)}, torch.device("cpu"))
     assert out["a"][1] == "s" and isinstance(out["b"], tuple)
+
+
+def test_ga_oracle_from_survey():
+    """SURVEY §2.4 verified oracle: 7 batches/epoch, GA=2, 2 epochs -> [0,1,0,1,0,1,1]*2, 8 updates."""
+    tree, probe, steps, _ = _ga_tree(n_batches=7, ga=2, epochs=2)
+    tree.launch()
+    assert [int(s) for s in probe.sync] == [0, 1, 0, 1, 0, 1, 1] * 2
+    assert len(steps) == 8
