@@ -179,6 +179,7 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "step_ms_p50": round(p50, 4),
+            "host_ms_p50": round(summ.get("host_ms_p50", 0.0), 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,

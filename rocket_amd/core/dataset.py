@@ -84,7 +84,10 @@ class Dataset(Capsule):
             if attrs.looper is not None:
                 attrs.looper.terminate = True
             return
-        attrs.batch = torch_move(data, self._accelerator.device)
+        if getattr(self._active_dataloader, "device_resident", False):
+            attrs.batch = data  # device/host loaders already delivered the batch on the device
+        else:
+            attrs.batch = torch_move(data, self._accelerator.device)
         if attrs.looper is not None:
             attrs.looper.terminate = False
         self._batch_idx += 1

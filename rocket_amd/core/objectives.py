@@ -94,6 +94,7 @@ class Loss(Capsule):
         self._slot = torch.zeros(1, dtype=torch.int64, device=dev)
         self._zero = torch.zeros(1, device=dev)
         self._one = torch.ones((), device=dev)
+        self._ring_views = list(self._ring.unbind(0))  # one 0-d view per slot, made once
 
     def graph_prepare(self, attrs: Attributes | None = None) -> None:
         v = self._value
@@ -103,8 +104,18 @@ class Loss(Capsule):
 
     def graph_device(self, attrs: Attributes) -> None:
         engine = self._accelerator
-        loss = self._objective(attrs.batch)
         sync_here = engine.sync_gradients and not attrs.graph_split
+        fused = getattr(self._objective, "loss_and_grad", None)
+        if fused is not None and engine.scaler is None:
+            # objective supplies loss AND d(outputs) in one launch, with the loss bookkeeping folded
+            # in: backward starts directly from the outputs (no loss node, no seed fill)
+            scale = 1.0 / engine.gradient_accumulation_steps
+            res = fused(attrs.batch, scale, (self._acc, self._ring, self._slot, scale, sync_here))
+            if res is not None:
+                _, outs, grads = res
+                torch.autograd.backward(outs, grads)
+                return
+        loss = self._objective(attrs.batch)
         _data_ops.loss_accum(loss.detach().reshape(1), self._acc, self._ring, self._slot,
                              1.0 / engine.gradient_accumulation_steps, sync_here)
         if loss.dtype == self._one.dtype and loss.dim() == 0:
@@ -121,7 +132,7 @@ class Loss(Capsule):
             self._acc_pending = True
             return
         self._acc_pending = False
-        value = LazyScalar(self._ring[self._slot_host])
+        value = LazyScalar(self._ring_views[self._slot_host])
         self._slot_host = (self._slot_host + 1) % self.RING
         if attrs.tracker is not None:
             attrs.tracker.scalars.append(Attributes(step=self._step, data={self._tag: value}))

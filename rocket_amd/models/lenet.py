@@ -87,6 +87,21 @@ class CrossEntropy(nn.Module):
         return F.cross_entropy(logits.float(), target)
 
 
+    def loss_and_grad(self, batch, grad_scale: float, accum=None):
+        """Training-step fast path (used by the Loss capsule under graph capture): loss and
+        d(logits) in one launch.  Returns ``(loss, outputs, output_grads)`` or None."""
+        logits, target = batch[2], batch[1]
+        if self._fused is False or logits.device.type != "cuda":
+            return None
+        from rocket_amd.ops.cross_entropy import ce_train
+
+        res = ce_train(logits, target, grad_scale, accum)
+        if res is None:
+            return None
+        loss, dlogits = res
+        return loss, [logits], [dlogits]
+
+
 def synthetic_mnist(n: int = 60000, device="cpu", seed: int = 0, dtype=torch.float32):
     """Random 1×28×28 images in [0,1) and labels in [0,10) (no network: no real MNIST)."""
     g = torch.Generator(device="cpu").manual_seed(seed)

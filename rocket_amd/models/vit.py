@@ -55,9 +55,12 @@ class Block(nn.Module):
         self.norm2 = FusedLayerNorm(dim, eps=1e-6)
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
 
-    def forward(self, x):
-        x = x + self.attn(self.norm1(x))
-        return x + self.mlp(self.norm2(x))
+    def forward(self, x, pending=None):
+        """x: fp32 residual stream; pending: the previous sub-layer's output, not yet added.
+        Each residual add is fused into the LayerNorm that follows it."""
+        x, h = self.norm1.add_forward(x, pending)
+        x, h = self.norm2.add_forward(x, self.attn(h))
+        return x, self.mlp(h)
 
 
 class VisionTransformer(nn.Module):
@@ -69,7 +72,7 @@ class VisionTransformer(nn.Module):
         n = (img_size // patch) ** 2
         self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
         self.pos_embed = nn.Parameter(torch.zeros(1, n + 1, dim))
-        self.blocks = nn.Sequential(*[Block(dim, heads, mlp_ratio) for _ in range(depth)])
+        self.blocks = nn.ModuleList([Block(dim, heads, mlp_ratio) for _ in range(depth)])
         self.norm = FusedLayerNorm(dim, eps=1e-6)
         self.head = nn.Linear(dim, num_classes)
         nn.init.trunc_normal_(self.pos_embed, std=0.02)
@@ -85,8 +88,11 @@ class VisionTransformer(nn.Module):
         x = self.patch_embed(x).flatten(2).transpose(1, 2)  # [B, 196, D]
         x = torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1)
         x = x.float() + self.pos_embed  # fp32 residual stream
-        x = self.blocks(x)
-        return self.head(self.norm(x)[:, 0])
+        pending = None
+        for blk in self.blocks:
+            x, pending = blk(x, pending)
+        _, h = self.norm.add_forward(x, pending)
+        return self.head(h[:, 0])
 
     def forward(self, batch):
         if isinstance(batch, torch.Tensor):

@@ -122,6 +122,78 @@ __global__ void __launch_bounds__(256) ce_bwd_kernel(const T* __restrict__ logit
   }
 }
 
+// Training-step variant (one launch instead of fwd + loss bookkeeping + bwd): every block
+// counts the valid targets of the whole batch itself (N <= 65536, a few L2-resident loads per
+// thread) so it can write its rows' d(logits) = grad_scale * w * (softmax - target dist)
+// immediately; the last block reduces the loss and folds it into the Loss capsule's device
+// accumulator / report ring (acc may be null).
+struct CeTrainAcc {
+  float* acc;
+  float* ring;
+  int64_t* slot;
+  int ring_size;
+  float scale;
+  int sync;
+};
+
+template <typename T, bool WAVE>
+__global__ void __launch_bounds__(256) ce_train_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
+                                                       T* __restrict__ dlogits, int N, int C, int64_t ignore_index,
+                                                       float smoothing, float grad_scale, float* partials,
+                                                       unsigned* counter, float* out, int mean, CeTrainAcc la) {
+  __shared__ float red[8];
+  __shared__ int flag;
+  float cnt = 0.f;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) cnt += target[i] != ignore_index ? 1.f : 0.f;
+  const float nvalid = block_sum(cnt, red);
+  const float w = grad_scale * (mean ? (nvalid > 0.f ? 1.f / nvalid : 0.f) : 1.f);
+  const int lane = threadIdx.x & 63;
+  const int rows_per_block = WAVE ? (blockDim.x >> 6) : blockDim.x;
+  const int row = blockIdx.x * rows_per_block + (WAVE ? (threadIdx.x >> 6) : threadIdx.x);
+  float loss = 0.f;
+  if (row < N) {
+    const T* x = logits + (int64_t)row * C;
+    T* dx = dlogits + (int64_t)row * C;
+    const int64_t t = target[row];
+    const int j0 = WAVE ? lane : 0, js = WAVE ? 64 : 1;
+    if (t == ignore_index) {
+      for (int j = j0; j < C; j += js) Ld<T>::put(dx, j, 0.f);
+    } else {
+      const RowStats st = row_stats<T, WAVE>(x, C, t, lane);
+      loss = (1.f - smoothing) * (st.lse - st.xt) + smoothing * (st.lse - st.xmean);
+      const float off = smoothing / C;
+      for (int j = j0; j < C; j += js) {
+        const float p = __expf(Ld<T>::get(x, j) - st.lse);
+        Ld<T>::put(dx, j, w * (p - off - (j == t ? (1.f - smoothing) : 0.f)));
+      }
+    }
+    if (WAVE && lane != 0) loss = 0.f;
+  }
+  const float bl = block_sum(loss, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = bl;
+  if (last_block_arrived(counter, &flag)) {
+    float sum = 0.f;
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) sum += partials[b];
+    sum = block_sum(sum, red);
+    if (threadIdx.x == 0) {
+      const float l = mean ? (nvalid > 0.f ? sum / nvalid : NAN) : sum;
+      out[0] = l;
+      out[1] = nvalid;
+      if (la.acc) {
+        float v = la.acc[0] + l * la.scale;
+        if (la.sync) {
+          const int64_t k = la.slot[0];
+          la.ring[k] = v;
+          la.slot[0] = (k + 1) % la.ring_size;
+          v = 0.f;
+        }
+        la.acc[0] = v;
+      }
+    }
+    reset_counter(counter);
+  }
+}
+
 template <typename T>
 hipError_t launch_fwd(const void* logits, const int64_t* target, int N, int C, int64_t ignore, float eps,
                       float* partials, unsigned* counter, float* out, int mean, hipStream_t s) {
@@ -166,6 +238,26 @@ RK_API int rk_ce_bwd(const void* logits, int dtype, const int64_t* target, void*
   if (N <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   return (int)(dtype == BF16 ? launch_bwd<uint16_t>(logits, target, dlogits, N, C, ignore_index, smoothing, grad_out, stats, mean, s)
                              : launch_bwd<float>(logits, target, dlogits, N, C, ignore_index, smoothing, grad_out, stats, mean, s));
+}
+
+RK_API int rk_ce_train(const void* logits, int dtype, const int64_t* target, void* dlogits, int N, int C,
+                       int64_t ignore_index, float smoothing, float grad_scale, float* partials, unsigned* counter,
+                       float* out, int mean, float* acc, float* ring, int64_t* slot, int ring_size, float acc_scale,
+                       int sync, hipStream_t s) {
+  if (N <= 0 || C <= 0 || N > 65536) return (int)hipErrorInvalidValue;
+  const bool wave = C > 64;
+  const int rows = wave ? 4 : 256;
+  const int grid = (N + rows - 1) / rows;
+  CeTrainAcc la{acc, ring, slot, ring_size, acc_scale, sync};
+#define RK_CT(T, W) ce_train_kernel<T, W><<<grid, 256, 0, s>>>((const T*)logits, target, (T*)dlogits, N, C, ignore_index, \
+                                                               smoothing, grad_scale, partials, counter, out, mean, la)
+  if (dtype == BF16) {
+    if (wave) RK_CT(uint16_t, true); else RK_CT(uint16_t, false);
+  } else {
+    if (wave) RK_CT(float, true); else RK_CT(float, false);
+  }
+#undef RK_CT
+  return (int)hipGetLastError();
 }
 
 RK_API int rk_ce_partials_needed(int N, int C) {

@@ -406,7 +406,8 @@ __device__ __forceinline__ void st4<uint16_t>(uint16_t* p, const float* v) {
 }
 
 template <typename T, typename TO, int NV>
-__global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ g,
+__global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const T* __restrict__ x, const TO* __restrict__ res,
+                                                      T* __restrict__ sum_out, const float* __restrict__ g,
                                                       const float* __restrict__ b, TO* __restrict__ y,
                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                       int64_t rows, int C, float eps) {
@@ -421,6 +422,13 @@ __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const T* __restrict__ x, c
     const int c = (j * 64 + lane) * 4;
     if (c < C) {
       ld4<T>(xr + c, v[j]);
+      if (res) {  // fused residual add: s = x + branch, written once for the next residual
+        float r[4];
+        ld4<TO>(res + row * C + c, r);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[j][k] += r[k];
+        st4<T>(sum_out + row * C + c, v[j]);
+      }
     } else {
       v[j][0] = v[j][1] = v[j][2] = v[j][3] = 0.f;
     }
@@ -460,6 +468,7 @@ template <typename T, typename TO, int NV>
 __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
                                                       const float* __restrict__ g, const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                      const T* __restrict__ dsum, TO* __restrict__ dres,
                                                       float* part, int64_t rows, int C, int rows_per_block) {
   extern __shared__ float sm[];  // [LN_W][2][C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -501,7 +510,14 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
         float o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) o[k] = rstd * (gy[j][k] - s1 - xh[j][k] * s2);
+        if (dsum) {  // the residual stream's own gradient joins here (fused add-norm)
+          float d[4];
+          ld4<T>(dsum + row * C + c, d);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o[k] += d[k];
+        }
         st4<T>(dx + row * C + c, o);
+        if (dres) st4<TO>(dres + row * C + c, o);  // gradient of the added branch
       }
     }
   }
@@ -640,12 +656,14 @@ RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void*
 }
 
 // LayerNorm forward over rows of C (C % 4 == 0, C <= 4096).  dt: x dtype, dto: y dtype.
-RK_API int rk_ln_fwd(int dt, int dto, const void* x, const float* g, const float* b, void* y, float* mean, float* rstd,
-                     int64_t rows, int C, float eps, hipStream_t s) {
+// res (dtype dto) / sum_out (dtype dt) may be null: y = LN(x [+ res]), sum_out = x + res
+RK_API int rk_ln_fwd(int dt, int dto, const void* x, const void* res, void* sum_out, const float* g, const float* b,
+                     void* y, float* mean, float* rstd, int64_t rows, int C, float eps, hipStream_t s) {
   if (C % 4 || C > 64 * 4 * LN_MAXV) return (int)hipErrorInvalidValue;
   const int grid = (int)((rows + LN_W - 1) / LN_W);
   const int nv = (C + 255) / 256;
-#define RK_LF(T, TO, NV) ln_fwd_kernel<T, TO, NV><<<grid, LN_T, 0, s>>>((const T*)x, g, b, (TO*)y, mean, rstd, rows, C, eps)
+#define RK_LF(T, TO, NV) \
+  ln_fwd_kernel<T, TO, NV><<<grid, LN_T, 0, s>>>((const T*)x, (const TO*)res, (T*)sum_out, g, b, (TO*)y, mean, rstd, rows, C, eps)
 #define RK_LFN(T, TO)                 \
   if (nv <= 1) RK_LF(T, TO, 1);       \
   else if (nv <= 2) RK_LF(T, TO, 2);  \
@@ -670,16 +688,18 @@ RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
 }
 
 // LayerNorm backward; dgamma/dbeta accumulated (+=). dt: x/dx dtype, dto: dy dtype.
+// dsum (dtype dt) / dres (dtype dto) may be null: dx = LN_bwd(dy) [+ dsum], dres = dx
 RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float* g, const float* mean,
-                     const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int C, float* ws,
-                     unsigned* counter, hipStream_t s) {
+                     const float* rstd, void* dx, const void* dsum, void* dres, float* dgamma, float* dbeta,
+                     int64_t rows, int C, float* ws, unsigned* counter, hipStream_t s) {
   if (C % 4 || C > 64 * 4 * LN_MAXV) return (int)hipErrorInvalidValue;
   const int rpb = LN_BWD_RPB;
   const int grid = (int)((rows + rpb - 1) / rpb);
   const int nv = (C + 255) / 256;
   const size_t smem = (size_t)LN_W * 2 * C * sizeof(float);
 #define RK_LB(T, TO, NV) \
-  ln_bwd_kernel<T, TO, NV><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx, ws, rows, C, rpb)
+  ln_bwd_kernel<T, TO, NV><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx, (const T*)dsum, \
+                                                    (TO*)dres, ws, rows, C, rpb)
 #define RK_LBN(T, TO)                 \
   if (nv <= 1) RK_LB(T, TO, 1);       \
   else if (nv <= 2) RK_LB(T, TO, 2);  \

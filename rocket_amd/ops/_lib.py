@@ -31,6 +31,8 @@ KERNEL_SIGS = {
     "rk_ce_fwd": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "rk_ce_bwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int64, c_float, c_void_p, c_void_p, c_int, c_void_p]),
     "rk_ce_partials_needed": (c_int, [c_int, c_int]),
+    "rk_ce_train": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int64, c_float, c_float, c_void_p,
+                            c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_float, c_int, c_void_p]),
     "rk_optim_chunk": (c_int, []),
     "rk_gemm": (c_int, [c_void_p, c_int, c_int64, c_int, c_void_p, c_int, c_int64, c_int, c_void_p, c_int, c_int64,
                         c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int,
@@ -59,13 +61,13 @@ KERNEL_SIGS = {
     "rk_bn_apply": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
                             c_void_p]),
     "rk_bn_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int] + [c_void_p] * 11),
-    "rk_ln_fwd": (c_int, [c_int, c_int] + [c_void_p] * 6 + [c_int64, c_int, c_float, c_void_p]),
+    "rk_ln_fwd": (c_int, [c_int, c_int] + [c_void_p] * 8 + [c_int64, c_int, c_float, c_void_p]),
     "rk_ln_workspace": (c_int64, [c_int64, c_int]),
     "rk_gelu_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_gelu_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_softmax_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p]),
     "rk_softmax_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p]),
-    "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 8 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
+    "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 10 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
 }
 
 

@@ -67,3 +67,36 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int 
         return F.cross_entropy(logits.float(), target, ignore_index=ignore_index,
                                label_smoothing=label_smoothing, reduction=reduction)
     return _FusedCE.apply(logits, target, ignore_index, label_smoothing, reduction == "mean")
+
+
+def ce_train(logits: torch.Tensor, target: torch.Tensor, grad_scale: float, accum=None, ignore_index: int = -100,
+             label_smoothing: float = 0.0, reduction: str = "mean"):
+    """Loss AND d(logits) of a training step in one launch (see ``ce_train_kernel``).
+
+    ``grad_scale`` is the upstream gradient of the loss (e.g. 1/GA); ``accum`` optionally
+    ``(acc, ring, slot, acc_scale, sync)`` — the Loss capsule's device bookkeeping, updated by the
+    same launch.  Returns ``(loss[0-d], dlogits)`` or ``None`` when the case is not covered.
+    """
+    if (logits.device.type != "cuda" or logits.dim() != 2 or target.dim() != 1 or target.dtype.is_floating_point
+            or reduction not in ("mean", "sum") or logits.dtype not in (torch.float32, torch.bfloat16)
+            or logits.shape[0] > 65536):
+        return None
+    lib = _lib.kernels()
+    logits = logits.detach().contiguous()
+    target = target.contiguous().to(torch.int64)
+    N, C = logits.shape
+    dev = logits.device
+    stats = torch.empty(2, dtype=torch.float32, device=dev)
+    partials = torch.empty(lib.rk_ce_partials_needed(N, C), dtype=torch.float32, device=dev)
+    dlogits = torch.empty_like(logits)
+    counter = _lib.Workspace.get(dev).counter("ce_train")
+    acc = ring = slot = None
+    acc_scale, sync = 0.0, 0
+    if accum is not None:
+        acc, ring, slot, acc_scale, sync = accum
+    _lib.check(lib.rk_ce_train(logits.data_ptr(), _lib.dtype_code(logits), target.data_ptr(), dlogits.data_ptr(), N, C,
+                               int(ignore_index), float(label_smoothing), float(grad_scale), partials.data_ptr(),
+                               counter, stats.data_ptr(), int(reduction == "mean"), _lib.ptr(acc), _lib.ptr(ring),
+                               _lib.ptr(slot), ring.numel() if ring is not None else 0, float(acc_scale), int(sync),
+                               _lib.stream_ptr(dev)), "rk_ce_train")
+    return stats[0], dlogits

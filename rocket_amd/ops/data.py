@@ -38,6 +38,38 @@ def gather_rows(srcs: Sequence[torch.Tensor], idx: torch.Tensor, outs: Sequence[
                "rk_gather_rows")
 
 
+class RowGather:
+    """Pre-bound :func:`gather_rows` for fixed source/destination tensors (a loader ring slot):
+    the argument arrays are built once, each call is one native launch."""
+
+    def __init__(self, srcs: Sequence[torch.Tensor], outs: Sequence[torch.Tensor]):
+        self.srcs, self.outs = list(srcs), list(outs)
+        self.native = outs[0].device.type == "cuda" and len(srcs) <= _MAX_GATHER
+        if self.native:
+            for s, o in zip(srcs, outs):
+                if not (s.is_contiguous() and o.is_contiguous() and s.dtype == o.dtype and s.shape[1:] == o.shape[1:]
+                        and s.device == o.device):
+                    raise ValueError("RowGather: contiguous same-dtype tensors on one device expected")
+            k = len(srcs)
+            self._args = ((ctypes.c_void_p * k)(*[s.data_ptr() for s in srcs]),
+                          (ctypes.c_void_p * k)(*[o.data_ptr() for o in outs]),
+                          (ctypes.c_int64 * k)(*[s[0].numel() * s.element_size() if s.shape[0] else 0 for s in srcs]),
+                          (ctypes.c_int64 * k)(*[s.shape[0] for s in srcs]))
+            self._k = k
+            self._fn = _lib.kernels().rk_gather_rows
+            self._dev = outs[0].device
+
+    def __call__(self, idx: torch.Tensor):
+        if not self.native:
+            for s, o in zip(self.srcs, self.outs):
+                torch.index_select(s, 0, idx, out=o)
+            return self.outs
+        code = self._fn(self._k, *self._args, idx.data_ptr(), idx.numel(), _lib.stream_ptr(self._dev))
+        if code:
+            _lib.check(code, "rk_gather_rows")
+        return self.outs
+
+
 def loss_accum(loss: torch.Tensor, acc: torch.Tensor, ring: torch.Tensor, slot: torch.Tensor, scale: float,
                sync: bool) -> None:
     """``acc += loss*scale``; if ``sync``: ``ring[slot] = acc; slot = (slot+1) % len(ring); acc = 0``.

@@ -157,7 +157,7 @@ class _LN(torch.autograd.Function):
         rstd = torch.empty(rows, dtype=torch.float32, device=dev)
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
-        _lib.check(lib.rk_ln_fwd(_dt(x), _dt(y), x.data_ptr(), _lib.ptr(w), _lib.ptr(b), y.data_ptr(),
+        _lib.check(lib.rk_ln_fwd(_dt(x), _dt(y), x.data_ptr(), None, None, _lib.ptr(w), _lib.ptr(b), y.data_ptr(),
                                  mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps), _lib.stream_ptr(dev)),
                    "rk_ln_fwd")
         ctx.params = (weight, bias)
@@ -182,16 +182,94 @@ class _LN(torch.autograd.Function):
         counter = _lib.Workspace.get(dev).counter("ln_bwd")
         w = weight.detach() if weight is not None else None
         _lib.check(lib.rk_ln_bwd(_dt(x), _dt(dy), dy.data_ptr(), x.data_ptr(), _lib.ptr(w), mean.data_ptr(),
-                                 rstd.data_ptr(), dx.data_ptr(), _lib.ptr(dgamma), _lib.ptr(dbeta), rows, C,
-                                 ws.data_ptr(), counter, _lib.stream_ptr(dev)), "rk_ln_bwd")
+                                 rstd.data_ptr(), dx.data_ptr(), None, None, _lib.ptr(dgamma), _lib.ptr(dbeta), rows,
+                                 C, ws.data_ptr(), counter, _lib.stream_ptr(dev)), "rk_ln_bwd")
         g = _finish(params, bufs, direct) if params else []
         gw = g[0] if weight is not None else None
         gb = g[-1] if bias is not None else None
         return dx, gw, gb, None, None
 
 
+class _AddLN(torch.autograd.Function):
+    """(s, y) = (x + r, LayerNorm(x + r)): the pre-norm transformer's residual add fused into its LN.
+
+    Backward: dx = LN_bwd(dy) + ds (the residual stream's own gradient) and dr = dx, both written
+    by the same kernel — no separate add / cast / gradient-accumulation passes."""
+
+    @staticmethod
+    def forward(ctx, x, r, weight, bias, eps, out_dtype):
+        lib = _lib.kernels()
+        x = x.contiguous()
+        r = r.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dev = x.device
+        ssum = torch.empty_like(x)
+        y = torch.empty(x.shape, dtype=out_dtype, device=dev)
+        mean = torch.empty(rows, dtype=torch.float32, device=dev)
+        rstd = torch.empty(rows, dtype=torch.float32, device=dev)
+        w = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        _lib.check(lib.rk_ln_fwd(_dt(x), _dt(y), x.data_ptr(), r.data_ptr(), ssum.data_ptr(), _lib.ptr(w),
+                                 _lib.ptr(b), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, C, float(eps),
+                                 _lib.stream_ptr(dev)), "rk_ln_fwd(add)")
+        ctx.params = (weight, bias)
+        ctx.r_dtype = r.dtype
+        ctx.save_for_backward(ssum, mean, rstd)
+        return ssum, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        lib = _lib.kernels()
+        ssum, mean, rstd = ctx.saved_tensors
+        weight, bias = ctx.params
+        C = ssum.shape[-1]
+        rows = ssum.numel() // C
+        dev = ssum.device
+        if dy is None:
+            dy = torch.zeros(ssum.shape, dtype=ctx.r_dtype, device=dev)
+        dy = dy.contiguous()
+        if dy.dtype != ctx.r_dtype:
+            dy = dy.to(ctx.r_dtype)
+        ds = ds.contiguous() if ds is not None else None
+        params = [p for p in (weight, bias) if p is not None]
+        bufs, direct = _grad_targets(params, dev) if params else ([], False)
+        dgamma = bufs[0] if weight is not None else None
+        dbeta = bufs[-1] if bias is not None else None
+        dx = torch.empty_like(ssum)
+        dr = torch.empty(ssum.shape, dtype=ctx.r_dtype, device=dev)
+        ws = torch.empty(int(lib.rk_ln_workspace(rows, C)), dtype=torch.float32, device=dev)
+        counter = _lib.Workspace.get(dev).counter("ln_bwd")
+        w = weight.detach() if weight is not None else None
+        _lib.check(lib.rk_ln_bwd(_dt(ssum), _dt(dy), dy.data_ptr(), ssum.data_ptr(), _lib.ptr(w), mean.data_ptr(),
+                                 rstd.data_ptr(), dx.data_ptr(), _lib.ptr(ds), dr.data_ptr(), _lib.ptr(dgamma),
+                                 _lib.ptr(dbeta), rows, C, ws.data_ptr(), counter, _lib.stream_ptr(dev)),
+                   "rk_ln_bwd(add)")
+        g = _finish(params, bufs, direct) if params else []
+        gw = g[0] if weight is not None else None
+        gb = g[-1] if bias is not None else None
+        return dx, dr, gw, gb, None, None
+
+
 class FusedLayerNorm(nn.LayerNorm):
-    """``LayerNorm`` over the last dim; under autocast the output is bf16 (it feeds a GEMM)."""
+    """``LayerNorm`` over the last dim; under autocast the output is bf16 (it feeds a GEMM).
+
+    ``add_forward(x, r)`` returns ``(x + r, LN(x + r))`` with the residual add fused (pre-norm
+    transformer blocks); ``r=None`` is a plain LN that passes ``x`` through.
+    """
+
+    def add_forward(self, x, r=None):
+        if r is None:
+            return x, self(x)
+        C = x.shape[-1]
+        if (_ops.fused_enabled() and x.is_cuda and len(self.normalized_shape) == 1 and C % 4 == 0 and C <= 4096
+                and x.dtype in (torch.float32, torch.bfloat16) and r.shape == x.shape):
+            out_dtype = torch.bfloat16 if (torch.is_autocast_enabled("cuda") or x.dtype == torch.bfloat16) else x.dtype
+            if r.dtype != out_dtype:
+                r = r.to(out_dtype)
+            return _AddLN.apply(x, r, self.weight, self.bias, self.eps, out_dtype)
+        s = x + r
+        return s, self(s)
 
     def forward(self, x):
         C = x.shape[-1]

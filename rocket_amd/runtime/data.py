@@ -406,11 +406,13 @@ class DeviceLoader(_LoaderBase):
             flat = flat.pin_memory().to(self.device, non_blocking=True)
         return list(torch.split(flat, lens))
 
+    device_resident = True  # batches are produced on the dataset's device: no torch_move needed
+
     def _gather(self, idx: torch.Tensor):
         tensors = self.dataset.tensors
         if self.device.type != "cuda":
             return tuple(t.index_select(0, idx) for t in tensors)
-        from rocket_amd.ops.data import gather_rows
+        from rocket_amd.ops.data import RowGather
 
         n = idx.numel()
         ring = self._rings.get(n)
@@ -420,13 +422,13 @@ class DeviceLoader(_LoaderBase):
                 bufs = tuple(torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device) for t in tensors)
                 for b in bufs:
                     b._rocket_persistent = True
-                ring.append(bufs)
+                ring.append((bufs, RowGather([t.contiguous() for t in tensors], bufs)))
             self._rings[n] = ring
         k = self._ring_pos.get(n, 0)
         self._ring_pos[n] = (k + 1) % self.RING
-        out = ring[k]
-        gather_rows([t.contiguous() for t in tensors], idx, out)
-        return out
+        bufs, gather = ring[k]
+        gather(idx)
+        return bufs
 
     def _batches(self):
         for idx in self.index_table():

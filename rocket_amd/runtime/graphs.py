@@ -112,6 +112,10 @@ class StepGraphs:
         self.captures = 0
         self._token = None
         self._checked = False
+        self._rep = False  # resolved lazily (the module is wrapped during setup)
+        self._preps = None  # bound graph_prepare / graph_host / graph_token methods of the children
+        self._hosts = None
+        self._toks = None
 
     def release(self) -> None:
         self.variants.clear()
@@ -120,10 +124,12 @@ class StepGraphs:
 
     # ------------------------------------------------------------------ checks
     def _replica(self):
-        from rocket_amd.parallel.ddp import DataParallel
+        if self._rep is False:
+            from rocket_amd.parallel.ddp import DataParallel
 
-        rep = self.mod._module
-        return rep if isinstance(rep, DataParallel) else None
+            rep = self.mod._module
+            self._rep = rep if isinstance(rep, DataParallel) else None
+        return self._rep
 
     def _children_ok(self) -> bool:
         for c in self.mod._capsules:
@@ -155,7 +161,7 @@ class StepGraphs:
         return v
 
     def _tokens(self):
-        return tuple(c.graph_token() for c in self.mod._capsules if hasattr(c, "graph_token"))
+        return tuple(t() for t in self._toks)
 
     def _predict_sync(self) -> bool:
         engine = self.mod._accelerator
@@ -190,6 +196,10 @@ class StepGraphs:
                     bind = getattr(c, "graph_bind", None)
                     if bind is not None:
                         bind(self)
+                caps = self.mod._capsules
+                self._preps = [c.graph_prepare for c in caps if hasattr(c, "graph_prepare")]
+                self._hosts = [c.graph_host for c in caps]
+                self._toks = [c.graph_token for c in caps if hasattr(c, "graph_token")]
             if len(self.variants) >= MAX_VARIANTS:
                 return False
             self.mod._accelerator._do_sync()
@@ -206,10 +216,8 @@ class StepGraphs:
         return True
 
     def _prepare(self, attrs: Attributes) -> None:
-        for c in self.mod._capsules:
-            prep = getattr(c, "graph_prepare", None)
-            if prep is not None:
-                prep(attrs)
+        for prep in self._preps:
+            prep(attrs)
 
     def _check_tokens(self) -> bool:
         tok = self._tokens()
@@ -287,8 +295,8 @@ class StepGraphs:
         self.replays += 1
 
     def _host(self, attrs: Attributes) -> None:
-        for c in self.mod._capsules:
-            c.graph_host(attrs)
+        for host in self._hosts:
+            host(attrs)
 
     def _replay(self, v: _Captured, attrs: Attributes, tens: List[torch.Tensor]) -> None:
         for dst, src, keep in zip(v.static_in, tens, v.persistent):

@@ -94,6 +94,7 @@ class HostLoader(_LoaderBase):
                           rank=rank, even_batches=even_batches, seed=seed, gradient_state=gradient_state,
                           device=device, num_threads=num_threads)
         self.device = device if device is not None else torch.device("cpu")
+        self.device_resident = device is not None
         self._threads = num_threads or max(1, min(8, (os.cpu_count() or 2) // 2))
         self._gather = None
         self._staging: dict = {}

@@ -68,16 +68,25 @@ class StepTimer(Capsule):
         self._i = 0
         self._events: List = []
         self._host: List[float] = []
+        self._pool = None
         self.t_start: Optional[float] = None
         self.t_end: Optional[float] = None
 
     def _mark(self) -> None:
-        dev = self._accelerator.device
-        if dev.type == "cuda":
-            ev = torch.cuda.Event(enable_timing=True)
+        if self._pool is not None:
+            ev = self._pool[len(self._events)] if len(self._events) < len(self._pool) else torch.cuda.Event(
+                enable_timing=True)
             ev.record()
             self._events.append(ev)
         self._host.append(time.perf_counter())
+
+    def setup(self, attrs: Attributes | None = None) -> None:
+        Capsule.setup(self, attrs)
+        # timing events are created up front: constructing one costs more than recording it
+        self._pool = None
+        if self._accelerator.device.type == "cuda":
+            n = (self.steps + 1) if self.steps is not None else 1024
+            self._pool = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
 
     def set(self, attrs: Attributes | None = None) -> None:
         if self.warmup == 0 and self.t_start is None:
@@ -112,12 +121,18 @@ class StepTimer(Capsule):
             return [a.elapsed_time(b) for a, b in zip(self._events[:-1], self._events[1:])]
         return [(b - a) * 1e3 for a, b in zip(self._host[:-1], self._host[1:])]
 
+    def host_ms_p50(self) -> float:
+        """Median host-side time between consecutive step marks (how fast the host enqueues)."""
+        h = [(b - a) * 1e3 for a, b in zip(self._host[:-1], self._host[1:])]
+        return statistics.median(h) if h else 0.0
+
     def summary(self) -> dict:
         t = self.step_times_ms()
         if not t:
             return {}
         t_sorted = sorted(t)
         return {
+            "host_ms_p50": self.host_ms_p50(),
             "step_ms_p50": statistics.median(t),
             "step_ms_p90": t_sorted[min(len(t) - 1, int(0.9 * len(t)))],
             "step_ms_min": t_sorted[0],

@@ -92,3 +92,26 @@ def test_fused_optimizer_matches_torch(kind):
     if kind.startswith("adam"):
         assert float(sd["state"][0]["step"]) == 5.0
         assert torch.allclose(sd["state"][4]["exp_avg"], ob.state_dict()["state"][4]["exp_avg"], atol=1e-6)
+
+
+@pytest.mark.parametrize("C,dtype", [(10, torch.float32), (1000, torch.bfloat16)])
+def test_ce_train_one_launch(C, dtype):
+    """ce_train: loss, d(logits) (scaled) and the loss bookkeeping in one launch vs torch."""
+    from rocket_amd.ops.cross_entropy import ce_train
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    x = torch.randn(300, C, device=dev).to(dtype)
+    t = torch.randint(0, C, (300,), device=dev)
+    t[::7] = -100  # ignored rows
+    acc = torch.full((1,), 0.5, device=dev)
+    ring = torch.zeros(8, device=dev)
+    slot = torch.full((1,), 7, dtype=torch.int64, device=dev)
+    loss, dx = ce_train(x, t, 0.25, (acc, ring, slot, 2.0, True))
+    xr = x.detach().float().requires_grad_(True)
+    lr = torch.nn.functional.cross_entropy(xr, t)
+    (lr * 0.25).backward()
+    torch.testing.assert_close(loss, lr.detach(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dx.float(), xr.grad, rtol=2e-2 if dtype == torch.bfloat16 else 1e-4, atol=1e-5)
+    assert abs(float(ring[7]) - (0.5 + 2.0 * float(lr))) < 1e-3  # acc + scale*loss reported
+    assert int(slot) == 0 and float(acc) == 0.0  # ring cursor wrapped, window reset

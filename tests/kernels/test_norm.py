@@ -86,3 +86,33 @@ def test_layernorm(in_dtype, autocast, C):
     assert _rel(x.grad, xr.grad) < gtol
     assert _rel(ln.weight.grad, w.grad) < gtol
     assert _rel(ln.bias.grad, b.grad) < gtol
+
+
+def test_fused_add_layernorm():
+    """(s, y) = (x + r, LN(x + r)) with the residual add fused; gradients of x, r, gamma, beta."""
+    from rocket_amd.ops.norm import FusedLayerNorm
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    C = 768
+    ln = FusedLayerNorm(C).to(dev)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(2, 197, C, device=dev).requires_grad_(True)
+    r = torch.randn(2, 197, C, device=dev).to(torch.bfloat16).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        s, y = ln.add_forward(x, r)
+    assert s.dtype == torch.float32 and y.dtype == torch.bfloat16
+    gs, gy = torch.randn_like(s), torch.randn(y.shape, device=dev).to(torch.bfloat16)
+    torch.autograd.backward([s, y], [gs, gy])
+    xr = x.detach().clone().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True)
+    w = ln.weight.detach().clone().requires_grad_(True)
+    b = ln.bias.detach().clone().requires_grad_(True)
+    sr = xr + rr
+    yr = F.layer_norm(sr, (C,), w, b, 1e-5)
+    torch.autograd.backward([sr, yr], [gs, gy.float()])
+    assert _rel(s, sr) < 1e-6 and _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2 and _rel(r.grad, rr.grad) < 1e-2
+    assert _rel(ln.weight.grad, w.grad) < 3e-2 and _rel(ln.bias.grad, b.grad) < 3e-2
