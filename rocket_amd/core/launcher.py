@@ -71,6 +71,26 @@ def notebook_launch(fn: Callable, args=(), num_processes: int = 1) -> None:
                        start_method="spawn", join=True)
 
 
+def notebook(method: Callable) -> Callable:
+    """Decorator (reference ``Launcher.notebook``, ``launcher.py:202``): in a Jupyter kernel the
+    wrapped ``method(self, attrs)`` runs on ``attrs.launcher.num_procs`` spawned workers, otherwise
+    in-process.  ``Launcher.launch`` applies the same logic; this is for user launchers."""
+
+    def wrapper(self, attrs: Attributes | None = None) -> None:
+        attrs = attrs if attrs is not None else Attributes()
+        if attrs.launcher is None:
+            attrs.launcher = Attributes()
+        attrs.launcher.setdefault("num_procs", getattr(self, "_num_procs", 1))
+        attrs.launcher.setdefault("num_nodes", getattr(self, "_num_nodes", 1))
+        if in_notebook() and (attrs.launcher.num_procs or 1) > 1:
+            notebook_launch(method, args=(self, attrs), num_processes=attrs.launcher.num_procs)
+        else:
+            method(self, attrs)
+
+    wrapper.__wrapped__ = method
+    return wrapper
+
+
 def latest_checkpoint(root: str) -> str | None:
     """Newest directory under ``root`` holding a complete checkpoint (``random_states_0.pkl`` is
     written last by the checkpoint writer), or None."""
@@ -182,6 +202,8 @@ class Launcher(Dispatcher):
 
     def reset(self, attrs: Attributes | None = None) -> None:
         return None
+
+    notebook = staticmethod(notebook)
 
     def _notebook_entry(self, attrs: Attributes) -> None:
         self._run(attrs)
