@@ -149,6 +149,7 @@ __global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
   const int cc = c0 + ch;
   float t1 = 0.f, t2 = 0.f;
   if (cc < a.C) {
+#pragma unroll 8
     for (int b = sub; b < (int)gridDim.y; b += 4) {
       const float* p = a.part + (int64_t)b * 2 * a.C;
       t1 += __builtin_nontemporal_load(p + cc);
@@ -308,6 +309,7 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
   const int cc = c0 + ch;
   float t1 = 0.f, t2 = 0.f;
   if (cc < a.C) {
+#pragma unroll 8
     for (int b = sub; b < (int)gridDim.y; b += 4) {
       const float* p = a.part + (int64_t)b * 2 * a.C;
       t1 += __builtin_nontemporal_load(p + cc);
@@ -573,11 +575,15 @@ __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ 
   }
 }
 
-int bn_grid_rows(int64_t R, int* rpb) {
-  // at most ~256 row blocks per channel column, >= 32 rows each, multiple of BN_RG
-  int64_t per = (R + 255) / 256;
-  per = (per + BN_RG - 1) / BN_RG * BN_RG;
-  if (per < BN_RG) per = BN_RG;
+int bn_grid_rows(int64_t R, int C, int* rpb) {
+  // enough blocks for a bandwidth-bound pass (>= 4 per CU) while keeping the serial finalize
+  // short; at least one full unrolled pass (BN_U * BN_RG rows) per block
+  const int ncol = (C + BN_CT - 1) / BN_CT;
+  int64_t rb = 1024 / ncol;  // ~1024 blocks; the column's last block sums rb partials
+  if (rb < 128) rb = 128;
+  if (rb > 512) rb = 512;
+  int64_t per = (R + rb - 1) / rb;
+  per = (per + BN_U * BN_RG - 1) / (BN_U * BN_RG) * (BN_U * BN_RG);
   *rpb = (int)per;
   return (int)((R + per - 1) / per);
 }
@@ -587,7 +593,7 @@ int bn_grid_rows(int64_t R, int* rpb) {
 // workspace needed by the BN reductions (floats): 2*C*RB
 RK_API int64_t rk_bn_workspace(int64_t R, int C) {
   int rpb;
-  const int rb = bn_grid_rows(R, &rpb);
+  const int rb = bn_grid_rows(R, C, &rpb);
   return (int64_t)rb * 2 * C;
 }
 
@@ -597,7 +603,7 @@ RK_API int rk_bn_stats(int dt, const void* x, int64_t R, int C, const float* gam
                        float momentum, float eps, float* ws, unsigned* counters, hipStream_t s) {
   if (C % 8 || R <= 0) return (int)hipErrorInvalidValue;
   BnStatsArgs a{x, R, C, 0, ws, counters, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, nbt, momentum, eps};
-  const int rb = bn_grid_rows(R, &a.rpb);
+  const int rb = bn_grid_rows(R, C, &a.rpb);
   dim3 grid((C + BN_CT - 1) / BN_CT, rb);
   if (dt == BF16)
     bn_stats_kernel<uint16_t><<<grid, BN_T, 0, s>>>(a);
@@ -637,7 +643,7 @@ RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void*
                      void* dres, float* ws, float* coef /*[3C]*/, unsigned* counters, hipStream_t s) {
   if (C % 8 || C > 8 * BN_T || R <= 0) return (int)hipErrorInvalidValue;
   BnBwdArgs a{dy, x, y, R, C, 0, mean, invstd, ws, counters, dgamma, dbeta, scale, coef};
-  const int rb = bn_grid_rows(R, &a.rpb);
+  const int rb = bn_grid_rows(R, C, &a.rpb);
   dim3 grid((C + BN_CT - 1) / BN_CT, rb);
   int eg;
   const int erpb = bn_elem_rows(R, C, &eg);
