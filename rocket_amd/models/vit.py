@@ -5,9 +5,9 @@ patches + [CLS] = 197 tokens, width 768.
 
 MI355X path: LayerNorm is the one-wave-per-row HIP kernel emitting bf16 straight
 into the next GEMM (:class:`~rocket_amd.ops.norm.FusedLayerNorm`); the GEMMs run
-on the library path (hipBLASLt, bias fused into the epilogue via ``addmm``); GELU
-and the scaled attention softmax are HIP kernels (:mod:`rocket_amd.ops.activation`)
-whose backward recompute from saved inputs/outputs.  The residual stream stays
+on the library path (hipBLASLt, bias fused into the epilogue via ``addmm``); attention is
+one fused MFMA kernel reading the packed QKV projection (``native/kernels/attn.hip``), GELU
+a HIP kernel; residual adds are fused into the following LayerNorm.  The residual stream stays
 fp32 (standard AMP numerics); everything feeding a GEMM is bf16.
 
 Forward contract: ``(img, label) -> (img, label, logits)``.
@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from rocket_amd.ops.activation import attention, gelu
+from rocket_amd.ops.activation import attention_qkv, gelu
 from rocket_amd.ops.norm import FusedLayerNorm
 
 
@@ -31,10 +31,8 @@ class Attention(nn.Module):
         self.proj = nn.Linear(dim, dim)
 
     def forward(self, x):
-        B, L, D = x.shape
-        qkv = self.qkv(x).view(B, L, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
-        o = attention(qkv[0], qkv[1], qkv[2])
-        return self.proj(o.transpose(1, 2).reshape(B, L, D))
+        # fused MFMA attention straight from the packed projection (no head permutes)
+        return self.proj(attention_qkv(self.qkv(x), self.heads))
 
 
 class Mlp(nn.Module):

@@ -6,6 +6,9 @@
 * :func:`attention` — ``softmax(q k^T * scale) v`` for short sequences (ViT: 197 tokens):
   the two batched GEMMs run on the library (hipBLASLt) path, the scaled softmax on the
   kernel above, so the score matrix is read and written once per direction.
+* :func:`attention_qkv` — the fused MFMA attention of ``native/kernels/attn.hip`` working
+  directly on the QKV projection output (token-major, no head permutes, scores never leave
+  the CU): one launch forward, two backward, writing d(qkv) as one tensor.
 """
 
 from __future__ import annotations
@@ -83,3 +86,51 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     s = torch.matmul(q, k.transpose(-2, -1))
     p = softmax(s, scale)
     return torch.matmul(p, v)
+
+
+class _AttnQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, heads: int, scale: float):
+        lib = _lib.kernels()
+        qkv = qkv.contiguous()
+        B, L, C3 = qkv.shape
+        HD = C3 // 3
+        out = torch.empty(B, L, HD, dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty(B * heads, L, dtype=torch.float32, device=qkv.device)
+        base, es = qkv.data_ptr(), qkv.element_size()
+        _lib.check(lib.rk_attn_fwd(base, base + HD * es, base + 2 * HD * es, C3, out.data_ptr(), HD, lse.data_ptr(),
+                                   B, L, heads, float(scale), _lib.stream_ptr(qkv.device)), "rk_attn_fwd")
+        ctx.cfg = (heads, scale)
+        ctx.save_for_backward(qkv, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = _lib.kernels()
+        qkv, out, lse = ctx.saved_tensors
+        heads, scale = ctx.cfg
+        B, L, C3 = qkv.shape
+        HD = C3 // 3
+        dout = dout.contiguous()
+        if dout.dtype != qkv.dtype:
+            dout = dout.to(qkv.dtype)
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(B * heads, L, dtype=torch.float32, device=qkv.device)
+        base, gbase, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
+        _lib.check(lib.rk_attn_bwd(base, base + HD * es, base + 2 * HD * es, C3, out.data_ptr(), dout.data_ptr(), HD,
+                                   lse.data_ptr(), delta.data_ptr(), gbase, gbase + HD * es, gbase + 2 * HD * es, C3,
+                                   B, L, heads, float(scale), _lib.stream_ptr(qkv.device)), "rk_attn_bwd")
+        return dqkv, None, None
+
+
+def attention_qkv(qkv: torch.Tensor, heads: int, scale: float | None = None) -> torch.Tensor:
+    """Multi-head self-attention from the packed projection ``qkv`` [B, L, 3*H*D] -> [B, L, H*D]."""
+    B, L, C3 = qkv.shape
+    D = C3 // (3 * heads)
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if (_ops.fused_enabled() and qkv.is_cuda and qkv.dtype == torch.bfloat16 and D == 64
+            and L <= _lib.kernels().rk_attn_max_len()):
+        return _AttnQKV.apply(qkv, heads, scale)
+    t = qkv.view(B, L, 3, heads, D).permute(2, 0, 3, 1, 4)
+    o = attention(t[0], t[1], t[2], scale)
+    return o.transpose(1, 2).reshape(B, L, heads * D)

@@ -116,3 +116,27 @@ def test_fused_add_layernorm():
     assert _rel(s, sr) < 1e-6 and _rel(y, yr) < 1e-2
     assert _rel(x.grad, xr.grad) < 1e-2 and _rel(r.grad, rr.grad) < 1e-2
     assert _rel(ln.weight.grad, w.grad) < 3e-2 and _rel(ln.bias.grad, b.grad) < 3e-2
+
+
+@pytest.mark.parametrize("B,L,H", [(2, 197, 12), (3, 50, 4), (1, 224, 2), (2, 17, 3)])
+def test_fused_attention_qkv(B, L, H):
+    """Fused MFMA attention (fwd + dQ/dK/dV) vs fp32 softmax attention on the same bf16 inputs."""
+    from rocket_amd.ops.activation import attention_qkv
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    D = 64
+    qkv = (torch.randn(B, L, 3 * H * D, device=dev) * 1.5).to(torch.bfloat16).requires_grad_(True)
+    o = attention_qkv(qkv, H)
+    g = torch.randn_like(o)
+    o.backward(g)
+    ref_in = qkv.detach().float().requires_grad_(True)
+    t = ref_in.view(B, L, 3, H, D).permute(2, 0, 3, 1, 4)
+    p = torch.softmax(t[0] @ t[1].transpose(-2, -1) / D ** 0.5, dim=-1)
+    ref = (p @ t[2]).transpose(1, 2).reshape(B, L, H * D)
+    ref.backward(g.float())
+    assert o.shape == (B, L, H * D)
+    assert _rel(o, ref) < 1.5e-2, _rel(o, ref)
+    gq, gr = qkv.grad.view(B, L, 3, H * D), ref_in.grad.view(B, L, 3, H * D)
+    for i, name in enumerate("qkv"):
+        assert _rel(gq[:, :, i], gr[:, :, i]) < 3e-2, (name, _rel(gq[:, :, i], gr[:, :, i]))
