@@ -7,12 +7,12 @@
 //
 // Whole-row softmax: a key sequence of <= 224 tokens fits in one tile row, so every kernel keeps
 // all keys of a head in LDS and needs no online-softmax rescaling:
-//   attn_fwd   block = (64 queries, head, batch), 4 waves x 16 queries.  S = Q K^T (13 MFMA tiles
+//   attn_fwd   block = (head, batch): K/V staged once, the 4 waves loop over 16-query tiles.  S = Q K^T (13 MFMA tiles
 //              in registers), row max/sum by 16-lane shuffles, P (bf16) through a wave-private LDS
 //              tile into O = P V; writes O and the row log-sum-exp (log2 domain).
-//   attn_bwd_q same grid: recompute P from the saved LSE, dP = dO V^T, dS = P (dP - delta) * scale,
+//   attn_bwd_q same decomposition: recompute P from the saved LSE, dP = dO V^T, dS = P (dP - delta) * scale,
 //              dQ = dS K; also writes delta = rowsum(dO * O) for attn_bwd_kv.
-//   attn_bwd_kv block = (64 keys, head, batch): per 16-key wave, S^T = K Q^T and dP^T = V dO^T over
+//   attn_bwd_kv block = (head, batch), waves loop over 16-key tiles: S^T = K Q^T and dP^T = V dO^T over
 //              all queries, dV = P^T dO, then dK = dS^T Q (P^T / dS^T reuse one LDS tile).
 // All operand fragments are 16-byte LDS reads (row-major copies for "consecutive d" operands,
 // transposed copies for "consecutive token" operands; row strides 72 / 232 bf16 keep the 16 rows
@@ -113,11 +113,13 @@ __global__ void __launch_bounds__(NTH) attn_fwd_kernel(AttnArgs a) {
   for (int i = lane; i < 16 * TS; i += 64) Ps[w][i] = 0;  // zero pads (cols >= 16*ntile)
   __syncthreads();
 
-  const int q0 = blockIdx.x * 64 + 16 * w;
+  const float sl = a.scale * LOG2E;
+  // the block owns every query tile of its (batch, head): K/V are staged once per head
+  for (int qt = w; qt < ntile; qt += 4) {
+  const int q0 = 16 * qt;
   bf16x8 qa[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) qa[ks] = gload_row(a.q, a.ld, b, L, q0 + lo, h, 32 * ks + 8 * hi);
-  const float sl = a.scale * LOG2E;
   f32x4 s[NT];
   float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
@@ -177,6 +179,8 @@ __global__ void __launch_bounds__(NTH) attn_fwd_kernel(AttnArgs a) {
       if (lo == 0) a.lse[((int64_t)b * a.H + h) * L + r] = m[i] + log2f(sum[i]);
     }
   }
+  wave_lds_sync();  // P of this tile fully consumed before the next tile overwrites it
+  }
 }
 
 // ------------------------------------------------------------------------------- backward: dQ
@@ -195,7 +199,8 @@ __global__ void __launch_bounds__(NTH) attn_bwd_q_kernel(AttnArgs a) {
   for (int i = lane; i < 16 * TS; i += 64) Ss[w][i] = 0;
   __syncthreads();
 
-  const int q0 = blockIdx.x * 64 + 16 * w;
+  for (int qt = w; qt < ntile; qt += 4) {
+  const int q0 = 16 * qt;
   bf16x8 qa[2], ga[2];
   float dot = 0.f;  // partial rowsum(dO * O) of row q0 + lo over this lane's 16 d values
 #pragma unroll
@@ -258,6 +263,8 @@ __global__ void __launch_bounds__(NTH) attn_bwd_q_kernel(AttnArgs a) {
       for (int nt = 0; nt < 4; ++nt) row[16 * nt + lo] = f2bf(dq[nt][i]);
     }
   }
+  wave_lds_sync();
+  }
 }
 
 // --------------------------------------------------------------------------- backward: dK, dV
@@ -284,14 +291,15 @@ __global__ void __launch_bounds__(NTH) attn_bwd_kv_kernel(AttnArgs a) {
   for (int i = lane; i < 16 * TS; i += 64) Ts[w][i] = 0;
   __syncthreads();
 
-  const int k0 = blockIdx.x * 64 + 16 * w;
+  const float sl = a.scale * LOG2E;
+  for (int kt = w; kt < ntile; kt += 4) {
+  const int k0 = 16 * kt;
   bf16x8 ka[2], va[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     ka[ks] = gload_row(a.k, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
     va[ks] = gload_row(a.v, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
   }
-  const float sl = a.scale * LOG2E;
   const int kst = (16 * ntile + 31) / 32;
   // pass 1: P^T (rows = keys 4hi+i, cols = queries) -> dV = P^T dO
 #pragma unroll 2
@@ -360,6 +368,8 @@ __global__ void __launch_bounds__(NTH) attn_bwd_kv_kernel(AttnArgs a) {
       for (int nt = 0; nt < 4; ++nt) row[16 * nt + lo] = f2bf(acc[nt][i]);
     }
   }
+  wave_lds_sync();
+  }
 }
 
 }  // namespace
@@ -374,7 +384,7 @@ RK_API int rk_attn_fwd(const void* q, const void* k, const void* v, int ld, void
   AttnArgs a{};
   a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v;
   a.out = (uint16_t*)out; a.lse = lse; a.ld = ld; a.ldo = ldo; a.L = L; a.H = H; a.scale = scale;
-  dim3 grid((L + 63) / 64, H, B);
+  dim3 grid(1, H, B);  // one block per (batch, head)
   attn_fwd_kernel<<<grid, NTH, 0, s>>>(a);
   return (int)hipGetLastError();
 }
@@ -391,7 +401,7 @@ RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, cons
   a.dq = (uint16_t*)dq; a.dk = (uint16_t*)dk; a.dv = (uint16_t*)dv;
   a.lse = (float*)lse; a.delta = delta;
   a.ld = ld; a.ldo = ldo; a.ldg = ldg; a.L = L; a.H = H; a.scale = scale;
-  dim3 grid((L + 63) / 64, H, B);
+  dim3 grid(1, H, B);
   attn_bwd_q_kernel<<<grid, NTH, 0, s>>>(a);
   attn_bwd_kv_kernel<<<grid, NTH, 0, s>>>(a);
   return (int)hipGetLastError();
