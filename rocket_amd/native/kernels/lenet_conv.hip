@@ -400,6 +400,30 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
   for (int rd = 0; rd < rounds; ++rd) {
     const int nbase = (blockIdx.x * rounds + rd) * SPB;
     __syncthreads();
+    // ---- phase A: stage
+    for (int i = threadIdx.x; i < SPB * IMGN; i += NTHR) {
+      const int sl = i / IMGN, e = i % IMGN;
+      const int n = nbase + sl;
+      const int r = e / IMGS - 2, c = e % IMGS - 2;
+      const bool in = n < N && r >= 0 && r < IMG && c >= 0 && c < IMG;
+      const float v = x[(int64_t)(n < N ? n : 0) * IMG * IMG + (in ? r * IMG + c : 0)];
+      sm.img[sl][e] = in ? v : 0.f;
+    }
+    for (int i = threadIdx.x; i < SPB * (A1N / 8); i += NTHR) {
+      const int sl = i / (A1N / 8), e = (i % (A1N / 8)) * 8;
+      const int n = nbase + sl, nc = n < N ? n : 0;
+      *(uint4*)(sm.a1[sl] + e) = *(const uint4*)(a1g + (int64_t)nc * A1N + e);
+      *(uint2*)(sm.c1[sl] + e) = *(const uint2*)(code1g + (int64_t)nc * A1N + e);
+    }
+    for (int i = threadIdx.x; i < SPB * (DCN + 16) / 8; i += NTHR) {  // zero dc2 (16-byte stores)
+      const int sl = i / ((DCN + 16) / 8), e = (i % ((DCN + 16) / 8)) * 8;
+      *(uint4*)(sm.dc2[sl] + e) = make_uint4(0, 0, 0, 0);
+    }
+    for (int i = threadIdx.x; i < SPB * C2 * DTS / 8; i += NTHR) {
+      const int sl = i / (C2 * DTS / 8), e = (i % (C2 * DTS / 8)) * 8;
+      *(uint4*)(sm.dcT[sl] + e) = make_uint4(0, 0, 0, 0);
+    }
+    // the classifier chain runs while the conv operands above are still in flight
     if constexpr (MLP) {
       // ---- classifier input-gradient chain (host guarantees N % 8 == 0: 4 live samples)
       if (threadIdx.x < SPB * DYP) {
@@ -450,29 +474,6 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
           for (int i = 0; i < 4; ++i) sm.da2[i][16 * t + lo] = f2bf(acc[i]);
         }
       }
-    }
-    // ---- phase A: stage
-    for (int i = threadIdx.x; i < SPB * IMGN; i += NTHR) {
-      const int sl = i / IMGN, e = i % IMGN;
-      const int n = nbase + sl;
-      const int r = e / IMGS - 2, c = e % IMGS - 2;
-      const bool in = n < N && r >= 0 && r < IMG && c >= 0 && c < IMG;
-      const float v = x[(int64_t)(n < N ? n : 0) * IMG * IMG + (in ? r * IMG + c : 0)];
-      sm.img[sl][e] = in ? v : 0.f;
-    }
-    for (int i = threadIdx.x; i < SPB * (A1N / 8); i += NTHR) {
-      const int sl = i / (A1N / 8), e = (i % (A1N / 8)) * 8;
-      const int n = nbase + sl, nc = n < N ? n : 0;
-      *(uint4*)(sm.a1[sl] + e) = *(const uint4*)(a1g + (int64_t)nc * A1N + e);
-      *(uint2*)(sm.c1[sl] + e) = *(const uint2*)(code1g + (int64_t)nc * A1N + e);
-    }
-    for (int i = threadIdx.x; i < SPB * (DCN + 16) / 8; i += NTHR) {  // zero dc2 (16-byte stores)
-      const int sl = i / ((DCN + 16) / 8), e = (i % ((DCN + 16) / 8)) * 8;
-      *(uint4*)(sm.dc2[sl] + e) = make_uint4(0, 0, 0, 0);
-    }
-    for (int i = threadIdx.x; i < SPB * C2 * DTS / 8; i += NTHR) {
-      const int sl = i / (C2 * DTS / 8), e = (i % (C2 * DTS / 8)) * 8;
-      *(uint4*)(sm.dcT[sl] + e) = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < SPB * A2N; i += NTHR) {  // scatter the pooled gradients
