@@ -94,7 +94,11 @@ class CrossEntropy(nn.Module):
         if self._fused is False or logits.device.type != "cuda":
             return None
         from rocket_amd.ops.cross_entropy import ce_train
+        from rocket_amd.ops.lenet import fuse_cross_entropy
 
+        fused = fuse_cross_entropy(logits, target, grad_scale, accum)  # CE inside the LeNet backward launch
+        if fused is not None:
+            return fused[0], [logits], [fused[1]]
         res = ce_train(logits, target, grad_scale, accum)
         if res is None:
             return None

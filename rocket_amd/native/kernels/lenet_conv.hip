@@ -351,6 +351,11 @@ struct BwdSmem {
   uint16_t d1l[SPB][H1P];           // d(fc1 out) masked, pad 120..
   uint16_t da2[SPB][A2N];           // d(pooled conv2 output)
   uint16_t zrow[H1P];
+  float dyf[SPB][F3];               // fused CE: fp32 d(logits) of the block's samples
+  float red[NTHR / 64];
+  float lossp[SPB];
+  float cecnt[NTHR / 64];  // fused CE: valid-target count per wave (waves 1..15)
+  int flag;
 };
 
 struct ClsBwd {
@@ -358,6 +363,22 @@ struct ClsBwd {
   const float* dy;                  // dlogits [N][10] (already scaled by the upstream gradient)
   const uint16_t *h1T, *h2T;        // forward activations (ReLU masks)
   uint16_t *dyT, *d2T, *d1T;        // transposed gradients for the weight-gradient launch
+  // fused softmax cross-entropy (ce != 0): d(logits) is derived here from the saved logits and
+  // the targets instead of being read from `dy`; the mean loss is reduced across blocks
+  // (last-block ticket) and folded into the Loss capsule's device accumulator / report ring.
+  int ce;
+  const float* logits;
+  const int64_t* target;
+  int64_t ignore_index;
+  float grad_scale;
+  float* partials;                  // [gridDim.x]
+  unsigned* counter;
+  float* loss_out;                  // [2]: loss, nvalid
+  float *acc, *ring;
+  int64_t* slot;
+  int ring_size;
+  float acc_scale;
+  int sync;
 };
 
 template <bool MLP>
@@ -389,16 +410,28 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
     sm.wfr[i] = v;
   }
 
-  float accb2 = 0.f;                       // waves 0..9: db2 partial (lane lo = co)
-  f32x4 g2 = {0.f, 0.f, 0.f, 0.f};         // waves 0..9: dW2 tile u = wave
-  f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  float sb1 = 0.f;
 
   if (MLP)
     for (int i = threadIdx.x; i < H1P; i += NTHR) sm.zrow[i] = 0;
+  if (MLP && cb.ce && threadIdx.x == 0) sm.lossp[0] = 0.f;
 
-  for (int rd = 0; rd < rounds; ++rd) {
+  const int nrounds = MLP ? 1 : rounds;  // fused variant: one round (no loop-invariant state to keep live)
+  for (int rd = 0; rd < nrounds; ++rd) {
     const int nbase = (blockIdx.x * rounds + rd) * SPB;
+    // fused cross-entropy operands, issued ahead of the conv staging loads (in-order vmcnt):
+    // wave 0 holds one logit per lane (lane = 16 * sample + class); in round 0 waves 1..15 count
+    // the batch's valid targets (mean reduction; every block counts them itself)
+    int64_t ce_t = 0;
+    float ce_x = 0.f, ce_cnt = 0.f;
+    if (MLP && cb.ce) {
+      if (wave == 0) {
+        const int n = nbase + (lane >> 4), o = lane & 15;
+        ce_t = cb.target[n];
+        ce_x = cb.logits[(int64_t)n * F3 + (o < F3 ? o : 0)];
+      } else if (rd == 0) {
+        for (int i = threadIdx.x - 64; i < N; i += NTHR - 64) ce_cnt += cb.target[i] != cb.ignore_index ? 1.f : 0.f;
+      }
+    }
     __syncthreads();
     // ---- phase A: stage
     for (int i = threadIdx.x; i < SPB * IMGN; i += NTHR) {
@@ -426,15 +459,59 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
     // the classifier chain runs while the conv operands above are still in flight
     if constexpr (MLP) {
       // ---- classifier input-gradient chain (host guarantees N % 8 == 0: 4 live samples)
-      if (threadIdx.x < SPB * DYP) {
-        const int sl = threadIdx.x / DYP, o = threadIdx.x % DYP;
-        sm.dyl[sl][o] = f2bf(o < F3 ? cb.dy[(int64_t)(nbase + sl) * F3 + o] : 0.f);
-      } else if (threadIdx.x >= 256 && threadIdx.x < 256 + F3) {
-        const int o = threadIdx.x - 256;
-        const float* d = cb.dy + (int64_t)nbase * F3 + o;
-        *(uint2*)(cb.dyT + (int64_t)o * N + nbase) = pack4(d[0], d[F3], d[2 * F3], d[3 * F3]);
+      if (cb.ce) {
+        // softmax cross-entropy backward in-kernel; d(logits) kept unnormalised in LDS until the
+        // valid-target count (reduced by the other waves meanwhile) is known
+        if (wave == 0) {
+          const int sl = lane >> 4, o = lane & 15;
+          const bool valid = ce_t != cb.ignore_index, oc = o < F3;
+          float mx = oc ? ce_x : -INFINITY;
+#pragma unroll
+          for (int k = 1; k < 16; k <<= 1) mx = fmaxf(mx, __shfl_xor(mx, k, 64));
+          const float e = oc ? __expf(ce_x - mx) : 0.f;
+          float se = e, xt = (oc && (int64_t)o == ce_t) ? ce_x : 0.f;
+#pragma unroll
+          for (int k = 1; k < 16; k <<= 1) {
+            se += __shfl_xor(se, k, 64);
+            xt += __shfl_xor(xt, k, 64);
+          }
+          if (oc) sm.dyf[sl][o] = valid ? e / se - ((int64_t)o == ce_t ? 1.f : 0.f) : 0.f;
+          float li = (o == 0 && valid) ? mx + __logf(se) - xt : 0.f;  // lanes 0/16/32/48: a sample's loss
+          li += __shfl_xor(li, 16, 64);
+          li += __shfl_xor(li, 32, 64);
+          if (lane == 0) sm.lossp[0] += li;  // block running sum over rounds (LDS: no live register)
+        } else if (rd == 0) {
+#pragma unroll
+          for (int k = 32; k >= 1; k >>= 1) ce_cnt += __shfl_xor(ce_cnt, k, 64);
+          if (lane == 0) sm.cecnt[wave] = ce_cnt;
+        }
+        __syncthreads();
+        if (threadIdx.x < SPB * DYP || (threadIdx.x >= 256 && threadIdx.x < 256 + F3)) {
+          float nv = 0.f;
+#pragma unroll
+          for (int w = 1; w < NTHR / 64; ++w) nv += sm.cecnt[w];
+          const float sc = nv > 0.f ? cb.grad_scale / nv : 0.f;
+          if (threadIdx.x < SPB * DYP) {
+            const int sl = threadIdx.x / DYP, o = threadIdx.x % DYP;
+            sm.dyl[sl][o] = f2bf(o < F3 ? sc * sm.dyf[sl][o] : 0.f);
+          } else {
+            const int o = threadIdx.x - 256;
+            *(uint2*)(cb.dyT + (int64_t)o * N + nbase) =
+                pack4(sc * sm.dyf[0][o], sc * sm.dyf[1][o], sc * sm.dyf[2][o], sc * sm.dyf[3][o]);
+          }
+        }
+        __syncthreads();
+      } else {
+        if (threadIdx.x < SPB * DYP) {
+          const int sl = threadIdx.x / DYP, o = threadIdx.x % DYP;
+          sm.dyl[sl][o] = f2bf(o < F3 ? cb.dy[(int64_t)(nbase + sl) * F3 + o] : 0.f);
+        } else if (threadIdx.x >= 256 && threadIdx.x < 256 + F3) {
+          const int o = threadIdx.x - 256;
+          const float* d = cb.dy + (int64_t)nbase * F3 + o;
+          *(uint2*)(cb.dyT + (int64_t)o * N + nbase) = pack4(d[0], d[F3], d[2 * F3], d[3 * F3]);
+        }
+        __syncthreads();
       }
-      __syncthreads();
       if (wave < 6) {  // fc3 dgrad: d2 = (dy W3) * [h2 > 0]
         const f32x4 acc = cls_tile<1>(&sm.dyl[0][0], DYP, sm.zrow, cb.frag, OFF_B3 + wave, lane);
         if (hi == 0) {
@@ -523,7 +600,12 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
     }
     __syncthreads();
 
-    // ---- phase C
+    // ---- phase C (accumulators live only from here to the per-round flush: nothing is held in
+    // registers across the classifier chain)
+    float accb2 = 0.f;                       // waves 0..9: db2 partial (lane lo = co)
+    f32x4 g2 = {0.f, 0.f, 0.f, 0.f};         // waves 0..9: dW2 tile u = wave
+    f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    float sb1 = 0.f;
     if (wave < 10) {
       // dW2 tile u = wave: rows co (16), cols r = 16u + lo; K = positions of 4 samples (4 x 4 k-steps)
       const int u = wave;
@@ -584,44 +666,72 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
         }
       }
     }
-  }
 
-  // ---- phase D: block totals -> global atomics
-  if (wave < 10) {
-    const int u = wave, col = 16 * u + lo;
+    // ---- phase D: block totals -> global atomics
+    if (wave < 10) {
+      const int u = wave, col = 16 * u + lo;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (col < R2) atomicAdd(dw2 + (4 * hi + i) * R2 + col, g2[i]);
-    if (u == 0) {  // db2[co]: lanes lo, lo+16, lo+32, lo+48 hold parts of channel lo
-      accb2 += __shfl_xor(accb2, 16, 64);
-      accb2 += __shfl_xor(accb2, 32, 64);
-      if (hi == 0 && db2) atomicAdd(db2 + lo, accb2);
+      for (int i = 0; i < 4; ++i)
+        if (col < R2) atomicAdd(dw2 + (4 * hi + i) * R2 + col, g2[i]);
+      if (u == 0) {  // db2[co]: lanes lo, lo+16, lo+32, lo+48 hold parts of channel lo
+        accb2 += __shfl_xor(accb2, 16, 64);
+        accb2 += __shfl_xor(accb2, 32, 64);
+        if (hi == 0 && db2) atomicAdd(db2 + lo, accb2);
+      }
+    } else {
+      const int wi = wave - 10;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sm.red1[wi][u][(4 * hi + i) * 16 + lo] = g1[u][i];
+      sb1 += __shfl_xor(sb1, 16, 64);
+      sb1 += __shfl_xor(sb1, 32, 64);
+      if (hi == 0) sm.rb1[wi][lo] = sb1;
     }
-  } else {
-    const int wi = wave - 10;
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * 256; e += NTHR) {
+      const int u = e >> 8, row = (e & 255) >> 4, col = 16 * u + (e & 15);
+      if (row < C1 && col < R1) {
+        float v = 0.f;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sm.red1[wi][u][(4 * hi + i) * 16 + lo] = g1[u][i];
-    sb1 += __shfl_xor(sb1, 16, 64);
-    sb1 += __shfl_xor(sb1, 32, 64);
-    if (hi == 0) sm.rb1[wi][lo] = sb1;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < 2 * 256; e += NTHR) {
-    const int u = e >> 8, row = (e & 255) >> 4, col = 16 * u + (e & 15);
-    if (row < C1 && col < R1) {
+        for (int w = 0; w < 6; ++w) v += sm.red1[w][u][e & 255];
+        atomicAdd(dw1 + row * R1 + col, v);
+      }
+    }
+    if (threadIdx.x < C1 && db1) {
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < 6; ++w) v += sm.red1[w][u][e & 255];
-      atomicAdd(dw1 + row * R1 + col, v);
+      for (int w = 0; w < 6; ++w) v += sm.rb1[w][threadIdx.x];
+      atomicAdd(db1 + threadIdx.x, v);
     }
   }
-  if (threadIdx.x < C1 && db1) {
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < 6; ++w) v += sm.rb1[w][threadIdx.x];
-    atomicAdd(db1 + threadIdx.x, v);
+  if constexpr (MLP) {
+    if (cb.ce) {  // batch loss: block partials -> last block -> loss + Loss-capsule bookkeeping
+      if (threadIdx.x == 0) cb.partials[blockIdx.x] = sm.lossp[0];
+      if (last_block_arrived(cb.counter, &sm.flag)) {
+        float t = 0.f;
+        for (int i = threadIdx.x; i < (int)gridDim.x; i += NTHR) t += cb.partials[i];
+        t = block_sum(t, sm.red);
+        if (threadIdx.x == 0) {
+          float nv = 0.f;
+          for (int w = 1; w < NTHR / 64; ++w) nv += sm.cecnt[w];
+          const float l = nv > 0.f ? t / nv : NAN;
+          cb.loss_out[0] = l;
+          cb.loss_out[1] = nv;
+          if (cb.acc) {
+            float v = cb.acc[0] + l * cb.acc_scale;
+            if (cb.sync) {
+              const int64_t k = cb.slot[0];
+              cb.ring[k] = v;
+              cb.slot[0] = (k + 1) % cb.ring_size;
+              v = 0.f;
+            }
+            cb.acc[0] = v;
+          }
+        }
+        reset_counter(cb.counter);
+      }
+    }
   }
 }
 
@@ -669,16 +779,54 @@ RK_API int rk_lenet_conv_bwd(const float* x, const void* a1, const void* code1, 
   return (int)hipGetLastError();
 }
 
-// Fused backward for N % 8 == 0 and N % (4*rounds) == 0: classifier input-gradient chain from
+// Fused backward for N % 8 == 0 (one block per 4 samples): classifier input-gradient chain from
 // dlogits, then the conv stack; writes dy^T, d2^T, d1^T for rk_mlp3_wgrad and ACCUMULATES the
 // conv weight/bias gradients.
+struct LenetCE {  // host-side description of the fused cross-entropy (see ClsBwd)
+  const float* logits;
+  const int64_t* target;
+  int64_t ignore_index;
+  float grad_scale;
+  float* partials;
+  unsigned* counter;
+  float* loss_out;
+  float *acc, *ring;
+  int64_t* slot;
+  int ring_size;
+  float acc_scale;
+  int sync;
+};
+
 RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const void* code2, const float* w2,
                         const void* frag, const float* dy, const void* h1T, const void* h2T, void* dyT, void* d2T,
-                        void* d1T, float* dw1, float* db1, float* dw2, float* db2, int N, int rounds, hipStream_t s) {
-  if (rounds < 1) rounds = 1;
-  if (N % 8 || N % (SPB * rounds)) return (int)hipErrorInvalidValue;
-  ClsBwd cb{(const bf16x8*)frag, dy, (const uint16_t*)h1T, (const uint16_t*)h2T, (uint16_t*)dyT, (uint16_t*)d2T,
-            (uint16_t*)d1T};
+                        void* d1T, float* dw1, float* db1, float* dw2, float* db2, int N, int rounds,
+                        const LenetCE* ce, hipStream_t s) {
+  rounds = 1;  // the fused kernel handles one group of SPB samples per block (argument kept for ABI)
+  if (N % 8 || N > 65536) return (int)hipErrorInvalidValue;
+  ClsBwd cb{};
+  cb.frag = (const bf16x8*)frag;
+  cb.dy = dy;
+  cb.h1T = (const uint16_t*)h1T;
+  cb.h2T = (const uint16_t*)h2T;
+  cb.dyT = (uint16_t*)dyT;
+  cb.d2T = (uint16_t*)d2T;
+  cb.d1T = (uint16_t*)d1T;
+  if (ce) {
+    cb.ce = 1;
+    cb.logits = ce->logits;
+    cb.target = ce->target;
+    cb.ignore_index = ce->ignore_index;
+    cb.grad_scale = ce->grad_scale;
+    cb.partials = ce->partials;
+    cb.counter = ce->counter;
+    cb.loss_out = ce->loss_out;
+    cb.acc = ce->acc;
+    cb.ring = ce->ring;
+    cb.slot = ce->slot;
+    cb.ring_size = ce->ring_size;
+    cb.acc_scale = ce->acc_scale;
+    cb.sync = ce->sync;
+  }
   lenet_conv_bwd<true><<<N / (SPB * rounds), NTHR, 0, s>>>(x, (const uint16_t*)a1, (const uint8_t*)code1, nullptr,
                                                            (const uint8_t*)code2, w2, dw1, db1, dw2, db2, N, rounds, cb);
   return (int)hipGetLastError();

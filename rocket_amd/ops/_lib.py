@@ -45,7 +45,7 @@ KERNEL_SIGS = {
     "rk_lenet_prep": (c_int, [c_void_p] * 5),
     "rk_lenet_frag_bytes": (c_int, []),
     "rk_lenet_fwd": (c_int, [c_void_p] * 16 + [c_int, c_void_p]),
-    "rk_lenet_bwd": (c_int, [c_void_p] * 16 + [c_int, c_int, c_void_p]),
+    "rk_lenet_bwd": (c_int, [c_void_p] * 16 + [c_int, c_int, c_void_p, c_void_p]),
     "rk_mlp3_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                             c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "rk_mlp3_dgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,

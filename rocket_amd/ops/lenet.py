@@ -145,10 +145,24 @@ class _MLPHead(torch.autograd.Function):
         return (dx, *_finish(params, bufs, direct))
 
 
+class _LenetCE(ctypes.Structure):
+    """Mirror of ``struct LenetCE`` (lenet_conv.hip): softmax cross-entropy fused into the backward."""
+
+    _fields_ = [("logits", ctypes.c_void_p), ("target", ctypes.c_void_p), ("ignore_index", ctypes.c_int64),
+                ("grad_scale", ctypes.c_float), ("partials", ctypes.c_void_p), ("counter", ctypes.c_void_p),
+                ("loss_out", ctypes.c_void_p), ("acc", ctypes.c_void_p), ("ring", ctypes.c_void_p),
+                ("slot", ctypes.c_void_p), ("ring_size", ctypes.c_int), ("acc_scale", ctypes.c_float),
+                ("sync", ctypes.c_int)]
+
+
 class _LeNetFused(torch.autograd.Function):
     """The whole LeNet: conv stack + classifier forward in ONE launch (after a tiny weight-fragment
     prep launch), classifier input-gradient chain + conv backward in ONE launch, the three
-    classifier weight gradients in one grouped launch.  Needs N % 8 == 0."""
+    classifier weight gradients in one grouped launch.  Needs N % 8 == 0.
+
+    Training fast path: :func:`fuse_cross_entropy` attaches a mean softmax-cross-entropy to the
+    logits' backward node; the backward launch then computes loss and d(logits) itself (the
+    incoming gradient is ignored) — forward, loss and backward are 3 launches + the wgrad."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, f1w, f1b, f2w, f2b, f3w, f3b):
@@ -175,28 +189,47 @@ class _LeNetFused(torch.autograd.Function):
                                     cw[9].data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(), a2T.data_ptr(),
                                     h1T.data_ptr(), h2T.data_ptr(), logits.data_ptr(), N, stream), "rk_lenet_fwd")
         ctx.params = (w1, b1, w2, b2, f1w, f1b, f2w, f2b, f3w, f3b)
-        ctx.save_for_backward(x, a1, c1, c2, a2T, h1T, h2T, frag, cw[2])
+        ctx.save_for_backward(x, a1, c1, c2, a2T, h1T, h2T, frag, cw[2], logits)
+        ctx.ce_spec = None
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         lib = _lib.kernels()
-        x, a1, c1, c2, a2T, h1T, h2T, frag, w2c = ctx.saved_tensors
+        x, a1, c1, c2, a2T, h1T, h2T, frag, w2c, logits = ctx.saved_tensors
         N = x.shape[0]
         dev = x.device
         stream = _lib.stream_ptr(dev)
-        dy = dlogits.contiguous().float()
+        rounds = 1  # one block per 4 samples (the kernel keeps no state across sample groups)
+        ce, keep = None, None
+        if ctx.ce_spec is not None:
+            target, grad_scale, accum, loss_out = ctx.ce_spec
+            ctx.ce_spec = None
+            acc = ring = slot = None
+            acc_scale, sync = 0.0, 0
+            if accum is not None:
+                acc, ring, slot, acc_scale, sync = accum
+            partials = torch.empty(N // 4, dtype=torch.float32, device=dev)
+            keep = (partials, target)
+            ce = _LenetCE(logits.data_ptr(), target.data_ptr(), -100, float(grad_scale), partials.data_ptr(),
+                          _lib.Workspace.get(dev).counter("lenet_ce"), loss_out.data_ptr(), _lib.ptr(acc),
+                          _lib.ptr(ring), _lib.ptr(slot), ring.numel() if ring is not None else 0, float(acc_scale),
+                          int(sync))
+            dy = logits  # unread
+        else:
+            dy = dlogits.contiguous().float()
         bf = dict(dtype=torch.bfloat16, device=dev)
         dyT = torch.empty(10, N, **bf)
         d2T = torch.empty(84, N, **bf)
         d1T = torch.empty(120, N, **bf)
         params = ctx.params
         bufs, direct = _grad_targets(params, dev)
-        rounds = 2 if N % 16 == 0 and N >= 4096 else 1
         _lib.check(lib.rk_lenet_bwd(x.data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(), w2c.data_ptr(),
                                     frag.data_ptr(), dy.data_ptr(), h1T.data_ptr(), h2T.data_ptr(), dyT.data_ptr(),
                                     d2T.data_ptr(), d1T.data_ptr(), bufs[0].data_ptr(), bufs[1].data_ptr(),
-                                    bufs[2].data_ptr(), bufs[3].data_ptr(), N, rounds, stream), "rk_lenet_bwd")
+                                    bufs[2].data_ptr(), bufs[3].data_ptr(), N, rounds,
+                                    ctypes.byref(ce) if ce is not None else None, stream), "rk_lenet_bwd")
+        del keep
         probs = ((dyT, h2T, bufs[8], bufs[9], 10, 84), (d2T, h1T, bufs[6], bufs[7], 84, 120),
                  (d1T, a2T, bufs[4], bufs[5], 120, 400))
         P = ctypes.c_void_p * 3
@@ -212,6 +245,21 @@ def lenet_forward(x, conv1, conv2, fc1, fc2, fc3):
     """Fused LeNet logits (N % 8 == 0)."""
     return _LeNetFused.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, fc1.weight, fc1.bias,
                              fc2.weight, fc2.bias, fc3.weight, fc3.bias)
+
+
+def fuse_cross_entropy(logits, target, grad_scale: float, accum=None):
+    """Attach a mean cross-entropy (ignore_index -100) to fused-LeNet ``logits`` so the backward
+    launch computes loss and d(logits) in-kernel.  Returns ``(loss[0-d], dummy_grad)`` to pass to
+    ``torch.autograd.backward([logits], [dummy_grad])``, or None if ``logits`` is not a fused-LeNet
+    output (or ``N > 65536``).  ``accum`` as in :func:`rocket_amd.ops.cross_entropy.ce_train`."""
+    fn = logits.grad_fn
+    if (fn is None or type(fn).__name__ != "_LeNetFusedBackward" or logits.dim() != 2 or logits.shape[0] > 65536
+            or target.dim() != 1 or target.dtype.is_floating_point):
+        return None
+    loss_out = torch.empty(2, dtype=torch.float32, device=logits.device)
+    fn.ce_spec = (target.contiguous().to(torch.int64), float(grad_scale), accum, loss_out)
+    # the incoming gradient is never read (the kernel derives d(logits) itself): no fill launch
+    return loss_out[0], torch.empty((), dtype=logits.dtype, device=logits.device).expand_as(logits)
 
 
 def mlp_head(x, layers: List[torch.nn.Linear]):

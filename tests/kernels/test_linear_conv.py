@@ -145,3 +145,43 @@ def test_lenet_whole_fused(N):
     yr.backward(g)
     for (name, p), pr in zip(net.named_parameters(), ref.parameters()):
         assert _rel(p.grad, pr.grad) < 3e-2, (name, _rel(p.grad, pr.grad))
+
+
+@pytest.mark.parametrize("N", [1024, 4096])
+def test_lenet_fused_cross_entropy(N):
+    """Cross-entropy computed inside the LeNet backward launch vs the two-launch path (ce_train's
+    d(logits) fed to the same backward): same bf16 contract, so gradients agree tightly; the loss
+    and the Loss-capsule bookkeeping (acc/ring/slot) are checked against F.cross_entropy."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.cross_entropy import ce_train
+    from rocket_amd.ops.lenet import fuse_cross_entropy, lenet_forward
+
+    torch.manual_seed(3)
+    net = LeNet(fused=False).cuda()
+    ref = LeNet(fused=False).cuda()
+    ref.load_state_dict(net.state_dict())
+    x = torch.rand(N, 1, 28, 28, device="cuda")
+    t = torch.randint(0, 10, (N,), device="cuda")
+    t[::7] = -100  # ignored rows
+    y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
+    acc = torch.full((1,), 0.5, device="cuda")
+    ring = torch.zeros(8, device="cuda")
+    slot = torch.full((1,), 3, dtype=torch.int64, device="cuda")
+    loss, dummy = fuse_cross_entropy(y, t, 0.5, (acc, ring, slot, 2.0, 1))
+    torch.autograd.backward([y], [dummy])
+    yr = lenet_forward(x, ref.conv1, ref.conv2, ref.fc1, ref.fc2, ref.fc3)
+    lr, dl = ce_train(yr, t, 0.5)
+    yr.backward(dl)
+    _, y32 = _ref_lenet(x, ref.conv1.weight, ref.conv1.bias, ref.conv2.weight, ref.conv2.bias, ref.fc1, ref.fc2,
+                        ref.fc3)
+    l32 = F.cross_entropy(y32, t)
+    torch.cuda.synchronize()
+    assert abs(float(loss) - float(lr)) < 1e-4 * abs(float(lr)), (float(loss), float(lr))
+    assert abs(float(loss) - float(l32)) < 1e-2 * abs(float(l32)), (float(loss), float(l32))
+    for (name, p), pr in zip(net.named_parameters(), ref.parameters()):
+        assert _rel(p.grad, pr.grad) < 1e-2, (name, _rel(p.grad, pr.grad))
+    assert int(slot) == 4 and float(acc) == 0.0
+    assert abs(float(ring[3]) - (0.5 + 2.0 * float(loss))) < 1e-5
+    # a second backward without the CE spec consumes dlogits again (spec is one-shot)
+    y2 = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
+    y2.backward(torch.zeros_like(y2))
