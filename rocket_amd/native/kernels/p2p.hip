@@ -1,0 +1,278 @@
+// One-shot peer-to-peer all-reduce over xGMI for small gradient buckets (SURVEY §5
+// "MI355X-native communication design": LeNet's 247 KB of fp32 gradients are latency-bound; RCCL's
+// small-message path costs tens of µs plus a host hop between two HIP graphs).
+//
+// Every rank owns, in its own HBM, a double-buffered STAGE area (2 x cap floats) and a FLAGS area
+// ([kMaxBlocks][8] u32, uncached).  Both are exported once with hipIpcGetMemHandle and mapped by
+// every peer, so a kernel can read a peer's stage and write a peer's flags directly over xGMI.
+//
+// rk_p2p_allreduce(data, n): block b owns the fixed stage region [b*kChunk, (b+1)*kChunk):
+//   1. copy data[region] into stage[parity][region]                         (local HBM)
+//   2. release (L2 write-back, system scope), then store this block's epoch into
+//      flags_peer[b][rank] of every peer; poll flags_self[b][peer] >= epoch for every peer
+//   3. acquire (system scope), read region from all W stages (W loads in flight per vector),
+//      sum in rank order 0..W-1 (bit-identical result on every rank), scale, write data[region].
+// The epoch counter of block b lives in device memory (graph-capturable: no host-side step value)
+// and selects the stage parity.  Double buffering makes a closing barrier unnecessary: a rank can
+// only overwrite stage[p] two launches later, after every peer has signalled the launch in
+// between, i.e. after every peer finished reading stage[p].  The block -> region map never
+// changes, so the argument holds per block even when n differs between launches (all ranks issue
+// the same sequence of launches).
+//
+// A poll that exceeds ~30 s records an error in host-mapped memory and gives up instead of hanging
+// the GPU (the Python side checks it); the kernel never waits on anything but peer flags.
+#include "rk_common.h"
+
+#include <cstring>
+#include <new>
+
+namespace {
+using rk::f32x4;
+
+constexpr int kMaxPeers = 8;
+constexpr int kThreads = 256;
+constexpr int kVec = 4;                              // floats per 16-byte vector
+constexpr int kUnroll = 2;                           // vectors per thread
+constexpr int kChunk = kThreads * kVec * kUnroll;    // 2048 floats per block (8 KB)
+constexpr uint64_t kTimeoutTicks = 30ull * 100000000ull;  // s_memrealtime runs at 100 MHz
+
+struct P2PArgs {
+  float* stage[kMaxPeers];      // every rank's stage base (self included), 2 * cap floats each
+  unsigned* flags[kMaxPeers];   // every rank's flags base, [kMaxBlocks][kMaxPeers]
+  unsigned* epoch;              // local, [kMaxBlocks]
+  unsigned* err;                // host-mapped error word
+  float* data;
+  int64_t n, cap;
+  float scale;
+  int rank, world;
+};
+
+__device__ __forceinline__ unsigned load_flag(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int W>
+__global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a) {
+  __shared__ unsigned s_ep;
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (t == 0) s_ep = a.epoch[b] + 1;
+  __syncthreads();
+  const unsigned ep = s_ep;
+  const int64_t par = (int64_t)(ep & 1) * a.cap;
+  const int64_t base = (int64_t)b * kChunk;
+
+  // 1. local contribution -> own stage
+  float* mine = a.stage[a.rank] + par;
+  const bool full = base + kChunk <= a.n;  // block-uniform: no per-vector bounds branches
+  if (full) {
+    f32x4 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) v[u] = *(const f32x4*)(a.data + base + (int64_t)(u * kThreads + t) * kVec);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) *(f32x4*)(mine + base + (int64_t)(u * kThreads + t) * kVec) = v[u];
+  } else {
+    for (int64_t j = base + t; j < a.n && j < base + kChunk; j += kThreads) mine[j] = a.data[j];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+
+  // 2. signal every peer, then wait for every peer's signal (wave 0, lane p <-> peer p)
+  if (t < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back this XCD's L2
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t < a.world) {
+      __hip_atomic_store(a.flags[t] + b * kMaxPeers + a.rank, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const unsigned* f = a.flags[a.rank] + b * kMaxPeers + t;
+      if ((int)(load_flag(f) - ep) < 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while ((int)(load_flag(f) - ep) < 0) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
+            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (t >= 64) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // this wave's view of the peers' stages
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+
+  // 3. reduce: all W contributions of each vector in flight, summed in rank order
+  if (full) {
+    f32x4 v[kUnroll][W];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+      for (int r = 0; r < W; ++r)
+        v[u][r] = __builtin_nontemporal_load((const f32x4*)(a.stage[r] + par + base + (int64_t)(u * kThreads + t) * kVec));
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      f32x4 s = v[u][0];
+#pragma unroll
+      for (int r = 1; r < W; ++r) s += v[u][r];
+      *(f32x4*)(a.data + base + (int64_t)(u * kThreads + t) * kVec) = s * a.scale;
+    }
+  } else {
+    for (int64_t j = base + t; j < a.n && j < base + kChunk; j += kThreads) {
+      float v[W];
+#pragma unroll
+      for (int r = 0; r < W; ++r) v[r] = __builtin_nontemporal_load(a.stage[r] + par + j);
+      float s = v[0];
+#pragma unroll
+      for (int r = 1; r < W; ++r) s += v[r];
+      a.data[j] = s * a.scale;
+    }
+  }
+  if (t == 0) a.epoch[b] = ep;
+}
+
+struct P2PCtx {
+  int rank = 0, world = 0, device = 0;
+  int64_t cap = 0;
+  int max_blocks = 0;
+  float* stage = nullptr;
+  unsigned* flags = nullptr;
+  unsigned* epoch = nullptr;
+  unsigned* err_h = nullptr;
+  unsigned* err_d = nullptr;
+  float* peer_stage[kMaxPeers] = {};
+  unsigned* peer_flags[kMaxPeers] = {};
+  bool mapped[kMaxPeers] = {};
+};
+
+constexpr int kHandleBytes = (int)sizeof(hipIpcMemHandle_t);
+
+void release(P2PCtx* c) {
+  for (int r = 0; r < kMaxPeers; ++r) {
+    if (!c->mapped[r]) continue;
+    (void)hipIpcCloseMemHandle(c->peer_stage[r]);
+    (void)hipIpcCloseMemHandle(c->peer_flags[r]);
+  }
+  if (c->stage) (void)hipFree(c->stage);
+  if (c->flags) (void)hipFree(c->flags);
+  if (c->epoch) (void)hipFree(c->epoch);
+  if (c->err_h) (void)hipHostFree(c->err_h);
+  delete c;
+}
+
+}  // namespace
+
+// bytes of one exported handle set (stage + flags)
+RK_API int rk_p2p_handle_bytes() { return 2 * kHandleBytes; }
+RK_API int rk_p2p_chunk() { return kChunk; }
+
+// Allocate this rank's stage/flags, export their IPC handles into `handles` (rk_p2p_handle_bytes()).
+RK_API int rk_p2p_create(int rank, int world, int64_t cap, void** out, void* handles) {
+  if (world < 1 || world > kMaxPeers || rank < 0 || rank >= world || cap <= 0) return (int)hipErrorInvalidValue;
+  auto* c = new (std::nothrow) P2PCtx();
+  if (!c) return (int)hipErrorOutOfMemory;
+  c->rank = rank;
+  c->world = world;
+  c->cap = (cap + kChunk - 1) / kChunk * kChunk;
+  c->max_blocks = (int)(c->cap / kChunk);
+  hipError_t e = hipGetDevice(&c->device);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->stage, 2 * c->cap * sizeof(float));
+  if (e == hipSuccess)
+    e = hipExtMallocWithFlags((void**)&c->flags, (size_t)c->max_blocks * kMaxPeers * sizeof(unsigned),
+                              hipDeviceMallocUncached);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->epoch, (size_t)c->max_blocks * sizeof(unsigned));
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->err_h, sizeof(unsigned), hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->err_d, c->err_h, 0);
+  if (e == hipSuccess) e = hipMemset(c->flags, 0, (size_t)c->max_blocks * kMaxPeers * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(c->epoch, 0, (size_t)c->max_blocks * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(c->stage, 0, 2 * c->cap * sizeof(float));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  hipIpcMemHandle_t hs, hf;
+  if (e == hipSuccess) e = hipIpcGetMemHandle(&hs, c->stage);
+  if (e == hipSuccess) e = hipIpcGetMemHandle(&hf, c->flags);
+  if (e != hipSuccess) {
+    release(c);
+    return (int)e;
+  }
+  *c->err_h = 0;
+  std::memcpy(handles, &hs, kHandleBytes);
+  std::memcpy((char*)handles + kHandleBytes, &hf, kHandleBytes);
+  *out = c;
+  return 0;
+}
+
+// Map every peer's stage/flags; `all` = world consecutive handle sets in rank order.
+RK_API int rk_p2p_open(void* ctx, const void* all) {
+  auto* c = (P2PCtx*)ctx;
+  for (int r = 0; r < c->world; ++r) {
+    if (r == c->rank) {
+      c->peer_stage[r] = c->stage;
+      c->peer_flags[r] = c->flags;
+      continue;
+    }
+    hipIpcMemHandle_t hs, hf;
+    std::memcpy(&hs, (const char*)all + (size_t)r * 2 * kHandleBytes, kHandleBytes);
+    std::memcpy(&hf, (const char*)all + (size_t)r * 2 * kHandleBytes + kHandleBytes, kHandleBytes);
+    void *ps = nullptr, *pf = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&ps, hs, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return (int)e;
+    e = hipIpcOpenMemHandle(&pf, hf, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      (void)hipIpcCloseMemHandle(ps);
+      return (int)e;
+    }
+    c->peer_stage[r] = (float*)ps;
+    c->peer_flags[r] = (unsigned*)pf;
+    c->mapped[r] = true;
+  }
+  return 0;
+}
+
+// data[0:n] <- scale * sum over ranks (in place, stream-ordered, graph-capturable).  16-byte
+// aligned data; n <= cap.
+RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipStream_t s) {
+  auto* c = (P2PCtx*)ctx;
+  if (n <= 0) return 0;
+  if (n > c->cap || ((uintptr_t)data & 15)) return (int)hipErrorInvalidValue;
+  P2PArgs a{};
+  for (int r = 0; r < c->world; ++r) {
+    if (!c->peer_stage[r]) return (int)hipErrorNotInitialized;
+    a.stage[r] = c->peer_stage[r];
+    a.flags[r] = c->peer_flags[r];
+  }
+  for (int r = c->world; r < kMaxPeers; ++r) {  // never dereferenced (r >= world), keep them valid anyway
+    a.stage[r] = c->stage;
+    a.flags[r] = c->flags;
+  }
+  a.epoch = c->epoch;
+  a.err = c->err_d;
+  a.data = data;
+  a.n = n;
+  a.cap = c->cap;
+  a.scale = scale;
+  a.rank = c->rank;
+  a.world = c->world;
+  const int blocks = (int)((n + kChunk - 1) / kChunk);
+  switch (c->world) {
+    case 1: p2p_allreduce_kernel<1><<<blocks, kThreads, 0, s>>>(a); break;
+    case 2: p2p_allreduce_kernel<2><<<blocks, kThreads, 0, s>>>(a); break;
+    case 3: p2p_allreduce_kernel<3><<<blocks, kThreads, 0, s>>>(a); break;
+    case 4: p2p_allreduce_kernel<4><<<blocks, kThreads, 0, s>>>(a); break;
+    case 5: p2p_allreduce_kernel<5><<<blocks, kThreads, 0, s>>>(a); break;
+    case 6: p2p_allreduce_kernel<6><<<blocks, kThreads, 0, s>>>(a); break;
+    case 7: p2p_allreduce_kernel<7><<<blocks, kThreads, 0, s>>>(a); break;
+    default: p2p_allreduce_kernel<8><<<blocks, kThreads, 0, s>>>(a); break;
+  }
+  return (int)hipGetLastError();
+}
+
+// 0 = healthy; 1 = a peer never signalled within the timeout (results of that launch are invalid)
+RK_API int rk_p2p_error(void* ctx) { return (int)__atomic_load_n(((P2PCtx*)ctx)->err_h, __ATOMIC_ACQUIRE); }
+
+RK_API int rk_p2p_destroy(void* ctx) {
+  if (!ctx) return 0;
+  (void)hipDeviceSynchronize();
+  release((P2PCtx*)ctx);
+  return 0;
+}

@@ -72,6 +72,13 @@ KERNEL_SIGS = {
     "rk_gelu_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_softmax_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p]),
     "rk_softmax_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p]),
+    "rk_p2p_handle_bytes": (c_int, []),
+    "rk_p2p_chunk": (c_int, []),
+    "rk_p2p_create": (c_int, [c_int, c_int, c_int64, c_void_p, c_void_p]),
+    "rk_p2p_open": (c_int, [c_void_p, c_void_p]),
+    "rk_p2p_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
+    "rk_p2p_error": (c_int, [c_void_p]),
+    "rk_p2p_destroy": (c_int, [c_void_p]),
     "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 10 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
 }
 

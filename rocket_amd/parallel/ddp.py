@@ -29,7 +29,9 @@ Design for MI355X + RCCL over xGMI (SURVEY §5 "communication design"):
   from rank 0 before each synchronised forward (N4, ``broadcast_buffers``).
 
 A native RCCL communicator (``rocket_amd.parallel.rccl``) can be plugged in
-through ``comm=``; the default uses the ``torch.distributed`` RCCL group.
+through ``comm=``; the default uses the ``torch.distributed`` RCCL group, except that when all
+buckets together are small (≤ 16 MB fp32, one node) they are reduced by the one-shot xGMI kernel
+of :mod:`rocket_amd.parallel.p2p` — stream-ordered and graph-capturable (``capturable``).
 """
 
 from __future__ import annotations
@@ -96,6 +98,17 @@ class _ScaleAfter:
         self.flat.mul_(self.scale)
 
 
+class _StreamOrdered:
+    """Work handle of a reduction already ordered on the compute stream (P2P kernel / native
+    reducer joined before the optimizer): nothing to wait for on the host."""
+
+    def wait(self):
+        pass
+
+
+_ISSUED = _StreamOrdered()
+
+
 class DataParallel(nn.Module):
     """Replicate ``module`` on every rank and average gradients across ranks."""
 
@@ -116,8 +129,11 @@ class DataParallel(nn.Module):
         self._build_buckets(bucket_cap_mb, first_bucket_mb)
         self._armed = False
         self._deferred = False
+        self._reduces = 0
         # native transport: per-bucket all-reduce on a side stream, one join before the optimizer
         self._native = self.comm.make_reducer([b.flat for b in self.buckets]) if hasattr(self.comm, "make_reducer") else None
+        # small models: one-shot xGMI all-reduce kernel (graph-capturable) instead of RCCL
+        self._p2p = self._make_p2p() if (comm is None and self._native is None) else None
 
     # ----------------------------------------------------------------- setup
     def _flat_broadcast(self, tensors: List[torch.Tensor]) -> None:
@@ -188,6 +204,31 @@ class DataParallel(nn.Module):
                 p.register_post_accumulate_grad_hook(self._on_grad)
         self.params = [p for b in self.buckets for p in b.params]
         self._ids = {id(p) for p in self.params}
+
+    def _make_p2p(self):
+        from rocket_amd.parallel import p2p
+        from rocket_amd.runtime import comm as rcomm
+
+        ctx = rcomm.context()
+        if (not p2p.enabled() or not isinstance(self.comm, _TorchDistComm)
+                or not (self.comm.avg_native or p2p.forced())
+                or ctx.local_world_size != ctx.world_size or ctx.world_size > 8 or not self.buckets
+                or any(b.flat.dtype != torch.float32 or b.flat.device.type != "cuda" for b in self.buckets)
+                or sum(b.flat.numel() for b in self.buckets) > p2p.MAX_ELEMS):
+            return None
+        return p2p.P2PAllReduce.create(max(b.flat.numel() for b in self.buckets), group=ctx.host_group,
+                                       device=self.buckets[0].flat.device)
+
+    def check_comm(self) -> None:
+        """Surface an asynchronous transport failure (P2P peer timeout) as an exception."""
+        if self._p2p is not None:
+            self._p2p.check()
+
+    @property
+    def capturable(self) -> bool:
+        """True when the gradient all-reduce is a plain kernel (P2P): a synchronising step can be
+        captured into ONE graph with the reduction between backward and optimizer."""
+        return self._p2p is not None
 
     # --------------------------------------------------------------- runtime
     @contextlib.contextmanager
@@ -294,9 +335,12 @@ class DataParallel(nn.Module):
                 b.work = None
 
     def _launch(self, b: _Bucket):
+        if self._p2p is not None:
+            self._p2p.all_reduce_(b.flat, 1.0 / self.comm.world)
+            return _ISSUED
         if self._native is not None:
             self._native.launch(b.index)
-            return None
+            return _ISSUED
         return self.comm.all_reduce_avg(b.flat)
 
     def owns(self, p) -> bool:

@@ -1,0 +1,105 @@
+"""One-shot peer-to-peer all-reduce over xGMI (``native/kernels/p2p.hip``).
+
+For gradient buckets that are latency-bound on RCCL — LeNet's whole gradient is 247 KB — every
+rank maps every peer's staging buffer once (HIP IPC handles exchanged over the host gloo group)
+and a single kernel reads all W contributions directly over the point-to-point xGMI links,
+sums them in rank order (bit-identical on every rank) and writes the average in place.  The
+kernel synchronises with its peers through per-block epoch flags in device memory, so it is
+stream-ordered and **graph-capturable**: a data-parallel training step becomes one HIP graph
+(forward, backward, all-reduce, optimizer) with no host hop between backward and optimizer.
+
+This replaces, for small buckets, the RCCL all-reduce DDP issues at the reference's
+``loss.py:119`` backward (SURVEY §2.6 C5, §5 "Tiny models such as LeNet ... one-shot P2P").
+Large buckets stay on RCCL, whose ring/direct algorithms are bandwidth-optimal.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import logging
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from rocket_amd.ops import _lib
+
+logger = logging.getLogger(__name__)
+
+#: largest total bucket size (fp32 elements) routed through the P2P kernel (16 MB)
+MAX_ELEMS = int(os.environ.get("ROCKET_P2P_MAX_ELEMS", str(4 << 20)))
+
+
+def enabled() -> bool:
+    """``ROCKET_P2P``: "1" (default: used with the RCCL backend), "0" (never), "force" (also with a
+    gloo tensor group — tests that put several ranks on one GPU, where RCCL cannot run)."""
+    return os.environ.get("ROCKET_P2P", "1").lower() not in ("0", "false", "no")
+
+
+def forced() -> bool:
+    return os.environ.get("ROCKET_P2P", "").lower() == "force"
+
+
+class P2PAllReduce:
+    """Per-process context: this rank's IPC-exported stage/flags plus every peer's mapping."""
+
+    def __init__(self, ctx: int, rank: int, world: int, cap: int, device: torch.device):
+        self._ctx = ctx
+        self.rank, self.world, self.cap, self.device = rank, world, cap, device
+        self.launches = 0
+
+    @classmethod
+    def create(cls, cap: int, group=None, device: Optional[torch.device] = None) -> Optional["P2PAllReduce"]:
+        """Collective over ``group`` (a host/gloo group): every rank gets a context, or every
+        rank gets None (any failure anywhere -> the caller keeps RCCL)."""
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        device = device or torch.device("cuda", torch.cuda.current_device())
+        lib = _lib.kernels()
+        ctx = ctypes.c_void_p()
+        hb = int(lib.rk_p2p_handle_bytes())
+        buf = (ctypes.c_char * hb)()
+        with torch.cuda.device(device):
+            rc = lib.rk_p2p_create(rank, world, int(cap), ctypes.byref(ctx), buf)
+        mine = bytes(buf) if rc == 0 else None
+        if rc != 0:
+            logger.warning(f"p2p all-reduce unavailable on rank {rank}: rk_p2p_create -> hipError {rc}")
+        every = [None] * world
+        dist.all_gather_object(every, mine, group=group)
+        if any(h is None for h in every):
+            if rc == 0:
+                lib.rk_p2p_destroy(ctx)
+            return None
+        with torch.cuda.device(device):
+            rc = lib.rk_p2p_open(ctx, b"".join(every))
+        if rc != 0:
+            logger.warning(f"p2p all-reduce unavailable on rank {rank}: rk_p2p_open -> hipError {rc}")
+        oks = [None] * world
+        dist.all_gather_object(oks, rc == 0, group=group)
+        if not all(oks):
+            lib.rk_p2p_destroy(ctx)
+            return None
+        dist.barrier(group=group)  # every mapping exists before any rank launches
+        return cls(ctx.value, rank, world, int(cap), device)
+
+    def all_reduce_(self, flat: torch.Tensor, scale: float = 1.0) -> None:
+        """``flat <- scale * sum_ranks(flat)`` in place on the current stream (graph-capturable)."""
+        if flat.dtype != torch.float32 or not flat.is_contiguous() or flat.numel() > self.cap:
+            raise ValueError("p2p all-reduce takes a contiguous fp32 buffer within the capacity")
+        _lib.check(_lib.kernels().rk_p2p_allreduce(self._ctx, flat.data_ptr(), flat.numel(), float(scale),
+                                                   _lib.stream_ptr(flat.device)), "rk_p2p_allreduce")
+        self.launches += 1
+        if self.launches % 256 == 0:
+            self.check()
+
+    def check(self) -> None:
+        """Raise if a launch ever timed out waiting for a peer (its results were invalid)."""
+        if self._ctx and _lib.kernels().rk_p2p_error(self._ctx):
+            raise RuntimeError("p2p all-reduce: a peer did not signal within the timeout (dead or desynchronised rank)")
+
+    def close(self) -> None:
+        """Unmap the peers and free the buffers (collective: every rank, when no launch is pending
+        anywhere).  Not done implicitly: at interpreter exit the mappings are simply left."""
+        if self._ctx:
+            _lib.kernels().rk_p2p_destroy(self._ctx)
+            self._ctx = 0

@@ -105,6 +105,7 @@ class StepGraphs:
         self.mod = module_capsule
         self.warmup = max(1, int(warmup))
         self.variants: Dict[Any, _Captured] = {}
+        self.parts = 0  # most graphs one captured step was split into (1 = whole step in one graph)
         self.seen = collections.Counter()
         self.pool = None
         self.disabled_reason = None
@@ -255,20 +256,23 @@ class StepGraphs:
         v.persistent = [bool(getattr(t, "_rocket_persistent", False)) for t in tens]
         v.static_in = [t if keep else t.detach().clone() for t, keep in zip(tens, v.persistent)]
         rep = self._replica()
-        split = v.sync and rep is not None
-        if split and rep.broadcast_buffers:
+        inline = v.sync and rep is not None and rep.capturable  # all-reduce kernel inside the graph
+        split = v.sync and rep is not None and not inline
+        if v.sync and rep is not None and rep.broadcast_buffers:
             rep.sync_buffers()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
         cap = Attributes(attrs)
         cap.batch = _rebuild(attrs.batch, iter(v.static_in))
         cap.capturing = True
-        cap.graph_split = split
+        cap.graph_split = v.sync and rep is not None  # a cross-rank reduce separates device / device_synced
         torch.cuda.synchronize()
         ga = torch.cuda.CUDAGraph()
         # thread_local: the RCCL watchdog thread keeps polling its events while we capture
         with torch.cuda.graph(ga, pool=self.pool, capture_error_mode="thread_local"):
             self._phase_a(cap)
+            if inline:
+                rep.reduce_now()
             if not split:
                 self._phase_b(cap)
         v.graphs.append(ga)
@@ -279,6 +283,7 @@ class StepGraphs:
             v.graphs.append(gb)
         v.out = cap.batch
         self.captures += 1
+        self.parts = max(self.parts, len(v.graphs))
         logger.info(f"captured HIP graph(s) for sync={v.sync} ({len(v.graphs)} part(s))")
         # the captured work has not run yet: replay it for this iteration
         self._run(v, rep if split else None)
@@ -302,10 +307,12 @@ class StepGraphs:
         for dst, src, keep in zip(v.static_in, tens, v.persistent):
             if not keep:
                 dst.copy_(src, non_blocking=True)
-        rep = self._replica() if len(v.graphs) > 1 else None
+        rep = self._replica() if v.sync else None
         if rep is not None and rep.broadcast_buffers:
             rep.sync_buffers()
-        self._run(v, rep)
+        if rep is not None and self.replays % 1024 == 1023:
+            rep.check_comm()
+        self._run(v, rep if len(v.graphs) > 1 else None)
         attrs.batch = v.out
         self._host(attrs)
 

@@ -1,8 +1,10 @@
-"""Data-parallel captured steps (graph A -> host all-reduce -> graph B) vs eager, 2 ranks on one GPU.
+"""Data-parallel captured steps vs eager, 2 ranks on one GPU.
 
 The ranks share ``cuda:0`` and talk over gloo (``ROCKET_DIST_BACKEND=gloo``):
-this rehearses the multi-GPU code path — deferred bucket reduction, side-channel
-loss averaging, two-part graphs — on the single-GPU box.
+this rehearses the multi-GPU code paths on the single-GPU box —
+* ``ROCKET_P2P=0``: graph A -> host-issued bucket all-reduce -> graph B (the RCCL path);
+* ``ROCKET_P2P=force``: the one-shot IPC all-reduce kernel captured INSIDE one graph per step —
+plus deferred bucket reduction and side-channel loss averaging in both.
 """
 
 import json
@@ -22,9 +24,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, p2p):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROCKET_DIST_BACKEND="gloo")
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROCKET_DIST_BACKEND="gloo", ROCKET_P2P=p2p)
     import rocket_amd as rocket
     from rocket_amd.core.capsule import Capsule
     from rocket_amd.models import CrossEntropy, LeNet
@@ -65,6 +67,8 @@ def _worker(rank, world, port, out_dir):
             losses=[float(v) for v in rec.losses],
             w=float(sum(p.detach().double().sum() for p in net.parameters())),
             replays=(mod._graphs.replays if mod._graphs is not None else 0),
+            parts=(mod._graphs.parts if mod._graphs is not None else 0),
+            p2p=bool(getattr(mod._module, "capturable", False)),
             reason=(mod._graphs.disabled_reason if mod._graphs is not None else None),
         )
     with open(os.path.join(out_dir, f"r{rank}.json"), "w") as fh:
@@ -75,13 +79,15 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_ddp_graph_two_ranks(tmp_path):
+@pytest.mark.parametrize("p2p", ["0", "force"])
+def test_ddp_graph_two_ranks(tmp_path, p2p):
     port = _free_port()
-    mp.start_processes(_worker, args=(2, port, str(tmp_path)), nprocs=2, start_method="spawn", join=True)
+    mp.start_processes(_worker, args=(2, port, str(tmp_path), p2p), nprocs=2, start_method="spawn", join=True)
     r = [json.load(open(tmp_path / f"r{i}.json")) for i in range(2)]
     for rank in range(2):
         e, g = r[rank]["False"], r[rank]["True"]
         assert g["replays"] > 0 and g["reason"] == "released", g
+        assert g["p2p"] == (p2p == "force") and g["parts"] == (1 if p2p == "force" else 2), g
         assert len(e["losses"]) == len(g["losses"]) > 0
         for a, b in zip(e["losses"], g["losses"]):
             assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (e["losses"], g["losses"])
