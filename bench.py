@@ -184,7 +184,8 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
             "dtype": "bf16" if args.mp == "bf16" else "fp32",
-            "data": "synthetic (random 1x28x28 MNIST-shaped images/labels in HBM, random-init weights)",
+            "data": f"synthetic (random {'x'.join(map(str, in_shape))} images / {classes}-class labels resident in HBM, "
+            "random-init weights)",
             "config": {
                 "model": desc,
                 "global_batch": args.batch * world,
