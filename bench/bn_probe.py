@@ -52,8 +52,9 @@ def main():
         tf = bench(fused)
         tt = bench(torch_path)
         elems = x.numel()
-        # fwd: stats read x; apply read x (+r) write y.  bwd: reduce read dy,x,y; apply read dy,x,y write dx (+dres)
-        nbytes = 2 * elems * (1 + 2 + (1 if res else 0) + 3 + 4 + (1 if res else 0))
+        # fwd: stats read x; apply read x (+r) write y + 1-bit ReLU mask.  bwd: reduce read dy,x,mask;
+        # apply read dy,x,mask write dx (+dres)
+        nbytes = 2 * elems * (1 + 2 + (1 if res else 0) + 2 + 3 + (1 if res else 0) + 3 / 16)
         print(json.dumps(dict(shape=[n, c, h, h], residual=res, fused_ms=round(tf, 3), torch_ms=round(tt, 3),
                               fused_GBps=round(nbytes / tf / 1e6, 1))), flush=True)
 

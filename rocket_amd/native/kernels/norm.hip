@@ -27,7 +27,12 @@ namespace {
 constexpr int BN_T = 256;        // threads per block
 constexpr int BN_CT = 64;        // channels per block column
 constexpr int BN_RG = BN_T / 8;  // row groups per block pass (each thread: 8 channels)
-constexpr int BN_U = 4;          // rows in flight per thread per loop iteration
+constexpr int BN_U = 4;          // rows in flight per thread per loop iteration (two-tensor passes)
+constexpr int BN_US = 8;         // rows in flight per thread in the one-tensor statistics pass
+constexpr int BN_GS = 16;        // row blocks per first-level finalize group
+constexpr int BN_MAXRB = 2048;   // row blocks per column (upper bound)
+constexpr int BN_CNT = 1 + BN_MAXRB / BN_GS;  // ticket counters per column: column + groups
+constexpr int BN_ROWQ = BN_US * BN_RG;       // row-block granularity (multiple of both unrolls)
 
 template <typename T> struct V8;
 template <> struct V8<uint16_t> {
@@ -73,12 +78,88 @@ __device__ __forceinline__ void reduce_rowgroups(const float* v, float (*lds)[BN
   __syncthreads();
 }
 
+// ---- two-level in-launch column reduction -------------------------------------------------
+// A reduction launch has grid (C/64 column blocks, RB row blocks).  Each block stores its 64x2
+// partial sums into part[b]; the last block (ticket) of every group of BN_GS row blocks sums that
+// group into part2[g]; the last group of the column sums the RB/BN_GS group totals.  Both serial
+// tails are short (<= 16 and <= 128 partials over 4 threads per channel), so the grid can be
+// ~2048 blocks — enough bytes in flight to stream HBM — without a long single-block finalize.
+// Hand-off without fences (cdna guide §6 G16 R1): partials are stored write-through (sc1, relaxed
+// agent atomics), every storing wave drains vmcnt before the workgroup barrier, lane 0 takes the
+// ticket, and the reducer reads EVERY partial with sc1 loads — no L2 write-back, no L1 invalidate.
+// Fixed summation order: results are deterministic.  Counters self-reset (graph replays).
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void bn_sum_parts(const float* part, int C, int c0, int b0, int b1, float& t1,
+                                             float& t2) {
+  const int ch = threadIdx.x >> 2, sub = threadIdx.x & 3, cc = c0 + ch;
+  float s1 = 0.f, s2 = 0.f;
+  if (cc < C) {
+#pragma unroll 8
+    for (int b = b0 + sub; b < b1; b += 4) {
+      const float* p = part + (int64_t)b * 2 * C;
+      s1 += ld_sc1(p + cc);
+      s2 += ld_sc1(p + C + cc);
+    }
+  }
+  s1 += __shfl_xor(s1, 1, 64);
+  s1 += __shfl_xor(s1, 2, 64);
+  s2 += __shfl_xor(s2, 1, 64);
+  s2 += __shfl_xor(s2, 2, 64);
+  t1 = s1;
+  t2 = s2;
+}
+
+// call from all threads after this block's sc1 stores; true in all threads of the block whose
+// ticket completes `total`
+__device__ __forceinline__ bool bn_ticket(unsigned* cnt, unsigned total, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *flag = (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1);
+  __syncthreads();
+  return *flag != 0;
+}
+
+// s1/s2: this block's 64 channel sums (LDS).  Returns true in the one finalising block of the
+// column; the column totals are then in (t1, t2) of the threads with (tid & 3) == 0, channel
+// c0 + tid / 4.
+__device__ __forceinline__ bool bn_column_reduce(const float* s1, const float* s2, float* part, int C, int c0,
+                                                 unsigned* cnt, float& t1, float& t2, int* flag) {
+  const int rb = gridDim.y, b = blockIdx.y, g = b / BN_GS, ng = (rb + BN_GS - 1) / BN_GS;
+  float* part2 = part + (int64_t)rb * 2 * C;
+  unsigned* col = cnt + blockIdx.x * BN_CNT;
+  if (threadIdx.x < BN_CT && c0 + threadIdx.x < C) {
+    st_sc1(part + (int64_t)b * 2 * C + c0 + threadIdx.x, s1[threadIdx.x]);
+    st_sc1(part + (int64_t)b * 2 * C + C + c0 + threadIdx.x, s2[threadIdx.x]);
+  }
+  const int gb0 = g * BN_GS, gb1 = min(rb, gb0 + BN_GS);
+  if (!bn_ticket(col + 1 + g, (unsigned)(gb1 - gb0), flag)) return false;
+  if (threadIdx.x == 0) __hip_atomic_store(col + 1 + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bn_sum_parts(part, C, c0, gb0, gb1, t1, t2);
+  if (ng == 1) return true;
+  const int ch = threadIdx.x >> 2;
+  if ((threadIdx.x & 3) == 0 && c0 + ch < C) {
+    st_sc1(part2 + (int64_t)g * 2 * C + c0 + ch, t1);
+    st_sc1(part2 + (int64_t)g * 2 * C + C + c0 + ch, t2);
+  }
+  if (!bn_ticket(col, (unsigned)ng, flag)) return false;
+  if (threadIdx.x == 0) __hip_atomic_store(col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bn_sum_parts(part2, C, c0, 0, ng, t1, t2);
+  return true;
+}
+
 struct BnStatsArgs {
   const void* x;
   int64_t R;
   int C, rpb;
-  float* part;  // [RB][2][C]
-  unsigned* counters;  // [C/64]
+  float* part;         // [RB][2][C] + [RB/BN_GS][2][C]
+  unsigned* counters;  // [C/64][BN_CNT]
   const float* gamma;
   const float* beta;
   float* mean;
@@ -91,6 +172,7 @@ struct BnStatsArgs {
   float momentum, eps;
 };
 
+// one tensor streamed: BN_US rows (16 B each) in flight per thread
 template <typename T>
 __global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
   __shared__ float lds[BN_RG][BN_CT + 1];
@@ -107,12 +189,12 @@ __global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
   V8<T>::load(x + (cok ? c : 0), piv);  // pivot: row 0 (same for every block)
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc1[k] = acc2[k] = 0.f;
-  for (int64_t r = r0 + rg; r < r1; r += BN_U * BN_RG) {
-    float v[BN_U][8];
+  for (int64_t r = r0 + rg; r < r1; r += BN_US * BN_RG) {
+    float v[BN_US][8];
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) V8<T>::load(x + min(r + u * BN_RG, r1 - 1) * a.C + (cok ? c : 0), v[u]);
+    for (int u = 0; u < BN_US; ++u) V8<T>::load(x + min(r + u * BN_RG, r1 - 1) * a.C + (cok ? c : 0), v[u]);
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < BN_US; ++u) {
       const bool ok = r + u * BN_RG < r1;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -128,39 +210,10 @@ __global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
   }
   reduce_rowgroups(acc1, lds, s1);
   reduce_rowgroups(acc2, lds, s2);
-  float* part = a.part + (int64_t)blockIdx.y * 2 * a.C;
-  if (threadIdx.x < BN_CT && c0 + threadIdx.x < a.C) {
-    part[c0 + threadIdx.x] = s1[threadIdx.x];
-    part[a.C + c0 + threadIdx.x] = s2[threadIdx.x];
-  }
-  // last block of this channel column finalises
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const unsigned t = __hip_atomic_fetch_add(a.counters + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = (t == gridDim.y - 1);
-    if (flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-  if (!flag) return;
-  // 4 threads per channel split the RB partials
-  const int ch = threadIdx.x >> 2, sub = threadIdx.x & 3;
-  const int cc = c0 + ch;
-  float t1 = 0.f, t2 = 0.f;
-  if (cc < a.C) {
-#pragma unroll 8
-    for (int b = sub; b < (int)gridDim.y; b += 4) {
-      const float* p = a.part + (int64_t)b * 2 * a.C;
-      t1 += __builtin_nontemporal_load(p + cc);
-      t2 += __builtin_nontemporal_load(p + a.C + cc);
-    }
-  }
-  t1 += __shfl_xor(t1, 1, 64);
-  t1 += __shfl_xor(t1, 2, 64);
-  t2 += __shfl_xor(t2, 1, 64);
-  t2 += __shfl_xor(t2, 2, 64);
-  if (sub == 0 && cc < a.C) {
+  float t1, t2;
+  if (!bn_column_reduce(s1, s2, a.part, a.C, c0, a.counters, t1, t2, &flag)) return;
+  const int cc = c0 + (threadIdx.x >> 2);
+  if ((threadIdx.x & 3) == 0 && cc < a.C) {
     const double n = (double)a.R;
     const float p0 = Ld<T>::get(x, cc);  // the pivot the partial sums were shifted by
     const float dm = (float)(t1 / n);
@@ -181,18 +234,19 @@ __global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
     }
   }
   if (threadIdx.x == 0 && blockIdx.x == 0 && a.nbt) a.nbt[0] += 1;
-  if (threadIdx.x == 0) __hip_atomic_store(a.counters + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Elementwise passes: thread t owns channel vector cv = t % CV (CV = C/8 <= 256) for the whole
 // launch, so its per-channel coefficients live in registers (loaded once), and walks rows
 // r = r0 + t / CV, stepping by RPP = BN_T / CV rows; 4 rows per iteration with clamped
 // (always valid) addresses keep 4 independent 16-byte loads in flight per tensor.
-// y = relu?(x*a + b + res?)
+// y = relu?(x*a + b + res?).  With ReLU the launch also writes the 1-bit mask [y > 0]
+// (mask[r][cv], bit k = channel 8cv + k): the backward reads 1 byte per 8 elements instead of y.
 template <typename T, typename TO>
 __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x, const TO* __restrict__ res,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
-                                                        TO* __restrict__ y, int64_t R, int C, int relu, int rpb) {
+                                                        TO* __restrict__ y, uint8_t* __restrict__ mask, int64_t R,
+                                                        int C, int relu, int rpb) {
   const int CV = C >> 3, RPP = BN_T / CV;
   if ((int)threadIdx.x >= RPP * CV) return;
   const int cv = threadIdx.x % CV, c = cv * 8;
@@ -214,14 +268,21 @@ __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x,
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
+      unsigned m = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float o = v[u][k] * A[k] + B[k];
         if (res) o += q[u][k];
-        if (relu) o = fmaxf(o, 0.f);
+        if (relu) {
+          o = fmaxf(o, 0.f);
+          m |= (o > 0.f ? 1u : 0u) << k;
+        }
         v[u][k] = o;
       }
-      if (r + u * RPP < r1) V8<TO>::store(y + (r + u * RPP) * C + c, v[u]);
+      if (r + u * RPP < r1) {
+        V8<TO>::store(y + (r + u * RPP) * C + c, v[u]);
+        if (mask) mask[(r + u * RPP) * CV + cv] = (uint8_t)m;
+      }
     }
   }
 }
@@ -229,7 +290,7 @@ __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x,
 struct BnBwdArgs {
   const void* dy;
   const void* x;
-  const void* y;  // fused-ReLU output (mask), may be null
+  const uint8_t* mask;  // fused-ReLU mask [R][C/8] (bit k: channel 8cv + k), may be null
   int64_t R;
   int C, rpb;
   const float* mean;
@@ -249,12 +310,13 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
   __shared__ int flag;
   const TO* dy = (const TO*)a.dy;
   const T* x = (const T*)a.x;
-  const TO* y = (const TO*)a.y;
+  const uint8_t* mk = a.mask;
   const int c0 = blockIdx.x * BN_CT;
   const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
   const int c = c0 + cg * 8;
   const bool cok = c < a.C;
   const int cs = cok ? c : 0;
+  const int CV = a.C >> 3, cv = cs >> 3;
   float mu[8], is[8], acc1[8], acc2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -265,20 +327,21 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
   const int64_t r0 = (int64_t)blockIdx.y * a.rpb;
   const int64_t r1 = min(a.R, r0 + a.rpb);
   for (int64_t r = r0 + rg; r < r1; r += BN_U * BN_RG) {
-    float g[BN_U][8], xv[BN_U][8], yv[BN_U][8];
+    float g[BN_U][8], xv[BN_U][8];
+    unsigned mb[BN_U];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const int64_t ru = min(r + u * BN_RG, r1 - 1);
       V8<TO>::load(dy + ru * a.C + cs, g[u]);
       V8<T>::load(x + ru * a.C + cs, xv[u]);
-      if (y) V8<TO>::load(y + ru * a.C + cs, yv[u]);
+      mb[u] = mk ? mk[ru * CV + cv] : 0xFFu;
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const bool ok = r + u * BN_RG < r1;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float gg = (ok && (!y || yv[u][k] > 0.f)) ? g[u][k] : 0.f;
+        const float gg = (ok && ((mb[u] >> k) & 1u)) ? g[u][k] : 0.f;
         acc1[k] += gg;
         acc2[k] += gg * (xv[u][k] - mu[k]) * is[k];
       }
@@ -290,37 +353,10 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
   reduce_rowgroups(acc1, lds, s1);
   reduce_rowgroups(acc2, lds, s2);
-  float* part = a.part + (int64_t)blockIdx.y * 2 * a.C;
-  if (threadIdx.x < BN_CT && c0 + threadIdx.x < a.C) {
-    part[c0 + threadIdx.x] = s1[threadIdx.x];
-    part[a.C + c0 + threadIdx.x] = s2[threadIdx.x];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const unsigned t = __hip_atomic_fetch_add(a.counters + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = (t == gridDim.y - 1);
-    if (flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-  if (!flag) return;
-  const int ch = threadIdx.x >> 2, sub = threadIdx.x & 3;
-  const int cc = c0 + ch;
-  float t1 = 0.f, t2 = 0.f;
-  if (cc < a.C) {
-#pragma unroll 8
-    for (int b = sub; b < (int)gridDim.y; b += 4) {
-      const float* p = a.part + (int64_t)b * 2 * a.C;
-      t1 += __builtin_nontemporal_load(p + cc);
-      t2 += __builtin_nontemporal_load(p + a.C + cc);
-    }
-  }
-  t1 += __shfl_xor(t1, 1, 64);
-  t1 += __shfl_xor(t1, 2, 64);
-  t2 += __shfl_xor(t2, 1, 64);
-  t2 += __shfl_xor(t2, 2, 64);
-  if (sub == 0 && cc < a.C) {
+  float t1, t2;
+  if (!bn_column_reduce(s1, s2, a.part, a.C, c0, a.counters, t1, t2, &flag)) return;
+  const int cc = c0 + (threadIdx.x >> 2);
+  if ((threadIdx.x & 3) == 0 && cc < a.C) {
     if (a.dbeta) a.dbeta[cc] += t1;
     if (a.dgamma) a.dgamma[cc] += t2;
     // dx = a*(dy' - k1 - xhat*k2), xhat = (x - mean)*invstd  ->  P*dy' + Q*x + S
@@ -330,15 +366,14 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
     a.coef[a.C + cc] = -sa * k2 * is;
     a.coef[2 * a.C + cc] = sa * (k2 * is * mu - k1);
   }
-  if (threadIdx.x == 0) __hip_atomic_store(a.counters + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // dx = P*dy' + Q*x + S (per-channel coefficients in registers); dres = dy'
 template <typename T, typename TO>
 __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
-                                                            const TO* __restrict__ y, const float* __restrict__ coef,
-                                                            T* __restrict__ dx, TO* __restrict__ dres, int64_t R, int C,
-                                                            int rpb) {
+                                                            const uint8_t* __restrict__ mask,
+                                                            const float* __restrict__ coef, T* __restrict__ dx,
+                                                            TO* __restrict__ dres, int64_t R, int C, int rpb) {
   const int CV = C >> 3, RPP = BN_T / CV;
   if ((int)threadIdx.x >= RPP * CV) return;
   const int cv = threadIdx.x % CV, c = cv * 8;
@@ -352,19 +387,20 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(const TO* __restrict
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = min(R, r0 + rpb);
   for (int64_t r = r0 + threadIdx.x / CV; r < r1; r += BN_U * RPP) {
-    float g[BN_U][8], xv[BN_U][8], yv[BN_U][8];
+    float g[BN_U][8], xv[BN_U][8];
+    unsigned mb[BN_U];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const int64_t ru = min(r + u * RPP, r1 - 1);
       V8<TO>::load(dy + ru * C + c, g[u]);
       V8<T>::load(x + ru * C + c, xv[u]);
-      if (y) V8<TO>::load(y + ru * C + c, yv[u]);
+      mb[u] = mask ? mask[ru * CV + cv] : 0xFFu;
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
-      if (y) {
+      if (mask) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) g[u][k] = yv[u][k] > 0.f ? g[u][k] : 0.f;
+        for (int k = 0; k < 8; ++k) g[u][k] = ((mb[u] >> k) & 1u) ? g[u][k] : 0.f;
       }
       const bool ok = r + u * RPP < r1;
       if (ok && dres) V8<TO>::store(dres + (r + u * RPP) * C + c, g[u]);
@@ -576,26 +612,29 @@ __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ 
 }
 
 int bn_grid_rows(int64_t R, int C, int* rpb) {
-  // enough blocks for a bandwidth-bound pass (>= 4 per CU) while keeping the serial finalize
-  // short; at least one full unrolled pass (BN_U * BN_RG rows) per block
+  // ~2048 blocks in total (8 per CU: enough loads in flight to stream HBM); the two-level
+  // finalize keeps the serial tail short at any block count
   const int ncol = (C + BN_CT - 1) / BN_CT;
-  int64_t rb = 1024 / ncol;  // ~1024 blocks; the column's last block sums rb partials
-  if (rb < 128) rb = 128;
-  if (rb > 512) rb = 512;
+  int64_t rb = 2048 / ncol;
+  if (rb < 1) rb = 1;
+  if (rb > BN_MAXRB) rb = BN_MAXRB;
   int64_t per = (R + rb - 1) / rb;
-  per = (per + BN_U * BN_RG - 1) / (BN_U * BN_RG) * (BN_U * BN_RG);
+  per = (per + BN_ROWQ - 1) / BN_ROWQ * BN_ROWQ;
   *rpb = (int)per;
   return (int)((R + per - 1) / per);
 }
 
 }  // namespace
 
-// workspace needed by the BN reductions (floats): 2*C*RB
+// workspace needed by the BN reductions (floats): block partials + group partials, 2*C each
 RK_API int64_t rk_bn_workspace(int64_t R, int C) {
   int rpb;
   const int rb = bn_grid_rows(R, C, &rpb);
-  return (int64_t)rb * 2 * C;
+  return (int64_t)(rb + (rb + BN_GS - 1) / BN_GS) * 2 * C;
 }
+
+// ticket counters needed by one BN reduction launch over C channels (zeroed once, self-resetting)
+RK_API int rk_bn_counters(int C) { return (C + BN_CT - 1) / BN_CT * BN_CNT; }
 
 // x: [R][C] (dt 0 f32 / 1 bf16). Training statistics + fused scale/shift + running stats.
 RK_API int rk_bn_stats(int dt, const void* x, int64_t R, int C, const float* gamma, const float* beta, float* mean,
@@ -622,13 +661,15 @@ static int bn_elem_rows(int64_t R, int C, int* grid) {
   return (int)per;
 }
 
-// y = relu?(x*scale + shift + res?); dt: x dtype, dto: y/res dtype
+// y = relu?(x*scale + shift + res?); dt: x dtype, dto: y/res dtype.  mask (uint8 [R][C/8], may be
+// null): the ReLU mask bits for rk_bn_bwd.
 RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const float* scale, const float* shift, void* y,
-                       int64_t R, int C, int relu, hipStream_t s) {
+                       void* mask, int64_t R, int C, int relu, hipStream_t s) {
   if (C % 8 || C > 8 * BN_T || R <= 0) return (int)hipErrorInvalidValue;
   int grid;
   const int rpb = bn_elem_rows(R, C, &grid);
-#define RK_BA(T, TO) bn_apply_kernel<T, TO><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y, R, C, relu, rpb)
+#define RK_BA(T, TO) bn_apply_kernel<T, TO><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y, \
+                                                            relu ? (uint8_t*)mask : nullptr, R, C, relu, rpb)
   if (dt == BF16 && dto == BF16) RK_BA(uint16_t, uint16_t);
   else if (dt == BF16) RK_BA(uint16_t, float);
   else if (dto == BF16) RK_BA(float, uint16_t);
@@ -637,12 +678,13 @@ RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const fl
   return (int)hipGetLastError();
 }
 
-// backward. dt: x/dx dtype; dto: dy/y/dres dtype. y (mask) may be null, dres may be null.
-RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void* y, int64_t R, int C,
+// backward. dt: x/dx dtype; dto: dy/dres dtype. mask (fused-ReLU bits from rk_bn_apply) may be
+// null, dres may be null.
+RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void* mask, int64_t R, int C,
                      const float* mean, const float* invstd, const float* scale, float* dgamma, float* dbeta, void* dx,
                      void* dres, float* ws, float* coef /*[3C]*/, unsigned* counters, hipStream_t s) {
   if (C % 8 || C > 8 * BN_T || R <= 0) return (int)hipErrorInvalidValue;
-  BnBwdArgs a{dy, x, y, R, C, 0, mean, invstd, ws, counters, dgamma, dbeta, scale, coef};
+  BnBwdArgs a{dy, x, (const uint8_t*)mask, R, C, 0, mean, invstd, ws, counters, dgamma, dbeta, scale, coef};
   const int rb = bn_grid_rows(R, C, &a.rpb);
   dim3 grid((C + BN_CT - 1) / BN_CT, rb);
   int eg;
@@ -650,7 +692,8 @@ RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void*
 #define RK_BB(T, TO)                                                                                               \
   do {                                                                                                             \
     bn_bwd_reduce_kernel<T, TO><<<grid, BN_T, 0, s>>>(a);                                                          \
-    bn_bwd_apply_kernel<T, TO><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x, (const TO*)y, coef, (T*)dx,         \
+    bn_bwd_apply_kernel<T, TO><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x, (const uint8_t*)mask, coef,      \
+                                                   (T*)dx,                                                         \
                                                    (TO*)dres, R, C, erpb);                                         \
   } while (0)
   if (dt == BF16 && dto == BF16) RK_BB(uint16_t, uint16_t);

@@ -58,8 +58,9 @@ KERNEL_SIGS = {
     "rk_bn_workspace": (c_int64, [c_int64, c_int]),
     "rk_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int] + [c_void_p] * 9 + [c_float, c_float, c_void_p, c_void_p,
                                                                                   c_void_p]),
-    "rk_bn_apply": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
-                            c_void_p]),
+    "rk_bn_apply": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int,
+                            c_int, c_void_p]),
+    "rk_bn_counters": (c_int, [c_int]),
     "rk_bn_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int] + [c_void_p] * 11),
     "rk_ln_fwd": (c_int, [c_int, c_int] + [c_void_p] * 8 + [c_int64, c_int, c_float, c_void_p]),
     "rk_ln_workspace": (c_int64, [c_int64, c_int]),
@@ -151,7 +152,7 @@ class Workspace:
     """
 
     _per_device: dict = {}
-    SIZE = 16384  # counters are reset by their last block, so one slot per (op, call-site) suffices
+    SIZE = 65536  # counters are reset by their last block, so one slot per (op, call-site) suffices
 
     def __init__(self, device: torch.device):
         self.counters = torch.zeros(self.SIZE, dtype=torch.int32, device=device)

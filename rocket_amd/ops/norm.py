@@ -58,8 +58,8 @@ class _BNAct(torch.autograd.Function):
         y = torch.empty_like(x, dtype=out_dtype, memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
         stats = torch.empty(4, C, dtype=torch.float32, device=dev)  # mean, invstd, scale, shift
         ws = torch.empty(int(lib.rk_bn_workspace(R, C)), dtype=torch.float32, device=dev)
-        ncol = (C + 63) // 64
-        counters = _lib.Workspace.get(dev).counter_array(f"bn{ncol}", ncol)
+        nctr = int(lib.rk_bn_counters(C))
+        counters = _lib.Workspace.get(dev).counter_array(f"bn{nctr}", nctr)
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         s = _lib.stream_ptr(dev)
@@ -70,20 +70,22 @@ class _BNAct(torch.autograd.Function):
         res = None
         if residual is not None:
             res = _channels_last(residual)
+        # fused ReLU: a 1-bit [y > 0] mask (R*C/8 bytes) is all the backward needs of y
+        mask = torch.empty(R * C // 8, dtype=torch.uint8, device=dev) if relu else None
         _lib.check(lib.rk_bn_apply(_dt(x), _dt(y), xr.data_ptr(), _lib.ptr(_rows_view(res)) if res is not None else None,
-                                   stats[2].data_ptr(), stats[3].data_ptr(), _rows_view(y).data_ptr(), R, C, int(relu), s),
-                   "rk_bn_apply")
+                                   stats[2].data_ptr(), stats[3].data_ptr(), _rows_view(y).data_ptr(), _lib.ptr(mask),
+                                   R, C, int(relu), s), "rk_bn_apply")
         ctx.params = (weight, bias)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.out_dtype = out_dtype
-        ctx.save_for_backward(x, y if relu else None, stats)
+        ctx.save_for_backward(x, mask, stats)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = _lib.kernels()
-        x, y, stats = ctx.saved_tensors
+        x, mask, stats = ctx.saved_tensors
         weight, bias = ctx.params
         C = x.shape[1]
         dev = x.device
@@ -98,10 +100,9 @@ class _BNAct(torch.autograd.Function):
         dres = torch.empty_like(dy) if ctx.has_res else None
         ws = torch.empty(int(lib.rk_bn_workspace(R, C)), dtype=torch.float32, device=dev)
         coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
-        ncol = (C + 63) // 64
-        counters = _lib.Workspace.get(dev).counter_array(f"bn{ncol}", ncol)
-        _lib.check(lib.rk_bn_bwd(_dt(x), _dt(dy), dyr.data_ptr(), xr.data_ptr(),
-                                 _rows_view(y).data_ptr() if y is not None else None, R, C, stats[0].data_ptr(),
+        nctr = int(lib.rk_bn_counters(C))
+        counters = _lib.Workspace.get(dev).counter_array(f"bn{nctr}", nctr)
+        _lib.check(lib.rk_bn_bwd(_dt(x), _dt(dy), dyr.data_ptr(), xr.data_ptr(), _lib.ptr(mask), R, C, stats[0].data_ptr(),
                                  stats[1].data_ptr(), stats[2].data_ptr(), _lib.ptr(dgamma), _lib.ptr(dbeta),
                                  _rows_view(dx).data_ptr(), _rows_view(dres).data_ptr() if dres is not None else None,
                                  ws.data_ptr(), coef.data_ptr(), counters, _lib.stream_ptr(dev)), "rk_bn_bwd")
