@@ -90,7 +90,7 @@ def main():
     gb = [torch.zeros_like(b) for b in B]
     probs = ((dyT, h2T, gw[2], gb[2], 10, 84), (d2T, h1T, gw[1], gb[1], 84, 120), (d1T, xT, gw[0], gb[0], 120, 400))
     args_w = (P(*[p[0].data_ptr() for p in probs]), P(*[p[1].data_ptr() for p in probs]), P(*[p[2].data_ptr() for p in probs]), P(*[p[3].data_ptr() for p in probs]), I(*[p[4] for p in probs]), I(*[p[5] for p in probs]))
-    res["mlp3_wgrad"] = timeit(lambda: lib.rk_mlp3_wgrad(3, *args_w, N, s), args.reps)
+    res["mlp3_wgrad"] = timeit(lambda: lib.rk_mlp3_wgrad(3, *args_w, N, None, 0, 0, None, None, s), args.reps)
     from rocket_amd.ops.cross_entropy import cross_entropy
 
     lg = logits.clone().requires_grad_()

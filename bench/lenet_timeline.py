@@ -1,0 +1,95 @@
+"""Phase timeline of the fused LeNet forward / backward launches (diagnostics).
+
+    python bench/lenet_timeline.py [--batch 1024] [--steps 20]
+
+Runs fused LeNet training steps (forward, fused cross-entropy + backward) with the kernels'
+phase stamps enabled (``rk_lenet_set_trace``): thread 0 of every block records
+``s_memrealtime`` (100 MHz) at each phase boundary.  Prints, per phase, the median over blocks
+of the time since the previous stamp and of the time since the launch's earliest block start,
+averaged over the last steps — where a latency-chain kernel spends its time.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+FWD = ["start", "stage img + w1", "conv1 tiles (wave 0)", "w2 frags + sync", "a1/code1 stores", "conv2 + sync",
+       "fc1 + sync", "fc2 + sync", "fc3 (end)"]
+BWD = ["start", "wfr + CE loads + sync", "stage issue (dc2/dcT zero)", "CE softmax + sync", "fc3 dgrad + sync",
+       "fc2 dgrad + sync", "fc1 dgrad + sync", "scatter + sync", "conv2 dgrad + sync", "dW1/dW2 MFMA (wave 0)",
+       "dW2 partials out + sync", "dW1 partials out", "CE loss ticket (end)"]
+BWD_MARKS = [0, 1, 2, 3, 5, 6, 7, 8, 9, 13, 10, 11, 12]
+
+
+def summarize(tr: torch.Tensor, names, marks):
+    t = tr[:, marks].double()
+    t0 = t[:, 0].min()
+    rows = []
+    for j, k in enumerate(marks):
+        col = t[:, j]
+        since0 = float((col - t0).median()) * 10.0 / 1e3  # 100 MHz ticks -> us
+        d = float((col - t[:, j - 1]).median()) * 10.0 / 1e3 if j else float((col - t0).median()) * 10.0 / 1e3
+        rows.append({"phase": names[j], "median_us_since_prev": round(d, 2), "median_us_since_launch": round(since0, 2),
+                     "max_us_since_launch": round(float((col - t0).max()) * 10.0 / 1e3, 2)})
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    from rocket_amd import ops
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops import _lib
+    from rocket_amd.ops.lenet import fuse_cross_entropy
+
+    ops.set_fused(True)
+    lib = _lib.kernels()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    net = LeNet(fused=True).to(dev)
+    x = torch.rand(a.batch, 1, 28, 28, device=dev)
+    y = torch.randint(0, 10, (a.batch,), device=dev)
+    blocks = a.batch // 4
+    ftr = torch.zeros(blocks, 16, dtype=torch.int64, device=dev)
+    btr = torch.zeros(blocks, 16, dtype=torch.int64, device=dev)
+    lib.rk_lenet_set_trace(ftr.data_ptr(), btr.data_ptr())
+    fw, bw = [], []
+    try:
+        for step in range(a.steps):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits = net.logits(x)
+            loss, g = fuse_cross_entropy(logits, y, 1.0)
+            torch.autograd.backward([logits], [g])
+            net.zero_grad(set_to_none=False)
+            torch.cuda.synchronize()
+            if step >= a.steps // 2:
+                fw.append(summarize(ftr.cpu(), FWD, list(range(9))))
+                bw.append(summarize(btr.cpu(), BWD, BWD_MARKS))
+    finally:
+        lib.rk_lenet_set_trace(None, None)
+
+    def avg(runs):
+        out = []
+        for j in range(len(runs[0])):
+            r = dict(runs[0][j])
+            for k in ("median_us_since_prev", "median_us_since_launch", "max_us_since_launch"):
+                r[k] = round(statistics.mean(run[j][k] for run in runs), 2)
+            out.append(r)
+        return out
+
+    print(json.dumps({"kernel": "lenet_fwd", "batch": a.batch, "phases": avg(fw)}))
+    print(json.dumps({"kernel": "lenet_bwd", "batch": a.batch, "phases": avg(bw)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -75,14 +75,14 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(const T* __restrict__ logit
   float bl = block_sum(loss, red);
   float bv = block_sum(valid, red);
   if (threadIdx.x == 0) {
-    partials[2 * blockIdx.x] = bl;
-    partials[2 * blockIdx.x + 1] = bv;
+    st_sc1(partials + 2 * blockIdx.x, bl);
+    st_sc1(partials + 2 * blockIdx.x + 1, bv);
   }
   if (last_block_arrived(counter, &flag)) {
     float s = 0.f, v = 0.f;
     for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) {
-      s += partials[2 * b];
-      v += partials[2 * b + 1];
+      s += ld_sc1(partials + 2 * b);
+      v += ld_sc1(partials + 2 * b + 1);
     }
     s = block_sum(s, red);
     v = block_sum(v, red);
@@ -170,10 +170,10 @@ __global__ void __launch_bounds__(256) ce_train_kernel(const T* __restrict__ log
     if (WAVE && lane != 0) loss = 0.f;
   }
   const float bl = block_sum(loss, red);
-  if (threadIdx.x == 0) partials[blockIdx.x] = bl;
+  if (threadIdx.x == 0) st_sc1(partials + blockIdx.x, bl);
   if (last_block_arrived(counter, &flag)) {
     float sum = 0.f;
-    for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) sum += partials[b];
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) sum += ld_sc1(partials + b);
     sum = block_sum(sum, red);
     if (threadIdx.x == 0) {
       const float l = mean ? (nvalid > 0.f ? sum / nvalid : NAN) : sum;

@@ -30,8 +30,23 @@ constexpr int A1N = C1 * Q1 * Q1;  // 1176 conv1 pooled outputs per sample
 constexpr int A2N = C2 * Q2 * Q2;  // 400
 constexpr int R1 = KS * KS;        // 25  conv1 reduction
 constexpr int R2 = C1 * KS * KS;   // 150 conv2 reduction
+constexpr int K1P = KS * 6;        // 30: conv1 reduction with kw padded to 6 (fused path: pair reads)
 
 __device__ __forceinline__ __bf16 tobf(float v) { return (__bf16)v; }
+
+// Optional phase timeline (diagnostics): thread 0 of every block stamps s_memrealtime (100 MHz)
+// at phase boundaries into trace[block][16]; a null trace pointer costs one uniform branch.
+#define RK_TR(tr, k)                                                                              \
+  do {                                                                                            \
+    if ((tr) != nullptr && threadIdx.x == 0) (tr)[(int64_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
+// Elements (x, x+1) of a bf16 row held twice (c0[i] = v[i], c1[i] = v[i+1]): one aligned 4-byte
+// LDS read from c0 at even x, from c1 at x - 1 for odd x.
+__device__ __forceinline__ uint32_t pair_at(const uint16_t* c0, const uint16_t* c1, int x) {
+  const uint16_t* p = (x & 1) ? c1 + (x - 1) : c0 + x;
+  return *(const uint32_t*)p;
+}
 
 // Intra-wave LDS producer/consumer ordering: drain this wave's LDS ops and stop the compiler
 // from moving memory accesses across (lanes read what other lanes of the same wave wrote).
@@ -77,14 +92,38 @@ constexpr int OFF_F3 = OFF_F2 + 6 * 4;     // fc3 fwd: 1 x 3
 constexpr int OFF_B3 = OFF_F3 + 1 * 3;     // fc3 dgrad: 6 n-tiles (84) x 1 k-step (10)
 constexpr int OFF_B2 = OFF_B3 + 6 * 1;     // fc2 dgrad: 8 (120) x 3 (84)
 constexpr int OFF_B1 = OFF_B2 + 8 * 3;     // fc1 dgrad: 25 (400) x 4 (120)
-constexpr int NFRAG = OFF_B1 + 25 * 4;     // 261 fragments x 64 lanes x 16 B
+constexpr int OFF_C1 = OFF_B1 + 25 * 4;    // conv1 fwd B: 1 k-step (25 taps)
+constexpr int OFF_C2 = OFF_C1 + 1;         // conv2 fwd B: 7 k-steps (25 taps x 8 padded channels)
+constexpr int OFF_D2 = OFF_C2 + 7;         // conv2 dgrad B: 13 k-steps (25 taps x 16 channels)
+constexpr int NFRAG = OFF_D2 + 13;         // 282 fragments x 64 lanes x 16 B
 constexpr int A2P = 432;                   // LDS row of pooled conv2 output: data 0..399, zero 400..415, trash 424
 constexpr int A2TRASH = 424;
 constexpr int H1P = 136, H2P = 104, DYP = 40;
 
 __global__ void __launch_bounds__(64) lenet_prep_kernel(const float* __restrict__ w1, const float* __restrict__ w2,
-                                                        const float* __restrict__ w3, bf16x8* __restrict__ frag) {
+                                                        const float* __restrict__ w3, const float* __restrict__ cw1,
+                                                        const float* __restrict__ cw2, bf16x8* __restrict__ frag) {
   const int f = blockIdx.x, lane = threadIdx.x, lo = lane & 15, hi = lane >> 4;
+  bf16x8 v;
+  if (f >= OFF_C1) {  // conv B fragments (the layouts the conv phases used to gather per block)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = 0.f;
+      if (f == OFF_C1) {  // B[k = (kh, kw) = (k / 6, k % 6), kw padded 5 -> 6][col = co lo], k = 8hi + j
+        const int k = 8 * hi + j, kh = k / 6, kw = k % 6;
+        if (lo < C1 && k < K1P && kw < KS) x = cw1[lo * R1 + kh * KS + kw];
+      } else if (f < OFF_D2) {  // B[k = (tap kk = 4s + hi, ci = j)][col = co lo]
+        const int kk = 4 * (f - OFF_C2) + hi;
+        if (kk < R1 && j < C1) x = cw2[(lo * C1 + j) * R1 + kk];
+      } else {  // dgrad B[k = (tap 2s + hi/2, co = 8(hi&1) + j)][col = ci lo]
+        const int kk = 2 * (f - OFF_D2) + (hi >> 1), co = 8 * (hi & 1) + j;
+        if (kk < R1 && lo < C1) x = cw2[(co * C1 + lo) * R1 + kk];
+      }
+      v[j] = (__bf16)x;
+    }
+    frag[f * 64 + lane] = v;
+    return;
+  }
   const float* W;
   int nout, nin, tile, ks, bwd;
   if (f < OFF_F2) { W = w1; nout = F1; nin = F0; tile = (f - OFF_F1) / 13; ks = (f - OFF_F1) % 13; bwd = 0; }
@@ -93,7 +132,6 @@ __global__ void __launch_bounds__(64) lenet_prep_kernel(const float* __restrict_
   else if (f < OFF_B2) { W = w3; nout = F3; nin = F2; tile = f - OFF_B3; ks = 0; bwd = 1; }
   else if (f < OFF_B1) { W = w2; nout = F2; nin = F1; tile = (f - OFF_B2) / 3; ks = (f - OFF_B2) % 3; bwd = 1; }
   else { W = w1; nout = F1; nin = F0; tile = (f - OFF_B1) / 4; ks = (f - OFF_B1) % 4; bwd = 1; }
-  bf16x8 v;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int a = bwd ? 32 * ks + 8 * hi + j : 16 * tile + lo;  // output-feature row of W
@@ -129,7 +167,7 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
 constexpr int A1CL = Q1 * Q1 * 8;  // channel-last conv1 output: [pixel][8 channels], 6 used
 
 struct FwdSmem {
-  float img[SPB][IMGN + 4];
+  uint16_t imgb[SPB][2][IMGN + 8];  // bf16 image, two copies for pair reads (see BwdSmem)
   uint16_t a1cl[SPB][A1CL + 16];  // zero pixel at A1CL (8 zeros), trash lanes at A1CL+8
   uint16_t a1[SPB][A1N + 8];  // zero slot at A1N, trash at A1N+4
   uint8_t c1[SPB][A1N + 8];
@@ -145,6 +183,7 @@ struct ClsFwd {  // classifier operands of the fused forward
   const float *fb1, *fb2, *fb3;
   uint16_t *a2T, *h1T, *h2T;  // transposed activations [features][N] for the weight gradients
   float* logits;              // [N][10]
+  uint64_t* trace;            // optional phase timeline [blocks][16]
 };
 
 template <bool MLP>
@@ -154,20 +193,32 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
                                                        uint8_t* __restrict__ code1, uint16_t* __restrict__ a2g,
                                                        uint8_t* __restrict__ code2, int N, ClsFwd cf) {
   __shared__ __attribute__((aligned(16))) FwdSmem sm;
+  RK_TR(cf.trace, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // conv B operands: the fused path loads the prep kernel's fragments first thing (one 16-byte
+  // load per k-step, latency hidden behind the image staging); the generic path gathers them
+  bf16x8 bw1, bw2[7];
+  if constexpr (MLP) {
+    bw1 = cf.frag[OFF_C1 * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) bw2[s] = cf.frag[(OFF_C2 + s) * 64 + lane];
+  }
   const int slot = wave / WPS, sw = wave % WPS, st = threadIdx.x % (64 * WPS);  // st: thread in sample group
   const int n = blockIdx.x * SPB + slot;
   const bool live = n < N;
   const int nc = live ? n : 0;
-  float* img = sm.img[slot];
+  uint16_t* img0 = sm.imgb[slot][0];
+  uint16_t* img1 = sm.imgb[slot][1];
   uint16_t* a1 = sm.a1[slot];
   uint8_t* c1 = sm.c1[slot];
 
-  for (int i = st; i < IMGN + 4; i += 64 * WPS) {
+  for (int i = st; i < IMGN + 8; i += 64 * WPS) {
     const int r = i / IMGS - 2, c = i % IMGS - 2;
     const bool in = i < IMGN && r >= 0 && r < IMG && c >= 0 && c < IMG;
     const float v = x[(int64_t)nc * IMG * IMG + (in ? r * IMG + c : 0)];
-    img[i] = in ? v : 0.f;
+    const uint16_t u = f2bf(in ? v : 0.f);
+    img0[i] = u;
+    if (i > 0) img1[i - 1] = u;
   }
   if (st < 8) a1[A1N + st] = 0;
   if (st < 16) sm.a1cl[slot][A1CL + st] = 0;
@@ -176,25 +227,40 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     for (int i = threadIdx.x; i < A2P; i += NTHR) sm.zrow[i] = 0;
   }
   const int hi = lane >> 4, lo = lane & 15;
-  bf16x8 bw1;
   int koff1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int r = 8 * hi + j;
-    const bool ok = lo < C1 && r < R1;
-    const float v = w1[ok ? lo * R1 + r : 0];
-    bw1[j] = tobf(ok ? v : 0.f);
+    if constexpr (!MLP) {
+      const bool ok = lo < C1 && r < R1;
+      const float v = w1[ok ? lo * R1 + r : 0];
+      bw1[j] = tobf(ok ? v : 0.f);
+    }
     koff1[j] = r < R1 ? (r / KS) * IMGS + (r % KS) : -100000;
+  }
+  int koffp[4];  // fused path: pair q covers taps k = 8hi + 2q, +1 of the kw-padded-to-6 order
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = 8 * hi + 2 * q;
+    koffp[q] = k < K1P ? (k / 6) * IMGS + (k % 6) : -100000;
   }
   const float bias1 = b1[lo < C1 ? lo : 0];
   __syncthreads();
+  RK_TR(cf.trace, 1);
 
   // ---- conv1: 49 tiles of 16 rows (4 windows x 4 positions), split over the sample's 4 waves
   for (int t = sw; t < 49; t += WPS) {
     const int pos = pos1(4 * t + (lo >> 2), lo & 3);
     bf16x8 a;
+    if constexpr (MLP) {  // taps ordered (kh, kw) with kw padded to 6: 4 aligned pair reads per lane
+      uint32_t w4[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = tobf(img[koff1[j] >= 0 ? pos + koff1[j] : IMGZ]);
+      for (int q = 0; q < 4; ++q) w4[q] = pair_at(img0, img1, koffp[q] >= 0 ? pos + koffp[q] : IMGZ);
+      a = __builtin_bit_cast(bf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = __builtin_bit_cast(__bf16, img0[koff1[j] >= 0 ? pos + koff1[j] : IMGZ]);
+    }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw1, acc, 0, 0, 0);
     float m = acc[0];
@@ -216,18 +282,21 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
   // conv2 operands, reduction ordered k = (kh*5 + kw)*8 + ci (ci padded 6 -> 8): a lane's 8
   // consecutive k are the 8 channels of one pixel of the channel-last image = ONE 16-byte read.
   // 200 -> 7 k-steps; lane (hi) covers (kh,kw) pair kk = 4s + hi.
-  bf16x8 bw2[7];
+  RK_TR(cf.trace, 2);
+  if constexpr (!MLP) {
 #pragma unroll
-  for (int s = 0; s < 7; ++s)
+    for (int s = 0; s < 7; ++s)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int kk = 4 * s + hi;
-      const bool ok = kk < R1 && j < C1;
-      const float v = w2[ok ? (lo * C1 + j) * R1 + kk : 0];
-      bw2[s][j] = tobf(ok ? v : 0.f);
-    }
+      for (int j = 0; j < 8; ++j) {
+        const int kk = 4 * s + hi;
+        const bool ok = kk < R1 && j < C1;
+        const float v = w2[ok ? (lo * C1 + j) * R1 + kk : 0];
+        bw2[s][j] = tobf(ok ? v : 0.f);
+      }
+  }
   const float bias2 = b2[lo];
   __syncthreads();
+  RK_TR(cf.trace, 3);
   if (live) {
     for (int i = st * 8; i < A1N; i += 64 * WPS * 8) {
       *(uint4*)(a1g + (int64_t)n * A1N + i) = *(const uint4*)(a1 + i);
@@ -235,6 +304,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     }
   }
 
+  RK_TR(cf.trace, 4);
   // ---- conv2: 25 windows -> 7 tiles, split over the 4 waves
   for (int t = sw; t < 7; t += WPS) {
     const int w = 4 * t + (lo >> 2);
@@ -265,6 +335,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     sm.c2[slot][o] = on ? (uint8_t)arg : 0xFF;
   }
   __syncthreads();
+  RK_TR(cf.trace, 5);
   if (live) {
     for (int i = st * 8; i < A2N; i += 64 * WPS * 8) {
       if (!MLP) *(uint4*)(a2g + (int64_t)n * A2N + i) = *(const uint4*)(sm.a2[slot] + i);
@@ -294,6 +365,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
       if (threadIdx.x - 512 < SPB * 8) sm.h1[(threadIdx.x - 512) >> 3][128 + ((threadIdx.x - 512) & 7)] = 0;
     }
     __syncthreads();
+    RK_TR(cf.trace, 6);
     if (wave < 6) {  // fc2: 6 n-tiles x 4 k-steps
       const f32x4 acc = cls_tile<4>(&sm.h1[0][0], H1P, sm.zrow, cf.frag, OFF_F2 + wave * 4, lane);
       if (hi == 0) {
@@ -309,6 +381,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
       }
     }
     __syncthreads();
+    RK_TR(cf.trace, 7);
     if (wave == 0) {  // fc3: 1 n-tile x 3 k-steps -> fp32 logits
       const f32x4 acc = cls_tile<3>(&sm.h2[0][0], H2P, sm.zrow, cf.frag, OFF_F3, lane);
       if (hi == 0 && lo < F3) {
@@ -317,6 +390,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
         for (int i = 0; i < 4; ++i) cf.logits[(int64_t)(n0 + i) * F3 + lo] = acc[i] + bb;
       }
     }
+    RK_TR(cf.trace, 8);
   }
 }
 
@@ -327,23 +401,33 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
 //  phase B  conv2 dgrad as a GATHER implicit GEMM: dX2[pixel][ci] = sum_{co,kh,kw}
 //           dConv2[co][ih+4-kh][iw+4-kw] . W2[co][ci][kh][kw]  (13 pixel tiles x 13 k-steps per
 //           sample, all 16 waves); every output element is written by exactly one lane
-//  phase C  waves 0..9: one 16-column tile of dW2 each, reducing over the 4 samples' positions
-//           in registers; waves 10..15: dW1 (2 column tiles) over a share of the 4 x 784 positions
-//  phase D  block totals -> global f32 atomics (one per element per block)
+//  phase C  dW2: waves 0..9 one 16-column tile each (issued alongside phase B — it needs no dX2),
+//           reducing over the 4 samples' positions in registers; then dW1 (2 column tiles) on all
+//           16 waves over a share of the 4 x 784 positions
+//  phase D  block totals -> one row of a per-block gradient slab (fused path; summed by the
+//           weight-gradient launch) or global f32 atomics (generic path)
 constexpr int DC = 18;             // dConv2 image side: 10 + 2*4 zero ring
 constexpr int DCN = DC * DC * C2;  // 5184, channel-last [y][x][co]; zero pixel at DCN
 constexpr int DTS = 128;           // row stride of dConv2^T [co][position] (100 used, zero padded)
 constexpr int K2P = 13;            // conv2-dgrad k-steps: (kh,kw,co) = 400 -> 416
+// fused path: per-block conv-gradient slab row [dW1 150 | db1 6 | dW2 2400 | db2 16] (+pad)
+constexpr int SL_W1 = 0, SL_B1 = SL_W1 + C1 * R1, SL_W2 = SL_B1 + C1, SL_B2 = SL_W2 + C2 * R2;
+constexpr int SLABN = SL_B2 + C2;  // 2572
+constexpr int SLABW = 2576;
 
 struct BwdSmem {
-  float img[SPB][IMGN + 4];  // + zero slot
+  // bf16 image in two copies: [0][i] = img[i], [1][i] = img[i + 1], so any pair (x, x+1) is ONE
+  // aligned 4-byte read (copy x & 1 at x & ~1) — the dW1 B operand is 4 pair reads per fragment.
+  // Zero pair at [0][IMGZ].
+  uint16_t imgb[SPB][2][IMGN + 8];
   float dx2[SPB][A1N + 4];          // dL/d a1 (conv2 input gradient)
   uint16_t a1[SPB][A1N + 8];        // + zero slot at A1N
+  uint16_t a1o[SPB][A1N + 8];       // a1 shifted by one element (pair reads for the dW2 B operand)
   uint8_t c1[SPB][A1N + 8];         // + never-matching slot at A1N
   uint16_t dc2[SPB][DCN + 16];      // dense channel-last dConv2 with zero ring; zero pixel at DCN
+                                    // (after phase B: the 16 waves' dW1 partials [16][2][256] f32)
   uint16_t dcT[SPB][C2 * DTS];      // dConv2^T [co][p = 4*window + quadrant] (wgrad2 A operand)
-  float red1[6][2][256];            // dW1 partials of waves 10..15
-  float rb1[6][16];
+  float rb1[NTHR / 64][16];         // db1 partials of the 16 waves (their dW1 partials alias dc2)
   bf16x8 wfr[K2P * 64];             // conv2-dgrad B fragments
   // fused classifier backward (MLP=true): gradients of the 4 samples as MFMA A rows
   uint16_t dyl[SPB][DYP];           // dlogits, K pad 10..39 zero
@@ -357,6 +441,8 @@ struct BwdSmem {
   float cecnt[NTHR / 64];  // fused CE: valid-target count per wave (waves 1..15)
   int flag;
 };
+static_assert(sizeof(((BwdSmem*)nullptr)->dc2) >= (NTHR / 64) * 2 * 256 * sizeof(float),
+              "dW1 partials alias dc2");
 
 struct ClsBwd {
   const bf16x8* frag;
@@ -379,6 +465,8 @@ struct ClsBwd {
   int ring_size;
   float acc_scale;
   int sync;
+  uint64_t* trace;                  // optional phase timeline [blocks][16]
+  float* slab;                      // [blocks][SLABW] conv weight/bias gradient partials
 };
 
 template <bool MLP>
@@ -390,6 +478,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
                                                        float* __restrict__ db1, float* __restrict__ dw2,
                                                        float* __restrict__ db2, int N, int rounds, ClsBwd cb) {
   __shared__ __attribute__((aligned(16))) BwdSmem sm;
+  RK_TR(cb.trace, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int hi = lane >> 4, lo = lane & 15;
 
@@ -397,6 +486,9 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
   // consecutive k share (kh, kw) and step co by 1: gather offsets are base + j*DC*DC.
   // B operand B[k][col = ci] = w2[co][ci][kh][kw]: 13 k-steps, lanes lo < 6.
   // kept in LDS in fragment order (wfr[s*64 + lane]), one ds_read_b128 per k-step
+  if constexpr (MLP) {
+    for (int i = threadIdx.x; i < K2P * 64; i += NTHR) sm.wfr[i] = cb.frag[OFF_D2 * 64 + i];
+  } else
   for (int i = threadIdx.x; i < K2P * 64; i += NTHR) {
     const int s = i >> 6, l = i & 63, h = l >> 4, c = l & 15;
     bf16x8 v;
@@ -433,6 +525,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
       }
     }
     __syncthreads();
+    RK_TR(cb.trace, 1);
     // ---- phase A: stage
     for (int i = threadIdx.x; i < SPB * IMGN; i += NTHR) {
       const int sl = i / IMGN, e = i % IMGN;
@@ -440,12 +533,21 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
       const int r = e / IMGS - 2, c = e % IMGS - 2;
       const bool in = n < N && r >= 0 && r < IMG && c >= 0 && c < IMG;
       const float v = x[(int64_t)(n < N ? n : 0) * IMG * IMG + (in ? r * IMG + c : 0)];
-      sm.img[sl][e] = in ? v : 0.f;
+      const uint16_t u = f2bf(in ? v : 0.f);
+      sm.imgb[sl][0][e] = u;
+      if (e > 0) sm.imgb[sl][1][e - 1] = u;
     }
     for (int i = threadIdx.x; i < SPB * (A1N / 8); i += NTHR) {
       const int sl = i / (A1N / 8), e = (i % (A1N / 8)) * 8;
       const int n = nbase + sl, nc = n < N ? n : 0;
-      *(uint4*)(sm.a1[sl] + e) = *(const uint4*)(a1g + (int64_t)nc * A1N + e);
+      const uint4 v = *(const uint4*)(a1g + (int64_t)nc * A1N + e);
+      *(uint4*)(sm.a1[sl] + e) = v;
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // a1o[e - 1 + j] = a1[e + j]
+        if (e + 2 * k > 0) sm.a1o[sl][e + 2 * k - 1] = (uint16_t)(w[k] & 0xffff);
+        sm.a1o[sl][e + 2 * k] = (uint16_t)(w[k] >> 16);
+      }
       *(uint2*)(sm.c1[sl] + e) = *(const uint2*)(code1g + (int64_t)nc * A1N + e);
     }
     for (int i = threadIdx.x; i < SPB * (DCN + 16) / 8; i += NTHR) {  // zero dc2 (16-byte stores)
@@ -456,6 +558,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
       const int sl = i / (C2 * DTS / 8), e = (i % (C2 * DTS / 8)) * 8;
       *(uint4*)(sm.dcT[sl] + e) = make_uint4(0, 0, 0, 0);
     }
+    RK_TR(cb.trace, 2);
     // the classifier chain runs while the conv operands above are still in flight
     if constexpr (MLP) {
       // ---- classifier input-gradient chain (host guarantees N % 8 == 0: 4 live samples)
@@ -486,6 +589,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
           if (lane == 0) sm.cecnt[wave] = ce_cnt;
         }
         __syncthreads();
+        RK_TR(cb.trace, 3);
         if (threadIdx.x < SPB * DYP || (threadIdx.x >= 256 && threadIdx.x < 256 + F3)) {
           float nv = 0.f;
 #pragma unroll
@@ -511,6 +615,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
           *(uint2*)(cb.dyT + (int64_t)o * N + nbase) = pack4(d[0], d[F3], d[2 * F3], d[3 * F3]);
         }
         __syncthreads();
+      RK_TR(cb.trace, 4);
       }
       if (wave < 6) {  // fc3 dgrad: d2 = (dy W3) * [h2 > 0]
         const f32x4 acc = cls_tile<1>(&sm.dyl[0][0], DYP, sm.zrow, cb.frag, OFF_B3 + wave, lane);
@@ -528,6 +633,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
         }
       }
       __syncthreads();
+      RK_TR(cb.trace, 5);
       if (wave < 8) {  // fc2 dgrad: d1 = (d2 W2) * [h1 > 0]
         const f32x4 acc = cls_tile<3>(&sm.d2l[0][0], H2P, sm.zrow, cb.frag, OFF_B2 + wave * 3, lane);
         if (hi == 0) {
@@ -544,6 +650,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
         }
       }
       __syncthreads();
+      RK_TR(cb.trace, 6);
       for (int t = wave; t < 25; t += 16) {  // fc1 dgrad: da2 = d1 W1 (400 outputs = 25 tiles)
         const f32x4 acc = cls_tile<4>(&sm.d1l[0][0], H1P, sm.zrow, cb.frag, OFF_B1 + t * 4, lane);
         if (hi == 0) {
@@ -553,6 +660,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
       }
     }
     __syncthreads();
+    RK_TR(cb.trace, 7);
     for (int i = threadIdx.x; i < SPB * A2N; i += NTHR) {  // scatter the pooled gradients
       const int sl = i / A2N, e = i % A2N, co = e / 25, w = e % 25;
       const int n = nbase + sl, nc = n < N ? n : 0;
@@ -567,45 +675,19 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
     if (threadIdx.x < SPB * 8) {
       const int sl = threadIdx.x >> 3, k = threadIdx.x & 7;
       sm.a1[sl][A1N + k] = 0;
+      sm.a1o[sl][A1N - 1 + k] = 0;
       sm.c1[sl][A1N + k] = 0xFE;
-      if (k < 4) sm.img[sl][IMGN + k] = 0.f;
+      sm.imgb[sl][0][IMGN + k] = 0;
+      sm.imgb[sl][1][IMGN - 1 + k] = 0;
     }
     __syncthreads();
+    RK_TR(cb.trace, 8);
 
-    // ---- phase B: conv2 dgrad, 4 samples x 13 pixel tiles, round-robin over the 16 waves
-    for (int tt = wave; tt < SPB * 13; tt += 16) {
-      const int sl = tt / 13, t = tt % 13;
-      const int pix = 16 * t + lo;  // A row of this lane
-      const bool pv = pix < Q1 * Q1;
-      const int ih = pv ? pix / Q1 : 0, iw = pv ? pix % Q1 : 0;
-      const int base = ih * DC + iw;  // pixel (ih, iw) reads dConv2 pixel (ih + 4 - kh, iw + 4 - kw)
-      const uint16_t* dc = sm.dc2[sl];
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int s = 0; s < K2P; ++s) {
-        const int kk = 2 * s + (hi >> 1);  // (kh, kw) pair of this lane's 8 k values (8 channels)
-        const bool ok = pv && kk < R1;
-        const int px = ok ? base + (4 - kk / KS) * DC + (4 - kk % KS) : DC * DC;  // DC*DC -> zero pixel
-        const bf16x8 a = *(const bf16x8*)(dc + px * C2 + 8 * (hi & 1));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, sm.wfr[s * 64 + lane], acc, 0, 0, 0);
-      }
-      // C[row = pixel 16t + 4hi + i][col = ci = lo]
-      if (lo < C1) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int p = 16 * t + 4 * hi + i;
-          if (p < Q1 * Q1) sm.dx2[sl][lo * (Q1 * Q1) + p] = acc[i];
-        }
-      }
-    }
-    __syncthreads();
-
-    // ---- phase C (accumulators live only from here to the per-round flush: nothing is held in
-    // registers across the classifier chain)
+    // ---- phase B: conv2 dgrad (4 samples x 13 pixel tiles) and dW2 (10 column tiles), which
+    // needs only dcT and a1: waves 0..9 take one dW2 tile + one dgrad tile, waves 10..15 seven
+    // dgrad tiles each (LDS-bound work split evenly; dW1, which needs dx2, follows on all waves)
     float accb2 = 0.f;                       // waves 0..9: db2 partial (lane lo = co)
     f32x4 g2 = {0.f, 0.f, 0.f, 0.f};         // waves 0..9: dW2 tile u = wave
-    f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    float sb1 = 0.f;
     if (wave < 10) {
       // dW2 tile u = wave: rows co (16), cols r = 16u + lo; K = positions of 4 samples (4 x 4 k-steps)
       const int u = wave;
@@ -613,6 +695,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
       const int cof = r < R2 ? (r / R1) * (Q1 * Q1) + ((r / KS) % KS) * Q1 + (r % KS) : -100000;
       for (int sl = 0; sl < SPB; ++sl) {
         const uint16_t* a1s = sm.a1[sl];
+        const uint16_t* a1os = sm.a1o[sl];
 #pragma unroll 2
         for (int ks = 0; ks < 4; ++ks) {
           // positions p = 32ks + 8hi + j, window-major: windows wa = 8ks+2hi (j<4), wa+1 (j>=4)
@@ -620,26 +703,73 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
           const int wa = 8 * ks + 2 * hi, wb = wa + 1;
           const int pa = wa < Q2 * Q2 && cof >= 0 ? pos2(wa, 0) + cof : -100000;
           const int pb = wb < Q2 * Q2 && cof >= 0 ? pos2(wb, 0) + cof : -100000;
-          bf16x8 b;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            accb2 += (float)a[j];
-            const int ofs = (j < 4 ? pa : pb) + ((j & 3) >> 1) * Q1 + (j & 1);
-            b[j] = __builtin_bit_cast(__bf16, a1s[ofs >= 0 ? ofs : A1N]);  // B[k = p][col = r]
+          for (int j = 0; j < 8; ++j) accb2 += (float)a[j];
+          // B[k = p][col = r]: element j at (j<4 ? pa : pb) + ((j&3)>>1)*Q1 + (j&1) = 4 pairs
+          uint32_t w4[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int xq = (k < 2 ? pa : pb) + (k & 1) * Q1;
+            w4[k] = pair_at(a1s, a1os, xq >= 0 ? xq : A1N);
           }
+          const bf16x8 b = __builtin_bit_cast(bf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
           g2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, g2, 0, 0, 0);
         }
       }
-    } else {
-      // dW1: 6 waves split the 4 x 25 k-steps (positions of the 14x14 pool grid)
-      const int wi = wave - 10;
+    }
+    {
+      constexpr int NDG = SPB * 13, NHEAVY = 42;  // dgrad tiles; [0, 42) -> waves 10..15
+      const int t_begin = wave >= 10 ? wave - 10 : NHEAVY + wave;
+      const int t_step = wave >= 10 ? 6 : 10;
+      const int t_end = wave >= 10 ? NHEAVY : NDG;
+      // fused path: this lane's B fragments read from LDS once per wave, not once per tile (the
+      // generic multi-round variant keeps re-reading them: registers would spill there)
+      bf16x8 wr[MLP ? K2P : 1];
+      if constexpr (MLP) {
+#pragma unroll
+        for (int s = 0; s < K2P; ++s) wr[s] = sm.wfr[s * 64 + lane];
+      }
+      for (int tt = t_begin; tt < t_end; tt += t_step) {
+        const int sl = tt / 13, t = tt % 13;
+        const int pix = 16 * t + lo;  // A row of this lane
+        const bool pv = pix < Q1 * Q1;
+        const int ih = pv ? pix / Q1 : 0, iw = pv ? pix % Q1 : 0;
+        const int base = ih * DC + iw;  // pixel (ih, iw) reads dConv2 pixel (ih + 4 - kh, iw + 4 - kw)
+        const uint16_t* dc = sm.dc2[sl];
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < K2P; ++s) {
+          const int kk = 2 * s + (hi >> 1);  // (kh, kw) pair of this lane's 8 k values (8 channels)
+          const bool ok = pv && kk < R1;
+          const int px = ok ? base + (4 - kk / KS) * DC + (4 - kk % KS) : DC * DC;  // DC*DC -> zero pixel
+          const bf16x8 a = *(const bf16x8*)(dc + px * C2 + 8 * (hi & 1));
+          if constexpr (MLP) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wr[s], acc, 0, 0, 0);
+          else acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, sm.wfr[s * 64 + lane], acc, 0, 0, 0);
+        }
+        // C[row = pixel 16t + 4hi + i][col = ci = lo]
+        if (lo < C1) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int p = 16 * t + 4 * hi + i;
+            if (p < Q1 * Q1) sm.dx2[sl][lo * (Q1 * Q1) + p] = acc[i];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    RK_TR(cb.trace, 9);
+
+    // ---- phase C: dW1 on all 16 waves (4 x 25 k-steps over the positions of the 14x14 pool grid)
+    f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    float sb1 = 0.f;
+    {
       int cw[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int r = 16 * u + lo;
         cw[u] = r < R1 ? (r / KS) * IMGS + (r % KS) : -100000;
       }
-      for (int it = wi; it < SPB * 25; it += 6) {
+      for (int it = wave; it < SPB * 25; it += NTHR / 64) {
         const int sl = it / 25, ks = it % 25;
         const int wa = 8 * ks + 2 * hi, wb = wa + 1;  // this lane's 2 windows (j<4 / j>=4)
         const bool va = lo < C1 && wa < Q1 * Q1, vb = lo < C1 && wb < Q1 * Q1;
@@ -656,61 +786,78 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          bf16x8 b;
+          uint32_t w4[4];  // element j at (j<4 ? pa : pb) + ((j&3)>>1)*IMGS + (j&1) + cw: 4 pairs
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int ofs = (j < 4 ? pa : pb) + ((j & 3) >> 1) * IMGS + (j & 1) + cw[u];
-            b[j] = tobf(sm.img[sl][ofs >= 0 ? ofs : IMGZ]);
+          for (int k = 0; k < 4; ++k) {
+            const int xq = (k < 2 ? pa : pb) + (k & 1) * IMGS + cw[u];
+            w4[k] = pair_at(sm.imgb[sl][0], sm.imgb[sl][1], xq >= 0 ? xq : IMGZ);
           }
+          const bf16x8 b = __builtin_bit_cast(bf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
           g1[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, g1[u], 0, 0, 0);
         }
       }
     }
 
-    // ---- phase D: block totals -> global atomics
+    RK_TR(cb.trace, 13);
+    // ---- phase D: block totals -> the fused path stores them as one row of the [blocks][SLABW]
+    // gradient slab (summed by the weight-gradient launch that follows: no contended atomics);
+    // the generic path adds them to the gradients with global atomics
+    float* srow = MLP ? cb.slab + (int64_t)blockIdx.x * SLABW : nullptr;
     if (wave < 10) {
       const int u = wave, col = 16 * u + lo;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (col < R2) atomicAdd(dw2 + (4 * hi + i) * R2 + col, g2[i]);
+        if (col < R2) {
+          if (MLP) srow[SL_W2 + (4 * hi + i) * R2 + col] = g2[i];
+          else atomicAdd(dw2 + (4 * hi + i) * R2 + col, g2[i]);
+        }
       if (u == 0) {  // db2[co]: lanes lo, lo+16, lo+32, lo+48 hold parts of channel lo
         accb2 += __shfl_xor(accb2, 16, 64);
         accb2 += __shfl_xor(accb2, 32, 64);
-        if (hi == 0 && db2) atomicAdd(db2 + lo, accb2);
+        if (hi == 0) {
+          if (MLP) srow[SL_B2 + lo] = accb2;
+          else if (db2) atomicAdd(db2 + lo, accb2);
+        }
       }
-    } else {
-      const int wi = wave - 10;
+    }
+    {  // dW1 partials of all 16 waves -> LDS (aliasing dc2: dead since phase B's barrier)
+      float (*red1)[2][256] = (float (*)[2][256])&sm.dc2[0][0];
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sm.red1[wi][u][(4 * hi + i) * 16 + lo] = g1[u][i];
+        for (int i = 0; i < 4; ++i) red1[wave][u][(4 * hi + i) * 16 + lo] = g1[u][i];
       sb1 += __shfl_xor(sb1, 16, 64);
       sb1 += __shfl_xor(sb1, 32, 64);
-      if (hi == 0) sm.rb1[wi][lo] = sb1;
+      if (hi == 0) sm.rb1[wave][lo] = sb1;
     }
     __syncthreads();
+    RK_TR(cb.trace, 10);
     for (int e = threadIdx.x; e < 2 * 256; e += NTHR) {
       const int u = e >> 8, row = (e & 255) >> 4, col = 16 * u + (e & 15);
       if (row < C1 && col < R1) {
+        const float (*red1)[2][256] = (const float (*)[2][256])&sm.dc2[0][0];
         float v = 0.f;
 #pragma unroll
-        for (int w = 0; w < 6; ++w) v += sm.red1[w][u][e & 255];
-        atomicAdd(dw1 + row * R1 + col, v);
+        for (int w = 0; w < NTHR / 64; ++w) v += red1[w][u][e & 255];
+        if (MLP) srow[SL_W1 + row * R1 + col] = v;
+        else atomicAdd(dw1 + row * R1 + col, v);
       }
     }
-    if (threadIdx.x < C1 && db1) {
+    if (threadIdx.x < C1) {
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < 6; ++w) v += sm.rb1[w][threadIdx.x];
-      atomicAdd(db1 + threadIdx.x, v);
+      for (int w = 0; w < NTHR / 64; ++w) v += sm.rb1[w][threadIdx.x];
+      if (MLP) srow[SL_B1 + threadIdx.x] = v;
+      else if (db1) atomicAdd(db1 + threadIdx.x, v);
     }
+  RK_TR(cb.trace, 11);
   }
   if constexpr (MLP) {
     if (cb.ce) {  // batch loss: block partials -> last block -> loss + Loss-capsule bookkeeping
-      if (threadIdx.x == 0) cb.partials[blockIdx.x] = sm.lossp[0];
+      if (threadIdx.x == 0) st_sc1(cb.partials + blockIdx.x, sm.lossp[0]);
       if (last_block_arrived(cb.counter, &sm.flag)) {
         float t = 0.f;
-        for (int i = threadIdx.x; i < (int)gridDim.x; i += NTHR) t += cb.partials[i];
+        for (int i = threadIdx.x; i < (int)gridDim.x; i += NTHR) t += ld_sc1(cb.partials + i);
         t = block_sum(t, sm.red);
         if (threadIdx.x == 0) {
           float nv = 0.f;
@@ -731,6 +878,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
         }
         reset_counter(cb.counter);
       }
+      RK_TR(cb.trace, 12);
     }
   }
 }
@@ -745,9 +893,10 @@ RK_API int rk_lenet_conv_fwd(const float* x, const float* w1, const float* b1, c
   return (int)hipGetLastError();
 }
 
-// fc weights (fp32 master) -> bf16 MFMA fragment table (NFRAG x 64 x 16 B)
-RK_API int rk_lenet_prep(const float* fc1w, const float* fc2w, const float* fc3w, void* frag, hipStream_t s) {
-  lenet_prep_kernel<<<NFRAG, 64, 0, s>>>(fc1w, fc2w, fc3w, (bf16x8*)frag);
+// fc + conv weights (fp32 masters) -> bf16 MFMA fragment table (NFRAG x 64 x 16 B)
+RK_API int rk_lenet_prep(const float* fc1w, const float* fc2w, const float* fc3w, const float* conv1w,
+                         const float* conv2w, void* frag, hipStream_t s) {
+  lenet_prep_kernel<<<NFRAG, 64, 0, s>>>(fc1w, fc2w, fc3w, conv1w, conv2w, (bf16x8*)frag);
   return (int)hipGetLastError();
 }
 
@@ -755,12 +904,20 @@ RK_API int rk_lenet_frag_bytes() { return NFRAG * 64 * 16; }
 
 // Whole LeNet forward (conv stack + classifier) for N % 8 == 0: logits [N][10] fp32, plus the
 // saved state of the fused backward (a1, codes) and the transposed activations of the wgrads.
+// Diagnostics: phase timelines of the fused launches ([blocks][16] u64 each, or null = off).
+static uint64_t* g_fwd_trace = nullptr;
+static uint64_t* g_bwd_trace = nullptr;
+RK_API void rk_lenet_set_trace(void* fwd, void* bwd) {
+  g_fwd_trace = (uint64_t*)fwd;
+  g_bwd_trace = (uint64_t*)bwd;
+}
+
 RK_API int rk_lenet_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                         const void* frag, const float* fb1, const float* fb2, const float* fb3, void* a1,
                         void* code1, void* code2, void* a2T, void* h1T, void* h2T, float* logits, int N,
                         hipStream_t s) {
   if (N % 8) return (int)hipErrorInvalidValue;
-  ClsFwd cf{(const bf16x8*)frag, fb1, fb2, fb3, (uint16_t*)a2T, (uint16_t*)h1T, (uint16_t*)h2T, logits};
+  ClsFwd cf{(const bf16x8*)frag, fb1, fb2, fb3, (uint16_t*)a2T, (uint16_t*)h1T, (uint16_t*)h2T, logits, g_fwd_trace};
   lenet_conv_fwd<true><<<N / SPB, NTHR, 0, s>>>(x, w1, b1, w2, b2, (uint16_t*)a1, (uint8_t*)code1, nullptr,
                                                 (uint8_t*)code2, N, cf);
   return (int)hipGetLastError();
@@ -780,8 +937,8 @@ RK_API int rk_lenet_conv_bwd(const float* x, const void* a1, const void* code1, 
 }
 
 // Fused backward for N % 8 == 0 (one block per 4 samples): classifier input-gradient chain from
-// dlogits, then the conv stack; writes dy^T, d2^T, d1^T for rk_mlp3_wgrad and ACCUMULATES the
-// conv weight/bias gradients.
+// dlogits, then the conv stack; writes dy^T, d2^T, d1^T and the conv-gradient slab for
+// rk_mlp3_wgrad, which accumulates all ten weight/bias gradients.
 struct LenetCE {  // host-side description of the fused cross-entropy (see ClsBwd)
   const float* logits;
   const int64_t* target;
@@ -797,13 +954,20 @@ struct LenetCE {  // host-side description of the fused cross-entropy (see ClsBw
   int sync;
 };
 
+// The conv weight/bias gradients are NOT accumulated here: each block writes its totals to
+// slab[block][rk_lenet_slab_width()] (N/4 rows), which rk_mlp3_wgrad then sums into dw1/db1/dw2/db2.
+RK_API int rk_lenet_slab_width() { return SLABW; }
+RK_API int rk_lenet_slab_cols() { return SLABN; }
+
 RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const void* code2, const float* w2,
                         const void* frag, const float* dy, const void* h1T, const void* h2T, void* dyT, void* d2T,
-                        void* d1T, float* dw1, float* db1, float* dw2, float* db2, int N, int rounds,
-                        const LenetCE* ce, hipStream_t s) {
+                        void* d1T, float* slab, int N, int rounds, const LenetCE* ce, hipStream_t s) {
   rounds = 1;  // the fused kernel handles one group of SPB samples per block (argument kept for ABI)
   if (N % 8 || N > 65536) return (int)hipErrorInvalidValue;
+  if (!slab) return (int)hipErrorInvalidValue;
   ClsBwd cb{};
+  cb.trace = g_bwd_trace;
+  cb.slab = slab;
   cb.frag = (const bf16x8*)frag;
   cb.dy = dy;
   cb.h1T = (const uint16_t*)h1T;
@@ -828,6 +992,7 @@ RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const
     cb.sync = ce->sync;
   }
   lenet_conv_bwd<true><<<N / (SPB * rounds), NTHR, 0, s>>>(x, (const uint16_t*)a1, (const uint8_t*)code1, nullptr,
-                                                           (const uint8_t*)code2, w2, dw1, db1, dw2, db2, N, rounds, cb);
+                                                           (const uint8_t*)code2, w2, nullptr, nullptr, nullptr,
+                                                           nullptr, N, rounds, cb);
   return (int)hipGetLastError();
 }

@@ -238,10 +238,49 @@ struct WgradProb {
   float* db;           // [N], accumulated (may be null)
   int N, K, tiles_k, tile_begin;
 };
+// optional column reduction riding on the same launch: dst[c] += sum_r slab[r][c] over the
+// [rows][width] slab of per-block partials (the fused LeNet backward's conv gradients); columns
+// [bound[i], bound[i+1]) go to dst[i] (null = dropped).
+struct SlabArgs {
+  const float* slab;
+  int rows, width, ncols, nblocks;
+  float* dst[4];
+  int bound[5];
+};
 struct WgradArgs {
   WgradProb p[3];
-  int nprob, M;
+  int nprob, M, tiles;
+  SlabArgs sl;
 };
+
+// one slab block: 64 columns x all rows; 8 row groups per block, 8 independent loads per thread
+// in flight, LDS reduce over the groups, one plain RMW per column (sole owner: deterministic)
+__device__ __forceinline__ void slab_reduce_block(const SlabArgs& s, int j, float (*red)[32 * 32]) {
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = j * 64 + cl;
+  const bool ok = c < s.ncols;
+  const float* base = s.slab + (ok ? c : 0);
+  float acc = 0.f;
+  int r = rg;
+  for (; r + 7 * NW < s.rows; r += 8 * NW) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = base[(int64_t)(r + u * NW) * s.width];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; r < s.rows; r += NW) acc += base[(int64_t)r * s.width];
+  red[rg][cl] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64 && ok) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < NW; ++g) t += red[g][threadIdx.x];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (c >= s.bound[i] && c < s.bound[i + 1] && s.dst[i]) s.dst[i][c - s.bound[i]] += t;
+  }
+}
 
 // 8 consecutive batch elements m0.. of row r of a [R][M] bf16 tensor; zero when out of range
 // (M % 8 == 0, so a group is all-in or all-out).
@@ -255,6 +294,10 @@ __device__ __forceinline__ bf16x8 rowfrag(const uint16_t* T, int R, int M, int r
 __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   __shared__ float red[NW][32 * 32];
   __shared__ float rsum[NW][32];
+  if ((int)blockIdx.x >= a.tiles) {
+    slab_reduce_block(a.sl, blockIdx.x - a.tiles, red);
+    return;
+  }
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < 3; ++i)
@@ -358,10 +401,13 @@ RK_API int rk_mlp3_dgrad(const float* dy, int N3, const float* w3, int N2, const
 }
 
 // Grouped dW_l += dT_l . xT_l^T, db_l += rowsum(dT_l) for up to 3 layers. M % 8 == 0.
+// slab (may be null): also dst[i][c - bound[i]] += sum over the slab_rows rows of slab[r][c] for
+// c in [bound[i], bound[i+1]), bound[0] = 0, c < bound[4] <= slab_width.
 RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT, float* const* dw, float* const* db,
-                         const int* Ns, const int* Ks, int M, hipStream_t s) {
+                         const int* Ns, const int* Ks, int M, const float* slab, int slab_rows, int slab_width,
+                         float* const* slab_dst, const int* slab_bound, hipStream_t s) {
   if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
-  WgradArgs a;
+  WgradArgs a{};
   a.nprob = nprob;
   a.M = M;
   int tiles = 0;
@@ -377,6 +423,18 @@ RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT
     a.p[i].tile_begin = tiles;
     if (i < nprob) tiles += ((Ns[j] + 31) / 32) * a.p[i].tiles_k;
   }
-  mlp3_wgrad_kernel<<<tiles, NT, 0, s>>>(a);
+  a.tiles = tiles;
+  int extra = 0;
+  if (slab) {
+    if (slab_rows < 1 || slab_bound[0] != 0 || slab_bound[4] > slab_width) return (int)hipErrorInvalidValue;
+    a.sl.slab = slab;
+    a.sl.rows = slab_rows;
+    a.sl.width = slab_width;
+    a.sl.ncols = slab_bound[4];
+    for (int i = 0; i < 4; ++i) a.sl.dst[i] = slab_dst[i];
+    for (int i = 0; i < 5; ++i) a.sl.bound[i] = slab_bound[i];
+    extra = (a.sl.ncols + 63) / 64;
+  }
+  mlp3_wgrad_kernel<<<tiles + extra, NT, 0, s>>>(a);
   return (int)hipGetLastError();
 }

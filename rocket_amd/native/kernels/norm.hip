@@ -88,13 +88,6 @@ __device__ __forceinline__ void reduce_rowgroups(const float* v, float (*lds)[BN
 // agent atomics), every storing wave drains vmcnt before the workgroup barrier, lane 0 takes the
 // ticket, and the reducer reads EVERY partial with sc1 loads — no L2 write-back, no L1 invalidate.
 // Fixed summation order: results are deterministic.  Counters self-reset (graph replays).
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __device__ __forceinline__ void bn_sum_parts(const float* part, int C, int c0, int b0, int b1, float& t1,
                                              float& t2) {
   const int ch = threadIdx.x >> 2, sub = threadIdx.x & 3, cc = c0 + ch;

@@ -14,15 +14,16 @@
 // `zero_grads` clears each gradient chunk after it is consumed (the
 // optimizer.step(); optimizer.zero_grad() pair in one pass over the gradient).
 //
-// Memory: each block streams a 4096-element chunk (16 fp32/thread, float4
-// vectorised): params/grads/exp_avg/exp_avg_sq read once, written once.
+// Memory: each block streams one chunk of J*1024 elements (J float4 per thread per array):
+// params/grads/exp_avg/exp_avg_sq read once, written once.  J = 4 (4096-element chunks) for big
+// models; J = 1 for small ones (LeNet's 61,706 parameters: 4x the blocks, one load round trip).
 #include "rk_common.h"
 
 using namespace rk;
 
 namespace {
 
-constexpr int kChunk = 4096;
+constexpr int kChunk = 4096;  // largest chunk (J = 4)
 constexpr int kThreads = 256;
 
 struct TensorRec {  // 6 x int64 per tensor, uploaded from the host
@@ -61,7 +62,7 @@ __device__ __forceinline__ void zero_chunk(G* g, int64_t start, int64_t end) {
   for (int64_t i = start + threadIdx.x; i < end; i += kThreads) g[i] = G(0);
 }
 
-template <typename G, bool ZG>
+template <typename G, bool ZG, int J>
 __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __restrict__ tensors,
                                                           const int2* __restrict__ blocks,
                                                           const AdamHyper* __restrict__ hyper, float* step,
@@ -85,8 +86,9 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
     const float decay = h.decoupled != 0.f ? 1.f - h.lr * h.wd : 1.f;
     const float l2 = h.decoupled != 0.f ? 0.f : h.wd;
     const float sgn = h.maximize != 0.f ? -1.f : 1.f;
-    const int64_t start = (int64_t)bt.y * kChunk;
-    const int64_t end = min(start + (int64_t)kChunk, tr.n);
+    constexpr int CH = J * 4 * kThreads;
+    const int64_t start = (int64_t)bt.y * CH;
+    const int64_t end = min(start + (int64_t)CH, tr.n);
     auto upd = [&](float& pp, float gg, float& mm, float& vv) {
       gg = sgn * gg * gs + l2 * pp;
       pp *= decay;
@@ -95,9 +97,8 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
       pp -= step_size * mm / (sqrtf(vv) * rbc2 + h.eps);
     };
     const bool vec = sizeof(G) == 4 && ((tr.p | tr.g | tr.s0 | tr.s1) & 15) == 0;
-    if (vec && end - start == kChunk) {
-      // full chunk: all 16 float4 loads of the thread in flight before the first update
-      constexpr int J = kChunk / (4 * kThreads);
+    if (vec && end - start == CH) {
+      // full chunk: all 4*J float4 loads of the thread in flight before the first update
       float4 pp[J], mm[J], vv[J], gg[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) {
@@ -146,10 +147,11 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
       }
     }
   } else if (ZG) {
+    constexpr int CH = J * 4 * kThreads;
     const int2 bt = blocks[blockIdx.x];
     const TensorRec tr = tensors[bt.x];
-    const int64_t start = (int64_t)bt.y * kChunk;
-    zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)kChunk, tr.n));
+    const int64_t start = (int64_t)bt.y * CH;
+    zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)CH, tr.n));
   }
 }
 
@@ -157,7 +159,7 @@ struct SgdHyper {  // 8 floats per group
   float lr, momentum, dampening, wd, nesterov, maximize, first, pad;
 };
 
-template <typename G, bool ZG>
+template <typename G, bool ZG, int J>
 __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __restrict__ tensors,
                                                          const int2* __restrict__ blocks,
                                                          const SgdHyper* __restrict__ hyper, float* step,
@@ -175,8 +177,9 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
     const bool first = cur == 0.f;  // momentum buffer initialised with the first gradient (torch semantics)
     const float gs = inv_scale ? inv_scale[0] : 1.f;
     const float sgn = h.maximize != 0.f ? -1.f : 1.f;
-    const int64_t start = (int64_t)bt.y * kChunk;
-    const int64_t end = min(start + (int64_t)kChunk, tr.n);
+    constexpr int CH = J * 4 * kThreads;
+    const int64_t start = (int64_t)bt.y * CH;
+    const int64_t end = min(start + (int64_t)CH, tr.n);
     for (int64_t i = start + threadIdx.x; i < end; i += kThreads) {
       float gg = gload<G>(g, i) * gs + h.wd * p[i];
       if (h.momentum != 0.f) {
@@ -188,27 +191,34 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
       if (ZG) g[i] = G(0);
     }
   } else if (ZG) {
+    constexpr int CH = J * 4 * kThreads;
     const int2 bt = blocks[blockIdx.x];
     const TensorRec tr = tensors[bt.x];
-    const int64_t start = (int64_t)bt.y * kChunk;
-    zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)kChunk, tr.n));
+    const int64_t start = (int64_t)bt.y * CH;
+    zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)CH, tr.n));
   }
 }
 
 }  // namespace
 
+// elements per block-table chunk for a parameter set of `total` elements (the host builds the
+// block table with it and passes it back to rk_optim_mt)
+RK_API int rk_optim_chunk_for(int64_t total) { return total <= (int64_t)(1 << 21) ? kChunk / 4 : kChunk; }
 RK_API int rk_optim_chunk() { return kChunk; }
 
-// kind: 0 = Adam/AdamW, 1 = SGD.  gdtype: grads dtype (0 f32, 1 bf16).
+// kind: 0 = Adam/AdamW, 1 = SGD.  gdtype: grads dtype (0 f32, 1 bf16).  chunk: 1024 or 4096.
 RK_API int rk_optim_mt(int kind, int gdtype, const void* tensors, const void* blocks, int nblocks, const void* hyper,
                        float* step, const float* inv_scale, const float* found_inf, unsigned* counter, int zero_grads,
-                       hipStream_t s) {
+                       int chunk, hipStream_t s) {
   if (nblocks <= 0) return 0;
+  if (chunk != kChunk && chunk != kChunk / 4) return (int)hipErrorInvalidValue;
   const TensorRec* t = (const TensorRec*)tensors;
   const int2* b = (const int2*)blocks;
-#define RK_OPT_LAUNCH(KERNEL, G, H)                                                                        \
-  (zero_grads ? KERNEL<G, true><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, inv_scale, found_inf, counter) \
-              : KERNEL<G, false><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, inv_scale, found_inf, counter))
+#define RK_OPT_LAUNCH_J(KERNEL, G, H, J)                                                                              \
+  (zero_grads ? KERNEL<G, true, J><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, inv_scale, found_inf, counter) \
+              : KERNEL<G, false, J><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, inv_scale, found_inf, counter))
+#define RK_OPT_LAUNCH(KERNEL, G, H) \
+  (chunk == kChunk ? RK_OPT_LAUNCH_J(KERNEL, G, H, 4) : RK_OPT_LAUNCH_J(KERNEL, G, H, 1))
   if (kind == 0) {
     if (gdtype == BF16)
       RK_OPT_LAUNCH(adam_mt_kernel, uint16_t, AdamHyper);
@@ -221,5 +231,6 @@ RK_API int rk_optim_mt(int kind, int gdtype, const void* tensors, const void* bl
       RK_OPT_LAUNCH(sgd_mt_kernel, float, SgdHyper);
   }
 #undef RK_OPT_LAUNCH
+#undef RK_OPT_LAUNCH_J
   return (int)hipGetLastError();
 }

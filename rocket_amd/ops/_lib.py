@@ -42,17 +42,22 @@ KERNEL_SIGS = {
     "rk_conv_pool_dgrad": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int] + [c_int] * 7 + [c_void_p]),
     "rk_lenet_conv_fwd": (c_int, [c_void_p] * 9 + [c_int, c_void_p]),
     "rk_lenet_conv_bwd": (c_int, [c_void_p] * 10 + [c_int, c_int, c_void_p]),
-    "rk_lenet_prep": (c_int, [c_void_p] * 5),
+    "rk_lenet_prep": (c_int, [c_void_p] * 7),
     "rk_lenet_frag_bytes": (c_int, []),
+    "rk_lenet_set_trace": (None, [c_void_p, c_void_p]),
     "rk_lenet_fwd": (c_int, [c_void_p] * 16 + [c_int, c_void_p]),
-    "rk_lenet_bwd": (c_int, [c_void_p] * 16 + [c_int, c_int, c_void_p, c_void_p]),
+    "rk_lenet_bwd": (c_int, [c_void_p] * 13 + [c_int, c_int, c_void_p, c_void_p]),
+    "rk_lenet_slab_width": (c_int, []),
+    "rk_lenet_slab_cols": (c_int, []),
     "rk_mlp3_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                             c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "rk_mlp3_dgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
-    "rk_mlp3_wgrad": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "rk_mlp3_wgrad": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                              c_int, c_void_p, c_void_p, c_void_p]),
     "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                            c_int, c_void_p]),
+                            c_int, c_int, c_void_p]),
+    "rk_optim_chunk_for": (c_int, [c_int64]),
     "rk_gather_rows": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_loss_accum": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_int, c_void_p]),
     "rk_bn_workspace": (c_int64, [c_int64, c_int]),

@@ -136,8 +136,8 @@ class _MLPHead(torch.autograd.Function):
             I = ctypes.c_int * 3
             _lib.check(lib.rk_mlp3_wgrad(3, P(*[p[0].data_ptr() for p in probs]), P(*[p[1].data_ptr() for p in probs]),
                                          P(*[p[2].data_ptr() for p in probs]), P(*[p[3].data_ptr() for p in probs]),
-                                         I(*[p[4] for p in probs]), I(*[p[5] for p in probs]), M, stream),
-                       "rk_mlp3_wgrad")
+                                         I(*[p[4] for p in probs]), I(*[p[5] for p in probs]), M, None, 0, 0, None,
+                                         None, stream), "rk_mlp3_wgrad")
         else:  # generic MFMA GEMM: dW[n][k] += sum_m dT[n][m] xT[k][m]
             for dT, inT, wbuf, bbuf, n_out, k_in in probs:
                 gemm(dT, inT, wbuf, M=n_out, N=k_in, K=M, lda=M, ldb=M, ldc=k_in, accumulate=True, rowsum=bbuf,
@@ -174,8 +174,8 @@ class _LeNetFused(torch.autograd.Function):
         stream = _lib.stream_ptr(dev)
         cw = [t.detach().float().contiguous() for t in (w1, b1, w2, b2, f1w, f1b, f2w, f2b, f3w, f3b)]
         frag = torch.empty(int(lib.rk_lenet_frag_bytes()), dtype=torch.uint8, device=dev)
-        _lib.check(lib.rk_lenet_prep(cw[4].data_ptr(), cw[6].data_ptr(), cw[8].data_ptr(), frag.data_ptr(), stream),
-                   "rk_lenet_prep")
+        _lib.check(lib.rk_lenet_prep(cw[4].data_ptr(), cw[6].data_ptr(), cw[8].data_ptr(), cw[0].data_ptr(),
+                                     cw[2].data_ptr(), frag.data_ptr(), stream), "rk_lenet_prep")
         bf = dict(dtype=torch.bfloat16, device=dev)
         a1 = torch.empty(N, 1176, **bf)
         c1 = torch.empty(N, 1176, dtype=torch.uint8, device=dev)
@@ -224,20 +224,26 @@ class _LeNetFused(torch.autograd.Function):
         d1T = torch.empty(120, N, **bf)
         params = ctx.params
         bufs, direct = _grad_targets(params, dev)
+        # conv weight/bias gradients: one slab row per backward block, summed by the wgrad launch
+        slab = torch.empty(N // 4, int(lib.rk_lenet_slab_width()), dtype=torch.float32, device=dev)
         _lib.check(lib.rk_lenet_bwd(x.data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(), w2c.data_ptr(),
                                     frag.data_ptr(), dy.data_ptr(), h1T.data_ptr(), h2T.data_ptr(), dyT.data_ptr(),
-                                    d2T.data_ptr(), d1T.data_ptr(), bufs[0].data_ptr(), bufs[1].data_ptr(),
-                                    bufs[2].data_ptr(), bufs[3].data_ptr(), N, rounds,
+                                    d2T.data_ptr(), d1T.data_ptr(), slab.data_ptr(), N, rounds,
                                     ctypes.byref(ce) if ce is not None else None, stream), "rk_lenet_bwd")
         del keep
         probs = ((dyT, h2T, bufs[8], bufs[9], 10, 84), (d2T, h1T, bufs[6], bufs[7], 84, 120),
                  (d1T, a2T, bufs[4], bufs[5], 120, 400))
         P = ctypes.c_void_p * 3
         I = ctypes.c_int * 3
+        # slab columns [dW1 150 | db1 6 | dW2 2400 | db2 16] -> conv1.weight/bias, conv2.weight/bias
+        sizes = [bufs[i].numel() for i in range(4)]
+        assert sum(sizes) == int(lib.rk_lenet_slab_cols()), "fused LeNet expects conv1 6x1x5x5 / conv2 16x6x5x5"
+        bounds = (ctypes.c_int * 5)(0, sizes[0], sizes[0] + sizes[1], sizes[0] + sizes[1] + sizes[2], sum(sizes))
         _lib.check(lib.rk_mlp3_wgrad(3, P(*[q[0].data_ptr() for q in probs]), P(*[q[1].data_ptr() for q in probs]),
                                      P(*[q[2].data_ptr() for q in probs]), P(*[q[3].data_ptr() for q in probs]),
-                                     I(*[q[4] for q in probs]), I(*[q[5] for q in probs]), N, stream),
-                   "rk_mlp3_wgrad")
+                                     I(*[q[4] for q in probs]), I(*[q[5] for q in probs]), N, slab.data_ptr(),
+                                     N // 4, slab.shape[1], (ctypes.c_void_p * 4)(*[bufs[i].data_ptr() for i in range(4)]),
+                                     bounds, stream), "rk_mlp3_wgrad")
         return (None, *_finish(params, bufs, direct))
 
 

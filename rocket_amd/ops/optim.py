@@ -43,6 +43,7 @@ class _FusedBase(torch.optim.Optimizer):
         self._device = None
         self._gdtype = 0
         self._nblocks = 0
+        self._chunk = 0
         self.version = 0  # bumped whenever a device table/state pointer changes (captured graphs go stale)
         self.grad_scale: Optional[torch.Tensor] = None  # 1/scale (AMP); device scalar
         self.found_inf: Optional[torch.Tensor] = None
@@ -116,7 +117,8 @@ class _FusedBase(torch.optim.Optimizer):
             self._hyper_host = host  # keep the pinned source alive until the copy has run
 
     def _build_tables(self, active, device) -> None:
-        chunk = _lib.kernels().rk_optim_chunk()
+        chunk = int(_lib.kernels().rk_optim_chunk_for(sum(p.numel() for _, p in active)))
+        self._chunk = chunk
         recs, blocks = [], []
         for ti, (gi, p) in enumerate(active):
             st = self.state[p]
@@ -139,7 +141,7 @@ class _FusedBase(torch.optim.Optimizer):
             lib.rk_optim_mt(self.KIND, self._gdtype, self._tables[0].data_ptr(), self._tables[1].data_ptr(),
                             self._nblocks, self._hyper_dev.data_ptr(), self._step_dev.data_ptr(),
                             _lib.ptr(self.grad_scale), _lib.ptr(self.found_inf),
-                            _lib.Workspace.get(dev).counter(f"optim_{id(self)}"), int(zero_grads),
+                            _lib.Workspace.get(dev).counter(f"optim_{id(self)}"), int(zero_grads), self._chunk,
                             _lib.stream_ptr(dev)),
             "rk_optim_mt",
         )

@@ -91,7 +91,10 @@ def test_ddp_graph_two_ranks(tmp_path, p2p):
         assert len(e["losses"]) == len(g["losses"]) > 0
         for a, b in zip(e["losses"], g["losses"]):
             assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (e["losses"], g["losses"])
-        assert abs(e["w"] - g["w"]) <= 1e-3 * max(1.0, abs(e["w"])), (e["w"], g["w"])
+        # weight sums: eager (separate CE launch, fp32 d(logits)) and captured (CE fused into the
+        # backward launch) round differently; Adam at lr 1e-2 turns near-zero gradients' rounding
+        # differences into +-lr steps, so this checksum gets a looser bound than the losses
+        assert abs(e["w"] - g["w"]) <= 5e-3 * max(1.0, abs(e["w"])), (e["w"], g["w"])
     # replicas stay identical across ranks, and the reported loss is the cross-rank mean
     assert abs(r[0]["True"]["w"] - r[1]["True"]["w"]) < 1e-6 * max(1.0, abs(r[0]["True"]["w"]))
     assert r[0]["True"]["losses"] == pytest.approx(r[1]["True"]["losses"], rel=1e-6)

@@ -1,8 +1,8 @@
 """HIP-graph capture of the training step must reproduce eager training.
 
 Same seeds, same data order, same fused kernels: the captured run replays the
-eager micro-step, so per-step losses and final weights agree to fp32 rounding
-(atomics in split-K weight gradients make it not bit-exact).
+eager micro-step, so per-step losses agree to rounding and final weights closely;
+each mode on its own is bitwise reproducible (no float atomics in the step).
 """
 
 import pytest
@@ -65,6 +65,21 @@ def test_graph_matches_eager(tmp_path, ga):
     assert len(le) == len(lg) and len(le) > 0
     for a, b in zip(le, lg):
         assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (le, lg)
-    for k in we:
-        d = (we[k] - wg[k]).norm() / we[k].norm().clamp_min(1e-6)
-        assert d < 5e-3, (k, float(d))
+    diffs = {k: float((we[k] - wg[k]).norm() / we[k].norm().clamp_min(1e-6)) for k in we}
+    print(f"ga={ga} eager-vs-graph relative weight differences: {diffs}")
+    # eager (separate CE launch) and captured (CE fused into the backward launch) differ by bf16
+    # rounding of d(logits); Adam's normalised steps amplify that for near-zero gradients, so the
+    # weights get a looser bound than the losses (bitwise reproducibility is tested below)
+    for k, d in diffs.items():
+        assert d < 1.5e-2, (k, d)
+
+
+@pytest.mark.parametrize("capture", [False, True])
+def test_training_bitwise_reproducible(tmp_path, capture):
+    """No float atomics anywhere in the fused LeNet step (slab-reduced conv gradients, fixed-order
+    grid reductions): two identical runs end with bit-identical weights, eager and captured."""
+    la, wa, _ = _train(tmp_path / "a", capture=capture, steps=8)
+    lb, wb, _ = _train(tmp_path / "b", capture=capture, steps=8)
+    assert la == lb
+    bad = {k: float((wa[k] - wb[k]).abs().max()) for k in wa if not torch.equal(wa[k], wb[k])}
+    assert not bad, bad

@@ -185,3 +185,25 @@ def test_lenet_fused_cross_entropy(N):
     # a second backward without the CE spec consumes dlogits again (spec is one-shot)
     y2 = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
     y2.backward(torch.zeros_like(y2))
+
+
+@pytest.mark.parametrize("N", [1024, 256])
+def test_lenet_fused_backward_deterministic(N):
+    """The fused backward has no float atomics (per-block gradient slab rows, reduced in a fixed
+    order by the weight-gradient launch): repeated runs give bit-identical gradients."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.lenet import lenet_forward
+
+    torch.manual_seed(5)
+    net = LeNet(fused=False).cuda()
+    x = torch.rand(N, 1, 28, 28, device="cuda")
+    g = torch.randn(N, 10, device="cuda")
+    grads = []
+    for _ in range(3):
+        net.zero_grad(set_to_none=True)
+        y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
+        y.backward(g)
+        grads.append([p.grad.clone() for p in net.parameters()])
+    for run in grads[1:]:
+        for (name, _), a, b in zip(net.named_parameters(), grads[0], run):
+            assert torch.equal(a, b), (name, float((a - b).abs().max()))
