@@ -1,0 +1,21 @@
+"""StepTimer grouping: with stride k the timer marks every k-th iteration and reports per-iteration
+means of the groups (host-timestamp path, CPU)."""
+
+import pytest
+
+from rocket_amd.runtime.profiling import StepTimer
+
+
+@pytest.mark.parametrize("steps,stride,expect", [(12, 4, [4, 4, 4]), (10, 4, [4, 4, 2]), (5, 1, [1] * 5)])
+def test_group_sizes(steps, stride, expect):
+    t = StepTimer(warmup=0, steps=steps, stride=stride)
+    t._host = [0.0] * (len(expect) + 1)
+    assert t._group_sizes() == expect
+
+
+def test_step_times_are_per_iteration_means():
+    t = StepTimer(warmup=0, steps=10, stride=4)
+    # marks after iterations 0 (start), 4, 8, 10 -> groups of 4, 4, 2 iterations
+    t._host = [0.0, 0.004, 0.008, 0.010]
+    assert t.step_times_ms() == pytest.approx([1.0, 1.0, 1.0])
+    assert t.host_ms_p50() == pytest.approx(1.0)
