@@ -5,18 +5,25 @@
 // per-head column blocks) and the output / input gradients are written in the same token-major
 // layout — the head split/merge permutes of the composite path never materialise.
 //
-// Whole-row softmax: a key sequence of <= 224 tokens fits in one tile row, so every kernel keeps
-// all keys of a head in LDS and needs no online-softmax rescaling:
-//   attn_fwd   block = (head, batch): K/V staged once, the 4 waves loop over 16-query tiles.  S = Q K^T (13 MFMA tiles
-//              in registers), row max/sum by 16-lane shuffles, P (bf16) through a wave-private LDS
-//              tile into O = P V; writes O and the row log-sum-exp (log2 domain).
-//   attn_bwd_q same decomposition: recompute P from the saved LSE, dP = dO V^T, dS = P (dP - delta) * scale,
-//              dQ = dS K; also writes delta = rowsum(dO * O) for attn_bwd_kv.
-//   attn_bwd_kv block = (head, batch), waves loop over 16-key tiles: S^T = K Q^T and dP^T = V dO^T over
-//              all queries, dV = P^T dO, then dK = dS^T Q (P^T / dS^T reuse one LDS tile).
-// All operand fragments are 16-byte LDS reads (row-major copies for "consecutive d" operands,
-// transposed copies for "consecutive token" operands; row strides 72 / 232 bf16 keep the 16 rows
-// of a fragment on distinct banks).
+// Whole-row softmax: a key sequence of <= 224 tokens fits in one tile row, so no online-softmax
+// rescaling.  Every kernel is "operand-on-the-lane": the score tile is computed with the token
+// whose softmax/reduction axis is NOT summed next on the MFMA lane, so the accumulator of one
+// product is already (lane-locally) the operand of the next:
+//   S^T = K Q^T puts the query on the lane (C[row = key 4hi+i][col = query lo]); for a 32-key
+//   k-step built from key tiles t0, t1 the lane's 8 k-values are keys {16t0+4hi+i, 16t1+4hi+i} —
+//   the MFMA reduction order is free, so the P^T B-operand of O^T = V^T P^T is just the packed
+//   accumulators.  The matching V^T A-operand is read from the ROW-MAJOR V image with the gfx950
+//   transpose read ds_read_b64_tr_b16 (4 keys x 16 d per 16-lane group), so no transposed copy is
+//   staged and P never touches LDS.
+//   attn_fwd    block = (head, batch), K/V row-major in LDS (64 KB: 2 blocks per CU), the 4 waves
+//               loop over 16-query tiles; writes O and the row log-sum-exp (log2 domain).
+//   attn_bwd_q  same shape: S^T, dP^T = V dO^T (query on the lane), dS^T = P^T (dP^T - delta),
+//               dQ = dS K with dS^T's accumulators as the A operand and K^T by transpose reads;
+//               also writes delta = rowsum(dO * O) for attn_bwd_kv.
+//   attn_bwd_kv block = (head, batch), Q/dO row-major in LDS, waves loop over 16-key tiles: S and
+//               dP with the KEY on the lane, so P^T / dS^T are the A operands of dV = P^T dO and
+//               dK = dS^T Q, with dO and Q read transposed.
+// Row strides of 72 bf16 keep the 16-byte row reads of a fragment on distinct bank groups.
 #include "rk_common.h"
 
 using namespace rk;
@@ -24,9 +31,10 @@ using namespace rk;
 namespace {
 
 constexpr int D = 64;
-constexpr int LMAX = 224;        // max tokens (K-dim padded to 32)
-constexpr int RS = D + 8;        // row-major stride (72)
-constexpr int TS = LMAX + 8;     // transposed stride (232)
+constexpr int LMAX = 224;        // max tokens: 14 tiles of 16 (7 k-steps of 32)
+constexpr int NT = LMAX / 16;    // 14
+constexpr int NKS = NT / 2;      // 7
+constexpr int RS = D + 8;        // row-major LDS stride (72 bf16 = 144 B: 16-B aligned rows)
 constexpr int NTH = 256;         // 4 waves
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -36,8 +44,8 @@ struct AttnArgs {
   const uint16_t* v;
   const uint16_t* o;   // forward output (bwd), row stride ldo
   const uint16_t* dout;
-  uint16_t* out;       // fwd: O;  bwd: dQ / dK / dV base (row stride ldg)
-  uint16_t* dq;
+  uint16_t* out;       // fwd: O
+  uint16_t* dq;        // bwd: gradients, row stride ldg
   uint16_t* dk;
   uint16_t* dv;
   float* lse;          // [B*H][L], log2 domain
@@ -47,17 +55,20 @@ struct AttnArgs {
   float scale;         // softmax scale (1/sqrt(D))
 };
 
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
 __device__ __forceinline__ bf16x8 ld16(const uint16_t* p) { return *(const bf16x8*)p; }
 __device__ __forceinline__ bf16x8 zero8() { return bf16x8{}; }
 
-// global token row r of head h (clamped + selected: branch-free, always a valid address)
+// global token row r of head h, 8 d-values from column c (clamped + selected: branch-free)
 __device__ __forceinline__ bf16x8 gload_row(const uint16_t* base, int ld, int b, int L, int r, int h, int c) {
   const int rc = r < L ? r : L - 1;
   const bf16x8 v = ld16(base + ((int64_t)b * L + rc) * ld + h * D + c);
   return r < L ? v : zero8();
 }
 
-// stage [LMAX][RS] row-major copy of a head's tokens (zero rows >= L)
+// stage a head's tokens row-major into [LMAX][RS] (zero rows >= L)
 __device__ __forceinline__ void stage_rows(uint16_t* dst, const uint16_t* src, int ld, int b, int L, int h) {
   for (int i = threadIdx.x; i < LMAX * (D / 8); i += NTH) {
     const int r = i >> 3, c = (i & 7) * 8;
@@ -65,121 +76,110 @@ __device__ __forceinline__ void stage_rows(uint16_t* dst, const uint16_t* src, i
   }
 }
 
-// stage [D][TS] transposed copy (token index contiguous), zero tokens >= L
-__device__ __forceinline__ void stage_trans(uint16_t* dst, const uint16_t* src, int ld, int b, int L, int h) {
-  for (int i = threadIdx.x; i < LMAX * (D / 8); i += NTH) {
-    const int r = i >> 3, c = (i & 7) * 8;
-    const int rc = r < L ? r : L - 1;
-    uint4 u = *(const uint4*)(src + ((int64_t)b * L + rc) * ld + h * D + c);
-    if (r >= L) u = make_uint4(0, 0, 0, 0);
-    const uint32_t wds[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      dst[(c + 2 * e) * TS + r] = (uint16_t)(wds[e] & 0xffffu);
-      dst[(c + 2 * e + 1) * TS + r] = (uint16_t)(wds[e] >> 16);
-    }
-  }
+// Transpose read of a row-major [.][RS] bf16 image: the calling 16-lane group (lanes 16g..16g+15)
+// gets rows r0..r0+3 (r0 = this group's first row), columns c0..c0+15: lane lo receives column
+// c0 + lo, element q = row r0 + q.  Every lane of the wave must execute it (EXEC all ones).
+__device__ __forceinline__ uint2 tr4(const uint16_t* img, int r0, int c0, int lo) {
+  const uint16_t* p = img + (r0 + (lo >> 2)) * RS + c0 + 4 * (lo & 3);
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+  return __builtin_bit_cast(uint2, v);
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
+// 16x16x32 operand whose 8 k-values are rows {r0a..r0a+3, r0b..r0b+3} of a row-major image at
+// columns c0 + lo (the "k = keys of tiles t0, t1" order of the accumulator hand-off)
+__device__ __forceinline__ bf16x8 tr_operand(const uint16_t* img, int r0a, int r0b, int c0, int lo) {
+  const uint2 a = tr4(img, r0a, c0, lo), b = tr4(img, r0b, c0, lo);
+  return __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
 }
 
-__device__ __forceinline__ float red16_max(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
-__device__ __forceinline__ float red16_sum(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// accumulators of tiles t0 (k 0..3) and t1 (k 4..7) -> one bf16x8 operand
+__device__ __forceinline__ bf16x8 pack_operand(const f32x4& x, const f32x4& y) {
+  return __builtin_bit_cast(bf16x8, make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(y[0], y[1]),
+                                               pack2(y[2], y[3])));
 }
 
-constexpr int NT = LMAX / 16;  // 14 key tiles max
+__device__ __forceinline__ float red4_max(float v) {  // over the 4 lanes sharing lo (hi = 0..3)
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float red4_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
 
 // --------------------------------------------------------------------------------- forward
 __global__ void __launch_bounds__(NTH) attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vt[D * TS];
-  __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * TS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[LMAX * RS];
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
   const int L = a.L;
   const int ntile = (L + 15) / 16;
   stage_rows(Ks, a.k, a.ld, b, L, h);
-  stage_trans(Vt, a.v, a.ld, b, L, h);
-  for (int i = lane; i < 16 * TS; i += 64) Ps[w][i] = 0;  // zero pads (cols >= 16*ntile)
+  stage_rows(Vs, a.v, a.ld, b, L, h);
   __syncthreads();
 
   const float sl = a.scale * LOG2E;
-  // the block owns every query tile of its (batch, head): K/V are staged once per head
+  const int64_t bh = (int64_t)b * a.H + h;
   for (int qt = w; qt < ntile; qt += 4) {
-  const int q0 = 16 * qt;
-  bf16x8 qa[2];
+    const int q0 = 16 * qt;
+    bf16x8 qb[2];  // B operand of S^T = K Q^T: n = query q0 + lo, k = d 32ks + 8hi + j
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) qa[ks] = gload_row(a.q, a.ld, b, L, q0 + lo, h, 32 * ks + 8 * hi);
-  f32x4 s[NT];
-  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int ks = 0; ks < 2; ++ks) qb[ks] = gload_row(a.q, a.ld, b, L, q0 + lo, h, 32 * ks + 8 * hi);
+    f32x4 s[NT];
+    float m = -INFINITY;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (t < ntile) {
+    for (int t = 0; t < NT; ++t) {
+      s[t] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      if (t < ntile) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], ld16(Ks + (16 * t + lo) * RS + 32 * ks + 8 * hi), s[t], 0, 0, 0);
-      const bool valid = 16 * t + lo < L;
+        for (int ks = 0; ks < 2; ++ks)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Ks + (16 * t + lo) * RS + 32 * ks + 8 * hi), qb[ks], acc,
+                                                        0, 0, 0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        s[t][i] = valid ? s[t][i] * sl : -INFINITY;
-        m[i] = fmaxf(m[i], s[t][i]);
+        for (int i = 0; i < 4; ++i) {  // C[row = key 16t + 4hi + i][col = query lo]
+          s[t][i] = 16 * t + 4 * hi + i < L ? acc[i] * sl : -INFINITY;
+          m = fmaxf(m, s[t][i]);
+        }
       }
     }
-  }
-  float sum[4];
+    m = red4_max(m);
+    float sum = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    m[i] = red16_max(m[i]);
-    sum[i] = 0.f;
-  }
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    if (t < ntile) {
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(s[t][i] - m[i]);
-        sum[i] += p;
-        Ps[w][(4 * hi + i) * TS + 16 * t + lo] = f2bf(p);
+        s[t][i] = exp2f(s[t][i] - m);  // masked / absent keys: exp2(-inf) = 0
+        sum += s[t][i];
+      }
+    sum = red4_sum(sum);
+    f32x4 o[4];  // O^T: C[row = d 16nt + 4hi + i][col = query lo]
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) o[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (32 * ks < 16 * ntile) {  // uniform
+        const bf16x8 pb = pack_operand(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          o[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              tr_operand(Vs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), pb, o[nt], 0, 0, 0);
       }
     }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) sum[i] = red16_sum(sum[i]);
-  wave_lds_sync();
-
-  const int kst = (16 * ntile + 31) / 32;
-  f32x4 o[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) o[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int ks = 0; ks < kst; ++ks) {
-    const bf16x8 pa = ld16(&Ps[w][lo * TS + 32 * ks + 8 * hi]);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-      o[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ld16(Vt + (16 * nt + lo) * TS + 32 * ks + 8 * hi), o[nt], 0, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = q0 + 4 * hi + i;
+    const int r = q0 + lo;
     if (r < L) {
-      const float inv = 1.f / sum[i];
+      const float inv = 1.f / sum;
       uint16_t* orow = a.out + ((int64_t)b * L + r) * a.ldo + h * D;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) orow[16 * nt + lo] = f2bf(o[nt][i] * inv);
-      if (lo == 0) a.lse[((int64_t)b * a.H + h) * L + r] = m[i] + log2f(sum[i]);
+      for (int nt = 0; nt < 4; ++nt)
+        *(uint2*)(orow + 16 * nt + 4 * hi) = make_uint2(pack2(o[nt][0] * inv, o[nt][1] * inv),
+                                                        pack2(o[nt][2] * inv, o[nt][3] * inv));
+      if (hi == 0) a.lse[bh * L + r] = m + log2f(sum);
     }
-  }
-  wave_lds_sync();  // P of this tile fully consumed before the next tile overwrites it
   }
 }
 
@@ -187,83 +187,76 @@ __global__ void __launch_bounds__(NTH) attn_fwd_kernel(AttnArgs a) {
 __global__ void __launch_bounds__(NTH) attn_bwd_q_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[LMAX * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Kt[D * TS];
-  __shared__ __attribute__((aligned(16))) uint16_t Ss[4][16 * TS];
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
   const int L = a.L;
   const int ntile = (L + 15) / 16;
   stage_rows(Ks, a.k, a.ld, b, L, h);
   stage_rows(Vs, a.v, a.ld, b, L, h);
-  stage_trans(Kt, a.k, a.ld, b, L, h);
-  for (int i = lane; i < 16 * TS; i += 64) Ss[w][i] = 0;
   __syncthreads();
 
-  for (int qt = w; qt < ntile; qt += 4) {
-  const int q0 = 16 * qt;
-  bf16x8 qa[2], ga[2];
-  float dot = 0.f;  // partial rowsum(dO * O) of row q0 + lo over this lane's 16 d values
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    qa[ks] = gload_row(a.q, a.ld, b, L, q0 + lo, h, 32 * ks + 8 * hi);
-    ga[ks] = gload_row(a.dout, a.ldo, b, L, q0 + lo, h, 32 * ks + 8 * hi);
-    const bf16x8 ov = gload_row(a.o, a.ldo, b, L, q0 + lo, h, 32 * ks + 8 * hi);
-    const uint4 gu = __builtin_bit_cast(uint4, ga[ks]), ou = __builtin_bit_cast(uint4, ov);
-    const uint32_t gw[4] = {gu.x, gu.y, gu.z, gu.w}, ow[4] = {ou.x, ou.y, ou.z, ou.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      dot += __uint_as_float(gw[e] << 16) * __uint_as_float(ow[e] << 16) +
-             __uint_as_float(gw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
-  }
-  dot += __shfl_xor(dot, 16, 64);
-  dot += __shfl_xor(dot, 32, 64);  // every lane with this lo holds delta(row q0 + lo)
-  const int64_t bh = (int64_t)b * a.H + h;
-  if (hi == 0 && q0 + lo < L) a.delta[bh * L + q0 + lo] = dot;
-  // per C-layout row r = 4hi + i: delta and lse of query q0 + r
-  float dl[4], ls[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    dl[i] = __shfl(dot, 4 * hi + i, 64);
-    const int r = q0 + 4 * hi + i;
-    ls[i] = a.lse[bh * L + (r < L ? r : L - 1)];
-  }
   const float sl = a.scale * LOG2E;
-#pragma unroll 2
-  for (int t = 0; t < ntile; ++t) {
-    f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+  const int64_t bh = (int64_t)b * a.H + h;
+  for (int qt = w; qt < ntile; qt += 4) {
+    const int q0 = 16 * qt;
+    bf16x8 qb[2], gb[2];  // B operands: n = query q0 + lo, k = d
+    float dot = 0.f;      // partial rowsum(dO * O) of query q0 + lo over this lane's 16 d values
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], ld16(Ks + (16 * t + lo) * RS + 32 * ks + 8 * hi), s, 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[ks], ld16(Vs + (16 * t + lo) * RS + 32 * ks + 8 * hi), dp, 0, 0, 0);
+      qb[ks] = gload_row(a.q, a.ld, b, L, q0 + lo, h, 32 * ks + 8 * hi);
+      gb[ks] = gload_row(a.dout, a.ldo, b, L, q0 + lo, h, 32 * ks + 8 * hi);
+      const bf16x8 ov = gload_row(a.o, a.ldo, b, L, q0 + lo, h, 32 * ks + 8 * hi);
+      const uint4 gu = __builtin_bit_cast(uint4, gb[ks]), ou = __builtin_bit_cast(uint4, ov);
+      const uint32_t gw[4] = {gu.x, gu.y, gu.z, gu.w}, ow[4] = {ou.x, ou.y, ou.z, ou.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        dot += __uint_as_float(gw[e] << 16) * __uint_as_float(ow[e] << 16) +
+               __uint_as_float(gw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
     }
-    const bool valid = 16 * t + lo < L;
+    const float delta = red4_sum(dot);  // every lane with this lo holds delta(query q0 + lo)
+    const int rq = q0 + lo;
+    if (hi == 0 && rq < L) a.delta[bh * L + rq] = delta;
+    const float lq = a.lse[bh * L + (rq < L ? rq : L - 1)];
+    f32x4 ds[NT];  // dS^T: C[row = key 16t + 4hi + i][col = query lo]
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      ds[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t < ntile) {
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Ks + (16 * t + lo) * RS + 32 * ks + 8 * hi), qb[ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Vs + (16 * t + lo) * RS + 32 * ks + 8 * hi), gb[ks], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = 16 * t + 4 * hi + i < L ? exp2f(s[i] * sl - lq) : 0.f;
+          ds[t][i] = p * (dp[i] - delta) * a.scale;
+        }
+      }
+    }
+    f32x4 dq[4];  // dQ: C[row = query 4hi + i][col = d 16nt + lo]
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dq[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (32 * ks < 16 * ntile) {
+        const bf16x8 sa = pack_operand(ds[2 * ks], ds[2 * ks + 1]);  // A: row = query lo, k = keys
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          dq[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              sa, tr_operand(Ks, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dq[nt], 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float p = valid ? exp2f(s[i] * sl - ls[i]) : 0.f;
-      Ss[w][(4 * hi + i) * TS + 16 * t + lo] = f2bf(p * (dp[i] - dl[i]) * a.scale);
+      const int r = q0 + 4 * hi + i;
+      if (r < L) {
+        uint16_t* row = a.dq + ((int64_t)b * L + r) * a.ldg + h * D;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) row[16 * nt + lo] = f2bf(dq[nt][i]);
+      }
     }
-  }
-  wave_lds_sync();
-  const int kst = (16 * ntile + 31) / 32;
-  f32x4 dq[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) dq[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int ks = 0; ks < kst; ++ks) {
-    const bf16x8 sa = ld16(&Ss[w][lo * TS + 32 * ks + 8 * hi]);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-      dq[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, ld16(Kt + (16 * nt + lo) * TS + 32 * ks + 8 * hi), dq[nt], 0, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = q0 + 4 * hi + i;
-    if (r < L) {
-      uint16_t* row = a.dq + ((int64_t)b * L + r) * a.ldg + h * D;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) row[16 * nt + lo] = f2bf(dq[nt][i]);
-    }
-  }
-  wave_lds_sync();
   }
 }
 
@@ -271,9 +264,6 @@ __global__ void __launch_bounds__(NTH) attn_bwd_q_kernel(AttnArgs a) {
 __global__ void __launch_bounds__(NTH) attn_bwd_kv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Qs[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Gs[LMAX * RS];  // dO row-major
-  __shared__ __attribute__((aligned(16))) uint16_t Qt[D * TS];
-  __shared__ __attribute__((aligned(16))) uint16_t Gt[D * TS];     // dO transposed
-  __shared__ __attribute__((aligned(16))) uint16_t Ts[4][16 * TS]; // P^T, then dS^T
   __shared__ float lse_s[LMAX], del_s[LMAX];
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
@@ -282,93 +272,70 @@ __global__ void __launch_bounds__(NTH) attn_bwd_kv_kernel(AttnArgs a) {
   const int64_t bh = (int64_t)b * a.H + h;
   stage_rows(Qs, a.q, a.ld, b, L, h);
   stage_rows(Gs, a.dout, a.ldo, b, L, h);
-  stage_trans(Qt, a.q, a.ld, b, L, h);
-  stage_trans(Gt, a.dout, a.ldo, b, L, h);
   for (int i = threadIdx.x; i < LMAX; i += NTH) {
     lse_s[i] = i < L ? a.lse[bh * L + i] : 0.f;
     del_s[i] = i < L ? a.delta[bh * L + i] : 0.f;
   }
-  for (int i = lane; i < 16 * TS; i += 64) Ts[w][i] = 0;
   __syncthreads();
 
   const float sl = a.scale * LOG2E;
   for (int kt = w; kt < ntile; kt += 4) {
-  const int k0 = 16 * kt;
-  bf16x8 ka[2], va[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    ka[ks] = gload_row(a.k, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
-    va[ks] = gload_row(a.v, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
-  }
-  const int kst = (16 * ntile + 31) / 32;
-  // pass 1: P^T (rows = keys 4hi+i, cols = queries) -> dV = P^T dO
-#pragma unroll 2
-  for (int t = 0; t < ntile; ++t) {
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[ks], ld16(Qs + (16 * t + lo) * RS + 32 * ks + 8 * hi), s, 0, 0, 0);
-    const int qi = 16 * t + lo;
-    const float lq = lse_s[qi];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) Ts[w][(4 * hi + i) * TS + qi] = f2bf(qi < L ? exp2f(s[i] * sl - lq) : 0.f);
-  }
-  wave_lds_sync();
-  f32x4 acc[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int ks = 0; ks < kst; ++ks) {
-    const bf16x8 pa = ld16(&Ts[w][lo * TS + 32 * ks + 8 * hi]);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ld16(Gt + (16 * nt + lo) * TS + 32 * ks + 8 * hi), acc[nt], 0, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = k0 + 4 * hi + i;
-    if (r < L) {
-      uint16_t* row = a.dv + ((int64_t)b * L + r) * a.ldg + h * D;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) row[16 * nt + lo] = f2bf(acc[nt][i]);
-    }
-  }
-  wave_lds_sync();  // every lane finished reading P^T before it is overwritten with dS^T
-  // pass 2: dS^T = P^T (dP^T - delta) * scale, dP^T = V dO^T -> dK = dS^T Q
-#pragma unroll 2
-  for (int t = 0; t < ntile; ++t) {
-    f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+    const int k0 = 16 * kt;
+    bf16x8 kb[2], vb[2];  // B operands of S = Q K^T and dP = dO V^T: n = key k0 + lo, k = d
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[ks], ld16(Qs + (16 * t + lo) * RS + 32 * ks + 8 * hi), s, 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[ks], ld16(Gs + (16 * t + lo) * RS + 32 * ks + 8 * hi), dp, 0, 0, 0);
+      kb[ks] = gload_row(a.k, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
+      vb[ks] = gload_row(a.v, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
     }
-    const int qi = 16 * t + lo;
-    const float lq = lse_s[qi], dq = del_s[qi];
+    f32x4 dk[4], dv[4];  // C[row = key 4hi + i][col = d 16nt + lo]
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dk[nt] = dv[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (32 * ks >= 16 * ntile) break;  // uniform
+      f32x4 p2[2], ds2[2];  // query tiles 2ks, 2ks+1: C[row = query 16qt + 4hi + i][col = key lo]
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int qt = 2 * ks + u;
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+        if (qt < ntile) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Qs + (16 * qt + lo) * RS + 32 * kk + 8 * hi), kb[kk], s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Gs + (16 * qt + lo) * RS + 32 * kk + 8 * hi), vb[kk], dp, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qi = 16 * qt + 4 * hi + i;
+          const float p = qi < L ? exp2f(s[i] * sl - lse_s[qi]) : 0.f;
+          p2[u][i] = p;
+          ds2[u][i] = p * (dp[i] - del_s[qi]) * a.scale;
+        }
+      }
+      // A operands: row = key lo, k = queries {32ks + 4hi + i, 32ks + 16 + 4hi + i}
+      const bf16x8 pa = pack_operand(p2[0], p2[1]);
+      const bf16x8 sa = pack_operand(ds2[0], ds2[1]);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        dv[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            pa, tr_operand(Gs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dv[nt], 0, 0, 0);
+        dk[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            sa, tr_operand(Qs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dk[nt], 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float p = qi < L ? exp2f(s[i] * sl - lq) : 0.f;
-      Ts[w][(4 * hi + i) * TS + qi] = f2bf(p * (dp[i] - dq) * a.scale);
+      const int r = k0 + 4 * hi + i;
+      if (r < L) {
+        uint16_t* rk = a.dk + ((int64_t)b * L + r) * a.ldg + h * D;
+        uint16_t* rv = a.dv + ((int64_t)b * L + r) * a.ldg + h * D;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          rk[16 * nt + lo] = f2bf(dk[nt][i]);
+          rv[16 * nt + lo] = f2bf(dv[nt][i]);
+        }
+      }
     }
-  }
-  wave_lds_sync();
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int ks = 0; ks < kst; ++ks) {
-    const bf16x8 sa = ld16(&Ts[w][lo * TS + 32 * ks + 8 * hi]);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, ld16(Qt + (16 * nt + lo) * TS + 32 * ks + 8 * hi), acc[nt], 0, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = k0 + 4 * hi + i;
-    if (r < L) {
-      uint16_t* row = a.dk + ((int64_t)b * L + r) * a.ldg + h * D;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) row[16 * nt + lo] = f2bf(acc[nt][i]);
-    }
-  }
-  wave_lds_sync();
   }
 }
 

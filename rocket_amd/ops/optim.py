@@ -101,6 +101,7 @@ class _FusedBase(torch.optim.Optimizer):
             self._build_tables(active, device)
             self._key = key
         self.refresh_hyper()
+        self._opt_called = True  # what torch's LR schedulers check for "optimizer.step() ran first"
         return True
 
     def refresh_hyper(self) -> None:

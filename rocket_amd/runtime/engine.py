@@ -198,6 +198,10 @@ class Engine:
         if mixed_precision not in _MP:
             raise ValueError(f"unsupported mixed_precision {mixed_precision!r}")
         self.ctx = _comm.init(cpu=cpu)
+        if self.ctx.device.type == "cuda":
+            from rocket_amd.runtime.tuning import use_tuned_gemms
+
+            use_tuned_gemms()  # measured hipBLASLt solutions for the library GEMMs
         self.device_placement = device_placement
         self.mixed_precision = mixed_precision or "no"
         self._amp_dtype = _MP[mixed_precision]

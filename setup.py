@@ -36,7 +36,7 @@ setup(
     version="0.1.0",
     description="MI355X-native training-loop engine with the capsule API of dsenushkin/rocket",
     packages=find_packages(include=["rocket_amd", "rocket_amd.*", "rocket", "rocket.*"]),
-    package_data={"rocket_amd": ["_lib/*.so", "native/kernels/*.hip", "native/kernels/*.h", "native/runtime/*.cpp"]},
+    package_data={"rocket_amd": ["_lib/*.so", "tuning/*.csv", "native/kernels/*.hip", "native/kernels/*.h", "native/runtime/*.cpp"]},
     python_requires=">=3.10",
     install_requires=["torch>=2.4", "numpy", "tqdm", "safetensors"],
     cmdclass={"build_py": BuildPy, "develop": Develop},

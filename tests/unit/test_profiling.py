@@ -19,3 +19,16 @@ def test_step_times_are_per_iteration_means():
     t._host = [0.0, 0.004, 0.008, 0.010]
     assert t.step_times_ms() == pytest.approx([1.0, 1.0, 1.0])
     assert t.host_ms_p50() == pytest.approx(1.0)
+
+
+def test_tuned_gemm_table_is_valid_csv():
+    """The shipped TunableOp table has the validator header and well-formed result rows."""
+    import csv
+
+    from rocket_amd.runtime.tuning import TABLE
+
+    rows = list(csv.reader(open(TABLE)))
+    assert rows[0][0] == "Validator" and any(r[1] == "GCN_ARCH_NAME" and r[2].startswith("gfx950") for r in rows
+                                             if r[0] == "Validator")
+    results = [r for r in rows if r[0] != "Validator"]
+    assert results and all(len(r) == 4 and float(r[3]) > 0 for r in results)
