@@ -9,6 +9,11 @@
 // in device memory: every block reads it first, and the last block to take a ticket
 // advances it, so bias corrections need no host round trip.
 //
+// Optional bf16 shadows: a tensor record may carry an index map (int32 [n][2], -1 = none) and a
+// bf16 buffer; every updated element is also written, rounded to bf16, to buf[map[i][0]] and
+// buf[map[i][1]].  A kernel that consumes the weights as pre-arranged bf16 MFMA fragments (the
+// fused LeNet's fragment table) then needs no per-step re-layout launch.
+//
 // Optional AMP hooks: `inv_scale` multiplies every gradient (GradScaler unscale
 // folded into the update) and a non-zero `found_inf` makes the launch a no-op.
 // `zero_grads` clears each gradient chunk after it is consumed (the
@@ -26,9 +31,18 @@ namespace {
 constexpr int kChunk = 4096;  // largest chunk (J = 4)
 constexpr int kThreads = 256;
 
-struct TensorRec {  // 6 x int64 per tensor, uploaded from the host
+struct TensorRec {  // 8 x int64 per tensor, uploaded from the host
   int64_t p, g, s0, s1, n, group;
+  int64_t shadow_map, shadow_buf;  // int32 [n][2] / bf16 buffer, or 0
 };
+
+__device__ __forceinline__ void shadow_store(const TensorRec& tr, int64_t i, float v) {
+  const int2 m = ((const int2*)tr.shadow_map)[i];
+  uint16_t* buf = (uint16_t*)tr.shadow_buf;
+  const uint16_t b = f2bf(v);
+  if (m.x >= 0) buf[m.x] = b;
+  if (m.y >= 0) buf[m.y] = b;
+}
 
 struct AdamHyper {  // 8 floats per group
   float lr, beta1, beta2, eps, wd, decoupled, maximize, pad;
@@ -119,6 +133,12 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
         *(float4*)(m + i) = mm[j];
         *(float4*)(v + i) = vv[j];
         if (ZG) *(float4*)((float*)g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tr.shadow_map) {
+          shadow_store(tr, i, pp[j].x);
+          shadow_store(tr, i + 1, pp[j].y);
+          shadow_store(tr, i + 2, pp[j].z);
+          shadow_store(tr, i + 3, pp[j].w);
+        }
       }
     } else if (vec) {
       for (int64_t i = start + 4 * threadIdx.x; i < end; i += 4 * kThreads) {
@@ -133,10 +153,17 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
           *(float4*)(m + i) = mm;
           *(float4*)(v + i) = vv;
           if (ZG) *(float4*)((float*)g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (tr.shadow_map) {
+            shadow_store(tr, i, pp.x);
+            shadow_store(tr, i + 1, pp.y);
+            shadow_store(tr, i + 2, pp.z);
+            shadow_store(tr, i + 3, pp.w);
+          }
         } else {
           for (int64_t k = i; k < end; ++k) {
             upd(p[k], gload<G>(g, k), m[k], v[k]);
             if (ZG) g[k] = G(0);
+            if (tr.shadow_map) shadow_store(tr, k, p[k]);
           }
         }
       }
@@ -144,6 +171,7 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
       for (int64_t i = start + threadIdx.x; i < end; i += kThreads) {
         upd(p[i], gload<G>(g, i), m[i], v[i]);
         if (ZG) g[i] = G(0);
+        if (tr.shadow_map) shadow_store(tr, i, p[i]);
       }
     }
   } else if (ZG) {
@@ -189,6 +217,7 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
       }
       p[i] -= sgn * h.lr * gg;
       if (ZG) g[i] = G(0);
+      if (tr.shadow_map) shadow_store(tr, i, p[i]);
     }
   } else if (ZG) {
     constexpr int CH = J * 4 * kThreads;

@@ -96,7 +96,7 @@ class _FusedBase(torch.optim.Optimizer):
         if len(gd) != 1 or next(iter(gd)) not in (torch.float32, torch.bfloat16):
             raise RuntimeError(f"{type(self).__name__}: unsupported gradient dtypes {gd}")
         self._gdtype = 0 if torch.float32 in gd else 1
-        key = tuple((gi, p.data_ptr(), p.grad.data_ptr()) for gi, p in active)
+        key = tuple((gi, p.data_ptr(), p.grad.data_ptr()) + self._shadow_ptrs(p) for gi, p in active)
         if key != self._key:
             self._build_tables(active, device)
             self._key = key
@@ -124,14 +124,31 @@ class _FusedBase(torch.optim.Optimizer):
         for ti, (gi, p) in enumerate(active):
             st = self.state[p]
             s = [st[k].data_ptr() for k in self.STATE_KEYS] + [0] * (2 - len(self.STATE_KEYS))
-            recs += [p.data_ptr(), p.grad.data_ptr(), s[0], s[1], p.numel(), gi]
+            recs += [p.data_ptr(), p.grad.data_ptr(), s[0], s[1], p.numel(), gi, *self._shadow_ptrs(p)]
             for c in range((p.numel() + chunk - 1) // chunk):
                 blocks += [ti, c]
         t_host = torch.tensor(recs, dtype=torch.int64).pin_memory()
         b_host = torch.tensor(blocks, dtype=torch.int32).pin_memory()
         self._tables = (t_host.to(device, non_blocking=True), b_host.to(device, non_blocking=True))
         self._nblocks = len(blocks) // 2
+        for _, p in active:  # the kernel now keeps these parameters' bf16 shadows current
+            if self._shadow_ptrs(p)[0]:
+                p._rocket_shadow_live = True
         self.version += 1
+
+    @staticmethod
+    def _shadow_ptrs(p) -> tuple:
+        """(index-map, bf16 buffer) pointers of a parameter's registered bf16 shadow, or (0, 0).
+
+        A consumer registers ``p._rocket_bf16_shadow = (index int32 [numel, 2], bf16 buffer)``;
+        every update then also writes bf16(p[i]) to ``buffer[index[i, 0/1]]`` (-1 = skip)."""
+        sh = getattr(p, "_rocket_bf16_shadow", None)
+        if sh is None:
+            return (0, 0)
+        idx, buf = sh
+        if idx.dtype != torch.int32 or idx.shape != (p.numel(), 2) or buf.dtype != torch.bfloat16 or idx.device != p.device:
+            raise RuntimeError("bf16 shadow: expected an int32 [numel, 2] index map and a bf16 buffer on the device")
+        return (idx.data_ptr(), buf.data_ptr())
 
     # --------------------------------------------------------- device side
     def launch(self, zero_grads: bool = False) -> None:

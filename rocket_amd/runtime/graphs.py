@@ -162,7 +162,10 @@ class StepGraphs:
         return v
 
     def _tokens(self):
-        return tuple(t() for t in self._toks)
+        # parameter versions: weights rewritten outside the captured step (checkpoint load, manual
+        # edits) invalidate the graphs — captured kernels may depend on derived state of them
+        # (e.g. the fused LeNet's optimizer-maintained bf16 fragment table)
+        return tuple(t() for t in self._toks) + (sum(p._version for p in self.mod._module.parameters()),)
 
     def _predict_sync(self) -> bool:
         engine = self.mod._accelerator

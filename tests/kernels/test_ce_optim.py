@@ -115,3 +115,38 @@ def test_ce_train_one_launch(C, dtype):
     torch.testing.assert_close(dx.float(), xr.grad, rtol=2e-2 if dtype == torch.bfloat16 else 1e-4, atol=1e-5)
     assert abs(float(ring[7]) - (0.5 + 2.0 * float(lr))) < 1e-3  # acc + scale*loss reported
     assert int(slot) == 0 and float(acc) == 0.0  # ring cursor wrapped, window reset
+
+
+def test_optimizer_maintains_lenet_fragment_table():
+    """The fused AdamW writes the bf16 MFMA fragment table of a fused LeNet while updating the
+    weights (registered bf16 shadows): after a step the table equals a fresh lenet_prep of the
+    new weights bit for bit, and the next forward skips the prep launch."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops import _lib
+    from rocket_amd.ops.lenet import lenet_forward
+    from rocket_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(4)
+    net = LeNet(fused=True).cuda()
+    opt = FusedAdamW(net.parameters(), lr=1e-2)
+    x = torch.rand(64, 1, 28, 28, device="cuda")
+    for _ in range(3):
+        y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
+        y.square().mean().backward()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+    frags = net.conv1._rocket_fragments
+    torch.cuda.synchronize()
+    ref = torch.empty_like(frags.frag)
+    ws = [p.detach() for p in (net.fc1.weight, net.fc2.weight, net.fc3.weight, net.conv1.weight, net.conv2.weight)]
+    _lib.check(_lib.kernels().rk_lenet_prep(*[w.data_ptr() for w in ws], ref.data_ptr(), _lib.stream_ptr(x.device)),
+               "rk_lenet_prep")
+    torch.cuda.synchronize()
+    assert torch.equal(frags.frag.view(torch.int16), ref.view(torch.int16))
+    v = frags.versions
+    lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
+    assert frags.versions == v  # live table: no prep
+    with torch.no_grad():
+        net.fc2.weight.mul_(0.5)  # an outside write bumps the version -> prep on the next forward
+    lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
+    assert frags.versions != v

@@ -32,3 +32,18 @@ def test_tuned_gemm_table_is_valid_csv():
                                              if r[0] == "Validator")
     results = [r for r in rows if r[0] != "Validator"]
     assert results and all(len(r) == 4 and float(r[3]) > 0 for r in results)
+
+
+def test_lenet_fragment_index_maps_cover_every_weight_once():
+    """Every LeNet weight element has exactly one forward-layout slot in the fused kernels'
+    fragment table (and fc / conv2 weights one input-gradient slot); no slot is shared."""
+    import numpy as np
+
+    from rocket_amd.ops.lenet import _NFRAG, _frag_index_maps
+
+    maps = _frag_index_maps()
+    slots = np.concatenate([m[m >= 0] for m in maps])
+    assert len(np.unique(slots)) == len(slots) and slots.max() < _NFRAG * 64 * 8
+    for name, m, has_bwd in zip(("fc1", "fc2", "fc3", "conv1", "conv2"), maps, (1, 1, 1, 0, 1)):
+        assert (m[:, 0] >= 0).all(), name
+        assert ((m[:, 1] >= 0).all() if has_bwd else (m[:, 1] < 0).all()), name
