@@ -60,10 +60,10 @@ def main():
     x = torch.rand(a.batch, 1, 28, 28, device=dev)
     y = torch.randint(0, 10, (a.batch,), device=dev)
     blocks = a.batch // 4
-    ftr = torch.zeros(blocks, 16, dtype=torch.int64, device=dev)
-    btr = torch.zeros(blocks, 16, dtype=torch.int64, device=dev)
+    ftr = torch.zeros(blocks, 48, dtype=torch.int64, device=dev)
+    btr = torch.zeros(blocks, 48, dtype=torch.int64, device=dev)
     lib.rk_lenet_set_trace(ftr.data_ptr(), btr.data_ptr())
-    fw, bw = [], []
+    fw, bw, waves = [], [], []
     try:
         for step in range(a.steps):
             with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -75,6 +75,10 @@ def main():
             if step >= a.steps // 2:
                 fw.append(summarize(ftr.cpu(), FWD, list(range(9))))
                 bw.append(summarize(btr.cpu(), BWD, BWD_MARKS))
+                b = btr.cpu().double()
+                start = b[:, 8:9]  # after scatter + sync: phase B begins
+                waves.append({"dW2_done_us": ((b[:, 16:26] - start).median(0).values * 0.01).tolist(),
+                              "dgrad_done_us": ((b[:, 32:48] - start).median(0).values * 0.01).tolist()})
     finally:
         lib.rk_lenet_set_trace(None, None)
 
@@ -89,6 +93,10 @@ def main():
 
     print(json.dumps({"kernel": "lenet_fwd", "batch": a.batch, "phases": avg(fw)}))
     print(json.dumps({"kernel": "lenet_bwd", "batch": a.batch, "phases": avg(bw)}))
+    n = len(waves)
+    print(json.dumps({"kernel": "lenet_bwd phase B per wave (us after phase start, median over blocks)",
+                      "dW2_done": [round(sum(w["dW2_done_us"][i] for w in waves) / n, 2) for i in range(10)],
+                      "dgrad_done": [round(sum(w["dgrad_done_us"][i] for w in waves) / n, 2) for i in range(16)]}))
 
 
 if __name__ == "__main__":

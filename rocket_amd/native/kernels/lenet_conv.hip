@@ -35,10 +35,18 @@ constexpr int K1P = KS * 6;        // 30: conv1 reduction with kw padded to 6 (f
 __device__ __forceinline__ __bf16 tobf(float v) { return (__bf16)v; }
 
 // Optional phase timeline (diagnostics): thread 0 of every block stamps s_memrealtime (100 MHz)
-// at phase boundaries into trace[block][16]; a null trace pointer costs one uniform branch.
+// at phase boundaries into trace[block][0..15]; RK_TRW stamps lane 0 of EVERY wave into
+// trace[block][base + wave] (per-wave view of a phase).  A null trace pointer costs one uniform branch.
+constexpr int kTraceStride = 48;
 #define RK_TR(tr, k)                                                                              \
   do {                                                                                            \
-    if ((tr) != nullptr && threadIdx.x == 0) (tr)[(int64_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if ((tr) != nullptr && threadIdx.x == 0)                                                      \
+      (tr)[(int64_t)blockIdx.x * kTraceStride + (k)] = __builtin_amdgcn_s_memrealtime();          \
+  } while (0)
+#define RK_TRW(tr, base)                                                                          \
+  do {                                                                                            \
+    if ((tr) != nullptr && (threadIdx.x & 63) == 0)                                               \
+      (tr)[(int64_t)blockIdx.x * kTraceStride + (base) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 // Elements (x, x+1) of a bf16 row held twice (c0[i] = v[i], c1[i] = v[i+1]): one aligned 4-byte
@@ -183,7 +191,7 @@ struct ClsFwd {  // classifier operands of the fused forward
   const float *fb1, *fb2, *fb3;
   uint16_t *a2T, *h1T, *h2T;  // transposed activations [features][N] for the weight gradients
   float* logits;              // [N][10]
-  uint64_t* trace;            // optional phase timeline [blocks][16]
+  uint64_t* trace;            // optional phase timeline [blocks][kTraceStride]
 };
 
 template <bool MLP>
@@ -408,7 +416,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
 //           weight-gradient launch) or global f32 atomics (generic path)
 constexpr int DC = 18;             // dConv2 image side: 10 + 2*4 zero ring
 constexpr int DCN = DC * DC * C2;  // 5184, channel-last [y][x][co]; zero pixel at DCN
-constexpr int DTS = 128;           // row stride of dConv2^T [co][position] (100 used, zero padded)
+constexpr int DTS = 136;           // row stride of dConv2^T [co][position] (100 used, zero padded; 272 B: rows on distinct LDS slots)
 constexpr int K2P = 13;            // conv2-dgrad k-steps: (kh,kw,co) = 400 -> 416
 // fused path: per-block conv-gradient slab row [dW1 150 | db1 6 | dW2 2400 | db2 16] (+pad)
 constexpr int SL_W1 = 0, SL_B1 = SL_W1 + C1 * R1, SL_W2 = SL_B1 + C1, SL_B2 = SL_W2 + C2 * R2;
@@ -427,7 +435,6 @@ struct BwdSmem {
   uint16_t dc2[SPB][DCN + 16];      // dense channel-last dConv2 with zero ring; zero pixel at DCN
                                     // (after phase B: the 16 waves' dW1 partials [16][2][256] f32)
   uint16_t dcT[SPB][C2 * DTS];      // dConv2^T [co][p = 4*window + quadrant] (wgrad2 A operand)
-  float rb1[NTHR / 64][16];         // db1 partials of the 16 waves (their dW1 partials alias dc2)
   bf16x8 wfr[K2P * 64];             // conv2-dgrad B fragments
   // fused classifier backward (MLP=true): gradients of the 4 samples as MFMA A rows
   uint16_t dyl[SPB][DYP];           // dlogits, K pad 10..39 zero
@@ -465,7 +472,7 @@ struct ClsBwd {
   int ring_size;
   float acc_scale;
   int sync;
-  uint64_t* trace;                  // optional phase timeline [blocks][16]
+  uint64_t* trace;                  // optional phase timeline [blocks][kTraceStride]
   float* slab;                      // [blocks][SLABW] conv weight/bias gradient partials
 };
 
@@ -674,51 +681,72 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
     }
     if (threadIdx.x < SPB * 8) {
       const int sl = threadIdx.x >> 3, k = threadIdx.x & 7;
-      sm.a1[sl][A1N + k] = 0;
+      // zero pair at [0..1], bf16 ones pair at [2..3]: the B operand of the "ones column" whose
+      // MFMA output is the bias gradient (row sums of the A operand)
+      const uint16_t zo = (k == 2 || k == 3) ? (uint16_t)0x3F80 : (uint16_t)0;
+      sm.a1[sl][A1N + k] = zo;
       sm.a1o[sl][A1N - 1 + k] = 0;
       sm.c1[sl][A1N + k] = 0xFE;
-      sm.imgb[sl][0][IMGN + k] = 0;
+      sm.imgb[sl][0][IMGN + k] = zo;
       sm.imgb[sl][1][IMGN - 1 + k] = 0;
     }
     __syncthreads();
     RK_TR(cb.trace, 8);
 
     // ---- phase B: conv2 dgrad (4 samples x 13 pixel tiles) and dW2 (10 column tiles), which
-    // needs only dcT and a1: waves 0..9 take one dW2 tile + one dgrad tile, waves 10..15 seven
-    // dgrad tiles each (LDS-bound work split evenly; dW1, which needs dx2, follows on all waves)
-    float accb2 = 0.f;                       // waves 0..9: db2 partial (lane lo = co)
-    f32x4 g2 = {0.f, 0.f, 0.f, 0.f};         // waves 0..9: dW2 tile u = wave
+    // needs only dcT and a1: waves 0..9 take one dW2 tile + two dgrad tiles, waves 10..15 five or
+    // six dgrad tiles each.  Per-lane address offsets are hoisted out of the tile loops (the phase is
+    // VALU-issue-bound, not MFMA- or LDS-bound), and the bias gradients come out of the MFMAs as
+    // "ones columns" (B column r = R2 of dW2 / r = R1 of dW1 is all ones -> C = row sums of A).
+    f32x4 g2 = {0.f, 0.f, 0.f, 0.f};         // waves 0..9: dW2 tile u = wave (col r = 150: db2)
     if (wave < 10) {
       // dW2 tile u = wave: rows co (16), cols r = 16u + lo; K = positions of 4 samples (4 x 4 k-steps)
       const int u = wave;
       const int r = 16 * u + lo;
       const int cof = r < R2 ? (r / R1) * (Q1 * Q1) + ((r / KS) % KS) * Q1 + (r % KS) : -100000;
-      for (int sl = 0; sl < SPB; ++sl) {
-        const uint16_t* a1s = sm.a1[sl];
-        const uint16_t* a1os = sm.a1o[sl];
-#pragma unroll 2
-        for (int ks = 0; ks < 4; ++ks) {
-          // positions p = 32ks + 8hi + j, window-major: windows wa = 8ks+2hi (j<4), wa+1 (j>=4)
-          const bf16x8 a = *(const bf16x8*)(sm.dcT[sl] + lo * DTS + 32 * ks + 8 * hi);  // A[co=lo][p]
-          const int wa = 8 * ks + 2 * hi, wb = wa + 1;
-          const int pa = wa < Q2 * Q2 && cof >= 0 ? pos2(wa, 0) + cof : -100000;
-          const int pb = wb < Q2 * Q2 && cof >= 0 ? pos2(wb, 0) + cof : -100000;
+      // B element j of k-step ks at a1 offset (j<4 ? pa : pb) + ((j&3)>>1)*Q1 + (j&1): 4 pairs,
+      // each one aligned 4-byte read from a1 (even x) or a1o (odd x), relative to sample 0's a1
+      constexpr int A1O = (int)(offsetof(BwdSmem, a1o) - offsetof(BwdSmem, a1)) / 2;
+      int pofs[4][4];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) accb2 += (float)a[j];
-          // B[k = p][col = r]: element j at (j<4 ? pa : pb) + ((j&3)>>1)*Q1 + (j&1) = 4 pairs
-          uint32_t w4[4];
+      for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int xq = (k < 2 ? pa : pb) + (k & 1) * Q1;
-            w4[k] = pair_at(a1s, a1os, xq >= 0 ? xq : A1N);
-          }
-          const bf16x8 b = __builtin_bit_cast(bf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
-          g2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, g2, 0, 0, 0);
+        for (int k = 0; k < 4; ++k) {
+          const int wv = 8 * ks + 2 * hi + (k >> 1);
+          int x = (wv < Q2 * Q2 && cof >= 0) ? pos2(wv, 0) + cof + (k & 1) * Q1 : A1N;
+          if (r == R2) x = A1N + 2;  // ones pair -> db2
+          pofs[ks][k] = (x & 1) ? A1O + x - 1 : x;
         }
+      const uint16_t* a1b = &sm.a1[0][0];
+      // 16 k-steps (4 samples x 4), operands of step i + 1 read before step i's MFMA
+      auto ld_a = [&](int i) {  // A[co = lo][p]
+        return *(const bf16x8*)(sm.dcT[i >> 2] + lo * DTS + 32 * (i & 3) + 8 * hi);
+      };
+      auto ld_b = [&](int i) {
+        const uint16_t* a1s = a1b + (i >> 2) * (A1N + 8);
+        const int ks = i & 3;
+        return make_uint4(*(const uint32_t*)(a1s + pofs[ks][0]), *(const uint32_t*)(a1s + pofs[ks][1]),
+                          *(const uint32_t*)(a1s + pofs[ks][2]), *(const uint32_t*)(a1s + pofs[ks][3]));
+      };
+      bf16x8 a_cur = ld_a(0);
+      uint4 b_cur = ld_b(0);
+#pragma unroll
+      for (int i = 0; i < 4 * SPB; ++i) {
+        bf16x8 a_nxt = a_cur;
+        uint4 b_nxt = b_cur;
+        if (i + 1 < 4 * SPB) {
+          a_nxt = ld_a(i + 1);
+          b_nxt = ld_b(i + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        g2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_cur, __builtin_bit_cast(bf16x8, b_cur), g2, 0, 0, 0);
+        a_cur = a_nxt;
+        b_cur = b_nxt;
       }
     }
+    RK_TRW(cb.trace, 16);  // per wave: dW2 tile done
     {
-      constexpr int NDG = SPB * 13, NHEAVY = 42;  // dgrad tiles; [0, 42) -> waves 10..15
+      constexpr int NDG = SPB * 13, NHEAVY = 32;  // dgrad tiles; [0, 32) -> waves 10..15, rest 2 per wave 0..9
       const int t_begin = wave >= 10 ? wave - 10 : NHEAVY + wave;
       const int t_step = wave >= 10 ? 6 : 10;
       const int t_end = wave >= 10 ? NHEAVY : NDG;
@@ -729,22 +757,43 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
 #pragma unroll
         for (int s = 0; s < K2P; ++s) wr[s] = sm.wfr[s * 64 + lane];
       }
+      // pixel (ih, iw) reads dConv2 pixel (ih + 4 - kh, iw + 4 - kw), tap kk = 2s + hi/2; the pad
+      // tap kk = 25 has zero weights, so it may read any finite pixel (clamped to tap 24)
+      int toff[K2P];
+#pragma unroll
+      for (int s = 0; s < K2P; ++s) {
+        const int kk = min(2 * s + (hi >> 1), R1 - 1);
+        toff[s] = ((4 - kk / KS) * DC + (4 - kk % KS)) * C2 + 8 * (hi & 1);
+      }
       for (int tt = t_begin; tt < t_end; tt += t_step) {
         const int sl = tt / 13, t = tt % 13;
-        const int pix = 16 * t + lo;  // A row of this lane
+        const int pix = 16 * t + lo;  // A row of this lane (pixels >= 196: rows discarded below)
         const bool pv = pix < Q1 * Q1;
         const int ih = pv ? pix / Q1 : 0, iw = pv ? pix % Q1 : 0;
-        const int base = ih * DC + iw;  // pixel (ih, iw) reads dConv2 pixel (ih + 4 - kh, iw + 4 - kw)
-        const uint16_t* dc = sm.dc2[sl];
+        const uint16_t* ab = sm.dc2[sl] + (ih * DC + iw) * C2;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        // A operands in chunks of 4 k-steps, the next chunk's LDS reads issued before this
+        // chunk's MFMAs (one read + wait per MFMA would expose the LDS latency every step)
+        constexpr int CH = 4, NCH = (K2P + CH - 1) / CH;
+        bf16x8 abuf[2][CH];
 #pragma unroll
-        for (int s = 0; s < K2P; ++s) {
-          const int kk = 2 * s + (hi >> 1);  // (kh, kw) pair of this lane's 8 k values (8 channels)
-          const bool ok = pv && kk < R1;
-          const int px = ok ? base + (4 - kk / KS) * DC + (4 - kk % KS) : DC * DC;  // DC*DC -> zero pixel
-          const bf16x8 a = *(const bf16x8*)(dc + px * C2 + 8 * (hi & 1));
-          if constexpr (MLP) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wr[s], acc, 0, 0, 0);
-          else acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, sm.wfr[s * 64 + lane], acc, 0, 0, 0);
+        for (int q = 0; q < CH; ++q) abuf[0][q] = *(const bf16x8*)(ab + toff[q]);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          if (c + 1 < NCH) {
+#pragma unroll
+            for (int q = 0; q < CH; ++q)
+              if ((c + 1) * CH + q < K2P) abuf[(c + 1) & 1][q] = *(const bf16x8*)(ab + toff[(c + 1) * CH + q]);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this chunk's MFMAs
+#pragma unroll
+          for (int q = 0; q < CH; ++q) {
+            const int s = c * CH + q;
+            if (s < K2P) {
+              if constexpr (MLP) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(abuf[c & 1][q], wr[s], acc, 0, 0, 0);
+              else acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(abuf[c & 1][q], sm.wfr[s * 64 + lane], acc, 0, 0, 0);
+            }
+          }
         }
         // C[row = pixel 16t + 4hi + i][col = ci = lo]
         if (lo < C1) {
@@ -756,18 +805,31 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
         }
       }
     }
+    RK_TRW(cb.trace, 32);  // per wave: dgrad tiles done
     __syncthreads();
     RK_TR(cb.trace, 9);
 
-    // ---- phase C: dW1 on all 16 waves (4 x 25 k-steps over the positions of the 14x14 pool grid)
+    // ---- phase C: dW1 on all 16 waves (4 x 25 k-steps over the positions of the 14x14 pool grid);
+    // column r = 25 of tile u = 1 is the ones column (db1)
     f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    float sb1 = 0.f;
     {
-      int cw[2];
+      // B element j of tile u at img offset pa(window) + cst[u][k]: the pair's copy (x & 1) does
+      // not depend on the window (pos1 offsets are even), so it is folded into cst once
+      int cst[2][4], pm[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int r = 16 * u + lo;
-        cw[u] = r < R1 ? (r / KS) * IMGS + (r % KS) : -100000;
+        const bool tap = r < R1;
+        pm[u] = tap ? 1 : 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (tap) {
+            const int x = (k & 1) * IMGS + (r / KS) * IMGS + (r % KS);
+            cst[u][k] = (x & 1) ? (IMGN + 8) + x - 1 : x;  // copy 1 holds img[x] at x - 1
+          } else {
+            cst[u][k] = r == R1 ? IMGN + 2 : IMGZ;  // ones pair (db1) / zero pair
+          }
+        }
       }
       for (int it = wave; it < SPB * 25; it += NTHR / 64) {
         const int sl = it / 25, ks = it % 25;
@@ -775,25 +837,23 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
         const bool va = lo < C1 && wa < Q1 * Q1, vb = lo < C1 && wb < Q1 * Q1;
         const int ia = va ? lo * 196 + wa : A1N, ib = vb ? lo * 196 + wb : A1N;
         const float da = sm.dx2[sl][va ? ia : 0], dbv = sm.dx2[sl][vb ? ib : 0];
-        const uint8_t ca = sm.c1[sl][ia], cb = sm.c1[sl][ib];
-        const int pa = wa < Q1 * Q1 ? pos1(wa, 0) : -100000, pb = wb < Q1 * Q1 ? pos1(wb, 0) : -100000;
-        bf16x8 a;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = j < 4 ? (ca == (j & 3) ? da : 0.f) : (cb == (j & 3) ? dbv : 0.f);
-          a[j] = tobf(v);
-          sb1 += v;
-        }
+        const uint32_t ca = sm.c1[sl][ia], cb = sm.c1[sl][ib];
+        // windows past the grid have an all-zero A; clamp them to a valid window for B
+        const int pa = pos1(min(wa, Q1 * Q1 - 1), 0), pb = pos1(min(wb, Q1 * Q1 - 1), 0);
+        const uint32_t ab = f2bf(da), bb = f2bf(dbv);
+        const uint4 aw = make_uint4((ca == 0 ? ab : 0u) | (ca == 1 ? ab << 16 : 0u),
+                                    (ca == 2 ? ab : 0u) | (ca == 3 ? ab << 16 : 0u),
+                                    (cb == 0 ? bb : 0u) | (cb == 1 ? bb << 16 : 0u),
+                                    (cb == 2 ? bb : 0u) | (cb == 3 ? bb << 16 : 0u));
+        const bf16x8 a = __builtin_bit_cast(bf16x8, aw);
+        const uint16_t* ib0 = &sm.imgb[sl][0][0];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          uint32_t w4[4];  // element j at (j<4 ? pa : pb) + ((j&3)>>1)*IMGS + (j&1) + cw: 4 pairs
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int xq = (k < 2 ? pa : pb) + (k & 1) * IMGS + cw[u];
-            w4[k] = pair_at(sm.imgb[sl][0], sm.imgb[sl][1], xq >= 0 ? xq : IMGZ);
-          }
-          const bf16x8 b = __builtin_bit_cast(bf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
-          g1[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, g1[u], 0, 0, 0);
+          const uint4 w = make_uint4(*(const uint32_t*)(ib0 + pa * pm[u] + cst[u][0]),
+                                     *(const uint32_t*)(ib0 + pa * pm[u] + cst[u][1]),
+                                     *(const uint32_t*)(ib0 + pb * pm[u] + cst[u][2]),
+                                     *(const uint32_t*)(ib0 + pb * pm[u] + cst[u][3]));
+          g1[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, w), g1[u], 0, 0, 0);
         }
       }
     }
@@ -803,20 +863,16 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
     // gradient slab (summed by the weight-gradient launch that follows: no contended atomics);
     // the generic path adds them to the gradients with global atomics
     float* srow = MLP ? cb.slab + (int64_t)blockIdx.x * SLABW : nullptr;
-    if (wave < 10) {
+    if (wave < 10) {  // C[row = co 4hi + i][col = r]; column r = R2 holds db2
       const int u = wave, col = 16 * u + lo;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
         if (col < R2) {
           if (MLP) srow[SL_W2 + (4 * hi + i) * R2 + col] = g2[i];
           else atomicAdd(dw2 + (4 * hi + i) * R2 + col, g2[i]);
-        }
-      if (u == 0) {  // db2[co]: lanes lo, lo+16, lo+32, lo+48 hold parts of channel lo
-        accb2 += __shfl_xor(accb2, 16, 64);
-        accb2 += __shfl_xor(accb2, 32, 64);
-        if (hi == 0) {
-          if (MLP) srow[SL_B2 + lo] = accb2;
-          else if (db2) atomicAdd(db2 + lo, accb2);
+        } else if (col == R2) {
+          if (MLP) srow[SL_B2 + 4 * hi + i] = g2[i];
+          else if (db2) atomicAdd(db2 + 4 * hi + i, g2[i]);
         }
       }
     }
@@ -826,29 +882,24 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int i = 0; i < 4; ++i) red1[wave][u][(4 * hi + i) * 16 + lo] = g1[u][i];
-      sb1 += __shfl_xor(sb1, 16, 64);
-      sb1 += __shfl_xor(sb1, 32, 64);
-      if (hi == 0) sm.rb1[wave][lo] = sb1;
     }
     __syncthreads();
     RK_TR(cb.trace, 10);
-    for (int e = threadIdx.x; e < 2 * 256; e += NTHR) {
+    for (int e = threadIdx.x; e < 2 * 256; e += NTHR) {  // column r = R1 (u = 1, lane 9) holds db1
       const int u = e >> 8, row = (e & 255) >> 4, col = 16 * u + (e & 15);
-      if (row < C1 && col < R1) {
+      if (row < C1 && col <= R1) {
         const float (*red1)[2][256] = (const float (*)[2][256])&sm.dc2[0][0];
         float v = 0.f;
 #pragma unroll
         for (int w = 0; w < NTHR / 64; ++w) v += red1[w][u][e & 255];
-        if (MLP) srow[SL_W1 + row * R1 + col] = v;
-        else atomicAdd(dw1 + row * R1 + col, v);
+        if (col < R1) {
+          if (MLP) srow[SL_W1 + row * R1 + col] = v;
+          else atomicAdd(dw1 + row * R1 + col, v);
+        } else {
+          if (MLP) srow[SL_B1 + row] = v;
+          else if (db1) atomicAdd(db1 + row, v);
+        }
       }
-    }
-    if (threadIdx.x < C1) {
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < NTHR / 64; ++w) v += sm.rb1[w][threadIdx.x];
-      if (MLP) srow[SL_B1 + threadIdx.x] = v;
-      else if (db1) atomicAdd(db1 + threadIdx.x, v);
     }
   RK_TR(cb.trace, 11);
   }
@@ -904,7 +955,7 @@ RK_API int rk_lenet_frag_bytes() { return NFRAG * 64 * 16; }
 
 // Whole LeNet forward (conv stack + classifier) for N % 8 == 0: logits [N][10] fp32, plus the
 // saved state of the fused backward (a1, codes) and the transposed activations of the wgrads.
-// Diagnostics: phase timelines of the fused launches ([blocks][16] u64 each, or null = off).
+// Diagnostics: phase timelines of the fused launches ([blocks][48] u64 each, or null = off).
 static uint64_t* g_fwd_trace = nullptr;
 static uint64_t* g_bwd_trace = nullptr;
 RK_API void rk_lenet_set_trace(void* fwd, void* bwd) {
