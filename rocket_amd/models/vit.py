@@ -5,7 +5,8 @@ patches + [CLS] = 197 tokens, width 768.
 
 MI355X path: LayerNorm is the one-wave-per-row HIP kernel emitting bf16 straight
 into the next GEMM (:class:`~rocket_amd.ops.norm.FusedLayerNorm`); the GEMMs run
-on the library path (hipBLASLt, bias fused into the epilogue via ``addmm``); attention is
+on the library path (hipBLASLt, bias fused into the epilogue via ``addmm``; the bias gradient is
+one column-sum launch, :class:`~rocket_amd.ops.linear.LibLinear`); attention is
 one fused MFMA kernel reading the packed QKV projection (``native/kernels/attn.hip``), GELU
 a HIP kernel; residual adds are fused into the following LayerNorm.  The residual stream stays
 fp32 (standard AMP numerics); everything feeding a GEMM is bf16.
@@ -20,6 +21,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops.activation import attention_qkv, gelu
+from rocket_amd.ops.linear import LibLinear
 from rocket_amd.ops.norm import FusedLayerNorm
 
 
@@ -27,8 +29,8 @@ class Attention(nn.Module):
     def __init__(self, dim: int, heads: int):
         super().__init__()
         self.heads = heads
-        self.qkv = nn.Linear(dim, 3 * dim)
-        self.proj = nn.Linear(dim, dim)
+        self.qkv = LibLinear(dim, 3 * dim)
+        self.proj = LibLinear(dim, dim)
 
     def forward(self, x):
         # fused MFMA attention straight from the packed projection (no head permutes)
@@ -38,8 +40,8 @@ class Attention(nn.Module):
 class Mlp(nn.Module):
     def __init__(self, dim: int, hidden: int):
         super().__init__()
-        self.fc1 = nn.Linear(dim, hidden)
-        self.fc2 = nn.Linear(hidden, dim)
+        self.fc1 = LibLinear(dim, hidden)
+        self.fc2 = LibLinear(hidden, dim)
 
     def forward(self, x):
         return self.fc2(gelu(self.fc1(x)))

@@ -229,6 +229,46 @@ __global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && a.nbt) a.nbt[0] += 1;
 }
 
+// Column sums of a [R][C] tensor accumulated into out[C] (+=): the bias gradient of a linear layer
+// (sum of d(out) over the rows).  Same grid / two-level reduction as bn_stats, one tensor stream.
+template <typename T>
+__global__ void __launch_bounds__(BN_T) colsum_acc_kernel(const T* __restrict__ x, int64_t R, int C, int rpb,
+                                                          float* part, unsigned* counters, float* out) {
+  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ float s1[BN_CT], s2[BN_CT];
+  __shared__ int flag;
+  const int c0 = blockIdx.x * BN_CT;
+  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int c = c0 + cg * 8;
+  const bool cok = c < C;
+  const int64_t r0 = (int64_t)blockIdx.y * rpb;
+  const int64_t r1 = min(R, r0 + rpb);
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  for (int64_t r = r0 + rg; r < r1; r += BN_US * BN_RG) {
+    float v[BN_US][8];
+#pragma unroll
+    for (int u = 0; u < BN_US; ++u) V8<T>::load(x + min(r + u * BN_RG, r1 - 1) * C + (cok ? c : 0), v[u]);
+#pragma unroll
+    for (int u = 0; u < BN_US; ++u) {
+      const bool ok = r + u * BN_RG < r1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += ok ? v[u][k] : 0.f;
+    }
+  }
+  if (!cok) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  }
+  reduce_rowgroups(acc, lds, s1);
+  if (threadIdx.x < BN_CT) s2[threadIdx.x] = 0.f;
+  float t1, t2;
+  if (!bn_column_reduce(s1, s2, part, C, c0, counters, t1, t2, &flag)) return;
+  const int cc = c0 + (threadIdx.x >> 2);
+  if ((threadIdx.x & 3) == 0 && cc < C) out[cc] += t1;
+}
+
 // Elementwise passes: thread t owns channel vector cv = t % CV (CV = C/8 <= 256) for the whole
 // launch, so its per-channel coefficients live in registers (loaded once), and walks rows
 // r = r0 + t / CV, stepping by RPP = BN_T / CV rows; 4 rows per iteration with clamped
@@ -652,6 +692,21 @@ static int bn_elem_rows(int64_t R, int C, int* grid) {
   if (per < rpp) per = rpp;
   *grid = (int)((R + per - 1) / per);
   return (int)per;
+}
+
+// out[c] += sum_r x[r][c]  (x: [R][C], dt 0 f32 / 1 bf16, C % 8 == 0); ws: rk_bn_workspace(R, C)
+// floats, counters: rk_bn_counters(C) zeroed uints (self-resetting)
+RK_API int rk_colsum_acc(int dt, const void* x, int64_t R, int C, float* out, float* ws, unsigned* counters,
+                         hipStream_t s) {
+  if (C % 8 || R <= 0) return (int)hipErrorInvalidValue;
+  int rpb;
+  const int rb = bn_grid_rows(R, C, &rpb);
+  dim3 grid((C + BN_CT - 1) / BN_CT, rb);
+  if (dt == BF16)
+    colsum_acc_kernel<uint16_t><<<grid, BN_T, 0, s>>>((const uint16_t*)x, R, C, rpb, ws, counters, out);
+  else
+    colsum_acc_kernel<float><<<grid, BN_T, 0, s>>>((const float*)x, R, C, rpb, ws, counters, out);
+  return (int)hipGetLastError();
 }
 
 // y = relu?(x*scale + shift + res?); dt: x dtype, dto: y/res dtype.  mask (uint8 [R][C/8], may be

@@ -66,6 +66,7 @@ KERNEL_SIGS = {
     "rk_bn_apply": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int,
                             c_int, c_void_p]),
     "rk_bn_counters": (c_int, [c_int]),
+    "rk_colsum_acc": (c_int, [c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_bn_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int] + [c_void_p] * 11),
     "rk_ln_fwd": (c_int, [c_int, c_int] + [c_void_p] * 8 + [c_int64, c_int, c_float, c_void_p]),
     "rk_ln_workspace": (c_int64, [c_int64, c_int]),

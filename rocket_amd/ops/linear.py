@@ -164,3 +164,62 @@ class FusedLinear(torch.nn.Linear):
 
     def forward(self, x):
         return linear(x, self.weight, self.bias, self.activation)
+
+
+class _LibLinear(torch.autograd.Function):
+    """``x @ W^T + b`` on the library GEMM (hipBLASLt, bf16 under autocast) whose bias gradient is
+    the column-sum kernel (``rk_colsum_acc``) instead of a generic reduction over the rows of
+    d(out); accumulated straight into a persistent ``bias.grad`` when the engine provides one."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, cdtype):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        w = weight.to(cdtype)
+        y = torch.addmm(bias.to(cdtype), x2.to(cdtype), w.t())
+        ctx.save_for_backward(x2, w)
+        ctx.bias = bias
+        ctx.shape = shape
+        return y.reshape(*shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        bias = ctx.bias
+        N = w.shape[0]
+        dy2 = dy.reshape(-1, N)
+        if dy2.dtype != w.dtype:
+            dy2 = dy2.to(w.dtype)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = (dy2 @ w).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
+        dw = (dy2.t() @ x2.to(w.dtype)).float() if ctx.needs_input_grad[1] else None
+        db = None
+        if ctx.needs_input_grad[2]:
+            direct = _direct(bias)
+            target = bias.grad if direct else torch.zeros(N, dtype=torch.float32, device=dy.device)
+            lib = _lib.kernels()
+            M = dy2.shape[0]
+            ws = torch.empty(int(lib.rk_bn_workspace(M, N)), dtype=torch.float32, device=dy.device)
+            nctr = int(lib.rk_bn_counters(N))
+            _lib.check(lib.rk_colsum_acc(_lib.dtype_code(dy2), dy2.data_ptr(), M, N, target.data_ptr(), ws.data_ptr(),
+                                         _lib.Workspace.get(dy.device).counter_array(f"bn{nctr}", nctr),
+                                         _lib.stream_ptr(dy.device)), "rk_colsum_acc")
+            if direct:
+                grad_ready(bias)
+            else:
+                db = target
+        return dx, dw, db, None
+
+
+class LibLinear(torch.nn.Linear):
+    """``nn.Linear`` (same parameters / state_dict) for the large projections that stay on the
+    library GEMM: under bf16 autocast on a HIP device the bias gradient is one column-sum launch
+    (``rk_colsum_acc``, fp32, into ``bias.grad``) instead of a row reduction plus a bf16->fp32
+    cast and an add; elsewhere it is exactly ``nn.Linear``."""
+
+    def forward(self, x):
+        if (x.is_cuda and self.bias is not None and _autocast_on() and self.out_features % 8 == 0
+                and torch.is_grad_enabled()):
+            return _LibLinear.apply(x, self.weight, self.bias, torch.get_autocast_dtype("cuda"))
+        return super().forward(x)

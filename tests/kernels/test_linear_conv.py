@@ -207,3 +207,26 @@ def test_lenet_fused_backward_deterministic(N):
     for run in grads[1:]:
         for (name, _), a, b in zip(net.named_parameters(), grads[0], run):
             assert torch.equal(a, b), (name, float((a - b).abs().max()))
+
+
+@pytest.mark.parametrize("M,K,N", [(25216, 768, 2304), (100, 64, 24), (37, 16, 8)])
+def test_lib_linear_bias_grad(M, K, N):
+    """LibLinear under bf16 autocast: same output / input and weight gradients as nn.Linear, bias
+    gradient from the column-sum kernel vs the fp32 row sum of d(out)."""
+    from rocket_amd.ops.linear import LibLinear
+
+    torch.manual_seed(1)
+    lin = LibLinear(K, N).cuda()
+    ref = torch.nn.Linear(K, N).cuda()
+    ref.load_state_dict(lin.state_dict())
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    g = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = lin(x)
+        yr = ref(x)
+    y.backward(g)
+    yr.backward(g)
+    assert y.dtype == torch.bfloat16 and torch.equal(y, yr)
+    assert _rel(lin.weight.grad, ref.weight.grad) < 1e-2
+    db = g.float().sum(0)
+    assert _rel(lin.bias.grad, db) < 1e-4, _rel(lin.bias.grad, db)
