@@ -11,7 +11,8 @@
 //
 // Optional bf16 shadows: a tensor record may carry an index map (int32 [n][2], -1 = none) and a
 // bf16 buffer; every updated element is also written, rounded to bf16, to buf[map[i][0]] and
-// buf[map[i][1]].  A kernel that consumes the weights as pre-arranged bf16 MFMA fragments (the
+// buf[map[i][1]] — or, with the map pointer 1 ("dense"), to buf[i] (a bf16 copy of the weights
+// that GEMMs read directly instead of casting the fp32 master every forward).  A kernel that consumes the weights as pre-arranged bf16 MFMA fragments (the
 // fused LeNet's fragment table) then needs no per-step re-layout launch.
 //
 // Optional AMP hooks: `inv_scale` multiplies every gradient (GradScaler unscale
@@ -33,15 +34,34 @@ constexpr int kThreads = 256;
 
 struct TensorRec {  // 8 x int64 per tensor, uploaded from the host
   int64_t p, g, s0, s1, n, group;
-  int64_t shadow_map, shadow_buf;  // int32 [n][2] / bf16 buffer, or 0
+  int64_t shadow_map, shadow_buf;  // int32 [n][2] (or 1 = dense) / bf16 buffer, or 0
 };
 
+constexpr int64_t kDenseShadow = 1;
+
 __device__ __forceinline__ void shadow_store(const TensorRec& tr, int64_t i, float v) {
-  const int2 m = ((const int2*)tr.shadow_map)[i];
   uint16_t* buf = (uint16_t*)tr.shadow_buf;
   const uint16_t b = f2bf(v);
+  if (tr.shadow_map == kDenseShadow) {
+    buf[i] = b;
+    return;
+  }
+  const int2 m = ((const int2*)tr.shadow_map)[i];
   if (m.x >= 0) buf[m.x] = b;
   if (m.y >= 0) buf[m.y] = b;
+}
+// four consecutive elements (i % 4 == 0, 16-byte aligned parameter rows): dense shadows take one
+// 8-byte store
+__device__ __forceinline__ void shadow_store4(const TensorRec& tr, int64_t i, const float4& v) {
+  if (tr.shadow_map == kDenseShadow) {
+    *(uint2*)((uint16_t*)tr.shadow_buf + i) = make_uint2((uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
+                                                         (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+    return;
+  }
+  shadow_store(tr, i, v.x);
+  shadow_store(tr, i + 1, v.y);
+  shadow_store(tr, i + 2, v.z);
+  shadow_store(tr, i + 3, v.w);
 }
 
 struct AdamHyper {  // 8 floats per group
@@ -133,12 +153,7 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
         *(float4*)(m + i) = mm[j];
         *(float4*)(v + i) = vv[j];
         if (ZG) *(float4*)((float*)g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (tr.shadow_map) {
-          shadow_store(tr, i, pp[j].x);
-          shadow_store(tr, i + 1, pp[j].y);
-          shadow_store(tr, i + 2, pp[j].z);
-          shadow_store(tr, i + 3, pp[j].w);
-        }
+        if (tr.shadow_map) shadow_store4(tr, i, pp[j]);
       }
     } else if (vec) {
       for (int64_t i = start + 4 * threadIdx.x; i < end; i += 4 * kThreads) {
@@ -153,12 +168,7 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
           *(float4*)(m + i) = mm;
           *(float4*)(v + i) = vv;
           if (ZG) *(float4*)((float*)g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (tr.shadow_map) {
-            shadow_store(tr, i, pp.x);
-            shadow_store(tr, i + 1, pp.y);
-            shadow_store(tr, i + 2, pp.z);
-            shadow_store(tr, i + 3, pp.w);
-          }
+          if (tr.shadow_map) shadow_store4(tr, i, pp);
         } else {
           for (int64_t k = i; k < end; ++k) {
             upd(p[k], gload<G>(g, k), m[k], v[k]);

@@ -172,11 +172,11 @@ class _LibLinear(torch.autograd.Function):
     d(out); accumulated straight into a persistent ``bias.grad`` when the engine provides one."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, cdtype):
+    def forward(ctx, x, weight, bias, cdtype, w16, b16):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
-        w = weight.to(cdtype)
-        y = torch.addmm(bias.to(cdtype), x2.to(cdtype), w.t())
+        w = w16 if w16 is not None else weight.to(cdtype)
+        y = torch.addmm(b16 if b16 is not None else bias.to(cdtype), x2.to(cdtype), w.t())
         ctx.save_for_backward(x2, w)
         ctx.bias = bias
         ctx.shape = shape
@@ -209,17 +209,41 @@ class _LibLinear(torch.autograd.Function):
                 grad_ready(bias)
             else:
                 db = target
-        return dx, dw, db, None
+        return dx, dw, db, None, None, None
+
+
+def _bf16_copy(module, name: str, p: torch.Tensor):
+    """bf16 copy of parameter ``p``, registered as its dense bf16 shadow: a fused optimizer keeps
+    it current while updating ``p`` (no per-forward cast).  Re-cast here whenever ``p`` was written
+    by anything else (its autograd version moved) or no fused optimizer maintains it."""
+    buf = getattr(module, name, None)
+    if buf is None or buf.shape != p.shape or buf.device != p.device or buf.stride() != p.stride():
+        buf = torch.empty_like(p, dtype=torch.bfloat16)
+        setattr(module, name, buf)
+        setattr(module, name + "_version", None)
+        p._rocket_bf16_shadow = (None, buf)
+    if not (getattr(p, "_rocket_shadow_live", False) and getattr(module, name + "_version") == p._version):
+        with torch.no_grad():
+            buf.copy_(p)
+        setattr(module, name + "_version", p._version)
+    return buf
 
 
 class LibLinear(torch.nn.Linear):
     """``nn.Linear`` (same parameters / state_dict) for the large projections that stay on the
     library GEMM: under bf16 autocast on a HIP device the bias gradient is one column-sum launch
     (``rk_colsum_acc``, fp32, into ``bias.grad``) instead of a row reduction plus a bf16->fp32
-    cast and an add; elsewhere it is exactly ``nn.Linear``."""
+    cast and an add, and the GEMM reads a bf16 weight copy that a fused optimizer maintains
+    (dense bf16 shadow) instead of casting the fp32 master every forward; elsewhere it is exactly
+    ``nn.Linear``."""
 
     def forward(self, x):
         if (x.is_cuda and self.bias is not None and _autocast_on() and self.out_features % 8 == 0
                 and torch.is_grad_enabled()):
-            return _LibLinear.apply(x, self.weight, self.bias, torch.get_autocast_dtype("cuda"))
+            cdtype = torch.get_autocast_dtype("cuda")
+            w16 = b16 = None
+            if cdtype == torch.bfloat16 and self.weight.dtype == torch.float32 and self.weight.is_contiguous():
+                w16 = _bf16_copy(self, "_w16", self.weight)
+                b16 = _bf16_copy(self, "_b16", self.bias)
+            return _LibLinear.apply(x, self.weight, self.bias, cdtype, w16, b16)
         return super().forward(x)

@@ -141,13 +141,20 @@ class _FusedBase(torch.optim.Optimizer):
         """(index-map, bf16 buffer) pointers of a parameter's registered bf16 shadow, or (0, 0).
 
         A consumer registers ``p._rocket_bf16_shadow = (index int32 [numel, 2], bf16 buffer)``;
-        every update then also writes bf16(p[i]) to ``buffer[index[i, 0/1]]`` (-1 = skip)."""
+        every update then also writes bf16(p[i]) to ``buffer[index[i, 0/1]]`` (-1 = skip).  With
+        ``index = None`` the shadow is dense: ``buffer`` is a bf16 tensor laid out like ``p``."""
         sh = getattr(p, "_rocket_bf16_shadow", None)
         if sh is None:
             return (0, 0)
         idx, buf = sh
-        if idx.dtype != torch.int32 or idx.shape != (p.numel(), 2) or buf.dtype != torch.bfloat16 or idx.device != p.device:
-            raise RuntimeError("bf16 shadow: expected an int32 [numel, 2] index map and a bf16 buffer on the device")
+        if buf.dtype != torch.bfloat16 or buf.device != p.device:
+            raise RuntimeError("bf16 shadow: expected a bf16 buffer on the parameter's device")
+        if idx is None:
+            if buf.shape != p.shape or buf.stride() != p.stride():
+                raise RuntimeError("dense bf16 shadow: buffer must have the parameter's shape and layout")
+            return (1, buf.data_ptr())
+        if idx.dtype != torch.int32 or idx.shape != (p.numel(), 2) or idx.device != p.device:
+            raise RuntimeError("bf16 shadow: expected an int32 [numel, 2] index map on the device")
         return (idx.data_ptr(), buf.data_ptr())
 
     # --------------------------------------------------------- device side

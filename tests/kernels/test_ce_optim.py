@@ -150,3 +150,28 @@ def test_optimizer_maintains_lenet_fragment_table():
         net.fc2.weight.mul_(0.5)  # an outside write bumps the version -> prep on the next forward
     lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
     assert frags.versions != v
+
+
+def test_optimizer_maintains_dense_bf16_weight_copy():
+    """LibLinear's bf16 weight copy is a dense bf16 shadow: after fused AdamW steps it equals the
+    bf16 rounding of the fp32 master exactly, and forwards stop re-casting (version unchanged)."""
+    from rocket_amd.ops.linear import LibLinear
+    from rocket_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(6)
+    lin = LibLinear(64, 48).cuda()
+    opt = FusedAdamW(lin.parameters(), lr=1e-2)
+    x = torch.randn(32, 64, device="cuda")
+    for _ in range(3):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = lin(x)
+        y.float().square().mean().backward()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+    torch.cuda.synchronize()
+    assert torch.equal(lin._w16, lin.weight.detach().to(torch.bfloat16))
+    assert torch.equal(lin._b16, lin.bias.detach().to(torch.bfloat16))
+    assert lin._w16_version == lin.weight._version
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ref = torch.nn.functional.linear(x, lin.weight, lin.bias)
+        assert torch.equal(lin(x), ref)
