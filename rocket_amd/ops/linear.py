@@ -20,6 +20,8 @@ otherwise they return fresh gradient tensors to autograd.
 
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -166,6 +168,30 @@ class FusedLinear(torch.nn.Linear):
         return linear(x, self.weight, self.bias, self.activation)
 
 
+def _wgrad_splits(M: int, N: int, K: int) -> int:
+    """K-split of a weight-gradient GEMM dW[N, K] = dY^T X (reduction over M rows): the output
+    has few tiles (ViT: 18-144 tiles of 128x128 for 256 CUs), so the rows are cut into S chunks
+    computed as ONE strided-batched GEMM and summed in fp32.  ``ROCKET_WGRAD_SPLITK=0`` disables."""
+    if os.environ.get("ROCKET_WGRAD_SPLITK", "1") == "0" or M < 4096:
+        return 1
+    tiles = ((N + 127) // 128) * ((K + 127) // 128)
+    s = 1
+    while s < 16 and tiles * s * 2 <= 640 and M % (2 * s) == 0 and M // (2 * s) >= 1024:
+        s *= 2
+    return s
+
+
+def _wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """fp32 dW = dy2^T @ x2 (bf16 operands, fp32 accumulation)."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    s = _wgrad_splits(M, N, K)
+    if s == 1:
+        return (dy2.t() @ x2).float()
+    part = torch.bmm(dy2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K))  # [s, N, K]
+    return part.sum(0, dtype=torch.float32)
+
+
 class _LibLinear(torch.autograd.Function):
     """``x @ W^T + b`` on the library GEMM (hipBLASLt, bf16 under autocast) whose bias gradient is
     the column-sum kernel (``rk_colsum_acc``) instead of a generic reduction over the rows of
@@ -193,7 +219,7 @@ class _LibLinear(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx = (dy2 @ w).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
-        dw = (dy2.t() @ x2.to(w.dtype)).float() if ctx.needs_input_grad[1] else None
+        dw = _wgrad(dy2, x2.to(w.dtype)) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.needs_input_grad[2]:
             direct = _direct(bias)
