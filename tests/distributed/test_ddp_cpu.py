@@ -117,15 +117,16 @@ def _train(world, out_file, bs):
     return net, losses
 
 
-def _launcher_worker(rank, world, port, out):
+def _launcher_worker(rank, world, port, out, bs):
     _env(rank, world, port)
-    _train(world, os.path.join(out, f"r{rank}.json"), bs=4)
+    _train(world, os.path.join(out, f"r{rank}.json"), bs=bs)
 
 
-def test_launcher_two_ranks_equals_global_batch(tmp_path):
-    _run(_launcher_worker, 2, str(tmp_path))
-    net, losses = _train(1, None, bs=8)  # same global batches: rank0 gets batches 0,2,.. rank1 1,3,..
-    for r in range(2):
+@pytest.mark.parametrize("world", [2, 4])
+def test_launcher_ranks_equal_global_batch(tmp_path, world):
+    _run(_launcher_worker, world, str(tmp_path), 8 // world)
+    net, losses = _train(1, None, bs=8)  # same global batches: rank r gets batches r, r+W, ...
+    for r in range(world):
         got = json.load(open(tmp_path / f"r{r}.json"))
         for g, p in zip(got["w"], net.parameters()):
             torch.testing.assert_close(torch.tensor(g), p.detach(), rtol=1e-5, atol=1e-6)
@@ -162,3 +163,23 @@ def test_gather_for_metrics_truncates_padding(tmp_path):
     for r in range(2):
         seen = json.load(open(tmp_path / f"m{r}.json"))
         assert sorted(seen) == list(range(10))
+
+
+def test_bench_multi_rank_cpu(tmp_path):
+    """bench.py under torch.distributed.run with 4 gloo ranks (the driver's N-GPU launch shape, CPU
+    edition): one JSON line from rank 0 with whole-job numbers."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(root, "bench.py"), "--gpus", "4", "--cpu",
+           "--steps", "3", "--warmup", "1", "--batch", "64"]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 4 and rec["steps"] == 3 and rec["config"]["global_batch"] == 256
+    assert rec["config"]["parallelism"] == "dp4" and rec["value"] > 0
