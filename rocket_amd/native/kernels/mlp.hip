@@ -260,25 +260,34 @@ __device__ __forceinline__ void slab_reduce_block(const SlabArgs& s, int j, floa
   const int c = j * 64 + cl;
   const bool ok = c < s.ncols;
   const float* base = s.slab + (ok ? c : 0);
+  // the destination value is read up front (this block is its only writer), and each thread keeps
+  // 32 slab rows in flight at once: the launch is one memory round trip, not four
+  float* dst = nullptr;
+  float old = 0.f;
+  if (threadIdx.x < 64 && ok) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (c >= s.bound[i] && c < s.bound[i + 1] && s.dst[i]) dst = s.dst[i] + (c - s.bound[i]);
+    if (dst) old = *dst;
+  }
+  constexpr int U = 32;
   float acc = 0.f;
   int r = rg;
-  for (; r + 7 * NW < s.rows; r += 8 * NW) {
-    float v[8];
+  for (; r + (U - 1) * NW < s.rows; r += U * NW) {
+    float v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = base[(int64_t)(r + u * NW) * s.width];
+    for (int u = 0; u < U; ++u) v[u] = base[(int64_t)(r + u * NW) * s.width];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc += v[u];
+    for (int u = 0; u < U; ++u) acc += v[u];
   }
   for (; r < s.rows; r += NW) acc += base[(int64_t)r * s.width];
   red[rg][cl] = acc;
   __syncthreads();
-  if (threadIdx.x < 64 && ok) {
+  if (dst) {
     float t = 0.f;
 #pragma unroll
     for (int g = 0; g < NW; ++g) t += red[g][threadIdx.x];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (c >= s.bound[i] && c < s.bound[i + 1] && s.dst[i]) s.dst[i][c - s.bound[i]] += t;
+    *dst = old + t;
   }
 }
 
@@ -308,16 +317,26 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
   const int per = ((a.M + NW * 64 - 1) / (NW * 64)) * 64;  // batch range per wave, multiple of 64
   const int mb = wv * per, me = min(a.M, mb + per);
+  // this block is the only writer of its dW tile / db rows: read their old values up front so the
+  // final accumulate does not wait on a memory round trip
+  float dw_old[32 * 32 / NT];
+#pragma unroll
+  for (int q = 0; q < 32 * 32 / NT; ++q) {
+    const int e = threadIdx.x + q * NT, r = e >> 5, c = e & 31;
+    dw_old[q] = (n0 + r < P.N && k0 + c < P.K) ? P.dw[(int64_t)(n0 + r) * P.K + k0 + c] : 0.f;
+  }
+  const bool has_db = k0 == 0 && P.db && threadIdx.x < 32 && n0 + (int)threadIdx.x < P.N;
+  const float db_old = has_db ? P.db[n0 + threadIdx.x] : 0.f;
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float rs[2] = {0.f, 0.f};
-  for (int m = mb; m < me; m += 64) {  // two k-steps per iteration, all loads issued first
-    bf16x8 af[2][2], bf[2][2];
+  for (int m = mb; m < me; m += 128) {  // four k-steps per iteration, all loads issued first
+    bf16x8 af[4][2], bf[4][2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < 4; ++s) {
       const int mk = m + 32 * s + 8 * hi;
       const int mm = mk < me ? mk : a.M;  // a.M -> zero fragment
 #pragma unroll
@@ -327,7 +346,7 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
       }
     }
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < 4; ++s) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -355,18 +374,19 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
     rsum[wv][16 + lo] = rs[1];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 32 * 32; e += NT) {
-    const int r = e >> 5, c = e & 31;
+#pragma unroll
+  for (int q = 0; q < 32 * 32 / NT; ++q) {
+    const int e = threadIdx.x + q * NT, r = e >> 5, c = e & 31;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[w][e];
-    if (n0 + r < P.N && k0 + c < P.K) P.dw[(int64_t)(n0 + r) * P.K + k0 + c] += v;
+    if (n0 + r < P.N && k0 + c < P.K) P.dw[(int64_t)(n0 + r) * P.K + k0 + c] = dw_old[q] + v;
   }
-  if (k0 == 0 && P.db && threadIdx.x < 32 && n0 + (int)threadIdx.x < P.N) {
+  if (has_db) {
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += rsum[w][threadIdx.x];
-    P.db[n0 + threadIdx.x] += v;
+    P.db[n0 + threadIdx.x] = db_old + v;
   }
 }
 
