@@ -9,6 +9,7 @@ kernels for the hot ops (:mod:`rocket_amd.ops`), RCCL over xGMI for data
 parallelism (:mod:`rocket_amd.parallel`) and HIP graphs for launch-bound steps.
 """
 
+from rocket_amd.runtime import hipenv as _hipenv  # noqa: F401  (before any HIP initialisation)
 from rocket_amd.core import (  # noqa: F401
     Attributes,
     Capsule,

@@ -127,8 +127,21 @@ def available() -> bool:
         return False
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    """hipStream_t of the current stream (a raw-handle lookup: ~10x cheaper on the host than
+    materialising a ``torch.cuda.Stream``, which matters for a ~60 µs launch-bound step)."""
+    if _raw_stream is None:
+        return torch.cuda.current_stream(device).cuda_stream
+    if device is None:
+        return _raw_stream(torch.cuda.current_device())
+    if isinstance(device, int):
+        return _raw_stream(device)
+    if not isinstance(device, torch.device):
+        device = torch.device(device)
+    return _raw_stream(device.index if device.index is not None else torch.cuda.current_device())
 
 
 def check(code: int, what: str) -> None:

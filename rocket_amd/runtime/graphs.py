@@ -117,6 +117,7 @@ class StepGraphs:
         self._preps = None  # bound graph_prepare / graph_host / graph_token methods of the children
         self._hosts = None
         self._toks = None
+        self._params = None  # parameter list for the version token (fixed once graphs exist)
 
     def release(self) -> None:
         self.variants.clear()
@@ -165,7 +166,9 @@ class StepGraphs:
         # parameter versions: weights rewritten outside the captured step (checkpoint load, manual
         # edits) invalidate the graphs — captured kernels may depend on derived state of them
         # (e.g. the fused LeNet's optimizer-maintained bf16 fragment table)
-        return tuple(t() for t in self._toks) + (sum(p._version for p in self.mod._module.parameters()),)
+        if self._params is None:
+            self._params = list(self.mod._module.parameters())
+        return tuple(t() for t in self._toks) + (sum(p._version for p in self._params),)
 
     def _predict_sync(self) -> bool:
         engine = self.mod._accelerator
