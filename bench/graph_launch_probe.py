@@ -4,14 +4,20 @@
 
 Captures a graph of K tiny kernels and times 2000 replays in a row: (a) replay only, (b) an eager
 kernel launch before every replay (the loader's gather), (c) plus a timing-event record per step
-(StepTimer), (d) the same K kernels launched eagerly, (e) one graph holding 4 steps (4K kernels).
+(StepTimer), (d) the same K kernels launched eagerly, (e) one graph holding 4 steps (4K kernels),
+(f) the graph replayed as a native launch list (rocket_amd.runtime.native.LaunchList), (g) an eager
+kernel plus the launch list.
 Prints one JSON line with microseconds per step for each variant.
 """
 
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def timed(fn, n=2000):
@@ -42,6 +48,15 @@ def main():
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         work()
+    gk = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(gk):
+        work()
+    from rocket_amd.runtime.native import LaunchList
+    from rocket_amd.ops import _lib
+
+    ll, why = LaunchList.build(gk)
+    assert ll is not None, why
+    sp = _lib.stream_ptr(dev)
     g4 = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g4):
         work(4 * K)
@@ -62,6 +77,8 @@ def main():
         "eager_K_kernels_us": timed(work),
         "graph_4_steps_per_replay_us": timed(g4.replay) / 4,
         "single_kernel_us": timed(lambda: y.add_(1.0)),
+        "launch_list_us": timed(lambda: ll.launch(sp)),
+        "kernel_plus_launch_list_us": timed(lambda: (y.add_(1.0), ll.launch(sp))),
     }
     print(json.dumps({k: round(v, 2) for k, v in res.items()}))
 

@@ -35,6 +35,13 @@ execution, as do unseen input signatures until warmed up, and CPU tensors.
 The first ``warmup`` iterations of each (sync, signature) variant run eagerly,
 which also primes lazily created state (optimizer moments, workspaces).
 
+Replay: each captured graph is walked once into a native *launch list*
+(``native/runtime/launchlist.cpp``) and re-issued as plain stream launches —
+hipGraphLaunch costs a fixed ~5-8 µs of GPU idle time per launch on MI355X,
+back-to-back dispatches ~1-2 µs; the graph object stays alive because the list
+points into its node argument arrays.  A graph with a node type the list does
+not support (or ``ROCKET_LAUNCH_LIST=0``) is replayed with ``graph.replay()``.
+
 Inputs: tensors flagged ``_rocket_persistent`` (the device loader's ring
 buffers) are captured in place and get one graph per buffer set — no copy per
 step; any other input is copied into a static buffer before replay.
@@ -43,16 +50,49 @@ step; any other input is copied into a static buffer before replay.
 from __future__ import annotations
 
 import collections
-from typing import Any, Dict, List, Tuple
+import os
+from typing import Any, Dict, List, Optional, Tuple
 
 import torch
 
 from rocket_amd.core.attributes import Attributes
+from rocket_amd.ops import _lib
 from rocket_amd.utils.logging import get_logger
 
 logger = get_logger(__name__)
 
 MAX_VARIANTS = 32
+
+
+def _use_launch_lists() -> bool:
+    return os.environ.get("ROCKET_LAUNCH_LIST", "1") != "0"
+
+
+class _Part:
+    """One captured graph and, when every node is supported, its launch list (preferred replay)."""
+
+    __slots__ = ("graph", "ll")
+
+    def __init__(self, graph):
+        self.graph = graph
+        self.ll = None
+
+    def finish(self) -> Optional[str]:
+        if not _use_launch_lists():
+            return "disabled (ROCKET_LAUNCH_LIST=0)"
+        from rocket_amd.runtime.native import LaunchList
+
+        try:
+            self.ll, why = LaunchList.build(self.graph)
+        except Exception as e:  # runtime library missing: graph replay still works
+            self.ll, why = None, f"{type(e).__name__}: {e}"
+        return why
+
+    def run(self, stream: int) -> None:
+        if self.ll is not None:
+            self.ll.launch(stream)
+        else:
+            self.graph.replay()
 
 
 def _signature(batch) -> Tuple:
@@ -93,7 +133,7 @@ class _Captured:
     __slots__ = ("graphs", "static_in", "persistent", "out", "sync")
 
     def __init__(self):
-        self.graphs: list = []   # [A] or [A, B] (B after the host-side gradient reduction)
+        self.graphs: list = []   # [_Part A] or [A, B] (B after the host-side gradient reduction)
         self.static_in = None
         self.persistent = None   # per input tensor: captured in place (no copy at replay)
         self.out = None
@@ -118,6 +158,9 @@ class StepGraphs:
         self._hosts = None
         self._toks = None
         self._params = None  # parameter list for the version token (fixed once graphs exist)
+        self._dev = None
+        self.launch_lists = 0  # captured parts replayed as native launch lists
+        self.launch_list_reason = None  # why a part kept hipGraphLaunch replay (first such part)
 
     def release(self) -> None:
         self.variants.clear()
@@ -273,7 +316,7 @@ class StepGraphs:
         cap.capturing = True
         cap.graph_split = v.sync and rep is not None  # a cross-rank reduce separates device / device_synced
         torch.cuda.synchronize()
-        ga = torch.cuda.CUDAGraph()
+        ga = torch.cuda.CUDAGraph(keep_graph=True)
         # thread_local: the RCCL watchdog thread keeps polling its events while we capture
         with torch.cuda.graph(ga, pool=self.pool, capture_error_mode="thread_local"):
             self._phase_a(cap)
@@ -281,12 +324,21 @@ class StepGraphs:
                 rep.reduce_now()
             if not split:
                 self._phase_b(cap)
-        v.graphs.append(ga)
+        v.graphs.append(_Part(ga))
         if split:
-            gb = torch.cuda.CUDAGraph()
+            gb = torch.cuda.CUDAGraph(keep_graph=True)
             with torch.cuda.graph(gb, pool=self.pool, capture_error_mode="thread_local"):
                 self._phase_b(cap)
-            v.graphs.append(gb)
+            v.graphs.append(_Part(gb))
+        for part in v.graphs:
+            why = part.finish()
+            if part.ll is not None:
+                self.launch_lists += 1
+            elif self.launch_list_reason is None:
+                self.launch_list_reason = why
+                logger.info(f"graph replay (no launch list): {why}")
+        if self._dev is None:
+            self._dev = engine.device
         v.out = cap.batch
         self.captures += 1
         self.parts = max(self.parts, len(v.graphs))
@@ -299,10 +351,11 @@ class StepGraphs:
 
     # ------------------------------------------------------------------ replay
     def _run(self, v: _Captured, rep) -> None:
-        v.graphs[0].replay()
+        stream = _lib.stream_ptr(self._dev)
+        v.graphs[0].run(stream)
         if len(v.graphs) > 1:
             rep.reduce_now()  # host-issued RCCL between the two graphs
-            v.graphs[1].replay()
+            v.graphs[1].run(stream)
         self.replays += 1
 
     def _host(self, attrs: Attributes) -> None:

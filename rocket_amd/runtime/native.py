@@ -1,5 +1,6 @@
 """ctypes bindings of ``librocket_runtime.so`` (``native/runtime/*.cpp``): RCCL communicator +
-bucket reducer (comm.cpp) and the host batch assembler (loader.cpp)."""
+bucket reducer (comm.cpp), the host batch assembler (loader.cpp) and the launch-list replay of
+captured HIP graphs (launchlist.cpp)."""
 
 from __future__ import annotations
 
@@ -30,6 +31,12 @@ RUNTIME_SIGS = {
     "rkl_submit": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p]),
     "rkl_wait": (c_int, [c_void_p, c_int]),
     "rkl_destroy": (c_int, [c_void_p]),
+    "rkg_last_error": (c_char_p, []),
+    "rkg_create": (c_int, [P, c_void_p]),
+    "rkg_size": (c_int, [c_void_p]),
+    "rkg_kind": (c_int, [c_void_p, c_int]),
+    "rkg_launch": (c_int, [c_void_p, c_void_p]),
+    "rkg_destroy": (c_int, [c_void_p]),
 }
 
 
@@ -45,3 +52,44 @@ def check(code: int, what: str) -> None:
     if code != 0:
         msg = runtime().rkr_last_error()
         raise RuntimeError_(f"{what} failed ({code}): {msg.decode() if msg else ''}")
+
+
+class LaunchList:
+    """Launch-list replay of a captured graph (``native/runtime/launchlist.cpp``): the graph's nodes
+    re-issued as plain stream launches, avoiding hipGraphLaunch's fixed boundary cost.  Holds a
+    reference to the ``torch.cuda.CUDAGraph`` (captured with ``keep_graph=True``) whose node
+    argument arrays the list points into.  ``LaunchList.build`` returns ``(list, None)`` or
+    ``(None, reason)`` when a node type is not supported (the caller keeps ``graph.replay()``)."""
+
+    def __init__(self, graph, handle):
+        self._graph = graph
+        self._h = handle
+        rt = runtime()
+        self._launch = rt.rkg_launch
+        self._destroy = rt.rkg_destroy
+        self.size = rt.rkg_size(handle)
+        self.kinds = [rt.rkg_kind(handle, i) for i in range(self.size)]
+
+    @classmethod
+    def build(cls, graph):
+        rt = runtime()
+        h = ctypes.c_void_p()
+        code = rt.rkg_create(ctypes.byref(h), ctypes.c_void_p(graph.raw_cuda_graph()))
+        if code != 0:
+            msg = rt.rkg_last_error()
+            return None, (msg.decode() if msg else f"rkg_create failed ({code})")
+        return cls(graph, h.value), None
+
+    def launch(self, stream: int) -> None:
+        code = self._launch(self._h, stream)
+        if code != 0:
+            msg = runtime().rkg_last_error()
+            raise RuntimeError_(f"launch-list replay failed ({code}): {msg.decode() if msg else ''}")
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            try:
+                self._destroy(h)
+            except Exception:
+                pass

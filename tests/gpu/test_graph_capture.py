@@ -62,6 +62,8 @@ def test_graph_matches_eager(tmp_path, ga):
     lg, wg, mod = _train(tmp_path / "g", capture=True, ga=ga)
     assert mod._graphs is not None and mod._graphs.disabled_reason == "released", mod._graphs.disabled_reason
     assert mod._graphs.replays > 0
+    # every captured part replays as a native launch list (no hipGraphLaunch on the hot path)
+    assert mod._graphs.launch_lists > 0 and mod._graphs.launch_list_reason is None, mod._graphs.launch_list_reason
     assert len(le) == len(lg) and len(le) > 0
     for a, b in zip(le, lg):
         assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (le, lg)
