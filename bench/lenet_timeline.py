@@ -25,7 +25,7 @@ FWD = ["start", "stage img + w1", "conv1 tiles (wave 0)", "w2 frags + sync", "a1
        "fc1 + sync", "fc2 + sync", "fc3 (end)"]
 BWD = ["start", "wfr + CE loads + sync", "stage issue (dc2/dcT zero)", "CE softmax + sync", "fc3 dgrad + sync",
        "fc2 dgrad + sync", "fc1 dgrad + sync", "scatter + sync", "conv2 dgrad + sync", "dW1/dW2 MFMA (wave 0)",
-       "dW2 partials out + sync", "dW1 partials out", "CE loss ticket (end)"]
+       "dW2 partials out + sync", "dW1 partials out", "CE loss partials (end)"]
 BWD_MARKS = [0, 1, 2, 3, 5, 6, 7, 8, 9, 13, 10, 11, 12]
 
 

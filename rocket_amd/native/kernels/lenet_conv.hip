@@ -253,6 +253,16 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     koffp[q] = k < K1P ? (k / 6) * IMGS + (k % 6) : -100000;
   }
   const float bias1 = b1[lo < C1 ? lo : 0];
+  // every later layer's bias, issued now: its global-load latency hides behind conv1 instead of
+  // stalling the conv2 / classifier epilogues (~1 us each after a barrier)
+  const float bias2 = b2[lo];
+  float fbias1 = 0.f, fbias2 = 0.f, fbias3 = 0.f;  // fc1 on waves 0-7, fc2 on 0-5, fc3 on wave 0
+  if constexpr (MLP) {
+    const int col = 16 * wave + lo;
+    if (wave < 8) fbias1 = cf.fb1[col < F1 ? col : 0];
+    if (wave < 6) fbias2 = cf.fb2[col < F2 ? col : 0];
+    if (wave == 0) fbias3 = cf.fb3[lo < F3 ? lo : 0];
+  }
   __syncthreads();
   RK_TR(cf.trace, 1);
 
@@ -302,7 +312,6 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
         bw2[s][j] = tobf(ok ? v : 0.f);
       }
   }
-  const float bias2 = b2[lo];
   __syncthreads();
   RK_TR(cf.trace, 3);
   if (live) {
@@ -357,7 +366,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
       const f32x4 acc = cls_tile<13>(&sm.a2[0][0], A2P, sm.zrow, cf.frag, OFF_F1 + wave * 13, lane);
       if (hi == 0) {
         const int col = 16 * wave + lo;
-        const float bb = cf.fb1[col < F1 ? col : 0];
+        const float bb = fbias1;
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -378,7 +387,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
       const f32x4 acc = cls_tile<4>(&sm.h1[0][0], H1P, sm.zrow, cf.frag, OFF_F2 + wave * 4, lane);
       if (hi == 0) {
         const int col = 16 * wave + lo;
-        const float bb = cf.fb2[col < F2 ? col : 0];
+        const float bb = fbias2;
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -393,7 +402,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     if (wave == 0) {  // fc3: 1 n-tile x 3 k-steps -> fp32 logits
       const f32x4 acc = cls_tile<3>(&sm.h2[0][0], H2P, sm.zrow, cf.frag, OFF_F3, lane);
       if (hi == 0 && lo < F3) {
-        const float bb = cf.fb3[lo];
+        const float bb = fbias3;
 #pragma unroll
         for (int i = 0; i < 4; ++i) cf.logits[(int64_t)(n0 + i) * F3 + lo] = acc[i] + bb;
       }
@@ -467,6 +476,7 @@ struct ClsBwd {
   float* partials;                  // [gridDim.x]
   unsigned* counter;
   float* loss_out;                  // [2]: loss, nvalid
+  int defer_loss;                   // 1: store block partials + nvalid only; the wgrad launch finalises
   float *acc, *ring;
   int64_t* slot;
   int ring_size;
@@ -904,7 +914,16 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
   RK_TR(cb.trace, 11);
   }
   if constexpr (MLP) {
-    if (cb.ce) {  // batch loss: block partials -> last block -> loss + Loss-capsule bookkeeping
+    if (cb.ce && cb.defer_loss) {  // partials + valid count; the next (wgrad) launch reduces them
+      if (threadIdx.x == 0) {
+        cb.partials[blockIdx.x] = sm.lossp[0];
+        if (blockIdx.x == 0) {
+          float nv = 0.f;
+          for (int w = 1; w < NTHR / 64; ++w) nv += sm.cecnt[w];
+          cb.loss_out[1] = nv;
+        }
+      }
+    } else if (cb.ce) {  // batch loss: block partials -> last block -> loss + Loss-capsule bookkeeping
       if (threadIdx.x == 0) st_sc1(cb.partials + blockIdx.x, sm.lossp[0]);
       if (last_block_arrived(cb.counter, &sm.flag)) {
         float t = 0.f;
@@ -929,8 +948,8 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
         }
         reset_counter(cb.counter);
       }
-      RK_TR(cb.trace, 12);
     }
+    if (cb.ce) RK_TR(cb.trace, 12);
   }
 }
 
@@ -1003,6 +1022,7 @@ struct LenetCE {  // host-side description of the fused cross-entropy (see ClsBw
   int ring_size;
   float acc_scale;
   int sync;
+  int defer_loss;  // 1: rk_mlp3_wgrad_loss finalises the loss (no last-block ticket in this launch)
 };
 
 // The conv weight/bias gradients are NOT accumulated here: each block writes its totals to
@@ -1041,6 +1061,7 @@ RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const
     cb.ring_size = ce->ring_size;
     cb.acc_scale = ce->acc_scale;
     cb.sync = ce->sync;
+    cb.defer_loss = ce->defer_loss;
   }
   lenet_conv_bwd<true><<<N / (SPB * rounds), NTHR, 0, s>>>(x, (const uint16_t*)a1, (const uint8_t*)code1, nullptr,
                                                            (const uint8_t*)code2, w2, nullptr, nullptr, nullptr,

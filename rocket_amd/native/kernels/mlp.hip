@@ -247,11 +247,52 @@ struct SlabArgs {
   float* dst[4];
   int bound[5];
 };
+// Batch-loss finalisation riding on the wgrad launch (the LeNet backward stores per-block CE
+// partials and the valid count; one extra block here sums them and does the Loss capsule's
+// accumulate / report-ring bookkeeping — no last-block ticket at the end of the backward).
+struct LossFin {
+  const float* partials;
+  int nparts;
+  float* loss_out;  // [2]: loss (written here), nvalid (written by the backward)
+  float *acc, *ring;
+  int64_t* slot;
+  int ring_size;
+  float acc_scale;
+  int sync;
+};
 struct WgradArgs {
   WgradProb p[3];
-  int nprob, M, tiles;
+  int nprob, M, tiles, nslab;
   SlabArgs sl;
+  int has_loss;
+  LossFin lf;
 };
+
+__device__ void loss_fin_block(const LossFin& f, float (*red)[32 * 32]) {
+  float t = 0.f;
+  for (int i = threadIdx.x; i < f.nparts; i += NT) t += f.partials[i];
+#pragma unroll
+  for (int k = 32; k >= 1; k >>= 1) t += __shfl_xor(t, k, 64);
+  if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < NT / 64; ++w) s += red[0][w];  // fixed order: deterministic
+    const float nv = f.loss_out[1];
+    const float l = nv > 0.f ? s / nv : NAN;
+    f.loss_out[0] = l;
+    if (f.acc) {
+      float v = f.acc[0] + l * f.acc_scale;
+      if (f.sync) {
+        const int64_t k = f.slot[0];
+        f.ring[k] = v;
+        f.slot[0] = (k + 1) % f.ring_size;
+        v = 0.f;
+      }
+      f.acc[0] = v;
+    }
+  }
+}
 
 // one slab block: 64 columns x all rows; 8 row groups per block, 8 independent loads per thread
 // in flight, LDS reduce over the groups, one plain RMW per column (sole owner: deterministic)
@@ -304,7 +345,8 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   __shared__ float red[NW][32 * 32];
   __shared__ float rsum[NW][32];
   if ((int)blockIdx.x >= a.tiles) {
-    slab_reduce_block(a.sl, blockIdx.x - a.tiles, red);
+    if ((int)blockIdx.x - a.tiles < a.nslab) slab_reduce_block(a.sl, blockIdx.x - a.tiles, red);
+    else loss_fin_block(a.lf, red);
     return;
   }
   int pi = 0;
@@ -423,9 +465,11 @@ RK_API int rk_mlp3_dgrad(const float* dy, int N3, const float* w3, int N2, const
 // Grouped dW_l += dT_l . xT_l^T, db_l += rowsum(dT_l) for up to 3 layers. M % 8 == 0.
 // slab (may be null): also dst[i][c - bound[i]] += sum over the slab_rows rows of slab[r][c] for
 // c in [bound[i], bound[i+1]), bound[0] = 0, c < bound[4] <= slab_width.
-RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT, float* const* dw, float* const* db,
-                         const int* Ns, const int* Ks, int M, const float* slab, int slab_rows, int slab_width,
-                         float* const* slab_dst, const int* slab_bound, hipStream_t s) {
+// loss (may be null): also finalise a batch loss from per-block partials (see LossFin).
+RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* const* xT, float* const* dw,
+                              float* const* db, const int* Ns, const int* Ks, int M, const float* slab, int slab_rows,
+                              int slab_width, float* const* slab_dst, const int* slab_bound, const LossFin* loss,
+                              hipStream_t s) {
   if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
   WgradArgs a{};
   a.nprob = nprob;
@@ -455,6 +499,21 @@ RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT
     for (int i = 0; i < 5; ++i) a.sl.bound[i] = slab_bound[i];
     extra = (a.sl.ncols + 63) / 64;
   }
+  a.nslab = extra;
+  if (loss) {
+    if (!loss->partials || !loss->loss_out || loss->nparts < 1 || (loss->acc && (!loss->ring || !loss->slot || loss->ring_size < 1)))
+      return (int)hipErrorInvalidValue;
+    a.has_loss = 1;
+    a.lf = *loss;
+    extra += 1;
+  }
   mlp3_wgrad_kernel<<<tiles + extra, NT, 0, s>>>(a);
   return (int)hipGetLastError();
+}
+
+RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT, float* const* dw, float* const* db,
+                         const int* Ns, const int* Ks, int M, const float* slab, int slab_rows, int slab_width,
+                         float* const* slab_dst, const int* slab_bound, hipStream_t s) {
+  return rk_mlp3_wgrad_loss(nprob, dT, xT, dw, db, Ns, Ks, M, slab, slab_rows, slab_width, slab_dst, slab_bound,
+                            nullptr, s);
 }

@@ -55,6 +55,8 @@ KERNEL_SIGS = {
                               c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "rk_mlp3_wgrad": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                               c_int, c_void_p, c_void_p, c_void_p]),
+    "rk_mlp3_wgrad_loss": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_int, c_void_p]),
     "rk_optim_chunk_for": (c_int, [c_int64]),

@@ -250,7 +250,16 @@ class _LenetCE(ctypes.Structure):
                 ("grad_scale", ctypes.c_float), ("partials", ctypes.c_void_p), ("counter", ctypes.c_void_p),
                 ("loss_out", ctypes.c_void_p), ("acc", ctypes.c_void_p), ("ring", ctypes.c_void_p),
                 ("slot", ctypes.c_void_p), ("ring_size", ctypes.c_int), ("acc_scale", ctypes.c_float),
-                ("sync", ctypes.c_int)]
+                ("sync", ctypes.c_int), ("defer_loss", ctypes.c_int)]
+
+
+class _LossFin(ctypes.Structure):
+    """Mirror of ``struct LossFin`` (mlp.hip): the batch loss finalised by the wgrad launch from the
+    backward's per-block partials (no last-block ticket at the tail of the backward)."""
+
+    _fields_ = [("partials", ctypes.c_void_p), ("nparts", ctypes.c_int), ("loss_out", ctypes.c_void_p),
+                ("acc", ctypes.c_void_p), ("ring", ctypes.c_void_p), ("slot", ctypes.c_void_p),
+                ("ring_size", ctypes.c_int), ("acc_scale", ctypes.c_float), ("sync", ctypes.c_int)]
 
 
 class _LeNetFused(torch.autograd.Function):
@@ -297,7 +306,7 @@ class _LeNetFused(torch.autograd.Function):
         dev = x.device
         stream = _lib.stream_ptr(dev)
         rounds = 1  # one block per 4 samples (the kernel keeps no state across sample groups)
-        ce, keep = None, None
+        ce, keep, fin = None, None, None
         if ctx.ce_spec is not None:
             target, grad_scale, accum, loss_out = ctx.ce_spec
             ctx.ce_spec = None
@@ -310,7 +319,9 @@ class _LeNetFused(torch.autograd.Function):
             ce = _LenetCE(logits.data_ptr(), target.data_ptr(), -100, float(grad_scale), partials.data_ptr(),
                           _lib.Workspace.get(dev).counter("lenet_ce"), loss_out.data_ptr(), _lib.ptr(acc),
                           _lib.ptr(ring), _lib.ptr(slot), ring.numel() if ring is not None else 0, float(acc_scale),
-                          int(sync))
+                          int(sync), 1)
+            fin = _LossFin(partials.data_ptr(), N // 4, loss_out.data_ptr(), _lib.ptr(acc), _lib.ptr(ring),
+                           _lib.ptr(slot), ring.numel() if ring is not None else 0, float(acc_scale), int(sync))
             dy = logits  # unread
         else:
             dy = dlogits.contiguous().float()
@@ -326,7 +337,6 @@ class _LeNetFused(torch.autograd.Function):
                                     frag.data_ptr(), dy.data_ptr(), h1T.data_ptr(), h2T.data_ptr(), dyT.data_ptr(),
                                     d2T.data_ptr(), d1T.data_ptr(), slab.data_ptr(), N, rounds,
                                     ctypes.byref(ce) if ce is not None else None, stream), "rk_lenet_bwd")
-        del keep
         probs = ((dyT, h2T, bufs[8], bufs[9], 10, 84), (d2T, h1T, bufs[6], bufs[7], 84, 120),
                  (d1T, a2T, bufs[4], bufs[5], 120, 400))
         P = ctypes.c_void_p * 3
@@ -335,11 +345,14 @@ class _LeNetFused(torch.autograd.Function):
         sizes = [bufs[i].numel() for i in range(4)]
         assert sum(sizes) == int(lib.rk_lenet_slab_cols()), "fused LeNet expects conv1 6x1x5x5 / conv2 16x6x5x5"
         bounds = (ctypes.c_int * 5)(0, sizes[0], sizes[0] + sizes[1], sizes[0] + sizes[1] + sizes[2], sum(sizes))
-        _lib.check(lib.rk_mlp3_wgrad(3, P(*[q[0].data_ptr() for q in probs]), P(*[q[1].data_ptr() for q in probs]),
-                                     P(*[q[2].data_ptr() for q in probs]), P(*[q[3].data_ptr() for q in probs]),
-                                     I(*[q[4] for q in probs]), I(*[q[5] for q in probs]), N, slab.data_ptr(),
-                                     N // 4, slab.shape[1], (ctypes.c_void_p * 4)(*[bufs[i].data_ptr() for i in range(4)]),
-                                     bounds, stream), "rk_mlp3_wgrad")
+        _lib.check(lib.rk_mlp3_wgrad_loss(3, P(*[q[0].data_ptr() for q in probs]), P(*[q[1].data_ptr() for q in probs]),
+                                          P(*[q[2].data_ptr() for q in probs]), P(*[q[3].data_ptr() for q in probs]),
+                                          I(*[q[4] for q in probs]), I(*[q[5] for q in probs]), N, slab.data_ptr(),
+                                          N // 4, slab.shape[1],
+                                          (ctypes.c_void_p * 4)(*[bufs[i].data_ptr() for i in range(4)]), bounds,
+                                          ctypes.byref(fin) if fin is not None else None, stream),
+                   "rk_mlp3_wgrad_loss")
+        del keep  # partials: read by the wgrad launch (stream-ordered before any reuse)
         return (None, *_finish(params, bufs, direct), None)
 
 
