@@ -32,7 +32,7 @@ namespace {
 constexpr int kChunk = 4096;  // largest chunk (J = 4)
 constexpr int kThreads = 256;
 
-struct TensorRec {  // 8 x int64 per tensor, uploaded from the host
+struct TensorRec {  // 8 x int64 per BLOCK (its tensor's record), uploaded from the host
   int64_t p, g, s0, s1, n, group;
   int64_t shadow_map, shadow_buf;  // int32 [n][2] (or 1 = dense) / bf16 buffer, or 0
 };
@@ -76,11 +76,17 @@ template <> __device__ __forceinline__ float gload<uint16_t>(const uint16_t* g, 
 // Every block reads the device step counter once (broadcast through LDS), then thread 0 takes a
 // ticket; the last block to take one advances the counter.  All blocks have already read the old
 // value when the last ticket is taken, so no block waits for its stores or fences at the end.
-__device__ __forceinline__ float read_step_and_ticket(float* step, unsigned* counter, bool skip) {
+// Device step counter: every block reads it first thing; each block takes a ticket at its END
+// (the atomic's round trip then overlaps nothing on the block's critical path) and the last one
+// advances the counter — every block has read the old value by then.
+__device__ __forceinline__ float read_step(const float* step) {
   __shared__ float s_step;
   if (threadIdx.x == 0) s_step = step[0];
   __syncthreads();
-  const float cur = s_step;
+  return s_step;
+}
+
+__device__ __forceinline__ void advance_step(float* step, unsigned* counter, bool skip, float cur) {
   if (threadIdx.x == 0) {
     const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
@@ -88,7 +94,6 @@ __device__ __forceinline__ float read_step_and_ticket(float* step, unsigned* cou
       __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  return cur;
 }
 
 template <typename G>
@@ -102,11 +107,14 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
                                                           const AdamHyper* __restrict__ hyper, float* step,
                                                           const float* inv_scale, const float* found_inf,
                                                           unsigned* counter) {
+  // block record + chunk index + step counter loads all in flight at once (the tensor table holds
+  // one record per BLOCK: no dependent table walk before the data loads)
+  const int2 bt = blocks[blockIdx.x];
+  const TensorRec tr = tensors[blockIdx.x];
   const bool skip = found_inf != nullptr && found_inf[0] != 0.f;
-  const float t = read_step_and_ticket(step, counter, skip) + 1.f;
+  const float cur = read_step(step);
+  const float t = cur + 1.f;
   if (!skip) {
-    const int2 bt = blocks[blockIdx.x];
-    const TensorRec tr = tensors[bt.x];
     const AdamHyper h = hyper[tr.group];
     float* __restrict__ p = (float*)tr.p;
     G* __restrict__ g = (G*)tr.g;
@@ -186,11 +194,10 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
     }
   } else if (ZG) {
     constexpr int CH = J * 4 * kThreads;
-    const int2 bt = blocks[blockIdx.x];
-    const TensorRec tr = tensors[bt.x];
     const int64_t start = (int64_t)bt.y * CH;
     zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)CH, tr.n));
   }
+  advance_step(step, counter, skip, cur);
 }
 
 struct SgdHyper {  // 8 floats per group
@@ -203,11 +210,11 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
                                                          const SgdHyper* __restrict__ hyper, float* step,
                                                          const float* inv_scale, const float* found_inf,
                                                          unsigned* counter) {
+  const int2 bt = blocks[blockIdx.x];
+  const TensorRec tr = tensors[blockIdx.x];
   const bool skip = found_inf != nullptr && found_inf[0] != 0.f;
-  const float cur = read_step_and_ticket(step, counter, skip);
+  const float cur = read_step(step);
   if (!skip) {
-    const int2 bt = blocks[blockIdx.x];
-    const TensorRec tr = tensors[bt.x];
     const SgdHyper h = hyper[tr.group];
     float* p = (float*)tr.p;
     G* g = (G*)tr.g;
@@ -231,11 +238,10 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
     }
   } else if (ZG) {
     constexpr int CH = J * 4 * kThreads;
-    const int2 bt = blocks[blockIdx.x];
-    const TensorRec tr = tensors[bt.x];
     const int64_t start = (int64_t)bt.y * CH;
     zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)CH, tr.n));
   }
+  advance_step(step, counter, skip, cur);
 }
 
 }  // namespace

@@ -124,8 +124,9 @@ class _FusedBase(torch.optim.Optimizer):
         for ti, (gi, p) in enumerate(active):
             st = self.state[p]
             s = [st[k].data_ptr() for k in self.STATE_KEYS] + [0] * (2 - len(self.STATE_KEYS))
-            recs += [p.data_ptr(), p.grad.data_ptr(), s[0], s[1], p.numel(), gi, *self._shadow_ptrs(p)]
+            rec = [p.data_ptr(), p.grad.data_ptr(), s[0], s[1], p.numel(), gi, *self._shadow_ptrs(p)]
             for c in range((p.numel() + chunk - 1) // chunk):
+                recs += rec  # one record per block: the kernel loads it without a dependent table walk
                 blocks += [ti, c]
         t_host = torch.tensor(recs, dtype=torch.int64).pin_memory()
         b_host = torch.tensor(blocks, dtype=torch.int32).pin_memory()
