@@ -50,18 +50,33 @@ __device__ __forceinline__ void shadow_store(const TensorRec& tr, int64_t i, flo
   if (m.x >= 0) buf[m.x] = b;
   if (m.y >= 0) buf[m.y] = b;
 }
+// Index-mapped shadows: the 4 map entries of elements i..i+3 (two 16-byte loads), fetched together
+// with the parameter data so the shadow stores do not wait on a dependent load after the update.
+struct Map4 {
+  int4 a, b;
+};
+__device__ __forceinline__ Map4 shadow_map4(const TensorRec& tr, int64_t i) {
+  if (tr.shadow_map <= kDenseShadow) return Map4{};
+  const int4* m = (const int4*)((const int2*)tr.shadow_map + i);
+  return Map4{m[0], m[1]};
+}
 // four consecutive elements (i % 4 == 0, 16-byte aligned parameter rows): dense shadows take one
-// 8-byte store
-__device__ __forceinline__ void shadow_store4(const TensorRec& tr, int64_t i, const float4& v) {
+// 8-byte store, mapped ones use the prefetched map entries
+__device__ __forceinline__ void shadow_store4(const TensorRec& tr, int64_t i, const float4& v, const Map4& mp) {
+  uint16_t* buf = (uint16_t*)tr.shadow_buf;
   if (tr.shadow_map == kDenseShadow) {
-    *(uint2*)((uint16_t*)tr.shadow_buf + i) = make_uint2((uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
-                                                         (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+    *(uint2*)(buf + i) = make_uint2((uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
+                                    (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
     return;
   }
-  shadow_store(tr, i, v.x);
-  shadow_store(tr, i + 1, v.y);
-  shadow_store(tr, i + 2, v.z);
-  shadow_store(tr, i + 3, v.w);
+  const int idx[8] = {mp.a.x, mp.a.y, mp.a.z, mp.a.w, mp.b.x, mp.b.y, mp.b.z, mp.b.w};
+  const float val[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint16_t b = f2bf(val[e]);
+    if (idx[2 * e] >= 0) buf[idx[2 * e]] = b;
+    if (idx[2 * e + 1] >= 0) buf[idx[2 * e + 1]] = b;
+  }
 }
 
 struct AdamHyper {  // 8 floats per group
@@ -73,9 +88,6 @@ __device__ __forceinline__ float gload(const G* g, int64_t i);
 template <> __device__ __forceinline__ float gload<float>(const float* g, int64_t i) { return g[i]; }
 template <> __device__ __forceinline__ float gload<uint16_t>(const uint16_t* g, int64_t i) { return bf2f(g[i]); }
 
-// Every block reads the device step counter once (broadcast through LDS), then thread 0 takes a
-// ticket; the last block to take one advances the counter.  All blocks have already read the old
-// value when the last ticket is taken, so no block waits for its stores or fences at the end.
 // Device step counter: every block reads it first thing; each block takes a ticket at its END
 // (the atomic's round trip then overlaps nothing on the block's critical path) and the last one
 // advances the counter — every block has read the old value by then.
@@ -142,6 +154,7 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
     if (vec && end - start == CH) {
       // full chunk: all 4*J float4 loads of the thread in flight before the first update
       float4 pp[J], mm[J], vv[J], gg[J];
+      Map4 mp[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const int64_t i = start + 4 * (threadIdx.x + j * kThreads);
@@ -149,6 +162,7 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
         mm[j] = *(const float4*)(m + i);
         vv[j] = *(const float4*)(v + i);
         gg[j] = *(const float4*)((const float*)g + i);
+        mp[j] = shadow_map4(tr, i);
       }
 #pragma unroll
       for (int j = 0; j < J; ++j) {
@@ -161,13 +175,14 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
         *(float4*)(m + i) = mm[j];
         *(float4*)(v + i) = vv[j];
         if (ZG) *(float4*)((float*)g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (tr.shadow_map) shadow_store4(tr, i, pp[j]);
+        if (tr.shadow_map) shadow_store4(tr, i, pp[j], mp[j]);
       }
     } else if (vec) {
       for (int64_t i = start + 4 * threadIdx.x; i < end; i += 4 * kThreads) {
         if (i + 4 <= end) {
           float4 pp = *(float4*)(p + i), mm = *(float4*)(m + i), vv = *(float4*)(v + i);
           float4 gg = *(const float4*)((const float*)g + i);
+          const Map4 mp = shadow_map4(tr, i);
           upd(pp.x, gg.x, mm.x, vv.x);
           upd(pp.y, gg.y, mm.y, vv.y);
           upd(pp.z, gg.z, mm.z, vv.z);
@@ -176,7 +191,7 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
           *(float4*)(m + i) = mm;
           *(float4*)(v + i) = vv;
           if (ZG) *(float4*)((float*)g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (tr.shadow_map) shadow_store4(tr, i, pp);
+          if (tr.shadow_map) shadow_store4(tr, i, pp, mp);
         } else {
           for (int64_t k = i; k < end; ++k) {
             upd(p[k], gload<G>(g, k), m[k], v[k]);

@@ -156,6 +156,10 @@ class _FusedBase(torch.optim.Optimizer):
             return (1, buf.data_ptr())
         if idx.dtype != torch.int32 or idx.shape != (p.numel(), 2) or idx.device != p.device:
             raise RuntimeError("bf16 shadow: expected an int32 [numel, 2] index map on the device")
+        if not idx.is_contiguous() or idx.data_ptr() % 16:
+            # the kernel fetches 4 elements' entries as two 16-byte loads: keep an aligned copy
+            idx = idx.contiguous().clone()
+            p._rocket_bf16_shadow = (idx, buf)
         return (idx.data_ptr(), buf.data_ptr())
 
     # --------------------------------------------------------- device side
