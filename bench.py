@@ -66,8 +66,10 @@ def _baseline_value(n_gpus: int):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    # defaults: LeNet 1000 timed steps (~60 ms: one host/runtime hiccup must not dominate the
+    # mean of a 58 us step) after 50 warmup; the large models 200 / 20
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--model", choices=sorted(MODELS), default="lenet")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default per model)")
     ap.add_argument("--impl", choices=["fused", "torch"], default="fused")
@@ -76,6 +78,10 @@ def main() -> int:
     ap.add_argument("--mp", default="bf16")
     ap.add_argument("--cpu", action="store_true")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 1000 if args.model == "lenet" else 200
+    if args.warmup is None:
+        args.warmup = 50 if args.model == "lenet" else 20
 
     import rocket_amd as rocket
     from rocket_amd.models import CrossEntropy, LeNet
@@ -183,6 +189,8 @@ def main() -> int:
             "ms_per_step": round(ms_per_step, 4),
             "step_ms_p50": round(p50, 4),
             "host_ms_p50": round(summ.get("host_ms_p50", 0.0), 4),
+            "step_ms_max": round(summ.get("step_ms_max", 0.0), 4),  # rank 0, worst timing group
+            "step_ms_max_at": summ.get("step_ms_max_at"),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,

@@ -157,4 +157,6 @@ class StepTimer(Capsule):
             "step_ms_p90": t_sorted[min(len(t) - 1, int(0.9 * len(t)))],
             "step_ms_min": t_sorted[0],
             "step_ms_mean": sum(t) / len(t),
+            "step_ms_max": t_sorted[-1],
+            "step_ms_max_at": t.index(t_sorted[-1]) * self.stride,  # iteration (within the timed run)
         }
