@@ -19,6 +19,8 @@ Parity:
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from rocket_amd.core.attributes import Attributes
@@ -203,15 +205,34 @@ class Optimizer(Capsule):
             inner.prepare()
         else:
             inner.refresh_hyper()  # pointers are frozen into the graph; only lr & co. can change
+        engine = self._accelerator
+        if hasattr(inner, "epilogue_armed"):
+            # exact only when the backward's gradients ARE the step's final gradients: one replica,
+            # a gradient-sync step and no AMP scaler.  A fused gradient producer (the LeNet weight-
+            # gradient launch) then applies the update itself; see _FusedBase.epilogue.
+            inner.epilogue_armed = (engine.sync_gradients and engine.num_processes == 1 and engine.scaler is None
+                                    and os.environ.get("ROCKET_OPT_EPILOGUE", "1") != "0")
+            if inner.epilogue_armed and not getattr(self, "_epi_tagged", False):
+                for g in inner.param_groups:
+                    for p in g["params"]:
+                        p._rocket_optimizer = inner
+                self._epi_tagged = True
 
     def graph_device(self, attrs: Attributes) -> None:
         return None  # the update needs reduced gradients: phase B
 
     def graph_device_synced(self, attrs: Attributes) -> None:
         if self._accelerator.sync_gradients:
-            self._optimizer.optimizer.launch(zero_grads=True)
+            inner = self._optimizer.optimizer
+            if getattr(inner, "epilogue_done", False):
+                inner.epilogue_done = False  # the gradient producer applied this step's update
+                return
+            inner.launch(zero_grads=True)
 
     def graph_host(self, attrs: Attributes) -> None:
+        inner = self._optimizer.optimizer
+        if getattr(inner, "epilogue_armed", False):
+            inner.epilogue_armed = False
         self.post(attrs)
 
     def destroy(self, attrs: Attributes | None = None) -> None:

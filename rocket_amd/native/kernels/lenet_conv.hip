@@ -180,7 +180,7 @@ struct FwdSmem {
   uint16_t a1[SPB][A1N + 8];  // zero slot at A1N, trash at A1N+4
   uint8_t c1[SPB][A1N + 8];
   uint16_t a2[SPB][A2P];  // data 0..399, zero pad 400..415, trash at A2TRASH
-  uint8_t c2[SPB][A2N + 8];
+  uint8_t c2[SPB][A2P];   // same row pitch as a2: the trash slot A2TRASH must stay inside the row
   uint16_t h1[SPB][H1P];  // classifier activations (bf16), zero pads for the next layer's K
   uint16_t h2[SPB][H2P];
   uint16_t zrow[A2P];

@@ -17,7 +17,7 @@
 //              and added once — deterministic, no atomics.
 //
 // Everything is branch-free in the load paths (clamped addresses + selects).
-#include "rk_common.h"
+#include "optim_common.h"
 
 using namespace rk;
 
@@ -266,6 +266,9 @@ struct WgradArgs {
   SlabArgs sl;
   int has_loss;
   LossFin lf;
+  // optional optimizer epilogue: records of the 3 dW / 3 db / 4 slab destinations' parameters
+  rk_opt::AdamEpi epi;
+  rk_opt::TensorRec rdw[3], rdb[3], rsl[4];
 };
 
 __device__ void loss_fin_block(const LossFin& f, float (*red)[32 * 32]) {
@@ -296,7 +299,9 @@ __device__ void loss_fin_block(const LossFin& f, float (*red)[32 * 32]) {
 
 // one slab block: 64 columns x all rows; 8 row groups per block, 8 independent loads per thread
 // in flight, LDS reduce over the groups, one plain RMW per column (sole owner: deterministic)
-__device__ __forceinline__ void slab_reduce_block(const SlabArgs& s, int j, float (*red)[32 * 32]) {
+__device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, float (*red)[32 * 32],
+                                                  const rk_opt::AdamStep* ks) {
+  const SlabArgs& s = a.sl;
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = j * 64 + cl;
   const bool ok = c < s.ncols;
@@ -305,11 +310,19 @@ __device__ __forceinline__ void slab_reduce_block(const SlabArgs& s, int j, floa
   // 32 slab rows in flight at once: the launch is one memory round trip, not four
   float* dst = nullptr;
   float old = 0.f;
+  int di = 0;
+  rk_opt::EpiElem ee{};
   if (threadIdx.x < 64 && ok) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (c >= s.bound[i] && c < s.bound[i + 1] && s.dst[i]) dst = s.dst[i] + (c - s.bound[i]);
-    if (dst) old = *dst;
+      if (c >= s.bound[i] && c < s.bound[i + 1] && s.dst[i]) {
+        dst = s.dst[i] + (c - s.bound[i]);
+        di = i;
+      }
+    if (dst) {
+      old = *dst;
+      if (ks) ee = rk_opt::epi_fetch(a.rsl[di], c - s.bound[di]);
+    }
   }
   constexpr int U = 32;
   float acc = 0.f;
@@ -328,7 +341,8 @@ __device__ __forceinline__ void slab_reduce_block(const SlabArgs& s, int j, floa
     float t = 0.f;
 #pragma unroll
     for (int g = 0; g < NW; ++g) t += red[g][threadIdx.x];
-    *dst = old + t;
+    if (ks) rk_opt::epi_apply(a.rsl[di], ks[a.rsl[di].group], c - s.bound[di], ee, old + t, a.epi.zero_grads);
+    else *dst = old + t;
   }
 }
 
@@ -341,14 +355,31 @@ __device__ __forceinline__ bf16x8 rowfrag(const uint16_t* T, int R, int M, int r
   return __builtin_bit_cast(bf16x8, ok ? v : z);
 }
 
+constexpr int kEpiGroups = 4;  // param groups the epilogue precomputes step constants for
+
+__device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks);
+
 __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   __shared__ float red[NW][32 * 32];
   __shared__ float rsum[NW][32];
-  if ((int)blockIdx.x >= a.tiles) {
-    if ((int)blockIdx.x - a.tiles < a.nslab) slab_reduce_block(a.sl, blockIdx.x - a.tiles, red);
-    else loss_fin_block(a.lf, red);
-    return;
+  __shared__ rk_opt::AdamStep s_ks[kEpiGroups];
+  float cur = 0.f;
+  if (a.epi.on) {  // optimizer epilogue: this launch performs the step's Adam update
+    cur = rk_opt::read_step(a.epi.step);
+    if (threadIdx.x < kEpiGroups) s_ks[threadIdx.x] = rk_opt::adam_step(a.epi.hyper[threadIdx.x < a.epi.on ? threadIdx.x : 0], cur + 1.f);
+    __syncthreads();
   }
+  const rk_opt::AdamStep* ks = a.epi.on ? s_ks : nullptr;
+  if ((int)blockIdx.x >= a.tiles) {
+    if ((int)blockIdx.x - a.tiles < a.nslab) slab_reduce_block(a, blockIdx.x - a.tiles, red, ks);
+    else loss_fin_block(a.lf, red);
+  } else {
+    wgrad_tile(a, red, rsum, ks);
+  }
+  if (a.epi.on) rk_opt::advance_step(a.epi.step, a.epi.counter, false, cur);
+}
+
+__device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks) {
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < 3; ++i)
@@ -362,13 +393,17 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   // this block is the only writer of its dW tile / db rows: read their old values up front so the
   // final accumulate does not wait on a memory round trip
   float dw_old[32 * 32 / NT];
+  rk_opt::EpiElem ew[32 * 32 / NT], eb{};
 #pragma unroll
   for (int q = 0; q < 32 * 32 / NT; ++q) {
     const int e = threadIdx.x + q * NT, r = e >> 5, c = e & 31;
-    dw_old[q] = (n0 + r < P.N && k0 + c < P.K) ? P.dw[(int64_t)(n0 + r) * P.K + k0 + c] : 0.f;
+    const bool in = n0 + r < P.N && k0 + c < P.K;
+    dw_old[q] = in ? P.dw[(int64_t)(n0 + r) * P.K + k0 + c] : 0.f;
+    if (ks && in) ew[q] = rk_opt::epi_fetch(a.rdw[pi], (int64_t)(n0 + r) * P.K + k0 + c);
   }
   const bool has_db = k0 == 0 && P.db && threadIdx.x < 32 && n0 + (int)threadIdx.x < P.N;
   const float db_old = has_db ? P.db[n0 + threadIdx.x] : 0.f;
+  if (ks && has_db) eb = rk_opt::epi_fetch(a.rdb[pi], n0 + threadIdx.x);
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -422,13 +457,18 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[w][e];
-    if (n0 + r < P.N && k0 + c < P.K) P.dw[(int64_t)(n0 + r) * P.K + k0 + c] = dw_old[q] + v;
+    if (n0 + r < P.N && k0 + c < P.K) {
+      const int64_t i = (int64_t)(n0 + r) * P.K + k0 + c;
+      if (ks) rk_opt::epi_apply(a.rdw[pi], ks[a.rdw[pi].group], i, ew[q], dw_old[q] + v, a.epi.zero_grads);
+      else P.dw[i] = dw_old[q] + v;
+    }
   }
   if (has_db) {
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += rsum[w][threadIdx.x];
-    P.db[n0 + threadIdx.x] = db_old + v;
+    if (ks) rk_opt::epi_apply(a.rdb[pi], ks[a.rdb[pi].group], n0 + threadIdx.x, eb, db_old + v, a.epi.zero_grads);
+    else P.db[n0 + threadIdx.x] = db_old + v;
   }
 }
 
@@ -465,11 +505,23 @@ RK_API int rk_mlp3_dgrad(const float* dy, int N3, const float* w3, int N2, const
 // Grouped dW_l += dT_l . xT_l^T, db_l += rowsum(dT_l) for up to 3 layers. M % 8 == 0.
 // slab (may be null): also dst[i][c - bound[i]] += sum over the slab_rows rows of slab[r][c] for
 // c in [bound[i], bound[i+1]), bound[0] = 0, c < bound[4] <= slab_width.
+// Host description of the optimizer epilogue (see rk_opt::AdamEpi): records of the parameters
+// whose gradients the launch produces, in the order dW[3], db[3] (the problems) and slab dst[4].
+struct WgradEpi {
+  const void* hyper;  // AdamHyper[ngroups]
+  float* step;
+  unsigned* counter;
+  int ngroups, zero_grads;
+  rk_opt::TensorRec rdw[3], rdb[3], rsl[4];
+};
+
 // loss (may be null): also finalise a batch loss from per-block partials (see LossFin).
+// epi (may be null): apply the Adam/AdamW update to every produced gradient element (the step's
+// optimizer launch is then skipped by the caller).  Every dW/db/slab destination needs a record.
 RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* const* xT, float* const* dw,
                               float* const* db, const int* Ns, const int* Ks, int M, const float* slab, int slab_rows,
                               int slab_width, float* const* slab_dst, const int* slab_bound, const LossFin* loss,
-                              hipStream_t s) {
+                              const WgradEpi* epi, hipStream_t s) {
   if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
   WgradArgs a{};
   a.nprob = nprob;
@@ -507,6 +559,28 @@ RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* cons
     a.lf = *loss;
     extra += 1;
   }
+  if (epi) {
+    if (!epi->hyper || !epi->step || !epi->counter || epi->ngroups < 1 || epi->ngroups > kEpiGroups || nprob != 3 ||
+        !slab)
+      return (int)hipErrorInvalidValue;
+    a.epi.hyper = (const rk_opt::AdamHyper*)epi->hyper;
+    a.epi.step = epi->step;
+    a.epi.counter = epi->counter;
+    a.epi.on = epi->ngroups;
+    a.epi.zero_grads = epi->zero_grads;
+    for (int i = 0; i < 3; ++i) {
+      a.rdw[i] = epi->rdw[i];
+      a.rdb[i] = epi->rdb[i];
+      // each record must describe the very gradient buffer this launch writes
+      if ((float*)a.rdw[i].g != dw[i] || (float*)a.rdb[i].g != db[i] || a.rdw[i].group >= epi->ngroups ||
+          a.rdb[i].group >= epi->ngroups)
+        return (int)hipErrorInvalidValue;
+    }
+    for (int i = 0; i < 4; ++i) {
+      a.rsl[i] = epi->rsl[i];
+      if ((float*)a.rsl[i].g != slab_dst[i] || a.rsl[i].group >= epi->ngroups) return (int)hipErrorInvalidValue;
+    }
+  }
   mlp3_wgrad_kernel<<<tiles + extra, NT, 0, s>>>(a);
   return (int)hipGetLastError();
 }
@@ -515,5 +589,5 @@ RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT
                          const int* Ns, const int* Ks, int M, const float* slab, int slab_rows, int slab_width,
                          float* const* slab_dst, const int* slab_bound, hipStream_t s) {
   return rk_mlp3_wgrad_loss(nprob, dT, xT, dw, db, Ns, Ks, M, slab, slab_rows, slab_width, slab_dst, slab_bound,
-                            nullptr, s);
+                            nullptr, nullptr, s);
 }

@@ -23,33 +23,16 @@
 // Memory: each block streams one chunk of J*1024 elements (J float4 per thread per array):
 // params/grads/exp_avg/exp_avg_sq read once, written once.  J = 4 (4096-element chunks) for big
 // models; J = 1 for small ones (LeNet's 61,706 parameters: 4x the blocks, one load round trip).
-#include "rk_common.h"
+#include "optim_common.h"
 
 using namespace rk;
+using namespace rk_opt;
 
 namespace {
 
 constexpr int kChunk = 4096;  // largest chunk (J = 4)
 constexpr int kThreads = 256;
 
-struct TensorRec {  // 8 x int64 per BLOCK (its tensor's record), uploaded from the host
-  int64_t p, g, s0, s1, n, group;
-  int64_t shadow_map, shadow_buf;  // int32 [n][2] (or 1 = dense) / bf16 buffer, or 0
-};
-
-constexpr int64_t kDenseShadow = 1;
-
-__device__ __forceinline__ void shadow_store(const TensorRec& tr, int64_t i, float v) {
-  uint16_t* buf = (uint16_t*)tr.shadow_buf;
-  const uint16_t b = f2bf(v);
-  if (tr.shadow_map == kDenseShadow) {
-    buf[i] = b;
-    return;
-  }
-  const int2 m = ((const int2*)tr.shadow_map)[i];
-  if (m.x >= 0) buf[m.x] = b;
-  if (m.y >= 0) buf[m.y] = b;
-}
 // Index-mapped shadows: the 4 map entries of elements i..i+3 (two 16-byte loads), fetched together
 // with the parameter data so the shadow stores do not wait on a dependent load after the update.
 struct Map4 {
@@ -79,34 +62,11 @@ __device__ __forceinline__ void shadow_store4(const TensorRec& tr, int64_t i, co
   }
 }
 
-struct AdamHyper {  // 8 floats per group
-  float lr, beta1, beta2, eps, wd, decoupled, maximize, pad;
-};
 
 template <typename G>
 __device__ __forceinline__ float gload(const G* g, int64_t i);
 template <> __device__ __forceinline__ float gload<float>(const float* g, int64_t i) { return g[i]; }
 template <> __device__ __forceinline__ float gload<uint16_t>(const uint16_t* g, int64_t i) { return bf2f(g[i]); }
-
-// Device step counter: every block reads it first thing; each block takes a ticket at its END
-// (the atomic's round trip then overlaps nothing on the block's critical path) and the last one
-// advances the counter — every block has read the old value by then.
-__device__ __forceinline__ float read_step(const float* step) {
-  __shared__ float s_step;
-  if (threadIdx.x == 0) s_step = step[0];
-  __syncthreads();
-  return s_step;
-}
-
-__device__ __forceinline__ void advance_step(float* step, unsigned* counter, bool skip, float cur) {
-  if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == gridDim.x - 1) {
-      if (!skip) step[0] = cur + 1.f;
-      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
 
 template <typename G>
 __device__ __forceinline__ void zero_chunk(G* g, int64_t start, int64_t end) {
@@ -132,24 +92,12 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
     G* __restrict__ g = (G*)tr.g;
     float* __restrict__ m = (float*)tr.s0;
     float* __restrict__ v = (float*)tr.s1;
-    const float bc1 = 1.f - __powf(h.beta1, t);
-    const float bc2 = 1.f - __powf(h.beta2, t);
-    const float step_size = h.lr / bc1;
-    const float rbc2 = rsqrtf(bc2);
+    const AdamStep k = adam_step(h, t);
     const float gs = inv_scale ? inv_scale[0] : 1.f;
-    const float decay = h.decoupled != 0.f ? 1.f - h.lr * h.wd : 1.f;
-    const float l2 = h.decoupled != 0.f ? 0.f : h.wd;
-    const float sgn = h.maximize != 0.f ? -1.f : 1.f;
     constexpr int CH = J * 4 * kThreads;
     const int64_t start = (int64_t)bt.y * CH;
     const int64_t end = min(start + (int64_t)CH, tr.n);
-    auto upd = [&](float& pp, float gg, float& mm, float& vv) {
-      gg = sgn * gg * gs + l2 * pp;
-      pp *= decay;
-      mm = h.beta1 * mm + (1.f - h.beta1) * gg;
-      vv = h.beta2 * vv + (1.f - h.beta2) * gg * gg;
-      pp -= step_size * mm / (sqrtf(vv) * rbc2 + h.eps);
-    };
+    auto upd = [&](float& pp, float gg, float& mm, float& vv) { adam_update(k, pp, gg * gs, mm, vv); };
     const bool vec = sizeof(G) == 4 && ((tr.p | tr.g | tr.s0 | tr.s1) & 15) == 0;
     if (vec && end - start == CH) {
       // full chunk: all 4*J float4 loads of the thread in flight before the first update

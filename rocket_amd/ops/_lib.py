@@ -56,7 +56,7 @@ KERNEL_SIGS = {
     "rk_mlp3_wgrad": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                               c_int, c_void_p, c_void_p, c_void_p]),
     "rk_mlp3_wgrad_loss": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_int, c_void_p]),
     "rk_optim_chunk_for": (c_int, [c_int64]),

@@ -262,6 +262,36 @@ class _LossFin(ctypes.Structure):
                 ("ring_size", ctypes.c_int), ("acc_scale", ctypes.c_float), ("sync", ctypes.c_int)]
 
 
+class _TensorRec(ctypes.Structure):
+    """Mirror of ``rk_opt::TensorRec`` (optim_common.h)."""
+
+    _fields_ = [(n, ctypes.c_int64) for n in ("p", "g", "s0", "s1", "n", "group", "shadow_map", "shadow_buf")]
+
+
+class _WgradEpi(ctypes.Structure):
+    """Mirror of ``struct WgradEpi`` (mlp.hip): the optimizer update applied by the wgrad launch."""
+
+    _fields_ = [("hyper", ctypes.c_void_p), ("step", ctypes.c_void_p), ("counter", ctypes.c_void_p),
+                ("ngroups", ctypes.c_int), ("zero_grads", ctypes.c_int), ("rdw", _TensorRec * 3),
+                ("rdb", _TensorRec * 3), ("rsl", _TensorRec * 4)]
+
+
+def _optimizer_epilogue(params, direct):
+    """The armed fused optimizer's update records for the 10 LeNet parameters (or None): the weight-
+    gradient launch then applies the step's Adam update as each final gradient element is formed."""
+    opt = getattr(params[4], "_rocket_optimizer", None)
+    if opt is None or not getattr(opt, "epilogue_armed", False) or not direct:
+        return None, None
+    spec = opt.epilogue(params)
+    if spec is None:
+        return None, None
+    ngroups, hyper, step, counter, recs = spec
+    r = [_TensorRec(*rec) for rec in recs]  # params order: w1 b1 w2 b2 f1w f1b f2w f2b f3w f3b
+    epi = _WgradEpi(hyper, step, counter, ngroups, 1, (_TensorRec * 3)(r[8], r[6], r[4]),
+                    (_TensorRec * 3)(r[9], r[7], r[5]), (_TensorRec * 4)(r[0], r[1], r[2], r[3]))
+    return epi, opt
+
+
 class _LeNetFused(torch.autograd.Function):
     """The whole LeNet: conv stack + classifier forward in ONE launch (after a tiny weight-fragment
     prep launch), classifier input-gradient chain + conv backward in ONE launch, the three
@@ -345,13 +375,17 @@ class _LeNetFused(torch.autograd.Function):
         sizes = [bufs[i].numel() for i in range(4)]
         assert sum(sizes) == int(lib.rk_lenet_slab_cols()), "fused LeNet expects conv1 6x1x5x5 / conv2 16x6x5x5"
         bounds = (ctypes.c_int * 5)(0, sizes[0], sizes[0] + sizes[1], sizes[0] + sizes[1] + sizes[2], sum(sizes))
+        epi, opt = _optimizer_epilogue(params, direct)
         _lib.check(lib.rk_mlp3_wgrad_loss(3, P(*[q[0].data_ptr() for q in probs]), P(*[q[1].data_ptr() for q in probs]),
                                           P(*[q[2].data_ptr() for q in probs]), P(*[q[3].data_ptr() for q in probs]),
                                           I(*[q[4] for q in probs]), I(*[q[5] for q in probs]), N, slab.data_ptr(),
                                           N // 4, slab.shape[1],
                                           (ctypes.c_void_p * 4)(*[bufs[i].data_ptr() for i in range(4)]), bounds,
-                                          ctypes.byref(fin) if fin is not None else None, stream),
+                                          ctypes.byref(fin) if fin is not None else None,
+                                          ctypes.byref(epi) if epi is not None else None, stream),
                    "rk_mlp3_wgrad_loss")
+        if opt is not None:
+            opt.epilogue_done = True  # the optimizer's own launch for this step is skipped
         del keep  # partials: read by the wgrad launch (stream-ordered before any reuse)
         return (None, *_finish(params, bufs, direct), None)
 

@@ -182,6 +182,9 @@ class _FusedBase(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self.epilogue_done:  # the gradient producer already applied this step's update
+            self.epilogue_done = False
+            return loss
         if self.prepare():
             self.launch()
         return loss
@@ -215,6 +218,35 @@ class _FusedBase(torch.optim.Optimizer):
     @property
     def device_step(self) -> Optional[torch.Tensor]:
         return self._step_dev
+
+    # ------------------------------------------------- update epilogue
+    # A kernel that produces parameters' FINAL gradients can apply the update itself (the fused
+    # LeNet weight-gradient launch does): the Optimizer capsule arms it for one step when that is
+    # exact (single replica, gradient-sync step, no AMP scaler); the producer asks for the records
+    # with ``epilogue(params)``, reports ``epilogue_done``, and the step's own launch is skipped.
+    epilogue_armed = False
+    epilogue_done = False
+
+    def epilogue(self, params) -> Optional[tuple]:
+        """``(ngroups, hyper_ptr, step_ptr, counter_ptr, records)`` when ``params`` are exactly this
+        optimizer's active parameters and the epilogue is armed; ``records[i]`` is the 8-int64 tensor
+        record of ``params[i]`` (p, grad, state0, state1, numel, group, shadow map, shadow buffer)."""
+        if not (self.epilogue_armed and self.KIND == 0 and self._tables is not None and self._gdtype == 0):
+            return None
+        active = self._active()
+        if len(active) != len(params) or {id(p) for _, p in active} != {id(p) for p in params}:
+            return None
+        if len(self.param_groups) > 4 or self.grad_scale is not None or self.found_inf is not None:
+            return None
+        gidx = {id(p): gi for gi, p in active}
+        recs = []
+        for p in params:
+            st = self.state[p]
+            s = [st[k].data_ptr() for k in self.STATE_KEYS]
+            recs.append((p.data_ptr(), p.grad.data_ptr(), s[0], s[1], p.numel(), gidx[id(p)], *self._shadow_ptrs(p)))
+        dev = self._device
+        return (len(self.param_groups), self._hyper_dev.data_ptr(), self._step_dev.data_ptr(),
+                _lib.Workspace.get(dev).counter(f"optim_{id(self)}"), recs)
 
 
 class FusedAdamW(_FusedBase):
