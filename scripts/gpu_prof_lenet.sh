@@ -5,11 +5,11 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/prof_lenet -o run -- python3 $R/bench.py --steps 200 --warmup 20 > $R/gpurun_out/prof_lenet.log 2>&1 || exit 1
-cd $R && f=$(find gpurun_out/prof_lenet -name '*kernel_trace.csv' | head -1) && python3 bench/summarize_trace.py "$f" --steps 50 --title "LeNet bs1024 fused step (HIP graph), 1x MI355X - rocprofv3 --kernel-trace" > gpurun_out/lenet_graph_kernels.md; rc=$?
+cd $R && f=$(find gpurun_out/prof_lenet -name '*kernel_trace.csv' | head -1) && python3 bench/summarize_trace.py "$f" --steps 50 --marker mlp3_wgrad_kernel --title "LeNet bs1024 fused step (captured, launch-list replay; AdamW fused into the wgrad launch), 1x MI355X - rocprofv3 --kernel-trace" > gpurun_out/lenet_graph_kernels.md; rc=$?
 python3 - "$f" > gpurun_out/lenet_graph_gaps.txt <<'PY'
 import csv, sys, statistics
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-rows = rows[-6 * 50:]
+rows = rows[-4 * 50:]
 prev = None
 gaps = {}
 for r in rows:
