@@ -10,7 +10,12 @@ the reference would run it.  Timing: a lowest-priority capsule records
 ``perf_counter`` deltas between consecutive iterations (the reference syncs the
 host every step via ``loss.item()``, so the deltas are true step times).
 
-Usage: ``python bench/reference_baseline.py --steps 60 --warmup 10 [--mp bf16]``
+``--device-data``: the synthetic tensors live on the GPU and the
+map-style dataset implements ``__getitems__`` (one ``index_select`` per batch, identity
+``collate_fn`` passed through the reference capsule's DataLoader kwargs), so the reference
+is not charged for host-side collation of 1024 samples per step.
+
+Usage: ``python bench/reference_baseline.py --steps 60 --warmup 10 [--mp bf16] [--device-data]``
 (single process; for N>1 launch under torchrun).  Prints one JSON line.
 """
 
@@ -55,12 +60,34 @@ class CE(nn.Module):
         return F.cross_entropy(b[2], b[1])
 
 
+class _DeviceBatches(torch.utils.data.Dataset):
+    """Map-style dataset over GPU tensors with batched fetching (``__getitems__``)."""
+
+    def __init__(self, x, y):
+        self.x, self.y = x, y
+
+    def __len__(self):
+        return self.x.shape[0]
+
+    def __getitem__(self, i):
+        return self.x[i], self.y[i]
+
+    def __getitems__(self, idx):
+        i = torch.as_tensor(idx, device=self.x.device)
+        return [self.x.index_select(0, i), self.y.index_select(0, i)]
+
+
+def _identity(batch):
+    return batch
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--mp", default="no")
+    ap.add_argument("--device-data", action="store_true")
     args = ap.parse_args()
 
     import rocket  # the reference package from _refbase
@@ -72,6 +99,11 @@ def main():
     X = torch.rand(n, 1, 28, 28, generator=g)
     Y = torch.randint(0, 10, (n,), generator=g)
     ds = torch.utils.data.TensorDataset(X, Y)
+    loader_kw = {}
+    if args.device_data:
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        ds = _DeviceBatches(X.to(dev), Y.to(dev))
+        loader_kw["collate_fn"] = _identity
 
     deltas = []
 
@@ -93,7 +125,7 @@ def main():
         [
             rocket.Looper(
                 [
-                    rocket.Dataset(ds, batch_size=args.batch),
+                    rocket.Dataset(ds, batch_size=args.batch, **loader_kw),
                     rocket.Module(net, capsules=[rocket.Loss(objective=CE()), rocket.Optimizer(opt), rocket.Scheduler(sched)]),
                     Timer(),
                 ],
@@ -112,6 +144,7 @@ def main():
     mean = sum(steady) / len(steady)
     rec = {
         "impl": "reference dsenushkin/rocket (accelerate + torch eager)",
+        "data": "GPU-resident, one index_select per batch" if args.device_data else "host TensorDataset + collate",
         "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu",
         "mixed_precision": args.mp,
         "world": world,

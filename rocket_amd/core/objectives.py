@@ -20,6 +20,7 @@ Parity:
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -27,11 +28,13 @@ from rocket_amd.core.attributes import Attributes
 from rocket_amd.core.capsule import Capsule
 from rocket_amd.ops import data as _data_ops
 from rocket_amd.runtime import comm as _comm
-from rocket_amd.utils.lazy import LazyScalar
+from rocket_amd.utils.lazy import LazyScalar, materialize
 
 
 class Loss(Capsule):
-    RING = 1024  # device slots for reported losses under graph replay (tracker flushes far sooner)
+    # device slots for reported losses under graph replay; values still unread when their slot is
+    # about to be rewritten (one lap later) are materialised first, in one D2H copy per lap
+    RING = 1024
 
     def __init__(self, objective: torch.nn.Module, tag: str = "train_loss", priority: int = 1100) -> None:
         super().__init__(statefull=True, priority=priority)
@@ -43,6 +46,7 @@ class Loss(Capsule):
         self._ring = None       # graph mode: reported values, one slot per sync step
         self._slot = None       # graph mode: device write cursor into the ring
         self._slot_host = 0
+        self._lap = []          # weak references to this lap's posted LazyScalars
         self._acc_pending = False
 
     def _mean_over_ranks(self, loss: torch.Tensor) -> torch.Tensor:
@@ -99,6 +103,11 @@ class Loss(Capsule):
         self._ring_views = list(self._ring.unbind(0))  # one 0-d view per slot, made once
 
     def graph_prepare(self, attrs: Attributes | None = None) -> None:
+        if self._slot_host == 0 and self._lap:
+            # the coming replay starts a new lap of the ring: resolve what the last lap posted
+            # (a consumer may keep a reported loss across >RING steps) before it is overwritten
+            materialize([r() for r in self._lap if r() is not None])
+            self._lap = []
         v = self._value
         if isinstance(v, torch.Tensor) or v != 0.0:  # fold an eager partial GA window
             self._acc.add_(v if isinstance(v, torch.Tensor) else float(v))
@@ -135,6 +144,7 @@ class Loss(Capsule):
             return
         self._acc_pending = False
         value = LazyScalar(self._ring_views[self._slot_host])
+        self._lap.append(weakref.ref(value))
         self._slot_host = (self._slot_host + 1) % self.RING
         if attrs.tracker is not None:
             attrs.tracker.scalars.append(Attributes(step=self._step, data={self._tag: value}))
@@ -194,7 +204,9 @@ class Optimizer(Capsule):
 
     # ---------------------------------------------------- HIP-graph protocol
     def graph_supported(self) -> bool:
-        return hasattr(self._optimizer, "fused_zero_ok") and self._optimizer.fused_zero_ok()
+        # fp16 steps are not captured: the scaler reports skipped steps through a host copy
+        return (hasattr(self._optimizer, "fused_zero_ok") and self._optimizer.fused_zero_ok()
+                and self._accelerator.scaler is None)
 
     def graph_token(self):
         return self._optimizer.optimizer.version

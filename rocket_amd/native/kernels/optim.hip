@@ -15,8 +15,9 @@
 // that GEMMs read directly instead of casting the fp32 master every forward).  A kernel that consumes the weights as pre-arranged bf16 MFMA fragments (the
 // fused LeNet's fragment table) then needs no per-step re-layout launch.
 //
-// Optional AMP hooks: `inv_scale` multiplies every gradient (GradScaler unscale
-// folded into the update) and a non-zero `found_inf` makes the launch a no-op.
+// Optional AMP (fp16 dynamic loss scaling, all on the device): rk_amp_check flags non-finite
+// gradients; the update multiplies every gradient by 1/scale (GradScaler's unscale folded into the
+// update), a set flag makes the launch a no-op, and its last block runs the scale update.
 // `zero_grads` clears each gradient chunk after it is consumed (the
 // optimizer.step(); optimizer.zero_grad() pair in one pass over the gradient).
 //
@@ -77,13 +78,12 @@ template <typename G, bool ZG, int J>
 __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __restrict__ tensors,
                                                           const int2* __restrict__ blocks,
                                                           const AdamHyper* __restrict__ hyper, float* step,
-                                                          const float* inv_scale, const float* found_inf,
-                                                          unsigned* counter) {
+                                                          float* amp, unsigned* counter) {
   // block record + chunk index + step counter loads all in flight at once (the tensor table holds
   // one record per BLOCK: no dependent table walk before the data loads)
   const int2 bt = blocks[blockIdx.x];
   const TensorRec tr = tensors[blockIdx.x];
-  const bool skip = found_inf != nullptr && found_inf[0] != 0.f;
+  const bool skip = amp != nullptr && amp[kAmpFound] != 0.f;
   const float cur = read_step(step);
   const float t = cur + 1.f;
   if (!skip) {
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
     float* __restrict__ m = (float*)tr.s0;
     float* __restrict__ v = (float*)tr.s1;
     const AdamStep k = adam_step(h, t);
-    const float gs = inv_scale ? inv_scale[0] : 1.f;
+    const float gs = amp ? amp[kAmpInv] : 1.f;
     constexpr int CH = J * 4 * kThreads;
     const int64_t start = (int64_t)bt.y * CH;
     const int64_t end = min(start + (int64_t)CH, tr.n);
@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(kThreads) adam_mt_kernel(const TensorRec* __re
     const int64_t start = (int64_t)bt.y * CH;
     zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)CH, tr.n));
   }
-  advance_step(step, counter, skip, cur);
+  advance_step(step, counter, skip, cur, amp);
 }
 
 struct SgdHyper {  // 8 floats per group
@@ -171,11 +171,10 @@ template <typename G, bool ZG, int J>
 __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __restrict__ tensors,
                                                          const int2* __restrict__ blocks,
                                                          const SgdHyper* __restrict__ hyper, float* step,
-                                                         const float* inv_scale, const float* found_inf,
-                                                         unsigned* counter) {
+                                                         float* amp, unsigned* counter) {
   const int2 bt = blocks[blockIdx.x];
   const TensorRec tr = tensors[blockIdx.x];
-  const bool skip = found_inf != nullptr && found_inf[0] != 0.f;
+  const bool skip = amp != nullptr && amp[kAmpFound] != 0.f;
   const float cur = read_step(step);
   if (!skip) {
     const SgdHyper h = hyper[tr.group];
@@ -183,7 +182,7 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
     G* g = (G*)tr.g;
     float* buf = (float*)tr.s0;
     const bool first = cur == 0.f;  // momentum buffer initialised with the first gradient (torch semantics)
-    const float gs = inv_scale ? inv_scale[0] : 1.f;
+    const float gs = amp ? amp[kAmpInv] : 1.f;
     const float sgn = h.maximize != 0.f ? -1.f : 1.f;
     constexpr int CH = J * 4 * kThreads;
     const int64_t start = (int64_t)bt.y * CH;
@@ -204,7 +203,7 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
     const int64_t start = (int64_t)bt.y * CH;
     zero_chunk<G>((G*)tr.g, start, min(start + (int64_t)CH, tr.n));
   }
-  advance_step(step, counter, skip, cur);
+  advance_step(step, counter, skip, cur, amp);
 }
 
 }  // namespace
@@ -214,17 +213,50 @@ __global__ void __launch_bounds__(kThreads) sgd_mt_kernel(const TensorRec* __res
 RK_API int rk_optim_chunk_for(int64_t total) { return total <= (int64_t)(1 << 21) ? kChunk / 4 : kChunk; }
 RK_API int rk_optim_chunk() { return kChunk; }
 
+// Non-finite check of every gradient of the tables (fp16 AMP): any inf/NaN in a block's chunk sets
+// amp[kAmpFound] (plain stores of the same value; the optimizer launch consumes and clears it).
+template <typename G, int J>
+__global__ void __launch_bounds__(kThreads) amp_check_kernel(const TensorRec* __restrict__ tensors,
+                                                            const int2* __restrict__ blocks, float* amp) {
+  const int2 bt = blocks[blockIdx.x];
+  const TensorRec tr = tensors[blockIdx.x];
+  constexpr int CH = J * 4 * kThreads;
+  const int64_t start = (int64_t)bt.y * CH;
+  const int64_t end = min(start + (int64_t)CH, tr.n);
+  const G* g = (const G*)tr.g;
+  bool bad = false;
+  for (int64_t i = start + threadIdx.x; i < end; i += kThreads) bad |= !(fabsf(gload<G>(g, i)) <= 3.4028235e38f);
+  if (__syncthreads_or(bad) && threadIdx.x == 0) amp[kAmpFound] = 1.f;
+}
+
+RK_API int rk_amp_check(int gdtype, const void* tensors, const void* blocks, int nblocks, float* amp, int chunk,
+                        hipStream_t s) {
+  if (nblocks <= 0) return 0;
+  if (chunk != kChunk && chunk != kChunk / 4) return (int)hipErrorInvalidValue;
+  const TensorRec* t = (const TensorRec*)tensors;
+  const int2* b = (const int2*)blocks;
+  if (gdtype == BF16)
+    chunk == kChunk ? amp_check_kernel<uint16_t, 4><<<nblocks, kThreads, 0, s>>>(t, b, amp)
+                    : amp_check_kernel<uint16_t, 1><<<nblocks, kThreads, 0, s>>>(t, b, amp);
+  else
+    chunk == kChunk ? amp_check_kernel<float, 4><<<nblocks, kThreads, 0, s>>>(t, b, amp)
+                    : amp_check_kernel<float, 1><<<nblocks, kThreads, 0, s>>>(t, b, amp);
+  return (int)hipGetLastError();
+}
+
 // kind: 0 = Adam/AdamW, 1 = SGD.  gdtype: grads dtype (0 f32, 1 bf16).  chunk: 1024 or 4096.
+// amp: nullptr, or the device loss-scaling state (AmpSlot layout): gradients are unscaled by
+// amp[kAmpInv] inside the update, a set found flag makes the step a no-op (step counter kept),
+// and the last block applies the scale update.
 RK_API int rk_optim_mt(int kind, int gdtype, const void* tensors, const void* blocks, int nblocks, const void* hyper,
-                       float* step, const float* inv_scale, const float* found_inf, unsigned* counter, int zero_grads,
-                       int chunk, hipStream_t s) {
+                       float* step, float* amp, unsigned* counter, int zero_grads, int chunk, hipStream_t s) {
   if (nblocks <= 0) return 0;
   if (chunk != kChunk && chunk != kChunk / 4) return (int)hipErrorInvalidValue;
   const TensorRec* t = (const TensorRec*)tensors;
   const int2* b = (const int2*)blocks;
 #define RK_OPT_LAUNCH_J(KERNEL, G, H, J)                                                                              \
-  (zero_grads ? KERNEL<G, true, J><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, inv_scale, found_inf, counter) \
-              : KERNEL<G, false, J><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, inv_scale, found_inf, counter))
+  (zero_grads ? KERNEL<G, true, J><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, amp, counter) \
+              : KERNEL<G, false, J><<<nblocks, kThreads, 0, s>>>(t, b, (const H*)hyper, step, amp, counter))
 #define RK_OPT_LAUNCH(KERNEL, G, H) \
   (chunk == kChunk ? RK_OPT_LAUNCH_J(KERNEL, G, H, 4) : RK_OPT_LAUNCH_J(KERNEL, G, H, 1))
   if (kind == 0) {

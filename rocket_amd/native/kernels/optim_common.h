@@ -41,11 +41,42 @@ __device__ __forceinline__ float read_step(const float* step) {
   return s_step;
 }
 
-__device__ __forceinline__ void advance_step(float* step, unsigned* counter, bool skip, float cur) {
+// Device-resident dynamic loss scaling (fp16 AMP; torch.amp.GradScaler semantics):
+//   amp[0] scale, amp[1] 1/scale, amp[2] found_inf (set by rk_amp_check, consumed + cleared here),
+//   amp[3] growth tracker, amp[4] growth factor, amp[5] backoff factor, amp[6] growth interval,
+//   amp[7] found_inf of the last step (read back by the host only when it must know).
+enum AmpSlot { kAmpScale = 0, kAmpInv, kAmpFound, kAmpTracker, kAmpGrowth, kAmpBackoff, kAmpInterval, kAmpLast };
+
+// torch._amp_update_scale_, executed by the optimizer launch's last block
+__device__ __forceinline__ void amp_update(float* amp) {
+  const float found = amp[kAmpFound];
+  float scale = amp[kAmpScale];
+  if (found != 0.f) {
+    scale *= amp[kAmpBackoff];
+    amp[kAmpTracker] = 0.f;
+  } else {
+    const float ok = amp[kAmpTracker] + 1.f;
+    if (ok >= amp[kAmpInterval]) {
+      const float grown = scale * amp[kAmpGrowth];
+      if (__builtin_isfinite(grown)) scale = grown;
+      amp[kAmpTracker] = 0.f;
+    } else {
+      amp[kAmpTracker] = ok;
+    }
+  }
+  amp[kAmpScale] = scale;
+  amp[kAmpInv] = 1.f / scale;
+  amp[kAmpLast] = found;
+  amp[kAmpFound] = 0.f;  // every block has read it: each took its ticket after its first read
+}
+
+__device__ __forceinline__ void advance_step(float* step, unsigned* counter, bool skip, float cur,
+                                             float* amp = nullptr) {
   if (threadIdx.x == 0) {
     const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
       if (!skip) step[0] = cur + 1.f;
+      if (amp) amp_update(amp);
       __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

@@ -19,8 +19,11 @@
 // changes, so the argument holds per block even when n differs between launches (all ranks issue
 // the same sequence of launches).
 //
-// A poll that exceeds ~30 s records an error in host-mapped memory and gives up instead of hanging
-// the GPU (the Python side checks it); the kernel never waits on anything but peer flags.
+// A poll that exceeds the timeout (30 s; a few seconds for the creation self-test) records an error
+// in host-mapped memory and gives up instead of hanging the GPU; the timed-out block then skips its
+// reduce and leaves its gradients untouched.  The host reads the error word (a plain host load)
+// on every launch and before the optimizer consumes reduced gradients.  The kernel never waits on
+// anything but peer flags.
 #include "rk_common.h"
 
 #include <cstring>
@@ -34,7 +37,7 @@ constexpr int kThreads = 256;
 constexpr int kVec = 4;                              // floats per 16-byte vector
 constexpr int kUnroll = 2;                           // vectors per thread
 constexpr int kChunk = kThreads * kVec * kUnroll;    // 2048 floats per block (8 KB)
-constexpr uint64_t kTimeoutTicks = 30ull * 100000000ull;  // s_memrealtime runs at 100 MHz
+constexpr uint64_t kTicksPerSecond = 100000000ull;   // s_memrealtime runs at 100 MHz
 
 struct P2PArgs {
   float* stage[kMaxPeers];      // every rank's stage base (self included), 2 * cap floats each
@@ -43,6 +46,7 @@ struct P2PArgs {
   unsigned* err;                // host-mapped error word
   float* data;
   int64_t n, cap;
+  uint64_t timeout_ticks;
   float scale;
   int rank, world;
 };
@@ -54,8 +58,12 @@ __device__ __forceinline__ unsigned load_flag(const unsigned* p) {
 template <int W>
 __global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a) {
   __shared__ unsigned s_ep;
+  __shared__ int s_timeout;
   const int b = blockIdx.x, t = threadIdx.x;
-  if (t == 0) s_ep = a.epoch[b] + 1;
+  if (t == 0) {
+    s_ep = a.epoch[b] + 1;
+    s_timeout = 0;
+  }
   __syncthreads();
   const unsigned ep = s_ep;
   const int64_t par = (int64_t)(ep & 1) * a.cap;
@@ -87,8 +95,9 @@ __global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while ((int)(load_flag(f) - ep) < 0) {
           __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
             __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_timeout = 1;
             break;
           }
         }
@@ -98,6 +107,9 @@ __global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  // a peer that never signalled: its stage holds stale data -- leave this block's gradients
+  // untouched (the host raises on the error word before they are used)
+  if (s_timeout) return;
   if (t >= 64) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // this wave's view of the peers' stages
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -134,6 +146,7 @@ __global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a) {
 
 struct P2PCtx {
   int rank = 0, world = 0, device = 0;
+  double timeout_s = 30.0;
   int64_t cap = 0;
   int max_blocks = 0;
   float* stage = nullptr;
@@ -251,6 +264,7 @@ RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipS
   a.n = n;
   a.cap = c->cap;
   a.scale = scale;
+  a.timeout_ticks = (uint64_t)(c->timeout_s * (double)kTicksPerSecond);
   a.rank = c->rank;
   a.world = c->world;
   const int blocks = (int)((n + kChunk - 1) / kChunk);
@@ -265,6 +279,22 @@ RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipS
     default: p2p_allreduce_kernel<8><<<blocks, kThreads, 0, s>>>(a); break;
   }
   return (int)hipGetLastError();
+}
+
+// Peer-poll timeout of later launches (seconds; default 30).  The creation self-test uses a short one.
+RK_API int rk_p2p_set_timeout(void* ctx, double seconds) {
+  if (!ctx || !(seconds > 0.0)) return (int)hipErrorInvalidValue;
+  ((P2PCtx*)ctx)->timeout_s = seconds;
+  return 0;
+}
+
+// Host address of the error word (host-mapped memory: Python polls it with a plain load).
+RK_API void* rk_p2p_error_ptr(void* ctx) { return ((P2PCtx*)ctx)->err_h; }
+
+// Clear the error word (after the caller has handled a reported timeout).
+RK_API int rk_p2p_clear_error(void* ctx) {
+  __atomic_store_n(((P2PCtx*)ctx)->err_h, 0u, __ATOMIC_RELEASE);
+  return 0;
 }
 
 // 0 = healthy; 1 = a peer never signalled within the timeout (results of that launch are invalid)

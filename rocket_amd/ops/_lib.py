@@ -57,8 +57,9 @@ KERNEL_SIGS = {
                               c_int, c_void_p, c_void_p, c_void_p]),
     "rk_mlp3_wgrad_loss": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                    c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_int, c_void_p]),
+    "rk_amp_check": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "rk_optim_chunk_for": (c_int, [c_int64]),
     "rk_gather_rows": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_loss_accum": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_int, c_void_p]),
@@ -87,6 +88,9 @@ KERNEL_SIGS = {
     "rk_p2p_open": (c_int, [c_void_p, c_void_p]),
     "rk_p2p_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     "rk_p2p_error": (c_int, [c_void_p]),
+    "rk_p2p_set_timeout": (c_int, [c_void_p, ctypes.c_double]),
+    "rk_p2p_clear_error": (c_int, [c_void_p]),
+    "rk_p2p_error_ptr": (c_void_p, [c_void_p]),
     "rk_p2p_destroy": (c_int, [c_void_p]),
     "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 10 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
 }

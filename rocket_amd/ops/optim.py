@@ -45,8 +45,11 @@ class _FusedBase(torch.optim.Optimizer):
         self._nblocks = 0
         self._chunk = 0
         self.version = 0  # bumped whenever a device table/state pointer changes (captured graphs go stale)
-        self.grad_scale: Optional[torch.Tensor] = None  # 1/scale (AMP); device scalar
-        self.found_inf: Optional[torch.Tensor] = None
+        # fp16 AMP: the device loss-scaling state of a FusedGradScaler (optim_common.h AmpSlot
+        # layout), set for the launches of a scaled step.  torch.amp.GradScaler instead drives the
+        # ``_step_supports_amp_scaling`` protocol below (grad_scale / found_inf tensors).
+        self.amp: Optional[torch.Tensor] = None
+        self._torch_amp = None
 
     # ----------------------------------------------------------- host side
     def _active(self) -> List[tuple]:
@@ -163,18 +166,43 @@ class _FusedBase(torch.optim.Optimizer):
         return (idx.data_ptr(), buf.data_ptr())
 
     # --------------------------------------------------------- device side
+    def amp_check(self, amp: torch.Tensor) -> None:
+        """Flag non-finite gradients into ``amp`` (one launch over the same block tables)."""
+        _lib.check(_lib.kernels().rk_amp_check(self._gdtype, self._tables[0].data_ptr(), self._tables[1].data_ptr(),
+                                               self._nblocks, amp.data_ptr(), self._chunk,
+                                               _lib.stream_ptr(self._device)), "rk_amp_check")
+
     def launch(self, zero_grads: bool = False) -> None:
         """Enqueue the fused update (graph-capturable); ``zero_grads`` also clears the consumed gradients."""
         lib = _lib.kernels()
         dev = self._device
+        amp = self.amp if self.amp is not None else self._torch_amp
         _lib.check(
             lib.rk_optim_mt(self.KIND, self._gdtype, self._tables[0].data_ptr(), self._tables[1].data_ptr(),
-                            self._nblocks, self._hyper_dev.data_ptr(), self._step_dev.data_ptr(),
-                            _lib.ptr(self.grad_scale), _lib.ptr(self.found_inf),
+                            self._nblocks, self._hyper_dev.data_ptr(), self._step_dev.data_ptr(), _lib.ptr(amp),
                             _lib.Workspace.get(dev).counter(f"optim_{id(self)}"), int(zero_grads), self._chunk,
                             _lib.stream_ptr(dev)),
             "rk_optim_mt",
         )
+
+    # torch.amp.GradScaler protocol: with this flag GradScaler.step() skips its own unscale and
+    # hands over `grad_scale` (the scale, or None when already unscaled) and `found_inf` tensors
+    _step_supports_amp_scaling = True
+
+    def _torch_amp_state(self) -> Optional[torch.Tensor]:
+        gs, fi = getattr(self, "grad_scale", None), getattr(self, "found_inf", None)
+        if gs is None and fi is None:
+            return None
+        # a private AmpSlot block: unscale by grad_scale, skip on found_inf; GradScaler.update()
+        # (host side) keeps owning the scale, so growth/backoff here are inert
+        amp = torch.zeros(8, dtype=torch.float32, device=self._device)
+        amp[1] = 1.0
+        amp[6] = float("inf")
+        if gs is not None:  # torch hands over the scale itself (its fused kernels divide by it)
+            amp[1:2].copy_(1.0 / gs.reshape(1).float())
+        if fi is not None:
+            amp[2:3].copy_(fi.reshape(1).float())
+        return amp
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -186,7 +214,11 @@ class _FusedBase(torch.optim.Optimizer):
             self.epilogue_done = False
             return loss
         if self.prepare():
-            self.launch()
+            self._torch_amp = self._torch_amp_state()
+            try:
+                self.launch()
+            finally:
+                self._torch_amp = None
         return loss
 
     # ------------------------------------------------------------- state
@@ -236,7 +268,7 @@ class _FusedBase(torch.optim.Optimizer):
         active = self._active()
         if len(active) != len(params) or {id(p) for _, p in active} != {id(p) for p in params}:
             return None
-        if len(self.param_groups) > 4 or self.grad_scale is not None or self.found_inf is not None:
+        if len(self.param_groups) > 4 or self.amp is not None:
             return None
         gidx = {id(p): gi for gi, p in active}
         recs = []

@@ -22,11 +22,13 @@ Design for MI355X + RCCL over xGMI (SURVEY §5 "communication design"):
   synchronisation;
 * **accumulation aware** – inside ``no_sync()`` nothing is communicated and
   gradients keep accumulating in the bucket views;
-* params that received no gradient in a step have their slot zeroed before
-  the final bucket is reduced (no stale data is ever averaged in);
+* params that received no gradient in the whole accumulation window have their
+  slot zeroed before the final bucket is reduced (no stale data is ever averaged
+  in); a param unused only in the sync micro-step keeps its accumulated gradient;
 * rank-0 parameters and buffers are broadcast once at construction as one flat
   buffer per dtype (N3); module buffers (BatchNorm statistics) are broadcast
-  from rank 0 before each synchronised forward (N4, ``broadcast_buffers``).
+  from rank 0 before each synchronised forward (N4, ``broadcast_buffers``) as
+  ONE persistent byte buffer: one multi-tensor copy + one collective.
 
 A native RCCL communicator (``rocket_amd.parallel.rccl``) can be plugged in
 through ``comm=``; the default uses the ``torch.distributed`` RCCL group, except that when all
@@ -49,7 +51,7 @@ SIDE_SLOTS = 16
 
 
 class _Bucket:
-    __slots__ = ("index", "params", "offsets", "flat", "pending", "work", "ready", "numel_params")
+    __slots__ = ("index", "params", "offsets", "flat", "pending", "work", "ready", "touched", "numel_params")
 
     def __init__(self, index: int, params: List[nn.Parameter], dtype, device, extra: int = 0):
         self.index = index
@@ -63,7 +65,8 @@ class _Bucket:
         self.flat = torch.zeros(n + extra, dtype=dtype, device=device)
         self.pending = len(params)
         self.work = None
-        self.ready: set = set()
+        self.ready: set = set()    # params that reported a gradient in this (sync) backward
+        self.touched: set = set()  # params that got a gradient anywhere in the accumulation window
 
     def view(self, i: int) -> torch.Tensor:
         from rocket_amd.parallel.flat_grads import _param_view
@@ -125,7 +128,11 @@ class DataParallel(nn.Module):
         self.comm = comm or _TorchDistComm()
         self.broadcast_buffers = broadcast_buffers
         self.require_backward_grad_sync = True
+        self._rank = getattr(self.comm, "rank", None)
+        if self._rank is None:
+            self._rank = dist.get_rank(getattr(self.comm, "group", None)) if dist.is_initialized() else 0
         self._sync_module_states()
+        self._flat_buffers = self._pack_buffers() if broadcast_buffers else None
         self._build_buckets(bucket_cap_mb, first_bucket_mb)
         self._armed = False
         self._deferred = False
@@ -153,6 +160,29 @@ class DataParallel(nn.Module):
         tensors = [p.data for p in self.module.parameters()] + list(self.module.buffers())
         if tensors:
             self._flat_broadcast(tensors)
+
+    def _pack_buffers(self) -> Optional[torch.Tensor]:
+        """Persistent byte buffer for the per-forward rank-0 broadcast of the module buffers
+        (BatchNorm running statistics, counters; N4): one collective on it per sync forward,
+        with one multi-tensor copy in (rank 0) or out (other ranks) -- not a cat, a broadcast
+        and a copy per buffer.  Each buffer keeps its own storage: views of one base would
+        share a version counter, and autograd checks the running statistics' versions."""
+        bufs, seen = [], set()
+        for b in self.module.buffers():
+            if b.numel() > 0 and id(b) not in seen:
+                seen.add(id(b))
+                bufs.append(b)
+        if not bufs or len({b.device for b in bufs}) != 1:
+            return None
+        offs, n = [], 0
+        for b in bufs:
+            offs.append(n)
+            n += (b.numel() * b.element_size() + 15) // 16 * 16  # every view 16-byte aligned
+        flat = torch.empty(n, dtype=torch.uint8, device=bufs[0].device)
+        self._bufs = bufs
+        self._buf_views = [flat[o : o + b.numel() * b.element_size()].view(b.dtype).view(b.shape)
+                           for o, b in zip(offs, bufs)]
+        return flat
 
     def _build_buckets(self, cap_mb: float, first_mb: float) -> None:
         params = [p for p in self.module.parameters() if p.requires_grad]
@@ -248,7 +278,16 @@ class DataParallel(nn.Module):
         return self.module(*args, **kwargs)
 
     def sync_buffers(self) -> None:
-        """Broadcast rank-0 module buffers (BatchNorm statistics) to every rank."""
+        """Broadcast rank-0 module buffers (BatchNorm statistics) to every rank: one collective on
+        the persistent flat buffer the buffers are views of."""
+        if self._flat_buffers is not None:
+            with torch.no_grad():
+                if self._rank == 0:
+                    torch._foreach_copy_(self._buf_views, self._bufs)
+                self.comm.broadcast(self._flat_buffers, 0)
+                if self._rank != 0:
+                    torch._foreach_copy_(self._bufs, self._buf_views)
+            return
         bufs = list(self.module.buffers())
         if bufs:
             self._flat_broadcast(bufs)
@@ -302,6 +341,7 @@ class DataParallel(nn.Module):
             with torch.no_grad():
                 view.copy_(p.grad)
             p.grad = view
+        b.touched.add(i)
         if self._deferred or not self._armed or i in b.ready:
             return
         if not self._finalize_queued:
@@ -323,10 +363,15 @@ class DataParallel(nn.Module):
             if b.work is None:
                 with torch.no_grad():
                     for i in range(len(b.params)):
-                        if i not in b.ready:
+                        # never-touched slots are zeroed (no stale data is averaged in); a param
+                        # unused in THIS micro-step but with gradient accumulated in earlier no_sync
+                        # micro-steps keeps it, as torch DDP all-reduces the defined local grad
+                        if i not in b.ready and i not in b.touched:
                             b.view(i).zero_()
                             b.params[i].grad = b.view(i)
                 b.work = self._launch(b)
+        for b in self.buckets:
+            b.touched.clear()  # the accumulation window ends with this reduction
         if self._native is not None:
             self._native.join()
         for b in self.buckets:
@@ -349,6 +394,7 @@ class DataParallel(nn.Module):
     def zero_(self) -> None:
         for b in self.buckets:
             b.flat.zero_()
+            b.touched.clear()
             for i, p in enumerate(b.params):
                 if p.grad is None or p.grad.data_ptr() != b.view(i).data_ptr():
                     p.grad = b.view(i)

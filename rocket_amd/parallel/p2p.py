@@ -48,6 +48,8 @@ class P2PAllReduce:
         self._ctx = ctx
         self.rank, self.world, self.cap, self.device = rank, world, cap, device
         self.launches = 0
+        # the kernel's error word lives in host-mapped memory: read it with a plain load, no call
+        self._err = ctypes.c_uint.from_address(_lib.kernels().rk_p2p_error_ptr(ctx))
 
     @classmethod
     def create(cls, cap: int, group=None, device: Optional[torch.device] = None) -> Optional["P2PAllReduce"]:
@@ -80,7 +82,41 @@ class P2PAllReduce:
             lib.rk_p2p_destroy(ctx)
             return None
         dist.barrier(group=group)  # every mapping exists before any rank launches
-        return cls(ctx.value, rank, world, int(cap), device)
+        out = cls(ctx.value, rank, world, int(cap), device)
+        ok = out._self_test()
+        oks = [None] * world
+        dist.all_gather_object(oks, ok, group=group)
+        if not all(oks):
+            if rank == 0:
+                logger.warning(f"p2p all-reduce failed its self-test on rank(s) "
+                               f"{[r for r, o in enumerate(oks) if not o]}; gradients stay on RCCL")
+            # the test launches have completed (or timed out) everywhere: safe to unmap
+            dist.barrier(group=group)
+            out.close()
+            return None
+        return out
+
+    def _self_test(self) -> bool:
+        """Reduce a rank-dependent pattern once (short peer timeout) and compare with its exact
+        sum.  Checks the cross-device IPC mappings and the flag protocol over the real links before
+        any gradient depends on them; a failure anywhere makes every rank fall back to RCCL."""
+        lib = _lib.kernels()
+        n = min(self.cap, 3 * 2048 + 17)  # several blocks and a partial tail block
+        try:
+            lib.rk_p2p_set_timeout(self._ctx, 5.0)
+            with torch.cuda.device(self.device):
+                i = torch.arange(n, device=self.device, dtype=torch.float32)
+                x = (i % 97) * (self.rank + 1)  # small integers: the fp32 sum is exact in any order
+                self.all_reduce_(x, 1.0)
+                torch.cuda.synchronize(self.device)
+                want = (i % 97) * (self.world * (self.world + 1) / 2)
+                ok = bool(torch.equal(x, want)) and not self._err.value
+        except Exception as e:  # pragma: no cover - depends on the platform
+            logger.warning(f"p2p self-test raised on rank {self.rank}: {e}")
+            ok = False
+        finally:
+            lib.rk_p2p_set_timeout(self._ctx, 30.0)
+        return ok
 
     def all_reduce_(self, flat: torch.Tensor, scale: float = 1.0) -> None:
         """``flat <- scale * sum_ranks(flat)`` in place on the current stream (graph-capturable)."""
@@ -89,17 +125,18 @@ class P2PAllReduce:
         _lib.check(_lib.kernels().rk_p2p_allreduce(self._ctx, flat.data_ptr(), flat.numel(), float(scale),
                                                    _lib.stream_ptr(flat.device)), "rk_p2p_allreduce")
         self.launches += 1
-        if self.launches % 256 == 0:
-            self.check()
+        self.check()  # a plain load of a host-mapped word: reports a timeout of any earlier launch
 
     def check(self) -> None:
-        """Raise if a launch ever timed out waiting for a peer (its results were invalid)."""
-        if self._ctx and _lib.kernels().rk_p2p_error(self._ctx):
+        """Raise if a launch ever timed out waiting for a peer (its timed-out blocks left their
+        gradients un-reduced).  Costs one host load: called on every launch and every replay."""
+        if self._ctx and self._err.value:
             raise RuntimeError("p2p all-reduce: a peer did not signal within the timeout (dead or desynchronised rank)")
 
     def close(self) -> None:
         """Unmap the peers and free the buffers (collective: every rank, when no launch is pending
         anywhere).  Not done implicitly: at interpreter exit the mappings are simply left."""
         if self._ctx:
+            self._err = ctypes.c_uint(0)  # the mapped word is freed with the context
             _lib.kernels().rk_p2p_destroy(self._ctx)
             self._ctx = 0

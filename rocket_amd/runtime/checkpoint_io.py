@@ -61,6 +61,38 @@ def _cpu_state_dict(model: torch.nn.Module) -> dict:
     return out
 
 
+def _tied_aliases(model: torch.nn.Module) -> dict:
+    """``{dropped key: kept key}`` for the tied entries :func:`_cpu_state_dict` leaves out."""
+    seen, alias = {}, {}
+    for k, v in model.state_dict().items():
+        if not isinstance(v, torch.Tensor) or not v.numel():
+            continue
+        key = (v.untyped_storage().data_ptr(), v.storage_offset(), tuple(v.shape))
+        if key in seen:
+            alias[k] = seen[key]
+        else:
+            seen[key] = k
+    return alias
+
+
+def load_model_strict(model: torch.nn.Module, sd: dict, where: str = "checkpoint") -> None:
+    """Load ``sd`` strictly (accelerate's ``load_state`` → safetensors ``load_model`` is strict too).
+
+    The only keys allowed to be missing are tied aliases whose storage IS another loaded key
+    (dropped at save time because safetensors refuses shared storage); every other missing or
+    unexpected key raises, naming them — a checkpoint of another architecture never loads silently.
+    """
+    alias = _tied_aliases(model)
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    missing = [k for k in missing if not (k in alias and alias[k] in sd)]
+    if missing or unexpected:
+        raise RuntimeError(
+            f"{where}: state dict does not match {type(model).__name__}: "
+            f"missing keys {sorted(missing)[:20]}{' ...' if len(missing) > 20 else ''}, "
+            f"unexpected keys {sorted(unexpected)[:20]}{' ...' if len(unexpected) > 20 else ''}"
+        )
+
+
 def _np_state_plain(st):
     # ('MT19937', uint32[624], pos, has_gauss, cached) with the key array as a tensor: weights_only-loadable
     return (st[0], torch.from_numpy(np.asarray(st[1], dtype=np.uint32).astype(np.int64)), int(st[2]), int(st[3]),
@@ -143,7 +175,7 @@ def load_state(engine, input_dir: str, load_custom: bool = True) -> None:
             sd = st_load(str(st), device="cpu")
         else:
             sd = _load(src / _suffixed("pytorch_model", "bin", i), map_location="cpu")
-        engine.unwrap_model(model).load_state_dict(sd, strict=False)
+        load_model_strict(engine.unwrap_model(model), sd, str(st if st.exists() else src))
     for i, opt in enumerate(engine._optimizers):
         opt.load_state_dict(_load(src / _suffixed("optimizer", "bin", i), map_location="cpu"))
     for i, sched in enumerate(engine._schedulers):

@@ -326,6 +326,20 @@ class ShardedLoader(_LoaderBase):
         return out
 
 
+def mark_ring(sets: List[tuple]) -> None:
+    """Flag a ring of persistent batch buffer sets (one tuple of tensors per slot).
+
+    Every buffer gets ``_rocket_persistent`` (a captured step reads it in place) and
+    ``_rocket_ring = (sets, slot, index)`` so the step executor can capture the graph
+    variants of ALL slots in one warm-up pass instead of one per slot as they come
+    round (:meth:`rocket_amd.runtime.graphs.StepGraphs.launch`).
+    """
+    for k, bufs in enumerate(sets):
+        for j, b in enumerate(bufs):
+            b._rocket_persistent = True
+            b._rocket_ring = (sets, k, j)
+
+
 class DeviceTensorDataset(torch.utils.data.Dataset):
     """A dataset of aligned tensors resident on one device (typically HBM).
 
@@ -420,9 +434,8 @@ class DeviceLoader(_LoaderBase):
             ring = []
             for _ in range(self.RING):
                 bufs = tuple(torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device) for t in tensors)
-                for b in bufs:
-                    b._rocket_persistent = True
                 ring.append((bufs, RowGather([t.contiguous() for t in tensors], bufs)))
+            mark_ring([bufs for bufs, _ in ring])
             self._rings[n] = ring
         k = self._ring_pos.get(n, 0)
         self._ring_pos[n] = (k + 1) % self.RING

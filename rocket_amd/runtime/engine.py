@@ -37,6 +37,7 @@ from torch import nn
 from rocket_amd.parallel.ddp import DataParallel, unwrap
 from rocket_amd.runtime import comm as _comm
 from rocket_amd.runtime import checkpoint_io
+from rocket_amd.runtime.amp import FusedGradScaler, make_scaler
 from rocket_amd.runtime.host_data import HostLoader, HostTensorDataset
 from rocket_amd.runtime.data import (
     DeviceLoader,
@@ -72,7 +73,21 @@ class EngineOptimizer:
     def __init__(self, optimizer: torch.optim.Optimizer, engine: "Engine"):
         self.optimizer = optimizer
         self.engine = engine
-        self.step_was_skipped = False
+        self._skipped = False
+        self._skip_lazy = False  # fp16 fused scaler: the flag lives on the device until asked for
+
+    @property
+    def step_was_skipped(self) -> bool:
+        """accelerate's ``step_was_skipped``.  With the device-resident scaler it is read back only
+        here (waiting for that step's update), not on every step."""
+        if self._skip_lazy:
+            self._skipped = self.engine.scaler.last_step_skipped()
+            self._skip_lazy = False
+        return self._skipped
+
+    @step_was_skipped.setter
+    def step_was_skipped(self, v: bool) -> None:
+        self._skipped, self._skip_lazy = bool(v), False
 
     @property
     def param_groups(self):
@@ -104,6 +119,10 @@ class EngineOptimizer:
         if not self.engine.sync_gradients:
             return None
         scaler = self.engine.scaler
+        if isinstance(scaler, FusedGradScaler):
+            out = scaler.step(self.optimizer, closure) if closure else scaler.step(self.optimizer)
+            self._skip_lazy = True
+            return out
         if scaler is not None:
             scale_before = scaler.get_scale()
             scaler.step(self.optimizer, closure) if closure else scaler.step(self.optimizer)
@@ -117,7 +136,7 @@ class EngineOptimizer:
         """True when the fused update kernel may clear the gradients itself (same result as zero_grad)."""
         opt = self.optimizer
         return (
-            self.engine.scaler is None
+            (self.engine.scaler is None or isinstance(self.engine.scaler, FusedGradScaler))
             and hasattr(opt, "launch")
             and all(getattr(p, "_rocket_direct_grad", False) for p in self._params() if p.requires_grad)
         )
@@ -127,6 +146,10 @@ class EngineOptimizer:
         if not self.engine.sync_gradients:
             return
         if self.fused_zero_ok():
+            if isinstance(self.engine.scaler, FusedGradScaler):
+                self.engine.scaler.step(self.optimizer, zero_grads=True)
+                self._skip_lazy = True
+                return
             self.step_was_skipped = False
             if self.optimizer.prepare():
                 self.optimizer.launch(zero_grads=True)
@@ -215,7 +238,7 @@ class Engine:
         self.step = 0
         self.scaler = None
         if self.mixed_precision == "fp16":
-            self.scaler = torch.amp.GradScaler(self.device.type)
+            self.scaler = make_scaler(self.device)
         self._models: List[nn.Module] = []
         self._wrapped: dict = {}
         self._grad_owners: list = []  # FlatGrads / DataParallel owning persistent .grad storage

@@ -44,7 +44,9 @@ not support (or ``ROCKET_LAUNCH_LIST=0``) is replayed with ``graph.replay()``.
 
 Inputs: tensors flagged ``_rocket_persistent`` (the device loader's ring
 buffers) are captured in place and get one graph per buffer set — no copy per
-step; any other input is copied into a static buffer before replay.
+step; the variants of every slot of a loader ring are captured together, on
+the first capture, so no capture lands in a later (timed) iteration.  Any
+other input is copied into a static buffer before replay.
 """
 
 from __future__ import annotations
@@ -255,15 +257,55 @@ class StepGraphs:
             self.mod._accelerator._do_sync()
             self._prepare(attrs)
             self._check_tokens()
-            self.variants[key] = self._capture(attrs, tens)
+            self._capture_all(sig, key, attrs, tens)
             return True
         self.mod._accelerator._do_sync()
         self._prepare(attrs)
         if self._check_tokens():  # tables re-allocated: every graph is stale, capture again
-            self.variants[key] = self._capture(attrs, tens)
+            self._capture_all(sig, key, attrs, tens)
             return True
         self._replay(v, attrs, tens)
         return True
+
+    @staticmethod
+    def _ring_peers(tens: List[torch.Tensor]) -> List[List[torch.Tensor]]:
+        """Input lists of the OTHER slots of the loader ring the persistent inputs come from.
+
+        A captured graph reads persistent loader buffers in place, so every ring slot is its own
+        variant.  Capturing them all when the first one is captured keeps every capture inside
+        the warm-up (one slot per iteration would put RING-1 captures into the first timed
+        iterations).  Empty when the inputs are not (all) from one ring slot."""
+        ring = slot = None
+        for t in tens:
+            tag = getattr(t, "_rocket_ring", None)
+            if tag is None:
+                if getattr(t, "_rocket_persistent", False):
+                    return []
+                continue
+            sets, k, j = tag
+            if ring is None:
+                ring, slot = sets, k
+            elif sets is not ring or k != slot or sets[k][j] is not t:
+                return []
+        if ring is None:
+            return []
+        out = []
+        for k in range(len(ring)):
+            if k == slot:
+                continue
+            alt = []
+            for t in tens:
+                tag = getattr(t, "_rocket_ring", None)
+                alt.append(ring[k][tag[2]] if tag is not None else t)
+            out.append(alt)
+        return out
+
+    def _capture_all(self, sig, key, attrs: Attributes, tens: List[torch.Tensor]) -> None:
+        for alt in self._ring_peers(tens):
+            akey = (sig, tuple(t.data_ptr() if getattr(t, "_rocket_persistent", False) else 0 for t in alt))
+            if akey not in self.variants and len(self.variants) < MAX_VARIANTS - 1:
+                self.variants[akey] = self._capture(attrs, alt, run=False)
+        self.variants[key] = self._capture(attrs, tens)
 
     def _prepare(self, attrs: Attributes) -> None:
         for prep in self._preps:
@@ -298,7 +340,8 @@ class StepGraphs:
             if fn is not None:
                 fn(attrs)
 
-    def _capture(self, attrs: Attributes, tens: List[torch.Tensor]) -> _Captured:
+    def _capture(self, attrs: Attributes, tens: List[torch.Tensor], run: bool = True) -> _Captured:
+        """Capture the micro-step for inputs ``tens``; ``run``: also replay it for this iteration."""
         engine = self.mod._accelerator
         v = _Captured()
         v.sync = engine.sync_gradients
@@ -343,6 +386,8 @@ class StepGraphs:
         self.captures += 1
         self.parts = max(self.parts, len(v.graphs))
         logger.info(f"captured HIP graph(s) for sync={v.sync} ({len(v.graphs)} part(s))")
+        if not run:
+            return v
         # the captured work has not run yet: replay it for this iteration
         self._run(v, rep if split else None)
         attrs.batch = v.out
@@ -369,8 +414,8 @@ class StepGraphs:
         rep = self._replica() if v.sync else None
         if rep is not None and rep.broadcast_buffers:
             rep.sync_buffers()
-        if rep is not None and self.replays % 1024 == 1023:
-            rep.check_comm()
+        if rep is not None:
+            rep.check_comm()  # P2P peer timeouts surface at the next step (one host load)
         self._run(v, rep if len(v.graphs) > 1 else None)
         attrs.batch = v.out
         self._host(attrs)

@@ -23,7 +23,7 @@ from typing import List
 import torch
 from torch.utils.data import BatchSampler
 
-from rocket_amd.runtime.data import EpochSampler, GradientState, ShardedBatchSampler, _LoaderBase
+from rocket_amd.runtime.data import EpochSampler, GradientState, ShardedBatchSampler, _LoaderBase, mark_ring
 
 
 class HostTensorDataset(torch.utils.data.Dataset):
@@ -124,9 +124,8 @@ class HostLoader(_LoaderBase):
             for _ in range(self.RING):
                 bufs = tuple(torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=self.device)
                              for t in self.dataset.tensors)
-                for b in bufs:
-                    b._rocket_persistent = True
                 ring.append(bufs)
+            mark_ring(ring)
             self._ring[n] = ring
         k = self._ring_pos.get(n, 0)
         self._ring_pos[n] = (k + 1) % self.RING

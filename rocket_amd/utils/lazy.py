@@ -21,7 +21,7 @@ import torch
 
 
 class LazyScalar(numbers.Real):
-    __slots__ = ("_t", "_v")
+    __slots__ = ("_t", "_v", "__weakref__")
 
     def __init__(self, value):
         if isinstance(value, torch.Tensor):
