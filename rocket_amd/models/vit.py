@@ -4,11 +4,12 @@ Pre-norm encoder, 12 layers × (MHSA 12 heads + MLP 3072), 224×224 input → 19
 patches + [CLS] = 197 tokens, width 768.
 
 MI355X path: LayerNorm is the one-wave-per-row HIP kernel emitting bf16 straight
-into the next GEMM (:class:`~rocket_amd.ops.norm.FusedLayerNorm`); the GEMMs run
-on the library path (hipBLASLt, bias fused into the epilogue via ``addmm``; the bias gradient is
-one column-sum launch, :class:`~rocket_amd.ops.linear.LibLinear`); attention is
-one fused MFMA kernel reading the packed QKV projection (``native/kernels/attn.hip``), GELU
-a HIP kernel; residual adds are fused into the following LayerNorm.  The residual stream stays
+into the next GEMM (:class:`~rocket_amd.ops.norm.FusedLayerNorm`); every projection runs on the
+native MFMA GEMM (``native/kernels/mgemm.hip`` via :class:`~rocket_amd.ops.mlinear.MLinear`:
+bias in the forward epilogue, K-major dgrad, split-K wgrad with the bias gradient from the same
+launch); the MLP is :class:`~rocket_amd.ops.mlinear.MMlp` (GELU in fc1's epilogue, gelu' in
+fc2's dgrad epilogue); attention is one fused MFMA kernel reading the packed QKV projection
+(``native/kernels/attn.hip``); residual adds are fused into the following LayerNorm.  The residual stream stays
 fp32 (standard AMP numerics); everything feeding a GEMM is bf16.
 
 Forward contract: ``(img, label) -> (img, label, logits)``.
@@ -20,8 +21,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from rocket_amd.ops.activation import attention_qkv, gelu
-from rocket_amd.ops.linear import LibLinear
+from rocket_amd.ops.activation import attention_qkv
+from rocket_amd.ops.mlinear import MLinear, MMlp
 from rocket_amd.ops.norm import FusedLayerNorm
 
 
@@ -29,22 +30,12 @@ class Attention(nn.Module):
     def __init__(self, dim: int, heads: int):
         super().__init__()
         self.heads = heads
-        self.qkv = LibLinear(dim, 3 * dim)
-        self.proj = LibLinear(dim, dim)
+        self.qkv = MLinear(dim, 3 * dim)
+        self.proj = MLinear(dim, dim)
 
     def forward(self, x):
         # fused MFMA attention straight from the packed projection (no head permutes)
         return self.proj(attention_qkv(self.qkv(x), self.heads))
-
-
-class Mlp(nn.Module):
-    def __init__(self, dim: int, hidden: int):
-        super().__init__()
-        self.fc1 = LibLinear(dim, hidden)
-        self.fc2 = LibLinear(hidden, dim)
-
-    def forward(self, x):
-        return self.fc2(gelu(self.fc1(x)))
 
 
 class Block(nn.Module):
@@ -53,7 +44,7 @@ class Block(nn.Module):
         self.norm1 = FusedLayerNorm(dim, eps=1e-6)
         self.attn = Attention(dim, heads)
         self.norm2 = FusedLayerNorm(dim, eps=1e-6)
-        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+        self.mlp = MMlp(dim, int(dim * mlp_ratio))
 
     def forward(self, x, pending=None):
         """x: fp32 residual stream; pending: the previous sub-layer's output, not yet added.

@@ -1,0 +1,652 @@
+// Large bf16 MFMA GEMM for the transformer projections (ViT-B/16 qkv, proj, fc1,
+// fc2 in all three directions) and, through the same core, anything else shaped like them.
+//
+//   C[M,N] (op)= epi( sum_k A(m,k) * B(n,k) )           bf16 operands, f32 accumulation
+//
+// Operand layouts (per operand, template flag):
+//   row   ("K-contiguous")  A(m,k) = a[m*lda + k]   e.g. activations X[M,K], nn.Linear W[N,K]
+//   kmaj  ("K-major")       A(m,k) = a[k*lda + m]   e.g. W read as [K_out][K_in] for the dgrad,
+//                                                     dY / X read token-major for the wgrad
+// so forward (row,row), dgrad (row,kmaj) and wgrad (kmaj,kmaj) all run without a transpose pass.
+//
+// Design for gfx950 (cdna guide §5):
+// * 512 threads = 8 waves as 2 (M) x 4 (N); block tile BM x BN x 64 (256x256, 256x128, 128x128);
+//   each wave owns (BM/2) x (BN/4) as 16x16 fragments of v_mfma_f32_16x16x32_bf16.
+// * Global -> LDS by global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip, 1 KiB per wave
+//   instruction), double-buffered: the DMA of k-tile t+1 is in flight while tile t is consumed;
+//   one barrier per k-tile.
+// * LDS images are lane-linear (the DMA writes base + 16*lane), so the bank-conflict swizzles
+//   are applied to the per-lane SOURCE address and undone on the read (guide rule 21):
+//     row image  [rows][64 k] (128-B rows):  16-B slot ^= (row >> 1) & 7
+//                -> every 16-lane ds_read_b128 group covers all 16 slots of a bank row;
+//     kmaj image [64 k][R cols] (2R-B rows): 16-B slot ^= ((k & 3) | ((k >> 1) & 4)) << 1
+//                -> the two ds_read_b64_tr_b16 (hardware transpose) reads of a fragment hit
+//                   16 distinct slots per 32-lane half.
+// * MFMA operands swapped (B fragment as the A operand) so every lane holds 4 CONSECUTIVE output
+//   columns: 8-byte bf16 / 16-byte f32 epilogue stores.
+// * Epilogue: + bias[n]; GELU (optionally also storing the pre-activation for the backward) or
+//   ReLU; or multiply by gelu'(aux[m][n]) / relu'(aux) (the dgrad of an activation fused into the
+//   GEMM that produces its input gradient); f32 or bf16 out; C += (persistent f32 grads);
+//   split-K over blocks with f32 atomics (weight gradients: few output tiles, long K).
+// * Optional row sums of A (bias gradient of a wgrad: db[m] = sum_k dY(m,k)) from extra MFMAs
+//   against a ones fragment, spread over the 4 N-waves of the blocks in tile column 0.
+// * Block ids remapped XCD-aware (consecutive tiles sharing an A panel share an L2).
+#include "rk_common.h"
+
+#include <algorithm>
+
+using namespace rk;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+enum Epi : int { kNone = 0, kRelu = 1, kGelu = 2, kMulGeluGrad = 3, kMulReluGrad = 4 };
+
+struct MArgs {
+  const uint16_t* a;
+  const uint16_t* b;
+  void* c;
+  void* c_pre;           // kGelu: pre-activation out (bf16/f32 like C), optional
+  const float* bias;     // [N] or null
+  const uint16_t* aux;   // kMulGeluGrad / kMulReluGrad: bf16 [M][ldc]
+  float* rowsum;         // [M] f32 += row sums of A, or null
+  float* slab;           // split-K partial tiles [splitk][M][N] f32 (reduced by mgemm_reduce), or null
+  int64_t lda, ldb, ldc;
+  int M, N, K;
+  int c_dt;
+  int epi;
+  int accumulate;
+  int splitk, k_per_split;
+};
+
+// erf for the GELU epilogues: Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16
+// output's 2^-9), one reciprocal + one exp + 5 FMAs instead of the ~20-instruction libm erff;
+// e^{-u^2} is shared with gelu'.  Returns erf(u) given e = exp(-u*u).
+__device__ __forceinline__ float erf_as(float u, float e) {
+  const float a = fabsf(u);
+  const float t = __frcp_rn(__builtin_fmaf(0.3275911f, a, 1.f));
+  float p = __builtin_fmaf(1.061405429f, t, -1.453152027f);
+  p = __builtin_fmaf(p, t, 1.421413741f);
+  p = __builtin_fmaf(p, t, -0.284496736f);
+  p = __builtin_fmaf(p, t, 0.254829592f);
+  const float r = __builtin_fmaf(-p * t, e, 1.f);
+  return copysignf(r, u);
+}
+__device__ __forceinline__ float gelu_f(float x) {
+  const float u = x * 0.7071067811865476f;
+  return 0.5f * x * (1.f + erf_as(u, __expf(-u * u)));
+}
+__device__ __forceinline__ float gelu_grad(float z) {
+  const float u = z * 0.7071067811865476f;
+  const float e = __expf(-u * u);  // = exp(-z^2/2): the Gaussian term of gelu' too
+  return 0.5f * (1.f + erf_as(u, e)) + z * 0.3989422804014327f * e;
+}
+
+// kmaj image slot swizzle (see header)
+__device__ __forceinline__ int kswz(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
+// row image slot swizzle: BK = 64 (128-B rows, 8 slots) / BK = 32 (64-B rows, 4 slots)
+template <int BK>
+__device__ __forceinline__ int rswz(int r) {
+  if constexpr (BK == 64) return (r >> 1) & 7;
+  else return (0x78 >> (2 * ((r >> 2) & 3))) & 3;  // [0, 2, 3, 1][(r >> 2) & 3]
+}
+
+// LDS-DMA of one operand's k-tile: R rows x BK (row image) or BK rows x R (kmaj image);
+// R*BK*2 bytes = NI wave instructions of 1 KiB per wave.  Every per-lane source offset is computed
+// once: per k-tile only the wave-uniform base moves (SGPR base + VGPR offset addressing).
+template <int R, int BK, bool KMAJ, int NW>
+struct Stager {
+  static constexpr int NI = R * BK / (512 * NW);
+  static_assert(NI >= 1 && R * BK % (512 * NW) == 0, "tile too small for the wave count");
+  uint32_t off[NI];  // byte offsets from the k-tile base
+  __device__ __forceinline__ void init(int64_t ld, int r0, int rdim, int wid, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = (wid * NI + i) * 64 + lane;  // 16-byte chunk index in the lane-linear image
+      if constexpr (!KMAJ) {
+        constexpr int CPR = BK / 8;
+        const int r = q / CPR, c = q % CPR;
+        const int chunk = c ^ rswz<BK>(r);
+        const int gr = min(r0 + r, rdim - 1);  // rows past the edge: any valid row (never stored)
+        off[i] = (uint32_t)(((int64_t)gr * ld + chunk * 8) * 2);
+      } else {
+        constexpr int CPR = R / 8;  // chunks per k-row
+        const int k = q / CPR, c = q % CPR;
+        const int chunk = c ^ kswz(k);
+        const int gc = min(r0 + chunk * 8, rdim - 8);
+        off[i] = (uint32_t)(((int64_t)k * ld + gc) * 2);
+      }
+    }
+  }
+  // base: wave-uniform address of element (row 0, k0) [row] / (k0, col 0) [kmaj]
+  __device__ __forceinline__ void issue(const char* base, char* lds, int wid) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(base + off[i]), (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0,
+                                       0);
+  }
+  // the partial last k-tile (kvalid < BK valid k): chunks past K are DMA'd from a zero page, so
+  // the MFMAs over the whole tile add exact zeros
+  __device__ __forceinline__ void issue_tail(const char* base, char* lds, int wid, int lane, int kvalid,
+                                             const char* zero) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = (wid * NI + i) * 64 + lane;
+      int kpos;
+      if constexpr (!KMAJ) {
+        constexpr int CPR = BK / 8;
+        kpos = ((q % CPR) ^ rswz<BK>(q / CPR)) * 8;
+      } else {
+        kpos = q / (R / 8);
+      }
+      const char* src = kpos < kvalid ? base + off[i] : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0, 0);
+    }
+  }
+};
+
+__device__ __attribute__((aligned(16))) uint4 g_mgemm_zero[1];  // 16 zero bytes (static storage)
+
+// Fragment reads (16 rows x 32 k, MFMA 16x16x32 operand map) of the NF fragments a wave owns,
+// rows rbase + 16*f.  Per-lane offsets are precomputed; k-step and fragment terms are immediates.
+//   row image: one ds_read_b128 per fragment; the slot swizzle depends only on (lane & 15), so
+//              fragment f is at +f*16 rows; one offset per k-step (the XOR flips slot bit 2).
+//   kmaj image: two ds_read_b64_tr_b16 (k rows 8g+q and 8g+4+q); kswz(k) reduces to a per-lane
+//              constant S (k & 3 = q, bit 3 of k = g & 1), so only the chunk term depends on f.
+template <int R, int BK, bool KMAJ, int NF>
+struct FragReader {
+  static constexpr int KK = BK / 32;
+  uint32_t off[KMAJ ? NF : KK];
+  __device__ __forceinline__ void init(int rbase, int lane) {
+    if constexpr (!KMAJ) {
+      const int row = rbase + (lane & 15);
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) off[kk] = row * (BK * 2) + (((kk * 4 + (lane >> 4)) ^ rswz<BK>(row)) << 4);
+    } else {
+      const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+      const int S = kswz(8 * g + q);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int chunk = (rbase >> 3) + 2 * f + (p >> 1);
+        off[f] = (8 * g + q) * (2 * R) + ((chunk ^ S) << 4) + ((p & 1) << 3);
+      }
+    }
+  }
+  __device__ __forceinline__ bf16x8 get(const char* img, int f, int kk) const {
+    if constexpr (!KMAJ) {
+      return *(const bf16x8*)(img + off[kk] + f * 16 * (BK * 2));
+    } else {
+      const char* p0 = img + off[f] + kk * 32 * (2 * R);
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * (2 * R)));
+      typedef __attribute__((ext_vector_type(8))) short s16x8;
+      const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
+};
+
+// s_waitcnt vmcnt(n) for a run-time n (the field is an immediate)
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// Epilogue of one wave's FM x FN fragments: lane holds C[m][n..n+3], m = mbase + 16 i + (lane & 15),
+// n = nbase + 16 j + 4 (lane >> 4).  PRE: the side inputs (aux / old bf16 C) were loaded before the
+// main loop into `side`; otherwise they are loaded here.
+template <int FM, int FN, bool PRE>
+__device__ __forceinline__ void store_tile(const MArgs& g, f32x4 (&acc)[FM][FN], const uint2 (&side)[FM][FN],
+                                           int mbase, int nbase, int lane, int split) {
+  if (g.splitk > 1) {  // partial tile -> this split's slab (plain stores; mgemm_reduce combines)
+    float* slab = g.slab + (int64_t)split * g.M * g.N;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nbase + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = mbase + i * 16 + (lane & 15);
+        if (m < g.M) *(float4*)(slab + (int64_t)m * g.N + n) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
+  }
+  // all side inputs were loaded before the main loop (aux / old C); compute, then store
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = nbase + j * 16 + 4 * (lane >> 4);
+    const bool nok = n < g.N;  // N % 4 == 0 (host-checked): a lane's 4 columns are all in or all out
+    float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g.bias && nok) bias = *(const float4*)(g.bias + n);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = mbase + i * 16 + (lane & 15);
+      if (!nok || m >= g.M) continue;
+      const int64_t off = (int64_t)m * g.ldc + n;
+      float v[4] = {acc[i][j][0] + bias.x, acc[i][j][1] + bias.y, acc[i][j][2] + bias.z, acc[i][j][3] + bias.w};
+      if (g.epi == kGelu || g.epi == kRelu) {
+        if (g.c_pre) {
+          if (g.c_dt == BF16)
+            *(uint2*)((uint16_t*)g.c_pre + off) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                                             (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+          else
+            *(float4*)((float*)g.c_pre + off) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = g.epi == kGelu ? gelu_f(v[e]) : fmaxf(v[e], 0.f);
+      } else if (g.epi == kMulGeluGrad || g.epi == kMulReluGrad) {
+        const uint2 z = PRE ? side[i][j] : *(const uint2*)(g.aux + off);
+        const float zz[4] = {__uint_as_float(z.x << 16), __uint_as_float(z.x & 0xffff0000u), __uint_as_float(z.y << 16),
+                             __uint_as_float(z.y & 0xffff0000u)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = g.epi == kMulGeluGrad ? v[e] * gelu_grad(zz[e]) : (zz[e] > 0.f ? v[e] : 0.f);
+      }
+      if (g.c_dt == BF16) {
+        uint16_t* c = (uint16_t*)g.c + off;
+        if (g.accumulate) {
+          const uint2 o = PRE ? side[i][j] : *(const uint2*)c;
+          v[0] += __uint_as_float(o.x << 16);
+          v[1] += __uint_as_float(o.x & 0xffff0000u);
+          v[2] += __uint_as_float(o.y << 16);
+          v[3] += __uint_as_float(o.y & 0xffff0000u);
+        }
+        *(uint2*)c = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+      } else {
+        float* c = (float*)g.c + off;
+        if (g.accumulate) {
+          const float4 o = *(const float4*)c;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int BK, int NS, int WM, int WN, int OCC, bool AK, bool BKM>
+__global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) mgemm_kernel(MArgs g) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;  // per-wave tile
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int KK = BK / 32;                // MFMA k-steps per k-tile
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int NL = (BM + BN) * BK / (512 * NW);  // LDS-DMA instructions per wave per k-tile
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE_BYTES];
+
+  const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lin / ntiles;
+  const int tile = lin % ntiles;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int kb = split * g.k_per_split;
+  const int ke = min(g.K, kb + g.k_per_split);
+  const int nt = (ke - kb + BK - 1) / BK;  // the last k-tile may be partial (K % BK != 0)
+  const int klast = (ke - kb) - (nt - 1) * BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // bias-gradient row sums: tile column 0 only; wave wn sums A fragments i = wn, wn+WN, ...
+  const bool want_rows = g.rowsum != nullptr && tn == 0;
+  constexpr int FR = (FM + WN - 1) / WN;
+  f32x4 racc[FR];
+#pragma unroll
+  for (int i = 0; i < FR; ++i) racc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+  Stager<BM, BK, AK, NW> sa;
+  Stager<BN, BK, BKM, NW> sb;
+  sa.init(g.lda, row0, g.M, wid, lane);
+  sb.init(g.ldb, col0, g.N, wid, lane);
+  // byte step of one k-tile: row image BK elements along the row, kmaj image BK rows
+  const int64_t a_step = AK ? (int64_t)BK * g.lda * 2 : BK * 2;
+  const int64_t b_step = BKM ? (int64_t)BK * g.ldb * 2 : BK * 2;
+  const char* a_k0 = (const char*)g.a + (AK ? (int64_t)kb * g.lda * 2 : (int64_t)kb * 2);
+  const char* b_k0 = (const char*)g.b + (BKM ? (int64_t)kb * g.ldb * 2 : (int64_t)kb * 2);
+  auto issue = [&](int t) {
+    char* buf = smem + (t % NS) * STAGE_BYTES;
+    if (t + 1 < nt || klast == BK) {
+      sa.issue(a_k0 + t * a_step, buf, wid);
+      sb.issue(b_k0 + t * b_step, buf + A_BYTES, wid);
+    } else {
+      const char* zero = (const char*)g_mgemm_zero;
+      sa.issue_tail(a_k0 + t * a_step, buf, wid, lane, klast, zero);
+      sb.issue_tail(b_k0 + t * b_step, buf + A_BYTES, wid, lane, klast, zero);
+    }
+  };
+  FragReader<BM, BK, AK, FM> ra;
+  FragReader<BN, BK, BKM, FN> rb;
+  ra.init(wm * TM, lane);
+  rb.init(wn * TN, lane);
+  // side inputs of the epilogue (gelu'/relu' operand, or the old bf16 C of an accumulate), loaded
+  // now so their latency hides under the main loop instead of serialising the epilogue
+  uint2 side[FM][FN];
+  {
+    const uint16_t* src = (g.epi == kMulGeluGrad || g.epi == kMulReluGrad) ? g.aux
+                          : (g.accumulate && g.c_dt == BF16 && g.splitk == 1) ? (const uint16_t*)g.c : nullptr;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int m = min(row0 + wm * TM + i * 16 + (lane & 15), g.M - 1);
+        const int n = min(col0 + wn * TN + j * 16 + 4 * (lane >> 4), g.N - 4);
+        side[i][j] = src ? *(const uint2*)(src + (int64_t)m * g.ldc + n) : make_uint2(0u, 0u);
+      }
+  }
+
+  // prologue: NS-1 k-tiles in flight
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nt) issue(t);
+
+  for (int t = 0; t < nt; ++t) {
+    // tile t has landed once at most the tiles issued after it (up to t+NS-2) are outstanding
+    wait_vm((min(nt - 1, t + NS - 2) - t) * NL);
+    // every wave's share of tile t is in LDS, and every wave has consumed tile t-1 (its
+    // fragments fed MFMAs before the wave got here): refill tile t-1's slot with tile t+NS-1
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + NS - 1 < nt) issue(t + NS - 1);
+    const char* As = smem + (t % NS) * STAGE_BYTES;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = rb.get(Bs, j, kk);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = ra.get(As, i, kk);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      if (want_rows) {  // static fragment index, wave-uniform condition (no runtime-indexed arrays)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          if (i % WN == wn) racc[i / WN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], racc[i / WN], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: lane holds C[m][n..n+3], m = .. + (lane & 15), n = .. + 4 * (lane >> 4) ----
+  if (want_rows && lane < 16) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = row0 + wm * TM + i * 16 + lane;
+      if (i % WN == wn && m < g.M) atomicAdd(g.rowsum + m, racc[i / WN][0]);
+    }
+  }
+  store_tile<FM, FN, true>(g, acc, side, row0 + wm * TM, col0 + wn * TN, lane, split);
+}
+
+// Large-tile kernel (one block per CU, 8 waves): BM x BN x 64 k-tiles in a 2-slot LDS ring, the
+// k-tile consumed in 4 phases (k-half x M-half of the wave's fragments).  Each phase issues the
+// LDS reads of the NEXT phase's operands, then its 8..16 MFMAs, so fragment reads run under the
+// matrix cores instead of in front of them (operands in 4 named register sets: B of the current /
+// next k-half, A of the current / next phase).  One barrier per k-tile, in its last phase: wait for
+// tile t+1's DMA, then refill tile t's slot with tile t+2 and read tile t+1's first operands.
+// Per-wave tile (BM/WM) x (BN/WN): with 128 x 64 the LDS reads per MFMA are half those of the
+// 64 x 32 wave tile of the 2-blocks-per-CU kernel, whose LDS port the MFMAs otherwise wait on.
+template <int BM, int BN, int WM, int WN, bool AK, bool BKM>
+__global__ void __launch_bounds__(64 * WM * WN, WM * WN / 4) mgemm_phase_kernel(MArgs g) {
+  constexpr int BK = 64, NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16, FH = FM / 2;
+  static_assert(FM % 2 == 0, "phases split the wave's A fragments in halves");
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+
+  const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin / tiles_n, tn = lin % tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int nt = (g.K + BK - 1) / BK;
+  const int klast = g.K - (nt - 1) * BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stager<BM, BK, AK, NW> sa;
+  Stager<BN, BK, BKM, NW> sb;
+  sa.init(g.lda, row0, g.M, wid, lane);
+  sb.init(g.ldb, col0, g.N, wid, lane);
+  constexpr int NL = (BM + BN) * BK / (512 * NW);
+  const int64_t a_step = AK ? (int64_t)BK * g.lda * 2 : BK * 2;
+  const int64_t b_step = BKM ? (int64_t)BK * g.ldb * 2 : BK * 2;
+  auto issue = [&](int t) {
+    char* buf = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nt || klast == BK) {
+      sa.issue((const char*)g.a + t * a_step, buf, wid);
+      sb.issue((const char*)g.b + t * b_step, buf + A_BYTES, wid);
+    } else {
+      const char* zero = (const char*)g_mgemm_zero;
+      sa.issue_tail((const char*)g.a + t * a_step, buf, wid, lane, klast, zero);
+      sb.issue_tail((const char*)g.b + t * b_step, buf + A_BYTES, wid, lane, klast, zero);
+    }
+  };
+  FragReader<BM, BK, AK, FM> ra;
+  FragReader<BN, BK, BKM, FN> rb;
+  ra.init(wm * TM, lane);
+  rb.init(wn * TN, lane);
+
+  bf16x8 Ba[FN], Bb[FN], Aa[FH], Ab[FH];
+  auto readB = [&](bf16x8 (&dst)[FN], int t, int kk) {
+    const char* Bs = smem + (t & 1) * STAGE_BYTES + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) dst[j] = rb.get(Bs, j, kk);
+  };
+  auto readA = [&](bf16x8 (&dst)[FH], int t, int kk, int mh) {
+    const char* As = smem + (t & 1) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < FH; ++i) dst[i] = ra.get(As, mh * FH + i, kk);
+  };
+  // MFMAs of fragments i in [i0, i1) of an M-half; sched_barrier keeps the LDS reads placed between
+  // two such groups where they are written: after the first MFMAs (whose operands arrived during
+  // the previous phase, so hipcc's lgkmcnt wait in front of them costs nothing) and before the rest
+  auto mma = [&](const bf16x8 (&B)[FN], const bf16x8 (&A)[FH], int mh, int i0, int i1) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < FH; ++i)
+      if (i >= i0 && i < i1)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[mh * FH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B[j], A[i], acc[mh * FH + i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  constexpr int I0 = 1;  // MFMA rows issued ahead of each phase's prefetch
+
+  issue(0);
+  if (nt > 1) issue(1);
+  if (nt > 1) wait_vm(NL); else wait_vm(0);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  readB(Ba, 0, 0);
+  readA(Aa, 0, 0, 0);
+
+  for (int t = 0; t < nt; ++t) {
+    // phase 1: (k-half 0, M-half 0); prefetch A(0, 1)
+    mma(Ba, Aa, 0, 0, I0);
+    readA(Ab, t, 0, 1);
+    mma(Ba, Aa, 0, I0, FH);
+    // phase 2: (0, 1); prefetch B(1), A(1, 0)
+    mma(Ba, Ab, 1, 0, I0);
+    readB(Bb, t, 1);
+    readA(Aa, t, 1, 0);
+    mma(Ba, Ab, 1, I0, FH);
+    // phase 3: (1, 0); prefetch A(1, 1)
+    mma(Bb, Aa, 0, 0, I0);
+    readA(Ab, t, 1, 1);
+    mma(Bb, Aa, 0, I0, FH);
+    // phase 4: (1, 1); cross into tile t+1
+    mma(Bb, Ab, 1, 0, I0);
+    if (t + 1 < nt) {
+      wait_vm(0);  // this wave's share of tile t+1 (nothing younger is in flight)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of tile t are done
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + 2 < nt) issue(t + 2);  // into tile t's slot
+      readB(Ba, t + 1, 0);
+      readA(Aa, t + 1, 0, 0);
+    }
+    mma(Bb, Ab, 1, I0, FH);
+  }
+
+  const uint2 nos[FM][FN] = {};
+  store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, 0);
+}
+
+// C[m][n] (+)= sum_s slab[s][m][n] + bias[n]  (f32 or bf16 C; N % 4 == 0)
+__global__ void __launch_bounds__(256) mgemm_reduce(const float* __restrict__ slab, int splitk, int M, int N,
+                                                    const float* __restrict__ bias, void* c, int c_dt, int64_t ldc,
+                                                    int accumulate) {
+  const int64_t nq = (int64_t)M * N / 4;
+  const int64_t plane = (int64_t)M * N;
+  for (int64_t q = blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+    const int64_t e = q * 4;
+    const int m = (int)(e / N), n = (int)(e % N);
+    float4 v = *(const float4*)(slab + e);
+    for (int s = 1; s < splitk; ++s) {
+      const float4 w = *(const float4*)(slab + s * plane + e);
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    if (bias) {
+      const float4 b = *(const float4*)(bias + n);
+      v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+    }
+    const int64_t off = (int64_t)m * ldc + n;
+    if (c_dt == BF16) {
+      uint16_t* o = (uint16_t*)c + off;
+      if (accumulate) {
+        const uint2 p = *(const uint2*)o;
+        v.x += __uint_as_float(p.x << 16); v.y += __uint_as_float(p.x & 0xffff0000u);
+        v.z += __uint_as_float(p.y << 16); v.w += __uint_as_float(p.y & 0xffff0000u);
+      }
+      *(uint2*)o = make_uint2((uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
+                              (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+    } else {
+      float* o = (float*)c + off;
+      if (accumulate) {
+        const float4 p = *(const float4*)o;
+        v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+      }
+      *(float4*)o = v;
+    }
+  }
+}
+
+template <int BM, int BN, int BK, int NS, int WM, int WN, int OCC>
+int launch_tile(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  const dim3 grid(tiles * g.splitk), block(64 * WM * WN);
+  if (!a_kmaj && !b_kmaj) mgemm_kernel<BM, BN, BK, NS, WM, WN, OCC, false, false><<<grid, block, 0, s>>>(g);
+  else if (!a_kmaj && b_kmaj) mgemm_kernel<BM, BN, BK, NS, WM, WN, OCC, false, true><<<grid, block, 0, s>>>(g);
+  else if (a_kmaj && b_kmaj) mgemm_kernel<BM, BN, BK, NS, WM, WN, OCC, true, true><<<grid, block, 0, s>>>(g);
+  else return (int)hipErrorInvalidValue;  // (kmaj, row) has no user
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_phase(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  const dim3 grid(tiles), block(64 * WM * WN);
+  if (!a_kmaj && !b_kmaj) mgemm_phase_kernel<BM, BN, WM, WN, false, false><<<grid, block, 0, s>>>(g);
+  else if (!a_kmaj && b_kmaj) mgemm_phase_kernel<BM, BN, WM, WN, false, true><<<grid, block, 0, s>>>(g);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// k-tile depth of each tile config (the K granularity a caller must respect)
+constexpr int kTileBK[] = {32, 64, 64, 64, 64, 32};
+
+}  // namespace
+
+// Tile configs (BM x BN x BK, LDS ring depth, waves, resident blocks per CU):
+//   0: 128x128x64 ring 2, 2x4 waves, 2/CU (64 KiB)    4: 128x128x64 ring 2, 2x2 waves, 2/CU (64 KiB)
+//   5: 128x128x32 ring 4, 2x4 waves, 2/CU (64 KiB)
+//   6: 256x256x64 phase-pipelined, 2x4 waves, 1/CU (128 KiB)   7: 256x128x64 phase, 4x2 waves (96 KiB)
+//      (row x row and row x kmaj only; no split-K / row sums)
+// (256x256, 256x128 and 128x256 tiles with 1-2 blocks per CU and 2-4 deep rings measured slower
+// at every ViT shape on this loop structure: bench/mgemm_probe.py, profiles/r2_mgemm_probe.md)
+// Requirements (hipErrorInvalidValue otherwise; the caller falls back): K % 8 == 0 (unless both
+// operands are kmaj), N % 8 == 0,
+// 16-byte aligned operands / leading dimensions, a kmaj operand's extent % 8 == 0.  splitk > 1
+// needs `slab` = splitk*M*N f32 scratch: the partial tiles are summed (+bias, +C) by a second launch.
+RK_API int rk_mgemm(const void* a, int64_t lda, int a_kmaj, const void* b, int64_t ldb, int b_kmaj, void* c, int c_dt,
+                    int64_t ldc, void* c_pre, const float* bias, const void* aux, int epi, int accumulate,
+                    float* rowsum, int M, int N, int K, int splitk, int tile, float* slab, hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (tile != 0 && tile != 4 && tile != 5 && tile != 6 && tile != 7) return (int)hipErrorInvalidValue;
+  if (tile >= 6 && (splitk > 1 || rowsum != nullptr || (a_kmaj && b_kmaj))) return (int)hipErrorInvalidValue;
+  // a row-layout operand moves K in 16-byte chunks (K % 8); a kmaj one in whole k-rows (any K)
+  if (K <= 0 || ((!a_kmaj || !b_kmaj) && K % 8) || N % 8 || (a_kmaj && M % 8) || ldc % 4) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)a | (uintptr_t)b) % 16 || (lda * 2) % 16 || (ldb * 2) % 16) return (int)hipErrorInvalidValue;
+  if ((epi == kMulGeluGrad || epi == kMulReluGrad) && aux == nullptr) return (int)hipErrorInvalidValue;
+  MArgs g;
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c; g.c_pre = c_pre; g.bias = bias;
+  g.aux = (const uint16_t*)aux; g.rowsum = rowsum; g.slab = slab;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K; g.c_dt = c_dt; g.epi = epi; g.accumulate = accumulate;
+  if (splitk < 1) splitk = 1;
+  const int kq = 64;  // split boundaries on 64 (a multiple of every config's BK)
+  int kps = ((K + kq - 1) / kq + splitk - 1) / splitk * kq;
+  splitk = (K + kps - 1) / kps;
+  if (splitk > 1 && (slab == nullptr || epi != kNone || c_pre)) return (int)hipErrorInvalidValue;
+  g.splitk = splitk;
+  g.k_per_split = kps;
+  int rc;
+  switch (tile) {
+    case 0: rc = launch_tile<128, 128, 64, 2, 2, 4, 2>(g, a_kmaj, b_kmaj, s); break;
+    case 4: rc = launch_tile<128, 128, 64, 2, 2, 2, 2>(g, a_kmaj, b_kmaj, s); break;
+    case 6: rc = launch_phase<256, 256, 2, 4>(g, a_kmaj, b_kmaj, s); break;
+    case 7: rc = launch_phase<256, 128, 4, 2>(g, a_kmaj, b_kmaj, s); break;
+    default: rc = launch_tile<128, 128, 32, 4, 2, 4, 2>(g, a_kmaj, b_kmaj, s); break;
+  }
+  if (rc || splitk == 1) return rc;
+  const int64_t nq = (int64_t)M * N / 4;
+  const int blocks = (int)std::min<int64_t>((nq + 255) / 256, 4096);
+  mgemm_reduce<<<blocks, 256, 0, s>>>(slab, splitk, M, N, bias, c, c_dt, ldc, accumulate);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,183 @@
+"""Numerics of the native MFMA GEMM (rk_mgemm) and the ViT linear/MLP built on it, against
+plain PyTorch fp32 references of the same ops (bf16-rounded operands, fp32 math)."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+TILES = [0, 4, 5]
+
+
+def _r(*s, scale=1.0):
+    return ((torch.rand(*s, device="cuda") * 2 - 1) * scale).to(torch.bfloat16)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("layout", ["fwd", "dgrad", "wgrad"])
+@pytest.mark.parametrize("M,N,K", [(25216, 768, 768), (300, 136, 200), (1000, 2304, 64), (792, 264, 88)])
+def test_mgemm_layouts(tile, layout, M, N, K):
+    """C = A.B^T for the three operand layouts, including M/N edges that are not tile multiples
+    (asymmetric random operands: a transposed C-write cannot pass)."""
+    from rocket_amd.ops.mgemm import mgemm
+
+    torch.manual_seed(tile)
+    if layout == "fwd":  # A [M,K] row, B [N,K] row
+        a, b = _r(M, K), _r(N, K)
+        ref = a.float() @ b.float().t()
+        kw = dict(lda=K, ldb=K)
+    elif layout == "dgrad":  # A [M,K] row, B stored [K,N] (kmaj)
+        a, b = _r(M, K), _r(K, N)
+        ref = a.float() @ b.float()
+        kw = dict(lda=K, ldb=N, b_kmaj=True)
+    else:  # A stored [K,M], B stored [K,N]
+        if M % 8:
+            pytest.skip("kmaj A needs M % 8 == 0")
+        a, b = _r(K, M), _r(K, N)
+        ref = a.float().t() @ b.float()
+        kw = dict(lda=M, ldb=N, a_kmaj=True, b_kmaj=True)
+    c = torch.empty(M, N, dtype=torch.float32, device="cuda")
+    mgemm(a, b, c, M=M, N=N, K=K, ldc=N, tile=tile, **kw)
+    assert _rel(c, ref) < 1e-5, _rel(c, ref)
+
+
+@pytest.mark.parametrize("tile", [0, 4])
+def test_mgemm_epilogues(tile):
+    from rocket_amd.ops.mgemm import mgemm
+
+    torch.manual_seed(1)
+    M, N, K = 777, 512, 256
+    a, b = _r(M, K), _r(N, K, scale=0.2)
+    bias = torch.randn(N, device="cuda")
+    z = a.float() @ b.float().t() + bias
+    # bias + GELU, pre-activation side output, bf16
+    c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    pre = torch.empty_like(c)
+    mgemm(a, b, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, epi="gelu", c_pre=pre, tile=tile)
+    assert _rel(pre, z) < 5e-3 and _rel(c, F.gelu(z)) < 5e-3
+    # relu
+    mgemm(a, b, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, epi="relu", tile=tile)
+    assert _rel(c, F.relu(z)) < 5e-3
+    # multiply by gelu'(aux): the GELU backward fused into a dgrad
+    aux = _r(M, N, scale=3.0)
+    zz = aux.float().requires_grad_()
+    F.gelu(zz).backward(torch.ones_like(zz))
+    mgemm(a, b, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, epi="mul_gelu_grad", aux=aux, tile=tile)
+    assert _rel(c, (a.float() @ b.float().t()) * zz.grad) < 5e-3
+    # accumulate into f32
+    c32 = torch.randn(M, N, device="cuda")
+    want = c32 + a.float() @ b.float().t()
+    mgemm(a, b, c32, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, accumulate=True, tile=tile)
+    assert _rel(c32, want) < 1e-5
+
+
+@pytest.mark.parametrize("split", [1, 3, 7])
+def test_mgemm_splitk_rowsum(split):
+    """wgrad shape: split-K slabs + combine (accumulating into an existing grad) and the fused
+    bias gradient (row sums of the K-major A operand)."""
+    from rocket_amd.ops.mgemm import mgemm
+
+    torch.manual_seed(2)
+    T, N, K = 4096 + 197, 384, 256  # tokens (not a k-tile multiple, odd), out features, in features
+    dy, x = _r(T, N), _r(T, K)
+    dw = torch.randn(N, K, device="cuda")
+    db = torch.randn(N, device="cuda")
+    want_w = dw + dy.float().t() @ x.float()
+    want_b = db + dy.float().sum(0)
+    mgemm(dy, x, dw, M=N, N=K, K=T, lda=N, ldb=K, ldc=K, a_kmaj=True, b_kmaj=True, rowsum=db, accumulate=True,
+          splitk=split, tile=0)
+    assert _rel(dw, want_w) < 1e-5
+    assert _rel(db, want_b) < 1e-5
+
+
+def test_mgemm_rejects_bad_shapes():
+    from rocket_amd.ops._lib import NativeError
+    from rocket_amd.ops.mgemm import mgemm
+
+    a, b = _r(64, 100), _r(64, 100)  # K % 8 != 0
+    c = torch.empty(64, 64, device="cuda")
+    with pytest.raises(NativeError):
+        mgemm(a, b, c, M=64, N=64, K=100, lda=100, ldb=100, ldc=64)
+
+
+def _ref_linear_grads(mod_ref, x, g):
+    xr = x.detach().float().requires_grad_()
+    y = mod_ref(xr)
+    y.backward(g.float())
+    return y, xr.grad
+
+
+def test_mlinear_matches_linear():
+    from rocket_amd.ops.mlinear import MLinear
+
+    torch.manual_seed(3)
+    m = MLinear(768, 2304).cuda()
+    ref = torch.nn.Linear(768, 2304).cuda()
+    ref.load_state_dict(m.state_dict())
+    with torch.no_grad():  # reference on the same bf16-rounded weights
+        ref.weight.copy_(ref.weight.to(torch.bfloat16).float())
+    x = _r(4, 197, 768).requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    assert y.dtype == torch.bfloat16 and y.shape == (4, 197, 2304)
+    g = _r(4, 197, 2304)
+    y.backward(g)
+    yr, dxr = _ref_linear_grads(ref, x, g)
+    assert _rel(y, yr) < 5e-3
+    assert _rel(x.grad, dxr) < 5e-3
+    assert _rel(m.weight.grad, ref.weight.grad) < 1e-3
+    assert _rel(m.bias.grad, ref.bias.grad) < 1e-3
+
+
+def test_mmlp_matches_unfused():
+    from rocket_amd.ops.mlinear import MMlp
+
+    torch.manual_seed(4)
+    m = MMlp(768, 3072).cuda()
+    fc1, fc2 = torch.nn.Linear(768, 3072).cuda(), torch.nn.Linear(3072, 768).cuda()
+    fc1.load_state_dict(m.fc1.state_dict())
+    fc2.load_state_dict(m.fc2.state_dict())
+    with torch.no_grad():
+        for lin in (fc1, fc2):
+            lin.weight.copy_(lin.weight.to(torch.bfloat16).float())
+    x = _r(2, 197, 768).requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    g = _r(2, 197, 768)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    yr = fc2(F.gelu(fc1(xr)))
+    yr.backward(g.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2
+    for a, b in ((m.fc1.weight, fc1.weight), (m.fc1.bias, fc1.bias), (m.fc2.weight, fc2.weight),
+                 (m.fc2.bias, fc2.bias)):
+        assert _rel(a.grad, b.grad) < 1e-2
+
+
+def test_mlinear_direct_grad_accumulates():
+    """With a persistent grad (engine flat buckets / graph capture) the wgrad accumulates in place."""
+    from rocket_amd.ops.mlinear import MLinear
+
+    torch.manual_seed(5)
+    m = MLinear(256, 512).cuda()
+    for p in m.parameters():
+        p.grad = torch.ones_like(p)
+        p._rocket_direct_grad = True
+    seen = []
+    for p in m.parameters():
+        p._rocket_grad_hook = lambda q: seen.append(q)
+    x = _r(1024, 256)
+    g = _r(1024, 512)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    y.backward(g)
+    assert len(seen) == 2
+    want_w = 1 + g.float().t() @ x.float()
+    want_b = 1 + g.float().sum(0)
+    assert _rel(m.weight.grad, want_w) < 1e-4 and _rel(m.bias.grad, want_b) < 1e-4
