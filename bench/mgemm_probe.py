@@ -81,7 +81,7 @@ def main():
                 rec["auto"] = list(pick_split(gM, gN, gK))
             else:
                 configs = [(t, 1) for t in TILES] if not args.quick else [(pick_tile(gM, gN, gK), 1)]
-                configs = [(t, s) for t, s in configs if not (t >= 6 and ak and bk)]
+                configs = [(t, s) for t, s in configs if not (t >= 6 and ak and bk) and t in (0, 4, 7, 8, 9)]
                 rec["auto"] = [pick_tile(gM, gN, gK), 1]
             for t, s in configs:
                 odt = torch.float32 if d == "wgrad" else torch.bfloat16

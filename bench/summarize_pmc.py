@@ -110,8 +110,8 @@ def main():
     print(f"# {a.title}\n")
     print(f"rocprofv3 --kernel-trace --pmc, {len(a.passes)} passes (one run each), per-kernel means over the last "
           f"{nsteps} steps.  Times are from the counter runs (kernels serialised by the profiler).\n")
-    print("| kernel | calls/step | us/call | share | grid/wg | VGPR/AGPR/LDS | active/wait/inst-stall % | VALU/LDS/MFMA inst per wave | MFMA util % | LDS bank-conflict % | HBM GB/s |")
-    print("|---|---:|---:|---:|---|---|---|---|---:|---:|---:|")
+    print("| kernel | calls/step | us/call | share | grid/wg | VGPR/AGPR/LDS | active/wait/inst-stall % | VALU/LDS/MFMA inst per wave | MFMA util % | LDS bank-conflict % | HBM GB/s | L2 hit % |")
+    print("|---|---:|---:|---:|---|---|---|---|---:|---:|---:|---:|")
     for n, m in rows[: a.top]:
         g = meta.get(n, (None,) * 5)
         wc = m.get("SQ_WAVE_CYCLES", 0.0)
@@ -125,8 +125,11 @@ def main():
         hbm = "-"
         if dur and ("FETCH_SIZE" in m or "WRITE_SIZE" in m):
             hbm = f"{(m.get('FETCH_SIZE', 0) + m.get('WRITE_SIZE', 0)) * 1024 / dur:.0f}"
+        hit = "-"
+        if m.get("TCC_HIT_sum", 0) + m.get("TCC_MISS_sum", 0):
+            hit = f"{100 * m['TCC_HIT_sum'] / (m['TCC_HIT_sum'] + m['TCC_MISS_sum']):.0f}"
         print(f"| `{n}` | {m['calls'] / nsteps:.1f} | {dur / 1e3:.1f} | {100 * m['us_step'] / tot:.1f}% | {g[0]}/{g[1]} | "
-              f"{g[3]}/{g[4]}/{g[2]} | {part} | {inst} | {mfma} | {lds} | {hbm} |")
+              f"{g[3]}/{g[4]}/{g[2]} | {part} | {inst} | {mfma} | {lds} | {hbm} | {hit} |")
 
 
 if __name__ == "__main__":

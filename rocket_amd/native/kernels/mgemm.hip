@@ -538,6 +538,128 @@ __global__ void __launch_bounds__(64 * WM * WN, WM * WN / 4) mgemm_phase_kernel(
   store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, 0);
 }
 
+// Deep-ring large-tile kernel: BM x BN x 32 k-tiles in a 4-slot LDS ring (3 tiles of DMA in
+// flight behind the one being consumed: the L2-miss latency of the panel slices that other XCDs
+// have not fetched yet is hidden ~3000 cycles deep), one block per CU, 8 waves.  Each k-tile is
+// consumed in 2 phases (the wave's A fragments in halves); a phase issues the LDS reads of the
+// next phase after its first MFMA row, so fragment reads run under the matrix cores.  B fragments
+// alternate between two register sets by tile parity (loop unrolled by 2 tiles).
+template <int BM, int BN, int WM, int WN, bool AK, bool BKM>
+__global__ void __launch_bounds__(64 * WM * WN, WM * WN / 4) mgemm_deep_kernel(MArgs g) {
+  constexpr int BK = 32, NS = 4, NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16, FH = FM / 2;
+  static_assert(FM % 2 == 0, "phases split the wave's A fragments in halves");
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int NL = (BM + BN) * BK / (512 * NW);
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE_BYTES];
+
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin / tiles_n, tn = lin % tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int nt = (g.K + BK - 1) / BK;
+  const int klast = g.K - (nt - 1) * BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stager<BM, BK, AK, NW> sa;
+  Stager<BN, BK, BKM, NW> sb;
+  sa.init(g.lda, row0, g.M, wid, lane);
+  sb.init(g.ldb, col0, g.N, wid, lane);
+  const int64_t a_step = AK ? (int64_t)BK * g.lda * 2 : BK * 2;
+  const int64_t b_step = BKM ? (int64_t)BK * g.ldb * 2 : BK * 2;
+  auto issue = [&](int t) {
+    char* buf = smem + (t % NS) * STAGE_BYTES;
+    if (t + 1 < nt || klast == BK) {
+      sa.issue((const char*)g.a + t * a_step, buf, wid);
+      sb.issue((const char*)g.b + t * b_step, buf + A_BYTES, wid);
+    } else {
+      const char* zero = (const char*)g_mgemm_zero;
+      sa.issue_tail((const char*)g.a + t * a_step, buf, wid, lane, klast, zero);
+      sb.issue_tail((const char*)g.b + t * b_step, buf + A_BYTES, wid, lane, klast, zero);
+    }
+  };
+  FragReader<BM, BK, AK, FM> ra;
+  FragReader<BN, BK, BKM, FN> rb;
+  ra.init(wm * TM, lane);
+  rb.init(wn * TN, lane);
+
+  bf16x8 Ba[FN], Bb[FN], Alo[FH], Ahi[FH];
+  auto readB = [&](bf16x8 (&dst)[FN], int t) {
+    const char* Bs = smem + (t % NS) * STAGE_BYTES + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) dst[j] = rb.get(Bs, j, 0);
+  };
+  auto readA = [&](bf16x8 (&dst)[FH], int t, int mh) {
+    const char* As = smem + (t % NS) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < FH; ++i) dst[i] = ra.get(As, mh * FH + i, 0);
+  };
+  auto mma = [&](const bf16x8 (&B)[FN], const bf16x8 (&A)[FH], int mh, int i0, int i1) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < FH; ++i)
+      if (i >= i0 && i < i1)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[mh * FH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B[j], A[i], acc[mh * FH + i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // the boundary into tile u: its DMA landed (tiles up to u+NS-2 may stay in flight) in every
+  // wave, every wave finished reading tile u-1: refill u-1's slot with tile u+NS-1
+  auto boundary = [&](int u) {
+    wait_vm((min(nt - 1, u + NS - 2) - u) * NL);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (u + NS - 1 < nt) issue(u + NS - 1);
+  };
+  // one k-tile: phase 1 (B, Alo) prefetching Ahi; phase 2 (B, Ahi) crossing into tile t+1 and
+  // prefetching its B (into BN) and Alo.  A macro, not a lambda taking array references: every
+  // fragment array is then a distinct named register block (no copies between them).
+#define RK_DEEP_TILE(t, B, BN)                        \
+  do {                                                \
+    mma(B, Alo, 0, 0, 1);                             \
+    readA(Ahi, (t), 1);                               \
+    mma(B, Alo, 0, 1, FH);                            \
+    mma(B, Ahi, 1, 0, 1);                             \
+    if ((t) + 1 < nt) {                               \
+      boundary((t) + 1);                              \
+      readB(BN, (t) + 1);                             \
+      readA(Alo, (t) + 1, 0);                         \
+    }                                                 \
+    mma(B, Ahi, 1, 1, FH);                            \
+  } while (0)
+
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nt) issue(t);
+  wait_vm((min(nt - 1, NS - 2)) * NL);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (NS - 1 < nt) issue(NS - 1);  // the ring's last slot (the boundaries refill from tile NS on)
+  readB(Ba, 0);
+  readA(Alo, 0, 0);
+  for (int t = 0; t < nt; t += 2) {
+    RK_DEEP_TILE(t, Ba, Bb);
+    if (t + 1 < nt) RK_DEEP_TILE(t + 1, Bb, Ba);
+  }
+#undef RK_DEEP_TILE
+
+  const uint2 nos[FM][FN] = {};
+  store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, 0);
+}
+
 // C[m][n] (+)= sum_s slab[s][m][n] + bias[n]  (f32 or bf16 C; N % 4 == 0)
 __global__ void __launch_bounds__(256) mgemm_reduce(const float* __restrict__ slab, int splitk, int M, int N,
                                                     const float* __restrict__ bias, void* c, int c_dt, int64_t ldc,
@@ -589,6 +711,16 @@ int launch_tile(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
 }
 
 template <int BM, int BN, int WM, int WN>
+int launch_deep(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  const dim3 grid(tiles), block(64 * WM * WN);
+  if (!a_kmaj && !b_kmaj) mgemm_deep_kernel<BM, BN, WM, WN, false, false><<<grid, block, 0, s>>>(g);
+  else if (!a_kmaj && b_kmaj) mgemm_deep_kernel<BM, BN, WM, WN, false, true><<<grid, block, 0, s>>>(g);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN>
 int launch_phase(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   const dim3 grid(tiles), block(64 * WM * WN);
@@ -607,7 +739,8 @@ constexpr int kTileBK[] = {32, 64, 64, 64, 64, 32};
 //   0: 128x128x64 ring 2, 2x4 waves, 2/CU (64 KiB)    4: 128x128x64 ring 2, 2x2 waves, 2/CU (64 KiB)
 //   5: 128x128x32 ring 4, 2x4 waves, 2/CU (64 KiB)
 //   6: 256x256x64 phase-pipelined, 2x4 waves, 1/CU (128 KiB)   7: 256x128x64 phase, 4x2 waves (96 KiB)
-//      (row x row and row x kmaj only; no split-K / row sums)
+//   8: 256x256x32 4-slot ring, 2x4 waves, 1/CU (128 KiB)      9: 256x128x32 4-slot ring, 4x2 (96 KiB)
+//      (6-9: row x row and row x kmaj only; no split-K / row sums)
 // (256x256, 256x128 and 128x256 tiles with 1-2 blocks per CU and 2-4 deep rings measured slower
 // at every ViT shape on this loop structure: bench/mgemm_probe.py, profiles/r2_mgemm_probe.md)
 // Requirements (hipErrorInvalidValue otherwise; the caller falls back): K % 8 == 0 (unless both
@@ -618,7 +751,7 @@ RK_API int rk_mgemm(const void* a, int64_t lda, int a_kmaj, const void* b, int64
                     int64_t ldc, void* c_pre, const float* bias, const void* aux, int epi, int accumulate,
                     float* rowsum, int M, int N, int K, int splitk, int tile, float* slab, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
-  if (tile != 0 && tile != 4 && tile != 5 && tile != 6 && tile != 7) return (int)hipErrorInvalidValue;
+  if (tile != 0 && (tile < 4 || tile > 9)) return (int)hipErrorInvalidValue;
   if (tile >= 6 && (splitk > 1 || rowsum != nullptr || (a_kmaj && b_kmaj))) return (int)hipErrorInvalidValue;
   // a row-layout operand moves K in 16-byte chunks (K % 8); a kmaj one in whole k-rows (any K)
   if (K <= 0 || ((!a_kmaj || !b_kmaj) && K % 8) || N % 8 || (a_kmaj && M % 8) || ldc % 4) return (int)hipErrorInvalidValue;
@@ -642,6 +775,8 @@ RK_API int rk_mgemm(const void* a, int64_t lda, int a_kmaj, const void* b, int64
     case 4: rc = launch_tile<128, 128, 64, 2, 2, 2, 2>(g, a_kmaj, b_kmaj, s); break;
     case 6: rc = launch_phase<256, 256, 2, 4>(g, a_kmaj, b_kmaj, s); break;
     case 7: rc = launch_phase<256, 128, 4, 2>(g, a_kmaj, b_kmaj, s); break;
+    case 8: rc = launch_deep<256, 256, 2, 4>(g, a_kmaj, b_kmaj, s); break;
+    case 9: rc = launch_deep<256, 128, 4, 2>(g, a_kmaj, b_kmaj, s); break;
     default: rc = launch_tile<128, 128, 32, 4, 2, 4, 2>(g, a_kmaj, b_kmaj, s); break;
   }
   if (rc || splitk == 1) return rc;

@@ -24,7 +24,7 @@ from rocket_amd.ops import _lib
 EPI = {"none": 0, "relu": 1, "gelu": 2, "mul_gelu_grad": 3, "mul_relu_grad": 4}
 # tile id -> (BM, BN, resident blocks per CU, relative per-CU throughput); see rk_mgemm
 TILES = {0: (128, 128, 2, 0.85), 4: (128, 128, 2, 0.85), 5: (128, 128, 2, 0.8), 6: (256, 256, 1, 1.0),
-         7: (256, 128, 1, 0.9)}
+         7: (256, 128, 1, 0.9), 8: (256, 256, 1, 1.0), 9: (256, 128, 1, 0.9)}
 N_CU = 256
 
 

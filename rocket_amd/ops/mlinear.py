@@ -11,10 +11,10 @@ launch of the wgrad):
   ``db = sum_tokens dy`` comes out of the same launch (MFMAs against a ones fragment), so there is
   no column-sum kernel.
 
-:class:`MMlp` fuses ``fc2(gelu(fc1(x)))``: fc1's epilogue applies GELU and keeps the pre-activation,
-and fc2's dgrad epilogue multiplies by ``gelu'(pre)`` — the GELU forward and backward kernels
-disappear.  The weights are read as bf16 copies that a fused optimizer keeps current (dense bf16
-shadows, :func:`rocket_amd.ops.linear._bf16_copy`), so there is no per-step cast either.
+:class:`MMlp` is ``fc2(gelu(fc1(x)))`` as one autograd node (pre-activation saved once, GELU
+forward/backward as single streaming kernels).  The weights are read as bf16 copies that a fused
+optimizer keeps current (dense bf16 shadows, :func:`rocket_amd.ops.linear._bf16_copy`), so there
+is no per-step cast either.  Which engine runs each product: ``MODE`` below.
 
 Everywhere else (CPU, no autocast, odd shapes) they are exactly ``nn.Linear`` / the unfused MLP.
 Reference anchor: the Linear layers of ``/root/reference/examples/mnist.py:49-51``.
@@ -22,21 +22,39 @@ Reference anchor: the Linear layers of ``/root/reference/examples/mnist.py:49-51
 
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops import _lib
 from rocket_amd.ops.linear import _autocast_on, _bf16_copy, _direct, grad_ready
+from rocket_amd.ops.linear import _wgrad as _lib_wgrad
 from rocket_amd.ops.mgemm import mgemm, pick_split
 
-# forward/dgrad tile per operand layout (bench/mgemm_probe.py at the ViT-B/16 shapes): the
-# 4-wave 128x128 tile wins the wide (N >= 2048) forwards, the 8-wave one everything else
+# Which engine runs each product.  ROCKET_VIT_GEMM:
+#   lib (default)  every product on the library GEMM (hipBLASLt with the shipped TunableOp table:
+#                  tuned 256-wide tiles, K-split strided-batched wgrad) - the fastest routing
+#                  measured in-model on 1x MI355X: ViT-B/16 5,058 img/s vs 4,629 hybrid and 4,290
+#                  native (profiles/r2_vit_gemm_routing.md);
+#   native         every product on mgemm (forward, K-major dgrad, split-K wgrad + fused bias grad);
+#   hybrid         mgemm where it won the isolated per-shape probe (bench/mgemm_probe.py): all
+#                  wgrads, the <= 2048-wide dgrads and the K = 3072 forward; the library elsewhere.
+MODE = os.environ.get("ROCKET_VIT_GEMM", "lib")
 _TILE_WIDE_FWD, _TILE_DEFAULT = 4, 0
 
 
 def _fwd_tile(N: int) -> int:
     return _TILE_WIDE_FWD if N >= 2048 else _TILE_DEFAULT
+
+
+def _lib_fwd(K: int) -> bool:
+    return MODE == "lib" or (MODE == "hybrid" and K < 2048)
+
+
+def _lib_dgrad(N_in: int) -> bool:
+    return MODE == "lib" or (MODE == "hybrid" and N_in > 2048)
 
 
 def _ok(x: torch.Tensor, N: int, K: int) -> bool:
@@ -51,12 +69,44 @@ def _as_bf16_2d(t: torch.Tensor, K: int) -> torch.Tensor:
     return t if t.is_contiguous() else t.contiguous()
 
 
+def _linear_fwd(x2: torch.Tensor, w16: torch.Tensor, bias: torch.Tensor, b16: torch.Tensor) -> torch.Tensor:
+    M, K = x2.shape
+    N = w16.shape[0]
+    if _lib_fwd(K):
+        return torch.addmm(b16, x2, w16.t())
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
+    mgemm(x2, w16, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, tile=_fwd_tile(N))
+    return y
+
+
+def _linear_dgrad(dy2: torch.Tensor, w16: torch.Tensor) -> torch.Tensor:
+    M, N = dy2.shape
+    K = w16.shape[1]
+    if _lib_dgrad(K):
+        return dy2 @ w16
+    dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy2.device)
+    mgemm(dy2, w16, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, b_kmaj=True, tile=_TILE_DEFAULT)
+    return dx
+
+
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, need_w: bool,
            need_b: bool):
     """dW = dy^T x (f32) and db = column sums of dy, accumulated into persistent grads when the
     engine provides them (returns None for those), else returned as new tensors."""
     M, N = dy.shape
     K = x.shape[1]
+    if MODE == "lib":
+        dw = _lib_wgrad(dy, x) if need_w else None
+        db = None
+        if need_b:
+            db = torch.zeros(N, dtype=torch.float32, device=dy.device)
+            lib = _lib.kernels()
+            ws = torch.empty(int(lib.rk_bn_workspace(M, N)), dtype=torch.float32, device=dy.device)
+            nctr = int(lib.rk_bn_counters(N))
+            _lib.check(lib.rk_colsum_acc(_lib.dtype_code(dy), dy.data_ptr(), M, N, db.data_ptr(), ws.data_ptr(),
+                                         _lib.Workspace.get(dy.device).counter_array(f"bn{nctr}", nctr),
+                                         _lib.stream_ptr(dy.device)), "rk_colsum_acc")
+        return dw, db
     direct = (not need_w or _direct(weight)) and (not need_b or _direct(bias))
     if direct:
         dw = weight.grad if need_w else torch.empty(N, K, dtype=torch.float32, device=dy.device)
@@ -78,14 +128,12 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
 
 class _MLinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, w16):
+    def forward(ctx, x, weight, bias, w16, b16):
         shape = x.shape
         K = shape[-1]
         N = w16.shape[0]
         x2 = _as_bf16_2d(x, K)
-        M = x2.shape[0]
-        y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-        mgemm(x2, w16, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, tile=_fwd_tile(N))
+        y = _linear_fwd(x2, w16, bias, b16)
         ctx.save_for_backward(x2, w16)
         ctx.params = (weight, bias)
         ctx.shape = shape
@@ -95,61 +143,61 @@ class _MLinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w16 = ctx.saved_tensors
         weight, bias = ctx.params
-        M, K = x2.shape
         N = w16.shape[0]
         dy2 = _as_bf16_2d(dy, N)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
-            mgemm(dy2, w16, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, b_kmaj=True, tile=_TILE_DEFAULT)
-            dx = dx.reshape(ctx.shape)
+        dx = _linear_dgrad(dy2, w16).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
         need_b = bias is not None and ctx.needs_input_grad[2]
         dw = db = None
         if ctx.needs_input_grad[1] or need_b:
             dw, db = _wgrad(dy2, x2, weight, bias, ctx.needs_input_grad[1], need_b)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
+
+
+def _gelu_fwd(z: torch.Tensor) -> torch.Tensor:
+    h = torch.empty_like(z)
+    _lib.check(_lib.kernels().rk_gelu_fwd(1, 1, z.data_ptr(), h.data_ptr(), z.numel(),
+                                          _lib.stream_ptr(z.device)), "rk_gelu_fwd")
+    return h
+
+
+def _gelu_bwd(dh: torch.Tensor, z: torch.Tensor) -> torch.Tensor:
+    dz = torch.empty_like(z)
+    _lib.check(_lib.kernels().rk_gelu_bwd(1, 1, dh.data_ptr(), z.data_ptr(), dz.data_ptr(),
+                                          z.numel(), _lib.stream_ptr(z.device)), "rk_gelu_bwd")
+    return dz
 
 
 class _MMlpFn(torch.autograd.Function):
-    """y = fc2(gelu(fc1(x))) with GELU in fc1's epilogue and gelu' in fc2's dgrad epilogue."""
+    """y = fc2(gelu(fc1(x))): GELU forward/backward as one streaming HIP kernel each (a GELU
+    epilogue inside the K = 768 GEMM costs more than that: the erf math runs in phase with the
+    MFMAs of every block instead of overlapping them)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, w1_16, w2_16):
+    def forward(ctx, x, w1, b1, w2, b2, w1_16, b1_16, w2_16, b2_16):
         shape = x.shape
         K = shape[-1]
-        H, N = w1_16.shape[0], w2_16.shape[0]
+        N = w2_16.shape[0]
         x2 = _as_bf16_2d(x, K)
-        M = x2.shape[0]
-        pre = torch.empty(M, H, dtype=torch.bfloat16, device=x.device)
-        h = torch.empty(M, H, dtype=torch.bfloat16, device=x.device)
-        mgemm(x2, w1_16, h, M=M, N=H, K=K, lda=K, ldb=K, ldc=H, bias=b1, epi="gelu", c_pre=pre, tile=_fwd_tile(H))
-        y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-        mgemm(h, w2_16, y, M=M, N=N, K=H, lda=H, ldb=H, ldc=N, bias=b2, tile=_fwd_tile(N))
-        ctx.save_for_backward(x2, pre, h, w1_16, w2_16)
+        z = _linear_fwd(x2, w1_16, b1, b1_16)
+        h = _gelu_fwd(z)
+        y = _linear_fwd(h, w2_16, b2, b2_16)
+        ctx.save_for_backward(x2, z, h, w1_16, w2_16)
         ctx.params = (w1, b1, w2, b2)
         ctx.shape = shape
         return y.reshape(*shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, pre, h, w1_16, w2_16 = ctx.saved_tensors
+        x2, z, h, w1_16, w2_16 = ctx.saved_tensors
         w1, b1, w2, b2 = ctx.params
-        M, K = x2.shape
-        H, N = w1_16.shape[0], w2_16.shape[0]
+        N = w2_16.shape[0]
         dy2 = _as_bf16_2d(dy, N)
-        # d(pre) = (dy W2) * gelu'(pre): the GELU backward is fc2's dgrad epilogue
-        dpre = torch.empty(M, H, dtype=torch.bfloat16, device=dy.device)
-        mgemm(dy2, w2_16, dpre, M=M, N=H, K=N, lda=N, ldb=H, ldc=H, b_kmaj=True, epi="mul_gelu_grad", aux=pre,
-              tile=_TILE_DEFAULT)
         g = ctx.needs_input_grad
+        dz = _gelu_bwd(_linear_dgrad(dy2, w2_16), z)
         dw2, db2 = _wgrad(dy2, h, w2, b2, g[3], b2 is not None and g[4])
-        dx = None
-        if g[0]:
-            dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy.device)
-            mgemm(dpre, w1_16, dx, M=M, N=K, K=H, lda=H, ldb=K, ldc=K, b_kmaj=True, tile=_TILE_DEFAULT)
-            dx = dx.reshape(ctx.shape)
-        dw1, db1 = _wgrad(dpre, x2, w1, b1, g[1], b1 is not None and g[2])
-        return dx, dw1, db1, dw2, db2, None, None
+        dx = _linear_dgrad(dz, w1_16).reshape(ctx.shape) if g[0] else None
+        dw1, db1 = _wgrad(dz, x2, w1, b1, g[1], b1 is not None and g[2])
+        return dx, dw1, db1, dw2, db2, None, None, None, None
 
 
 def _native(module: nn.Linear, x: torch.Tensor) -> bool:
@@ -162,9 +210,10 @@ class MLinear(nn.Linear):
     """``nn.Linear`` on the native MFMA GEMM under bf16 autocast (module docstring)."""
 
     def forward(self, x):
-        if _native(self, x):
+        if _native(self, x) and self.bias is not None:
             w16 = _bf16_copy(self, "_w16", self.weight)
-            return _MLinearFn.apply(x, self.weight, self.bias, w16)
+            b16 = _bf16_copy(self, "_b16", self.bias)
+            return _MLinearFn.apply(x, self.weight, self.bias, w16, b16)
         return super().forward(x)
 
 
@@ -180,7 +229,8 @@ class MMlp(nn.Module):
     def forward(self, x):
         if _native(self.fc1, x) and _ok(x, self.fc2.out_features, self.fc2.in_features) and \
                 self.fc2.weight.is_contiguous() and self.fc1.bias is not None and self.fc2.bias is not None:
-            w1 = _bf16_copy(self.fc1, "_w16", self.fc1.weight)
-            w2 = _bf16_copy(self.fc2, "_w16", self.fc2.weight)
-            return _MMlpFn.apply(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, w1, w2)
+            f1, f2 = self.fc1, self.fc2
+            return _MMlpFn.apply(x, f1.weight, f1.bias, f2.weight, f2.bias, _bf16_copy(f1, "_w16", f1.weight),
+                                 _bf16_copy(f1, "_b16", f1.bias), _bf16_copy(f2, "_w16", f2.weight),
+                                 _bf16_copy(f2, "_b16", f2.bias))
         return self.fc2(F.gelu(self.fc1(x)))
