@@ -1,8 +1,9 @@
 """ResNet-18 (CIFAR-10 variant) and ResNet-50 (ImageNet shape) for the BASELINE DDP configs.
 
-MI355X layout: activations are channels-last (NHWC) end to end — MIOpen's bf16
-convolutions prefer it and the fused BatchNorm kernels (:mod:`rocket_amd.ops.norm`)
-reduce over contiguous channels.  Every ``conv → BN (→ +identity) → ReLU`` tail is
+MI355X layout: activations are channels-last (NHWC) end to end — the native implicit-GEMM
+convolutions (:class:`~rocket_amd.ops.iconv.IConv2d`, ``native/kernels/conv.hip``) gather NHWC
+pixels straight into LDS and the fused BatchNorm kernels (:mod:`rocket_amd.ops.norm`) reduce over
+contiguous channels.  Every ``conv → BN (→ +identity) → ReLU`` tail is
 one BN-statistics launch plus one fused apply launch (``BatchNormAct2d``), so the
 residual add and the ReLU never make their own pass over HBM.
 
@@ -19,11 +20,13 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from rocket_amd.ops.iconv import IConv2d
 from rocket_amd.ops.norm import BatchNormAct2d
 
 
 def _conv(cin, cout, k, stride=1):
-    return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False)
+    # native implicit-GEMM MFMA conv (ops/iconv.py); the 3-channel stem falls back to nn.Conv2d
+    return IConv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False)
 
 
 class BasicBlock(nn.Module):

@@ -1,0 +1,343 @@
+// Implicit-GEMM convolutions (NHWC bf16, f32 accumulation) on the MFMA GEMM core (mgemm_core.h)
+// for the ResNet configs (reference anchor examples/mnist.py:47-48).
+//
+// Tensors are channels-last: X [N][H][W][C], weights [Cout][R][S][Cin] (the memory order of a
+// channels_last nn.Conv2d weight), Y [N][OH][OW][Cout].  No im2col buffer: the LDS-DMA stager of
+// the gathered operand computes every 16-byte chunk's source pixel itself, and chunks that fall
+// into the zero padding (or past the last pixel) are DMA'd from a zero page.
+//
+//   forward  Y  = X (*) W      GEMM M = N*OH*OW pixels, N = Cout, K = R*S*Cin (r, s, ci order)
+//            A(m, k) = X[n, oh*st - pad + r, ow*st - pad + s, ci]          gathered, row image
+//            B(co, k) = W[co][r][s][ci]                                     plain row image
+//   dgrad    dX = dY (*) W^T   (stride 1) GEMM M = N*H*W, N = Cin, K = R*S*Cout (r, s, co order)
+//            A(m, k) = dY[n, ih + pad - r, iw + pad - s, co]               gathered, row image
+//            B(ci, k) = W[co][r][s][ci]                                     K-major, per-tile base
+//   wgrad    dW = dY^T (*) X   GEMM M = Cout, N = R*S*Cin, K = N*OH*OW pixels (split-K)
+//            A(co, m) = dY[m][co]                                           plain K-major image
+//            B(k', m) = X[n, oh*st - pad + r, ow*st - pad + s, ci]          gathered, K-major image
+//
+// A k-tile (64 deep) must sit inside one (r, s) tap: Cin % 64 == 0 (forward / wgrad columns:
+// Cin % 8), Cout % 64 == 0 for the dgrad.  So the tap (r, s, c0) of a k-tile is wave-uniform
+// (scalar), and a lane only adds it to its precomputed pixel coordinates.
+// Tile: 128 x 128 x 64, 8 waves (2 x 4), two blocks per CU, 2-slot LDS ring (mgemm.hip tile 0).
+#include "mgemm_core.h"
+
+using namespace rk;
+
+namespace {
+
+enum ConvMode : int { kConvFwd = 0, kConvDgrad = 1, kConvWgrad = 2 };
+
+struct ConvGeom {
+  int N, H, W, C;        // the gathered tensor (fwd/wgrad: X; dgrad: dY), NHWC
+  int GH, GW;            // the pixel grid the GEMM rows/k run over (fwd/wgrad: OH x OW; dgrad: H x W)
+  int R, S, stride, pad;
+  int taps_c;            // channels per tap of the GEMM K order (fwd: Cin; dgrad: Cout)
+  int64_t w_tap_stride;  // dgrad: elements between taps in W (= Cin); wgrad/fwd unused
+  int64_t w_co_stride;   // dgrad: elements between output channels in W (= R*S*Cin)
+  float inv_gw, inv_gh;  // 1/GW, 1/GH (pixel decomposition of the wgrad k index)
+};
+
+// (n, gh, gw) of grid pixel m (exact for m < 2^24 after the correction steps)
+__device__ __forceinline__ void split_pixel(int m, const ConvGeom& cg, int& n, int& gh, int& gw) {
+  int q = (int)((float)m * cg.inv_gw);
+  q -= (q * cg.GW > m);
+  q += ((q + 1) * cg.GW <= m);
+  gw = m - q * cg.GW;
+  int nn = (int)((float)q * cg.inv_gh);
+  nn -= (nn * cg.GH > q);
+  nn += ((nn + 1) * cg.GH <= q);
+  gh = q - nn * cg.GH;
+  n = nn;
+}
+
+// Gathered row-image operand (forward / dgrad A): rows are grid pixels, k runs over (r, s, c).
+template <int R, int NW, int MODE>
+struct GatherRows {
+  static constexpr int BK = 64, NI = R * BK / (512 * NW);
+  int nb[NI], h0[NI], w0[NI], coff[NI];
+  bool mok[NI];
+  __device__ __forceinline__ void init(const ConvGeom& cg, int row0, int M, int wid, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = (wid * NI + i) * 64 + lane;
+      const int r = q >> 3, c = q & 7;
+      const int m = row0 + r;
+      mok[i] = m < M;
+      const int mm = mok[i] ? m : 0;
+      const int gw = mm % cg.GW, t = mm / cg.GW;
+      const int gh = t % cg.GH, n = t / cg.GH;
+      nb[i] = n * cg.H;
+      if (MODE == kConvFwd) {
+        h0[i] = gh * cg.stride - cg.pad;
+        w0[i] = gw * cg.stride - cg.pad;
+      } else {  // dgrad, stride 1: oh = ih + pad - r
+        h0[i] = gh + cg.pad;
+        w0[i] = gw + cg.pad;
+      }
+      coff[i] = (c ^ rswz<BK>(r)) * 8;
+    }
+  }
+  // k-tile at tap (tr, ts), channel offset c0
+  __device__ __forceinline__ void issue(const uint16_t* x, const ConvGeom& cg, int tr, int ts, int c0, char* lds,
+                                        int wid, const char* zero) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int h = MODE == kConvFwd ? h0[i] + tr : h0[i] - tr;
+      const int w = MODE == kConvFwd ? w0[i] + ts : w0[i] - ts;
+      const bool ok = mok[i] && (unsigned)h < (unsigned)cg.H && (unsigned)w < (unsigned)cg.W;
+      const int64_t e = ((int64_t)(nb[i] + h) * cg.W + w) * cg.C + c0 + coff[i];
+      const char* src = ok ? (const char*)(x + e) : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0, 0);
+    }
+  }
+};
+
+// Gathered K-major operand (wgrad B): k rows are output pixels, columns are (r, s, ci) chunks.
+template <int R, int NW>
+struct GatherCols {
+  static constexpr int BK = 64, NI = R * BK / (512 * NW), CPR = R / 8;
+  int krow[NI], tr[NI], ts[NI], ci[NI];
+  bool cok[NI];
+  __device__ __forceinline__ void init(const ConvGeom& cg, int col0, int Ncols, int wid, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = (wid * NI + i) * 64 + lane;
+      const int k = q / CPR, c = q % CPR;
+      krow[i] = k;
+      const int col = col0 + (c ^ kswz<R>(k)) * 8;
+      cok[i] = col < Ncols;
+      const int cc = cok[i] ? col : 0;
+      const int tap = cc / cg.C;
+      ci[i] = cc - tap * cg.C;
+      tr[i] = tap / cg.S;
+      ts[i] = tap - tr[i] * cg.S;
+    }
+  }
+  __device__ __forceinline__ void issue(const uint16_t* x, const ConvGeom& cg, int k0, int kend, char* lds, int wid,
+                                        const char* zero) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int m = k0 + krow[i];
+      int n, oh, ow;
+      split_pixel(min(m, kend - 1), cg, n, oh, ow);
+      const int h = oh * cg.stride - cg.pad + tr[i];
+      const int w = ow * cg.stride - cg.pad + ts[i];
+      const bool ok = cok[i] && m < kend && (unsigned)h < (unsigned)cg.H && (unsigned)w < (unsigned)cg.W;
+      const int64_t e = ((int64_t)(n * cg.H + h) * cg.W + w) * cg.C + ci[i];
+      const char* src = ok ? (const char*)(x + e) : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0, 0);
+    }
+  }
+};
+
+template <int MODE, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MArgs g, ConvGeom cg) {
+  constexpr int BK = 64, NS = 2, NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16, KK = BK / 32;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr bool AK = MODE == kConvWgrad;   // A K-major (dY read pixel-major)
+  constexpr bool BKM = MODE != kConvFwd;    // B K-major (dgrad: W per tap; wgrad: gathered X)
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE_BYTES];
+
+  const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lin / ntiles;
+  const int tile = lin % ntiles;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int kb = split * g.k_per_split;
+  const int ke = min(g.K, kb + g.k_per_split);
+  const int nt = (ke - kb + BK - 1) / BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const char* zero = (const char*)g_mgemm_zero;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // operand stagers per mode
+  GatherRows<BM, NW, MODE == kConvDgrad ? kConvDgrad : kConvFwd> ga;  // fwd/dgrad A
+  Stager<BM, BK, true, NW> sa_k;                                      // wgrad A (dY K-major)
+  Stager<BN, BK, false, NW> sb_row;                                    // fwd B (W rows)
+  Stager<BN, BK, true, NW> sb_k;                                       // dgrad B (W per tap)
+  GatherCols<BN, NW> gb;                                               // wgrad B
+  if constexpr (MODE == kConvWgrad) {
+    sa_k.init(g.lda, row0, g.M, wid, lane);
+    gb.init(cg, col0, g.N, wid, lane);
+  } else {
+    ga.init(cg, row0, g.M, wid, lane);
+    if constexpr (MODE == kConvFwd) sb_row.init(g.ldb, col0, g.N, wid, lane);
+    else sb_k.init(g.ldb, col0, g.N, wid, lane);
+  }
+
+  auto issue = [&](int t) {
+    char* buf = smem + (t % NS) * STAGE_BYTES;
+    const int k0 = kb + t * BK;
+    if constexpr (MODE == kConvWgrad) {
+      if (k0 + BK <= ke) sa_k.issue((const char*)g.a + (int64_t)k0 * g.lda * 2, buf, wid);
+      else sa_k.issue_tail((const char*)g.a + (int64_t)k0 * g.lda * 2, buf, wid, lane, ke - k0, zero);
+      gb.issue(g.b, cg, k0, ke, buf + A_BYTES, wid, zero);
+    } else {
+      const int tap = k0 / cg.taps_c, c0 = k0 - tap * cg.taps_c;
+      const int tr = tap / cg.S, ts = tap - tr * cg.S;
+      ga.issue(g.a, cg, tr, ts, c0, buf, wid, zero);
+      if constexpr (MODE == kConvFwd)
+        sb_row.issue((const char*)g.b + (int64_t)k0 * 2, buf + A_BYTES, wid);
+      else  // W[co][tap][ci]: k-tile rows co = c0.., columns ci
+        sb_k.issue((const char*)g.b + ((int64_t)tap * cg.w_tap_stride + (int64_t)c0 * cg.w_co_stride) * 2,
+                   buf + A_BYTES, wid);
+    }
+  };
+  FragReader<BM, BK, AK, FM> ra;
+  FragReader<BN, BK, BKM, FN> rb;
+  ra.init(wm * TM, lane);
+  rb.init(wn * TN, lane);
+
+  const bool want_rows = g.rowsum != nullptr && tn == 0;
+  constexpr int FR = (FM + WN - 1) / WN;
+  f32x4 racc[FR];
+#pragma unroll
+  for (int i = 0; i < FR; ++i) racc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+  if (nt > 0) issue(0);
+  for (int t = 0; t < nt; ++t) {
+    wait_vm(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 1 < nt) issue(t + 1);
+    const char* As = smem + (t % NS) * STAGE_BYTES;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = rb.get(Bs, j, kk);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = ra.get(As, i, kk);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      if (want_rows) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          if (i % WN == wn) racc[i / WN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], racc[i / WN], 0, 0, 0);
+      }
+    }
+  }
+  if (want_rows && lane < 16) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = row0 + wm * TM + i * 16 + lane;
+      if (i % WN == wn && m < g.M) atomicAdd(g.rowsum + m, racc[i / WN][0]);
+    }
+  }
+  const uint2 nos[FM][FN] = {};
+  store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split);
+}
+
+template <int MODE>
+int launch_conv(const MArgs& g, const ConvGeom& cg, hipStream_t s) {
+  // 64-wide GEMM side (Cout / Cin = 64 layers): a 64-wide tile with 4 waves instead of half an
+  // empty 128-wide one; everything else 128 x 128 with 8 waves
+  if (MODE != kConvWgrad && g.N <= 64) {
+    const int tiles = ((g.M + 127) / 128) * ((g.N + 63) / 64);
+    conv_kernel<MODE, 128, 64, 2, 2><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+  } else if (MODE == kConvWgrad && g.M <= 64) {
+    const int tiles = ((g.M + 63) / 64) * ((g.N + 127) / 128);
+    conv_kernel<MODE, 64, 128, 2, 2><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+  } else {
+    const int tiles = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+    conv_kernel<MODE, 128, 128, 2, 4><<<tiles * g.splitk, 512, 0, s>>>(g, cg);
+  }
+  return (int)hipGetLastError();
+}
+
+ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stride, int pad, int taps_c) {
+  ConvGeom cg;
+  cg.N = N; cg.H = H; cg.W = W; cg.C = C; cg.GH = GH; cg.GW = GW;
+  cg.R = R; cg.S = S; cg.stride = stride; cg.pad = pad; cg.taps_c = taps_c;
+  cg.w_tap_stride = 0; cg.w_co_stride = 0;
+  cg.inv_gw = 1.f / (float)GW;
+  cg.inv_gh = 1.f / (float)GH;
+  return cg;
+}
+
+MArgs margs(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int c_dt, int64_t ldc, int M, int N,
+            int K) {
+  MArgs g = {};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.M = M; g.N = N; g.K = K; g.c_dt = c_dt;
+  g.splitk = 1; g.k_per_split = K;
+  return g;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+// Y[N*OH*OW][Cout] (bf16 or f32) = conv(X, W) (+ bias[Cout]).  Cin % 64 == 0, Cout % 8 == 0.
+RK_API int rk_conv_fwd(const void* x, const void* w, void* y, int y_dt, const float* bias, int N, int H, int W, int Cin,
+                       int Cout, int R, int S, int stride, int pad, int OH, int OW, hipStream_t s) {
+  if (Cin % 64 || Cout % 8 || !aligned16(x) || !aligned16(w) || !aligned16(y)) return (int)hipErrorInvalidValue;
+  if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
+  const int M = N * OH * OW, K = R * S * Cin;
+  MArgs g = margs(x, 0, w, K, y, y_dt, Cout, M, Cout, K);
+  g.bias = bias;
+  ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
+  return launch_conv<kConvFwd>(g, cg, s);
+}
+
+// dX[N*H*W][Cin] (bf16/f32) = conv_transpose(dY, W), stride 1 only.  Cout % 64 == 0, Cin % 8 == 0.
+RK_API int rk_conv_dgrad(const void* dy, const void* w, void* dx, int dx_dt, int N, int H, int W, int Cin, int Cout,
+                         int R, int S, int stride, int pad, int OH, int OW, hipStream_t s) {
+  if (stride != 1 || Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx))
+    return (int)hipErrorInvalidValue;
+  if (OH != H + 2 * pad - R + 1 || OW != W + 2 * pad - S + 1) return (int)hipErrorInvalidValue;
+  const int M = N * H * W, K = R * S * Cout;
+  MArgs g = margs(dy, 0, w, (int64_t)R * S * Cin, dx, dx_dt, Cin, M, Cin, K);
+  ConvGeom cg = geom(N, OH, OW, Cout, H, W, R, S, 1, pad, Cout);
+  cg.w_tap_stride = Cin;
+  cg.w_co_stride = (int64_t)R * S * Cin;
+  return launch_conv<kConvDgrad>(g, cg, s);
+}
+
+// dW[Cout][R*S*Cin] f32 (+)= dY^T (*) X; split-K over the N*OH*OW pixels into `slab`
+// (splitk*Cout*R*S*Cin floats) + one combine launch.  Cin % 8 == 0, Cout % 8 == 0.
+// db (optional, f32 [Cout]) += column sums of dY (the bias gradient) from the same launch.
+RK_API int rk_conv_wgrad(const void* dy, const void* x, float* dw, int accumulate, float* db, int N, int H, int W,
+                         int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, int splitk, float* slab,
+                         hipStream_t s) {
+  if (Cin % 8 || Cout % 8 || !aligned16(dy) || !aligned16(x)) return (int)hipErrorInvalidValue;
+  const int P = N * OH * OW, Ncol = R * S * Cin;
+  MArgs g = margs(dy, Cout, x, 0, dw, F32, Ncol, Cout, Ncol, P);
+  g.rowsum = db;
+  g.accumulate = accumulate;
+  if (splitk < 1) splitk = 1;
+  int kps = ((P + 63) / 64 + splitk - 1) / splitk * 64;
+  splitk = (P + kps - 1) / kps;
+  if (splitk > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
+  g.splitk = splitk;
+  g.k_per_split = kps;
+  g.slab = slab;
+  ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
+  int rc = launch_conv<kConvWgrad>(g, cg, s);
+  if (rc || splitk == 1) return rc;
+  const int64_t nq = (int64_t)Cout * Ncol / 4;
+  const int blocks = (int)std::min<int64_t>((nq + 255) / 256, 4096);
+  mgemm_reduce<<<blocks, 256, 0, s>>>(slab, splitk, Cout, Ncol, nullptr, dw, F32, Ncol, accumulate);
+  return (int)hipGetLastError();
+}

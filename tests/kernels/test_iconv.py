@@ -1,0 +1,66 @@
+"""Native implicit-GEMM convolutions (conv.hip via ops/iconv.py) vs the fp32 PyTorch conv of the
+same bf16-rounded operands, at every distinct ResNet-18 (CIFAR) / ResNet-50 conv shape the
+native path takes (batch reduced to keep the test short; the kernels' indexing does not depend
+on it beyond the pixel count)."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+# (N, Cin, H, W, Cout, k, stride)
+SHAPES = [
+    # ResNet-50 (ImageNet 224): bottleneck 1x1 / 3x3 / 1x1 and the strided 3x3 / 1x1 downsamples
+    (4, 64, 56, 56, 64, 1, 1), (4, 64, 56, 56, 64, 3, 1), (4, 64, 56, 56, 256, 1, 1), (4, 256, 56, 56, 64, 1, 1),
+    (4, 128, 56, 56, 128, 3, 2), (4, 256, 56, 56, 512, 1, 2), (4, 128, 28, 28, 128, 3, 1),
+    (4, 512, 28, 28, 128, 1, 1), (4, 256, 14, 14, 256, 3, 1), (4, 1024, 14, 14, 256, 1, 1),
+    (4, 512, 7, 7, 512, 3, 1), (4, 2048, 7, 7, 512, 1, 1), (4, 512, 14, 14, 512, 3, 2),
+    # ResNet-18 CIFAR (32x32)
+    (8, 64, 32, 32, 64, 3, 1), (8, 64, 32, 32, 128, 3, 2), (8, 128, 16, 16, 128, 3, 1), (8, 256, 8, 8, 256, 3, 1),
+    (8, 256, 4, 4, 512, 1, 2), (8, 512, 4, 4, 512, 3, 1),
+]
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Cout,k,stride", SHAPES)
+def test_iconv_fwd_bwd(N, Cin, H, W, Cout, k, stride):
+    from rocket_amd.ops.iconv import IConv2d
+
+    torch.manual_seed(0)
+    conv = IConv2d(Cin, Cout, k, stride=stride, padding=k // 2, bias=False).cuda()
+    conv = conv.to(memory_format=torch.channels_last)
+    x = torch.randn(N, Cin, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv(x)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    yr = F.conv2d(xr, wr, stride=stride, padding=k // 2)
+    yr.backward(g.float())
+    assert _rel(y, yr) < 1e-2, _rel(y, yr)
+    assert _rel(x.grad, xr.grad) < 1e-2, _rel(x.grad, xr.grad)
+    assert _rel(conv.weight.grad, wr.grad) < 2e-3, _rel(conv.weight.grad, wr.grad)
+
+
+def test_iconv_wgrad_accumulates_into_persistent_grad():
+    from rocket_amd.ops.iconv import IConv2d
+
+    torch.manual_seed(1)
+    conv = IConv2d(64, 64, 3, padding=1, bias=False).cuda().to(memory_format=torch.channels_last)
+    conv.weight.grad = torch.ones_like(conv.weight)
+    conv.weight._rocket_direct_grad = True
+    x = torch.randn(2, 64, 20, 20, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    F.conv2d(x.float(), wr, padding=1).backward(g.float())
+    assert _rel(conv.weight.grad - 1, wr.grad) < 2e-3

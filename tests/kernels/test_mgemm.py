@@ -112,7 +112,15 @@ def _ref_linear_grads(mod_ref, x, g):
     return y, xr.grad
 
 
-def test_mlinear_matches_linear():
+@pytest.fixture(params=["native", "hybrid", "lib"])
+def gemm_mode(request, monkeypatch):
+    import rocket_amd.ops.mlinear as ml
+
+    monkeypatch.setattr(ml, "MODE", request.param)
+    return request.param
+
+
+def test_mlinear_matches_linear(gemm_mode):
     from rocket_amd.ops.mlinear import MLinear
 
     torch.manual_seed(3)
@@ -130,11 +138,12 @@ def test_mlinear_matches_linear():
     yr, dxr = _ref_linear_grads(ref, x, g)
     assert _rel(y, yr) < 5e-3
     assert _rel(x.grad, dxr) < 5e-3
-    assert _rel(m.weight.grad, ref.weight.grad) < 1e-3
-    assert _rel(m.bias.grad, ref.bias.grad) < 1e-3
+    tol = 1e-3 if gemm_mode != "lib" else 5e-3  # the library wgrad rounds dW to bf16
+    assert _rel(m.weight.grad, ref.weight.grad) < tol
+    assert _rel(m.bias.grad, ref.bias.grad) < tol
 
 
-def test_mmlp_matches_unfused():
+def test_mmlp_matches_unfused(gemm_mode):
     from rocket_amd.ops.mlinear import MMlp
 
     torch.manual_seed(4)
@@ -160,10 +169,12 @@ def test_mmlp_matches_unfused():
         assert _rel(a.grad, b.grad) < 1e-2
 
 
-def test_mlinear_direct_grad_accumulates():
-    """With a persistent grad (engine flat buckets / graph capture) the wgrad accumulates in place."""
+def test_mlinear_direct_grad_accumulates(monkeypatch):
+    """With a persistent grad (engine flat buckets / graph capture) the native wgrad accumulates in place."""
+    import rocket_amd.ops.mlinear as ml
     from rocket_amd.ops.mlinear import MLinear
 
+    monkeypatch.setattr(ml, "MODE", "native")
     torch.manual_seed(5)
     m = MLinear(256, 512).cuda()
     for p in m.parameters():
