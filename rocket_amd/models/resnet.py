@@ -25,8 +25,11 @@ from rocket_amd.ops.norm import BatchNormAct2d
 
 
 def _conv(cin, cout, k, stride=1):
-    # native implicit-GEMM MFMA conv (ops/iconv.py); the 3-channel stem falls back to nn.Conv2d
-    return IConv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False)
+    # native implicit-GEMM MFMA conv (ops/iconv.py; the 3-channel stem falls back to nn.Conv2d).
+    # Every conv here feeds a BatchNormAct2d: its epilogue emits the BatchNorm's tile statistics.
+    conv = IConv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False)
+    conv.emit_bn_stats = True
+    return conv
 
 
 class BasicBlock(nn.Module):

@@ -36,6 +36,7 @@ struct ConvGeom {
   int64_t w_tap_stride;  // dgrad: elements between taps in W (= Cin); wgrad/fwd unused
   int64_t w_co_stride;   // dgrad: elements between output channels in W (= R*S*Cin)
   float inv_gw, inv_gh;  // 1/GW, 1/GH (pixel decomposition of the wgrad k index)
+  float* bnpart;         // forward: per row-tile BatchNorm partials [tiles_m][2][Cout] (tile mean, M2) or null
 };
 
 // (n, gh, gw) of grid pixel m (exact for m < 2^24 after the correction steps)
@@ -130,6 +131,55 @@ struct GatherCols {
     }
   }
 };
+
+// BatchNorm statistics of the forward output, from the accumulators (rounded to the bf16 the tile
+// is stored as, so they describe exactly the tensor the BatchNorm normalises): every wave writes,
+// per channel of its columns, the sum and sum of squares of its TM-row slice of the tile — one
+// register pass and a 16-lane xor-shuffle reduction, no LDS, no barrier.  The following BatchNorm
+// merges these (rk_bn_finalize, pivoted on slice 0's mean) instead of re-reading the activation.
+template <int BM, int BN, int WM, int WN, int FM, int FN>
+__device__ __forceinline__ void tile_bn_stats(const MArgs& g, const ConvGeom& cg, f32x4 (&acc)[FM][FN], int tm,
+                                              int row0, int col0, int wm, int wn, int lane) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  const int mbase = row0 + wm * TM;
+  float s1[FN][4], s2[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const bool ok = mbase + i * 16 + (lane & 15) < g.M;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = ok ? bf2f(f2bf(acc[i][j][e])) : 0.f;
+        s1[j][e] += v;
+        s2[j][e] = __builtin_fmaf(v, v, s2[j][e]);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[j][e] += __shfl_xor(s1[j][e], o, 64);
+        s2[j][e] += __shfl_xor(s2[j][e], o, 64);
+      }
+  if ((lane & 15) == 0) {
+    float* part = cg.bnpart + (int64_t)(tm * WM + wm) * 2 * g.N;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = col0 + wn * TN + j * 16 + 4 * (lane >> 4);
+      if (n < g.N) {  // N % 4 == 0: all four columns in
+        *(float4*)(part + n) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
+        *(float4*)(part + g.N + n) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
+      }
+    }
+  }
+}
 
 template <int MODE, int BM, int BN, int WM, int WN>
 __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MArgs g, ConvGeom cg) {
@@ -245,12 +295,16 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
       if (i % WN == wn && m < g.M) atomicAdd(g.rowsum + m, racc[i / WN][0]);
     }
   }
+  if constexpr (MODE == kConvFwd) {
+    if (cg.bnpart != nullptr) tile_bn_stats<BM, BN, WM, WN, FM, FN>(g, cg, acc, tm, row0, col0, wm, wn, lane);
+  }
   const uint2 nos[FM][FN] = {};
   store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split);
 }
 
 template <int MODE>
 int launch_conv(const MArgs& g, const ConvGeom& cg, hipStream_t s) {
+  // (the forward's wave row slice is 64 pixels in every variant: the BatchNorm partials rely on it)
   // 64-wide GEMM side (Cout / Cin = 64 layers): a 64-wide tile with 4 waves instead of half an
   // empty 128-wide one; everything else 128 x 128 with 8 waves
   if (MODE != kConvWgrad && g.N <= 64) {
@@ -270,7 +324,7 @@ ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stri
   ConvGeom cg;
   cg.N = N; cg.H = H; cg.W = W; cg.C = C; cg.GH = GH; cg.GW = GW;
   cg.R = R; cg.S = S; cg.stride = stride; cg.pad = pad; cg.taps_c = taps_c;
-  cg.w_tap_stride = 0; cg.w_co_stride = 0;
+  cg.w_tap_stride = 0; cg.w_co_stride = 0; cg.bnpart = nullptr;
   cg.inv_gw = 1.f / (float)GW;
   cg.inv_gh = 1.f / (float)GH;
   return cg;
@@ -290,14 +344,17 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 }  // namespace
 
 // Y[N*OH*OW][Cout] (bf16 or f32) = conv(X, W) (+ bias[Cout]).  Cin % 64 == 0, Cout % 8 == 0.
+// bnpart (optional): f32 [ceil(N*OH*OW / 64)][2][Cout] per 64-pixel slice (sum, sum of squares)
+// BatchNorm partials for rk_bn_finalize.
 RK_API int rk_conv_fwd(const void* x, const void* w, void* y, int y_dt, const float* bias, int N, int H, int W, int Cin,
-                       int Cout, int R, int S, int stride, int pad, int OH, int OW, hipStream_t s) {
+                       int Cout, int R, int S, int stride, int pad, int OH, int OW, float* bnpart, hipStream_t s) {
   if (Cin % 64 || Cout % 8 || !aligned16(x) || !aligned16(w) || !aligned16(y)) return (int)hipErrorInvalidValue;
   if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW, K = R * S * Cin;
   MArgs g = margs(x, 0, w, K, y, y_dt, Cout, M, Cout, K);
   g.bias = bias;
   ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
+  cg.bnpart = bnpart;
   return launch_conv<kConvFwd>(g, cg, s);
 }
 

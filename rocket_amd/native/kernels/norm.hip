@@ -229,6 +229,74 @@ __global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && a.nbt) a.nbt[0] += 1;
 }
 
+// Statistics from per-row-slice partials written by the producing convolution's epilogue
+// (conv.hip tile_bn_stats: sum and sum of squares per channel over slices of `tile_rows` rows).
+// Each slice contributes shifted sums S1 = s - n p, S2 = q - 2 p s + n p^2 with the pivot p =
+// slice 0's mean, so the column reduction and the finalisation are bn_stats' own (mean =
+// p + S1/n, var = S2/n - (S1/n)^2).  "Rows" of this launch are the slices.
+__global__ void __launch_bounds__(BN_T) bn_finalize_kernel(BnStatsArgs a, const float* __restrict__ tp, int ntiles,
+                                                           int tile_rows) {
+  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ float s1[BN_CT], s2[BN_CT];
+  __shared__ int flag;
+  const int c0 = blockIdx.x * BN_CT;
+  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int c = c0 + cg * 8;
+  const bool cok = c < a.C;
+  const int cs = cok ? c : 0;
+  const int64_t t0 = (int64_t)blockIdx.y * a.rpb;
+  const int64_t t1e = min((int64_t)ntiles, t0 + a.rpb);
+  const float n0 = (float)min((int64_t)tile_rows, a.R);
+  float piv[8], acc1[8], acc2[8];
+  V8<float>::load(tp + cs, piv);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    piv[k] /= n0;
+    acc1[k] = acc2[k] = 0.f;
+  }
+  for (int64_t t = t0 + rg; t < t1e; t += BN_RG) {
+    float sm[8], sq[8];
+    V8<float>::load(tp + t * 2 * a.C + cs, sm);
+    V8<float>::load(tp + t * 2 * a.C + a.C + cs, sq);
+    const float n = (float)min((int64_t)tile_rows, a.R - t * tile_rows);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      acc1[k] += sm[k] - n * piv[k];
+      acc2[k] += sq[k] - 2.f * piv[k] * sm[k] + n * piv[k] * piv[k];
+    }
+  }
+  if (!cok) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc1[k] = acc2[k] = 0.f;
+  }
+  reduce_rowgroups(acc1, lds, s1);
+  reduce_rowgroups(acc2, lds, s2);
+  float t1, t2;
+  if (!bn_column_reduce(s1, s2, a.part, a.C, c0, a.counters, t1, t2, &flag)) return;
+  const int cc = c0 + (threadIdx.x >> 2);
+  if ((threadIdx.x & 3) == 0 && cc < a.C) {
+    const double n = (double)a.R;
+    const float p0 = tp[cc] / (float)min((int64_t)tile_rows, a.R);
+    const float dm = (float)(t1 / n);
+    const float mean = p0 + dm;
+    float var = (float)(t2 / n) - dm * dm;
+    var = fmaxf(var, 0.f);
+    const float inv = rsqrtf(var + a.eps);
+    a.mean[cc] = mean;
+    a.invstd[cc] = inv;
+    const float g = a.gamma ? a.gamma[cc] : 1.f;
+    const float bb = a.beta ? a.beta[cc] : 0.f;
+    a.scale[cc] = g * inv;
+    a.shift[cc] = bb - mean * g * inv;
+    if (a.run_mean) {
+      const float unb = a.R > 1 ? var * (float)(n / (n - 1.0)) : var;
+      a.run_mean[cc] = (1.f - a.momentum) * a.run_mean[cc] + a.momentum * mean;
+      a.run_var[cc] = (1.f - a.momentum) * a.run_var[cc] + a.momentum * unb;
+    }
+  }
+  if (threadIdx.x == 0 && blockIdx.x == 0 && a.nbt) a.nbt[0] += 1;
+}
+
 // Column sums of a [R][C] tensor accumulated into out[C] (+=): the bias gradient of a linear layer
 // (sum of d(out) over the rows).  Same grid / two-level reduction as bn_stats, one tensor stream.
 template <typename T>
@@ -681,6 +749,27 @@ RK_API int rk_bn_stats(int dt, const void* x, int64_t R, int C, const float* gam
     bn_stats_kernel<uint16_t><<<grid, BN_T, 0, s>>>(a);
   else
     bn_stats_kernel<float><<<grid, BN_T, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
+
+// Same outputs as rk_bn_stats, from the per-row-tile partials tp ([ntiles][2][C]: tile mean, M2) of
+// an R-row activation cut into tiles of tile_rows rows.  ws / counters as for rk_bn_stats(R, C).
+RK_API int rk_bn_finalize(const float* tp, int ntiles, int tile_rows, int64_t R, int C, const float* gamma,
+                          const float* beta, float* mean, float* invstd, float* scale, float* shift, float* run_mean,
+                          float* run_var, int64_t* nbt, float momentum, float eps, float* ws, unsigned* counters,
+                          hipStream_t s) {
+  if (C % 8 || R <= 0 || ntiles <= 0 || (int64_t)ntiles * tile_rows < R) return (int)hipErrorInvalidValue;
+  BnStatsArgs a{nullptr, R, C, 0, ws, counters, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, nbt,
+                momentum, eps};
+  // tiles per block: whole passes of BN_RG, at most the row blocks rk_bn_workspace(R, C) sized for
+  int rpb_rows;
+  const int rb_max = bn_grid_rows(R, C, &rpb_rows);
+  int per = (ntiles + rb_max - 1) / rb_max;
+  per = (per + BN_RG - 1) / BN_RG * BN_RG;
+  a.rpb = per;
+  const int rb = (ntiles + per - 1) / per;
+  dim3 grid((C + BN_CT - 1) / BN_CT, rb);
+  bn_finalize_kernel<<<grid, BN_T, 0, s>>>(a, tp, ntiles, tile_rows);
   return (int)hipGetLastError();
 }
 

@@ -40,27 +40,31 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
 
 
 def _wgrad_split(cout: int, ncol: int, pixels: int) -> int:
-    """K-split of a conv weight gradient: few output tiles (Cout x R*S*Cin) over a long pixel
-    reduction, so split the pixels until the grid fills the resident slots; each split costs one
-    more f32 slab written and re-read by the combine launch."""
-    bm = 64 if cout <= 64 else 128
+    """K-split of a conv weight gradient (few output tiles, long pixel reduction): minimise
+    modelled time = waves of resident blocks x per-block MFMA time + the split-K slab traffic
+    (each split writes one f32 [Cout][R*S*Cin] slab that the combine launch re-reads)."""
+    bm, per_cu = (64, 3) if cout <= 64 else (128, 2)
     tiles = -(-cout // bm) * -(-ncol // 128)
-    slots = 768 if bm == 64 else N_SLOTS  # 64x128 tile: 48 KiB LDS, 3 blocks per CU
+    rate_cu = 3.5e12  # sustained bf16 FLOP/s per CU of this kernel (~0.9 PF/s over 256 CUs)
     best, arg = None, 1
     for s in range(1, 257):
-        if pixels // s < 512:
+        if s > 1 and pixels // s < 256:
             break
-        waves = -(-(tiles * s) // slots)
-        slab_cost = 0.02 * s * tiles / slots  # combine traffic ~ one extra wave per 50 splits of the grid
-        c = waves / s + slab_cost
+        waves = -(-(tiles * s) // (256 * per_cu))
+        t_gemm = waves * (2.0 * bm * 128 * (pixels / s)) * per_cu / rate_cu
+        t_slab = 0.0 if s == 1 else (2.0 * s * cout * ncol * 4) / 4.0e12 + 3e-6
+        c = t_gemm + t_slab
         if best is None or c < best:
             best, arg = c, s
     return arg
 
 
+TILE_ROWS = 64  # rows per wave slice of every conv.hip forward variant (BatchNorm partials granularity)
+
+
 class _IConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, w16, stride: int, pad: int):
+    def forward(ctx, x, weight, w16, stride: int, pad: int, bnpart):
         xc = _cl(x)
         N, C, H, W = xc.shape
         Co, _, R, S = w16.shape
@@ -68,7 +72,8 @@ class _IConvFn(torch.autograd.Function):
         OW = (W + 2 * pad - S) // stride + 1
         y = torch.empty((N, Co, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         _lib.check(_lib.kernels().rk_conv_fwd(xc.data_ptr(), w16.data_ptr(), y.data_ptr(), 1, None, N, H, W, C, Co, R, S,
-                                               stride, pad, OH, OW, _lib.stream_ptr(x.device)), "rk_conv_fwd")
+                                               stride, pad, OH, OW, _lib.ptr(bnpart), _lib.stream_ptr(x.device)),
+                   "rk_conv_fwd")
         ctx.save_for_backward(xc, w16)
         ctx.weight = weight
         ctx.geo = (N, C, H, W, Co, R, S, stride, pad, OH, OW)
@@ -104,7 +109,7 @@ class _IConvFn(torch.autograd.Function):
                 grad_ready(weight)
             else:
                 dw = target
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def native_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -116,7 +121,14 @@ def native_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 
 
 class IConv2d(nn.Conv2d):
-    """``nn.Conv2d`` on the native implicit-GEMM kernels (module docstring)."""
+    """``nn.Conv2d`` on the native implicit-GEMM kernels (module docstring).
+
+    ``emit_bn_stats = True`` (set by models whose conv feeds a :class:`BatchNormAct2d`): the
+    forward epilogue also writes per-64-pixel BatchNorm partials (sum and sum of squares per
+    channel), attached to the output as ``_rocket_bn_partials``; the BatchNorm then merges those
+    instead of re-reading the activation for its statistics."""
+
+    emit_bn_stats = False
 
     def forward(self, x):
         if native_ok(self, x):
@@ -124,7 +136,17 @@ class IConv2d(nn.Conv2d):
                 with torch.no_grad():
                     self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
             w16 = _bf16_copy(self, "_w16", self.weight)
-            return _IConvFn.apply(x, self.weight, w16, self.stride[0], self.padding[0])
+            part = None
+            if self.emit_bn_stats:
+                N, _, H, W = x.shape
+                OH = (H + 2 * self.padding[0] - self.kernel_size[0]) // self.stride[0] + 1
+                OW = (W + 2 * self.padding[1] - self.kernel_size[1]) // self.stride[1] + 1
+                ntiles = -(-(N * OH * OW) // TILE_ROWS)
+                part = torch.empty(ntiles * 2 * self.out_channels, dtype=torch.float32, device=x.device)
+            y = _IConvFn.apply(x, self.weight, w16, self.stride[0], self.padding[0], part)
+            if part is not None:
+                y._rocket_bn_partials = (part, part.numel() // (2 * self.out_channels), TILE_ROWS)
+            return y
         return super().forward(x)
 
 

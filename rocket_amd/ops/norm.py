@@ -47,7 +47,7 @@ def _channels_last(x: torch.Tensor) -> torch.Tensor:
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, partials):
         lib = _lib.kernels()
         x = _channels_last(x)
         C = x.shape[1]
@@ -63,10 +63,18 @@ class _BNAct(torch.autograd.Function):
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         s = _lib.stream_ptr(dev)
-        _lib.check(lib.rk_bn_stats(_dt(x), xr.data_ptr(), R, C, _lib.ptr(w), _lib.ptr(b), stats[0].data_ptr(),
-                                   stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
-                                   _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(nbt), float(momentum), float(eps),
-                                   ws.data_ptr(), counters, s), "rk_bn_stats")
+        if partials is not None:  # the producing conv's epilogue already reduced its output tiles
+            tp, ntiles, tile_rows = partials
+            _lib.check(lib.rk_bn_finalize(tp.data_ptr(), ntiles, tile_rows, R, C, _lib.ptr(w), _lib.ptr(b),
+                                          stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(),
+                                          stats[3].data_ptr(), _lib.ptr(running_mean), _lib.ptr(running_var),
+                                          _lib.ptr(nbt), float(momentum), float(eps), ws.data_ptr(), counters, s),
+                       "rk_bn_finalize")
+        else:
+            _lib.check(lib.rk_bn_stats(_dt(x), xr.data_ptr(), R, C, _lib.ptr(w), _lib.ptr(b), stats[0].data_ptr(),
+                                       stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
+                                       _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(nbt), float(momentum),
+                                       float(eps), ws.data_ptr(), counters, s), "rk_bn_stats")
         res = None
         if residual is not None:
             res = _channels_last(residual)
@@ -109,7 +117,7 @@ class _BNAct(torch.autograd.Function):
         g = _finish(params, bufs, direct) if params else []
         gw = g[0] if weight is not None else None
         gb = g[-1] if bias is not None else None
-        return dx, gw, gb, dres, None, None, None, None, None, None
+        return dx, gw, gb, dres, None, None, None, None, None, None, None
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -132,11 +140,15 @@ class BatchNormAct2d(nn.BatchNorm2d):
         if self._fused_ok(x, residual):
             if residual is not None and residual.dtype != x.dtype:
                 residual = residual.to(x.dtype)
+            partials = getattr(x, "_rocket_bn_partials", None)
+            if partials is not None and not (x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+                                             and partials[0].numel() == 2 * partials[1] * x.shape[1]):
+                partials = None
             return _BNAct.apply(x, self.weight, self.bias, residual,
                                 self.running_mean if self.track_running_stats else None,
                                 self.running_var if self.track_running_stats else None,
                                 self.num_batches_tracked if self.track_running_stats else None,
-                                self.momentum, self.eps, self.relu)
+                                self.momentum, self.eps, self.relu, partials)
         if x.is_cuda and self.training and _ops.fused_enabled():
             _lib.kernels()  # a HIP device without the native library is an error, not a fallback
         y = super().forward(x)

@@ -64,3 +64,27 @@ def test_iconv_wgrad_accumulates_into_persistent_grad():
     wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
     F.conv2d(x.float(), wr, padding=1).backward(g.float())
     assert _rel(conv.weight.grad - 1, wr.grad) < 2e-3
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Cout,k,stride", [(4, 64, 56, 56, 64, 3, 1), (3, 128, 14, 14, 256, 1, 1),
+                                                     (8, 256, 7, 7, 512, 3, 2)])
+def test_conv_emitted_bn_stats_match_bn(N, Cin, H, W, Cout, k, stride):
+    """BatchNorm statistics merged from the conv epilogue's tile partials (rk_bn_finalize) equal
+    the BatchNorm of the stored bf16 conv output (fp32 torch batch_norm reference)."""
+    from rocket_amd.ops.iconv import IConv2d
+    from rocket_amd.ops.norm import BatchNormAct2d
+
+    torch.manual_seed(3)
+    conv = IConv2d(Cin, Cout, k, stride=stride, padding=k // 2, bias=False).cuda().to(memory_format=torch.channels_last)
+    conv.emit_bn_stats = True
+    bn = BatchNormAct2d(Cout, relu=True).cuda()
+    ref = torch.nn.BatchNorm2d(Cout).cuda()
+    x = (torch.randn(N, Cin, H, W, device="cuda") + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv(x)
+        assert getattr(y, "_rocket_bn_partials", None) is not None
+        out = bn(y)
+    want = torch.relu(ref(y.float()))
+    assert _rel(out, want) < 1e-2, _rel(out, want)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-3, atol=1e-4)
