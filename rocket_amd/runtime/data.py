@@ -31,6 +31,7 @@ MI355X-first differences:
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Iterator, List, Optional, Sequence
 
 import torch
@@ -378,6 +379,13 @@ class DeviceLoader(_LoaderBase):
     """
 
     RING = 4
+    #: ROCKET_PREFETCH=1: gather each batch on a side stream, overlapped with the previous step.
+    #: Ordering: the gather into ring slot k waits for the step that last read slot k (an event
+    #: recorded on the compute stream RING-1 batches earlier), and the compute stream waits for the
+    #: gather before the step that reads it.  Off by default: on the LeNet step (4.6 us gather,
+    #: 55 us step) the cross-queue event wait costs more than the overlap saves (17.3M -> 13.7M
+    #: samples/s measured on 1x MI355X).
+    PREFETCH = os.environ.get("ROCKET_PREFETCH", "0") == "1"
 
     def __init__(
         self,
@@ -440,11 +448,44 @@ class DeviceLoader(_LoaderBase):
         k = self._ring_pos.get(n, 0)
         self._ring_pos[n] = (k + 1) % self.RING
         bufs, gather = ring[k]
-        gather(idx)
+        if not self.PREFETCH or torch.cuda.is_current_stream_capturing():
+            gather(idx)
+            return bufs
+        compute = torch.cuda.current_stream(self.device)
+        side = self._side_stream()
+        # compute has queued every step up to the previous batch: mark that point; the gather into
+        # slot k may start once the step of batch j - RING (the last reader of slot k) is done
+        mark = torch.cuda.Event()
+        mark.record(compute)
+        self._marks.append(mark)
+        if len(self._marks) >= self.RING:
+            side.wait_event(self._marks[-self.RING])
+        if len(self._marks) > self.RING:
+            self._marks.pop(0)
+        if self._idx_ready is not None:  # this epoch's index table was uploaded on the compute stream
+            side.wait_event(self._idx_ready)
+            self._idx_ready = None
+        with torch.cuda.stream(side):
+            gather(idx)
+        done = torch.cuda.Event()
+        done.record(side)
+        compute.wait_event(done)
         return bufs
 
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+            self._marks = []
+            self._idx_ready = None
+        return self._side
+
     def _batches(self):
-        for idx in self.index_table():
+        table = self.index_table()
+        if table and self.PREFETCH and self.device.type == "cuda":
+            self._side_stream()
+            self._idx_ready = torch.cuda.Event()
+            self._idx_ready.record(torch.cuda.current_stream(self.device))
+        for idx in table:
             yield self._gather(idx)
 
     def with_skip(self, num_batches: int) -> "DeviceLoader":

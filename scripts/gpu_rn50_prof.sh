@@ -3,8 +3,8 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R; mkdir -p gpurun_out; export TMPDIR=/tmp
-cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/prof_rn50 -o run -- python3 $R/bench.py --model resnet50 --steps 4 --warmup 2 > $R/gpurun_out/prof_rn50.log 2>&1 || exit 1
-cd $R && f=$(find gpurun_out/prof_rn50 -name '*kernel_trace.csv' | head -1) && python3 bench/summarize_trace.py "$f" --steps 3 --title "ResNet-50 bf16 bs256 native convs - rocprofv3 --kernel-trace" > gpurun_out/rn50_kernels.md
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/prof_rn50 -o run -- python3 $R/bench.py --model ${MODEL:-resnet50} --steps 4 --warmup 2 > $R/gpurun_out/prof_rn50.log 2>&1 || exit 1
+cd $R && f=$(find gpurun_out/prof_rn50 -name '*kernel_trace.csv' | head -1) && python3 bench/summarize_trace.py "$f" --steps 3 --title "${MODEL:-resnet50} bf16 native convs - rocprofv3 --kernel-trace" > gpurun_out/rn50_kernels.md
 python3 - "$f" > gpurun_out/rn50_conv_calls.txt <<'PY'
 import csv, sys, collections
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
