@@ -1,6 +1,6 @@
 // Elementwise / row-wise activation kernels for the transformer path (ViT-B/16):
 //
-//   gelu_fwd     y = gelu(x) (exact erf form), bf16/f32 in, bf16/f32 out, 4 elements per access.
+//   gelu_fwd     y = gelu(x) (erf form; erf to 1.5e-7, rk_common.h), bf16/f32 in/out, 4 elements per access.
 //   gelu_bwd     dx = dy * gelu'(x), recomputed from the saved pre-activation (no extra tensor).
 //   softmax_fwd  y = softmax(x * scale) over rows of length L (attention scores), one wave per
 //                row, values held in registers (L <= 1024): one read, one write.
@@ -35,13 +35,6 @@ template <> struct V4<uint16_t> {
   }
 };
 
-__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
-
 // 4 elements per thread per iteration (8-byte bf16 / 16-byte f32 accesses); n % 4 == 0 (host)
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(T) gelu_fwd_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
@@ -49,7 +42,7 @@ __global__ void __launch_bounds__(T) gelu_fwd_kernel(const TI* __restrict__ x, T
     float v[4];
     V4<TI>::load(x + i, v);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = gelu(v[k]);
+    for (int k = 0; k < 4; ++k) v[k] = gelu_f(v[k]);
     V4<TO>::store(y + i, v);
   }
 }

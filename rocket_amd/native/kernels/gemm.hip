@@ -49,11 +49,6 @@ __device__ __forceinline__ float load_any(const void* p, int dt, int64_t i) {
   return dt == BF16 ? bf2f(((const uint16_t*)p)[i]) : ((const float*)p)[i];
 }
 
-__device__ __forceinline__ float gelu_grad(float z) {
-  const float kA = 0.7071067811865476f, kB = 0.3989422804014327f;
-  return 0.5f * (1.f + erff(z * kA)) + z * kB * __expf(-0.5f * z * z);
-}
-
 __device__ __forceinline__ float apply_mask(float v, float m, int mode) {
   if (mode == 1) return m > 0.f ? v : 0.f;
   if (mode == 2) return v * gelu_grad(m);

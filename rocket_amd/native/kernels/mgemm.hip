@@ -446,7 +446,87 @@ int launch_phase(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
 // k-tile depth of each tile config (the K granularity a caller must respect)
 constexpr int kTileBK[] = {32, 64, 64, 64, 64, 32};
 
+// dst[i] (+)= sum_s part[s][i]: the combine of a library split-K weight gradient (strided-batched
+// partial products, bf16 or f32) straight into the fp32 weight.grad — one pass instead of a
+// reduction launch, a temporary and an accumulation launch.  8 elements per thread, all split
+// loads issued before the first add.
+template <bool BF>
+__global__ void __launch_bounds__(256) slab_acc_kernel(const void* __restrict__ part, int splits, int64_t count,
+                                                       float* __restrict__ dst, int accumulate) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= count) return;
+  float acc[8];
+  if (accumulate) {
+    const float4 d0 = *(const float4*)(dst + i), d1 = *(const float4*)(dst + i + 4);
+    acc[0] = d0.x; acc[1] = d0.y; acc[2] = d0.z; acc[3] = d0.w;
+    acc[4] = d1.x; acc[5] = d1.y; acc[6] = d1.z; acc[7] = d1.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  }
+  int s = 0;
+  for (; s + 4 <= splits; s += 4) {
+    if constexpr (BF) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *(const uint4*)((const uint16_t*)part + (int64_t)(s + u) * count + i);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          acc[2 * k] += __uint_as_float(w[k] << 16);
+          acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+        }
+      }
+    } else {
+      float4 v[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* p = (const float*)part + (int64_t)(s + u) * count + i;
+        v[u][0] = *(const float4*)p;
+        v[u][1] = *(const float4*)(p + 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[0] += v[u][0].x; acc[1] += v[u][0].y; acc[2] += v[u][0].z; acc[3] += v[u][0].w;
+        acc[4] += v[u][1].x; acc[5] += v[u][1].y; acc[6] += v[u][1].z; acc[7] += v[u][1].w;
+      }
+    }
+  }
+  for (; s < splits; ++s) {
+    if constexpr (BF) {
+      const uint4 v = *(const uint4*)((const uint16_t*)part + (int64_t)s * count + i);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[2 * k] += __uint_as_float(w[k] << 16);
+        acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+      }
+    } else {
+      const float* p = (const float*)part + (int64_t)s * count + i;
+      const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+      acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+      acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+    }
+  }
+  *(float4*)(dst + i) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *(float4*)(dst + i + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+
 }  // namespace
+
+// dst[count] (+)= sum over `splits` partial arrays part[s][count] (dt 0 f32 / 1 bf16); count % 8 == 0,
+// 16-byte aligned pointers.
+RK_API int rk_slab_acc(const void* part, int dt, int splits, int64_t count, float* dst, int accumulate,
+                       hipStream_t s) {
+  if (count <= 0) return 0;
+  if (count % 8 || splits < 1 || ((uintptr_t)part | (uintptr_t)dst) % 16) return (int)hipErrorInvalidValue;
+  const int64_t blocks = (count / 8 + 255) / 256;
+  if (dt == 1) slab_acc_kernel<true><<<(unsigned)blocks, 256, 0, s>>>(part, splits, count, dst, accumulate);
+  else slab_acc_kernel<false><<<(unsigned)blocks, 256, 0, s>>>(part, splits, count, dst, accumulate);
+  return (int)hipGetLastError();
+}
 
 // Tile configs (BM x BN x BK, LDS ring depth, waves, resident blocks per CU):
 //   0: 128x128x64 ring 2, 2x4 waves, 2/CU (64 KiB)    4: 128x128x64 ring 2, 2x2 waves, 2/CU (64 KiB)

@@ -337,6 +337,52 @@ __global__ void __launch_bounds__(BN_T) colsum_acc_kernel(const T* __restrict__ 
   if ((threadIdx.x & 3) == 0 && cc < C) out[cc] += t1;
 }
 
+// dz = dh * gelu'(z) (bf16 [R][C]) AND out[c] += sum_r dz[r][c]: the transformer MLP's GELU
+// backward fused with fc1's bias gradient, so the [tokens x hidden] gradient is read once instead of
+// twice.  Grid and two-level reduction as colsum_acc_kernel.
+__global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const uint16_t* __restrict__ dh,
+                                                               const uint16_t* __restrict__ z, uint16_t* __restrict__ dz,
+                                                               int64_t R, int C, int rpb, float* part,
+                                                               unsigned* counters, float* out) {
+  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ float s1[BN_CT], s2[BN_CT];
+  __shared__ int flag;
+  const int c0 = blockIdx.x * BN_CT;
+  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int c = c0 + cg * 8;
+  const bool cok = c < C;
+  const int64_t r0 = (int64_t)blockIdx.y * rpb;
+  const int64_t r1 = min(R, r0 + rpb);
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  for (int64_t r = r0 + rg; r < r1; r += BN_U * BN_RG) {
+    float g[BN_U][8], v[BN_U][8];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const int64_t off = min(r + u * BN_RG, r1 - 1) * C + (cok ? c : 0);
+      V8<uint16_t>::load(dh + off, g[u]);
+      V8<uint16_t>::load(z + off, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const bool ok = r + u * BN_RG < r1 && cok;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[u][k] = g[u][k] * gelu_grad(v[u][k]);
+        acc[k] += ok ? v[u][k] : 0.f;
+      }
+      if (ok) V8<uint16_t>::store(dz + (r + u * BN_RG) * C + c, v[u]);
+    }
+  }
+  reduce_rowgroups(acc, lds, s1);
+  if (threadIdx.x < BN_CT) s2[threadIdx.x] = 0.f;
+  float t1, t2;
+  if (!bn_column_reduce(s1, s2, part, C, c0, counters, t1, t2, &flag)) return;
+  const int cc = c0 + (threadIdx.x >> 2);
+  if ((threadIdx.x & 3) == 0 && cc < C) out[cc] += t1;
+}
+
 // Elementwise passes: thread t owns channel vector cv = t % CV (CV = C/8 <= 256) for the whole
 // launch, so its per-channel coefficients live in registers (loaded once), and walks rows
 // r = r0 + t / CV, stepping by RPP = BN_T / CV rows; 4 rows per iteration with clamped
@@ -795,6 +841,19 @@ RK_API int rk_colsum_acc(int dt, const void* x, int64_t R, int C, float* out, fl
     colsum_acc_kernel<uint16_t><<<grid, BN_T, 0, s>>>((const uint16_t*)x, R, C, rpb, ws, counters, out);
   else
     colsum_acc_kernel<float><<<grid, BN_T, 0, s>>>((const float*)x, R, C, rpb, ws, counters, out);
+  return (int)hipGetLastError();
+}
+
+// dz = dh * gelu'(z) and out[c] += sum_r dz[r][c] (all bf16 [R][C] except out; C % 8 == 0); ws /
+// counters as rk_colsum_acc
+RK_API int rk_gelu_bwd_colsum(const void* dh, const void* z, void* dz, int64_t R, int C, float* out, float* ws,
+                              unsigned* counters, hipStream_t s) {
+  if (C % 8 || R <= 0) return (int)hipErrorInvalidValue;
+  int rpb;
+  const int rb = bn_grid_rows(R, C, &rpb);
+  dim3 grid((C + BN_CT - 1) / BN_CT, rb);
+  gelu_bwd_colsum_kernel<<<grid, BN_T, 0, s>>>((const uint16_t*)dh, (const uint16_t*)z, (uint16_t*)dz, R, C, rpb, ws,
+                                               counters, out);
   return (int)hipGetLastError();
 }
 

@@ -39,6 +39,7 @@ KERNEL_SIGS = {
                         c_int, c_int, c_void_p]),
     "rk_mgemm": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p,
                          c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "rk_slab_acc": (c_int, [c_void_p, c_int, c_int, c_int64, c_void_p, c_int, c_void_p]),
     "rk_conv_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 11 + [c_void_p, c_void_p]),
     "rk_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_int64, c_int] + [c_void_p] * 9 + [c_float, c_float, c_void_p,
                                                                                             c_void_p, c_void_p]),
@@ -77,6 +78,8 @@ KERNEL_SIGS = {
                             c_int, c_void_p]),
     "rk_bn_counters": (c_int, [c_int]),
     "rk_colsum_acc": (c_int, [c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_gelu_bwd_colsum": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]),
     "rk_bn_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int] + [c_void_p] * 11),
     "rk_ln_fwd": (c_int, [c_int, c_int] + [c_void_p] * 8 + [c_int64, c_int, c_float, c_void_p]),
     "rk_ln_workspace": (c_int64, [c_int64, c_int]),

@@ -192,6 +192,39 @@ def _wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return part.sum(0, dtype=torch.float32)
 
 
+# ROCKET_WGRAD_F32=1: the split-K partial products come out of the library GEMM in fp32 (bmm with
+# out_dtype) instead of bf16 - exact partials for twice the combine traffic.
+_WGRAD_F32 = os.environ.get("ROCKET_WGRAD_F32", "0") == "1"
+
+
+def wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, target: torch.Tensor, accumulate: bool) -> None:
+    """target (+)= dy2^T @ x2 in fp32 (target: contiguous fp32 [N, K], e.g. a persistent
+    ``weight.grad``): the library GEMM's split-K partial products are summed (and accumulated)
+    by ONE ``rk_slab_acc`` launch - no reduction temporary, no separate accumulation add."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    s = _wgrad_splits(M, N, K)
+    if s == 1:
+        part = torch.mm(dy2.t(), x2, out_dtype=torch.float32) if _WGRAD_F32 else dy2.t() @ x2
+    else:
+        a, b = dy2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K)
+        part = torch.bmm(a, b, out_dtype=torch.float32) if _WGRAD_F32 else torch.bmm(a, b)
+    part = part.contiguous()
+    _lib.check(_lib.kernels().rk_slab_acc(part.data_ptr(), _lib.dtype_code(part), s, N * K, target.data_ptr(),
+                                          int(accumulate), _lib.stream_ptr(dy2.device)), "rk_slab_acc")
+
+
+def bias_grad_into(dy2: torch.Tensor, target: torch.Tensor) -> None:
+    """target += column sums of dy2 [M, N] (fp32 target, e.g. a persistent ``bias.grad``)."""
+    M, N = dy2.shape
+    lib = _lib.kernels()
+    ws = torch.empty(int(lib.rk_bn_workspace(M, N)), dtype=torch.float32, device=dy2.device)
+    nctr = int(lib.rk_bn_counters(N))
+    _lib.check(lib.rk_colsum_acc(_lib.dtype_code(dy2), dy2.data_ptr(), M, N, target.data_ptr(), ws.data_ptr(),
+                                 _lib.Workspace.get(dy2.device).counter_array(f"bn{nctr}", nctr),
+                                 _lib.stream_ptr(dy2.device)), "rk_colsum_acc")
+
+
 class _LibLinear(torch.autograd.Function):
     """``x @ W^T + b`` on the library GEMM (hipBLASLt, bf16 under autocast) whose bias gradient is
     the column-sum kernel (``rk_colsum_acc``) instead of a generic reduction over the rows of
@@ -204,6 +237,7 @@ class _LibLinear(torch.autograd.Function):
         w = w16 if w16 is not None else weight.to(cdtype)
         y = torch.addmm(b16 if b16 is not None else bias.to(cdtype), x2.to(cdtype), w.t())
         ctx.save_for_backward(x2, w)
+        ctx.weight = weight
         ctx.bias = bias
         ctx.shape = shape
         return y.reshape(*shape[:-1], w.shape[0])
@@ -219,23 +253,35 @@ class _LibLinear(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx = (dy2 @ w).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
-        dw = _wgrad(dy2, x2.to(w.dtype)) if ctx.needs_input_grad[1] else None
-        db = None
-        if ctx.needs_input_grad[2]:
-            direct = _direct(bias)
-            target = bias.grad if direct else torch.zeros(N, dtype=torch.float32, device=dy.device)
-            lib = _lib.kernels()
-            M = dy2.shape[0]
-            ws = torch.empty(int(lib.rk_bn_workspace(M, N)), dtype=torch.float32, device=dy.device)
-            nctr = int(lib.rk_bn_counters(N))
-            _lib.check(lib.rk_colsum_acc(_lib.dtype_code(dy2), dy2.data_ptr(), M, N, target.data_ptr(), ws.data_ptr(),
-                                         _lib.Workspace.get(dy.device).counter_array(f"bn{nctr}", nctr),
-                                         _lib.stream_ptr(dy.device)), "rk_colsum_acc")
-            if direct:
-                grad_ready(bias)
-            else:
-                db = target
+        dw, db = lib_param_grads(dy2, x2.to(w.dtype), ctx.weight, bias, ctx.needs_input_grad[1],
+                                 ctx.needs_input_grad[2])
         return dx, dw, db, None, None, None
+
+
+def lib_param_grads(dy2: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None,
+                    need_w: bool, need_b: bool):
+    """Library-GEMM weight gradient + column-sum bias gradient, written straight into persistent
+    ``weight.grad`` / ``bias.grad`` when the engine provides them (returns None for those), else
+    returned as new fp32 tensors."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    dw = db = None
+    if need_w:
+        if _direct(weight) and weight.grad.is_contiguous():
+            wgrad_into(dy2, x2, weight.grad, True)
+            grad_ready(weight)
+        else:
+            dw = torch.empty(N, K, dtype=torch.float32, device=dy2.device)
+            wgrad_into(dy2, x2, dw, False)
+    if need_b:
+        direct = _direct(bias)
+        target = bias.grad if direct else torch.zeros(N, dtype=torch.float32, device=dy2.device)
+        bias_grad_into(dy2, target)
+        if direct:
+            grad_ready(bias)
+        else:
+            db = target
+    return dw, db
 
 
 def _bf16_copy(module, name: str, p: torch.Tensor):

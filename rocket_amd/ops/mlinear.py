@@ -29,8 +29,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops import _lib
-from rocket_amd.ops.linear import _autocast_on, _bf16_copy, _direct, grad_ready
-from rocket_amd.ops.linear import _wgrad as _lib_wgrad
+from rocket_amd.ops.linear import _autocast_on, _bf16_copy, _direct, grad_ready, lib_param_grads
 from rocket_amd.ops.mgemm import mgemm, pick_split
 
 # Which engine runs each product.  ROCKET_VIT_GEMM:
@@ -96,17 +95,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
     M, N = dy.shape
     K = x.shape[1]
     if MODE == "lib":
-        dw = _lib_wgrad(dy, x) if need_w else None
-        db = None
-        if need_b:
-            db = torch.zeros(N, dtype=torch.float32, device=dy.device)
-            lib = _lib.kernels()
-            ws = torch.empty(int(lib.rk_bn_workspace(M, N)), dtype=torch.float32, device=dy.device)
-            nctr = int(lib.rk_bn_counters(N))
-            _lib.check(lib.rk_colsum_acc(_lib.dtype_code(dy), dy.data_ptr(), M, N, db.data_ptr(), ws.data_ptr(),
-                                         _lib.Workspace.get(dy.device).counter_array(f"bn{nctr}", nctr),
-                                         _lib.stream_ptr(dy.device)), "rk_colsum_acc")
-        return dw, db
+        return lib_param_grads(dy, x, weight, bias, need_w, need_b)
     direct = (not need_w or _direct(weight)) and (not need_b or _direct(bias))
     if direct:
         dw = weight.grad if need_w else torch.empty(N, K, dtype=torch.float32, device=dy.device)
@@ -167,6 +156,25 @@ def _gelu_bwd(dh: torch.Tensor, z: torch.Tensor) -> torch.Tensor:
     return dz
 
 
+def _gelu_bwd_bias(dh: torch.Tensor, z: torch.Tensor, bias: torch.Tensor):
+    """(dz = dh * gelu'(z), column sums of dz added to the bias gradient) in one launch; returns
+    (dz, db) with db None when it went straight into a persistent ``bias.grad``."""
+    M, N = z.shape
+    direct = _direct(bias)
+    target = bias.grad if direct else torch.zeros(N, dtype=torch.float32, device=z.device)
+    dz = torch.empty_like(z)
+    lib = _lib.kernels()
+    ws = torch.empty(int(lib.rk_bn_workspace(M, N)), dtype=torch.float32, device=z.device)
+    nctr = int(lib.rk_bn_counters(N))
+    _lib.check(lib.rk_gelu_bwd_colsum(dh.data_ptr(), z.data_ptr(), dz.data_ptr(), M, N, target.data_ptr(),
+                                      ws.data_ptr(), _lib.Workspace.get(z.device).counter_array(f"bn{nctr}", nctr),
+                                      _lib.stream_ptr(z.device)), "rk_gelu_bwd_colsum")
+    if direct:
+        grad_ready(bias)
+        return dz, None
+    return dz, target
+
+
 class _MMlpFn(torch.autograd.Function):
     """y = fc2(gelu(fc1(x))): GELU forward/backward as one streaming HIP kernel each (a GELU
     epilogue inside the K = 768 GEMM costs more than that: the erf math runs in phase with the
@@ -193,11 +201,18 @@ class _MMlpFn(torch.autograd.Function):
         N = w2_16.shape[0]
         dy2 = _as_bf16_2d(dy, N)
         g = ctx.needs_input_grad
-        dz = _gelu_bwd(_linear_dgrad(dy2, w2_16), z)
+        need_b1 = b1 is not None and g[2]
+        db1 = None
+        if MODE == "lib" and need_b1:
+            # GELU backward and fc1's bias gradient in one pass over the [tokens, hidden] gradient
+            dz, db1 = _gelu_bwd_bias(_linear_dgrad(dy2, w2_16), z, b1)
+            need_b1 = False
+        else:
+            dz = _gelu_bwd(_linear_dgrad(dy2, w2_16), z)
         dw2, db2 = _wgrad(dy2, h, w2, b2, g[3], b2 is not None and g[4])
         dx = _linear_dgrad(dz, w1_16).reshape(ctx.shape) if g[0] else None
-        dw1, db1 = _wgrad(dz, x2, w1, b1, g[1], b1 is not None and g[2])
-        return dx, dw1, db1, dw2, db2, None, None, None, None
+        dw1, db1_ = _wgrad(dz, x2, w1, b1, g[1], need_b1)
+        return dx, dw1, (db1 if db1_ is None else db1_), dw2, db2, None, None, None, None
 
 
 def _native(module: nn.Linear, x: torch.Tensor) -> bool:

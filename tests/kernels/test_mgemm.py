@@ -192,3 +192,64 @@ def test_mlinear_direct_grad_accumulates(monkeypatch):
     want_w = 1 + g.float().t() @ x.float()
     want_b = 1 + g.float().sum(0)
     assert _rel(m.weight.grad, want_w) < 1e-4 and _rel(m.bias.grad, want_b) < 1e-4
+
+
+@pytest.mark.parametrize("f32", [False, True])
+@pytest.mark.parametrize("direct", [False, True])
+def test_lib_direct_grads_split(monkeypatch, f32, direct):
+    """Library routing: split-K partial products combined by rk_slab_acc straight into the persistent
+    weight.grad (bf16 or fp32 partials), bias gradient by column sums - against fp32 math."""
+    import rocket_amd.ops.linear as lin
+    import rocket_amd.ops.mlinear as ml
+    from rocket_amd.ops.mlinear import MLinear
+
+    monkeypatch.setattr(ml, "MODE", "lib")
+    monkeypatch.setattr(lin, "_WGRAD_F32", f32)
+    torch.manual_seed(6)
+    m = MLinear(384, 768).cuda()
+    if direct:
+        for p in m.parameters():
+            p.grad = torch.full_like(p, 0.5)
+            p._rocket_direct_grad = True
+    x = _r(8192, 384)
+    g = _r(8192, 768)
+    assert lin._wgrad_splits(8192, 768, 384) > 1
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    y.backward(g)
+    base = 0.5 if direct else 0.0
+    want_w = base + g.float().t() @ x.float()
+    want_b = base + g.float().sum(0)
+    assert _rel(m.weight.grad, want_w) < (1e-4 if f32 else 5e-3)
+    assert _rel(m.bias.grad, want_b) < 1e-4
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("splits", [1, 3, 4, 9])
+def test_slab_acc(dt, splits):
+    from rocket_amd.ops import _lib
+
+    part = (torch.randn(splits, 1000, 24, device="cuda")).to(dt)
+    dst = torch.randn(1000, 24, device="cuda")
+    want = dst + part.float().sum(0)
+    _lib.check(_lib.kernels().rk_slab_acc(part.data_ptr(), _lib.dtype_code(part), splits, dst.numel(),
+                                          dst.data_ptr(), 1, _lib.stream_ptr(dst.device)), "rk_slab_acc")
+    torch.testing.assert_close(dst, want, rtol=1e-5, atol=1e-5)
+    _lib.check(_lib.kernels().rk_slab_acc(part.data_ptr(), _lib.dtype_code(part), splits, dst.numel(),
+                                          dst.data_ptr(), 0, _lib.stream_ptr(dst.device)), "rk_slab_acc")
+    torch.testing.assert_close(dst, part.float().sum(0), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N", [(25216, 3072), (300, 136)])
+def test_gelu_bwd_colsum(M, N):
+    from rocket_amd.ops.mlinear import _gelu_bwd_bias
+
+    torch.manual_seed(7)
+    z = _r(M, N, scale=3.0)
+    dh = _r(M, N)
+    b = torch.nn.Parameter(torch.zeros(N, device="cuda"))
+    dz, db = _gelu_bwd_bias(dh, z, b)
+    zr = z.float().requires_grad_()
+    F.gelu(zr).backward(dh.float())
+    assert _rel(dz, zr.grad) < 5e-3
+    assert _rel(db, zr.grad.sum(0)) < 1e-4
