@@ -26,7 +26,19 @@ using namespace rk;
 
 namespace {
 
-enum ConvMode : int { kConvFwd = 0, kConvDgrad = 1, kConvWgrad = 2 };
+enum ConvMode : int { kConvFwd = 0, kConvDgrad = 1, kConvWgrad = 2, kConvDgradS = 3 };
+
+// Strided input gradient, one GEMM per parity class (py, px) of the dX pixels: pixel
+// (2*gi + py, 2*gj + px) receives only the taps r = r0y + 2j, s = r0x + 2l (those with
+// ih + pad - r even), from dY pixel (gi + hoff - j, gj + woff - l) — a stride-1 gather over a
+// (GH x GW) sub-grid with Rv x Sv taps.  The four classes share one launch (interleaved blocks).
+struct DgCls {
+  int M, K;            // N*GH*GW rows, Rv*Sv*Cout reduction
+  int GH, GW, Sv;      // sub-grid, taps per row
+  int r0y, r0x;        // first tap of the class
+  int hoff, woff;      // dY row/col of (gi, gj) at tap (j, l) = (gi + hoff - j, gj + woff - l)
+  int py, px;          // parity of the class's dX pixels
+};
 
 struct ConvGeom {
   int N, H, W, C;        // the gathered tensor (fwd/wgrad: X; dgrad: dY), NHWC
@@ -37,6 +49,13 @@ struct ConvGeom {
   int64_t w_co_stride;   // dgrad: elements between output channels in W (= R*S*Cin)
   float inv_gw, inv_gh;  // 1/GW, 1/GH (pixel decomposition of the wgrad k index)
   float* bnpart;         // forward: per row-tile BatchNorm partials [tiles_m][2][Cout] (tile mean, M2) or null
+  int hoff, woff;        // dgrad: dY pixel of grid pixel (gh, gw) at tap (tr, ts) = (gh + hoff - tr, gw + woff - ts)
+  int dx_h, dx_w;        // strided dgrad: dX extent (the epilogue's pixel map)
+  int w_s;               // strided dgrad: the weight's full kernel width S (tap index r*S + s)
+  int ncls;              // strided dgrad: parity classes in the launch
+  int zero_nb;           // strided dgrad, 1x1 kernel: only class (0, 0) has taps; its tiles also zero
+                         // the three odd-parity neighbours of each of their pixels
+  DgCls cls[4];
 };
 
 // (n, gh, gw) of grid pixel m (exact for m < 2^24 after the correction steps)
@@ -72,9 +91,9 @@ struct GatherRows {
       if (MODE == kConvFwd) {
         h0[i] = gh * cg.stride - cg.pad;
         w0[i] = gw * cg.stride - cg.pad;
-      } else {  // dgrad, stride 1: oh = ih + pad - r
-        h0[i] = gh + cg.pad;
-        w0[i] = gw + cg.pad;
+      } else {  // dgrad (stride 1: hoff = woff = pad; strided: per parity class)
+        h0[i] = gh + cg.hoff;
+        w0[i] = gw + cg.woff;
       }
       coff[i] = (c ^ rswz<BK>(r)) * 8;
     }
@@ -181,8 +200,18 @@ __device__ __forceinline__ void tile_bn_stats(const MArgs& g, const ConvGeom& cg
   }
 }
 
+// dX row of sub-grid pixel m of a strided-dgrad parity class
+struct ClsRow {
+  int GH, GW, H, W, py, px;
+  __device__ __forceinline__ int64_t operator()(int m) const {
+    const int gj = m % GW, t = m / GW;
+    const int gi = t % GH, n = t / GH;
+    return ((int64_t)n * H + 2 * gi + py) * W + 2 * gj + px;
+  }
+};
+
 template <int MODE, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MArgs g, ConvGeom cg) {
+__global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MArgs g, const ConvGeom cg0) {
   constexpr int BK = 64, NS = 2, NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16, KK = BK / 32;
@@ -192,9 +221,27 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
   constexpr bool BKM = MODE != kConvFwd;    // B K-major (dgrad: W per tap; wgrad: gathered X)
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE_BYTES];
 
+  int lin = xcd_remap(blockIdx.x, gridDim.x);
+  ConvGeom cg = cg0;
+  int r0y = 0, r0x = 0;
+  ClsRow crow = {};
+  if constexpr (MODE == kConvDgradS) {  // find this block's parity class; specialise the geometry
+    // constant-index field selects only: a runtime index into the argument struct (or a select of
+    // whole structs) puts the geometry in scratch memory
+    // classes interleaved block by block (class = lin % ncls): every XCD's share of the grid mixes
+    // the heavy classes (most taps) with the light ones (1x1 stride 2: three classes of zeros)
+    const int c = lin % cg0.ncls;
+    lin /= cg0.ncls;
+#define RK_SEL(f) (c == 0 ? cg0.cls[0].f : c == 1 ? cg0.cls[1].f : c == 2 ? cg0.cls[2].f : cg0.cls[3].f)
+    g.M = RK_SEL(M); g.K = RK_SEL(K); g.k_per_split = g.K;
+    cg.GH = RK_SEL(GH); cg.GW = RK_SEL(GW); cg.S = RK_SEL(Sv); cg.hoff = RK_SEL(hoff); cg.woff = RK_SEL(woff);
+    r0y = RK_SEL(r0y); r0x = RK_SEL(r0x);
+    crow = ClsRow{cg.GH, cg.GW, cg0.dx_h, cg0.dx_w, RK_SEL(py), RK_SEL(px)};
+#undef RK_SEL
+  }
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  if (MODE == kConvDgradS && lin >= ntiles) return;  // this class has fewer tiles than the largest
   const int split = lin / ntiles;
   const int tile = lin % ntiles;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
@@ -215,7 +262,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // operand stagers per mode
-  GatherRows<BM, NW, MODE == kConvDgrad ? kConvDgrad : kConvFwd> ga;  // fwd/dgrad A
+  GatherRows<BM, NW, MODE == kConvFwd ? kConvFwd : kConvDgrad> ga;  // fwd/dgrad A
   Stager<BM, BK, true, NW> sa_k;                                      // wgrad A (dY K-major)
   Stager<BN, BK, false, NW> sb_row;                                    // fwd B (W rows)
   Stager<BN, BK, true, NW> sb_k;                                       // dgrad B (W per tap)
@@ -242,9 +289,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
       ga.issue(g.a, cg, tr, ts, c0, buf, wid, zero);
       if constexpr (MODE == kConvFwd)
         sb_row.issue((const char*)g.b + (int64_t)k0 * 2, buf + A_BYTES, wid);
-      else  // W[co][tap][ci]: k-tile rows co = c0.., columns ci
-        sb_k.issue((const char*)g.b + ((int64_t)tap * cg.w_tap_stride + (int64_t)c0 * cg.w_co_stride) * 2,
+      else {  // W[co][tap][ci]: k-tile rows co = c0.., columns ci (strided: the class's tap (j, l))
+        const int wtap = MODE == kConvDgradS ? (r0y + 2 * tr) * cg.w_s + r0x + 2 * ts : tap;
+        sb_k.issue((const char*)g.b + ((int64_t)wtap * cg.w_tap_stride + (int64_t)c0 * cg.w_co_stride) * 2,
                    buf + A_BYTES, wid);
+      }
     }
   };
   FragReader<BM, BK, AK, FM> ra;
@@ -299,22 +348,56 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
     if (cg.bnpart != nullptr) tile_bn_stats<BM, BN, WM, WN, FM, FN>(g, cg, acc, tm, row0, col0, wm, wn, lane);
   }
   const uint2 nos[FM][FN] = {};
-  store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split);
+  if constexpr (MODE == kConvDgradS) {
+    store_tile<FM, FN, false, ClsRow>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split, crow);
+    if (cg0.zero_nb && !g.accumulate) {  // classes without taps: zeros next to this tile's pixels
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = col0 + wn * TN + j * 16 + 4 * (lane >> 4);
+        if (n >= g.N) continue;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int m = row0 + wm * TM + i * 16 + (lane & 15);
+          if (m >= g.M) continue;
+          const int gj = m % crow.GW, t = m / crow.GW;
+          const int gi = t % crow.GH, img = t / crow.GH;
+          const int64_t p0 = ((int64_t)img * crow.H + 2 * gi) * crow.W + 2 * gj;
+          const bool right = 2 * gj + 1 < crow.W, down = 2 * gi + 1 < crow.H;
+          uint16_t* c = (uint16_t*)g.c + n;
+          if (right) *(uint2*)(c + (p0 + 1) * g.ldc) = make_uint2(0u, 0u);
+          if (down) *(uint2*)(c + (p0 + crow.W) * g.ldc) = make_uint2(0u, 0u);
+          if (right && down) *(uint2*)(c + (p0 + crow.W + 1) * g.ldc) = make_uint2(0u, 0u);
+        }
+      }
+    }
+  } else
+    store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split);
+}
+
+// tiles of a launch: one GEMM, or (strided dgrad) the parity classes' GEMMs back to back
+template <int MODE>
+int conv_tiles(const MArgs& g, const ConvGeom& cg, int bm, int bn) {
+  if constexpr (MODE == kConvDgradS) {  // classes interleaved: ncls x the largest class's tiles
+    int t = 0;
+    for (int c = 0; c < cg.ncls; ++c) t = std::max(t, ((cg.cls[c].M + bm - 1) / bm) * ((g.N + bn - 1) / bn));
+    return t * cg.ncls;
+  }
+  return ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn);
 }
 
 template <int MODE>
-int launch_conv(const MArgs& g, const ConvGeom& cg, hipStream_t s) {
+int launch_conv(const MArgs& g, ConvGeom cg, hipStream_t s) {
   // (the forward's wave row slice is 64 pixels in every variant: the BatchNorm partials rely on it)
   // 64-wide GEMM side (Cout / Cin = 64 layers): a 64-wide tile with 4 waves instead of half an
   // empty 128-wide one; everything else 128 x 128 with 8 waves
   if (MODE != kConvWgrad && g.N <= 64) {
-    const int tiles = ((g.M + 127) / 128) * ((g.N + 63) / 64);
+    const int tiles = conv_tiles<MODE>(g, cg, 128, 64);
     conv_kernel<MODE, 128, 64, 2, 2><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
   } else if (MODE == kConvWgrad && g.M <= 64) {
     const int tiles = ((g.M + 63) / 64) * ((g.N + 127) / 128);
     conv_kernel<MODE, 64, 128, 2, 2><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
   } else {
-    const int tiles = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+    const int tiles = conv_tiles<MODE>(g, cg, 128, 128);
     conv_kernel<MODE, 128, 128, 2, 4><<<tiles * g.splitk, 512, 0, s>>>(g, cg);
   }
   return (int)hipGetLastError();
@@ -325,6 +408,7 @@ ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stri
   cg.N = N; cg.H = H; cg.W = W; cg.C = C; cg.GH = GH; cg.GW = GW;
   cg.R = R; cg.S = S; cg.stride = stride; cg.pad = pad; cg.taps_c = taps_c;
   cg.w_tap_stride = 0; cg.w_co_stride = 0; cg.bnpart = nullptr;
+  cg.hoff = cg.woff = pad; cg.dx_h = cg.dx_w = 0; cg.w_s = S; cg.ncls = 0; cg.zero_nb = 0;
   cg.inv_gw = 1.f / (float)GW;
   cg.inv_gh = 1.f / (float)GH;
   return cg;
@@ -358,18 +442,49 @@ RK_API int rk_conv_fwd(const void* x, const void* w, void* y, int y_dt, const fl
   return launch_conv<kConvFwd>(g, cg, s);
 }
 
-// dX[N*H*W][Cin] (bf16/f32) = conv_transpose(dY, W), stride 1 only.  Cout % 64 == 0, Cin % 8 == 0.
-RK_API int rk_conv_dgrad(const void* dy, const void* w, void* dx, int dx_dt, int N, int H, int W, int Cin, int Cout,
-                         int R, int S, int stride, int pad, int OH, int OW, hipStream_t s) {
-  if (stride != 1 || Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx))
+// dX[N*H*W][Cin] (bf16/f32) (+)= conv_transpose(dY, W), stride 1 or 2.  Cout % 64 == 0, Cin % 8 == 0.
+// accumulate: dX += (e.g. the residual-branch gradient already in dX).  Stride 2: the four parity
+// classes of dX pixels as four stride-1 gathers in one launch (classes without taps store zeros).
+RK_API int rk_conv_dgrad(const void* dy, const void* w, void* dx, int dx_dt, int accumulate, int N, int H, int W,
+                         int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, hipStream_t s) {
+  if ((stride != 1 && stride != 2) || Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx))
     return (int)hipErrorInvalidValue;
-  if (OH != H + 2 * pad - R + 1 || OW != W + 2 * pad - S + 1) return (int)hipErrorInvalidValue;
+  if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
   const int M = N * H * W, K = R * S * Cout;
   MArgs g = margs(dy, 0, w, (int64_t)R * S * Cin, dx, dx_dt, Cin, M, Cin, K);
-  ConvGeom cg = geom(N, OH, OW, Cout, H, W, R, S, 1, pad, Cout);
+  g.accumulate = accumulate;
+  ConvGeom cg = geom(N, OH, OW, Cout, H, W, R, S, stride, pad, Cout);
   cg.w_tap_stride = Cin;
   cg.w_co_stride = (int64_t)R * S * Cin;
-  return launch_conv<kConvDgrad>(g, cg, s);
+  if (stride == 1) return launch_conv<kConvDgrad>(g, cg, s);
+  cg.dx_h = H;
+  cg.dx_w = W;
+  cg.ncls = 0;
+  for (int py = 0; py < 2; ++py)
+    for (int px = 0; px < 2; ++px) {
+      DgCls k = {};
+      k.py = py; k.px = px;
+      k.GH = (H - py + 1) / 2;
+      k.GW = (W - px + 1) / 2;
+      k.r0y = (py + pad) & 1;
+      k.r0x = (px + pad) & 1;
+      const int rv = k.r0y < R ? (R - k.r0y + 1) / 2 : 0, sv = k.r0x < S ? (S - k.r0x + 1) / 2 : 0;
+      k.Sv = sv > 0 ? sv : 1;
+      k.hoff = (py + pad - k.r0y) / 2;
+      k.woff = (px + pad - k.r0x) / 2;
+      k.M = N * k.GH * k.GW;
+      k.K = rv * sv * Cout;
+      if (k.M > 0 && k.K > 0) cg.cls[cg.ncls++] = k;
+    }
+  // a 1x1 kernel (pad 0) leaves three classes without taps: class (0, 0)'s tiles zero them (a
+  // tile launch per zero class measured ~3x slower than the whole GEMM)
+  if (R == 1 && S == 1 && pad == 0) {
+    if (cg.ncls != 1 || dx_dt != BF16) return (int)hipErrorInvalidValue;
+    cg.zero_nb = 1;
+  } else if (cg.ncls != 4) {
+    return (int)hipErrorInvalidValue;  // every class must have taps (or be zeroed by its neighbour)
+  }
+  return launch_conv<kConvDgradS>(g, cg, s);
 }
 
 // dW[Cout][R*S*Cin] f32 (+)= dY^T (*) X; split-K over the N*OH*OW pixels into `slab`

@@ -172,9 +172,13 @@ __device__ __forceinline__ void wait_vm(int n) {
 // Epilogue of one wave's FM x FN fragments: lane holds C[m][n..n+3], m = mbase + 16 i + (lane & 15),
 // n = nbase + 16 j + 4 (lane >> 4).  PRE: the side inputs (aux / old bf16 C) were loaded before the
 // main loop into `side`; otherwise they are loaded here.
-template <int FM, int FN, bool PRE>
+struct IdRow {  // GEMM row m is output row m
+  __device__ __forceinline__ int64_t operator()(int m) const { return m; }
+};
+
+template <int FM, int FN, bool PRE, typename RowMap = IdRow>
 __device__ __forceinline__ void store_tile(const MArgs& g, f32x4 (&acc)[FM][FN], const uint2 (&side)[FM][FN],
-                                           int mbase, int nbase, int lane, int split) {
+                                           int mbase, int nbase, int lane, int split, const RowMap& rowmap = RowMap()) {
   if (g.splitk > 1) {  // partial tile -> this split's slab (plain stores; mgemm_reduce combines)
     float* slab = g.slab + (int64_t)split * g.M * g.N;
 #pragma unroll
@@ -200,7 +204,7 @@ __device__ __forceinline__ void store_tile(const MArgs& g, f32x4 (&acc)[FM][FN],
     for (int i = 0; i < FM; ++i) {
       const int m = mbase + i * 16 + (lane & 15);
       if (!nok || m >= g.M) continue;
-      const int64_t off = (int64_t)m * g.ldc + n;
+      const int64_t off = rowmap(m) * g.ldc + n;
       float v[4] = {acc[i][j][0] + bias.x, acc[i][j][1] + bias.y, acc[i][j][2] + bias.z, acc[i][j][3] + bias.w};
       if (g.epi == kGelu || g.epi == kRelu) {
         if (g.c_pre) {

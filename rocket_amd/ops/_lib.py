@@ -43,7 +43,7 @@ KERNEL_SIGS = {
     "rk_conv_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 11 + [c_void_p, c_void_p]),
     "rk_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_int64, c_int] + [c_void_p] * 9 + [c_float, c_float, c_void_p,
                                                                                             c_void_p, c_void_p]),
-    "rk_conv_dgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_int] + [c_int] * 11 + [c_void_p]),
+    "rk_conv_dgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_int] * 11 + [c_void_p]),
     "rk_conv_wgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p, c_void_p]),
     "rk_conv_pool_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 7 + [c_void_p]),
     "rk_conv_pool_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),

@@ -7,8 +7,8 @@ split-K combine of the weight gradient) — no im2col buffer, no MIOpen solution
 
 * forward: gathered NHWC activations x channels_last weights (read as a bf16 copy a fused
   optimizer keeps current: dense bf16 shadow, ``_bf16_copy``);
-* dgrad (stride 1): dY gathered with the flipped taps x the weights read K-major per tap;
-  strided convs take the library path for their input gradient;
+* dgrad: dY gathered with the flipped taps x the weights read K-major per tap; stride 2 as the
+  four parity classes of dX pixels (each a stride-1 gather over its taps) in one launch;
 * wgrad: dY x gathered X, split-K over the pixels into f32 slabs, accumulated straight into a
   persistent ``weight.grad`` when the engine provides one.
 
@@ -30,6 +30,8 @@ from rocket_amd.ops.linear import _autocast_on, _bf16_copy, _direct, grad_ready
 from rocket_amd.ops.mgemm import _slab
 
 MODE = os.environ.get("ROCKET_CONV", "native")
+# strided (stride-2) input gradients: native parity-class launch or the library
+SDGRAD = os.environ.get("ROCKET_CONV_SDGRAD", "native")
 N_SLOTS = 512  # resident 128x128 conv blocks (2 per CU)
 
 
@@ -57,6 +59,12 @@ def _wgrad_split(cout: int, ncol: int, pixels: int) -> int:
         if best is None or c < best:
             best, arg = c, s
     return arg
+
+
+def _sdgrad_ok(R: int, S: int, pad: int) -> bool:
+    # every parity class of a stride-2 input gradient needs taps, except the 1x1 / pad-0 case whose
+    # three empty classes the (0, 0) tiles zero themselves
+    return (R > 1 and S > 1) or (R == 1 and S == 1 and pad == 0)
 
 
 TILE_ROWS = 64  # rows per wave slice of every conv.hip forward variant (BatchNorm partials granularity)
@@ -89,10 +97,10 @@ class _IConvFn(torch.autograd.Function):
         st = _lib.stream_ptr(dy.device)
         dx = None
         if ctx.needs_input_grad[0]:
-            if stride == 1 and Co % 64 == 0:
+            if (stride == 1 or (stride == 2 and SDGRAD == "native" and _sdgrad_ok(R, S, pad))) and Co % 64 == 0:
                 dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dy.device, memory_format=torch.channels_last)
-                _lib.check(lib.rk_conv_dgrad(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), 1, N, H, W, C, Co, R, S,
-                                             stride, pad, OH, OW, st), "rk_conv_dgrad")
+                _lib.check(lib.rk_conv_dgrad(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), 1, 0, N, H, W, C, Co, R,
+                                             S, stride, pad, OH, OW, st), "rk_conv_dgrad")
             else:
                 dx = torch.nn.grad.conv2d_input((N, C, H, W), w16, dyc, stride=stride, padding=pad)
         dw = None

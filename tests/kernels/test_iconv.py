@@ -19,6 +19,8 @@ SHAPES = [
     # ResNet-18 CIFAR (32x32)
     (8, 64, 32, 32, 64, 3, 1), (8, 64, 32, 32, 128, 3, 2), (8, 128, 16, 16, 128, 3, 1), (8, 256, 8, 8, 256, 3, 1),
     (8, 256, 4, 4, 512, 1, 2), (8, 512, 4, 4, 512, 3, 1),
+    # strided input gradients on odd extents / wider kernels (parity classes of unequal size)
+    (2, 64, 15, 15, 128, 3, 2), (2, 64, 15, 13, 128, 1, 2), (2, 64, 9, 11, 64, 7, 2), (2, 128, 7, 7, 64, 5, 2),
 ]
 
 
@@ -88,3 +90,23 @@ def test_conv_emitted_bn_stats_match_bn(N, Cin, H, W, Cout, k, stride):
     assert _rel(out, want) < 1e-2, _rel(out, want)
     torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("k,stride", [(3, 1), (3, 2), (1, 2)])
+def test_conv_dgrad_accumulate(k, stride):
+    """rk_conv_dgrad with accumulate=1 adds the input gradient onto what dX already holds (the
+    residual-branch gradient of a ResNet block entry)."""
+    from rocket_amd.ops import _lib
+
+    torch.manual_seed(1)
+    N, C, H, W, Co = 2, 64, 14, 14, 128
+    pad = k // 2
+    OH = (H + 2 * pad - k) // stride + 1
+    w = torch.randn(Co, C, k, k, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, Co, OH, OH, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    base = torch.randn(N, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dx = base.clone()
+    _lib.check(_lib.kernels().rk_conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 1, 1, N, H, W, C, Co, k, k,
+                                            stride, pad, OH, OH, _lib.stream_ptr(dy.device)), "rk_conv_dgrad")
+    want = base.float() + torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), stride=stride, padding=pad)
+    assert _rel(dx, want) < 1e-2
