@@ -5,7 +5,9 @@ convolutions (:class:`~rocket_amd.ops.iconv.IConv2d`, ``native/kernels/conv.hip`
 pixels straight into LDS and the fused BatchNorm kernels (:mod:`rocket_amd.ops.norm`) reduce over
 contiguous channels.  Every ``conv → BN (→ +identity) → ReLU`` tail is
 one BN-statistics launch plus one fused apply launch (``BatchNormAct2d``), so the
-residual add and the ReLU never make their own pass over HBM.
+residual add and the ReLU never make their own pass over HBM; a block's first conv and its
+shortcut form one autograd node (:func:`~rocket_amd.ops.iconv.conv_entry`), so the two gradients
+of the block input meet in a conv epilogue instead of an add kernel.
 
 The forward follows the reference batch contract: ``(img, label) -> (img, label, logits)``.
 Architecture per He et al. (basic/bottleneck blocks, stride on the 3×3 conv as in
@@ -20,7 +22,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from rocket_amd.ops.iconv import IConv2d
+from rocket_amd.ops.iconv import IConv2d, conv_entry
 from rocket_amd.ops.norm import BatchNormAct2d
 
 
@@ -47,8 +49,10 @@ class BasicBlock(nn.Module):
             self.down = nn.Sequential(_conv(cin, cout, 1, stride), BatchNormAct2d(cout))
 
     def forward(self, x):
-        identity = x if self.down is None else self.down(x)
-        out = self.bn1(self.conv1(x))
+        # conv1 and the shortcut as one node: x's two input gradients meet in conv1's dgrad epilogue
+        y1, short = conv_entry(x, self.conv1, self.down[0] if self.down is not None else None)
+        identity = short if self.down is None else self.down[1](short)
+        out = self.bn1(y1)
         return self.bn2(self.conv2(out), residual=identity)
 
 
@@ -69,8 +73,9 @@ class Bottleneck(nn.Module):
             self.down = nn.Sequential(_conv(cin, cout, 1, stride), BatchNormAct2d(cout))
 
     def forward(self, x):
-        identity = x if self.down is None else self.down(x)
-        out = self.bn1(self.conv1(x))
+        y1, short = conv_entry(x, self.conv1, self.down[0] if self.down is not None else None)
+        identity = short if self.down is None else self.down[1](short)
+        out = self.bn1(y1)
         out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out), residual=identity)
 

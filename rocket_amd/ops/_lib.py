@@ -160,9 +160,21 @@ def stream_ptr(device=None) -> int:
     return _raw_stream(device.index if device.index is not None else torch.cuda.current_device())
 
 
+# Serialised debug mode: ROCKET_DEBUG_SYNC=1 synchronises the device after every
+# native launch outside graph capture, so an asynchronous fault (out-of-bounds access, failed
+# assertion in a kernel) is reported at the launch that caused it, by name.  runtime/hipenv.py also
+# turns on the runtime's own kernel serialisation for that mode.
+DEBUG_SYNC = os.environ.get("ROCKET_DEBUG_SYNC", "0") == "1"
+
+
 def check(code: int, what: str) -> None:
     if code != 0:
         raise NativeError(f"{what} failed with hipError {code}")
+    if DEBUG_SYNC and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # the fault surfaced here: name the launch
+            raise NativeError(f"{what}: device error after launch (ROCKET_DEBUG_SYNC): {e}") from e
 
 
 def ptr(t) -> int | None:

@@ -32,6 +32,8 @@ from rocket_amd.ops.mgemm import _slab
 MODE = os.environ.get("ROCKET_CONV", "native")
 # strided (stride-2) input gradients: native parity-class launch or the library
 SDGRAD = os.environ.get("ROCKET_CONV_SDGRAD", "native")
+# residual-block entries (first conv + shortcut) as one autograd node: ROCKET_CONV_ENTRY=0 disables
+ENTRY = os.environ.get("ROCKET_CONV_ENTRY", "1") != "0"
 N_SLOTS = 512  # resident 128x128 conv blocks (2 per CU)
 
 
@@ -70,54 +72,116 @@ def _sdgrad_ok(R: int, S: int, pad: int) -> bool:
 TILE_ROWS = 64  # rows per wave slice of every conv.hip forward variant (BatchNorm partials granularity)
 
 
+def _conv_fwd(xc: torch.Tensor, w16: torch.Tensor, stride: int, pad: int, bnpart) -> torch.Tensor:
+    N, C, H, W = xc.shape
+    Co, _, R, S = w16.shape
+    OH = (H + 2 * pad - R) // stride + 1
+    OW = (W + 2 * pad - S) // stride + 1
+    y = torch.empty((N, Co, OH, OW), dtype=torch.bfloat16, device=xc.device, memory_format=torch.channels_last)
+    _lib.check(_lib.kernels().rk_conv_fwd(xc.data_ptr(), w16.data_ptr(), y.data_ptr(), 1, None, N, H, W, C, Co, R, S,
+                                           stride, pad, OH, OW, _lib.ptr(bnpart), _lib.stream_ptr(xc.device)),
+               "rk_conv_fwd")
+    return y
+
+
+def _geo(xc: torch.Tensor, w16: torch.Tensor, stride: int, pad: int):
+    N, C, H, W = xc.shape
+    Co, _, R, S = w16.shape
+    return (N, C, H, W, Co, R, S, stride, pad, (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1)
+
+
+def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | None) -> torch.Tensor:
+    """Input gradient of one conv; with ``dx`` given it is ADDED to dx (in place, native epilogue
+    accumulate) and dx is returned."""
+    N, C, H, W, Co, R, S, stride, pad, OH, OW = geo
+    if (stride == 1 or (stride == 2 and SDGRAD == "native" and _sdgrad_ok(R, S, pad))) and Co % 64 == 0:
+        acc = dx is not None
+        if dx is None:
+            dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
+        _lib.check(_lib.kernels().rk_conv_dgrad(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), 1, int(acc), N, H, W,
+                                                C, Co, R, S, stride, pad, OH, OW, _lib.stream_ptr(dyc.device)),
+                   "rk_conv_dgrad")
+        return dx
+    g = torch.nn.grad.conv2d_input((N, C, H, W), w16, dyc, stride=stride, padding=pad)
+    return g if dx is None else dx.add_(g)
+
+
+def _conv_wgrad(dyc: torch.Tensor, xc: torch.Tensor, weight: torch.Tensor, geo):
+    """Weight gradient, accumulated straight into a persistent ``weight.grad`` when the engine
+    provides one (returns None then), else returned."""
+    N, C, H, W, Co, R, S, stride, pad, OH, OW = geo
+    direct = _direct(weight) and weight.grad.is_contiguous(memory_format=torch.channels_last)
+    target = weight.grad if direct else torch.empty(weight.shape, dtype=torch.float32, device=dyc.device,
+                                                    memory_format=torch.channels_last)
+    P, ncol = N * OH * OW, R * S * C
+    split = _wgrad_split(Co, ncol, P)
+    slab = _slab(dyc.device, split * Co * ncol) if split > 1 else None
+    _lib.check(_lib.kernels().rk_conv_wgrad(dyc.data_ptr(), xc.data_ptr(), target.data_ptr(), int(direct), None, N, H,
+                                            W, C, Co, R, S, stride, pad, OH, OW, split, _lib.ptr(slab),
+                                            _lib.stream_ptr(dyc.device)), "rk_conv_wgrad")
+    if direct:
+        grad_ready(weight)
+        return None
+    return target
+
+
 class _IConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, w16, stride: int, pad: int, bnpart):
         xc = _cl(x)
-        N, C, H, W = xc.shape
-        Co, _, R, S = w16.shape
-        OH = (H + 2 * pad - R) // stride + 1
-        OW = (W + 2 * pad - S) // stride + 1
-        y = torch.empty((N, Co, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-        _lib.check(_lib.kernels().rk_conv_fwd(xc.data_ptr(), w16.data_ptr(), y.data_ptr(), 1, None, N, H, W, C, Co, R, S,
-                                               stride, pad, OH, OW, _lib.ptr(bnpart), _lib.stream_ptr(x.device)),
-                   "rk_conv_fwd")
+        y = _conv_fwd(xc, w16, stride, pad, bnpart)
         ctx.save_for_backward(xc, w16)
         ctx.weight = weight
-        ctx.geo = (N, C, H, W, Co, R, S, stride, pad, OH, OW)
+        ctx.geo = _geo(xc, w16, stride, pad)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         xc, w16 = ctx.saved_tensors
-        weight = ctx.weight
-        N, C, H, W, Co, R, S, stride, pad, OH, OW = ctx.geo
         dyc = _cl(dy)
-        lib = _lib.kernels()
-        st = _lib.stream_ptr(dy.device)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            if (stride == 1 or (stride == 2 and SDGRAD == "native" and _sdgrad_ok(R, S, pad))) and Co % 64 == 0:
-                dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dy.device, memory_format=torch.channels_last)
-                _lib.check(lib.rk_conv_dgrad(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), 1, 0, N, H, W, C, Co, R,
-                                             S, stride, pad, OH, OW, st), "rk_conv_dgrad")
-            else:
-                dx = torch.nn.grad.conv2d_input((N, C, H, W), w16, dyc, stride=stride, padding=pad)
-        dw = None
-        if ctx.needs_input_grad[1]:
-            direct = _direct(weight) and weight.grad.is_contiguous(memory_format=torch.channels_last)
-            target = weight.grad if direct else torch.empty(weight.shape, dtype=torch.float32, device=dy.device,
-                                                            memory_format=torch.channels_last)
-            P, ncol = N * OH * OW, R * S * C
-            split = _wgrad_split(Co, ncol, P)
-            slab = _slab(dy.device, split * Co * ncol) if split > 1 else None
-            _lib.check(lib.rk_conv_wgrad(dyc.data_ptr(), xc.data_ptr(), target.data_ptr(), int(direct), None, N, H, W,
-                                         C, Co, R, S, stride, pad, OH, OW, split, _lib.ptr(slab), st), "rk_conv_wgrad")
-            if direct:
-                grad_ready(weight)
-            else:
-                dw = target
+        dx = _conv_dgrad(dyc, w16, ctx.geo, None) if ctx.needs_input_grad[0] else None
+        dw = _conv_wgrad(dyc, xc, ctx.weight, ctx.geo) if ctx.needs_input_grad[1] else None
         return dx, dw, None, None, None, None
+
+
+class _EntryFn(torch.autograd.Function):
+    """A residual block's entry: ``(conv_a(x), conv_b(x) or x)`` as ONE autograd node.
+
+    x feeds the block's first conv and its shortcut (identity or downsample conv).  As separate
+    nodes autograd would sum the two input gradients with an add kernel over x; here the backward
+    gets both output gradients at once and the second input gradient is accumulated by the conv
+    dgrad epilogue into the first (the shortcut's gradient for an identity)."""
+
+    @staticmethod
+    def forward(ctx, x, wa, wa16, sa, pa, parta, wb, wb16, sb, pb, partb):
+        xc = _cl(x)
+        ya = _conv_fwd(xc, wa16, sa, pa, parta)
+        yb = _conv_fwd(xc, wb16, sb, pb, partb) if wb is not None else xc.view_as(xc)
+        ctx.save_for_backward(xc, wa16, wb16 if wb is not None else None)
+        ctx.weights = (wa, wb)
+        ctx.geo = (_geo(xc, wa16, sa, pa), _geo(xc, wb16, sb, pb) if wb is not None else None)
+        return ya, yb
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        xc, wa16, wb16 = ctx.saved_tensors
+        wa, wb = ctx.weights
+        geo_a, geo_b = ctx.geo
+        need = ctx.needs_input_grad
+        dx = None
+        gac = _cl(ga) if ga is not None else None
+        gbc = _cl(gb) if gb is not None else None
+        if need[0]:
+            if gbc is not None:
+                # shortcut first: downsample dgrad into a fresh dx / the identity's gradient as dx
+                dx = _conv_dgrad(gbc, wb16, geo_b, None) if wb is not None else gbc
+            if gac is not None:
+                dx = _conv_dgrad(gac, wa16, geo_a, dx)
+            if dx is None:
+                dx = torch.zeros_like(xc)
+        dwa = _conv_wgrad(gac, xc, wa, geo_a) if need[1] and gac is not None else None
+        dwb = _conv_wgrad(gbc, xc, wb, geo_b) if wb is not None and need[6] and gbc is not None else None
+        return dx, dwa, None, None, None, None, dwb, None, None, None, None
 
 
 def native_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -138,24 +202,52 @@ class IConv2d(nn.Conv2d):
 
     emit_bn_stats = False
 
+    def _prep(self, x):
+        """(bf16 weight copy, BN partials buffer or None) for a native forward."""
+        if not self.weight.is_contiguous(memory_format=torch.channels_last):
+            with torch.no_grad():
+                self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
+        w16 = _bf16_copy(self, "_w16", self.weight)
+        part = None
+        if self.emit_bn_stats:
+            N, _, H, W = x.shape
+            OH = (H + 2 * self.padding[0] - self.kernel_size[0]) // self.stride[0] + 1
+            OW = (W + 2 * self.padding[1] - self.kernel_size[1]) // self.stride[1] + 1
+            ntiles = -(-(N * OH * OW) // TILE_ROWS)
+            part = torch.empty(ntiles * 2 * self.out_channels, dtype=torch.float32, device=x.device)
+        return w16, part
+
+    def _attach(self, y, part):
+        if part is not None:
+            y._rocket_bn_partials = (part, part.numel() // (2 * self.out_channels), TILE_ROWS)
+        return y
+
     def forward(self, x):
         if native_ok(self, x):
-            if not self.weight.is_contiguous(memory_format=torch.channels_last):
-                with torch.no_grad():
-                    self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
-            w16 = _bf16_copy(self, "_w16", self.weight)
-            part = None
-            if self.emit_bn_stats:
-                N, _, H, W = x.shape
-                OH = (H + 2 * self.padding[0] - self.kernel_size[0]) // self.stride[0] + 1
-                OW = (W + 2 * self.padding[1] - self.kernel_size[1]) // self.stride[1] + 1
-                ntiles = -(-(N * OH * OW) // TILE_ROWS)
-                part = torch.empty(ntiles * 2 * self.out_channels, dtype=torch.float32, device=x.device)
-            y = _IConvFn.apply(x, self.weight, w16, self.stride[0], self.padding[0], part)
-            if part is not None:
-                y._rocket_bn_partials = (part, part.numel() // (2 * self.out_channels), TILE_ROWS)
-            return y
+            w16, part = self._prep(x)
+            return self._attach(_IConvFn.apply(x, self.weight, w16, self.stride[0], self.padding[0], part), part)
         return super().forward(x)
+
+
+def conv_entry(x: torch.Tensor, conv_a: nn.Conv2d, conv_b: nn.Conv2d | None):
+    """``(conv_a(x), conv_b(x) if conv_b else x)`` - a residual block's first conv and its shortcut -
+    as one autograd node (:class:`_EntryFn`: no add kernel for x's two input gradients), when both
+    convs run natively; otherwise the plain modules."""
+    if (ENTRY and isinstance(conv_a, IConv2d) and native_ok(conv_a, x)
+            and (conv_b is None or (isinstance(conv_b, IConv2d) and native_ok(conv_b, x)))):
+        wa16, pa = conv_a._prep(x)
+        wb16 = pb = None
+        if conv_b is not None:
+            wb16, pb = conv_b._prep(x)
+        ya, yb = _EntryFn.apply(x, conv_a.weight, wa16, conv_a.stride[0], conv_a.padding[0], pa,
+                                conv_b.weight if conv_b is not None else None, wb16,
+                                conv_b.stride[0] if conv_b is not None else 1,
+                                conv_b.padding[0] if conv_b is not None else 0, pb)
+        conv_a._attach(ya, pa)
+        if conv_b is not None:
+            conv_b._attach(yb, pb)
+        return ya, yb
+    return conv_a(x), (conv_b(x) if conv_b is not None else x)
 
 
 def conv2d_reference(x, w, stride, pad):

@@ -38,6 +38,8 @@ of :mod:`rocket_amd.parallel.p2p` — stream-ordered and graph-capturable (``cap
 
 from __future__ import annotations
 
+import os
+
 import contextlib
 from typing import Dict, List, Optional
 
@@ -137,6 +139,8 @@ class DataParallel(nn.Module):
         self._armed = False
         self._deferred = False
         self._reduces = 0
+        self._debug = os.environ.get("ROCKET_DEBUG_SYNC", "0") == "1"
+        self._launched: List[int] = []
         # native transport: per-bucket all-reduce on a side stream, one join before the optimizer
         self._native = self.comm.make_reducer([b.flat for b in self.buckets]) if hasattr(self.comm, "make_reducer") else None
         # small models: one-shot xGMI all-reduce kernel (graph-capturable) instead of RCCL
@@ -311,6 +315,7 @@ class DataParallel(nn.Module):
 
     def reduce_now(self) -> None:
         """Average every bucket (incl. the side channel) across ranks; stream-ordered, no host wait."""
+        self._launched = []
         works = [self._launch(b) for b in self.buckets]
         if self._native is not None:
             self._native.join()
@@ -333,6 +338,25 @@ class DataParallel(nn.Module):
             b.work = None
         self._armed = True
         self._finalize_queued = False
+        self._launched = []
+        if self._debug and torch.cuda.is_available() and self.buckets and self.buckets[0].flat.is_cuda:
+            self._stream0 = torch.cuda.current_stream(self.buckets[0].flat.device)
+
+    def _debug_check_launch(self, b: _Bucket) -> None:
+        """ROCKET_DEBUG_SYNC=1 stream-ordering / bucket assertions: a bucket is
+        reduced once per sync step, only after every gradient in it was written into its flat
+        view, on the stream the backward ran on (the side-stream reducer forks from it)."""
+        if b.index in self._launched:
+            raise RuntimeError(f"DDP debug: bucket {b.index} reduced twice in one step")
+        for i, p in enumerate(b.params):
+            if p.grad is not None and p.grad.data_ptr() != b.view(i).data_ptr():
+                raise RuntimeError(f"DDP debug: bucket {b.index} param {i} gradient is not its flat view")
+        if self._armed and b.pending != 0:
+            raise RuntimeError(f"DDP debug: bucket {b.index} launched with {b.pending} gradients outstanding")
+        s0 = getattr(self, "_stream0", None)
+        if s0 is not None and torch.cuda.current_stream(b.flat.device) != s0:
+            raise RuntimeError(f"DDP debug: bucket {b.index} launched on a different stream than backward")
+        self._launched.append(b.index)
 
     def _on_grad(self, p: nn.Parameter) -> None:
         b, i = self._slot[id(p)]
@@ -370,6 +394,8 @@ class DataParallel(nn.Module):
                             b.view(i).zero_()
                             b.params[i].grad = b.view(i)
                 b.work = self._launch(b)
+        if self._debug and sorted(self._launched) != list(range(len(self.buckets))):
+            raise RuntimeError(f"DDP debug: buckets reduced this step {self._launched} != all {len(self.buckets)}")
         for b in self.buckets:
             b.touched.clear()  # the accumulation window ends with this reduction
         if self._native is not None:
@@ -380,6 +406,8 @@ class DataParallel(nn.Module):
                 b.work = None
 
     def _launch(self, b: _Bucket):
+        if self._debug:
+            self._debug_check_launch(b)
         if self._p2p is not None:
             self._p2p.all_reduce_(b.flat, 1.0 / self.comm.world)
             return _ISSUED

@@ -10,6 +10,11 @@ headline: 5 kernels, ~60 µs of GPU work) is GPU-bound, so the per-node submissi
 measured on 1x MI355X, LeNet bs1024 0.0672 -> 0.0630 ms/step (15.2M -> 16.2M samples/s, two
 alternating A/B runs each, ``scripts/gpu_envprobe2.sh``; ``profiles/r1_hip_env_ab.md``).  The
 host pays ~5 µs more per replay, still below the GPU step time.
+
+``ROCKET_DEBUG_SYNC=1`` (serialised debug mode) additionally sets
+``AMD_SERIALIZE_KERNEL=3`` / ``AMD_SERIALIZE_COPY=3`` (the runtime waits for every kernel and copy
+before the next) and ``HIP_LAUNCH_BLOCKING=1``; ``ops/_lib.check`` then synchronises after each
+native launch, so a fault is attributed to the launch that caused it.
 """
 
 import os
@@ -19,7 +24,17 @@ DEFAULTS = {
 }
 
 
+DEBUG = {
+    "AMD_SERIALIZE_KERNEL": "3",
+    "AMD_SERIALIZE_COPY": "3",
+    "HIP_LAUNCH_BLOCKING": "1",
+}
+
+
 def apply() -> None:
+    if os.environ.get("ROCKET_DEBUG_SYNC", "0") == "1":
+        for k, v in DEBUG.items():
+            os.environ.setdefault(k, v)
     if os.environ.get("ROCKET_HIP_DEFAULTS", "1") == "0":
         return
     for k, v in DEFAULTS.items():

@@ -328,3 +328,44 @@ def test_bn_buffers_single_flat_broadcast(tmp_path):
     # rank 0's statistics moved away from the init values (updates go through the views) and the
     # counters count every training forward on rank 0 (3) -- broadcast and in-place updates compose
     assert b0[2] == 3 and b0[0] != [0.0] * 4
+
+
+def _debug_worker(rank, world, port, out):
+    os.environ["ROCKET_DEBUG_SYNC"] = "1"
+    _reducer_worker(rank, world, port, out)
+
+
+def test_reducer_debug_assertions(tmp_path):
+    """ROCKET_DEBUG_SYNC=1: the reducer's bucket / stream-ordering assertions hold on a correct
+    multi-bucket run (W=2 gloo) and the result is unchanged."""
+    _run(_debug_worker, 2, str(tmp_path))
+    got = [json.load(open(tmp_path / f"g{r}.json")) for r in range(2)]
+    assert got[0]["nb"] > 1 and got[0]["grads"] == got[1]["grads"]
+
+
+def test_reducer_debug_detects_double_launch():
+    from rocket_amd.parallel.ddp import DataParallel
+
+    class _Comm:
+        rank, world = 0, 1
+
+        def all_reduce_avg(self, flat):
+            class _W:
+                def wait(self):
+                    pass
+
+            return _W()
+
+        def broadcast(self, t, src=0):
+            return None
+
+    os.environ["ROCKET_DEBUG_SYNC"] = "1"
+    try:
+        dp = DataParallel(torch.nn.Linear(4, 4), comm=_Comm())
+    finally:
+        os.environ.pop("ROCKET_DEBUG_SYNC")
+    dp(torch.randn(2, 4)).sum().backward()
+    b = dp.buckets[0]
+    dp._launched = [b.index]
+    with pytest.raises(RuntimeError, match="reduced twice"):
+        dp._launch(b)

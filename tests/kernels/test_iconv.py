@@ -110,3 +110,33 @@ def test_conv_dgrad_accumulate(k, stride):
                                             stride, pad, OH, OH, _lib.stream_ptr(dy.device)), "rk_conv_dgrad")
     want = base.float() + torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), stride=stride, padding=pad)
     assert _rel(dx, want) < 1e-2
+
+
+@pytest.mark.parametrize("kind,cin,width,stride", [("bottleneck", 256, 64, 1), ("bottleneck", 256, 128, 2),
+                                                   ("basic", 64, 64, 1), ("basic", 64, 128, 2)])
+def test_block_entry_matches_separate(monkeypatch, kind, cin, width, stride):
+    """A residual block whose first conv + shortcut form one autograd node (_EntryFn) has the same
+    gradients as with separate nodes (autograd's add of the two input gradients)."""
+    import rocket_amd.ops.iconv as ic
+    from rocket_amd.models.resnet import BasicBlock, Bottleneck
+
+    torch.manual_seed(2)
+    blk = (Bottleneck if kind == "bottleneck" else BasicBlock)(cin, width, stride).cuda()
+    blk = blk.to(memory_format=torch.channels_last)
+    x0 = torch.randn(4, cin, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for entry in (True, False):
+        monkeypatch.setattr(ic, "ENTRY", entry)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = blk(x)
+        torch.manual_seed(3)
+        g = torch.randn(y.shape, device="cuda").to(y.dtype).contiguous(memory_format=torch.channels_last)
+        y.backward(g)
+        outs.append((y.detach().float(), x.grad.float(), [p.grad.float().clone() for p in blk.parameters()]))
+    (y1, dx1, g1), (y2, dx2, g2) = outs
+    assert _rel(y1, y2) < 1e-3
+    assert _rel(dx1, dx2) < 1e-2, _rel(dx1, dx2)
+    for a, b in zip(g1, g2):
+        assert _rel(a, b) < 1e-2
