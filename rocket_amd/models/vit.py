@@ -22,6 +22,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops.activation import attention_qkv
+from rocket_amd.ops.linear import PatchEmbed
 from rocket_amd.ops.mlinear import MLinear, MMlp
 from rocket_amd.ops.norm import FusedLayerNorm
 
@@ -59,7 +60,7 @@ class VisionTransformer(nn.Module):
                  mlp_ratio=4.0):
         super().__init__()
         self.patch = patch
-        self.patch_embed = nn.Conv2d(in_chans, dim, patch, stride=patch)
+        self.patch_embed = PatchEmbed(in_chans, dim, patch)  # conv k=16/s=16 as patchify + one GEMM
         n = (img_size // patch) ** 2
         self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
         self.pos_embed = nn.Parameter(torch.zeros(1, n + 1, dim))
@@ -76,7 +77,7 @@ class VisionTransformer(nn.Module):
     def logits(self, x):
         if not torch.is_autocast_enabled(x.device.type):
             x = x.to(self.fc.weight.dtype if hasattr(self, "fc") else self.head.weight.dtype)  # bf16-stored images
-        x = self.patch_embed(x).flatten(2).transpose(1, 2)  # [B, 196, D]
+        x = self.patch_embed(x)  # [B, 196, D]
         x = torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1)
         x = x.float() + self.pos_embed  # fp32 residual stream
         pending = None

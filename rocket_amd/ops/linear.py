@@ -319,3 +319,64 @@ class LibLinear(torch.nn.Linear):
                 b16 = _bf16_copy(self, "_b16", self.bias)
             return _LibLinear.apply(x, self.weight, self.bias, cdtype, w16, b16)
         return super().forward(x)
+
+
+class _PatchEmbedFn(torch.autograd.Function):
+    """Non-overlapping patch embedding (conv with stride == kernel) as patchify + ONE library GEMM:
+    the im2col of a stride-k / kernel-k conv is a pure permutation of the image (no duplication), so
+    the conv is ``patches [B*P, C*k*k] @ W^T + b``.  Backward: weight/bias gradients only (the image
+    takes no gradient), straight into persistent grads."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, w16, b16, k):
+        B, C, H, W = x.shape
+        gh, gw = H // k, W // k
+        p = x.to(torch.bfloat16).reshape(B, C, gh, k, gw, k).permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * k * k)
+        y = torch.addmm(b16, p, w16.reshape(w16.shape[0], -1).t())
+        ctx.save_for_backward(p)
+        ctx.params = (weight, bias)
+        return y.view(B, gh * gw, -1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (p,) = ctx.saved_tensors
+        weight, bias = ctx.params
+        N = weight.shape[0]
+        dy2 = dy.reshape(-1, N)
+        if dy2.dtype != torch.bfloat16:
+            dy2 = dy2.to(torch.bfloat16)
+        dy2 = dy2.contiguous()
+        w2 = _FlatParam(weight)
+        dw, db = lib_param_grads(dy2, p, w2, bias, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        return None, (dw.view_as(weight) if dw is not None else None), db, None, None, None
+
+
+class _FlatParam:
+    """A [N, K] view of a conv weight (and of its persistent grad) for :func:`lib_param_grads`."""
+
+    def __init__(self, p: torch.Tensor):
+        self._p = p
+        self.grad = p.grad.view(p.shape[0], -1) if p.grad is not None else None
+        self._rocket_direct_grad = getattr(p, "_rocket_direct_grad", False)
+        hook = getattr(p, "_rocket_grad_hook", None)
+        if hook is not None:
+            self._rocket_grad_hook = lambda _q: hook(p)
+
+
+class PatchEmbed(torch.nn.Conv2d):
+    """``nn.Conv2d(C, D, k, stride=k)`` (same parameters / state_dict) whose forward under bf16
+    autocast on a HIP device returns the token matrix ``[B, (H/k)*(W/k), D]`` from one patchify
+    copy + one library GEMM (:class:`_PatchEmbedFn`); elsewhere ``conv(x).flatten(2).transpose(1, 2)``."""
+
+    def __init__(self, in_chans: int, dim: int, patch: int):
+        super().__init__(in_chans, dim, patch, stride=patch)
+
+    def forward(self, x):
+        k = self.kernel_size[0]
+        if (x.is_cuda and _autocast_on() and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.dim() == 4
+                and x.shape[2] % k == 0 and x.shape[3] % k == 0 and self.weight.is_contiguous()
+                and self.weight.dtype == torch.float32):
+            w16 = _bf16_copy(self, "_w16", self.weight)
+            b16 = _bf16_copy(self, "_b16", self.bias)
+            return _PatchEmbedFn.apply(x, self.weight, self.bias, w16, b16, k)
+        return super().forward(x).flatten(2).transpose(1, 2)

@@ -253,3 +253,32 @@ def test_gelu_bwd_colsum(M, N):
     F.gelu(zr).backward(dh.float())
     assert _rel(dz, zr.grad) < 5e-3
     assert _rel(db, zr.grad.sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("direct", [False, True])
+def test_patch_embed_matches_conv(direct):
+    """ViT patch embedding as patchify + library GEMM vs an fp32 nn.Conv2d on the same bf16 weights."""
+    from rocket_amd.ops.linear import PatchEmbed
+
+    torch.manual_seed(8)
+    pe = PatchEmbed(3, 768, 16).cuda()
+    ref = torch.nn.Conv2d(3, 768, 16, stride=16).cuda()
+    ref.load_state_dict(pe.state_dict())
+    with torch.no_grad():
+        ref.weight.copy_(ref.weight.to(torch.bfloat16).float())
+    if direct:
+        for p in pe.parameters():
+            p.grad = torch.full_like(p, 0.25)
+            p._rocket_direct_grad = True
+    x = torch.randn(4, 3, 224, 224, device="cuda").to(torch.bfloat16)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = pe(x)
+    assert y.shape == (4, 196, 768)
+    g = _r(4, 196, 768)
+    y.backward(g)
+    yr = ref(x.float()).flatten(2).transpose(1, 2)
+    yr.backward(g.float())
+    base = 0.25 if direct else 0.0
+    assert _rel(y, yr) < 1e-2
+    assert _rel(pe.weight.grad - base, ref.weight.grad) < 1e-2
+    assert _rel(pe.bias.grad - base, ref.bias.grad) < 1e-3
