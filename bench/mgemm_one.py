@@ -14,7 +14,7 @@ import torch  # noqa: E402
 
 from rocket_amd.ops.mgemm import mgemm  # noqa: E402
 
-LAYERS = {"qkv": (768, 2304), "proj": (768, 768), "fc1": (768, 3072), "fc2": (3072, 768)}
+LAYERS = {"qkv": (768, 2304), "proj": (768, 768), "fc1": (768, 3072), "fc2": (3072, 768), "sq": (4096, 4096)}
 
 
 def main():

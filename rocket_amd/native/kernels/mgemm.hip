@@ -412,6 +412,295 @@ __global__ void __launch_bounds__(64 * WM * WN, WM * WN / 4) mgemm_deep_kernel(M
   store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, 0);
 }
 
+// Ping-pong kernel (tile 10; cdna guide §5 "256² 8-phase template", T1-T5): 256 x 256 x 64
+// k-tiles, one PERSISTENT block per CU, 8 waves in two GROUPS of 4 (group wr owns output rows
+// wr*128..+127 of a tile, wave wc of a group columns wc*64..+63).  Group 1 runs one barrier
+// behind group 0, so on every SIMD (one wave of each group) one wave issues MFMAs while the other
+// issues its LDS reads and LDS-DMAs: the matrix core does not wait on the LDS port or on staging.
+// A k-tile is 4 phases; a phase = [R: fragment reads + one half-tile DMA, lgkmcnt(0)] barrier
+// [M: 16 MFMAs = one 64 x 32 quadrant x K 64] barrier.  Quadrant order (mq,nq): 00 01 11 10, so
+// each operand fragment is read once per k-tile: B (both nq) + A(mq 0) in phase 0, A(mq 1) in
+// phase 2 (16 / 0 / 8 / 0 ds_read_b128 per wave; a 12 / 4 / 8 / 0 split measured slower).
+// Persistence: block b owns output tiles pos(b), pos(b) + grid, ... (pos XCD-aware: the blocks
+// of one XCD run neighbouring tiles) and consumes their k-tiles as ONE stream, so the DMA of the
+// next tile's first k-tiles runs under the current tile's last MFMAs and the epilogue stores of a
+// tile overlap the next tile's loads (no per-tile pipeline fill / drain, no lock-step store bursts).
+// LDS: 2 stream-slot buffers x [A0 | A1 | B0 | B1] half-tiles of 128 rows x 64 k (16 KiB each,
+// the swizzled lane-linear images of the other kernels).  Staging schedule, stream k-tile s read
+// from buffer s&1: phase 0 DMAs A1 of s+1; phases 1-3 DMA B0, B1, A0 of s+2 into buffer s&1 --
+// each only after every wave has retired (lgkmcnt(0) before a barrier) its last read of that
+// half: B in phase 0, A0 in phase 2 (group 0), A1 in phase 2 (group 1, one barrier later), s+2's
+// A1 then following in s+1's phase 0.  Phase 3 waits vmcnt(6) (the 3 half-tiles of s+2 stay in
+// flight; loads retire in order, so older epilogue stores cannot satisfy the count early),
+// retiring this wave's share of s+1; the two barriers that follow publish it to both groups.
+template <bool KMAJ>
+struct PStager {  // one 128-row (row image) / 128-column (kmaj image) half of a 64-deep k-tile
+  uint32_t u[2], v[2];  // row: u = row in the half, v = k of the chunk; kmaj: u = k row, v = column
+  __device__ __forceinline__ void init(int wid, int lane) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = (wid * 2 + i) * 64 + lane;  // 16-byte chunk of the lane-linear image
+      if constexpr (!KMAJ) {
+        const int r = q >> 3;
+        u[i] = r;
+        v[i] = ((q & 7) ^ rswz<64>(r)) * 8;
+      } else {
+        const int k = q >> 4;
+        u[i] = k;
+        v[i] = ((q & 15) ^ kswz<128>(k)) * 8;
+      }
+    }
+  }
+  // rows (cols) r0.. of k-tile kt; chunks at k >= kvalid come from the zero page.  (Addresses are
+  // recomputed per DMA -- min, multiply-add, select -- which measured faster than precomputed
+  // per-lane offsets plus a block-uniform edge branch.)
+  __device__ __forceinline__ void issue(const uint16_t* base, int64_t ld, int r0, int rdim, int kt, int kvalid,
+                                        char* lds, int wid) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint16_t* src;
+      int kpos;
+      if constexpr (!KMAJ) {
+        const int gr = min(r0 + (int)u[i], rdim - 1);
+        src = base + (int64_t)gr * ld + kt * 64 + v[i];
+        kpos = v[i];
+      } else {
+        const int gc = min(r0 + (int)v[i], rdim - 8);
+        src = base + (int64_t)(kt * 64 + (int)u[i]) * ld + gc;
+        kpos = u[i];
+      }
+      if (kpos >= kvalid) src = (const uint16_t*)g_mgemm_zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * 2 + i) * 1024), 16, 0, 0);
+    }
+  }
+};
+
+struct PCursor {  // one position of a block's k-tile stream
+  int i, kt, r0, c0;
+};
+
+template <bool BKM>
+__global__ void __launch_bounds__(512, 2) mgemm_pp_kernel(MArgs g) {
+  constexpr int NW = 8;
+  constexpr int HB = 128 * 64 * 2;  // half-tile bytes
+  constexpr int BUF = 4 * HB;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF + 3 * 1024];  // + 3 tile-bias buffers
+  (void)NW;
+  float* const bias_lds = (float*)(smem + 2 * BUF);
+
+  const int tiles_n = (g.N + 255) / 256;
+  const int ntiles = ((g.M + 255) / 256) * tiles_n;
+  const int grid = gridDim.x;
+  const int pos = xcd_remap(blockIdx.x, grid);
+  const int my_tiles = (ntiles - pos + grid - 1) / grid;
+  const int nt = (g.K + 63) / 64;
+  const int klast = g.K - (nt - 1) * 64;
+  const int S = my_tiles * nt;  // k-tiles in this block's stream
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  PStager<false> sa;
+  PStager<BKM> sb;
+  sa.init(wid, lane);
+  sb.init(wid, lane);
+  auto place = [&](PCursor& c) {
+    const int lin = pos + c.i * grid;
+    const int tm = lin / tiles_n;
+    c.r0 = tm * 256;
+    c.c0 = (lin - tm * tiles_n) * 256;
+  };
+  auto advance = [&](PCursor c) {
+    if (++c.kt == nt) {
+      c.kt = 0;
+      ++c.i;
+      if (c.i < my_tiles) place(c);
+    }
+    return c;
+  };
+  // half h (0 = A0, 1 = A1, 2 = B0, 3 = B1; a constant at every call site) of stream slot s at c
+  auto stage = [&](const PCursor& c, int s, int h) {
+    char* dst = smem + (s & 1) * BUF + h * HB;
+    const int kvalid = c.kt + 1 == nt ? klast : 64;
+    if (h < 2) sa.issue(g.a, g.lda, c.r0 + h * 128, g.M, c.kt, kvalid, dst, wid);
+    else sb.issue(g.b, g.ldb, c.c0 + (h - 2) * 128, g.N, c.kt, kvalid, dst, wid);
+  };
+  FragReader<128, 64, false, 8> ra;
+  FragReader<128, 64, BKM, 4> rb;
+  ra.init(0, lane);
+  rb.init((wc & 1) * 64, lane);
+  const int a_half = wr * HB, b_half = (2 + (wc >> 1)) * HB;
+
+  bf16x8 Bf[2][2][2];  // [nq][fragment][k-step]
+  bf16x8 Af[4][2];     // [fragment][k-step] of the current M quadrant
+  auto readB = [&](const char* buf, int q) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) Bf[q][f][kk] = rb.get(buf + b_half, q * 2 + f, kk);
+  };
+  auto readA = [&](const char* buf, int mq) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) Af[f][kk] = ra.get(buf + a_half, mq * 4 + f, kk);
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto lds_done = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // M part of a phase: quadrant (mq, nq), K = 64
+  auto mma = [&](int mq, int nq) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mq * 4 + f][nq * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(Bf[nq][j][kk], Af[f][kk], acc[mq * 4 + f][nq * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // bias[c0 .. c0+255] of tile i -> bias buffer i%3 (three: with one k-tile per tile, group 1
+  // still reads tile i-1's bias while group 0 issues tile i+1's; waves 0-3, one 4-byte DMA per lane; counted
+  // by those waves' vmcnt like the half-tiles it is issued with, and older than every half-tile
+  // the phase-3 wait leaves in flight)
+  auto stage_bias = [&](const PCursor& c) {
+    if (g.bias != nullptr && wid < 4) {
+      const int n = min(c.c0 + wid * 64 + lane, g.N - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(g.bias + n),
+                                       (lds_void*)(smem + 2 * BUF + (c.i % 3) * 1024 + wid * 256), 4, 0, 0);
+    }
+  };
+  // epilogue of tile c: + bias (from LDS), ReLU / GELU (pre-activation side output optional),
+  // bf16 or f32 stores -- no global loads, so no vmcnt wait drains the next tile's DMAs
+  auto epilogue = [&](const PCursor& c) {
+    // the tile's bias by inline-asm LDS reads: a plain read of an LDS array that DMAs write makes
+    // hipcc wait vmcnt(0) first, draining the next tile's half-tiles
+    f32x4 b4[4];
+    if (g.bias) {
+      const uint32_t base = (uint32_t)(uintptr_t)(const lds_void*)(bias_lds + (c.i % 3) * 256 + wc * 64 + 4 * (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(b4[j]) : "v"(base), "i"(j * 64));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int mbase = c.r0 + wr * 128;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = c.c0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = mbase + i * 16 + (lane & 15);
+        if (m >= g.M) continue;
+        const int64_t off = (int64_t)m * g.ldc + n;
+        float v[4] = {acc[i][j][0] + b4[j][0], acc[i][j][1] + b4[j][1], acc[i][j][2] + b4[j][2],
+                      acc[i][j][3] + b4[j][3]};
+        if (g.epi != kNone) {
+          if (g.c_pre) {
+            if (g.c_dt == BF16)
+              *(uint2*)((uint16_t*)g.c_pre + off) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                                               (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+            else
+              *(float4*)((float*)g.c_pre + off) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = g.epi == kGelu ? gelu_f(v[e]) : fmaxf(v[e], 0.f);
+        }
+        if (g.c_dt == BF16)
+          *(uint2*)((uint16_t*)g.c + off) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                                       (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+        else
+          *(float4*)((float*)g.c + off) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+
+  // prologue: slot 0 whole, slot 1's B0, B1, A0 (the loop's first phase 0 adds its A1)
+  PCursor c0{0, 0, 0, 0};
+  place(c0);
+  PCursor c1 = advance(c0);
+  PCursor c2 = advance(c1);
+  stage_bias(c0);
+  stage(c0, 0, 2); stage(c0, 0, 3); stage(c0, 0, 0); stage(c0, 0, 1);
+  if (S > 1) {
+    stage(c1, 1, 2); stage(c1, 1, 3); stage(c1, 1, 0);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+  if (wr == 1) bar();  // group 1 runs one barrier behind
+
+  for (int s = 0; s < S; ++s) {
+    const char* buf = smem + (s & 1) * BUF;
+    const bool more1 = s + 1 < S, more2 = s + 2 < S;
+    // phase 0: quadrant (0, 0)
+    readB(buf, 0);
+    readB(buf, 1);
+    readA(buf, 0);
+    if (more1) {
+      if (c1.kt == 0) stage_bias(c1);
+      stage(c1, s + 1, 1);
+    }
+    lds_done();
+    bar();
+    mma(0, 0);
+    bar();
+    // phase 1: quadrant (0, 1)
+    if (more2) stage(c2, s + 2, 2);
+    bar();
+    mma(0, 1);
+    bar();
+    // phase 2: quadrant (1, 1)
+    readA(buf, 1);
+    if (more2) stage(c2, s + 2, 3);
+    lds_done();
+    bar();
+    mma(1, 1);
+    bar();
+    // phase 3: quadrant (1, 0); retire this wave's share of s+1
+    if (more2) {
+      stage(c2, s + 2, 0);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    mma(1, 0);
+    bar();
+    if (c0.kt + 1 == nt) {  // the tile is complete: epilogue under the next tile's DMAs
+      epilogue(c0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    c0 = c1;
+    c1 = c2;
+    c2 = advance(c2);
+  }
+  if (wr == 0) bar();  // equal barrier counts in both groups
+}
+
 template <int BM, int BN, int BK, int NS, int WM, int WN, int OCC>
 int launch_tile(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
@@ -440,6 +729,28 @@ int launch_phase(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
   if (!a_kmaj && !b_kmaj) mgemm_phase_kernel<BM, BN, WM, WN, false, false><<<grid, block, 0, s>>>(g);
   else if (!a_kmaj && b_kmaj) mgemm_phase_kernel<BM, BN, WM, WN, false, true><<<grid, block, 0, s>>>(g);
   else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// compute units of the current device (cached; the persistent kernels size their grid by it)
+int rk_num_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cus[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+int launch_pp(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
+  const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  if (a_kmaj || g.accumulate || g.epi > kGelu) return (int)hipErrorInvalidValue;
+  const int grid = std::min(tiles, rk_num_cus());  // persistent: one block per CU
+  if (b_kmaj) mgemm_pp_kernel<true><<<grid, 512, 0, s>>>(g);
+  else mgemm_pp_kernel<false><<<grid, 512, 0, s>>>(g);
   return (int)hipGetLastError();
 }
 
@@ -533,7 +844,8 @@ RK_API int rk_slab_acc(const void* part, int dt, int splits, int64_t count, floa
 //   5: 128x128x32 ring 4, 2x4 waves, 2/CU (64 KiB)
 //   6: 256x256x64 phase-pipelined, 2x4 waves, 1/CU (128 KiB)   7: 256x128x64 phase, 4x2 waves (96 KiB)
 //   8: 256x256x32 4-slot ring, 2x4 waves, 1/CU (128 KiB)      9: 256x128x32 4-slot ring, 4x2 (96 KiB)
-//      (6-9: row x row and row x kmaj only; no split-K / row sums)
+//     10: 256x256x64 ping-pong (two staggered wave groups, 4 phases per k-tile), 1/CU (128 KiB)
+//      (6-10: row x row and row x kmaj only; no split-K / row sums)
 // (256x256, 256x128 and 128x256 tiles with 1-2 blocks per CU and 2-4 deep rings measured slower
 // at every ViT shape on this loop structure: bench/mgemm_probe.py, profiles/r2_mgemm_probe.md)
 // Requirements (hipErrorInvalidValue otherwise; the caller falls back): K % 8 == 0 (unless both
@@ -544,7 +856,7 @@ RK_API int rk_mgemm(const void* a, int64_t lda, int a_kmaj, const void* b, int64
                     int64_t ldc, void* c_pre, const float* bias, const void* aux, int epi, int accumulate,
                     float* rowsum, int M, int N, int K, int splitk, int tile, float* slab, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
-  if (tile != 0 && (tile < 4 || tile > 9)) return (int)hipErrorInvalidValue;
+  if (tile != 0 && (tile < 4 || tile > 10)) return (int)hipErrorInvalidValue;
   if (tile >= 6 && (splitk > 1 || rowsum != nullptr || (a_kmaj && b_kmaj))) return (int)hipErrorInvalidValue;
   // a row-layout operand moves K in 16-byte chunks (K % 8); a kmaj one in whole k-rows (any K)
   if (K <= 0 || ((!a_kmaj || !b_kmaj) && K % 8) || N % 8 || (a_kmaj && M % 8) || ldc % 4) return (int)hipErrorInvalidValue;
@@ -570,6 +882,7 @@ RK_API int rk_mgemm(const void* a, int64_t lda, int a_kmaj, const void* b, int64
     case 7: rc = launch_phase<256, 128, 4, 2>(g, a_kmaj, b_kmaj, s); break;
     case 8: rc = launch_deep<256, 256, 2, 4>(g, a_kmaj, b_kmaj, s); break;
     case 9: rc = launch_deep<256, 128, 4, 2>(g, a_kmaj, b_kmaj, s); break;
+    case 10: rc = launch_pp(g, a_kmaj, b_kmaj, s); break;
     default: rc = launch_tile<128, 128, 32, 4, 2, 4, 2>(g, a_kmaj, b_kmaj, s); break;
   }
   if (rc || splitk == 1) return rc;

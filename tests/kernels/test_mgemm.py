@@ -282,3 +282,51 @@ def test_patch_embed_matches_conv(direct):
     assert _rel(y, yr) < 1e-2
     assert _rel(pe.weight.grad - base, ref.weight.grad) < 1e-2
     assert _rel(pe.bias.grad - base, ref.bias.grad) < 1e-3
+
+
+@pytest.mark.parametrize("layout", ["fwd", "dgrad"])
+@pytest.mark.parametrize("M,N,K", [(25216, 768, 768), (4096, 2304, 3072), (300, 136, 200), (1000, 2304, 64),
+                                   (792, 264, 88), (512, 512, 128), (257, 520, 192), (4196, 4096, 64),
+                                   (9000, 3000, 136)])
+def test_mgemm_pingpong(layout, M, N, K):
+    """Tile 10 (two staggered wave groups, half-tile DMA schedule): edges, partial k-tiles, 1-3
+    k-tile loops; repeated launches must agree bitwise (a mis-ordered LDS hand-off shows up as
+    run-to-run differences before it shows up as a large error)."""
+    from rocket_amd.ops.mgemm import mgemm
+
+    torch.manual_seed(K)
+    if layout == "fwd":
+        a, b = _r(M, K), _r(N, K)
+        ref = a.float() @ b.float().t()
+        kw = dict(lda=K, ldb=K)
+    else:
+        a, b = _r(M, K), _r(K, N)
+        ref = a.float() @ b.float()
+        kw = dict(lda=K, ldb=N, b_kmaj=True)
+    # persistent blocks: > 256 tiles puts several tiles (and their k-tile streams) on one block
+    bias = torch.randn(N, device="cuda") if N % 3 == 0 else None
+    if bias is not None:
+        ref = ref + bias
+        kw["bias"] = bias
+    c = torch.empty(M, N, dtype=torch.float32, device="cuda")
+    mgemm(a, b, c, M=M, N=N, K=K, ldc=N, tile=10, **kw)
+    assert _rel(c, ref) < 1e-5, _rel(c, ref)
+    first = c.clone()
+    for _ in range(4):
+        c.zero_()
+        mgemm(a, b, c, M=M, N=N, K=K, ldc=N, tile=10, **kw)
+        assert torch.equal(c, first)
+
+
+def test_mgemm_pingpong_epilogue():
+    from rocket_amd.ops.mgemm import mgemm
+
+    torch.manual_seed(3)
+    M, N, K = 1000, 768, 320
+    a, b = _r(M, K), _r(N, K, scale=0.2)
+    bias = torch.randn(N, device="cuda")
+    z = a.float() @ b.float().t() + bias
+    c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    pre = torch.empty_like(c)
+    mgemm(a, b, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, epi="gelu", c_pre=pre, tile=10)
+    assert _rel(pre, z) < 5e-3 and _rel(c, F.gelu(z)) < 5e-3
