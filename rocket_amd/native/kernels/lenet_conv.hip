@@ -56,6 +56,15 @@ __device__ __forceinline__ uint32_t pair_at(const uint16_t* c0, const uint16_t* 
   return *(const uint32_t*)p;
 }
 
+// Block barrier for LDS hand-offs only: waits for this wave's LDS ops, not its global loads
+// (__syncthreads() also drains vmcnt, exposing the latency of prefetched operands at every phase
+// boundary).  Global memory is never exchanged between the waves of a block here.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Intra-wave LDS producer/consumer ordering: drain this wave's LDS ops and stop the compiler
 // from moving memory accesses across (lanes read what other lanes of the same wave wrote).
 __device__ __forceinline__ void wave_lds_sync() {
@@ -167,6 +176,19 @@ __device__ __forceinline__ f32x4 cls_tile(const uint16_t* act, int stride, const
   return acc;
 }
 
+// same with the B fragments already in registers (prefetched early by the caller)
+template <int KS>
+__device__ __forceinline__ f32x4 cls_tile_pre(const uint16_t* act, int stride, const uint16_t* zrow,
+                                              const bf16x8 (&b)[KS], int lane) {
+  const int lo = lane & 15, hi = lane >> 4;
+  const uint16_t* row = lo < SPB ? act + lo * stride : zrow;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(row + 32 * ks + 8 * hi), b[ks], acc, 0, 0, 0);
+  return acc;
+}
+
 __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
   return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
 }
@@ -206,6 +228,8 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
   // conv B operands: the fused path loads the prep kernel's fragments first thing (one 16-byte
   // load per k-step, latency hidden behind the image staging); the generic path gathers them
   bf16x8 bw1, bw2[7];
+  bf16x8 fr1[13], fr2[4], fr3[3];  // classifier B fragments (fused path), prefetched: their global
+                                   // latency hides under the convolutions instead of after a barrier
   if constexpr (MLP) {
     bw1 = cf.frag[OFF_C1 * 64 + lane];
 #pragma unroll
@@ -263,39 +287,122 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     if (wave < 6) fbias2 = cf.fb2[col < F2 ? col : 0];
     if (wave == 0) fbias3 = cf.fb3[lo < F3 ? lo : 0];
   }
-  __syncthreads();
+  lds_barrier();
   RK_TR(cf.trace, 1);
 
-  // ---- conv1: 49 tiles of 16 rows (4 windows x 4 positions), split over the sample's 4 waves
-  for (int t = sw; t < 49; t += WPS) {
-    const int pos = pos1(4 * t + (lo >> 2), lo & 3);
-    bf16x8 a;
-    if constexpr (MLP) {  // taps ordered (kh, kw) with kw padded to 6: 4 aligned pair reads per lane
-      uint32_t w4[4];
+  // ---- conv1: 49 tiles of 16 rows (4 windows x 4 positions), split over the sample's 4 waves;
+  // U1 tiles per iteration: all their LDS gathers, then their MFMAs, then their epilogues (four
+  // independent chains in flight instead of one read -> MFMA -> max -> store chain at a time)
+  constexpr int U1 = 4;
+  if constexpr (MLP) {
+    // Issue-bound phase (4 waves per SIMD, ~100 instructions per tile when every address is
+    // derived from the tile index): addresses are per-lane constants plus an incrementally
+    // stepped window position.  The parity of pos1(w, q) is (q>>1 ^ q&1), independent of w, and
+    // so is the parity of every tap offset: each lane's choice between the two image copies (the
+    // aligned pair read) is fixed, as are its output slots up to a per-tile stride.
+    const int q4 = lo & 3;
+    const int par = ((q4 >> 1) ^ q4) & 1;
+    uint32_t pb[4], pm[4];  // per pair: LDS byte base (copy + tap offset), mask on the window position
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w4[q] = pair_at(img0, img1, koffp[q] >= 0 ? pos + koffp[q] : IMGZ);
-      a = __builtin_bit_cast(bf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = __builtin_bit_cast(__bf16, img0[koff1[j] >= 0 ? pos + koff1[j] : IMGZ]);
+    for (int q = 0; q < 4; ++q) {
+      const int kp = koffp[q];
+      const bool ok = kp >= 0;
+      const int xp = par ^ (ok ? (kp & 1) : 0);  // parity of pos + kp
+      const uint16_t* basep = ok ? (xp ? img1 - 1 + kp : img0 + kp) : img0 + IMGZ;
+      pb[q] = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint16_t*)basep;
+      pm[q] = ok ? 0xffffffffu : 0u;
     }
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw1, acc, 0, 0, 0);
-    float m = acc[0];
-    int arg = 0;
+    // window of tile t: w = 4t + (lo >> 2), stepped by 16 (= one pool row + 2) per WPS tiles
+    int wc = (4 * sw + (lo >> 2)) % Q1, wr = (4 * sw + (lo >> 2)) / Q1;
+    int pos = (2 * wr + (q4 >> 1)) * IMGS + 2 * wc + (q4 & 1);
+    const int ostep = lo < C1 ? 4 * WPS : 0;
+    int o = lo < C1 ? lo * (Q1 * Q1) + 4 * sw + hi : A1N + 4;
+    const int cstep = lo < 8 ? 4 * WPS * 8 : 0;
+    int oc = lo < 8 ? (4 * sw + hi) * 8 + lo : A1CL + 8;
+    uint16_t* const a1cl = sm.a1cl[slot];
+    for (int t0 = sw; t0 < 49; t0 += U1 * WPS) {
+      bf16x8 a[U1];
+      int pu = pos, wcu = wc;
 #pragma unroll
-    for (int i = 1; i < 4; ++i) {
-      const bool gt = acc[i] > m;
-      m = gt ? acc[i] : m;
-      arg = gt ? i : arg;
+      for (int u = 0; u < U1; ++u) {
+        const int pc = min(pu, (PADI - 1) * IMGS);  // tiles past 48: any in-image position, never stored
+        uint32_t w4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          w4[q] = *(const __attribute__((address_space(3))) uint32_t*)(uintptr_t)(pb[q] + 2u * ((uint32_t)pc & pm[q]));
+        a[u] = __builtin_bit_cast(bf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
+        // step 16 windows: +1 pool row (+66) and +2 columns (+4); wrapping a row: +2 rows, -12 columns
+        wcu += 2;
+        const bool wrap = wcu >= Q1;
+        wcu = wrap ? wcu - Q1 : wcu;
+        pu += wrap ? 2 * 2 * IMGS + 4 - 2 * Q1 : 2 * IMGS + 4;
+      }
+      f32x4 acc[U1];
+#pragma unroll
+      for (int u = 0; u < U1; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bw1, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        if (t0 + u * WPS >= 49) break;  // wave-uniform
+        float m = acc[u][0];
+        int arg = 0;
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+          const bool gt = acc[u][i] > m;
+          m = gt ? acc[u][i] : m;
+          arg = gt ? i : arg;
+        }
+        m += bias1;
+        const bool on = m > 0.f;
+        const uint16_t v = f2bf(on ? m : 0.f);
+        a1[o + u * ostep] = v;
+        c1[o + u * ostep] = on ? (uint8_t)arg : 0xFF;
+        a1cl[oc + u * cstep] = lo < C1 ? v : (uint16_t)0;
+      }
+      pos = pu;
+      wc = wcu;
+      o += U1 * ostep;
+      oc += U1 * cstep;
     }
-    m += bias1;
-    const bool on = m > 0.f;
-    const int o = lo < C1 ? lo * (Q1 * Q1) + 4 * t + hi : A1N + 4;
-    const uint16_t v = f2bf(on ? m : 0.f);
-    a1[o] = v;
-    c1[o] = on ? (uint8_t)arg : 0xFF;
-    sm.a1cl[slot][lo < 8 ? (4 * t + hi) * 8 + lo : A1CL + 8] = lo < C1 ? v : (uint16_t)0;
+  } else {
+    for (int t0 = sw; t0 < 49; t0 += U1 * WPS) {
+      bf16x8 a[U1];
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        const int t = min(t0 + u * WPS, 48);  // past the end: a duplicate of tile 48, never stored
+        const int pos = pos1(4 * t + (lo >> 2), lo & 3);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[u][j] = __builtin_bit_cast(__bf16, img0[koff1[j] >= 0 ? pos + koff1[j] : IMGZ]);
+      }
+      f32x4 acc[U1];
+#pragma unroll
+      for (int u = 0; u < U1; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bw1, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        const int t = t0 + u * WPS;
+        if (t >= 49) break;  // wave-uniform
+        float m = acc[u][0];
+        int arg = 0;
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+          const bool gt = acc[u][i] > m;
+          m = gt ? acc[u][i] : m;
+          arg = gt ? i : arg;
+        }
+        m += bias1;
+        const bool on = m > 0.f;
+        const int o = lo < C1 ? lo * (Q1 * Q1) + 4 * t + hi : A1N + 4;
+        const uint16_t v = f2bf(on ? m : 0.f);
+        a1[o] = v;
+        c1[o] = on ? (uint8_t)arg : 0xFF;
+        sm.a1cl[slot][lo < 8 ? (4 * t + hi) * 8 + lo : A1CL + 8] = lo < C1 ? v : (uint16_t)0;
+      }
+    }
+  }
+  if constexpr (MLP) {  // fc1 fragments (bw1 is dead now)
+    if (wave < 8) {
+#pragma unroll
+      for (int ks = 0; ks < 13; ++ks) fr1[ks] = cf.frag[(OFF_F1 + wave * 13 + ks) * 64 + lane];
+    }
   }
   // conv2 operands, reduction ordered k = (kh*5 + kw)*8 + ci (ci padded 6 -> 8): a lane's 8
   // consecutive k are the 8 channels of one pixel of the channel-last image = ONE 16-byte read.
@@ -312,7 +419,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
         bw2[s][j] = tobf(ok ? v : 0.f);
       }
   }
-  __syncthreads();
+  lds_barrier();
   RK_TR(cf.trace, 3);
   if (live) {
     for (int i = st * 8; i < A1N; i += 64 * WPS * 8) {
@@ -322,36 +429,60 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
   }
 
   RK_TR(cf.trace, 4);
-  // ---- conv2: 25 windows -> 7 tiles, split over the 4 waves
-  for (int t = sw; t < 7; t += WPS) {
-    const int w = 4 * t + (lo >> 2);
-    const bool wvalid = w < Q2 * Q2;
-    const int pos = pos2(wvalid ? w : 0, lo & 3);  // conv2 output position = pixel of a1
+  // ---- conv2: 25 windows -> 7 tiles, split over the 4 waves; a wave's two tiles (sw, sw + 4)
+  // run as two interleaved 7-MFMA chains
+  {
     const uint16_t* acl = sm.a1cl[slot];
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const bool two = sw + WPS < 7;  // wave-uniform
+    int pos[2];
+    bool wvalid[2];
 #pragma unroll
-    for (int s = 0; s < 7; ++s) {
-      const int kk = 4 * s + hi;
-      const int px = (wvalid && kk < R1) ? pos + (kk / KS) * Q1 + (kk % KS) : Q1 * Q1;  // Q1*Q1 -> zero pixel
-      const bf16x8 a = *(const bf16x8*)(acl + px * 8);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[s], acc, 0, 0, 0);
+    for (int u = 0; u < 2; ++u) {
+      const int t = u ? (two ? sw + WPS : sw) : sw;
+      const int w = 4 * t + (lo >> 2);
+      wvalid[u] = w < Q2 * Q2;
+      pos[u] = pos2(wvalid[u] ? w : 0, lo & 3);  // conv2 output position = pixel of a1
     }
-    const int wq = 4 * t + hi;
-    float m = acc[0];
-    int arg = 0;
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int i = 1; i < 4; ++i) {
-      const bool gt = acc[i] > m;
-      m = gt ? acc[i] : m;
-      arg = gt ? i : arg;
+    for (int s = 0; s < 7; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kk = 4 * s + hi;
+        const int px = (wvalid[u] && kk < R1) ? pos[u] + (kk / KS) * Q1 + (kk % KS) : Q1 * Q1;  // Q1*Q1 -> zero pixel
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(acl + px * 8), bw2[s], acc[u], 0, 0, 0);
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      const int t = sw + u * WPS;
+      const int wq = 4 * t + hi;
+      float m = acc[u][0];
+      int arg = 0;
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {
+        const bool gt = acc[u][i] > m;
+        m = gt ? acc[u][i] : m;
+        arg = gt ? i : arg;
+      }
+      m += bias2;
+      const bool on = m > 0.f;
+      const int o = wq < Q2 * Q2 ? lo * (Q2 * Q2) + wq : (MLP ? A2TRASH : A2N);  // flatten order (C, H, W)
+      sm.a2[slot][o] = f2bf(on ? m : 0.f);
+      sm.c2[slot][o] = on ? (uint8_t)arg : 0xFF;
     }
-    m += bias2;
-    const bool on = m > 0.f;
-    const int o = wq < Q2 * Q2 ? lo * (Q2 * Q2) + wq : (MLP ? A2TRASH : A2N);  // flatten order (C, H, W)
-    sm.a2[slot][o] = f2bf(on ? m : 0.f);
-    sm.c2[slot][o] = on ? (uint8_t)arg : 0xFF;
   }
-  __syncthreads();
+  if constexpr (MLP) {  // fc2 / fc3 fragments (bw2 is dead now; fc1 hides their latency)
+    if (wave < 6) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) fr2[ks] = cf.frag[(OFF_F2 + wave * 4 + ks) * 64 + lane];
+    }
+    if (wave == 0) {
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) fr3[ks] = cf.frag[(OFF_F3 + ks) * 64 + lane];
+    }
+  }
+  lds_barrier();
   RK_TR(cf.trace, 5);
   if (live) {
     for (int i = st * 8; i < A2N; i += 64 * WPS * 8) {
@@ -363,7 +494,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
     // the host guarantees N % 8 == 0, so every block holds 4 live samples
     const int n0 = blockIdx.x * SPB;
     if (wave < 8) {  // fc1: n-tile = wave, 13 k-steps
-      const f32x4 acc = cls_tile<13>(&sm.a2[0][0], A2P, sm.zrow, cf.frag, OFF_F1 + wave * 13, lane);
+      const f32x4 acc = cls_tile_pre<13>(&sm.a2[0][0], A2P, sm.zrow, fr1, lane);
       if (hi == 0) {
         const int col = 16 * wave + lo;
         const float bb = fbias1;
@@ -381,10 +512,10 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
             (uint32_t)sm.a2[0][f] | ((uint32_t)sm.a2[1][f] << 16), (uint32_t)sm.a2[2][f] | ((uint32_t)sm.a2[3][f] << 16));
       if (threadIdx.x - 512 < SPB * 8) sm.h1[(threadIdx.x - 512) >> 3][128 + ((threadIdx.x - 512) & 7)] = 0;
     }
-    __syncthreads();
+    lds_barrier();
     RK_TR(cf.trace, 6);
     if (wave < 6) {  // fc2: 6 n-tiles x 4 k-steps
-      const f32x4 acc = cls_tile<4>(&sm.h1[0][0], H1P, sm.zrow, cf.frag, OFF_F2 + wave * 4, lane);
+      const f32x4 acc = cls_tile_pre<4>(&sm.h1[0][0], H1P, sm.zrow, fr2, lane);
       if (hi == 0) {
         const int col = 16 * wave + lo;
         const float bb = fbias2;
@@ -397,10 +528,10 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
         if (col < F2) *(uint2*)(cf.h2T + (int64_t)col * N + n0) = pack4(v[0], v[1], v[2], v[3]);
       }
     }
-    __syncthreads();
+    lds_barrier();
     RK_TR(cf.trace, 7);
     if (wave == 0) {  // fc3: 1 n-tile x 3 k-steps -> fp32 logits
-      const f32x4 acc = cls_tile<3>(&sm.h2[0][0], H2P, sm.zrow, cf.frag, OFF_F3, lane);
+      const f32x4 acc = cls_tile_pre<3>(&sm.h2[0][0], H2P, sm.zrow, fr3, lane);
       if (hi == 0 && lo < F3) {
         const float bb = fbias3;
 #pragma unroll

@@ -20,7 +20,8 @@ import threading
 import torch  # noqa: F401  (must precede loading the HIP library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIBDIR = os.path.join(os.path.dirname(_HERE), "_lib")
+# ROCKET_LIBDIR: load the native libraries from another directory (A/B of two builds in one tree)
+LIBDIR = os.environ.get("ROCKET_LIBDIR") or os.path.join(os.path.dirname(_HERE), "_lib")
 _lock = threading.Lock()
 _libs: dict = {}
 
