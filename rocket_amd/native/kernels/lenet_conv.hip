@@ -244,13 +244,39 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
   uint16_t* a1 = sm.a1[slot];
   uint8_t* c1 = sm.c1[slot];
 
-  for (int i = st; i < IMGN + 8; i += 64 * WPS) {
-    const int r = i / IMGS - 2, c = i % IMGS - 2;
-    const bool in = i < IMGN && r >= 0 && r < IMG && c >= 0 && c < IMG;
-    const float v = x[(int64_t)nc * IMG * IMG + (in ? r * IMG + c : 0)];
-    const uint16_t u = f2bf(in ? v : 0.f);
-    img0[i] = u;
-    if (i > 0) img1[i - 1] = u;
+  // the sample's 784 pixels as 196 float4 loads (one per thread), written at their padded
+  // position (row stride IMGS, 2-pixel zero border) into both image copies; the 280 border /
+  // zero-slot elements are written by the other threads (disjoint addresses: no ordering needed)
+  {
+    static_assert(64 * WPS >= IMG * IMG / 4, "one vector per thread");
+    const float4* xs = (const float4*)(x + (int64_t)nc * IMG * IMG);
+    float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (st < IMG * IMG / 4) v4 = xs[st];
+    for (int b = st; b < 4 * IMGS + IMG * 5 + 8; b += 64 * WPS) {  // border / zero-slot elements
+      int bi;
+      if (b < 4 * IMGS) {  // rows 0, 1, 30, 31
+        const int r = b / IMGS;
+        bi = (r < 2 ? r : r + IMG) * IMGS + b % IMGS;
+      } else if (b < 4 * IMGS + IMG * 5) {  // columns 0, 1, 30, 31, 32 of rows 2..29
+        const int u = b - 4 * IMGS, c5 = u % 5;
+        bi = (2 + u / 5) * IMGS + (c5 < 2 ? c5 : c5 + IMG);
+      } else {
+        bi = IMGN + (b - 4 * IMGS - IMG * 5);  // zero slots past the image
+      }
+      img0[bi] = 0;
+      if (bi > 0) img1[bi - 1] = 0;
+    }
+    if (st < IMG * IMG / 4) {
+      const int p = 4 * st, r = p / IMG, c = p - r * IMG;
+      const int i = (r + 2) * IMGS + c + 2;
+      const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint16_t u = f2bf(live ? vv[j] : 0.f);
+        img0[i + j] = u;
+        img1[i + j - 1] = u;
+      }
+    }
   }
   if (st < 8) a1[A1N + st] = 0;
   if (st < 16) sm.a1cl[slot][A1CL + st] = 0;
@@ -654,6 +680,32 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
   if (MLP)
     for (int i = threadIdx.x; i < H1P; i += NTHR) sm.zrow[i] = 0;
   if (MLP && cb.ce && threadIdx.x == 0) sm.lossp[0] = 0.f;
+  // fused path: the classifier dgrad B fragments and ReLU masks are loaded now, so the chain below
+  // runs on registers and LDS only (each was one global round trip after a barrier)
+  bf16x8 fb3, fb2[3], fb1[2][4];
+  uint2 mk2 = make_uint2(0u, 0u), mk1 = make_uint2(0u, 0u);
+  if constexpr (MLP) {
+    const int nb = blockIdx.x * rounds * SPB;
+    if (wave < 6) {
+      fb3 = cb.frag[(OFF_B3 + wave) * 64 + lane];
+      const int col = 16 * wave + lo;
+      if (hi == 0) mk2 = *(const uint2*)(cb.h2T + (int64_t)(col < F2 ? col : 0) * N + nb);
+    }
+    if (wave < 8) {
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) fb2[ks] = cb.frag[(OFF_B2 + wave * 3 + ks) * 64 + lane];
+      const int col = 16 * wave + lo;
+      if (hi == 0) mk1 = *(const uint2*)(cb.h1T + (int64_t)(col < F1 ? col : 0) * N + nb);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = wave + 16 * u;
+      if (t < 25) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) fb1[u][ks] = cb.frag[(OFF_B1 + t * 4 + ks) * 64 + lane];
+      }
+    }
+  }
 
   const int nrounds = MLP ? 1 : rounds;  // fused variant: one round (no loop-invariant state to keep live)
   for (int rd = 0; rd < nrounds; ++rd) {
@@ -672,9 +724,40 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
         for (int i = threadIdx.x - 64; i < N; i += NTHR - 64) ce_cnt += cb.target[i] != cb.ignore_index ? 1.f : 0.f;
       }
     }
-    __syncthreads();
+    if constexpr (MLP) lds_barrier();
+    else __syncthreads();
     RK_TR(cb.trace, 1);
-    // ---- phase A: stage
+    // ---- phase A: stage.  Fused path: the image and a1 / code1 loads go to registers here and are
+    // written to LDS after the classifier chain (their latency hides under it); the image border
+    // and the dc2 / dcT zero fills need no loads and are written now.
+    float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint4 a1v = make_uint4(0u, 0u, 0u, 0u);
+    uint2 c1v = make_uint2(0u, 0u);
+    if constexpr (MLP) {
+      static_assert(SPB * IMG * IMG / 4 <= NTHR && SPB * (A1N / 8) <= NTHR, "one vector per thread");
+      if (threadIdx.x < SPB * IMG * IMG / 4) {
+        const int sl = threadIdx.x / (IMG * IMG / 4), v = threadIdx.x % (IMG * IMG / 4);
+        xv = *(const float4*)(x + (int64_t)(nbase + sl) * IMG * IMG + 4 * v);
+      }
+      if (threadIdx.x < SPB * (A1N / 8)) {
+        const int sl = threadIdx.x / (A1N / 8), e = (threadIdx.x % (A1N / 8)) * 8;
+        a1v = *(const uint4*)(a1g + (int64_t)(nbase + sl) * A1N + e);
+        c1v = *(const uint2*)(code1g + (int64_t)(nbase + sl) * A1N + e);
+      }
+      for (int t = threadIdx.x; t < SPB * 272; t += NTHR) {  // border of the padded image (rows/cols)
+        const int sl = t / 272, b = t % 272;
+        int bi;
+        if (b < 4 * IMGS) {
+          const int r = b / IMGS;
+          bi = (r < 2 ? r : r + IMG) * IMGS + b % IMGS;
+        } else {
+          const int u = b - 4 * IMGS, c5 = u % 5;
+          bi = (2 + u / 5) * IMGS + (c5 < 2 ? c5 : c5 + IMG);
+        }
+        sm.imgb[sl][0][bi] = 0;
+        if (bi > 0) sm.imgb[sl][1][bi - 1] = 0;
+      }
+    } else
     for (int i = threadIdx.x; i < SPB * IMGN; i += NTHR) {
       const int sl = i / IMGN, e = i % IMGN;
       const int n = nbase + sl;
@@ -685,6 +768,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
       sm.imgb[sl][0][e] = u;
       if (e > 0) sm.imgb[sl][1][e - 1] = u;
     }
+    if (!MLP)
     for (int i = threadIdx.x; i < SPB * (A1N / 8); i += NTHR) {
       const int sl = i / (A1N / 8), e = (i % (A1N / 8)) * 8;
       const int n = nbase + sl, nc = n < N ? n : 0;
@@ -736,7 +820,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
           for (int k = 32; k >= 1; k >>= 1) ce_cnt += __shfl_xor(ce_cnt, k, 64);
           if (lane == 0) sm.cecnt[wave] = ce_cnt;
         }
-        __syncthreads();
+        lds_barrier();
         RK_TR(cb.trace, 3);
         if (threadIdx.x < SPB * DYP || (threadIdx.x >= 256 && threadIdx.x < 256 + F3)) {
           float nv = 0.f;
@@ -752,7 +836,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
                 pack4(sc * sm.dyf[0][o], sc * sm.dyf[1][o], sc * sm.dyf[2][o], sc * sm.dyf[3][o]);
           }
         }
-        __syncthreads();
+        lds_barrier();
       } else {
         if (threadIdx.x < SPB * DYP) {
           const int sl = threadIdx.x / DYP, o = threadIdx.x % DYP;
@@ -762,14 +846,15 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
           const float* d = cb.dy + (int64_t)nbase * F3 + o;
           *(uint2*)(cb.dyT + (int64_t)o * N + nbase) = pack4(d[0], d[F3], d[2 * F3], d[3 * F3]);
         }
-        __syncthreads();
+        lds_barrier();
       RK_TR(cb.trace, 4);
       }
       if (wave < 6) {  // fc3 dgrad: d2 = (dy W3) * [h2 > 0]
-        const f32x4 acc = cls_tile<1>(&sm.dyl[0][0], DYP, sm.zrow, cb.frag, OFF_B3 + wave, lane);
+        const bf16x8 fb3a[1] = {fb3};
+        const f32x4 acc = cls_tile_pre<1>(&sm.dyl[0][0], DYP, sm.zrow, fb3a, lane);
         if (hi == 0) {
           const int col = 16 * wave + lo;
-          const uint2 m = *(const uint2*)(cb.h2T + (int64_t)(col < F2 ? col : 0) * N + nbase);
+          const uint2 m = mk2;
           const float mk[4] = {bf2f(m.x & 0xffff), bf2f(m.x >> 16), bf2f(m.y & 0xffff), bf2f(m.y >> 16)};
           float v[4];
 #pragma unroll
@@ -780,13 +865,13 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
           if (col < F2) *(uint2*)(cb.d2T + (int64_t)col * N + nbase) = pack4(v[0], v[1], v[2], v[3]);
         }
       }
-      __syncthreads();
+      lds_barrier();
       RK_TR(cb.trace, 5);
       if (wave < 8) {  // fc2 dgrad: d1 = (d2 W2) * [h1 > 0]
-        const f32x4 acc = cls_tile<3>(&sm.d2l[0][0], H2P, sm.zrow, cb.frag, OFF_B2 + wave * 3, lane);
+        const f32x4 acc = cls_tile_pre<3>(&sm.d2l[0][0], H2P, sm.zrow, fb2, lane);
         if (hi == 0) {
           const int col = 16 * wave + lo;
-          const uint2 m = *(const uint2*)(cb.h1T + (int64_t)(col < F1 ? col : 0) * N + nbase);
+          const uint2 m = mk1;
           const float mk[4] = {bf2f(m.x & 0xffff), bf2f(m.x >> 16), bf2f(m.y & 0xffff), bf2f(m.y >> 16)};
           float v[4];
 #pragma unroll
@@ -797,14 +882,42 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
           if (col < F1) *(uint2*)(cb.d1T + (int64_t)col * N + nbase) = pack4(v[0], v[1], v[2], v[3]);
         }
       }
-      __syncthreads();
+      lds_barrier();
       RK_TR(cb.trace, 6);
-      for (int t = wave; t < 25; t += 16) {  // fc1 dgrad: da2 = d1 W1 (400 outputs = 25 tiles)
-        const f32x4 acc = cls_tile<4>(&sm.d1l[0][0], H1P, sm.zrow, cb.frag, OFF_B1 + t * 4, lane);
-        if (hi == 0) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) sm.da2[i][16 * t + lo] = f2bf(acc[i]);
+      for (int u = 0; u < 2; ++u) {  // fc1 dgrad: da2 = d1 W1 (400 outputs = 25 tiles)
+        const int t = wave + 16 * u;
+        if (t < 25) {
+          const f32x4 acc = cls_tile_pre<4>(&sm.d1l[0][0], H1P, sm.zrow, fb1[u], lane);
+          if (hi == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sm.da2[i][16 * t + lo] = f2bf(acc[i]);
+          }
         }
+      }
+      // the staged conv operands, loaded before the chain
+      if (threadIdx.x < SPB * IMG * IMG / 4) {
+        const int sl = threadIdx.x / (IMG * IMG / 4), p = 4 * (threadIdx.x % (IMG * IMG / 4));
+        const int r = p / IMG, c = p - r * IMG;
+        const int i = (r + 2) * IMGS + c + 2;
+        const float vv[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint16_t u = f2bf(vv[j]);
+          sm.imgb[sl][0][i + j] = u;
+          sm.imgb[sl][1][i + j - 1] = u;
+        }
+      }
+      if (threadIdx.x < SPB * (A1N / 8)) {
+        const int sl = threadIdx.x / (A1N / 8), e = (threadIdx.x % (A1N / 8)) * 8;
+        *(uint4*)(sm.a1[sl] + e) = a1v;
+        const uint32_t w[4] = {a1v.x, a1v.y, a1v.z, a1v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // a1o[e - 1 + j] = a1[e + j]
+          if (e + 2 * k > 0) sm.a1o[sl][e + 2 * k - 1] = (uint16_t)(w[k] & 0xffff);
+          sm.a1o[sl][e + 2 * k] = (uint16_t)(w[k] >> 16);
+        }
+        *(uint2*)(sm.c1[sl] + e) = c1v;
       }
     }
     __syncthreads();
@@ -1088,6 +1201,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
 
 RK_API int rk_lenet_conv_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                              void* a1, void* code1, void* a2, void* code2, int N, hipStream_t s) {
+  if ((uintptr_t)x & 15) return (int)hipErrorInvalidValue;  // float4 image loads
   const int grid = (N + SPB - 1) / SPB;
   lenet_conv_fwd<false><<<grid, NTHR, 0, s>>>(x, w1, b1, w2, b2, (uint16_t*)a1, (uint8_t*)code1, (uint16_t*)a2,
                                               (uint8_t*)code2, N, ClsFwd{});
@@ -1117,7 +1231,7 @@ RK_API int rk_lenet_fwd(const float* x, const float* w1, const float* b1, const 
                         const void* frag, const float* fb1, const float* fb2, const float* fb3, void* a1,
                         void* code1, void* code2, void* a2T, void* h1T, void* h2T, float* logits, int N,
                         hipStream_t s) {
-  if (N % 8) return (int)hipErrorInvalidValue;
+  if (N % 8 || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
   ClsFwd cf{(const bf16x8*)frag, fb1, fb2, fb3, (uint16_t*)a2T, (uint16_t*)h1T, (uint16_t*)h2T, logits, g_fwd_trace};
   lenet_conv_fwd<true><<<N / SPB, NTHR, 0, s>>>(x, w1, b1, w2, b2, (uint16_t*)a1, (uint8_t*)code1, nullptr,
                                                 (uint8_t*)code2, N, cf);
@@ -1165,7 +1279,7 @@ RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const
                         const void* frag, const float* dy, const void* h1T, const void* h2T, void* dyT, void* d2T,
                         void* d1T, float* slab, int N, int rounds, const LenetCE* ce, hipStream_t s) {
   rounds = 1;  // the fused kernel handles one group of SPB samples per block (argument kept for ABI)
-  if (N % 8 || N > 65536) return (int)hipErrorInvalidValue;
+  if (N % 8 || N > 65536 || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;  // float4 image loads
   if (!slab) return (int)hipErrorInvalidValue;
   ClsBwd cb{};
   cb.trace = g_bwd_trace;

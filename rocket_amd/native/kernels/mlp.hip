@@ -299,8 +299,21 @@ __device__ void loss_fin_block(const LossFin& f, float (*red)[32 * 32]) {
 
 // one slab block: 64 columns x all rows; 8 row groups per block, 8 independent loads per thread
 // in flight, LDS reduce over the groups, one plain RMW per column (sole owner: deterministic)
+constexpr int kEpiGroups = 4;  // param groups the epilogue precomputes step constants for
+
+// per-group Adam constants of this launch's step, written to LDS before the caller's barrier
+struct StepFill {
+  const WgradArgs* a;
+  float cur;
+  rk_opt::AdamStep* s_ks;
+  __device__ __forceinline__ void operator()() const {
+    if (a->epi.on && threadIdx.x < kEpiGroups)
+      s_ks[threadIdx.x] = rk_opt::adam_step(a->epi.hyper[threadIdx.x < a->epi.on ? threadIdx.x : 0], cur + 1.f);
+  }
+};
+
 __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, float (*red)[32 * 32],
-                                                  const rk_opt::AdamStep* ks) {
+                                                  const rk_opt::AdamStep* ks, const StepFill& sf) {
   const SlabArgs& s = a.sl;
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = j * 64 + cl;
@@ -336,6 +349,7 @@ __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, flo
   }
   for (; r < s.rows; r += NW) acc += base[(int64_t)r * s.width];
   red[rg][cl] = acc;
+  sf();
   __syncthreads();
   if (dst) {
     float t = 0.f;
@@ -355,31 +369,31 @@ __device__ __forceinline__ bf16x8 rowfrag(const uint16_t* T, int R, int M, int r
   return __builtin_bit_cast(bf16x8, ok ? v : z);
 }
 
-constexpr int kEpiGroups = 4;  // param groups the epilogue precomputes step constants for
 
-__device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks);
+__device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks,
+                           const StepFill& sf);
 
 __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   __shared__ float red[NW][32 * 32];
   __shared__ float rsum[NW][32];
   __shared__ rk_opt::AdamStep s_ks[kEpiGroups];
-  float cur = 0.f;
-  if (a.epi.on) {  // optimizer epilogue: this launch performs the step's Adam update
-    cur = rk_opt::read_step(a.epi.step);
-    if (threadIdx.x < kEpiGroups) s_ks[threadIdx.x] = rk_opt::adam_step(a.epi.hyper[threadIdx.x < a.epi.on ? threadIdx.x : 0], cur + 1.f);
-    __syncthreads();
-  }
+  // optimizer epilogue: the step counter is loaded now but consumed only where each block type
+  // already synchronises (its LDS reduction), so its memory round trip overlaps the gradient loads
+  // instead of preceding them
+  const float cur = a.epi.on ? a.epi.step[0] : 0.f;
+  const StepFill sf{&a, cur, s_ks};
   const rk_opt::AdamStep* ks = a.epi.on ? s_ks : nullptr;
   if ((int)blockIdx.x >= a.tiles) {
-    if ((int)blockIdx.x - a.tiles < a.nslab) slab_reduce_block(a, blockIdx.x - a.tiles, red, ks);
+    if ((int)blockIdx.x - a.tiles < a.nslab) slab_reduce_block(a, blockIdx.x - a.tiles, red, ks, sf);
     else loss_fin_block(a.lf, red);
   } else {
-    wgrad_tile(a, red, rsum, ks);
+    wgrad_tile(a, red, rsum, ks, sf);
   }
   if (a.epi.on) rk_opt::advance_step(a.epi.step, a.epi.counter, false, cur);
 }
 
-__device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks) {
+__device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks,
+                           const StepFill& sf) {
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < 3; ++i)
@@ -450,6 +464,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     rsum[wv][lo] = rs[0];
     rsum[wv][16 + lo] = rs[1];
   }
+  sf();
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < 32 * 32 / NT; ++q) {
