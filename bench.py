@@ -236,7 +236,7 @@ def main() -> int:
                 "input_shape": list(in_shape),
                 "optimizer": ("SGD(momentum)" if args.model.startswith("resnet") else "AdamW") + " + StepLR(100)",
                 "parallelism": f"dp{world}",
-                "impl": ("fused-hip" + ("+hipgraph" if (not args.no_graph and (args.model == "lenet" or args.graph)) else ""))
+                "impl": ("fused-hip" + ("" if args.no_graph else "+hipgraph"))
                 if fused else "torch-eager",
             },
             "wall_s": round(wall, 2),
