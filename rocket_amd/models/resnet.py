@@ -88,7 +88,8 @@ class ResNet(nn.Module):
         if cifar_stem:
             self.stem = nn.Sequential(_conv(3, 64, 3), BatchNormAct2d(64, relu=True))
         else:
-            self.stem = nn.Sequential(_conv(3, 64, 7, 2), BatchNormAct2d(64, relu=True))
+            # BN + ReLU + the 3x3/s2 max-pool in one pass (norm.hip bn_relu_maxpool)
+            self.stem = nn.Sequential(_conv(3, 64, 7, 2), BatchNormAct2d(64, relu=True, maxpool=True))
         cin = 64
         stages = []
         for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
@@ -116,9 +117,7 @@ class ResNet(nn.Module):
         if not torch.is_autocast_enabled(x.device.type):
             x = x.to(self.fc.weight.dtype if hasattr(self, "fc") else self.head.weight.dtype)  # bf16-stored images
         x = x.contiguous(memory_format=torch.channels_last)
-        x = self.stem(x)
-        if not self.cifar_stem:
-            x = F.max_pool2d(x, 3, 2, 1)
+        x = self.stem(x)  # ImageNet stem: the max-pool is inside its BatchNormAct2d
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

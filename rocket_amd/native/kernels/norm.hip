@@ -515,6 +515,52 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
 }
 
+// bn_bwd_reduce's result from per-64-row partials (sum dy', sum dy'*xhat) written by the stride-1
+// conv dgrad that produced dy' (conv.hip store_tile_bnb): "rows" of this launch are the slices.
+__global__ void __launch_bounds__(BN_T) bn_bwd_finalize_kernel(BnBwdArgs a, const float* __restrict__ tp, int ntiles) {
+  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ float s1[BN_CT], s2[BN_CT];
+  __shared__ int flag;
+  const int c0 = blockIdx.x * BN_CT;
+  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int c = c0 + cg * 8;
+  const bool cok = c < a.C;
+  const int cs = cok ? c : 0;
+  const int64_t t0 = (int64_t)blockIdx.y * a.rpb;
+  const int64_t t1e = min((int64_t)ntiles, t0 + a.rpb);
+  float acc1[8], acc2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc1[k] = acc2[k] = 0.f;
+  for (int64_t t = t0 + rg; t < t1e; t += BN_RG) {
+    float sm[8], sq[8];
+    V8<float>::load(tp + t * 2 * a.C + cs, sm);
+    V8<float>::load(tp + t * 2 * a.C + a.C + cs, sq);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      acc1[k] += sm[k];
+      acc2[k] += sq[k];
+    }
+  }
+  if (!cok) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc1[k] = acc2[k] = 0.f;
+  }
+  reduce_rowgroups(acc1, lds, s1);
+  reduce_rowgroups(acc2, lds, s2);
+  float t1, t2;
+  if (!bn_column_reduce(s1, s2, a.part, a.C, c0, a.counters, t1, t2, &flag)) return;
+  const int cc = c0 + (threadIdx.x >> 2);
+  if ((threadIdx.x & 3) == 0 && cc < a.C) {
+    if (a.dbeta) a.dbeta[cc] += t1;
+    if (a.dgamma) a.dgamma[cc] += t2;
+    const float k1 = t1 / (float)a.R, k2 = t2 / (float)a.R;
+    const float sa = a.scale[cc], is = a.invstd[cc], mu = a.mean[cc];
+    a.coef[cc] = sa;
+    a.coef[a.C + cc] = -sa * k2 * is;
+    a.coef[2 * a.C + cc] = sa * (k2 * is * mu - k1);
+  }
+}
+
 // dx = P*dy' + Q*x + S (per-channel coefficients in registers); dres = dy'
 template <typename T, typename TO>
 __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
@@ -758,6 +804,111 @@ __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ 
   }
 }
 
+// ---- BatchNorm + ReLU + 3x3/stride-2/pad-1 max-pool (the ImageNet ResNet stem) -------------------
+// Forward: one thread per (n, oh, ow, 8-channel vector): the nine window pixels are normalised in
+// registers (relu(x*a + b)) and max-reduced; the full-resolution activation never reaches HBM.
+// Per channel a 1-byte code records the window tap (kh*3 + kw) of the max, or 0xFF when the max is
+// 0 (every tap <= 0: ReLU kills the gradient).  Strict '>' keeps the first max, as max_pool2d does.
+// Backward (gather, no atomics): one thread per input pixel vector sums the pooled gradients of
+// the <= 2x2 windows whose code names it; the result is the ReLU-masked gradient of the BN output,
+// handed to bn_bwd with no mask.  256 % (C/8) == 0 (host check): a thread's channel vector is
+// fixed across the grid-stride loop, so the coefficients stay in registers.
+constexpr int MP_T = 256;
+
+template <typename T>
+__global__ void __launch_bounds__(MP_T) bn_relu_maxpool_kernel(const T* __restrict__ x, const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, T* __restrict__ y,
+                                                               uint8_t* __restrict__ code, int N, int H, int W, int C,
+                                                               int OH, int OW) {
+  const int CV = C >> 3;
+  const int64_t total = (int64_t)N * OH * OW * CV;
+  int64_t q = (int64_t)blockIdx.x * MP_T + threadIdx.x;
+  const int cv = (int)(q % CV), c = cv * 8;
+  float A[8], B[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    A[k] = scale[c + k];
+    B[k] = shift[c + k];
+  }
+  for (; q < total; q += (int64_t)gridDim.x * MP_T) {
+    const int64_t p = q / CV;  // output pixel
+    const int ow = (int)(p % OW), oh = (int)((p / OW) % OH), n = (int)(p / ((int64_t)OW * OH));
+    float best[8];
+    unsigned idx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      best[k] = 0.f;
+      idx[k] = 0xFFu;
+    }
+    const int64_t img = (int64_t)n * H * W;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+      if (ih < 0 || ih >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * ow - 1 + kw;
+        if (iw < 0 || iw >= W) continue;
+        float v[8];
+        V8<T>::load(x + (img + (int64_t)ih * W + iw) * C + c, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float o = v[k] * A[k] + B[k];
+          if (o > best[k]) {
+            best[k] = o;
+            idx[k] = (unsigned)(kh * 3 + kw);
+          }
+        }
+      }
+    }
+    V8<T>::store(y + p * C + c, best);
+    *(uint2*)(code + p * C + c) = make_uint2(idx[0] | (idx[1] << 8) | (idx[2] << 16) | (idx[3] << 24),
+                                             idx[4] | (idx[5] << 8) | (idx[6] << 16) | (idx[7] << 24));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(MP_T) maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ code,
+                                                           T* __restrict__ dx, int N, int H, int W, int C, int OH,
+                                                           int OW) {
+  const int CV = C >> 3;
+  const int64_t total = (int64_t)N * H * W * CV;
+  for (int64_t q = (int64_t)blockIdx.x * MP_T + threadIdx.x; q < total; q += (int64_t)gridDim.x * MP_T) {
+    const int c = (int)(q % CV) * 8;
+    const int64_t p = q / CV;  // input pixel
+    const int iw = (int)(p % W), ih = (int)((p / W) % H), n = (int)(p / ((int64_t)W * H));
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const int oh = (ih + 1) / 2 - dh, kh = ih - 2 * oh + 1;
+      if (oh < 0 || oh >= OH || kh > 2) continue;
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int ow = (iw + 1) / 2 - dw, kw = iw - 2 * ow + 1;
+        if (ow < 0 || ow >= OW || kw > 2) continue;
+        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c;
+        const uint2 cd = *(const uint2*)(code + o);
+        float g[8];
+        V8<T>::load(dy + o, g);
+        const unsigned t = (unsigned)(kh * 3 + kw);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const unsigned ck = ((k < 4 ? cd.x : cd.y) >> (8 * (k & 3))) & 0xFFu;
+          acc[k] += ck == t ? g[k] : 0.f;
+        }
+      }
+    }
+    V8<T>::store(dx + p * C + c, acc);
+  }
+}
+
+int mp_grid(int64_t work) {
+  const int64_t b = (work + MP_T - 1) / MP_T;
+  return (int)(b < 256 * 16 ? b : 256 * 16);
+}
+
 int bn_grid_rows(int64_t R, int C, int* rpb) {
   // ~2048 blocks in total (8 per CU: enough loads in flight to stream HBM); the two-level
   // finalize keeps the serial tail short at any block count
@@ -782,6 +933,34 @@ RK_API int64_t rk_bn_workspace(int64_t R, int C) {
 
 // ticket counters needed by one BN reduction launch over C channels (zeroed once, self-resetting)
 RK_API int rk_bn_counters(int C) { return (C + BN_CT - 1) / BN_CT * BN_CNT; }
+
+// Stem BatchNorm + ReLU + 3x3/s2/p1 max-pool over NHWC x [N][H][W][C] -> y, code [N][OH][OW][C]
+RK_API int rk_bn_relu_maxpool(int dt, const void* x, const float* scale, const float* shift, void* y, void* code, int N,
+                              int H, int W, int C, int OH, int OW, hipStream_t s) {
+  if (C % 8 || MP_T % (C / 8) || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return (int)hipErrorInvalidValue;
+  const int g = mp_grid((int64_t)N * OH * OW * (C / 8));
+  if (dt == BF16)
+    bn_relu_maxpool_kernel<uint16_t><<<g, MP_T, 0, s>>>((const uint16_t*)x, scale, shift, (uint16_t*)y,
+                                                         (uint8_t*)code, N, H, W, C, OH, OW);
+  else
+    bn_relu_maxpool_kernel<float><<<g, MP_T, 0, s>>>((const float*)x, scale, shift, (float*)y, (uint8_t*)code, N, H,
+                                                      W, C, OH, OW);
+  return (int)hipGetLastError();
+}
+
+// gradient of rk_bn_relu_maxpool's pool + ReLU: dy [N][OH][OW][C] -> dx [N][H][W][C] (same dtype)
+RK_API int rk_maxpool_bwd(int dt, const void* dy, const void* code, void* dx, int N, int H, int W, int C, int OH,
+                          int OW, hipStream_t s) {
+  if (C % 8 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return (int)hipErrorInvalidValue;
+  const int g = mp_grid((int64_t)N * H * W * (C / 8));
+  if (dt == BF16)
+    maxpool_bwd_kernel<uint16_t><<<g, MP_T, 0, s>>>((const uint16_t*)dy, (const uint8_t*)code, (uint16_t*)dx, N, H,
+                                                     W, C, OH, OW);
+  else
+    maxpool_bwd_kernel<float><<<g, MP_T, 0, s>>>((const float*)dy, (const uint8_t*)code, (float*)dx, N, H, W, C,
+                                                  OH, OW);
+  return (int)hipGetLastError();
+}
 
 // x: [R][C] (dt 0 f32 / 1 bf16). Training statistics + fused scale/shift + running stats.
 RK_API int rk_bn_stats(int dt, const void* x, int64_t R, int C, const float* gamma, const float* beta, float* mean,
@@ -902,6 +1081,35 @@ RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void*
 
 // LayerNorm forward over rows of C (C % 4 == 0, C <= 4096).  dt: x dtype, dto: y dtype.
 // res (dtype dto) / sum_out (dtype dt) may be null: y = LN(x [+ res]), sum_out = x + res
+// BatchNorm backward from the producing dgrad's partials (tp [ntiles][2][C], ntiles = ceil(R / 64)
+// slices): dy is already ReLU-masked, so the input-gradient pass reads no mask.  dt: x / dx dtype,
+// dto: dy / dres dtype.
+RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, const float* tp, int ntiles, int64_t R,
+                              int C, const float* mean, const float* invstd, const float* scale, float* dgamma,
+                              float* dbeta, void* dx, void* dres, float* ws, float* coef, unsigned* counters,
+                              hipStream_t s) {
+  if (C % 8 || C > 8 * BN_T || R <= 0 || ntiles <= 0 || (int64_t)ntiles * 64 < R) return (int)hipErrorInvalidValue;
+  BnBwdArgs a{dy, x, nullptr, R, C, 0, mean, invstd, ws, counters, dgamma, dbeta, scale, coef};
+  int rpb_rows;
+  const int rb_max = bn_grid_rows(R, C, &rpb_rows);  // the workspace rk_bn_workspace(R, C) sized
+  int per = (ntiles + rb_max - 1) / rb_max;
+  per = (per + BN_RG - 1) / BN_RG * BN_RG;
+  a.rpb = per;
+  dim3 grid((C + BN_CT - 1) / BN_CT, (ntiles + per - 1) / per);
+  bn_bwd_finalize_kernel<<<grid, BN_T, 0, s>>>(a, tp, ntiles);
+  int eg;
+  const int erpb = bn_elem_rows(R, C, &eg);
+#define RK_BP(T, TO)                                                                                      \
+  bn_bwd_apply_kernel<T, TO><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x, nullptr, coef, (T*)dx, (TO*)dres, R, C, \
+                                                 erpb)
+  if (dt == BF16 && dto == BF16) RK_BP(uint16_t, uint16_t);
+  else if (dt == BF16) RK_BP(uint16_t, float);
+  else if (dto == BF16) RK_BP(float, uint16_t);
+  else RK_BP(float, float);
+#undef RK_BP
+  return (int)hipGetLastError();
+}
+
 RK_API int rk_ln_fwd(int dt, int dto, const void* x, const void* res, void* sum_out, const float* g, const float* b,
                      void* y, float* mean, float* rstd, int64_t rows, int C, float eps, hipStream_t s) {
   if (C % 4 || C > 64 * 4 * LN_MAXV) return (int)hipErrorInvalidValue;

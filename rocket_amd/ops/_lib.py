@@ -44,6 +44,8 @@ KERNEL_SIGS = {
     "rk_conv_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 11 + [c_void_p, c_void_p]),
     "rk_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_int64, c_int] + [c_void_p] * 9 + [c_float, c_float, c_void_p,
                                                                                             c_void_p, c_void_p]),
+    "rk_conv_dgrad_bn": (c_int, [c_void_p] * 3 + [c_int] * 9 + [c_void_p] * 6),
+    "rk_bn_bwd_partials": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_int] + [c_void_p] * 11),
     "rk_conv_dgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_int] * 11 + [c_void_p]),
     "rk_conv_wgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p, c_void_p]),
     "rk_conv_pool_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 7 + [c_void_p]),
@@ -78,6 +80,8 @@ KERNEL_SIGS = {
     "rk_bn_apply": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int,
                             c_int, c_void_p]),
     "rk_bn_counters": (c_int, [c_int]),
+    "rk_bn_relu_maxpool": (c_int, [c_int] + [c_void_p] * 5 + [c_int] * 6 + [c_void_p]),
+    "rk_maxpool_bwd": (c_int, [c_int] + [c_void_p] * 3 + [c_int] * 6 + [c_void_p]),
     "rk_colsum_acc": (c_int, [c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rk_gelu_bwd_colsum": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),

@@ -23,9 +23,15 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+import os
+
 import rocket_amd.ops as _ops
 from rocket_amd.ops import _lib
 from rocket_amd.ops.lenet import _finish, _grad_targets
+
+
+# ROCKET_BN_BWD_FUSE=0: every BatchNorm backward does its own reduction pass
+BWD_FUSE = os.environ.get("ROCKET_BN_BWD_FUSE", "1") != "0"
 
 
 def _dt(t: torch.Tensor) -> int:
@@ -45,9 +51,16 @@ def _channels_last(x: torch.Tensor) -> torch.Tensor:
     return x.contiguous()
 
 
+# BatchNorm input data_ptr -> (dy data_ptr, dy version, partials, ntiles): backward reductions already
+# done by the stride-1 conv dgrad that produced the BatchNorm output's gradient (iconv.py); consumed
+# (popped) by that BatchNorm's backward when its incoming gradient is exactly that tensor, unmodified.
+_BWD_PARTIALS: dict = {}
+
+
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, partials):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, partials,
+                pool=False, box=None):
         lib = _lib.kernels()
         x = _channels_last(x)
         C = x.shape[1]
@@ -75,6 +88,18 @@ class _BNAct(torch.autograd.Function):
                                        stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
                                        _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(nbt), float(momentum),
                                        float(eps), ws.data_ptr(), counters, s), "rk_bn_stats")
+        if pool:  # stem: relu(bn(x)) max-pooled 3x3/s2/p1 in the same pass (codes instead of a mask)
+            N, _, H, W = x.shape
+            OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+            y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=dev, memory_format=torch.channels_last)
+            code = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=dev)
+            _lib.check(lib.rk_bn_relu_maxpool(_dt(x), x.data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
+                                              y.data_ptr(), code.data_ptr(), N, H, W, C, OH, OW, s),
+                       "rk_bn_relu_maxpool")
+            ctx.params = (weight, bias)
+            ctx.relu, ctx.has_res, ctx.out_dtype, ctx.pool = True, False, x.dtype, True
+            ctx.save_for_backward(x, code, stats)
+            return y
         res = None
         if residual is not None:
             res = _channels_last(residual)
@@ -87,7 +112,10 @@ class _BNAct(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.out_dtype = out_dtype
+        ctx.pool = False
         ctx.save_for_backward(x, mask, stats)
+        if box is not None:  # what a consuming conv's dgrad epilogue needs to do this backward's reduction
+            box.append((x, mask, stats))
         return y
 
     @staticmethod
@@ -98,6 +126,14 @@ class _BNAct(torch.autograd.Function):
         C = x.shape[1]
         dev = x.device
         dy = _channels_last(dy if dy.dtype == ctx.out_dtype else dy.to(ctx.out_dtype))
+        if ctx.pool:  # route the pooled gradient through the codes: the ReLU-masked d(bn output)
+            N, _, H, W = x.shape
+            OH, OW = dy.shape[2], dy.shape[3]
+            dfull = torch.empty_like(x)
+            _lib.check(lib.rk_maxpool_bwd(_dt(x), dy.data_ptr(), mask.data_ptr(), dfull.data_ptr(), N, H, W, C, OH, OW,
+                                          _lib.stream_ptr(dev)), "rk_maxpool_bwd")
+            dy, mask = dfull, None
+        done = _BWD_PARTIALS.pop(x.data_ptr(), None)
         xr, dyr = _rows_view(x), _rows_view(dy)
         R = xr.shape[0]
         params = [p for p in (weight, bias) if p is not None]
@@ -110,30 +146,44 @@ class _BNAct(torch.autograd.Function):
         coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
         nctr = int(lib.rk_bn_counters(C))
         counters = _lib.Workspace.get(dev).counter_array(f"bn{nctr}", nctr)
-        _lib.check(lib.rk_bn_bwd(_dt(x), _dt(dy), dyr.data_ptr(), xr.data_ptr(), _lib.ptr(mask), R, C, stats[0].data_ptr(),
-                                 stats[1].data_ptr(), stats[2].data_ptr(), _lib.ptr(dgamma), _lib.ptr(dbeta),
-                                 _rows_view(dx).data_ptr(), _rows_view(dres).data_ptr() if dres is not None else None,
-                                 ws.data_ptr(), coef.data_ptr(), counters, _lib.stream_ptr(dev)), "rk_bn_bwd")
+        if done is not None and done[0] == dy.data_ptr() and done[1] == dy._version:
+            # dy is the masked gradient the conv dgrad epilogue stored, its reductions are in done[2]
+            _lib.check(lib.rk_bn_bwd_partials(_dt(x), _dt(dy), dyr.data_ptr(), xr.data_ptr(), done[2].data_ptr(),
+                                              done[3], R, C, stats[0].data_ptr(), stats[1].data_ptr(),
+                                              stats[2].data_ptr(), _lib.ptr(dgamma), _lib.ptr(dbeta),
+                                              _rows_view(dx).data_ptr(),
+                                              _rows_view(dres).data_ptr() if dres is not None else None, ws.data_ptr(),
+                                              coef.data_ptr(), counters, _lib.stream_ptr(dev)), "rk_bn_bwd_partials")
+        else:
+            _lib.check(lib.rk_bn_bwd(_dt(x), _dt(dy), dyr.data_ptr(), xr.data_ptr(), _lib.ptr(mask), R, C,
+                                     stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), _lib.ptr(dgamma),
+                                     _lib.ptr(dbeta), _rows_view(dx).data_ptr(),
+                                     _rows_view(dres).data_ptr() if dres is not None else None, ws.data_ptr(),
+                                     coef.data_ptr(), counters, _lib.stream_ptr(dev)), "rk_bn_bwd")
         g = _finish(params, bufs, direct) if params else []
         gw = g[0] if weight is not None else None
         gb = g[-1] if bias is not None else None
-        return dx, gw, gb, dres, None, None, None, None, None, None, None
+        return dx, gw, gb, dres, None, None, None, None, None, None, None, None, None
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
     """``BatchNorm2d`` with optional fused residual add and ReLU: ``relu?(bn(x) + residual?)``."""
 
     def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True, relu=False,
-                 **kw):
+                 maxpool=False, **kw):
         super().__init__(num_features, eps=eps, momentum=momentum, affine=affine,
                          track_running_stats=track_running_stats, **kw)
-        self.relu = relu
+        self.relu = relu or maxpool
+        # ``maxpool``: the ImageNet ResNet stem's max_pool2d(3, 2, 1) after the ReLU, fused into the
+        # same pass (the full-resolution activation is never written)
+        self.maxpool = maxpool
 
     def _fused_ok(self, x, residual) -> bool:
         return (
             _ops.fused_enabled() and x.is_cuda and self.training and x.dim() in (2, 4) and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
             and x.dtype in (torch.float32, torch.bfloat16) and self.momentum is not None
             and (residual is None or residual.shape == x.shape)
+            and (not self.maxpool or (residual is None and x.dim() == 4 and 256 % (x.shape[1] // 8) == 0))
         )
 
     def forward(self, x, residual=None):
@@ -144,17 +194,22 @@ class BatchNormAct2d(nn.BatchNorm2d):
             if partials is not None and not (x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
                                              and partials[0].numel() == 2 * partials[1] * x.shape[1]):
                 partials = None
-            return _BNAct.apply(x, self.weight, self.bias, residual,
-                                self.running_mean if self.track_running_stats else None,
-                                self.running_var if self.track_running_stats else None,
-                                self.num_batches_tracked if self.track_running_stats else None,
-                                self.momentum, self.eps, self.relu, partials)
+            box = [] if (BWD_FUSE and not self.maxpool and x.dim() == 4 and x.dtype == torch.bfloat16) else None
+            y = _BNAct.apply(x, self.weight, self.bias, residual,
+                             self.running_mean if self.track_running_stats else None,
+                             self.running_var if self.track_running_stats else None,
+                             self.num_batches_tracked if self.track_running_stats else None,
+                             self.momentum, self.eps, self.relu, partials, self.maxpool, box)
+            if box:
+                y._rocket_bn_bwd_src = box[0]  # (input, ReLU mask, stats) for a consuming conv's dgrad
+            return y
         if x.is_cuda and self.training and _ops.fused_enabled():
             _lib.kernels()  # a HIP device without the native library is an error, not a fallback
         y = super().forward(x)
         if residual is not None:
             y = y + residual
-        return F.relu(y) if self.relu else y
+        y = F.relu(y) if self.relu else y
+        return F.max_pool2d(y, 3, 2, 1) if self.maxpool else y
 
 
 class _LN(torch.autograd.Function):

@@ -140,3 +140,39 @@ def test_fused_attention_qkv(B, L, H):
     gq, gr = qkv.grad.view(B, L, 3, H * D), ref_in.grad.view(B, L, 3, H * D)
     for i, name in enumerate("qkv"):
         assert _rel(gq[:, :, i], gr[:, :, i]) < 3e-2, (name, _rel(gq[:, :, i], gr[:, :, i]))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 64, 28, 28), (4, 32, 15, 15), (2, 256, 9, 10)])
+def test_batchnorm_relu_maxpool(dtype, shape):
+    """The ResNet stem's BN + ReLU + max_pool2d(3, 2, 1) as one pass (norm.hip bn_relu_maxpool) and its
+    gather-form backward, against the fp32 composition of the three torch ops."""
+    from rocket_amd.ops.norm import BatchNormAct2d
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    C = shape[1]
+    bn = BatchNormAct2d(C, relu=True, maxpool=True).to(dev)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    x = (torch.randn(shape, device=dev) * 2 + 0.5).to(memory_format=torch.channels_last).to(dtype).requires_grad_(True)
+    y = bn(x)
+    OH, OW = (shape[2] - 1) // 2 + 1, (shape[3] - 1) // 2 + 1
+    assert y.shape == (shape[0], C, OH, OW) and y.dtype == dtype
+    gy = torch.randn_like(y)
+    y.backward(gy)
+
+    xr = x.detach().float().requires_grad_(True)
+    w = bn.weight.detach().clone().requires_grad_(True)
+    b = bn.bias.detach().clone().requires_grad_(True)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    ref = F.max_pool2d(F.relu(F.batch_norm(xr, rm, rv, w, b, training=True, momentum=0.1, eps=1e-5)), 3, 2, 1)
+    ref.backward(gy.float())
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(y, ref) < tol
+    assert _rel(bn.running_mean, rm) < 1e-5 and _rel(bn.running_var, rv) < 1e-4
+    gtol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert _rel(x.grad, xr.grad) < gtol
+    assert _rel(bn.weight.grad, w.grad) < gtol
+    assert _rel(bn.bias.grad, b.grad) < gtol
