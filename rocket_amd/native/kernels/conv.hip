@@ -51,6 +51,14 @@ struct ConvGeom {
   float* bnpart;         // forward: per row-tile BatchNorm partials [tiles_m][2][Cout] (tile mean, M2) or null
   int hoff, woff;        // dgrad: dY pixel of grid pixel (gh, gw) at tap (tr, ts) = (gh + hoff - tr, gw + woff - ts)
   int dx_h, dx_w;        // strided dgrad: dX extent (the epilogue's pixel map)
+  // stride-1 dgrad whose dX is the gradient of a BatchNorm(+ReLU) output (ResNet: every conv input
+  // but the stem's): the epilogue applies that BatchNorm's ReLU mask, stores the masked dX and writes
+  // per-64-row partials (sum dX', sum dX' * xhat) of the BatchNorm backward, [tiles][2][C]
+  const uint16_t* bnb_x;   // the BatchNorm's input [M][C] (bf16), or null: no BN epilogue
+  const uint8_t* bnb_mask; // its ReLU mask [M][C/8] (bit k: channel 8*(c/8) + k), or null
+  const float* bnb_mean;
+  const float* bnb_invstd;
+  float* bnb_part;
   int w_s;               // strided dgrad: the weight's full kernel width S (tap index r*S + s)
   int ncls;              // strided dgrad: parity classes in the launch
   int zero_nb;           // strided dgrad, 1x1 kernel: only class (0, 0) has taps; its tiles also zero
@@ -193,6 +201,81 @@ __device__ __forceinline__ void tile_bn_stats(const MArgs& g, const ConvGeom& cg
     for (int j = 0; j < FN; ++j) {
       const int n = col0 + wn * TN + j * 16 + 4 * (lane >> 4);
       if (n < g.N) {  // N % 4 == 0: all four columns in
+        *(float4*)(part + n) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
+        *(float4*)(part + g.N + n) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
+      }
+    }
+  }
+}
+
+// Stride-1 dgrad epilogue fused with the BatchNorm backward's reduction (see ConvGeom::bnb_x):
+// dX' = mask ? dX (+ old dX) : 0, stored bf16; the partial sums use the stored (rounded) values and
+// the BN input at the same pixel, per 64-row wave slice (16-lane xor-shuffle, no LDS).
+template <int FM, int FN>
+__device__ __forceinline__ void store_tile_bnb(const MArgs& g, const ConvGeom& cg, f32x4 (&acc)[FM][FN], int mbase,
+                                               int nbase, int lane, int slice) {
+  const int CB = g.N >> 3;  // mask bytes per row
+  // every side input of the tile first (one round trip; stores to dX could alias them otherwise)
+  uint2 xz[FM][FN], old[FM][FN];
+  unsigned mb[FM][FN];
+  float4 mu[FN], is[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = min(nbase + j * 16 + 4 * (lane >> 4), g.N - 4);
+    mu[j] = *(const float4*)(cg.bnb_mean + n);
+    is[j] = *(const float4*)(cg.bnb_invstd + n);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = min(mbase + i * 16 + (lane & 15), g.M - 1);
+      const int64_t off = (int64_t)m * g.ldc + n;
+      xz[i][j] = *(const uint2*)(cg.bnb_x + off);
+      old[i][j] = g.accumulate ? *(const uint2*)((const uint16_t*)g.c + off) : make_uint2(0u, 0u);
+      mb[i][j] = cg.bnb_mask ? (unsigned)cg.bnb_mask[(int64_t)m * CB + (n >> 3)] >> (n & 7) : 0xFu;
+    }
+  }
+  float s1[FN][4], s2[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = nbase + j * 16 + 4 * (lane >> 4);
+    const float muv[4] = {mu[j].x, mu[j].y, mu[j].z, mu[j].w}, isv[4] = {is[j].x, is[j].y, is[j].z, is[j].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = mbase + i * 16 + (lane & 15);
+      if (n >= g.N || m >= g.M) continue;
+      const uint2 o = old[i][j], xq = xz[i][j];
+      const float v[4] = {acc[i][j][0] + __uint_as_float(o.x << 16), acc[i][j][1] + __uint_as_float(o.x & 0xffff0000u),
+                          acc[i][j][2] + __uint_as_float(o.y << 16), acc[i][j][3] + __uint_as_float(o.y & 0xffff0000u)};
+      const float xv[4] = {__uint_as_float(xq.x << 16), __uint_as_float(xq.x & 0xffff0000u),
+                           __uint_as_float(xq.y << 16), __uint_as_float(xq.y & 0xffff0000u)};
+      uint16_t h[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        h[e] = ((mb[i][j] >> e) & 1u) ? f2bf(v[e]) : (uint16_t)0;
+        const float r = bf2f(h[e]);
+        s1[j][e] += r;
+        s2[j][e] = __builtin_fmaf(r, (xv[e] - muv[e]) * isv[e], s2[j][e]);
+      }
+      *(uint2*)((uint16_t*)g.c + (int64_t)m * g.ldc + n) =
+          make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[j][e] += __shfl_xor(s1[j][e], o, 64);
+        s2[j][e] += __shfl_xor(s2[j][e], o, 64);
+      }
+  if ((lane & 15) == 0) {
+    float* part = cg.bnb_part + (int64_t)slice * 2 * g.N;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nbase + j * 16 + 4 * (lane >> 4);
+      if (n < g.N) {
         *(float4*)(part + n) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
         *(float4*)(part + g.N + n) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
       }
@@ -370,6 +453,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
         }
       }
     }
+  } else if (MODE == kConvDgrad && cg.bnb_x != nullptr) {
+    store_tile_bnb<FM, FN>(g, cg, acc, row0 + wm * TM, col0 + wn * TN, lane, tm * WM + wm);
   } else
     store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split);
 }
@@ -408,6 +493,7 @@ ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stri
   cg.N = N; cg.H = H; cg.W = W; cg.C = C; cg.GH = GH; cg.GW = GW;
   cg.R = R; cg.S = S; cg.stride = stride; cg.pad = pad; cg.taps_c = taps_c;
   cg.w_tap_stride = 0; cg.w_co_stride = 0; cg.bnpart = nullptr;
+  cg.bnb_x = nullptr; cg.bnb_mask = nullptr; cg.bnb_mean = nullptr; cg.bnb_invstd = nullptr; cg.bnb_part = nullptr;
   cg.hoff = cg.woff = pad; cg.dx_h = cg.dx_w = 0; cg.w_s = S; cg.ncls = 0; cg.zero_nb = 0;
   cg.inv_gw = 1.f / (float)GW;
   cg.inv_gh = 1.f / (float)GH;
@@ -445,6 +531,32 @@ RK_API int rk_conv_fwd(const void* x, const void* w, void* y, int y_dt, const fl
 // dX[N*H*W][Cin] (bf16/f32) (+)= conv_transpose(dY, W), stride 1 or 2.  Cout % 64 == 0, Cin % 8 == 0.
 // accumulate: dX += (e.g. the residual-branch gradient already in dX).  Stride 2: the four parity
 // classes of dX pixels as four stride-1 gathers in one launch (classes without taps store zeros).
+// Stride-1 dX of a conv whose input is a BatchNorm(+ReLU) output, fused with that BatchNorm's
+// backward reduction: dX' = relu-mask * dX (+ old dX) is stored (bf16) and part (f32
+// [ceil(N*H*W / 64)][2][Cin]) receives per-64-pixel (sum dX', sum dX' * (x - mean) * invstd) for
+// rk_bn_bwd_partials.  mask may be null (BatchNorm without ReLU).
+RK_API int rk_conv_dgrad_bn(const void* dy, const void* w, void* dx, int accumulate, int N, int H, int W, int Cin,
+                            int Cout, int R, int S, int pad, const void* bn_x, const void* bn_mask, const float* mean,
+                            const float* invstd, float* part, hipStream_t s) {
+  if (Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx) || !aligned16(bn_x) || !part ||
+      !aligned16(mean) || !aligned16(invstd) || !aligned16(part))
+    return (int)hipErrorInvalidValue;
+  const int OH = H + 2 * pad - R + 1, OW = W + 2 * pad - S + 1;
+  if (OH <= 0 || OW <= 0) return (int)hipErrorInvalidValue;
+  const int M = N * H * W, K = R * S * Cout;
+  MArgs g = margs(dy, 0, w, (int64_t)R * S * Cin, dx, BF16, Cin, M, Cin, K);
+  g.accumulate = accumulate;
+  ConvGeom cg = geom(N, OH, OW, Cout, H, W, R, S, 1, pad, Cout);
+  cg.w_tap_stride = Cin;
+  cg.w_co_stride = (int64_t)R * S * Cin;
+  cg.bnb_x = (const uint16_t*)bn_x;
+  cg.bnb_mask = (const uint8_t*)bn_mask;
+  cg.bnb_mean = mean;
+  cg.bnb_invstd = invstd;
+  cg.bnb_part = part;
+  return launch_conv<kConvDgrad>(g, cg, s);
+}
+
 RK_API int rk_conv_dgrad(const void* dy, const void* w, void* dx, int dx_dt, int accumulate, int N, int H, int W,
                          int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, hipStream_t s) {
   if ((stride != 1 && stride != 2) || Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx))

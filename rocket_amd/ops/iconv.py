@@ -90,10 +90,39 @@ def _geo(xc: torch.Tensor, w16: torch.Tensor, stride: int, pad: int):
     return (N, C, H, W, Co, R, S, stride, pad, (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1)
 
 
-def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | None) -> torch.Tensor:
+def _bn_src(x: torch.Tensor, stride: int):
+    """(BatchNorm input, ReLU mask, stats) when ``x`` is a fused BatchNorm's output that a stride-1
+    dgrad can finish the backward reduction of (``norm.py`` ``_rocket_bn_bwd_src``), else None."""
+    src = getattr(x, "_rocket_bn_bwd_src", None)
+    if src is None or stride != 1:
+        return None
+    z = src[0]
+    if z.shape != x.shape or z.dtype != torch.bfloat16 or not z.is_contiguous(memory_format=torch.channels_last):
+        return None
+    return src
+
+
+def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | None, bn=None) -> torch.Tensor:
     """Input gradient of one conv; with ``dx`` given it is ADDED to dx (in place, native epilogue
-    accumulate) and dx is returned."""
+    accumulate) and dx is returned.  ``bn`` (:func:`_bn_src`): the input is that BatchNorm's output —
+    the epilogue also applies its ReLU mask and writes its backward reduction partials, registered
+    for the BatchNorm's backward (``norm._BWD_PARTIALS``)."""
     N, C, H, W, Co, R, S, stride, pad, OH, OW = geo
+    if bn is not None and stride == 1 and Co % 64 == 0 and C % 8 == 0:
+        from rocket_amd.ops.norm import _BWD_PARTIALS
+
+        z, mask, stats = bn
+        acc = dx is not None
+        if dx is None:
+            dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
+        ntiles = -(-(N * H * W) // TILE_ROWS)
+        part = torch.empty(ntiles * 2 * C, dtype=torch.float32, device=dyc.device)
+        _lib.check(_lib.kernels().rk_conv_dgrad_bn(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), int(acc), N, H, W, C,
+                                                   Co, R, S, pad, z.data_ptr(), _lib.ptr(mask), stats[0].data_ptr(),
+                                                   stats[1].data_ptr(), part.data_ptr(), _lib.stream_ptr(dyc.device)),
+                   "rk_conv_dgrad_bn")
+        _BWD_PARTIALS[z.data_ptr()] = (dx.data_ptr(), dx._version, part, ntiles)
+        return dx
     if (stride == 1 or (stride == 2 and SDGRAD == "native" and _sdgrad_ok(R, S, pad))) and Co % 64 == 0:
         acc = dx is not None
         if dx is None:
@@ -127,11 +156,12 @@ def _conv_wgrad(dyc: torch.Tensor, xc: torch.Tensor, weight: torch.Tensor, geo):
 
 class _IConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, w16, stride: int, pad: int, bnpart):
+    def forward(ctx, x, weight, w16, stride: int, pad: int, bnpart, bn=None):
         xc = _cl(x)
         y = _conv_fwd(xc, w16, stride, pad, bnpart)
         ctx.save_for_backward(xc, w16)
         ctx.weight = weight
+        ctx.bn = bn
         ctx.geo = _geo(xc, w16, stride, pad)
         return y
 
@@ -139,9 +169,10 @@ class _IConvFn(torch.autograd.Function):
     def backward(ctx, dy):
         xc, w16 = ctx.saved_tensors
         dyc = _cl(dy)
-        dx = _conv_dgrad(dyc, w16, ctx.geo, None) if ctx.needs_input_grad[0] else None
+        dx = _conv_dgrad(dyc, w16, ctx.geo, None, ctx.bn) if ctx.needs_input_grad[0] else None
         dw = _conv_wgrad(dyc, xc, ctx.weight, ctx.geo) if ctx.needs_input_grad[1] else None
-        return dx, dw, None, None, None, None
+        ctx.bn = None
+        return dx, dw, None, None, None, None, None
 
 
 class _EntryFn(torch.autograd.Function):
@@ -153,7 +184,8 @@ class _EntryFn(torch.autograd.Function):
     dgrad epilogue into the first (the shortcut's gradient for an identity)."""
 
     @staticmethod
-    def forward(ctx, x, wa, wa16, sa, pa, parta, wb, wb16, sb, pb, partb):
+    def forward(ctx, x, wa, wa16, sa, pa, parta, wb, wb16, sb, pb, partb, bn=None):
+        ctx.bn = bn  # conv_a's dgrad is the last write of dx: it finishes x's BatchNorm reduction
         xc = _cl(x)
         ya = _conv_fwd(xc, wa16, sa, pa, parta)
         yb = _conv_fwd(xc, wb16, sb, pb, partb) if wb is not None else xc.view_as(xc)
@@ -176,12 +208,13 @@ class _EntryFn(torch.autograd.Function):
                 # shortcut first: downsample dgrad into a fresh dx / the identity's gradient as dx
                 dx = _conv_dgrad(gbc, wb16, geo_b, None) if wb is not None else gbc
             if gac is not None:
-                dx = _conv_dgrad(gac, wa16, geo_a, dx)
+                dx = _conv_dgrad(gac, wa16, geo_a, dx, ctx.bn)
             if dx is None:
                 dx = torch.zeros_like(xc)
         dwa = _conv_wgrad(gac, xc, wa, geo_a) if need[1] and gac is not None else None
         dwb = _conv_wgrad(gbc, xc, wb, geo_b) if wb is not None and need[6] and gbc is not None else None
-        return dx, dwa, None, None, None, None, dwb, None, None, None, None
+        ctx.bn = None
+        return dx, dwa, None, None, None, None, dwb, None, None, None, None, None
 
 
 def native_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -225,7 +258,8 @@ class IConv2d(nn.Conv2d):
     def forward(self, x):
         if native_ok(self, x):
             w16, part = self._prep(x)
-            return self._attach(_IConvFn.apply(x, self.weight, w16, self.stride[0], self.padding[0], part), part)
+            return self._attach(_IConvFn.apply(x, self.weight, w16, self.stride[0], self.padding[0], part,
+                                               _bn_src(x, self.stride[0])), part)
         return super().forward(x)
 
 
@@ -242,7 +276,7 @@ def conv_entry(x: torch.Tensor, conv_a: nn.Conv2d, conv_b: nn.Conv2d | None):
         ya, yb = _EntryFn.apply(x, conv_a.weight, wa16, conv_a.stride[0], conv_a.padding[0], pa,
                                 conv_b.weight if conv_b is not None else None, wb16,
                                 conv_b.stride[0] if conv_b is not None else 1,
-                                conv_b.padding[0] if conv_b is not None else 0, pb)
+                                conv_b.padding[0] if conv_b is not None else 0, pb, _bn_src(x, conv_a.stride[0]))
         conv_a._attach(ya, pa)
         if conv_b is not None:
             conv_b._attach(yb, pb)

@@ -140,3 +140,61 @@ def test_block_entry_matches_separate(monkeypatch, kind, cin, width, stride):
     assert _rel(dx1, dx2) < 1e-2, _rel(dx1, dx2)
     for a, b in zip(g1, g2):
         assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["bottleneck", "basic"])
+def test_bn_backward_reduction_in_dgrad_epilogue(monkeypatch, kind):
+    """BatchNorm backward reductions done by the consuming stride-1 conv's dgrad epilogue
+    (rk_conv_dgrad_bn + rk_bn_bwd_partials) give the gradients of the two-pass BN backward, through
+    plain convs, block entries with identity / strided shortcuts, and strided convs (fallback)."""
+    import rocket_amd.ops.norm as nm
+    from rocket_amd.models.resnet import BasicBlock, Bottleneck
+    from rocket_amd.ops.norm import BatchNormAct2d
+
+    class Hits(dict):
+        n = 0
+
+        def pop(self, k, d=None):
+            v = super().pop(k, d)
+            Hits.n += v is not None
+            return v
+
+    torch.manual_seed(4)
+    if kind == "bottleneck":
+        net = torch.nn.Sequential(BatchNormAct2d(256, relu=True), Bottleneck(256, 64, 1), Bottleneck(256, 128, 2),
+                                  Bottleneck(512, 128, 1))
+        cin = 256
+    else:
+        net = torch.nn.Sequential(BatchNormAct2d(64, relu=True), BasicBlock(64, 64, 1), BasicBlock(64, 128, 2),
+                                  BasicBlock(128, 128, 1))
+        cin = 64
+    net = net.cuda().to(memory_format=torch.channels_last)
+    for m in net.modules():  # non-trivial affine parameters (the zero-init residual BN too)
+        if isinstance(m, BatchNormAct2d):
+            with torch.no_grad():
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    state = {k: v.clone() for k, v in net.state_dict().items()}
+    x0 = torch.randn(4, cin, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for fuse in (True, False):
+        net.load_state_dict(state)
+        monkeypatch.setattr(nm, "BWD_FUSE", fuse)
+        monkeypatch.setattr(nm, "_BWD_PARTIALS", Hits())
+        Hits.n = 0
+        net.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = net(x)
+        torch.manual_seed(5)
+        g = torch.randn(y.shape, device="cuda").to(y.dtype).contiguous(memory_format=torch.channels_last)
+        y.backward(g)
+        torch.cuda.synchronize()
+        outs.append((y.detach().float(), x.grad.float(), [p.grad.float().clone() for p in net.parameters()], Hits.n))
+        assert len(nm._BWD_PARTIALS) == 0
+    (y1, dx1, g1, hits), (y2, dx2, g2, nohits) = outs
+    assert nohits == 0 and hits >= (7 if kind == "bottleneck" else 4), hits
+    assert _rel(y1, y2) < 1e-3
+    assert _rel(dx1, dx2) < 2e-2, _rel(dx1, dx2)
+    for a, b in zip(g1, g2):
+        assert _rel(a, b) < 2e-2, _rel(a, b)
