@@ -283,6 +283,55 @@ __device__ __forceinline__ void store_tile_bnb(const MArgs& g, const ConvGeom& c
   }
 }
 
+// Row-coalesced bf16 tile store through LDS (plain / accumulate, no bias / activation / split-K):
+// the accumulators are parked in an f32 LDS image and every thread then moves 16-byte (8-channel)
+// row chunks, so a wave instruction covers whole row segments instead of the MFMA layout's 16 rows x
+// 32 bytes (which streamed at about half of HBM bandwidth on the memory-bound 1x1 convs).  One pass
+// per wave row (wm): its TM x BN f32 slice fits in the dead operand stages.  Values are rounded to
+// bf16 once, after the optional accumulate.  Called by all threads after the main loop.
+template <int BM, int BN, int WM, int WN, int FM, int FN, typename RowMap>
+__device__ __forceinline__ void store_tile_lds(const MArgs& g, f32x4 (&acc)[FM][FN], char* smem, int row0, int col0,
+                                               int wm, int wn, int lane, const RowMap& rowmap) {
+  constexpr int TM = BM / WM, TN = BN / WN, LS = BN + 4, NT = 64 * WM * WN, CPR = BN / 8;
+  static_assert(TM * CPR % NT == 0, "whole chunk passes");
+  float* img = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < WM; ++h) {
+    __syncthreads();  // operand stages (h = 0) / the previous slice's image (h > 0) are dead
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          *(f32x4*)(img + (i * 16 + (lane & 15)) * LS + wn * TN + j * 16 + 4 * (lane >> 4)) = acc[i][j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TM * CPR / NT; ++k) {
+      const int q = k * NT + (int)threadIdx.x;
+      const int r = q / CPR, c = (q % CPR) * 8;
+      const int m = row0 + h * TM + r, n = col0 + c;
+      if (m >= g.M || n >= g.N) continue;  // N % 8 == 0: a chunk is all in or all out
+      const f32x4 a = *(const f32x4*)(img + r * LS + c), b = *(const f32x4*)(img + r * LS + c + 4);
+      float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+      uint16_t* dst = (uint16_t*)g.c + rowmap(m) * g.ldc + n;
+      if (g.accumulate) {
+        const uint4 o = *(const uint4*)dst;
+        const uint32_t po[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          v[2 * w] += __uint_as_float(po[w] << 16);
+          v[2 * w + 1] += __uint_as_float(po[w] & 0xffff0000u);
+        }
+      }
+      uint32_t pv[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) pv[w] = (uint32_t)f2bf(v[2 * w]) | ((uint32_t)f2bf(v[2 * w + 1]) << 16);
+      *(uint4*)dst = make_uint4(pv[0], pv[1], pv[2], pv[3]);
+    }
+  }
+}
+
 // dX row of sub-grid pixel m of a strided-dgrad parity class
 struct ClsRow {
   int GH, GW, H, W, py, px;
@@ -432,7 +481,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
   }
   const uint2 nos[FM][FN] = {};
   if constexpr (MODE == kConvDgradS) {
-    store_tile<FM, FN, false, ClsRow>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split, crow);
+    if (g.lds_epi)
+      store_tile_lds<BM, BN, WM, WN, FM, FN>(g, acc, smem, row0, col0, wm, wn, lane, crow);
+    else
+      store_tile<FM, FN, false, ClsRow>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split, crow);
     if (cg0.zero_nb && !g.accumulate) {  // classes without taps: zeros next to this tile's pixels
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -455,6 +507,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
     }
   } else if (MODE == kConvDgrad && cg.bnb_x != nullptr) {
     store_tile_bnb<FM, FN>(g, cg, acc, row0 + wm * TM, col0 + wn * TN, lane, tm * WM + wm);
+  } else if (MODE != kConvWgrad && g.lds_epi) {
+    store_tile_lds<BM, BN, WM, WN, FM, FN>(g, acc, smem, row0, col0, wm, wn, lane, IdRow());
   } else
     store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split);
 }
@@ -511,6 +565,8 @@ MArgs margs(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+int g_lds_epi = 1;  // rk_conv_set_lds_epi
+
 }  // namespace
 
 // Y[N*OH*OW][Cout] (bf16 or f32) = conv(X, W) (+ bias[Cout]).  Cin % 64 == 0, Cout % 8 == 0.
@@ -523,6 +579,7 @@ RK_API int rk_conv_fwd(const void* x, const void* w, void* y, int y_dt, const fl
   const int M = N * OH * OW, K = R * S * Cin;
   MArgs g = margs(x, 0, w, K, y, y_dt, Cout, M, Cout, K);
   g.bias = bias;
+  g.lds_epi = g_lds_epi && y_dt == BF16 && bias == nullptr;
   ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
   cg.bnpart = bnpart;
   return launch_conv<kConvFwd>(g, cg, s);
@@ -531,6 +588,13 @@ RK_API int rk_conv_fwd(const void* x, const void* w, void* y, int y_dt, const fl
 // dX[N*H*W][Cin] (bf16/f32) (+)= conv_transpose(dY, W), stride 1 or 2.  Cout % 64 == 0, Cin % 8 == 0.
 // accumulate: dX += (e.g. the residual-branch gradient already in dX).  Stride 2: the four parity
 // classes of dX pixels as four stride-1 gathers in one launch (classes without taps store zeros).
+// 1 (default): bf16 forward / input-gradient tiles are stored through LDS in row-contiguous 16-byte
+// chunks; 0: straight from the MFMA accumulator layout (A/B switch, ROCKET_CONV_LDS_EPI)
+RK_API int rk_conv_set_lds_epi(int on) {
+  g_lds_epi = on != 0;
+  return 0;
+}
+
 // Stride-1 dX of a conv whose input is a BatchNorm(+ReLU) output, fused with that BatchNorm's
 // backward reduction: dX' = relu-mask * dX (+ old dX) is stored (bf16) and part (f32
 // [ceil(N*H*W / 64)][2][Cin]) receives per-64-pixel (sum dX', sum dX' * (x - mean) * invstd) for
@@ -565,6 +629,7 @@ RK_API int rk_conv_dgrad(const void* dy, const void* w, void* dx, int dx_dt, int
   const int M = N * H * W, K = R * S * Cout;
   MArgs g = margs(dy, 0, w, (int64_t)R * S * Cin, dx, dx_dt, Cin, M, Cin, K);
   g.accumulate = accumulate;
+  g.lds_epi = g_lds_epi && dx_dt == BF16;
   ConvGeom cg = geom(N, OH, OW, Cout, H, W, R, S, stride, pad, Cout);
   cg.w_tap_stride = Cin;
   cg.w_co_stride = (int64_t)R * S * Cin;

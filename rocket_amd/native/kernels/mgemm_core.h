@@ -33,6 +33,7 @@ struct MArgs {
   int epi;
   int accumulate;
   int splitk, k_per_split;
+  int lds_epi;  // conv.hip: bf16 tile stored through LDS in row-contiguous 16-byte chunks
 };
 
 // kmaj image slot swizzle (see header)

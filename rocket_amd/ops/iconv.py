@@ -35,6 +35,19 @@ SDGRAD = os.environ.get("ROCKET_CONV_SDGRAD", "native")
 # residual-block entries (first conv + shortcut) as one autograd node: ROCKET_CONV_ENTRY=0 disables
 ENTRY = os.environ.get("ROCKET_CONV_ENTRY", "1") != "0"
 N_SLOTS = 512  # resident 128x128 conv blocks (2 per CU)
+# bf16 conv outputs / input gradients stored through LDS in row-contiguous chunks (conv.hip
+# store_tile_lds); ROCKET_CONV_LDS_EPI=0 stores straight from the MFMA accumulator layout
+LDS_EPI = os.environ.get("ROCKET_CONV_LDS_EPI", "1") != "0"
+_epi_set = False
+
+
+def _kernels():
+    global _epi_set
+    lib = _lib.kernels()
+    if not _epi_set:
+        lib.rk_conv_set_lds_epi(int(LDS_EPI))
+        _epi_set = True
+    return lib
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:
@@ -78,7 +91,7 @@ def _conv_fwd(xc: torch.Tensor, w16: torch.Tensor, stride: int, pad: int, bnpart
     OH = (H + 2 * pad - R) // stride + 1
     OW = (W + 2 * pad - S) // stride + 1
     y = torch.empty((N, Co, OH, OW), dtype=torch.bfloat16, device=xc.device, memory_format=torch.channels_last)
-    _lib.check(_lib.kernels().rk_conv_fwd(xc.data_ptr(), w16.data_ptr(), y.data_ptr(), 1, None, N, H, W, C, Co, R, S,
+    _lib.check(_kernels().rk_conv_fwd(xc.data_ptr(), w16.data_ptr(), y.data_ptr(), 1, None, N, H, W, C, Co, R, S,
                                            stride, pad, OH, OW, _lib.ptr(bnpart), _lib.stream_ptr(xc.device)),
                "rk_conv_fwd")
     return y
@@ -127,7 +140,7 @@ def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | No
         acc = dx is not None
         if dx is None:
             dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
-        _lib.check(_lib.kernels().rk_conv_dgrad(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), 1, int(acc), N, H, W,
+        _lib.check(_kernels().rk_conv_dgrad(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), 1, int(acc), N, H, W,
                                                 C, Co, R, S, stride, pad, OH, OW, _lib.stream_ptr(dyc.device)),
                    "rk_conv_dgrad")
         return dx
