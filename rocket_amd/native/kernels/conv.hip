@@ -53,7 +53,7 @@ struct ConvGeom {
   int dx_h, dx_w;        // strided dgrad: dX extent (the epilogue's pixel map)
   // stride-1 dgrad whose dX is the gradient of a BatchNorm(+ReLU) output (ResNet: every conv input
   // but the stem's): the epilogue applies that BatchNorm's ReLU mask, stores the masked dX and writes
-  // per-64-row partials (sum dX', sum dX' * xhat) of the BatchNorm backward, [tiles][2][C]
+  // per-128-row-tile partials (sum dX', sum dX' * xhat) of the BatchNorm backward, [tiles][2][C]
   const uint16_t* bnb_x;   // the BatchNorm's input [M][C] (bf16), or null: no BN epilogue
   const uint8_t* bnb_mask; // its ReLU mask [M][C/8] (bit k: channel 8*(c/8) + k), or null
   const float* bnb_mean;
@@ -208,93 +208,36 @@ __device__ __forceinline__ void tile_bn_stats(const MArgs& g, const ConvGeom& cg
   }
 }
 
-// Stride-1 dgrad epilogue fused with the BatchNorm backward's reduction (see ConvGeom::bnb_x):
-// dX' = mask ? dX (+ old dX) : 0, stored bf16; the partial sums use the stored (rounded) values and
-// the BN input at the same pixel, per 64-row wave slice (16-lane xor-shuffle, no LDS).
-template <int FM, int FN>
-__device__ __forceinline__ void store_tile_bnb(const MArgs& g, const ConvGeom& cg, f32x4 (&acc)[FM][FN], int mbase,
-                                               int nbase, int lane, int slice) {
-  const int CB = g.N >> 3;  // mask bytes per row
-  // every side input of the tile first (one round trip; stores to dX could alias them otherwise)
-  uint2 xz[FM][FN], old[FM][FN];
-  unsigned mb[FM][FN];
-  float4 mu[FN], is[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = min(nbase + j * 16 + 4 * (lane >> 4), g.N - 4);
-    mu[j] = *(const float4*)(cg.bnb_mean + n);
-    is[j] = *(const float4*)(cg.bnb_invstd + n);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = min(mbase + i * 16 + (lane & 15), g.M - 1);
-      const int64_t off = (int64_t)m * g.ldc + n;
-      xz[i][j] = *(const uint2*)(cg.bnb_x + off);
-      old[i][j] = g.accumulate ? *(const uint2*)((const uint16_t*)g.c + off) : make_uint2(0u, 0u);
-      mb[i][j] = cg.bnb_mask ? (unsigned)cg.bnb_mask[(int64_t)m * CB + (n >> 3)] >> (n & 7) : 0xFu;
-    }
-  }
-  float s1[FN][4], s2[FN][4];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = nbase + j * 16 + 4 * (lane >> 4);
-    const float muv[4] = {mu[j].x, mu[j].y, mu[j].z, mu[j].w}, isv[4] = {is[j].x, is[j].y, is[j].z, is[j].w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = mbase + i * 16 + (lane & 15);
-      if (n >= g.N || m >= g.M) continue;
-      const uint2 o = old[i][j], xq = xz[i][j];
-      const float v[4] = {acc[i][j][0] + __uint_as_float(o.x << 16), acc[i][j][1] + __uint_as_float(o.x & 0xffff0000u),
-                          acc[i][j][2] + __uint_as_float(o.y << 16), acc[i][j][3] + __uint_as_float(o.y & 0xffff0000u)};
-      const float xv[4] = {__uint_as_float(xq.x << 16), __uint_as_float(xq.x & 0xffff0000u),
-                           __uint_as_float(xq.y << 16), __uint_as_float(xq.y & 0xffff0000u)};
-      uint16_t h[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        h[e] = ((mb[i][j] >> e) & 1u) ? f2bf(v[e]) : (uint16_t)0;
-        const float r = bf2f(h[e]);
-        s1[j][e] += r;
-        s2[j][e] = __builtin_fmaf(r, (xv[e] - muv[e]) * isv[e], s2[j][e]);
-      }
-      *(uint2*)((uint16_t*)g.c + (int64_t)m * g.ldc + n) =
-          make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < FN; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        s1[j][e] += __shfl_xor(s1[j][e], o, 64);
-        s2[j][e] += __shfl_xor(s2[j][e], o, 64);
-      }
-  if ((lane & 15) == 0) {
-    float* part = cg.bnb_part + (int64_t)slice * 2 * g.N;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = nbase + j * 16 + 4 * (lane >> 4);
-      if (n < g.N) {
-        *(float4*)(part + n) = make_float4(s1[j][0], s1[j][1], s1[j][2], s1[j][3]);
-        *(float4*)(part + g.N + n) = make_float4(s2[j][0], s2[j][1], s2[j][2], s2[j][3]);
-      }
-    }
-  }
-}
-
 // Row-coalesced bf16 tile store through LDS (plain / accumulate, no bias / activation / split-K):
 // the accumulators are parked in an f32 LDS image and every thread then moves 16-byte (8-channel)
 // row chunks, so a wave instruction covers whole row segments instead of the MFMA layout's 16 rows x
 // 32 bytes (which streamed at about half of HBM bandwidth on the memory-bound 1x1 convs).  One pass
 // per wave row (wm): its TM x BN f32 slice fits in the dead operand stages.  Values are rounded to
 // bf16 once, after the optional accumulate.  Called by all threads after the main loop.
-template <int BM, int BN, int WM, int WN, int FM, int FN, typename RowMap>
-__device__ __forceinline__ void store_tile_lds(const MArgs& g, f32x4 (&acc)[FM][FN], char* smem, int row0, int col0,
-                                               int wm, int wn, int lane, const RowMap& rowmap) {
+//
+// BNB (stride-1 dgrad, ConvGeom::bnb_x): the stored dX' = ReLU-mask * dX (+ old dX) also feeds the
+// BatchNorm backward's reduction — each thread owns one 8-channel column chunk for the whole tile,
+// reads the BN input / mask byte of its chunks row-contiguously like the store, and the per-thread
+// sums are combined (xor-shuffles over the lanes sharing the chunk, then LDS over the waves) into one
+// [2][BN] partial row per 128-row tile.
+template <int BM, int BN, int WM, int WN, int FM, int FN, bool BNB, typename RowMap>
+__device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& cg, f32x4 (&acc)[FM][FN], char* smem,
+                                               int row0, int col0, int tm, int wm, int wn, int lane,
+                                               const RowMap& rowmap) {
   constexpr int TM = BM / WM, TN = BN / WN, LS = BN + 4, NT = 64 * WM * WN, CPR = BN / 8;
-  static_assert(TM * CPR % NT == 0, "whole chunk passes");
+  static_assert(TM * CPR % NT == 0 && NT % CPR == 0 && CPR <= 64, "whole chunk passes, fixed chunk column");
   float* img = (float*)smem;
+  const int cc = ((int)threadIdx.x % CPR) * 8;  // this thread's chunk column (fixed: NT % CPR == 0)
+  float s1[8], s2[8], mu[8], is[8];
+  if constexpr (BNB) {
+    const int n = min(col0 + cc, g.N - 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = s2[e] = 0.f;
+      mu[e] = cg.bnb_mean[n + e];
+      is[e] = cg.bnb_invstd[n + e];
+    }
+  }
 #pragma unroll
   for (int h = 0; h < WM; ++h) {
     __syncthreads();  // operand stages (h = 0) / the previous slice's image (h > 0) are dead
@@ -308,13 +251,19 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, f32x4 (&acc)[FM][
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < TM * CPR / NT; ++k) {
-      const int q = k * NT + (int)threadIdx.x;
-      const int r = q / CPR, c = (q % CPR) * 8;
-      const int m = row0 + h * TM + r, n = col0 + c;
+      const int r = (k * NT + (int)threadIdx.x) / CPR;
+      const int m = row0 + h * TM + r, n = col0 + cc;
       if (m >= g.M || n >= g.N) continue;  // N % 8 == 0: a chunk is all in or all out
-      const f32x4 a = *(const f32x4*)(img + r * LS + c), b = *(const f32x4*)(img + r * LS + c + 4);
+      const int64_t off = rowmap(m) * g.ldc + n;
+      uint4 xz = make_uint4(0u, 0u, 0u, 0u);
+      unsigned mb = 0xFFu;
+      if constexpr (BNB) {
+        xz = *(const uint4*)(cg.bnb_x + off);
+        if (cg.bnb_mask) mb = cg.bnb_mask[(int64_t)m * (g.N >> 3) + (n >> 3)];
+      }
+      const f32x4 a = *(const f32x4*)(img + r * LS + cc), b = *(const f32x4*)(img + r * LS + cc + 4);
       float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-      uint16_t* dst = (uint16_t*)g.c + rowmap(m) * g.ldc + n;
+      uint16_t* dst = (uint16_t*)g.c + off;
       if (g.accumulate) {
         const uint4 o = *(const uint4*)dst;
         const uint32_t po[4] = {o.x, o.y, o.z, o.w};
@@ -324,10 +273,51 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, f32x4 (&acc)[FM][
           v[2 * w + 1] += __uint_as_float(po[w] & 0xffff0000u);
         }
       }
-      uint32_t pv[4];
+      uint16_t hv[8];
 #pragma unroll
-      for (int w = 0; w < 4; ++w) pv[w] = (uint32_t)f2bf(v[2 * w]) | ((uint32_t)f2bf(v[2 * w + 1]) << 16);
-      *(uint4*)dst = make_uint4(pv[0], pv[1], pv[2], pv[3]);
+      for (int e = 0; e < 8; ++e) hv[e] = ((mb >> e) & 1u) ? f2bf(v[e]) : (uint16_t)0;
+      if constexpr (BNB) {
+        const uint32_t px[4] = {xz.x, xz.y, xz.z, xz.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = __uint_as_float((e & 1) ? (px[e >> 1] & 0xffff0000u) : (px[e >> 1] << 16));
+          const float rr = bf2f(hv[e]);
+          s1[e] += rr;
+          s2[e] = __builtin_fmaf(rr, (x - mu[e]) * is[e], s2[e]);
+        }
+      }
+      *(uint4*)dst = make_uint4((uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16),
+                                (uint32_t)hv[4] | ((uint32_t)hv[5] << 16), (uint32_t)hv[6] | ((uint32_t)hv[7] << 16));
+    }
+  }
+  if constexpr (BNB) {
+    // lanes sharing the chunk column: lane % CPR equal
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    constexpr int NW = WM * WN;
+    float* red = img;  // [NW][2][BN]
+    __syncthreads();   // the last slice's image is dead
+    const int w = (int)threadIdx.x >> 6;
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(w * 2) * BN + cc + e] = s1[e];
+        red[(w * 2 + 1) * BN + cc + e] = s2[e];
+      }
+    }
+    __syncthreads();
+    for (int t = (int)threadIdx.x; t < 2 * BN; t += NT) {
+      const int which = t / BN, c = t % BN;
+      if (col0 + c >= g.N) continue;
+      float u = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) u += red[(ww * 2 + which) * BN + c];
+      cg.bnb_part[((int64_t)tm * 2 + which) * g.N + col0 + c] = u;
     }
   }
 }
@@ -482,7 +472,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
   const uint2 nos[FM][FN] = {};
   if constexpr (MODE == kConvDgradS) {
     if (g.lds_epi)
-      store_tile_lds<BM, BN, WM, WN, FM, FN>(g, acc, smem, row0, col0, wm, wn, lane, crow);
+      store_tile_lds<BM, BN, WM, WN, FM, FN, false>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, crow);
     else
       store_tile<FM, FN, false, ClsRow>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split, crow);
     if (cg0.zero_nb && !g.accumulate) {  // classes without taps: zeros next to this tile's pixels
@@ -506,9 +496,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
       }
     }
   } else if (MODE == kConvDgrad && cg.bnb_x != nullptr) {
-    store_tile_bnb<FM, FN>(g, cg, acc, row0 + wm * TM, col0 + wn * TN, lane, tm * WM + wm);
+    store_tile_lds<BM, BN, WM, WN, FM, FN, true>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, IdRow());
   } else if (MODE != kConvWgrad && g.lds_epi) {
-    store_tile_lds<BM, BN, WM, WN, FM, FN>(g, acc, smem, row0, col0, wm, wn, lane, IdRow());
+    store_tile_lds<BM, BN, WM, WN, FM, FN, false>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, IdRow());
   } else
     store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split);
 }
@@ -597,7 +587,7 @@ RK_API int rk_conv_set_lds_epi(int on) {
 
 // Stride-1 dX of a conv whose input is a BatchNorm(+ReLU) output, fused with that BatchNorm's
 // backward reduction: dX' = relu-mask * dX (+ old dX) is stored (bf16) and part (f32
-// [ceil(N*H*W / 64)][2][Cin]) receives per-64-pixel (sum dX', sum dX' * (x - mean) * invstd) for
+// [ceil(N*H*W / 128)][2][Cin]) receives per-128-pixel (sum dX', sum dX' * (x - mean) * invstd) for
 // rk_bn_bwd_partials.  mask may be null (BatchNorm without ReLU).
 RK_API int rk_conv_dgrad_bn(const void* dy, const void* w, void* dx, int accumulate, int N, int H, int W, int Cin,
                             int Cout, int R, int S, int pad, const void* bn_x, const void* bn_mask, const float* mean,

@@ -515,8 +515,8 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
 }
 
-// bn_bwd_reduce's result from per-64-row partials (sum dy', sum dy'*xhat) written by the stride-1
-// conv dgrad that produced dy' (conv.hip store_tile_bnb): "rows" of this launch are the slices.
+// bn_bwd_reduce's result from per-tile partials (sum dy', sum dy'*xhat) written by the stride-1
+// conv dgrad that produced dy' (conv.hip store_tile_lds<BNB>): "rows" of this launch are the tiles.
 __global__ void __launch_bounds__(BN_T) bn_bwd_finalize_kernel(BnBwdArgs a, const float* __restrict__ tp, int ntiles) {
   __shared__ float lds[BN_RG][BN_CT + 1];
   __shared__ float s1[BN_CT], s2[BN_CT];
@@ -1081,14 +1081,14 @@ RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void*
 
 // LayerNorm forward over rows of C (C % 4 == 0, C <= 4096).  dt: x dtype, dto: y dtype.
 // res (dtype dto) / sum_out (dtype dt) may be null: y = LN(x [+ res]), sum_out = x + res
-// BatchNorm backward from the producing dgrad's partials (tp [ntiles][2][C], ntiles = ceil(R / 64)
-// slices): dy is already ReLU-masked, so the input-gradient pass reads no mask.  dt: x / dx dtype,
+// BatchNorm backward from the producing dgrad's partials (tp [ntiles][2][C], one row per output
+// tile of the dgrad): dy is already ReLU-masked, so the input-gradient pass reads no mask.  dt: x / dx dtype,
 // dto: dy / dres dtype.
 RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, const float* tp, int ntiles, int64_t R,
                               int C, const float* mean, const float* invstd, const float* scale, float* dgamma,
                               float* dbeta, void* dx, void* dres, float* ws, float* coef, unsigned* counters,
                               hipStream_t s) {
-  if (C % 8 || C > 8 * BN_T || R <= 0 || ntiles <= 0 || (int64_t)ntiles * 64 < R) return (int)hipErrorInvalidValue;
+  if (C % 8 || C > 8 * BN_T || R <= 0 || ntiles <= 0) return (int)hipErrorInvalidValue;
   BnBwdArgs a{dy, x, nullptr, R, C, 0, mean, invstd, ws, counters, dgamma, dbeta, scale, coef};
   int rpb_rows;
   const int rb_max = bn_grid_rows(R, C, &rpb_rows);  // the workspace rk_bn_workspace(R, C) sized

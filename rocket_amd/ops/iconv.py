@@ -128,7 +128,7 @@ def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | No
         acc = dx is not None
         if dx is None:
             dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
-        ntiles = -(-(N * H * W) // TILE_ROWS)
+        ntiles = -(-(N * H * W) // 128)  # one partial row per 128-pixel dgrad tile
         part = torch.empty(ntiles * 2 * C, dtype=torch.float32, device=dyc.device)
         _lib.check(_lib.kernels().rk_conv_dgrad_bn(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), int(acc), N, H, W, C,
                                                    Co, R, S, pad, z.data_ptr(), _lib.ptr(mask), stats[0].data_ptr(),

@@ -30,11 +30,11 @@ from rocket_amd.ops import _lib
 from rocket_amd.ops.lenet import _finish, _grad_targets
 
 
-# ROCKET_BN_BWD_FUSE=1: a BatchNorm whose output feeds a stride-1 native conv leaves its backward
-# reduction to that conv's dgrad epilogue (conv.hip store_tile_bnb).  Off by default: measured on
-# ResNet-50 it saves the reduction pass (2.8 -> 0.8 ms/step) but the dgrads grow by as much (the
-# epilogue's extra x / mask reads), net -0.2 ms (profiles/r2_bn_bwd_fusion_ab.md).
-BWD_FUSE = os.environ.get("ROCKET_BN_BWD_FUSE", "0") == "1"
+# ROCKET_BN_BWD_FUSE (default 1): a BatchNorm whose output feeds a stride-1 native conv leaves its
+# backward reduction to that conv's LDS-staged dgrad epilogue (conv.hip store_tile_lds<BNB>), which
+# already holds dy' on chip: the bn_bwd_reduce pass over (dy, x, mask) disappears for 44 of ResNet-50's
+# 53 BatchNorms (9,625 -> 9,900 img/s; profiles/r2_bn_bwd_fusion_ab.md).  0: a separate reduction pass.
+BWD_FUSE = os.environ.get("ROCKET_BN_BWD_FUSE", "1") != "0"
 
 
 def _dt(t: torch.Tensor) -> int:
