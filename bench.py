@@ -146,7 +146,7 @@ def main() -> int:
 
         net = {"resnet18": lambda: models.resnet18(classes), "resnet50": lambda: models.resnet50(classes),
                "vit_b16": lambda: models.vit_b16(classes)}[args.model]()
-        if on_gpu:
+        if on_gpu and args.model.startswith("resnet"):  # NHWC convs; ViT's patch embedding is a GEMM
             net = net.to(memory_format=torch.channels_last)
     if fused:
         from rocket_amd.ops.optim import FusedAdamW, FusedSGD

@@ -22,7 +22,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops.activation import attention_qkv
-from rocket_amd.ops.linear import PatchEmbed
+from rocket_amd.ops.linear import LibLinear, PatchEmbed
 from rocket_amd.ops.mlinear import MLinear, MMlp
 from rocket_amd.ops.norm import FusedLayerNorm
 
@@ -55,6 +55,27 @@ class Block(nn.Module):
         return x, self.mlp(h)
 
 
+class _Embed(torch.autograd.Function):
+    """``cat([cls, patches]).float() + pos`` -> the fp32 residual stream, with a backward that reads
+    d(stream) once for the position gradient (a contiguous reduction over the batch) and takes the
+    [CLS] gradient from its first row (sum over the batch of d(stream)[:, 0] is exactly that row), so
+    no concatenation and no separate bf16 reduction over the expanded [CLS] token."""
+
+    @staticmethod
+    def forward(ctx, patches, cls, pos):
+        B, P, D = patches.shape
+        x = torch.empty(B, P + 1, D, dtype=torch.float32, device=patches.device)
+        x[:, 1:] = patches.float() + pos[:, 1:]
+        x[:, :1] = (cls.float() + pos[:, :1]).expand(B, 1, D)
+        ctx.pdtype = patches.dtype
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        dpos = dx.sum(0, keepdim=True)
+        return dx[:, 1:].to(ctx.pdtype), dpos[:, :1].clone(), dpos
+
+
 class VisionTransformer(nn.Module):
     def __init__(self, img_size=224, patch=16, in_chans=3, num_classes=1000, dim=768, depth=12, heads=12,
                  mlp_ratio=4.0):
@@ -66,7 +87,7 @@ class VisionTransformer(nn.Module):
         self.pos_embed = nn.Parameter(torch.zeros(1, n + 1, dim))
         self.blocks = nn.ModuleList([Block(dim, heads, mlp_ratio) for _ in range(depth)])
         self.norm = FusedLayerNorm(dim, eps=1e-6)
-        self.head = nn.Linear(dim, num_classes)
+        self.head = LibLinear(dim, num_classes)  # nn.Linear; column-sum bias gradient on the GPU
         nn.init.trunc_normal_(self.pos_embed, std=0.02)
         nn.init.trunc_normal_(self.cls_token, std=0.02)
         for m in self.modules():
@@ -78,8 +99,7 @@ class VisionTransformer(nn.Module):
         if not torch.is_autocast_enabled(x.device.type):
             x = x.to(self.fc.weight.dtype if hasattr(self, "fc") else self.head.weight.dtype)  # bf16-stored images
         x = self.patch_embed(x)  # [B, 196, D]
-        x = torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1)
-        x = x.float() + self.pos_embed  # fp32 residual stream
+        x = _Embed.apply(x, self.cls_token, self.pos_embed)  # fp32 residual stream
         pending = None
         for blk in self.blocks:
             x, pending = blk(x, pending)
