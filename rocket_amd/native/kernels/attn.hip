@@ -35,7 +35,9 @@ constexpr int LMAX = 224;        // max tokens: 14 tiles of 16 (7 k-steps of 32)
 constexpr int NT = LMAX / 16;    // 14
 constexpr int NKS = NT / 2;      // 7
 constexpr int RS = D + 8;        // row-major LDS stride (72 bf16 = 144 B: 16-B aligned rows)
-constexpr int NTH = 256;         // 4 waves
+// threads per block (template parameter NTH of each kernel): 4 or 8 waves looping over the head's
+// 16-row tiles (13 at L = 197: 8 waves finish in 2 rounds instead of 4); rk_attn_set_waves
+int g_waves[3] = {8, 8, 8};  // fwd, bwd_q, bwd_kv
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct AttnArgs {
@@ -69,6 +71,7 @@ __device__ __forceinline__ bf16x8 gload_row(const uint16_t* base, int ld, int b,
 }
 
 // stage a head's tokens row-major into [LMAX][RS] (zero rows >= L)
+template <int NTH>
 __device__ __forceinline__ void stage_rows(uint16_t* dst, const uint16_t* src, int ld, int b, int L, int h) {
   for (int i = threadIdx.x; i < LMAX * (D / 8); i += NTH) {
     const int r = i >> 3, c = (i & 7) * 8;
@@ -111,6 +114,7 @@ __device__ __forceinline__ float red4_sum(float v) {
 }
 
 // --------------------------------------------------------------------------------- forward
+template <int NTH>
 __global__ void __launch_bounds__(NTH) attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[LMAX * RS];
@@ -118,13 +122,13 @@ __global__ void __launch_bounds__(NTH) attn_fwd_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
   const int L = a.L;
   const int ntile = (L + 15) / 16;
-  stage_rows(Ks, a.k, a.ld, b, L, h);
-  stage_rows(Vs, a.v, a.ld, b, L, h);
+  stage_rows<NTH>(Ks, a.k, a.ld, b, L, h);
+  stage_rows<NTH>(Vs, a.v, a.ld, b, L, h);
   __syncthreads();
 
   const float sl = a.scale * LOG2E;
   const int64_t bh = (int64_t)b * a.H + h;
-  for (int qt = w; qt < ntile; qt += 4) {
+  for (int qt = w; qt < ntile; qt += NTH / 64) {
     const int q0 = 16 * qt;
     bf16x8 qb[2];  // B operand of S^T = K Q^T: n = query q0 + lo, k = d 32ks + 8hi + j
 #pragma unroll
@@ -184,6 +188,7 @@ __global__ void __launch_bounds__(NTH) attn_fwd_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------- backward: dQ
+template <int NTH>
 __global__ void __launch_bounds__(NTH) attn_bwd_q_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[LMAX * RS];
@@ -191,13 +196,13 @@ __global__ void __launch_bounds__(NTH) attn_bwd_q_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
   const int L = a.L;
   const int ntile = (L + 15) / 16;
-  stage_rows(Ks, a.k, a.ld, b, L, h);
-  stage_rows(Vs, a.v, a.ld, b, L, h);
+  stage_rows<NTH>(Ks, a.k, a.ld, b, L, h);
+  stage_rows<NTH>(Vs, a.v, a.ld, b, L, h);
   __syncthreads();
 
   const float sl = a.scale * LOG2E;
   const int64_t bh = (int64_t)b * a.H + h;
-  for (int qt = w; qt < ntile; qt += 4) {
+  for (int qt = w; qt < ntile; qt += NTH / 64) {
     const int q0 = 16 * qt;
     bf16x8 qb[2], gb[2];  // B operands: n = query q0 + lo, k = d
     float dot = 0.f;      // partial rowsum(dO * O) of query q0 + lo over this lane's 16 d values
@@ -261,6 +266,7 @@ __global__ void __launch_bounds__(NTH) attn_bwd_q_kernel(AttnArgs a) {
 }
 
 // --------------------------------------------------------------------------- backward: dK, dV
+template <int NTH>
 __global__ void __launch_bounds__(NTH) attn_bwd_kv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Qs[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Gs[LMAX * RS];  // dO row-major
@@ -270,8 +276,8 @@ __global__ void __launch_bounds__(NTH) attn_bwd_kv_kernel(AttnArgs a) {
   const int L = a.L;
   const int ntile = (L + 15) / 16;
   const int64_t bh = (int64_t)b * a.H + h;
-  stage_rows(Qs, a.q, a.ld, b, L, h);
-  stage_rows(Gs, a.dout, a.ldo, b, L, h);
+  stage_rows<NTH>(Qs, a.q, a.ld, b, L, h);
+  stage_rows<NTH>(Gs, a.dout, a.ldo, b, L, h);
   for (int i = threadIdx.x; i < LMAX; i += NTH) {
     lse_s[i] = i < L ? a.lse[bh * L + i] : 0.f;
     del_s[i] = i < L ? a.delta[bh * L + i] : 0.f;
@@ -279,7 +285,7 @@ __global__ void __launch_bounds__(NTH) attn_bwd_kv_kernel(AttnArgs a) {
   __syncthreads();
 
   const float sl = a.scale * LOG2E;
-  for (int kt = w; kt < ntile; kt += 4) {
+  for (int kt = w; kt < ntile; kt += NTH / 64) {
     const int k0 = 16 * kt;
     bf16x8 kb[2], vb[2];  // B operands of S = Q K^T and dP = dO V^T: n = key k0 + lo, k = d
 #pragma unroll
@@ -343,6 +349,16 @@ __global__ void __launch_bounds__(NTH) attn_bwd_kv_kernel(AttnArgs a) {
 
 RK_API int rk_attn_max_len() { return LMAX; }
 
+// waves per block (4 or 8) of the forward, dQ and dK/dV kernels (A/B switch: ROCKET_ATTN_WAVES)
+RK_API int rk_attn_set_waves(int fwd, int bwd_q, int bwd_kv) {
+  const int w[3] = {fwd, bwd_q, bwd_kv};
+  for (int i = 0; i < 3; ++i) {
+    if (w[i] != 4 && w[i] != 8) return (int)hipErrorInvalidValue;
+    g_waves[i] = w[i];
+  }
+  return 0;
+}
+
 // q/k/v: bf16 token-major (row stride ld elements), out: [B*L][ldo] with head h at column h*64;
 // lse: [B*H][L] f32.  head dim 64, L <= 224.
 RK_API int rk_attn_fwd(const void* q, const void* k, const void* v, int ld, void* out, int ldo, float* lse, int B,
@@ -352,7 +368,8 @@ RK_API int rk_attn_fwd(const void* q, const void* k, const void* v, int ld, void
   a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v;
   a.out = (uint16_t*)out; a.lse = lse; a.ld = ld; a.ldo = ldo; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);  // one block per (batch, head)
-  attn_fwd_kernel<<<grid, NTH, 0, s>>>(a);
+  if (g_waves[0] == 8) attn_fwd_kernel<512><<<grid, 512, 0, s>>>(a);
+  else attn_fwd_kernel<256><<<grid, 256, 0, s>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -369,7 +386,9 @@ RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, cons
   a.lse = (float*)lse; a.delta = delta;
   a.ld = ld; a.ldo = ldo; a.ldg = ldg; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);
-  attn_bwd_q_kernel<<<grid, NTH, 0, s>>>(a);
-  attn_bwd_kv_kernel<<<grid, NTH, 0, s>>>(a);
+  if (g_waves[1] == 8) attn_bwd_q_kernel<512><<<grid, 512, 0, s>>>(a);
+  else attn_bwd_q_kernel<256><<<grid, 256, 0, s>>>(a);
+  if (g_waves[2] == 8) attn_bwd_kv_kernel<512><<<grid, 512, 0, s>>>(a);
+  else attn_bwd_kv_kernel<256><<<grid, 256, 0, s>>>(a);
   return (int)hipGetLastError();
 }

@@ -14,6 +14,7 @@
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -88,10 +89,24 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return torch.matmul(p, v)
 
 
+# waves per (batch, head) block of the attention kernels: fwd,bwd_q,bwd_kv (4 or 8 each)
+ATTN_WAVES = tuple(int(v) for v in os.environ.get("ROCKET_ATTN_WAVES", "8,8,8").split(","))
+_waves_set = False
+
+
+def _attn_lib():
+    global _waves_set
+    lib = _lib.kernels()
+    if not _waves_set:
+        _lib.check(lib.rk_attn_set_waves(*ATTN_WAVES), "rk_attn_set_waves")
+        _waves_set = True
+    return lib
+
+
 class _AttnQKV(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, heads: int, scale: float):
-        lib = _lib.kernels()
+        lib = _attn_lib()
         qkv = qkv.contiguous()
         B, L, C3 = qkv.shape
         HD = C3 // 3
@@ -106,7 +121,7 @@ class _AttnQKV(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        lib = _lib.kernels()
+        lib = _attn_lib()
         qkv, out, lse = ctx.saved_tensors
         heads, scale = ctx.cfg
         B, L, C3 = qkv.shape
