@@ -162,7 +162,7 @@ def main() -> int:
     sched = torch.optim.lr_scheduler.StepLR(opt, 100)
     # step-time p50 from timing events every `stride` steps (an event per ~80 us LeNet step would
     # itself cost ~5 us of queue time); the headline number is the barrier/sync-bracketed wall time
-    stride = max(5, args.steps // 50) if args.model == "lenet" else 1
+    stride = max(10, args.steps // 50) if args.model == "lenet" else 1
     timer = StepTimer(warmup=args.warmup, steps=args.steps, stride=stride)
     launcher = rocket.Launcher(
         [
