@@ -257,7 +257,18 @@ __global__ void __launch_bounds__(256) mgemm_reduce(const float* __restrict__ sl
     const int64_t e = q * 4;
     const int m = (int)(e / N), n = (int)(e % N);
     float4 v = *(const float4*)(slab + e);
-    for (int s = 1; s < splitk; ++s) {
+    int s = 1;
+    for (; s + 3 < splitk; s += 4) {  // four independent slab loads in flight per thread
+      const float4 w0 = *(const float4*)(slab + s * plane + e);
+      const float4 w1 = *(const float4*)(slab + (s + 1) * plane + e);
+      const float4 w2 = *(const float4*)(slab + (s + 2) * plane + e);
+      const float4 w3 = *(const float4*)(slab + (s + 3) * plane + e);
+      v.x += (w0.x + w1.x) + (w2.x + w3.x);
+      v.y += (w0.y + w1.y) + (w2.y + w3.y);
+      v.z += (w0.z + w1.z) + (w2.z + w3.z);
+      v.w += (w0.w + w1.w) + (w2.w + w3.w);
+    }
+    for (; s < splitk; ++s) {
       const float4 w = *(const float4*)(slab + s * plane + e);
       v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
     }
