@@ -144,20 +144,21 @@ class _BNAct(torch.autograd.Function):
         dgamma = bufs[0] if weight is not None else None
         dbeta = bufs[-1] if bias is not None else None
         dx = torch.empty_like(x)
-        dres = torch.empty_like(dy) if ctx.has_res else None
         ws = torch.empty(int(lib.rk_bn_workspace(R, C)), dtype=torch.float32, device=dev)
         coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
         nctr = int(lib.rk_bn_counters(C))
         counters = _lib.Workspace.get(dev).counter_array(f"bn{nctr}", nctr)
         if done is not None and done[0] == dy.data_ptr() and done[1] == dy._version:
-            # dy is the masked gradient the conv dgrad epilogue stored, its reductions are in done[2]
+            # dy is the masked gradient the conv dgrad epilogue stored, its reductions are in done[2];
+            # the residual's gradient IS that masked dy: handed on as is, not copied
+            dres = dy if ctx.has_res else None
             _lib.check(lib.rk_bn_bwd_partials(_dt(x), _dt(dy), dyr.data_ptr(), xr.data_ptr(), done[2].data_ptr(),
                                               done[3], R, C, stats[0].data_ptr(), stats[1].data_ptr(),
                                               stats[2].data_ptr(), _lib.ptr(dgamma), _lib.ptr(dbeta),
-                                              _rows_view(dx).data_ptr(),
-                                              _rows_view(dres).data_ptr() if dres is not None else None, ws.data_ptr(),
+                                              _rows_view(dx).data_ptr(), None, ws.data_ptr(),
                                               coef.data_ptr(), counters, _lib.stream_ptr(dev)), "rk_bn_bwd_partials")
         else:
+            dres = torch.empty_like(dy) if ctx.has_res else None
             _lib.check(lib.rk_bn_bwd(_dt(x), _dt(dy), dyr.data_ptr(), xr.data_ptr(), _lib.ptr(mask), R, C,
                                      stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), _lib.ptr(dgamma),
                                      _lib.ptr(dbeta), _rows_view(dx).data_ptr(),
