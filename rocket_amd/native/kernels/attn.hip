@@ -37,7 +37,7 @@ constexpr int NKS = NT / 2;      // 7
 constexpr int RS = D + 8;        // row-major LDS stride (72 bf16 = 144 B: 16-B aligned rows)
 // threads per block (template parameter NTH of each kernel): 4 or 8 waves looping over the head's
 // 16-row tiles (13 at L = 197: 8 waves finish in 2 rounds instead of 4); rk_attn_set_waves
-int g_waves[3] = {8, 8, 8};  // fwd, bwd_q, bwd_kv
+int g_waves[3] = {8, 82, 82};  // fwd, bwd_q, bwd_kv (82: 8 waves bounded to 128 VGPRs, 2 blocks/CU)
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct AttnArgs {
@@ -114,8 +114,8 @@ __device__ __forceinline__ float red4_sum(float v) {
 }
 
 // --------------------------------------------------------------------------------- forward
-template <int NTH>
-__global__ void __launch_bounds__(NTH) attn_fwd_kernel(AttnArgs a) {
+template <int NTH, int MINW = 1>  // MINW: minimum waves per SIMD (launch_bounds)
+__global__ void __launch_bounds__(NTH, MINW) attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[LMAX * RS];
   const int b = blockIdx.z, h = blockIdx.y;
@@ -188,8 +188,8 @@ __global__ void __launch_bounds__(NTH) attn_fwd_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------- backward: dQ
-template <int NTH>
-__global__ void __launch_bounds__(NTH) attn_bwd_q_kernel(AttnArgs a) {
+template <int NTH, int MINW = 1>  // MINW: minimum waves per SIMD (launch_bounds)
+__global__ void __launch_bounds__(NTH, MINW) attn_bwd_q_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[LMAX * RS];
   const int b = blockIdx.z, h = blockIdx.y;
@@ -266,8 +266,8 @@ __global__ void __launch_bounds__(NTH) attn_bwd_q_kernel(AttnArgs a) {
 }
 
 // --------------------------------------------------------------------------- backward: dK, dV
-template <int NTH>
-__global__ void __launch_bounds__(NTH) attn_bwd_kv_kernel(AttnArgs a) {
+template <int NTH, int MINW = 1>  // MINW: minimum waves per SIMD (launch_bounds)
+__global__ void __launch_bounds__(NTH, MINW) attn_bwd_kv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Qs[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Gs[LMAX * RS];  // dO row-major
   __shared__ float lse_s[LMAX], del_s[LMAX];
@@ -353,7 +353,7 @@ RK_API int rk_attn_max_len() { return LMAX; }
 RK_API int rk_attn_set_waves(int fwd, int bwd_q, int bwd_kv) {
   const int w[3] = {fwd, bwd_q, bwd_kv};
   for (int i = 0; i < 3; ++i) {
-    if (w[i] != 4 && w[i] != 8) return (int)hipErrorInvalidValue;
+    if (w[i] != 4 && w[i] != 8 && w[i] != 82) return (int)hipErrorInvalidValue;  // 82: 8 waves, >= 4 waves per SIMD (2 blocks/CU)
     g_waves[i] = w[i];
   }
   return 0;
@@ -368,7 +368,8 @@ RK_API int rk_attn_fwd(const void* q, const void* k, const void* v, int ld, void
   a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v;
   a.out = (uint16_t*)out; a.lse = lse; a.ld = ld; a.ldo = ldo; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);  // one block per (batch, head)
-  if (g_waves[0] == 8) attn_fwd_kernel<512><<<grid, 512, 0, s>>>(a);
+  if (g_waves[0] == 82) attn_fwd_kernel<512, 4><<<grid, 512, 0, s>>>(a);
+  else if (g_waves[0] == 8) attn_fwd_kernel<512><<<grid, 512, 0, s>>>(a);
   else attn_fwd_kernel<256><<<grid, 256, 0, s>>>(a);
   return (int)hipGetLastError();
 }
@@ -386,9 +387,11 @@ RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, cons
   a.lse = (float*)lse; a.delta = delta;
   a.ld = ld; a.ldo = ldo; a.ldg = ldg; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);
-  if (g_waves[1] == 8) attn_bwd_q_kernel<512><<<grid, 512, 0, s>>>(a);
+  if (g_waves[1] == 82) attn_bwd_q_kernel<512, 4><<<grid, 512, 0, s>>>(a);
+  else if (g_waves[1] == 8) attn_bwd_q_kernel<512><<<grid, 512, 0, s>>>(a);
   else attn_bwd_q_kernel<256><<<grid, 256, 0, s>>>(a);
-  if (g_waves[2] == 8) attn_bwd_kv_kernel<512><<<grid, 512, 0, s>>>(a);
+  if (g_waves[2] == 82) attn_bwd_kv_kernel<512, 4><<<grid, 512, 0, s>>>(a);
+  else if (g_waves[2] == 8) attn_bwd_kv_kernel<512><<<grid, 512, 0, s>>>(a);
   else attn_bwd_kv_kernel<256><<<grid, 256, 0, s>>>(a);
   return (int)hipGetLastError();
 }

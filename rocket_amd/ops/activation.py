@@ -89,8 +89,9 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return torch.matmul(p, v)
 
 
-# waves per (batch, head) block of the attention kernels: fwd,bwd_q,bwd_kv (4 or 8 each)
-ATTN_WAVES = tuple(int(v) for v in os.environ.get("ROCKET_ATTN_WAVES", "8,8,8").split(","))
+# waves per (batch, head) block of the attention kernels: fwd,bwd_q,bwd_kv (4 or 8 each; 82 = 8 waves
+# register-bounded to 128 VGPRs so two blocks share a CU; profiles/r2_attn_waves_ab.txt)
+ATTN_WAVES = tuple(int(v) for v in os.environ.get("ROCKET_ATTN_WAVES", "8,82,82").split(","))
 _waves_set = False
 
 
