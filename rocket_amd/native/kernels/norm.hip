@@ -712,7 +712,7 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
   const int64_t re = min(rows, rb + rows_per_block);
   for (int64_t row = rb + w; row < re; row += LN_W) {
     const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[NV][4], gy[NV][4];
+    float xh[NV][4], gy[NV][4], ds[NV][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
@@ -721,6 +721,7 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
         float xv[4], dv[4];
         ld4<T>(x + row * C + c, xv);
         ld4<TO>(dy + row * C + c, dv);
+        if (dsum) ld4<T>(dsum + row * C + c, ds[j]);  // in flight with x / dy, not after the reductions
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           xh[j][k] = (xv[k] - mean) * rstd;
@@ -742,10 +743,8 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
 #pragma unroll
         for (int k = 0; k < 4; ++k) o[k] = rstd * (gy[j][k] - s1 - xh[j][k] * s2);
         if (dsum) {  // the residual stream's own gradient joins here (fused add-norm)
-          float d[4];
-          ld4<T>(dsum + row * C + c, d);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) o[k] += d[k];
+          for (int k = 0; k < 4; ++k) o[k] += ds[j][k];
         }
         st4<T>(dx + row * C + c, o);
         if (dres) st4<TO>(dres + row * C + c, o);  // gradient of the added branch
@@ -1133,7 +1132,7 @@ RK_API int rk_ln_fwd(int dt, int dto, const void* x, const void* res, void* sum_
   return (int)hipGetLastError();
 }
 
-constexpr int LN_BWD_RPB = 32;
+constexpr int LN_BWD_RPB = 16;  // rows per block (4 per wave): ~1600 blocks for ViT's 25k rows
 
 RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
   const int64_t rpb = LN_BWD_RPB;
