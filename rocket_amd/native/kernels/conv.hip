@@ -675,8 +675,6 @@ RK_API int rk_conv_wgrad(const void* dy, const void* x, float* dw, int accumulat
   ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
   int rc = launch_conv<kConvWgrad>(g, cg, s);
   if (rc || splitk == 1) return rc;
-  const int64_t nq = (int64_t)Cout * Ncol / 4;
-  const int blocks = (int)std::min<int64_t>((nq + 255) / 256, 4096);
-  mgemm_reduce<<<blocks, 256, 0, s>>>(slab, splitk, Cout, Ncol, nullptr, dw, F32, Ncol, accumulate);
+  launch_mgemm_reduce(slab, splitk, Cout, Ncol, nullptr, dw, F32, Ncol, accumulate, s);
   return (int)hipGetLastError();
 }

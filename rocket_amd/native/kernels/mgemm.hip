@@ -886,8 +886,6 @@ RK_API int rk_mgemm(const void* a, int64_t lda, int a_kmaj, const void* b, int64
     default: rc = launch_tile<128, 128, 32, 4, 2, 4, 2>(g, a_kmaj, b_kmaj, s); break;
   }
   if (rc || splitk == 1) return rc;
-  const int64_t nq = (int64_t)M * N / 4;
-  const int blocks = (int)std::min<int64_t>((nq + 255) / 256, 4096);
-  mgemm_reduce<<<blocks, 256, 0, s>>>(slab, splitk, M, N, bias, c, c_dt, ldc, accumulate);
+  launch_mgemm_reduce(slab, splitk, M, N, bias, c, c_dt, ldc, accumulate, s);
   return (int)hipGetLastError();
 }

@@ -247,31 +247,44 @@ __device__ __forceinline__ void store_tile(const MArgs& g, f32x4 (&acc)[FM][FN],
   }
 }
 
-// C[m][n] (+)= sum_s slab[s][m][n] + bias[n]  (f32 or bf16 C; N % 4 == 0)
+// C[m][n] (+)= sum_s slab[s][m][n] + bias[n]  (f32 or bf16 C; N % 4 == 0).  G consecutive lanes share
+// one output float4, lane g summing the slabs s = g, g + G, ... (four loads in flight), combined by
+// xor-shuffles: small outputs with many splits (ResNet wgrads: 9k float4 x 32 splits) get G-fold more
+// loads in flight instead of a long serial slab loop per thread.  Fixed order: deterministic.
+template <int G>
 __global__ void __launch_bounds__(256) mgemm_reduce(const float* __restrict__ slab, int splitk, int M, int N,
                                                     const float* __restrict__ bias, void* c, int c_dt, int64_t ldc,
                                                     int accumulate) {
   const int64_t nq = (int64_t)M * N / 4;
   const int64_t plane = (int64_t)M * N;
-  for (int64_t q = blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+  const int g = (int)(threadIdx.x % G);
+  for (int64_t q = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G; q < nq; q += (int64_t)gridDim.x * (256 / G)) {
     const int64_t e = q * 4;
-    const int m = (int)(e / N), n = (int)(e % N);
-    float4 v = *(const float4*)(slab + e);
-    int s = 1;
-    for (; s + 3 < splitk; s += 4) {  // four independent slab loads in flight per thread
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    int s = g;
+    for (; s + 3 * G < splitk; s += 4 * G) {  // four independent slab loads in flight per lane
       const float4 w0 = *(const float4*)(slab + s * plane + e);
-      const float4 w1 = *(const float4*)(slab + (s + 1) * plane + e);
-      const float4 w2 = *(const float4*)(slab + (s + 2) * plane + e);
-      const float4 w3 = *(const float4*)(slab + (s + 3) * plane + e);
+      const float4 w1 = *(const float4*)(slab + (s + G) * plane + e);
+      const float4 w2 = *(const float4*)(slab + (s + 2 * G) * plane + e);
+      const float4 w3 = *(const float4*)(slab + (s + 3 * G) * plane + e);
       v.x += (w0.x + w1.x) + (w2.x + w3.x);
       v.y += (w0.y + w1.y) + (w2.y + w3.y);
       v.z += (w0.z + w1.z) + (w2.z + w3.z);
       v.w += (w0.w + w1.w) + (w2.w + w3.w);
     }
-    for (; s < splitk; ++s) {
+    for (; s < splitk; s += G) {
       const float4 w = *(const float4*)(slab + s * plane + e);
       v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
     }
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) {
+      v.x += __shfl_xor(v.x, o, 64);
+      v.y += __shfl_xor(v.y, o, 64);
+      v.z += __shfl_xor(v.z, o, 64);
+      v.w += __shfl_xor(v.w, o, 64);
+    }
+    if (g != 0) continue;
+    const int m = (int)(e / N), n = (int)(e % N);
     if (bias) {
       const float4 b = *(const float4*)(bias + n);
       v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
@@ -294,6 +307,19 @@ __global__ void __launch_bounds__(256) mgemm_reduce(const float* __restrict__ sl
       }
       *(float4*)o = v;
     }
+  }
+}
+
+// launch the split-K combine: 4 lanes per output float4 once there are >= 8 slabs
+inline void launch_mgemm_reduce(const float* slab, int splitk, int M, int N, const float* bias, void* c, int c_dt,
+                                int64_t ldc, int accumulate, hipStream_t s) {
+  const int64_t nq = (int64_t)M * N / 4;
+  if (splitk >= 8) {
+    const int blocks = (int)std::min<int64_t>((nq * 4 + 255) / 256, 8192);
+    mgemm_reduce<4><<<blocks, 256, 0, s>>>(slab, splitk, M, N, bias, c, c_dt, ldc, accumulate);
+  } else {
+    const int blocks = (int)std::min<int64_t>((nq + 255) / 256, 4096);
+    mgemm_reduce<1><<<blocks, 256, 0, s>>>(slab, splitk, M, N, bias, c, c_dt, ldc, accumulate);
   }
 }
 

@@ -33,6 +33,7 @@ constexpr int BN_GS = 16;        // row blocks per first-level finalize group
 constexpr int BN_MAXRB = 2048;   // row blocks per column (upper bound)
 constexpr int BN_CNT = 1 + BN_MAXRB / BN_GS;  // ticket counters per column: column + groups
 constexpr int BN_ROWQ = BN_US * BN_RG;       // row-block granularity (multiple of both unrolls)
+constexpr int BN_FU = 4;                     // partial-tile rows in flight per thread (finalize launches)
 
 template <typename T> struct V8;
 template <> struct V8<uint16_t> {
@@ -254,15 +255,24 @@ __global__ void __launch_bounds__(BN_T) bn_finalize_kernel(BnStatsArgs a, const 
     piv[k] /= n0;
     acc1[k] = acc2[k] = 0.f;
   }
-  for (int64_t t = t0 + rg; t < t1e; t += BN_RG) {
-    float sm[8], sq[8];
-    V8<float>::load(tp + t * 2 * a.C + cs, sm);
-    V8<float>::load(tp + t * 2 * a.C + a.C + cs, sq);
-    const float n = (float)min((int64_t)tile_rows, a.R - t * tile_rows);
+  for (int64_t t = t0 + rg; t < t1e; t += BN_FU * BN_RG) {  // BN_FU tiles' loads in flight per thread
+    float sm[BN_FU][8], sq[BN_FU][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      acc1[k] += sm[k] - n * piv[k];
-      acc2[k] += sq[k] - 2.f * piv[k] * sm[k] + n * piv[k] * piv[k];
+    for (int u = 0; u < BN_FU; ++u) {
+      const int64_t tu = min(t + u * BN_RG, t1e - 1);
+      V8<float>::load(tp + tu * 2 * a.C + cs, sm[u]);
+      V8<float>::load(tp + tu * 2 * a.C + a.C + cs, sq[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_FU; ++u) {
+      const int64_t tu = t + u * BN_RG;
+      const float n = tu < t1e ? (float)min((int64_t)tile_rows, a.R - tu * tile_rows) : 0.f;
+      const float on = tu < t1e ? 1.f : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc1[k] += on * sm[u][k] - n * piv[k];
+        acc2[k] += on * (sq[u][k] - 2.f * piv[k] * sm[u][k]) + n * piv[k] * piv[k];
+      }
     }
   }
   if (!cok) {
@@ -531,14 +541,22 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_finalize_kernel(BnBwdArgs a, cons
   float acc1[8], acc2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc1[k] = acc2[k] = 0.f;
-  for (int64_t t = t0 + rg; t < t1e; t += BN_RG) {
-    float sm[8], sq[8];
-    V8<float>::load(tp + t * 2 * a.C + cs, sm);
-    V8<float>::load(tp + t * 2 * a.C + a.C + cs, sq);
+  for (int64_t t = t0 + rg; t < t1e; t += BN_FU * BN_RG) {  // BN_FU tiles' loads in flight per thread
+    float sm[BN_FU][8], sq[BN_FU][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      acc1[k] += sm[k];
-      acc2[k] += sq[k];
+    for (int u = 0; u < BN_FU; ++u) {
+      const int64_t tu = min(t + u * BN_RG, t1e - 1);
+      V8<float>::load(tp + tu * 2 * a.C + cs, sm[u]);
+      V8<float>::load(tp + tu * 2 * a.C + a.C + cs, sq[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_FU; ++u) {
+      const float on = t + u * BN_RG < t1e ? 1.f : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc1[k] += on * sm[u][k];
+        acc2[k] += on * sq[u][k];
+      }
     }
   }
   if (!cok) {

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Multi-lane split-K combine: GEMM / conv numerics, ResNet benches, ResNet-18 trace.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest tests/kernels/test_mgemm.py tests/kernels/test_iconv.py tests/kernels/test_norm.py tests/kernels/test_linear_conv.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/red2_tests.log 2>&1 || exit 1
+for m in resnet18 resnet50; do
+  timeout -k 10 300 python bench.py --model $m --steps 20 --warmup 5 >> gpurun_out/red2_bench.jsonl 2> gpurun_out/red2_bench.err || exit 1
+done
+MODELS="resnet18" bash scripts/gpu_prof_models.sh
