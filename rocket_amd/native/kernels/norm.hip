@@ -664,18 +664,25 @@ __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const T* __restrict__ x, c
   const int64_t row = (int64_t)blockIdx.x * LN_W + (threadIdx.x >> 6);
   if (row >= rows) return;
   const T* xr = x + row * C;
-  float v[NV][4];
+  float v[NV][4], r[NV][4], ga[NV][4], be[NV][4];
   float s = 0.f;
+  // every load of the row (x, the residual branch, gamma / beta) is issued before any use
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * 64 + lane) * 4;
+    const int cc = c < C ? c : 0;
+    ld4<T>(xr + cc, v[j]);
+    if (res) ld4<TO>(res + row * C + cc, r[j]);
+    if (g) ld4<float>(g + cc, ga[j]);
+    if (b) ld4<float>(b + cc, be[j]);
+  }
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c = (j * 64 + lane) * 4;
     if (c < C) {
-      ld4<T>(xr + c, v[j]);
       if (res) {  // fused residual add: s = x + branch, written once for the next residual
-        float r[4];
-        ld4<TO>(res + row * C + c, r);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[j][k] += r[k];
+        for (int k = 0; k < 4; ++k) v[j][k] += r[j][k];
         st4<T>(sum_out + row * C + c, v[j]);
       }
     } else {
@@ -707,7 +714,7 @@ __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const T* __restrict__ x, c
     if (c < C) {
       float o[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = (v[j][k] - mean) * rstd * (g ? g[c + k] : 1.f) + (b ? b[c + k] : 0.f);
+      for (int k = 0; k < 4; ++k) o[k] = (v[j][k] - mean) * rstd * (g ? ga[j][k] : 1.f) + (b ? be[j][k] : 0.f);
       st4<TO>(y + row * C + c, o);
     }
   }
