@@ -845,18 +845,20 @@ __global__ void __launch_bounds__(MP_T) bn_relu_maxpool_kernel(const T* __restri
                                                                uint8_t* __restrict__ code, int N, int H, int W, int C,
                                                                int OH, int OW) {
   const int CV = C >> 3;
-  const int64_t total = (int64_t)N * OH * OW * CV;
-  int64_t q = (int64_t)blockIdx.x * MP_T + threadIdx.x;
-  const int cv = (int)(q % CV), c = cv * 8;
+  const int total = N * OH * OW * CV;  // < 2^31 (host check)
+  int q = blockIdx.x * MP_T + threadIdx.x;
+  const int cv = q % CV, c = cv * 8;
   float A[8], B[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     A[k] = scale[c + k];
     B[k] = shift[c + k];
   }
-  for (; q < total; q += (int64_t)gridDim.x * MP_T) {
-    const int64_t p = q / CV;  // output pixel
-    const int ow = (int)(p % OW), oh = (int)((p / OW) % OH), n = (int)(p / ((int64_t)OW * OH));
+  for (; q < total; q += gridDim.x * MP_T) {
+    // 32-bit index math (host check: N*H*W*C/8 < 2^31; 64-bit division is a long emulated sequence)
+    const int pq = q / CV;  // output pixel
+    const int t = pq / OW, ow = pq - t * OW, n = t / OH, oh = t - n * OH;
+    const int64_t p = pq;
     float best[8];
     unsigned idx[8];
 #pragma unroll
@@ -897,10 +899,11 @@ __global__ void __launch_bounds__(MP_T) maxpool_bwd_kernel(const T* __restrict__
                                                            int OW) {
   const int CV = C >> 3;
   const int64_t total = (int64_t)N * H * W * CV;
-  for (int64_t q = (int64_t)blockIdx.x * MP_T + threadIdx.x; q < total; q += (int64_t)gridDim.x * MP_T) {
-    const int c = (int)(q % CV) * 8;
-    const int64_t p = q / CV;  // input pixel
-    const int iw = (int)(p % W), ih = (int)((p / W) % H), n = (int)(p / ((int64_t)W * H));
+  for (int q = blockIdx.x * MP_T + threadIdx.x; q < (int)total; q += gridDim.x * MP_T) {
+    const int c = (q % CV) * 8;
+    const int pq = q / CV;  // input pixel (32-bit index math, host-checked range)
+    const int t = pq / W, iw = pq - t * W, n = t / H, ih = t - n * H;
+    const int64_t p = pq;
     float acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0.f;
@@ -962,6 +965,7 @@ RK_API int rk_bn_counters(int C) { return (C + BN_CT - 1) / BN_CT * BN_CNT; }
 RK_API int rk_bn_relu_maxpool(int dt, const void* x, const float* scale, const float* shift, void* y, void* code, int N,
                               int H, int W, int C, int OH, int OW, hipStream_t s) {
   if (C % 8 || MP_T % (C / 8) || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return (int)hipErrorInvalidValue;
+  if ((int64_t)N * H * W * (C / 8) >= ((int64_t)1 << 31) - 2 * 256 * 16 * MP_T) return (int)hipErrorInvalidValue;
   const int g = mp_grid((int64_t)N * OH * OW * (C / 8));
   if (dt == BF16)
     bn_relu_maxpool_kernel<uint16_t><<<g, MP_T, 0, s>>>((const uint16_t*)x, scale, shift, (uint16_t*)y,
@@ -976,6 +980,7 @@ RK_API int rk_bn_relu_maxpool(int dt, const void* x, const float* scale, const f
 RK_API int rk_maxpool_bwd(int dt, const void* dy, const void* code, void* dx, int N, int H, int W, int C, int OH,
                           int OW, hipStream_t s) {
   if (C % 8 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return (int)hipErrorInvalidValue;
+  if ((int64_t)N * H * W * (C / 8) >= ((int64_t)1 << 31) - 2 * 256 * 16 * MP_T) return (int)hipErrorInvalidValue;
   const int g = mp_grid((int64_t)N * H * W * (C / 8));
   if (dt == BF16)
     maxpool_bwd_kernel<uint16_t><<<g, MP_T, 0, s>>>((const uint16_t*)dy, (const uint8_t*)code, (uint16_t*)dx, N, H,
