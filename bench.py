@@ -9,8 +9,9 @@ What runs: the reference ``examples/mnist.py`` topology built from this
 framework's capsules — ``Launcher → Looper → {Dataset, Module(LeNet) →
 {Loss(CrossEntropy), Optimizer(AdamW), Scheduler(StepLR(100))}, StepTimer}`` —
 bf16 mixed precision, per-GPU batch 1024 (weak scaling: global batch 1024·N),
-synthetic MNIST-shaped data (random 1×28×28 images / labels, resident in HBM
-and reshuffled every epoch on-device), random-init weights.  Every timed step
+synthetic MNIST-shaped data (random 1×28×28 images / labels, each rank generating
+and holding only its own shard in HBM, reshuffled every epoch on-device),
+random-init weights.  Every timed step
 does the full work: batch gather, forward, loss, backward, gradient all-reduce
 (N>1), AdamW update, LR schedule, loss accounting.
 
@@ -131,12 +132,14 @@ def main() -> int:
     bs_default, in_shape, classes, desc = MODELS[args.model]
     args.batch = args.batch or bs_default
     total_iters = args.warmup + args.steps
-    n = (total_iters + 1) * args.batch * world  # one epoch covers the whole run on every rank
-    g = torch.Generator(device=dev).manual_seed(1234)
+    # each rank generates only its own shard (weak scaling: per-rank data is fixed as N grows);
+    # one epoch covers the whole run
+    n = (total_iters + 1) * args.batch
+    g = torch.Generator(device=dev).manual_seed(1234 + ctx.rank)
     img_dtype = torch.float32 if args.model == "lenet" else torch.bfloat16
     x = torch.rand((n,) + in_shape, generator=g, device=dev, dtype=img_dtype)
     y = torch.randint(0, classes, (n,), generator=g, device=dev)
-    data = DeviceTensorDataset(x, y)
+    data = DeviceTensorDataset(x, y, pre_sharded=True)
 
     torch.manual_seed(0)
     if args.model == "lenet":

@@ -6,7 +6,8 @@
 // ([kMaxBlocks][8] u32, uncached).  Both are exported once with hipIpcGetMemHandle and mapped by
 // every peer, so a kernel can read a peer's stage and write a peer's flags directly over xGMI.
 //
-// rk_p2p_allreduce(data, n): block b owns the fixed stage region [b*kChunk, (b+1)*kChunk):
+// rk_p2p_allreduce(data, n): region b is the fixed stage range [b*kChunk, (b+1)*kChunk), handled by
+// block b % grid (at most kMaxGrid blocks, block-stride):
 //   1. copy data[region] into stage[parity][region]                         (local HBM)
 //   2. release (L2 write-back, system scope), then store this block's epoch into
 //      flags_peer[b][rank] of every peer; poll flags_self[b][peer] >= epoch for every peer
@@ -21,9 +22,12 @@
 //
 // A poll that exceeds the timeout (30 s; a few seconds for the creation self-test) records an error
 // in host-mapped memory and gives up instead of hanging the GPU; the timed-out block then skips its
-// reduce and leaves its gradients untouched.  The host reads the error word (a plain host load)
-// on every launch and before the optimizer consumes reduced gradients.  The kernel never waits on
-// anything but peer flags.
+// reduce and leaves its gradients untouched.  So that no rank applies those un-reduced gradients,
+// the timed-out block also raises the found flag of up to two device loss-scaling blocks
+// (optim_common.h AmpSlot: the optimizer's fault guard, and the fp16 scaler's state): the fused
+// optimizer launch that follows in the same stream/graph then skips the whole update, step counter
+// included, exactly as for an fp16 overflow.  The host reads the error word (a plain host load) on
+// every launch and replay and raises.  The kernel never waits on anything but peer flags.
 #include "rk_common.h"
 
 #include <cstring>
@@ -37,6 +41,7 @@ constexpr int kThreads = 256;
 constexpr int kVec = 4;                              // floats per 16-byte vector
 constexpr int kUnroll = 2;                           // vectors per thread
 constexpr int kChunk = kThreads * kVec * kUnroll;    // 2048 floats per block (8 KB)
+constexpr int kMaxGrid = 256;                        // blocks per launch (block-stride over regions)
 constexpr uint64_t kTicksPerSecond = 100000000ull;   // s_memrealtime runs at 100 MHz
 
 struct P2PArgs {
@@ -44,6 +49,7 @@ struct P2PArgs {
   unsigned* flags[kMaxPeers];   // every rank's flags base, [kMaxBlocks][kMaxPeers]
   unsigned* epoch;              // local, [kMaxBlocks]
   unsigned* err;                // host-mapped error word
+  float* skip[2];               // AmpSlot found flags raised on a timeout (or null)
   float* data;
   int64_t n, cap;
   uint64_t timeout_ticks;
@@ -55,11 +61,10 @@ __device__ __forceinline__ unsigned load_flag(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// One region b (kChunk floats): stage, signal, wait, reduce.  False when a peer timed out.
 template <int W>
-__global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a) {
-  __shared__ unsigned s_ep;
-  __shared__ int s_timeout;
-  const int b = blockIdx.x, t = threadIdx.x;
+__device__ __forceinline__ bool p2p_region(const P2PArgs& a, int b, unsigned& s_ep, int& s_timeout) {
+  const int t = threadIdx.x;
   if (t == 0) {
     s_ep = a.epoch[b] + 1;
     s_timeout = 0;
@@ -97,6 +102,8 @@ __global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a) {
           __builtin_amdgcn_s_sleep(1);
           if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
             __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            for (int k = 0; k < 2; ++k)
+              if (a.skip[k]) __hip_atomic_store(a.skip[k] + 2, 1.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_timeout = 1;
             break;
           }
@@ -108,8 +115,8 @@ __global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a) {
   }
   __syncthreads();
   // a peer that never signalled: its stage holds stale data -- leave this block's gradients
-  // untouched (the host raises on the error word before they are used)
-  if (s_timeout) return;
+  // untouched (the raised skip flags make the following optimizer launch a no-op)
+  if (s_timeout) return false;
   if (t >= 64) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // this wave's view of the peers' stages
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -142,6 +149,19 @@ __global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a) {
     }
   }
   if (t == 0) a.epoch[b] = ep;
+  __syncthreads();  // s_ep / s_timeout are rewritten by the next region
+  return true;
+}
+
+// A grid of at most kMaxGrid blocks walks the regions (block-stride): the number of spinning
+// blocks is bounded whatever the bucket size, so the kernels of all ranks stay co-resident even
+// when several ranks share one device (the single-GPU rehearsal of the multi-GPU paths).
+template <int W>
+__global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a, int nregions) {
+  __shared__ unsigned s_ep;
+  __shared__ int s_timeout;
+  for (int b = blockIdx.x; b < nregions; b += gridDim.x)
+    if (!p2p_region<W>(a, b, s_ep, s_timeout)) return;
 }
 
 struct P2PCtx {
@@ -154,6 +174,7 @@ struct P2PCtx {
   unsigned* epoch = nullptr;
   unsigned* err_h = nullptr;
   unsigned* err_d = nullptr;
+  float* skip[2] = {nullptr, nullptr};
   float* peer_stage[kMaxPeers] = {};
   unsigned* peer_flags[kMaxPeers] = {};
   bool mapped[kMaxPeers] = {};
@@ -260,6 +281,8 @@ RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipS
   }
   a.epoch = c->epoch;
   a.err = c->err_d;
+  a.skip[0] = c->skip[0];
+  a.skip[1] = c->skip[1];
   a.data = data;
   a.n = n;
   a.cap = c->cap;
@@ -267,16 +290,17 @@ RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipS
   a.timeout_ticks = (uint64_t)(c->timeout_s * (double)kTicksPerSecond);
   a.rank = c->rank;
   a.world = c->world;
-  const int blocks = (int)((n + kChunk - 1) / kChunk);
+  const int regions = (int)((n + kChunk - 1) / kChunk);
+  const int blocks = regions < kMaxGrid ? regions : kMaxGrid;
   switch (c->world) {
-    case 1: p2p_allreduce_kernel<1><<<blocks, kThreads, 0, s>>>(a); break;
-    case 2: p2p_allreduce_kernel<2><<<blocks, kThreads, 0, s>>>(a); break;
-    case 3: p2p_allreduce_kernel<3><<<blocks, kThreads, 0, s>>>(a); break;
-    case 4: p2p_allreduce_kernel<4><<<blocks, kThreads, 0, s>>>(a); break;
-    case 5: p2p_allreduce_kernel<5><<<blocks, kThreads, 0, s>>>(a); break;
-    case 6: p2p_allreduce_kernel<6><<<blocks, kThreads, 0, s>>>(a); break;
-    case 7: p2p_allreduce_kernel<7><<<blocks, kThreads, 0, s>>>(a); break;
-    default: p2p_allreduce_kernel<8><<<blocks, kThreads, 0, s>>>(a); break;
+    case 1: p2p_allreduce_kernel<1><<<blocks, kThreads, 0, s>>>(a, regions); break;
+    case 2: p2p_allreduce_kernel<2><<<blocks, kThreads, 0, s>>>(a, regions); break;
+    case 3: p2p_allreduce_kernel<3><<<blocks, kThreads, 0, s>>>(a, regions); break;
+    case 4: p2p_allreduce_kernel<4><<<blocks, kThreads, 0, s>>>(a, regions); break;
+    case 5: p2p_allreduce_kernel<5><<<blocks, kThreads, 0, s>>>(a, regions); break;
+    case 6: p2p_allreduce_kernel<6><<<blocks, kThreads, 0, s>>>(a, regions); break;
+    case 7: p2p_allreduce_kernel<7><<<blocks, kThreads, 0, s>>>(a, regions); break;
+    default: p2p_allreduce_kernel<8><<<blocks, kThreads, 0, s>>>(a, regions); break;
   }
   return (int)hipGetLastError();
 }
@@ -285,6 +309,15 @@ RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipS
 RK_API int rk_p2p_set_timeout(void* ctx, double seconds) {
   if (!ctx || !(seconds > 0.0)) return (int)hipErrorInvalidValue;
   ((P2PCtx*)ctx)->timeout_s = seconds;
+  return 0;
+}
+
+// Device loss-scaling blocks (AmpSlot, >= 3 floats) whose found flag a timed-out launch raises, so
+// the optimizer launch after it skips the update; null = none.  Later launches use them.
+RK_API int rk_p2p_set_skip(void* ctx, float* a, float* b) {
+  if (!ctx) return (int)hipErrorInvalidValue;
+  ((P2PCtx*)ctx)->skip[0] = a;
+  ((P2PCtx*)ctx)->skip[1] = b;
   return 0;
 }
 

@@ -8,13 +8,14 @@
 // tables, ...), but instead of instantiating it we walk its nodes once, in topological order,
 // and re-issue them with plain stream launches on every replay: one ctypes call, N dispatches.
 //
-// Supported nodes: kernel (hipLaunchKernel with the node's own argument array, which stays
+// Supported graphs: chains (single-stream captures).  Supported nodes: kernel (hipLaunchKernel with the node's own argument array, which stays
 // valid while the graph is alive) and empty.  Anything else (memset/memcpy/event/host/child-graph
 // nodes, module launches with an `extra` buffer) makes create() fail and the caller keeps
 // replaying the instantiated graph.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <string>
@@ -73,6 +74,10 @@ RKG_API int rkg_create(void** out, void* graph_ptr) {
     succ[a->second].push_back(b->second);
     indeg[b->second]++;
   }
+  // a single-stream capture is a chain; parallel branches (multi-stream capture, e.g. an
+  // all-reduce forked off backward) would be serialised by a one-stream launch list
+  for (size_t i = 0; i < n; ++i)
+    if (succ[i].size() > 1 || indeg[i] > 1) return fail("graph has parallel branches");
   std::vector<size_t> order, ready;
   for (size_t i = 0; i < n; ++i)
     if (indeg[i] == 0) ready.push_back(i);
@@ -134,6 +139,45 @@ RKG_API int rkg_create(void** out, void* graph_ptr) {
   }
   *out = ll;
   return 0;
+}
+
+// Text description of a graph's structure (tests / diagnostics): one line per node
+// "N <index> <type> <kernel name or ->" in node-list order, then one line per edge "E <from> <to>".
+// Returns the bytes needed (including the terminating NUL); writes at most `cap` bytes to `buf`.
+RKG_API int64_t rkg_describe(void* graph_ptr, char* buf, int64_t cap) {
+  hipGraph_t graph = (hipGraph_t)graph_ptr;
+  size_t n = 0, ne = 0;
+  if (hipGraphGetNodes(graph, nullptr, &n) != hipSuccess) return -1;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n && hipGraphGetNodes(graph, nodes.data(), &n) != hipSuccess) return -1;
+  if (hipGraphGetEdges(graph, nullptr, nullptr, &ne) != hipSuccess) return -1;
+  std::vector<hipGraphNode_t> from(ne), to(ne);
+  if (ne && hipGraphGetEdges(graph, from.data(), to.data(), &ne) != hipSuccess) return -1;
+  std::map<hipGraphNode_t, size_t> pos;
+  std::string out;
+  for (size_t i = 0; i < n; ++i) {
+    pos[nodes[i]] = i;
+    hipGraphNodeType t;
+    (void)hipGraphNodeGetType(nodes[i], &t);
+    std::string name = "-";
+    if (t == hipGraphNodeTypeKernel) {
+      hipKernelNodeParams p{};
+      if (hipGraphKernelNodeGetParams(nodes[i], &p) == hipSuccess && p.func) {
+        const char* nm = hipKernelNameRefByPtr(p.func, nullptr);
+        if (nm) name = nm;
+      }
+    }
+    out += "N " + std::to_string(i) + " " + std::to_string((int)t) + " " + name + "\n";
+  }
+  for (size_t e = 0; e < ne; ++e)
+    out += "E " + std::to_string(pos[from[e]]) + " " + std::to_string(pos[to[e]]) + "\n";
+  const int64_t need = (int64_t)out.size() + 1;
+  if (buf && cap > 0) {
+    const int64_t k = std::min<int64_t>(cap - 1, (int64_t)out.size());
+    std::memcpy(buf, out.data(), (size_t)k);
+    buf[k] = 0;
+  }
+  return need;
 }
 
 RKG_API int rkg_size(void* h) { return h ? (int)((LaunchList*)h)->ops.size() : 0; }

@@ -104,27 +104,25 @@ def _geo(xc: torch.Tensor, w16: torch.Tensor, stride: int, pad: int):
 
 
 def _bn_src(x: torch.Tensor, stride: int):
-    """(BatchNorm input, ReLU mask, stats) when ``x`` is a fused BatchNorm's output that a stride-1
-    dgrad can finish the backward reduction of (``norm.py`` ``_rocket_bn_bwd_src``), else None."""
-    src = getattr(x, "_rocket_bn_bwd_src", None)
-    if src is None or stride != 1:
+    """The :class:`norm.BwdLink` when ``x`` is a fused BatchNorm's output that a stride-1 dgrad can
+    finish the backward reduction of (``norm.py`` ``_rocket_bn_bwd_src``), else None."""
+    link = getattr(x, "_rocket_bn_bwd_src", None)
+    if link is None or link.src is None or stride != 1:
         return None
-    z = src[0]
+    z = link.src[0]
     if z.shape != x.shape or z.dtype != torch.bfloat16 or not z.is_contiguous(memory_format=torch.channels_last):
         return None
-    return src
+    return link
 
 
 def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | None, bn=None) -> torch.Tensor:
     """Input gradient of one conv; with ``dx`` given it is ADDED to dx (in place, native epilogue
     accumulate) and dx is returned.  ``bn`` (:func:`_bn_src`): the input is that BatchNorm's output —
-    the epilogue also applies its ReLU mask and writes its backward reduction partials, registered
-    for the BatchNorm's backward (``norm._BWD_PARTIALS``)."""
+    the epilogue also applies its ReLU mask and writes its backward reduction partials, handed to
+    the BatchNorm's backward through the link (``norm.BwdLink.done``)."""
     N, C, H, W, Co, R, S, stride, pad, OH, OW = geo
-    if bn is not None and stride == 1 and Co % 64 == 0 and C % 8 == 0:
-        from rocket_amd.ops.norm import _BWD_PARTIALS
-
-        z, mask, stats = bn
+    if bn is not None and bn.src is not None and stride == 1 and Co % 64 == 0 and C % 8 == 0:
+        z, mask, stats = bn.src
         acc = dx is not None
         if dx is None:
             dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
@@ -134,7 +132,7 @@ def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | No
                                                    Co, R, S, pad, z.data_ptr(), _lib.ptr(mask), stats[0].data_ptr(),
                                                    stats[1].data_ptr(), part.data_ptr(), _lib.stream_ptr(dyc.device)),
                    "rk_conv_dgrad_bn")
-        _BWD_PARTIALS[z.data_ptr()] = (dx.data_ptr(), dx._version, part, ntiles)
+        bn.done = (dx.data_ptr(), dx._version, part, ntiles)
         return dx
     if (stride == 1 or (stride == 2 and SDGRAD == "native" and _sdgrad_ok(R, S, pad))) and Co % 64 == 0:
         acc = dx is not None

@@ -53,14 +53,21 @@ def pick_split(M: int, N: int, K: int, max_split: int = 16) -> tuple[int, int]:
 
 
 _slabs: dict = {}
+_retired: list = []  # outgrown slabs: captured HIP graphs may still write into them on replay
 
 
 def _slab(device: torch.device, numel: int) -> torch.Tensor:
     """Split-K scratch, one per device, grown on demand (stream-ordered reuse: every launch on
-    the stream consumes its slab before the next one writes it)."""
+    the stream consumes its slab before the next one writes it).
+
+    A slab that is outgrown is retired, never freed: graphs captured while it was current keep
+    its raw pointer and write their split-K partials into it on every replay, so returning it to
+    the caching allocator would let another tensor alias those writes."""
     key = (device.type, device.index)
     buf = _slabs.get(key)
     if buf is None or buf.numel() < numel:
+        if buf is not None:
+            _retired.append(buf)
         buf = _slabs[key] = torch.empty(numel, dtype=torch.float32, device=device)
     return buf
 

@@ -54,10 +54,24 @@ def _channels_last(x: torch.Tensor) -> torch.Tensor:
     return x.contiguous()
 
 
-# BatchNorm input data_ptr -> (dy data_ptr, dy version, partials, ntiles): backward reductions already
-# done by the stride-1 conv dgrad that produced the BatchNorm output's gradient (iconv.py); consumed
-# (popped) by that BatchNorm's backward when its incoming gradient is exactly that tensor, unmodified.
-_BWD_PARTIALS: dict = {}
+LINK_HITS = 0  # BatchNorm backwards that used a conv dgrad epilogue's reductions (tests)
+
+
+class BwdLink:
+    """Hand-off between a fused BatchNorm and the conv that consumes its output.
+
+    ``src`` = (BatchNorm input, ReLU mask, stats), set by the BatchNorm forward; ``done`` =
+    (dy data_ptr, dy version, partials, ntiles), set by the consuming stride-1 conv's dgrad
+    (iconv.py) when its epilogue already did this BatchNorm's backward reductions, and consumed by
+    the BatchNorm's backward when its incoming gradient is exactly that tensor, unmodified.  The
+    link lives on the autograd graph (the BatchNorm's ctx and its output), so a pruned or partial
+    backward leaves nothing behind that a later step could pick up."""
+
+    __slots__ = ("src", "done")
+
+    def __init__(self):
+        self.src = None
+        self.done = None
 
 
 class _BNAct(torch.autograd.Function):
@@ -101,6 +115,7 @@ class _BNAct(torch.autograd.Function):
                        "rk_bn_relu_maxpool")
             ctx.params = (weight, bias)
             ctx.relu, ctx.has_res, ctx.out_dtype, ctx.pool = True, False, x.dtype, True
+            ctx.link = None
             ctx.save_for_backward(x, code, stats)
             return y
         res = None
@@ -117,8 +132,9 @@ class _BNAct(torch.autograd.Function):
         ctx.out_dtype = out_dtype
         ctx.pool = False
         ctx.save_for_backward(x, mask, stats)
+        ctx.link = box
         if box is not None:  # what a consuming conv's dgrad epilogue needs to do this backward's reduction
-            box.append((x, mask, stats))
+            box.src = (x, mask, stats)
         return y
 
     @staticmethod
@@ -136,7 +152,10 @@ class _BNAct(torch.autograd.Function):
             _lib.check(lib.rk_maxpool_bwd(_dt(x), dy.data_ptr(), mask.data_ptr(), dfull.data_ptr(), N, H, W, C, OH, OW,
                                           _lib.stream_ptr(dev)), "rk_maxpool_bwd")
             dy, mask = dfull, None
-        done = _BWD_PARTIALS.pop(x.data_ptr(), None)
+        link, ctx.link = ctx.link, None
+        done = None
+        if link is not None:
+            done, link.done, link.src = link.done, None, None
         xr, dyr = _rows_view(x), _rows_view(dy)
         R = xr.shape[0]
         params = [p for p in (weight, bias) if p is not None]
@@ -149,6 +168,8 @@ class _BNAct(torch.autograd.Function):
         nctr = int(lib.rk_bn_counters(C))
         counters = _lib.Workspace.get(dev).counter_array(f"bn{nctr}", nctr)
         if done is not None and done[0] == dy.data_ptr() and done[1] == dy._version:
+            global LINK_HITS
+            LINK_HITS += 1
             # dy is the masked gradient the conv dgrad epilogue stored, its reductions are in done[2];
             # the residual's gradient IS that masked dy: handed on as is, not copied
             dres = dy if ctx.has_res else None
@@ -198,14 +219,14 @@ class BatchNormAct2d(nn.BatchNorm2d):
             if partials is not None and not (x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
                                              and partials[0].numel() == 2 * partials[1] * x.shape[1]):
                 partials = None
-            box = [] if (BWD_FUSE and not self.maxpool and x.dim() == 4 and x.dtype == torch.bfloat16) else None
+            box = BwdLink() if (BWD_FUSE and not self.maxpool and x.dim() == 4 and x.dtype == torch.bfloat16) else None
             y = _BNAct.apply(x, self.weight, self.bias, residual,
                              self.running_mean if self.track_running_stats else None,
                              self.running_var if self.track_running_stats else None,
                              self.num_batches_tracked if self.track_running_stats else None,
                              self.momentum, self.eps, self.relu, partials, self.maxpool, box)
-            if box:
-                y._rocket_bn_bwd_src = box[0]  # (input, ReLU mask, stats) for a consuming conv's dgrad
+            if box is not None and box.src is not None:
+                y._rocket_bn_bwd_src = box  # for a consuming conv's dgrad (BwdLink)
             return y
         if x.is_cuda and self.training and _ops.fused_enabled():
             _lib.kernels()  # a HIP device without the native library is an error, not a fallback

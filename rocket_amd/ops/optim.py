@@ -50,6 +50,9 @@ class _FusedBase(torch.optim.Optimizer):
         # ``_step_supports_amp_scaling`` protocol below (grad_scale / found_inf tensors).
         self.amp: Optional[torch.Tensor] = None
         self._torch_amp = None
+        # data parallel over the P2P kernel: an identity AmpSlot block whose found flag a timed-out
+        # reduction raises (parallel/p2p.py), read by unscaled launches so they skip that update
+        self.guard: Optional[torch.Tensor] = None
 
     # ----------------------------------------------------------- host side
     def _active(self) -> List[tuple]:
@@ -176,7 +179,7 @@ class _FusedBase(torch.optim.Optimizer):
         """Enqueue the fused update (graph-capturable); ``zero_grads`` also clears the consumed gradients."""
         lib = _lib.kernels()
         dev = self._device
-        amp = self.amp if self.amp is not None else self._torch_amp
+        amp = self.amp if self.amp is not None else self._torch_amp if self._torch_amp is not None else self.guard
         _lib.check(
             lib.rk_optim_mt(self.KIND, self._gdtype, self._tables[0].data_ptr(), self._tables[1].data_ptr(),
                             self._nblocks, self._hyper_dev.data_ptr(), self._step_dev.data_ptr(), _lib.ptr(amp),

@@ -141,10 +141,12 @@ class DataParallel(nn.Module):
         self._reduces = 0
         self._debug = os.environ.get("ROCKET_DEBUG_SYNC", "0") == "1"
         self._launched: List[int] = []
-        # native transport: per-bucket all-reduce on a side stream, one join before the optimizer
-        self._native = self.comm.make_reducer([b.flat for b in self.buckets]) if hasattr(self.comm, "make_reducer") else None
         # small models: one-shot xGMI all-reduce kernel (graph-capturable) instead of RCCL
-        self._p2p = self._make_p2p() if (comm is None and self._native is None) else None
+        self._p2p = self._make_p2p()
+        # native transport: per-bucket all-reduce on a side stream, one join before the optimizer
+        self._native = None
+        if self._p2p is None and hasattr(self.comm, "make_reducer"):
+            self._native = self.comm.make_reducer([b.flat for b in self.buckets])
 
     # ----------------------------------------------------------------- setup
     def _flat_broadcast(self, tensors: List[torch.Tensor]) -> None:
@@ -244,8 +246,8 @@ class DataParallel(nn.Module):
         from rocket_amd.runtime import comm as rcomm
 
         ctx = rcomm.context()
-        if (not p2p.enabled() or not isinstance(self.comm, _TorchDistComm)
-                or not (self.comm.avg_native or p2p.forced())
+        rccl = getattr(self.comm, "native", False) or (isinstance(self.comm, _TorchDistComm) and self.comm.avg_native)
+        if (not p2p.enabled() or not (rccl or (isinstance(self.comm, _TorchDistComm) and p2p.forced()))
                 or ctx.local_world_size != ctx.world_size or ctx.world_size > 8 or not self.buckets
                 or any(b.flat.dtype != torch.float32 or b.flat.device.type != "cuda" for b in self.buckets)
                 or sum(b.flat.numel() for b in self.buckets) > p2p.MAX_ELEMS):
@@ -259,10 +261,27 @@ class DataParallel(nn.Module):
             self._p2p.check()
 
     @property
+    def capture_mode(self) -> str:
+        """How a captured gradient-sync step reduces (``runtime/graphs.py``):
+
+        * ``"overlap"`` — native RCCL reducer: each bucket's all-reduce is launched from the
+          gradient hooks *during capture*, forked onto the reducer's side stream and joined before
+          the optimizer, so the step is ONE graph whose all-reduce nodes run in parallel branches
+          with the rest of backward;
+        * ``"inline"`` — P2P one-shot kernel: one reduction between backward and optimizer, in
+          the same graph (small models: the whole gradient is one latency-bound bucket);
+        * ``"split"`` — torch.distributed group (ProcessGroupNCCL's own streams cannot be
+          captured): two graphs with the host-issued bucket all-reduce between them."""
+        if self._p2p is not None:
+            return "inline"
+        if self._native is not None:
+            return "overlap"
+        return "split"
+
+    @property
     def capturable(self) -> bool:
-        """True when the gradient all-reduce is a plain kernel (P2P): a synchronising step can be
-        captured into ONE graph with the reduction between backward and optimizer."""
-        return self._p2p is not None
+        """True when a synchronising step can be captured as ONE graph (P2P or native reducer)."""
+        return self.capture_mode != "split"
 
     # --------------------------------------------------------------- runtime
     @contextlib.contextmanager

@@ -50,6 +50,23 @@ class P2PAllReduce:
         self.launches = 0
         # the kernel's error word lives in host-mapped memory: read it with a plain load, no call
         self._err = ctypes.c_uint.from_address(_lib.kernels().rk_p2p_error_ptr(ctx))
+        # fault guard: an identity loss-scaling block (optim_common.h AmpSlot: scale 1, growth and
+        # backoff 1) handed to the fused optimizers of the replicated model.  A timed-out launch
+        # raises its found flag, so the update that would consume un-reduced gradients is skipped.
+        self.fault = torch.tensor([1.0, 1.0, 0.0, 0.0, 1.0, 1.0, float("inf"), 0.0], device=device)
+        self._scaler_state = None
+        self._set_skip()
+
+    def _set_skip(self) -> None:
+        sc = self._scaler_state
+        _lib.check(_lib.kernels().rk_p2p_set_skip(self._ctx, self.fault.data_ptr(),
+                                                  sc.data_ptr() if sc is not None else None), "rk_p2p_set_skip")
+
+    def guard_scaler(self, state: Optional[torch.Tensor]) -> None:
+        """Also raise the found flag of an fp16 scaler's device state on a timeout (the fused
+        optimizer reads that block instead of the fault guard on scaled steps)."""
+        self._scaler_state = state
+        self._set_skip()
 
     @classmethod
     def create(cls, cap: int, group=None, device: Optional[torch.device] = None) -> Optional["P2PAllReduce"]:
@@ -102,6 +119,7 @@ class P2PAllReduce:
         any gradient depends on them; a failure anywhere makes every rank fall back to RCCL."""
         lib = _lib.kernels()
         n = min(self.cap, 3 * 2048 + 17)  # several blocks and a partial tail block
+        lib.rk_p2p_set_skip(self._ctx, None, None)  # a timed-out self-test only reports
         try:
             lib.rk_p2p_set_timeout(self._ctx, 5.0)
             with torch.cuda.device(self.device):
@@ -116,6 +134,7 @@ class P2PAllReduce:
             ok = False
         finally:
             lib.rk_p2p_set_timeout(self._ctx, 30.0)
+            self._set_skip()
         return ok
 
     def all_reduce_(self, flat: torch.Tensor, scale: float = 1.0) -> None:
@@ -128,8 +147,10 @@ class P2PAllReduce:
         self.check()  # a plain load of a host-mapped word: reports a timeout of any earlier launch
 
     def check(self) -> None:
-        """Raise if a launch ever timed out waiting for a peer (its timed-out blocks left their
-        gradients un-reduced).  Costs one host load: called on every launch and every replay."""
+        """Raise if a launch ever timed out waiting for a peer.  Its timed-out blocks left their
+        gradients un-reduced, and raised the fault guard's found flag, so the optimizer launch of
+        that same step (same stream / graph) skipped its update; this surfaces the failure on the
+        host.  Costs one host load: called on every launch and every replay."""
         if self._ctx and self._err.value:
             raise RuntimeError("p2p all-reduce: a peer did not signal within the timeout (dead or desynchronised rank)")
 
@@ -140,3 +161,91 @@ class P2PAllReduce:
             self._err = ctypes.c_uint(0)  # the mapped word is freed with the context
             _lib.kernels().rk_p2p_destroy(self._ctx)
             self._ctx = 0
+
+
+class P2PComm:
+    """A complete data-parallel transport on the P2P kernel (no RCCL): every gradient bucket is
+    reduced by :meth:`P2PAllReduce.all_reduce_` on a side stream forked off backward when the
+    bucket completes, joined before the optimizer — the same stream/event structure as the native
+    RCCL reducer (``DataParallel.capture_mode == "overlap"``), fully graph-capturable.
+
+    RCCL needs one device per rank; this transport does not, so it is how the overlapped,
+    captured DP step (per-bucket all-reduce branches, in-graph rank-0 buffer broadcast, side-channel
+    loss) is rehearsed with several ranks on ONE GPU (``ROCKET_DP_COMM=p2p``,
+    ``tests/gpu/test_ddp_graph.py``).  Single node only; bandwidth is not its purpose (each rank
+    reads every peer's whole bucket)."""
+
+    native = False  # not RCCL: DataParallel must not route small models to its own P2P path
+
+    def __init__(self, ar: P2PAllReduce):
+        self.ar = ar
+        self.rank, self.world = ar.rank, ar.world
+        self.avg_native = True
+
+    @classmethod
+    def create(cls, cap: int, group=None, device: Optional[torch.device] = None) -> "P2PComm":
+        ar = P2PAllReduce.create(cap, group=group, device=device)
+        if ar is None:
+            raise RuntimeError("P2PComm: the P2P all-reduce could not be set up on every rank")
+        return cls(ar)
+
+    def all_reduce_avg(self, flat: torch.Tensor):
+        self._reduce(flat, 1.0 / self.world)
+        return _Issued()
+
+    def _reduce(self, t: torch.Tensor, scale: float) -> None:
+        """``t <- scale * sum_ranks(t)`` for any dtype / size: fp32 staging in cap-sized chunks
+        (integers and bytes below 2^24 are exact in fp32)."""
+        flat = t.reshape(-1)
+        f32 = flat if (flat.dtype == torch.float32 and flat.is_contiguous()) else flat.to(torch.float32)
+        for off in range(0, f32.numel(), self.ar.cap):
+            self.ar.all_reduce_(f32[off : off + self.ar.cap], scale)
+        if f32 is not flat:
+            flat.copy_(f32.round() if not flat.dtype.is_floating_point else f32)
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
+        """Rank ``src``'s values everywhere: the other ranks contribute zeros to a sum (stream-
+        ordered, capturable)."""
+        with torch.no_grad():
+            if self.rank != src:
+                t.zero_()
+            self._reduce(t, 1.0)
+
+    def make_reducer(self, flats):
+        return _P2PReducer(self, flats)
+
+
+class _Issued:
+    def wait(self):
+        return None
+
+
+class _P2PReducer:
+    """Per-bucket reduction on a side stream, event fork/join with the compute stream (the
+    Python twin of ``native/runtime/comm.cpp``'s reducer)."""
+
+    def __init__(self, comm: P2PComm, flats):
+        self.comm = comm
+        self.flats = list(flats)
+        dev = self.flats[0].device
+        self.stream = torch.cuda.Stream(device=dev, priority=-1)
+        self.done = [torch.cuda.Event() for _ in self.flats]
+        self.pending = set()
+
+    def launch(self, i: int) -> None:
+        cur = torch.cuda.current_stream(self.flats[i].device)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        self.stream.wait_event(ready)
+        with torch.cuda.stream(self.stream):
+            self.comm.ar.all_reduce_(self.flats[i], 1.0 / self.comm.world)
+            self.done[i].record(self.stream)
+        self.pending.add(i)
+
+    def join(self) -> None:
+        if not self.pending:
+            return
+        cur = torch.cuda.current_stream(self.flats[0].device)
+        for i in sorted(self.pending):
+            cur.wait_event(self.done[i])
+        self.pending.clear()

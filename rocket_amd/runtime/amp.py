@@ -53,7 +53,9 @@ class FusedGradScaler:
         if not self._enabled:
             return outputs
         if isinstance(outputs, torch.Tensor):
-            return outputs * self.state[SCALE].to(outputs.dtype)
+            # the fp32 0-dim scale promotes a 0-dim fp16 loss to fp32 (as torch's GradScaler):
+            # 65536 cast to fp16 would be inf and skip every growth step
+            return outputs * self.state[SCALE]
         return type(outputs)(self.scale(o) for o in outputs)
 
     def _grads(self, optimizer):
@@ -79,6 +81,10 @@ class FusedGradScaler:
         unscaled = id(optimizer) in self._unscaled
         if isinstance(optimizer, _FusedBase) and not args and not kwargs:
             if not optimizer.prepare():
+                # no gradient to update: torch still runs the scale update on the (clear) flag,
+                # and this step's skip state and the unscaled set must not leak into the next
+                self._update_host_side()
+                self._record_last()
                 return None
             if not unscaled:
                 optimizer.amp_check(self.state)

@@ -346,15 +346,21 @@ class DeviceTensorDataset(torch.utils.data.Dataset):
 
     Indexing returns a tuple of per-sample views, so it is also usable by host
     loaders; :class:`DeviceLoader` batches it with on-device gathers instead.
+
+    ``pre_sharded=True``: the tensors are THIS rank's shard only (each rank generated or loaded
+    its own part, e.g. synthetic benchmark data): the loader batches all of it locally instead of
+    taking every W-th batch of a global set, so no rank holds the other ranks' samples.  Every rank
+    must then hold the same number of samples (equal batch counts keep the ranks in step).
     """
 
-    def __init__(self, *tensors: torch.Tensor):
+    def __init__(self, *tensors: torch.Tensor, pre_sharded: bool = False):
         if not tensors:
             raise ValueError("DeviceTensorDataset needs at least one tensor")
         n = tensors[0].shape[0]
         if any(t.shape[0] != n for t in tensors):
             raise ValueError("all tensors must share their first dimension")
         self.tensors = tensors
+        self.pre_sharded = bool(pre_sharded)
 
     @property
     def device(self) -> torch.device:
@@ -403,6 +409,8 @@ class DeviceLoader(_LoaderBase):
     ):
         sampler = EpochSampler(len(dataset), shuffle=shuffle, seed=seed)
         bs = BatchSampler(sampler, batch_size, drop_last)
+        if getattr(dataset, "pre_sharded", False):  # already this rank's shard: batch all of it
+            num_replicas, rank = 1, 0
         super().__init__(dataset, ShardedBatchSampler(bs, num_replicas, rank, even_batches, skip), gradient_state)
         self._ctor = dict(
             batch_size=batch_size,

@@ -243,8 +243,10 @@ class Engine:
         self._wrapped: dict = {}
         self._grad_owners: list = []  # FlatGrads / DataParallel owning persistent .grad storage
         self.flat_grads = self.device.type == "cuda" if flat_grads is None else bool(flat_grads)
-        # data-parallel transport: "torch" (ProcessGroupNCCL = RCCL) or "native" (own RCCL communicator)
-        self.comm_backend = comm or ("native" if os.environ.get("ROCKET_NATIVE_COMM") == "1" else "torch")
+        # data-parallel transport: "native" (own RCCL communicator + side-stream bucket reducer; the
+        # default on GPUs: graph-capturable, so a captured DP step overlaps its all-reduce with
+        # backward) or "torch" (ProcessGroupNCCL = RCCL; ROCKET_NATIVE_COMM=0)
+        self.comm_backend = comm or ("torch" if os.environ.get("ROCKET_NATIVE_COMM", "1") == "0" else "native")
         self._native_comm = None
         self._optimizers: List[EngineOptimizer] = []
         self._schedulers: List[EngineScheduler] = []
@@ -330,6 +332,7 @@ class Engine:
             wrapped = DataParallel(model, bucket_cap_mb=self.bucket_cap_mb, comm=self._dp_comm())
             self._wrapped[id(model)] = wrapped
             self._grad_owners.append(wrapped)
+            self._wire_fault_guards()
             return wrapped
         if self.flat_grads and any(p.requires_grad for p in model.parameters()):
             from rocket_amd.parallel.flat_grads import FlatGrads
@@ -338,12 +341,26 @@ class Engine:
         return model
 
     def _dp_comm(self):
-        if self.comm_backend != "native" or self.device.type != "cuda":
+        if os.environ.get("ROCKET_DP_COMM") == "p2p" and self.device.type == "cuda":
+            # P2P-kernel transport (parallel/p2p.py P2PComm): overlapped + capturable like the native
+            # reducer, and it runs with several ranks on one device (single-GPU rehearsals)
+            if self._native_comm is None:
+                from rocket_amd.parallel.p2p import P2PComm
+
+                cap = int(os.environ.get("ROCKET_P2P_COMM_CAP", str(16 << 20)))
+                self._native_comm = P2PComm.create(cap, group=_comm.context().host_group, device=self.device)
+            return self._native_comm
+        if self.comm_backend != "native" or self.device.type != "cuda" or _comm.context().backend != "nccl":
             return None  # DataParallel's default: the torch.distributed RCCL/gloo group
         if self._native_comm is None:
             from rocket_amd.parallel.rccl import RcclComm
 
-            self._native_comm = RcclComm(self.device)
+            try:
+                self._native_comm = RcclComm(self.device)
+            except Exception as e:  # every rank takes the same branch: ncclCommInitRank is collective
+                logger.warning(f"native RCCL communicator unavailable ({e}); using the torch.distributed group")
+                self.comm_backend = "torch"
+                return None
         return self._native_comm
 
     def grad_owner(self, p):
@@ -389,7 +406,23 @@ class Engine:
                         state[k] = v.to(self.device)
         wrapped = EngineOptimizer(optimizer, self)
         self._optimizers.append(wrapped)
+        self._wire_fault_guards()
         return wrapped
+
+    def _wire_fault_guards(self) -> None:
+        """Fused optimizers of a model reduced by the P2P kernel read its fault guard (a peer
+        timeout then skips the update that would apply un-reduced gradients); with the fp16
+        scaler the kernel also raises the scaler's found flag (parallel/p2p.py)."""
+        for o in self._grad_owners:
+            p2p = getattr(o, "_p2p", None)
+            if p2p is None:
+                continue
+            if isinstance(self.scaler, FusedGradScaler):
+                p2p.guard_scaler(self.scaler.state)
+            for eo in self._optimizers:
+                opt = eo.optimizer
+                if hasattr(opt, "guard") and any(o.owns(p) for g in opt.param_groups for p in g["params"]):
+                    opt.guard = p2p.fault
 
     def prepare_scheduler(self, scheduler) -> EngineScheduler:
         opts = [o for o in self._optimizers if o.optimizer is getattr(scheduler, "optimizer", None)]

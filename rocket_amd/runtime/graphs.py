@@ -12,12 +12,24 @@ by input signature) and replays them every iteration, while every host-side
 duty of the capsules still runs each iteration: loss/lr reporting to the
 tracker and progress bar, scheduler stepping, GA bookkeeping.
 
-Data parallel (W>1): collectives never run inside a graph.  A sync step is two
-graphs — ``A`` (forward/backward, gradients land in the reducer's flat
-buckets) and ``B`` (post-reduction work: optimizer) — with the RCCL bucket
-all-reduce issued from the host between them (stream-ordered, no host wait).
+Data parallel (W>1), by the replica's ``capture_mode`` (``parallel/ddp.py``):
+
+* ``overlap`` (default on GPUs: the native RCCL communicator) — the whole sync
+  step is ONE graph.  During capture every bucket's ``ncclAllReduce`` is
+  launched from the gradient hooks the moment the bucket is complete, forked
+  onto the reducer's high-priority side stream with an event and joined back
+  before the optimizer; the instantiated graph therefore holds each bucket's
+  all-reduce as a parallel branch that runs while the rest of backward
+  continues (replayed with hipGraphLaunch, which keeps the branches parallel).
+  The rank-0 BatchNorm buffer broadcast is captured in the forward as well;
+* ``inline`` (small models: the one-shot P2P xGMI kernel) — one graph with the
+  reduction kernel between backward and optimizer;
+* ``split`` (torch.distributed fallback) — two graphs, ``A`` (forward/backward,
+  gradients land in the reducer's flat buckets) and ``B`` (optimizer), with the
+  bucket all-reduce issued from the host between them.
+
 The loss scalar rides in the reducer's side channel, so it is averaged by the
-same collective.
+same collective as the gradients.
 
 Protocol for children of a captured ``Module`` (built-ins implement it):
 
@@ -132,7 +144,7 @@ def _rebuild(batch, it):
 
 
 class _Captured:
-    __slots__ = ("graphs", "static_in", "persistent", "out", "sync")
+    __slots__ = ("graphs", "static_in", "persistent", "out", "sync", "host_sync_buffers")
 
     def __init__(self):
         self.graphs: list = []   # [_Part A] or [A, B] (B after the host-side gradient reduction)
@@ -140,6 +152,7 @@ class _Captured:
         self.persistent = None   # per input tensor: captured in place (no copy at replay)
         self.out = None
         self.sync = False
+        self.host_sync_buffers = False
 
 
 class StepGraphs:
@@ -323,13 +336,14 @@ class StepGraphs:
         return False
 
     # ----------------------------------------------------------------- capture
-    def _phase_a(self, attrs: Attributes) -> None:
+    def _phase_a(self, attrs: Attributes, overlap: bool = False) -> None:
         mod = self.mod
         engine = mod._accelerator
         rep = self._replica()
         with engine.autocast():
             with engine.no_sync(mod._module) if not engine.sync_gradients else _null():
-                with rep.deferred() if rep is not None else _null():
+                # overlap: the gradient hooks launch every bucket's all-reduce during capture
+                with rep.deferred() if (rep is not None and not overlap) else _null():
                     attrs.batch = mod._module(attrs.batch)
                     for c in mod._capsules:
                         c.graph_device(attrs)
@@ -348,9 +362,12 @@ class StepGraphs:
         v.persistent = [bool(getattr(t, "_rocket_persistent", False)) for t in tens]
         v.static_in = [t if keep else t.detach().clone() for t, keep in zip(tens, v.persistent)]
         rep = self._replica()
-        inline = v.sync and rep is not None and rep.capturable  # all-reduce kernel inside the graph
-        split = v.sync and rep is not None and not inline
-        if v.sync and rep is not None and rep.broadcast_buffers:
+        mode = rep.capture_mode if (v.sync and rep is not None) else None
+        inline = mode == "inline"    # P2P kernel between backward and optimizer, same graph
+        overlap = mode == "overlap"  # bucket all-reduces forked off backward, same graph
+        split = mode == "split"      # host-issued all-reduce between two graphs
+        v.host_sync_buffers = v.sync and rep is not None and rep.broadcast_buffers and not overlap
+        if v.host_sync_buffers:
             rep.sync_buffers()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
@@ -362,7 +379,7 @@ class StepGraphs:
         ga = torch.cuda.CUDAGraph(keep_graph=True)
         # thread_local: the RCCL watchdog thread keeps polling its events while we capture
         with torch.cuda.graph(ga, pool=self.pool, capture_error_mode="thread_local"):
-            self._phase_a(cap)
+            self._phase_a(cap, overlap)
             if inline:
                 rep.reduce_now()
             if not split:
@@ -374,7 +391,9 @@ class StepGraphs:
                 self._phase_b(cap)
             v.graphs.append(_Part(gb))
         for part in v.graphs:
-            why = part.finish()
+            # a graph with parallel branches (the overlapped all-reduce) keeps hipGraphLaunch:
+            # a launch list would serialise the branches onto one stream
+            why = part.finish() if not overlap else "parallel branches (overlapped all-reduce)"
             if part.ll is not None:
                 self.launch_lists += 1
             elif self.launch_list_reason is None:
@@ -412,8 +431,8 @@ class StepGraphs:
             if not keep:
                 dst.copy_(src, non_blocking=True)
         rep = self._replica() if v.sync else None
-        if rep is not None and rep.broadcast_buffers:
-            rep.sync_buffers()
+        if rep is not None and v.host_sync_buffers:
+            rep.sync_buffers()  # (an overlapped step broadcasts inside its graph)
         if rep is not None:
             rep.check_comm()  # P2P peer timeouts surface at the next step (one host load)
         self._run(v, rep if len(v.graphs) > 1 else None)

@@ -33,6 +33,7 @@ RUNTIME_SIGS = {
     "rkl_destroy": (c_int, [c_void_p]),
     "rkg_last_error": (c_char_p, []),
     "rkg_create": (c_int, [P, c_void_p]),
+    "rkg_describe": (c_int64, [c_void_p, c_char_p, c_int64]),
     "rkg_size": (c_int, [c_void_p]),
     "rkg_kind": (c_int, [c_void_p, c_int]),
     "rkg_launch": (c_int, [c_void_p, c_void_p]),
@@ -93,3 +94,24 @@ class LaunchList:
                 self._destroy(h)
             except Exception:
                 pass
+
+
+def describe_graph(graph):
+    """Structure of a captured graph (``torch.cuda.CUDAGraph`` with ``keep_graph=True``):
+    ``(nodes, edges)`` with ``nodes[i] = (type, kernel name or "-")`` and ``edges = [(from, to)]``
+    (``native/runtime/launchlist.cpp`` ``rkg_describe``)."""
+    rt = runtime()
+    g = ctypes.c_void_p(graph.raw_cuda_graph())
+    need = rt.rkg_describe(g, None, 0)
+    if need < 0:
+        raise RuntimeError_("rkg_describe failed")
+    buf = ctypes.create_string_buffer(int(need))
+    rt.rkg_describe(g, buf, need)
+    nodes, edges = [], []
+    for line in buf.value.decode(errors="replace").splitlines():
+        parts = line.split(" ", 3)
+        if parts[0] == "N":
+            nodes.append((int(parts[2]), parts[3] if len(parts) > 3 else "-"))
+        elif parts[0] == "E":
+            edges.append((int(parts[1]), int(parts[2])))
+    return nodes, edges

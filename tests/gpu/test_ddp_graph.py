@@ -1,10 +1,18 @@
 """Data-parallel captured steps vs eager, 2 ranks on one GPU.
 
-The ranks share ``cuda:0`` and talk over gloo (``ROCKET_DIST_BACKEND=gloo``):
-this rehearses the multi-GPU code paths on the single-GPU box —
-* ``ROCKET_P2P=0``: graph A -> host-issued bucket all-reduce -> graph B (the RCCL path);
-* ``ROCKET_P2P=force``: the one-shot IPC all-reduce kernel captured INSIDE one graph per step —
-plus deferred bucket reduction and side-channel loss averaging in both.
+The ranks share ``cuda:0`` and their host group is gloo (``ROCKET_DIST_BACKEND=gloo``): this
+rehearses the multi-GPU code paths on the single-GPU box, one per ``DataParallel.capture_mode`` —
+
+* ``split`` (``ROCKET_P2P=0``, torch.distributed transport): graph A -> host-issued bucket
+  all-reduce -> graph B;
+* ``inline`` (``ROCKET_P2P=force``, LeNet): the one-shot IPC all-reduce kernel captured INSIDE one
+  graph per step;
+* ``overlap`` (``ROCKET_DP_COMM=p2p``): every bucket's all-reduce forked onto a side stream from
+  the gradient hooks during capture and joined before the optimizer — ONE graph whose reduction
+  branches run alongside the rest of backward (the structure the native RCCL reducer captures on
+  real multi-GPU nodes), with the rank-0 BatchNorm buffer broadcast captured in the forward —
+
+plus side-channel loss averaging in all of them, for LeNet and a BatchNorm ResNet-18.
 """
 
 import json
@@ -24,13 +32,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, p2p):
+_ENV = {"split": dict(ROCKET_P2P="0"), "inline": dict(ROCKET_P2P="force"),
+        "overlap": dict(ROCKET_P2P="0", ROCKET_DP_COMM="p2p")}
+
+
+def _worker(rank, world, port, out_dir, mode, model):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROCKET_DIST_BACKEND="gloo", ROCKET_P2P=p2p)
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROCKET_DIST_BACKEND="gloo", **_ENV[mode])
     import rocket_amd as rocket
     from rocket_amd.core.capsule import Capsule
-    from rocket_amd.models import CrossEntropy, LeNet
-    from rocket_amd.ops.optim import FusedAdamW
+    from rocket_amd.models import CrossEntropy, LeNet, resnet18
+    from rocket_amd.ops.optim import FusedAdamW, FusedSGD
 
     class Rec(Capsule):
         def __init__(self):
@@ -45,16 +57,22 @@ def _worker(rank, world, port, out_dir, p2p):
     for capture in (False, True):
         dev = torch.device("cuda", 0)
         g = torch.Generator(device=dev).manual_seed(3)
-        x = torch.rand(256 * 24, 1, 28, 28, generator=g, device=dev)
-        y = torch.randint(0, 10, (256 * 24,), generator=g, device=dev)
+        bs = 128 if model == "lenet" else 32
+        shape = (1, 28, 28) if model == "lenet" else (3, 32, 32)
+        x = torch.rand((bs * 2 * 12,) + shape, generator=g, device=dev)
+        y = torch.randint(0, 10, (bs * 2 * 12,), generator=g, device=dev)
         torch.manual_seed(0)
-        net = LeNet(fused=True)
-        opt = FusedAdamW(net.parameters(), lr=1e-2)
+        if model == "lenet":
+            net = LeNet(fused=True)
+            opt = FusedAdamW(net.parameters(), lr=1e-2)
+        else:
+            net = resnet18(10).to(memory_format=torch.channels_last)
+            opt = FusedSGD(net.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-5)
         rec = Rec()
         mod = rocket.Module(net, [rocket.Loss(CrossEntropy(fused=True)), rocket.Optimizer(opt)], capture=capture,
                             warmup=2)
         rocket.Launcher(
-            [rocket.Looper([rocket.Dataset(rocket.DeviceTensorDataset(x, y), batch_size=128), mod, rec],
+            [rocket.Looper([rocket.Dataset(rocket.DeviceTensorDataset(x, y), batch_size=bs), mod, rec],
                            repeats=12, progress=False)],
             logging_dir=os.path.join(out_dir, f"logs{int(capture)}"),
             mixed_precision="bf16",
@@ -66,9 +84,10 @@ def _worker(rank, world, port, out_dir, p2p):
         res[str(capture)] = dict(
             losses=[float(v) for v in rec.losses],
             w=float(sum(p.detach().double().sum() for p in net.parameters())),
+            bufs=float(sum(b.detach().double().sum() for b in net.buffers())),
             replays=(mod._graphs.replays if mod._graphs is not None else 0),
             parts=(mod._graphs.parts if mod._graphs is not None else 0),
-            p2p=bool(getattr(mod._module, "capturable", False)),
+            mode=getattr(mod._module, "capture_mode", None),
             reason=(mod._graphs.disabled_reason if mod._graphs is not None else None),
         )
     with open(os.path.join(out_dir, f"r{rank}.json"), "w") as fh:
@@ -79,22 +98,30 @@ def _worker(rank, world, port, out_dir, p2p):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("p2p", ["0", "force"])
-def test_ddp_graph_two_ranks(tmp_path, p2p):
+@pytest.mark.parametrize("mode,model", [("split", "lenet"), ("inline", "lenet"), ("overlap", "lenet"),
+                                        ("split", "resnet18"), ("overlap", "resnet18")])
+def test_ddp_graph_two_ranks(tmp_path, mode, model):
     port = _free_port()
-    mp.start_processes(_worker, args=(2, port, str(tmp_path), p2p), nprocs=2, start_method="spawn", join=True)
+    mp.start_processes(_worker, args=(2, port, str(tmp_path), mode, model), nprocs=2, start_method="spawn",
+                       join=True)
     r = [json.load(open(tmp_path / f"r{i}.json")) for i in range(2)]
+    # BatchNorm-trained ResNet steps amplify bf16 rounding differences between eager and captured
+    # kernels more than LeNet's: looser bounds there
+    tol_l, tol_w = (2e-3, 5e-3) if model == "lenet" else (2e-2, 2e-2)
     for rank in range(2):
         e, g = r[rank]["False"], r[rank]["True"]
         assert g["replays"] > 0 and g["reason"] == "released", g
-        assert g["p2p"] == (p2p == "force") and g["parts"] == (1 if p2p == "force" else 2), g
+        assert g["mode"] == mode and g["parts"] == (2 if mode == "split" else 1), g
         assert len(e["losses"]) == len(g["losses"]) > 0
         for a, b in zip(e["losses"], g["losses"]):
-            assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (e["losses"], g["losses"])
+            assert abs(a - b) <= tol_l * max(1.0, abs(a)), (e["losses"], g["losses"])
         # weight sums: eager (separate CE launch, fp32 d(logits)) and captured (CE fused into the
         # backward launch) round differently; Adam at lr 1e-2 turns near-zero gradients' rounding
         # differences into +-lr steps, so this checksum gets a looser bound than the losses
-        assert abs(e["w"] - g["w"]) <= 5e-3 * max(1.0, abs(e["w"])), (e["w"], g["w"])
-    # replicas stay identical across ranks, and the reported loss is the cross-rank mean
+        assert abs(e["w"] - g["w"]) <= tol_w * max(1.0, abs(e["w"])), (e["w"], g["w"])
+    # replicas stay identical across ranks (weights AND rank-0-broadcast buffers), and the
+    # reported loss is the cross-rank mean
     assert abs(r[0]["True"]["w"] - r[1]["True"]["w"]) < 1e-6 * max(1.0, abs(r[0]["True"]["w"]))
     assert r[0]["True"]["losses"] == pytest.approx(r[1]["True"]["losses"], rel=1e-6)
+    if model != "lenet":
+        assert abs(r[0]["True"]["bufs"] - r[1]["True"]["bufs"]) < 1e-6 * max(1.0, abs(r[0]["True"]["bufs"]))

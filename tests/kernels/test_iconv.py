@@ -151,14 +151,6 @@ def test_bn_backward_reduction_in_dgrad_epilogue(monkeypatch, kind):
     from rocket_amd.models.resnet import BasicBlock, Bottleneck
     from rocket_amd.ops.norm import BatchNormAct2d
 
-    class Hits(dict):
-        n = 0
-
-        def pop(self, k, d=None):
-            v = super().pop(k, d)
-            Hits.n += v is not None
-            return v
-
     torch.manual_seed(4)
     if kind == "bottleneck":
         net = torch.nn.Sequential(BatchNormAct2d(256, relu=True), Bottleneck(256, 64, 1), Bottleneck(256, 128, 2),
@@ -180,8 +172,7 @@ def test_bn_backward_reduction_in_dgrad_epilogue(monkeypatch, kind):
     for fuse in (True, False):
         net.load_state_dict(state)
         monkeypatch.setattr(nm, "BWD_FUSE", fuse)
-        monkeypatch.setattr(nm, "_BWD_PARTIALS", Hits())
-        Hits.n = 0
+        hits0 = nm.LINK_HITS
         net.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_()
         with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -190,8 +181,8 @@ def test_bn_backward_reduction_in_dgrad_epilogue(monkeypatch, kind):
         g = torch.randn(y.shape, device="cuda").to(y.dtype).contiguous(memory_format=torch.channels_last)
         y.backward(g)
         torch.cuda.synchronize()
-        outs.append((y.detach().float(), x.grad.float(), [p.grad.float().clone() for p in net.parameters()], Hits.n))
-        assert len(nm._BWD_PARTIALS) == 0
+        outs.append((y.detach().float(), x.grad.float(), [p.grad.float().clone() for p in net.parameters()],
+                     nm.LINK_HITS - hits0))
     (y1, dx1, g1, hits), (y2, dx2, g2, nohits) = outs
     assert nohits == 0 and hits >= (7 if kind == "bottleneck" else 4), hits
     assert _rel(y1, y2) < 1e-3

@@ -203,3 +203,18 @@ def test_ga_oracle_from_survey():
     tree.launch()
     assert [int(s) for s in probe.sync] == [0, 1, 0, 1, 0, 1, 1] * 2
     assert len(steps) == 8
+
+
+def test_pre_sharded_device_dataset_batches_all_local_samples():
+    """A pre-sharded DeviceTensorDataset (this rank's samples only) is batched whole on every rank,
+    not split again by rank."""
+    from rocket_amd.runtime.data import DeviceLoader, DeviceTensorDataset
+
+    x = torch.arange(40).float().reshape(40, 1)
+    ds = DeviceTensorDataset(x, torch.arange(40), pre_sharded=True)
+    for rank in (0, 1):
+        dl = DeviceLoader(ds, batch_size=8, num_replicas=2, rank=rank, drop_last=True)
+        seen = sorted(int(v) for b in dl for v in b[1])
+        assert seen == list(range(40))
+    glob = DeviceLoader(DeviceTensorDataset(x, torch.arange(40)), batch_size=8, num_replicas=2, rank=1)
+    assert sum(len(b[1]) for b in glob) < 40
