@@ -10,9 +10,13 @@ separate queues, (b) takes about half of (a).
 """
 
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def chain(x, n):

@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from rocket_amd.ops.iconv import IConv2d, conv_entry
+from rocket_amd.ops.iconv import IConv2d, conv_entry, stem_ok
 from rocket_amd.ops.norm import BatchNormAct2d
 
 
@@ -116,7 +116,8 @@ class ResNet(nn.Module):
     def logits(self, x: torch.Tensor) -> torch.Tensor:
         if not torch.is_autocast_enabled(x.device.type):
             x = x.to(self.fc.weight.dtype if hasattr(self, "fc") else self.head.weight.dtype)  # bf16-stored images
-        x = x.contiguous(memory_format=torch.channels_last)
+        if not stem_ok(self.stem[0], x):  # the native stem reads the image in any layout
+            x = x.contiguous(memory_format=torch.channels_last)
         x = self.stem(x)  # ImageNet stem: the max-pool is inside its BatchNormAct2d
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -23,7 +23,14 @@
 //   attn_bwd_kv block = (head, batch), Q/dO row-major in LDS, waves loop over 16-key tiles: S and
 //               dP with the KEY on the lane, so P^T / dS^T are the A operands of dV = P^T dO and
 //               dK = dS^T Q, with dO and Q read transposed.
-// Row strides of 72 bf16 keep the 16-byte row reads of a fragment on distinct bank groups.
+// LDS images are unpadded 128-B rows (64 bf16) whose 16-B chunks are XOR-swizzled per row pair,
+// chunk' = chunk ^ (((row >> 1) & 3) << 1): both access kinds are then bank-conflict free --
+//  * ds_read_b128 fragment reads (16 rows, chunk 4ks + hi): each of the instruction's four 16-lane
+//    groups is 8 rows at one chunk + the other 8 rows at the next chunk, landing on 16 distinct
+//    16-B slots of the 256-B bank row (two rows per bank row);
+//  * ds_read_b64_tr_b16 transpose reads (per 32-lane half: 8 consecutive rows x 2 chunks).
+// (The round-2 layout, 144-B padded rows, put 2 lanes of every b128 group on one slot: 39-47 %
+// SQ_LDS_BANK_CONFLICT, profiles/r2_pmc_vit_b16.md.)
 #include "rk_common.h"
 
 using namespace rk;
@@ -34,7 +41,7 @@ constexpr int D = 64;
 constexpr int LMAX = 224;        // max tokens: 14 tiles of 16 (7 k-steps of 32)
 constexpr int NT = LMAX / 16;    // 14
 constexpr int NKS = NT / 2;      // 7
-constexpr int RS = D + 8;        // row-major LDS stride (72 bf16 = 144 B: 16-B aligned rows)
+constexpr int RS = D;            // row-major LDS stride (64 bf16 = 128 B), chunk-swizzled (eoff)
 // threads per block (template parameter NTH of each kernel): 4 or 8 waves looping over the head's
 // 16-row tiles (13 at L = 197: 8 waves finish in 2 rounds instead of 4); rk_attn_set_waves
 int g_waves[3] = {8, 82, 82};  // fwd, bwd_q, bwd_kv (82: 8 waves bounded to 128 VGPRs, 2 blocks/CU)
@@ -70,20 +77,27 @@ __device__ __forceinline__ bf16x8 gload_row(const uint16_t* base, int ld, int b,
   return r < L ? v : zero8();
 }
 
+// element offset of 8-element chunk ch of row r in a swizzled [LMAX][64] image (header comment)
+__device__ __forceinline__ int eoff(int r, int ch) { return r * RS + ((ch ^ (((r >> 1) & 3) << 1)) << 3); }
+
 // stage a head's tokens row-major into [LMAX][RS] (zero rows >= L)
 template <int NTH>
 __device__ __forceinline__ void stage_rows(uint16_t* dst, const uint16_t* src, int ld, int b, int L, int h) {
   for (int i = threadIdx.x; i < LMAX * (D / 8); i += NTH) {
-    const int r = i >> 3, c = (i & 7) * 8;
-    *(bf16x8*)(dst + r * RS + c) = gload_row(src, ld, b, L, r, h, c);
+    const int r = i >> 3, ch = i & 7;
+    *(bf16x8*)(dst + eoff(r, ch)) = gload_row(src, ld, b, L, r, h, ch * 8);
   }
 }
+
+// fragment row read: 8 d-values (chunk ch) of row r
+__device__ __forceinline__ bf16x8 frag(const uint16_t* img, int r, int ch) { return ld16(img + eoff(r, ch)); }
 
 // Transpose read of a row-major [.][RS] bf16 image: the calling 16-lane group (lanes 16g..16g+15)
 // gets rows r0..r0+3 (r0 = this group's first row), columns c0..c0+15: lane lo receives column
 // c0 + lo, element q = row r0 + q.  Every lane of the wave must execute it (EXEC all ones).
 __device__ __forceinline__ uint2 tr4(const uint16_t* img, int r0, int c0, int lo) {
-  const uint16_t* p = img + (r0 + (lo >> 2)) * RS + c0 + 4 * (lo & 3);
+  const int c = c0 + 4 * (lo & 3);
+  const uint16_t* p = img + eoff(r0 + (lo >> 2), c >> 3) + (c & 7);
   const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
   return __builtin_bit_cast(uint2, v);
 }
@@ -142,7 +156,7 @@ __global__ void __launch_bounds__(NTH, MINW) attn_fwd_kernel(AttnArgs a) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Ks + (16 * t + lo) * RS + 32 * ks + 8 * hi), qb[ks], acc,
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Ks, 16 * t + lo, 4 * ks + hi), qb[ks], acc,
                                                         0, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {  // C[row = key 16t + 4hi + i][col = query lo]
@@ -230,8 +244,8 @@ __global__ void __launch_bounds__(NTH, MINW) attn_bwd_q_kernel(AttnArgs a) {
         f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Ks + (16 * t + lo) * RS + 32 * ks + 8 * hi), qb[ks], s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Vs + (16 * t + lo) * RS + 32 * ks + 8 * hi), gb[ks], dp, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Ks, 16 * t + lo, 4 * ks + hi), qb[ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Vs, 16 * t + lo, 4 * ks + hi), gb[ks], dp, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -306,8 +320,8 @@ __global__ void __launch_bounds__(NTH, MINW) attn_bwd_kv_kernel(AttnArgs a) {
         if (qt < ntile) {
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk) {
-            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Qs + (16 * qt + lo) * RS + 32 * kk + 8 * hi), kb[kk], s, 0, 0, 0);
-            dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld16(Gs + (16 * qt + lo) * RS + 32 * kk + 8 * hi), vb[kk], dp, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Qs, 16 * qt + lo, 4 * kk + hi), kb[kk], s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Gs, 16 * qt + lo, 4 * kk + hi), vb[kk], dp, 0, 0, 0);
           }
         }
 #pragma unroll

@@ -26,7 +26,7 @@ using namespace rk;
 
 namespace {
 
-enum ConvMode : int { kConvFwd = 0, kConvDgrad = 1, kConvWgrad = 2, kConvDgradS = 3 };
+enum ConvMode : int { kConvFwd = 0, kConvDgrad = 1, kConvWgrad = 2, kConvDgradS = 3, kConvFwdC8 = 4 };
 
 // Strided input gradient, one GEMM per parity class (py, px) of the dX pixels: pixel
 // (2*gi + py, 2*gj + px) receives only the taps r = r0y + 2j, s = r0x + 2l (those with
@@ -48,6 +48,7 @@ struct ConvGeom {
   int64_t w_tap_stride;  // dgrad: elements between taps in W (= Cin); wgrad/fwd unused
   int64_t w_co_stride;   // dgrad: elements between output channels in W (= R*S*Cin)
   float inv_gw, inv_gh;  // 1/GW, 1/GH (pixel decomposition of the wgrad k index)
+  float inv_s;           // 1/S (tap decomposition of the C = 8 stem gather)
   float* bnpart;         // forward: per row-tile BatchNorm partials [tiles_m][2][Cout] (tile mean, M2) or null
   int hoff, woff;        // dgrad: dY pixel of grid pixel (gh, gw) at tap (tr, ts) = (gh + hoff - tr, gw + woff - ts)
   int dx_h, dx_w;        // strided dgrad: dX extent (the epilogue's pixel map)
@@ -115,6 +116,48 @@ struct GatherRows {
       const int w = MODE == kConvFwd ? w0[i] + ts : w0[i] - ts;
       const bool ok = mok[i] && (unsigned)h < (unsigned)cg.H && (unsigned)w < (unsigned)cg.W;
       const int64_t e = ((int64_t)(nb[i] + h) * cg.W + w) * cg.C + c0 + coff[i];
+      const char* src = ok ? (const char*)(x + e) : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0, 0);
+    }
+  }
+};
+
+// Gathered row image for a stem conv on a channel-padded image (C = 8: the 3 image channels + 5
+// zero channels, one 16-byte chunk per pixel): a 64-deep k-tile spans 8 taps, so every chunk of a
+// row is its own tap, (k0 / 8 + chunk).  K = R*S*8 is padded to whole k-tiles: taps >= R*S (and
+// pixels outside the image) come from the zero page, the weights' pad columns are zero.
+template <int R, int NW>
+struct GatherRowsC8 {
+  static constexpr int BK = 64, NI = R * BK / (512 * NW);
+  int pix[NI], h0[NI], w0[NI], j[NI];
+  bool mok[NI];
+  __device__ __forceinline__ void init(const ConvGeom& cg, int row0, int M, int wid, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = (wid * NI + i) * 64 + lane;
+      const int r = q >> 3, c = q & 7;
+      const int m = row0 + r;
+      mok[i] = m < M;
+      const int mm = mok[i] ? m : 0;
+      const int gw = mm % cg.GW, t = mm / cg.GW;
+      const int gh = t % cg.GH, n = t / cg.GH;
+      pix[i] = n * cg.H;
+      h0[i] = gh * cg.stride - cg.pad;
+      w0[i] = gw * cg.stride - cg.pad;
+      j[i] = c ^ rswz<BK>(r);  // the logical chunk (tap offset within the k-tile) this lane fetches
+    }
+  }
+  __device__ __forceinline__ void issue(const uint16_t* x, const ConvGeom& cg, int k0, char* lds, int wid,
+                                        const char* zero) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int tap = (k0 >> 3) + j[i];
+      const int tr = (int)((float)tap * cg.inv_s);  // tap < 2^12: the float quotient is exact after the fixup
+      const int trc = tr - (tr * cg.S > tap) + ((tr + 1) * cg.S <= tap);
+      const int ts = tap - trc * cg.S;
+      const int h = h0[i] + trc, w = w0[i] + ts;
+      const bool ok = mok[i] && tap < cg.R * cg.S && (unsigned)h < (unsigned)cg.H && (unsigned)w < (unsigned)cg.W;
+      const int64_t e = ((int64_t)(pix[i] + h) * cg.W + w) * 8;
       const char* src = ok ? (const char*)(x + e) : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0, 0);
     }
@@ -339,8 +382,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
   constexpr int FM = TM / 16, FN = TN / 16, KK = BK / 32;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr bool FWD = MODE == kConvFwd || MODE == kConvFwdC8;
   constexpr bool AK = MODE == kConvWgrad;   // A K-major (dY read pixel-major)
-  constexpr bool BKM = MODE != kConvFwd;    // B K-major (dgrad: W per tap; wgrad: gathered X)
+  constexpr bool BKM = !FWD;                // B K-major (dgrad: W per tap; wgrad: gathered X)
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE_BYTES];
 
   int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -385,6 +429,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
 
   // operand stagers per mode
   GatherRows<BM, NW, MODE == kConvFwd ? kConvFwd : kConvDgrad> ga;  // fwd/dgrad A
+  GatherRowsC8<BM, NW> ga8;                                            // stem fwd A (C = 8)
   Stager<BM, BK, true, NW> sa_k;                                      // wgrad A (dY K-major)
   Stager<BN, BK, false, NW> sb_row;                                    // fwd B (W rows)
   Stager<BN, BK, true, NW> sb_k;                                       // dgrad B (W per tap)
@@ -392,6 +437,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
   if constexpr (MODE == kConvWgrad) {
     sa_k.init(g.lda, row0, g.M, wid, lane);
     gb.init(cg, col0, g.N, wid, lane);
+  } else if constexpr (MODE == kConvFwdC8) {
+    ga8.init(cg, row0, g.M, wid, lane);
+    sb_row.init(g.ldb, col0, g.N, wid, lane);
   } else {
     ga.init(cg, row0, g.M, wid, lane);
     if constexpr (MODE == kConvFwd) sb_row.init(g.ldb, col0, g.N, wid, lane);
@@ -405,6 +453,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
       if (k0 + BK <= ke) sa_k.issue((const char*)g.a + (int64_t)k0 * g.lda * 2, buf, wid);
       else sa_k.issue_tail((const char*)g.a + (int64_t)k0 * g.lda * 2, buf, wid, lane, ke - k0, zero);
       gb.issue(g.b, cg, k0, ke, buf + A_BYTES, wid, zero);
+    } else if constexpr (MODE == kConvFwdC8) {
+      ga8.issue(g.a, cg, k0, buf, wid, zero);
+      sb_row.issue((const char*)g.b + (int64_t)k0 * 2, buf + A_BYTES, wid);
     } else {
       const int tap = k0 / cg.taps_c, c0 = k0 - tap * cg.taps_c;
       const int tr = tap / cg.S, ts = tap - tr * cg.S;
@@ -466,7 +517,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
       if (i % WN == wn && m < g.M) atomicAdd(g.rowsum + m, racc[i / WN][0]);
     }
   }
-  if constexpr (MODE == kConvFwd) {
+  if constexpr (FWD) {
     if (cg.bnpart != nullptr) tile_bn_stats<BM, BN, WM, WN, FM, FN>(g, cg, acc, tm, row0, col0, wm, wn, lane);
   }
   const uint2 nos[FM][FN] = {};
@@ -541,6 +592,7 @@ ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stri
   cg.hoff = cg.woff = pad; cg.dx_h = cg.dx_w = 0; cg.w_s = S; cg.ncls = 0; cg.zero_nb = 0;
   cg.inv_gw = 1.f / (float)GW;
   cg.inv_gh = 1.f / (float)GH;
+  cg.inv_s = 1.f / (float)S;
   return cg;
 }
 
@@ -573,6 +625,48 @@ RK_API int rk_conv_fwd(const void* x, const void* w, void* y, int y_dt, const fl
   ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
   cg.bnpart = bnpart;
   return launch_conv<kConvFwd>(g, cg, s);
+}
+
+// Stem conv on a channel-padded image: X8 [N][H][W][8] bf16 (image channels + zeros), W8
+// [Cout][Kp] bf16 with the taps' 8 channels in (r, s, c) order and Kp = R*S*8 rounded up to 64
+// (zero pad columns).  Otherwise as rk_conv_fwd (bf16 Y, BatchNorm partials).
+RK_API int rk_conv_fwd_c8(const void* x8, const void* w8, void* y, int N, int H, int W, int Cout, int R, int S,
+                          int stride, int pad, int OH, int OW, float* bnpart, hipStream_t s) {
+  if (Cout % 8 || !aligned16(x8) || !aligned16(w8) || !aligned16(y) || R * S > 4096) return (int)hipErrorInvalidValue;
+  if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
+  const int M = N * OH * OW, Kp = (R * S * 8 + 63) / 64 * 64;
+  MArgs g = margs(x8, 0, w8, Kp, y, BF16, Cout, M, Cout, Kp);
+  g.lds_epi = g_lds_epi;
+  ConvGeom cg = geom(N, H, W, 8, OH, OW, R, S, stride, pad, 8);
+  cg.bnpart = bnpart;
+  return launch_conv<kConvFwdC8>(g, cg, s);
+}
+
+// Image [N][C][H][W] in any memory layout (element (n, c, pixel) at n*sn + c*sc + pixel*sp; C <= 8,
+// 2-byte elements) -> [N][H][W][8] with zero channels C..7 (the stem operand of rk_conv_fwd_c8 /
+// rk_conv_wgrad): one pixel per thread, one 16-byte store.  Reads NCHW batches directly, so the
+// image needs no channels_last copy first.
+__global__ void __launch_bounds__(256) pad_c8_kernel(const uint16_t* __restrict__ x, uint4* __restrict__ y,
+                                                     int64_t pixels, int hw, int C, int64_t sn, int64_t sc, int64_t sp) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= pixels) return;
+  const int64_t n = p / hw, q = p - n * hw;
+  const uint16_t* src = x + n * sn + q * sp;
+  uint16_t v[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) v[c] = c < C ? src[c * sc] : (uint16_t)0;
+  y[p] = make_uint4((uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+                    (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16));
+}
+
+RK_API int rk_pad_c8(const void* x, void* y, int N, int C, int H, int W, int64_t sn, int64_t sc, int64_t sp,
+                     hipStream_t s) {
+  if (C < 1 || C > 8 || !aligned16(y)) return (int)hipErrorInvalidValue;
+  const int64_t pixels = (int64_t)N * H * W;
+  if (pixels <= 0) return 0;
+  pad_c8_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, s>>>((const uint16_t*)x, (uint4*)y, pixels, H * W, C,
+                                                                  sn, sc, sp);
+  return (int)hipGetLastError();
 }
 
 // dX[N*H*W][Cin] (bf16/f32) (+)= conv_transpose(dY, W), stride 1 or 2.  Cout % 64 == 0, Cin % 8 == 0.

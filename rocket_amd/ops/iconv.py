@@ -12,9 +12,12 @@ split-K combine of the weight gradient) — no im2col buffer, no MIOpen solution
 * wgrad: dY x gathered X, split-K over the pixels into f32 slabs, accumulated straight into a
   persistent ``weight.grad`` when the engine provides one.
 
-Shape rules (else the layer is exactly ``nn.Conv2d``): groups = 1, dilation = 1, Cin % 64 == 0
-(the stem conv with 3 input channels stays on the library), Cout % 8 == 0.
-``ROCKET_CONV=native`` (default) | ``lib``.
+Shape rules (else the layer is exactly ``nn.Conv2d``): groups = 1, dilation = 1, Cin % 64 == 0,
+Cout % 8 == 0.  The stem conv (Cin <= 8, an input that takes no gradient: the image) runs natively
+too (:class:`_StemFn`): the image is padded to 8 channels (one 16-byte chunk per pixel) by one
+launch, the forward gathers one tap per chunk (``rk_conv_fwd_c8``, BatchNorm statistics in its
+epilogue) and the weight gradient is the ordinary wgrad kernel on the padded image, its pad
+columns dropped.  ``ROCKET_CONV=native`` (default) | ``lib``.
 """
 
 from __future__ import annotations
@@ -26,7 +29,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops import _lib
-from rocket_amd.ops.linear import _autocast_on, _bf16_copy, _direct, grad_ready
+from rocket_amd.ops.linear import _bf16_copy, _direct, grad_ready, native_route
 from rocket_amd.ops.mgemm import _slab
 
 MODE = os.environ.get("ROCKET_CONV", "native")
@@ -228,8 +231,78 @@ class _EntryFn(torch.autograd.Function):
         return dx, dwa, None, None, None, None, dwb, None, None, None, None, None
 
 
+def _stem_weight(weight: torch.Tensor) -> torch.Tensor:
+    """[Cout][Cin][R][S] fp32 -> bf16 [Cout][Kp], taps' 8 (zero-padded) channels in (r, s, c)
+    order, K padded to whole 64-deep k-tiles."""
+    co, ci, R, S = weight.shape
+    kp = -(-(R * S * 8) // 64) * 64
+    w8 = torch.zeros(co, kp, dtype=torch.bfloat16, device=weight.device)
+    with torch.no_grad():
+        w8[:, : R * S * 8].view(co, R, S, 8)[..., :ci].copy_(weight.detach().permute(0, 2, 3, 1))
+    return w8
+
+
+class _StemFn(torch.autograd.Function):
+    """Stem conv (Cin <= 8) on the native kernels; the input (the image) takes no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pad: int, bnpart):
+        N, C, H, W = x.shape
+        co, _, R, S = weight.shape
+        OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+        dev = x.device
+        s = _lib.stream_ptr(dev)
+        lib = _kernels()
+        xc = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+        sn, sc, sh, sw = xc.stride()
+        if not (sh == W * sw and (sw == 1 or sw == C)):  # pixels must be evenly strided (NCHW or NHWC)
+            xc = xc.contiguous(memory_format=torch.channels_last)
+            sn, sc, sh, sw = xc.stride()
+        x8 = torch.empty((N, H, W, 8), dtype=torch.bfloat16, device=dev)
+        _lib.check(lib.rk_pad_c8(xc.data_ptr(), x8.data_ptr(), N, C, H, W, sn, sc, sw, s), "rk_pad_c8")
+        w8 = _stem_weight(weight)
+        y = torch.empty((N, co, OH, OW), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+        _lib.check(lib.rk_conv_fwd_c8(x8.data_ptr(), w8.data_ptr(), y.data_ptr(), N, H, W, co, R, S, stride, pad, OH,
+                                      OW, _lib.ptr(bnpart), s), "rk_conv_fwd_c8")
+        ctx.save_for_backward(x8)
+        ctx.weight = weight
+        ctx.geo = (N, 8, H, W, co, R, S, stride, pad, OH, OW)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x8,) = ctx.saved_tensors
+        weight = ctx.weight
+        N, C8, H, W, co, R, S, stride, pad, OH, OW = ctx.geo
+        if not ctx.needs_input_grad[1]:
+            return None, None, None, None, None
+        dyc = _cl(dy)
+        dev = dy.device
+        P, ncol = N * OH * OW, R * S * C8
+        t8 = torch.empty(co, ncol, dtype=torch.float32, device=dev)
+        split = _wgrad_split(co, ncol, P)
+        slab = _slab(dev, split * co * ncol) if split > 1 else None
+        _lib.check(_lib.kernels().rk_conv_wgrad(dyc.data_ptr(), x8.data_ptr(), t8.data_ptr(), 0, None, N, H, W, C8, co,
+                                                R, S, stride, pad, OH, OW, split, _lib.ptr(slab),
+                                                _lib.stream_ptr(dev)), "rk_conv_wgrad(stem)")
+        g = t8.view(co, R, S, C8)[..., : weight.shape[1]].permute(0, 3, 1, 2)  # [Cout][Cin][R][S] view
+        if _direct(weight):
+            weight.grad.add_(g)
+            grad_ready(weight)
+            return None, None, None, None, None
+        return None, g.contiguous(memory_format=torch.channels_last), None, None, None
+
+
+def stem_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    return (MODE == "native" and x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and conv.groups == 1 and conv.dilation == (1, 1) and conv.bias is None and conv.in_channels <= 8
+            and conv.out_channels % 8 == 0 and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+            and isinstance(conv.padding[0], int) and conv.weight.dtype == torch.float32 and x.dim() == 4
+            and not x.requires_grad and _lib.available())
+
+
 def native_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
-    return (MODE == "native" and x.is_cuda and _autocast_on() and torch.get_autocast_dtype("cuda") == torch.bfloat16
+    return (MODE == "native" and x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") == torch.bfloat16
             and conv.groups == 1 and conv.dilation == (1, 1) and conv.bias is None
             and conv.in_channels % 64 == 0 and conv.out_channels % 8 == 0 and conv.stride[0] == conv.stride[1]
             and conv.padding[0] == conv.padding[1] and isinstance(conv.padding[0], int)
@@ -267,6 +340,15 @@ class IConv2d(nn.Conv2d):
         return y
 
     def forward(self, x):
+        if stem_ok(self, x):
+            part = None
+            if self.emit_bn_stats:
+                N, _, H, W = x.shape
+                OH = (H + 2 * self.padding[0] - self.kernel_size[0]) // self.stride[0] + 1
+                OW = (W + 2 * self.padding[1] - self.kernel_size[1]) // self.stride[1] + 1
+                part = torch.empty(-(-(N * OH * OW) // TILE_ROWS) * 2 * self.out_channels, dtype=torch.float32,
+                                   device=x.device)
+            return self._attach(_StemFn.apply(x, self.weight, self.stride[0], self.padding[0], part), part)
         if native_ok(self, x):
             w16, part = self._prep(x)
             return self._attach(_IConvFn.apply(x, self.weight, w16, self.stride[0], self.padding[0], part,

@@ -41,6 +41,15 @@ def _autocast_on() -> bool:
         return torch.is_autocast_enabled()
 
 
+def native_route() -> bool:
+    """bf16/fp16 autocast is on and the fused kernels are enabled (``rocket_amd.ops.set_fused``):
+    the model-level layers (IConv2d, MLinear, MMlp, LibLinear, PatchEmbed) take their native paths;
+    otherwise they are exactly the stock torch modules (the ``--impl torch`` A/B and parity runs)."""
+    from rocket_amd.ops import fused_enabled
+
+    return fused_enabled() and _autocast_on()
+
+
 def grad_ready(p: torch.Tensor) -> None:
     hook = getattr(p, "_rocket_grad_hook", None)
     if hook is not None:
@@ -310,7 +319,7 @@ class LibLinear(torch.nn.Linear):
     ``nn.Linear``."""
 
     def forward(self, x):
-        if (x.is_cuda and self.bias is not None and _autocast_on() and self.out_features % 8 == 0
+        if (x.is_cuda and self.bias is not None and native_route() and self.out_features % 8 == 0
                 and torch.is_grad_enabled()):
             cdtype = torch.get_autocast_dtype("cuda")
             w16 = b16 = None
@@ -373,7 +382,7 @@ class PatchEmbed(torch.nn.Conv2d):
 
     def forward(self, x):
         k = self.kernel_size[0]
-        if (x.is_cuda and _autocast_on() and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.dim() == 4
+        if (x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.dim() == 4
                 and x.shape[2] % k == 0 and x.shape[3] % k == 0 and self.weight.is_contiguous()
                 and self.weight.dtype == torch.float32):
             w16 = _bf16_copy(self, "_w16", self.weight)

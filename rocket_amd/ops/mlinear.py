@@ -29,7 +29,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops import _lib
-from rocket_amd.ops.linear import _autocast_on, _bf16_copy, _direct, grad_ready, lib_param_grads
+from rocket_amd.ops.linear import native_route, _bf16_copy, _direct, grad_ready, lib_param_grads
 from rocket_amd.ops.mgemm import mgemm, pick_split
 
 # Which engine runs each product.  ROCKET_VIT_GEMM:
@@ -216,7 +216,7 @@ class _MMlpFn(torch.autograd.Function):
 
 
 def _native(module: nn.Linear, x: torch.Tensor) -> bool:
-    return (x.is_cuda and _autocast_on() and torch.get_autocast_dtype("cuda") == torch.bfloat16
+    return (x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") == torch.bfloat16
             and module.weight.dtype == torch.float32 and module.weight.is_contiguous()
             and _ok(x, module.out_features, module.in_features))
 

@@ -246,6 +246,8 @@ class DataParallel(nn.Module):
         from rocket_amd.runtime import comm as rcomm
 
         ctx = rcomm.context()
+        if ctx.world_size < 2 or not dist.is_initialized():
+            return None
         rccl = getattr(self.comm, "native", False) or (isinstance(self.comm, _TorchDistComm) and self.comm.avg_native)
         if (not p2p.enabled() or not (rccl or (isinstance(self.comm, _TorchDistComm) and p2p.forced()))
                 or ctx.local_world_size != ctx.world_size or ctx.world_size > 8 or not self.buckets

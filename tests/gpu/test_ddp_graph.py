@@ -124,4 +124,8 @@ def test_ddp_graph_two_ranks(tmp_path, mode, model):
     assert abs(r[0]["True"]["w"] - r[1]["True"]["w"]) < 1e-6 * max(1.0, abs(r[0]["True"]["w"]))
     assert r[0]["True"]["losses"] == pytest.approx(r[1]["True"]["losses"], rel=1e-6)
     if model != "lenet":
-        assert abs(r[0]["True"]["bufs"] - r[1]["True"]["bufs"]) < 1e-6 * max(1.0, abs(r[0]["True"]["bufs"]))
+        # BatchNorm statistics are rank 0's at the start of every synchronised forward (torch DDP's
+        # broadcast_buffers semantics), then each rank folds in its own batch: after the last step
+        # they differ only by that one local momentum update (momentum 0.1)
+        b0, b1 = r[0]["True"]["bufs"], r[1]["True"]["bufs"]
+        assert abs(b0 - b1) < 2e-3 * max(1.0, abs(b0)), (b0, b1)

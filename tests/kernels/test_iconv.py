@@ -189,3 +189,30 @@ def test_bn_backward_reduction_in_dgrad_epilogue(monkeypatch, kind):
     assert _rel(dx1, dx2) < 2e-2, _rel(dx1, dx2)
     for a, b in zip(g1, g2):
         assert _rel(a, b) < 2e-2, _rel(a, b)
+
+
+@pytest.mark.parametrize("R,stride,pad,H", [(7, 2, 3, 32), (3, 1, 1, 16)])
+@pytest.mark.parametrize("layout", ["nchw", "nhwc"])
+def test_stem_conv_vs_fp32(R, stride, pad, H, layout):
+    """Native stem conv (Cin = 3 padded to 8 channels, rk_conv_fwd_c8 forward with BatchNorm
+    partials, wgrad on the padded image) vs fp32 F.conv2d, the ImageNet 7x7/s2 and CIFAR 3x3 stems."""
+    from rocket_amd.ops.iconv import IConv2d, TILE_ROWS
+
+    torch.manual_seed(5)
+    conv = IConv2d(3, 64, R, stride=stride, padding=pad, bias=False).cuda()
+    conv.emit_bn_stats = True
+    x = torch.randn(4, 3, H, H, device="cuda").to(torch.bfloat16)
+    if layout == "nhwc":
+        x = x.contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv(x)
+    ref = F.conv2d(x.float(), conv.weight.float(), stride=stride, padding=pad)
+    assert _rel(y, ref) < 1e-2
+    part, ntiles, rows = y._rocket_bn_partials
+    assert rows == TILE_ROWS
+    s1 = part.view(ntiles, 2, 64)[:, 0].sum(0)
+    torch.testing.assert_close(s1, y.float().sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    g = torch.randn(y.shape, device="cuda").to(torch.bfloat16)
+    y.backward(g)
+    wref = torch.nn.grad.conv2d_weight(x.float(), conv.weight.shape, g.float(), stride=stride, padding=pad)
+    assert _rel(conv.weight.grad, wref) < 1e-2
