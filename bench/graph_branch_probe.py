@@ -2,9 +2,10 @@
 
 The overlapped data-parallel step (``runtime/graphs.py``, capture mode ``overlap``) relies on it:
 each bucket all-reduce is a branch forked off backward.  Two chains of small latency-bound
-kernels (each fills only a few CUs) are captured (a) on one stream, (b) on two streams forked
-from the capture stream and joined at the end; if hipGraphLaunch executes the branches on
-separate queues, (b) takes about half of (a).
+spin kernels (each holds one CU for a fixed time) are captured (a) on one stream, (b) on two
+streams forked from the capture stream and joined at the end; if hipGraphLaunch executes the
+branches concurrently, (b) takes about half of (a).  Reported for the current
+DEBUG_CLR_GRAPH_PACKET_CAPTURE setting (run it with both).
 
     python bench/graph_branch_probe.py   ->  one JSON line
 """
@@ -19,9 +20,16 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+SPIN_US, N_SPIN = 100.0, 4
+
+
 def chain(x, n):
-    for _ in range(n):
-        x.mul_(1.0001).add_(1e-6)
+    """n spin kernels of SPIN_US each on one CU (known duration, tiny footprint)."""
+    from rocket_amd.ops import _lib
+
+    lib = _lib.kernels()
+    for _ in range(N_SPIN):
+        lib.rk_spin(SPIN_US, 1, x.data_ptr(), _lib.stream_ptr(x.device))
     return x
 
 
@@ -56,7 +64,7 @@ def main():
         chain(a, n)
         cur.wait_stream(side)
 
-    out = {}
+    out = {"packet_capture": os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE"), "spin_us": SPIN_US, "spins": N_SPIN}
     for name, fn in (("serial", serial), ("forked", forked)):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())

@@ -4,13 +4,16 @@ Pre-norm encoder, 12 layers × (MHSA 12 heads + MLP 3072), 224×224 input → 19
 patches + [CLS] = 197 tokens, width 768.
 
 MI355X path: LayerNorm is the one-wave-per-row HIP kernel emitting bf16 straight
-into the next GEMM (:class:`~rocket_amd.ops.norm.FusedLayerNorm`); every projection runs on the
-native MFMA GEMM (``native/kernels/mgemm.hip`` via :class:`~rocket_amd.ops.mlinear.MLinear`:
-bias in the forward epilogue, K-major dgrad, split-K wgrad with the bias gradient from the same
-launch); the MLP is :class:`~rocket_amd.ops.mlinear.MMlp` (GELU in fc1's epilogue, gelu' in
-fc2's dgrad epilogue); attention is one fused MFMA kernel reading the packed QKV projection
-(``native/kernels/attn.hip``); residual adds are fused into the following LayerNorm.  The residual stream stays
-fp32 (standard AMP numerics); everything feeding a GEMM is bf16.
+into the next GEMM (:class:`~rocket_amd.ops.norm.FusedLayerNorm`), with the residual add fused in;
+attention is one fused MFMA kernel reading the packed QKV projection, forward and one fused
+backward kernel (``native/kernels/attn.hip``); GELU forward and backward (with fc1's bias
+gradient) are single streaming kernels.  The projections (:class:`~rocket_amd.ops.mlinear.MLinear`,
+:class:`~rocket_amd.ops.mlinear.MMlp`) are routed by ``ROCKET_VIT_GEMM``: ``lib`` (default:
+hipBLASLt with the shipped TunableOp table and a bf16 weight copy kept by the fused optimizer,
+K-split wgrads), ``native`` (every product on ``native/kernels/mgemm.hip``: bias / GELU epilogues,
+gelu' in fc2's dgrad epilogue, split-K wgrad with the bias gradient from the same launch) or
+``hybrid``; the default is the faster one measured in-model (``profiles/r2_vit_gemm_routing.md``).
+The residual stream stays fp32 (standard AMP numerics); everything feeding a GEMM is bf16.
 
 Forward contract: ``(img, label) -> (img, label, logits)``.
 """

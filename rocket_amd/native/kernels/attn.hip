@@ -359,9 +359,170 @@ __global__ void __launch_bounds__(NTH, MINW) attn_bwd_kv_kernel(AttnArgs a) {
   }
 }
 
+// ------------------------------------------------------------- backward: fused dQ, dK, dV
+// One block per (head, batch) with ONE WAVE PER 16-KEY TILE (ntile <= 14 waves): S = Q K^T and
+// dP = dO V^T are computed once (the split kernels above compute both twice), with the key on the
+// lane as in attn_bwd_kv, so dV = P^T dO and dK = dS^T Q accumulate in the wave's registers.
+// dQ = dS K sums over ALL key tiles, i.e. over waves: each wave parks its dS chunk (16 keys x 32
+// queries, bf16) in a private 1 KiB LDS image [key][query], reads it back transposed
+// (ds_read_b64_tr_b16: query on the lane, 4 keys per lane = the A operand of a 16x16x16 MFMA) and
+// multiplies by its key tile's K^T fragments (registers, loaded once), adding the 32 x 64 result
+// into an f32 dQ image in LDS (ds_add).  delta = rowsum(dO * O) is formed while dO is staged.
+// LDS: Q, dO images 2 x 28 KiB + dQ 224 x 68 f32 (59.5 KiB) + lse / delta + 14 x 1 KiB.
+constexpr int DQS = D + 4;  // dQ image row stride (f32): rows 4 apart land 16 banks apart
+constexpr int FUSED_MAXW = LMAX / 16;
+
+typedef short s16x4b __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[LMAX * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Gs[LMAX * RS];
+  __shared__ __attribute__((aligned(16))) float dQs[LMAX * DQS];
+  __shared__ float lse_s[LMAX], del_s[LMAX];
+  __shared__ __attribute__((aligned(16))) uint16_t dSs[FUSED_MAXW][16 * 32];
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int nthr = blockDim.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
+  const int L = a.L;
+  const int ntile = (L + 15) / 16;
+  const int64_t bh = (int64_t)b * a.H + h;
+  // stage Q and dO (swizzled row images), delta = rowsum(dO * O) per query, lse; clear dQ
+  for (int i = threadIdx.x; i < LMAX * (D / 8); i += nthr) {  // 8 consecutive threads = one row
+    const int r = i >> 3, ch = i & 7;
+    *(bf16x8*)(Qs + eoff(r, ch)) = gload_row(a.q, a.ld, b, L, r, h, ch * 8);
+    const bf16x8 gv = gload_row(a.dout, a.ldo, b, L, r, h, ch * 8);
+    const bf16x8 ov = gload_row(a.o, a.ldo, b, L, r, h, ch * 8);
+    *(bf16x8*)(Gs + eoff(r, ch)) = gv;
+    const uint4 gu = __builtin_bit_cast(uint4, gv), ou = __builtin_bit_cast(uint4, ov);
+    const uint32_t gw[4] = {gu.x, gu.y, gu.z, gu.w}, ow[4] = {ou.x, ou.y, ou.z, ou.w};
+    float dot = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      dot += __uint_as_float(gw[e] << 16) * __uint_as_float(ow[e] << 16) +
+             __uint_as_float(gw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+    dot += __shfl_xor(dot, 1, 64);
+    dot += __shfl_xor(dot, 2, 64);
+    dot += __shfl_xor(dot, 4, 64);
+    if (ch == 0) {
+      del_s[r] = dot;
+      lse_s[r] = r < L ? a.lse[bh * L + r] : 0.f;
+    }
+  }
+  for (int i = threadIdx.x; i < LMAX * DQS / 4; i += nthr) *(float4*)(dQs + 4 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+
+  const float sl = a.scale * LOG2E;
+  const int kt = w;  // this wave's key tile (every wave of the block has one: blockDim = 64 * ntile)
+  const int k0 = 16 * kt;
+  bf16x8 kb[2], vb[2];  // B operands of S = Q K^T / dP = dO V^T: n = key k0 + lo, k = d
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    kb[ks] = gload_row(a.k, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
+    vb[ks] = gload_row(a.v, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
+  }
+  // K^T fragments of the dQ MFMA (16x16x16 B operand): B[k = key 4hi + j][n = d 16nt + lo]
+  s16x4b kt4[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = k0 + 4 * hi + j;
+      kt4[nt][j] = r < L ? (short)a.k[((int64_t)b * L + r) * a.ld + h * D + 16 * nt + lo] : (short)0;
+    }
+  f32x4 dk[4], dv[4];  // C[row = key 4hi + i][col = d 16nt + lo]
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) dk[nt] = dv[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint16_t* dsw = dSs[w];
+  for (int ks = 0; ks < NKS; ++ks) {
+    if (32 * ks >= 16 * ntile) break;  // uniform
+    f32x4 p2[2], ds2[2];  // query tiles 2ks, 2ks+1: C[row = query 16qt + 4hi + i][col = key lo]
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qt = 2 * ks + u;
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      if (qt < ntile) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Qs, 16 * qt + lo, 4 * kk + hi), kb[kk], sv, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Gs, 16 * qt + lo, 4 * kk + hi), vb[kk], dp, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qi = 16 * qt + 4 * hi + i;
+        const bool ok = qi < L && k0 + lo < L;
+        const float p = ok ? exp2f(sv[i] * sl - lse_s[qi]) : 0.f;
+        p2[u][i] = p;
+        ds2[u][i] = p * (dp[i] - del_s[qi]) * a.scale;
+      }
+    }
+    // A operands: row = key lo, k = queries {32ks + 4hi + i, 32ks + 16 + 4hi + i}
+    const bf16x8 pa = pack_operand(p2[0], p2[1]);
+    const bf16x8 sa = pack_operand(ds2[0], ds2[1]);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      dv[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+          pa, tr_operand(Gs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dv[nt], 0, 0, 0);
+      dk[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+          sa, tr_operand(Qs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dk[nt], 0, 0, 0);
+    }
+    // dQ[32 queries][64 d] += dS[queries][this tile's keys] K[keys][d]: dS -> [key][query] image
+    // (row = key lo, 64 B), then transposed reads give query-on-lane A operands
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      *(uint2*)(dsw + lo * 32 + 16 * u + 4 * hi) = make_uint2(pack2(ds2[u][0], ds2[u][1]), pack2(ds2[u][2], ds2[u][3]));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's image writes landed (wave-private)
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      // lane lo: query 32ks + 16qh + lo, element j = key 4hi + j
+      const uint16_t* p = dsw + (4 * hi + (lo >> 2)) * 32 + 16 * qh + 4 * (lo & 3);
+      const s16x4 av = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+      const s16x4b aq = __builtin_bit_cast(s16x4b, av);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const f32x4 c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(aq, kt4[nt], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // C[row = query 4hi + i][col = d lo]
+          const int q = 32 * ks + 16 * qh + 4 * hi + i;
+          atomicAdd(dQs + q * DQS + 16 * nt + lo, c[i]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = k0 + 4 * hi + i;
+    if (r < L) {
+      uint16_t* rk = a.dk + ((int64_t)b * L + r) * a.ldg + h * D;
+      uint16_t* rv = a.dv + ((int64_t)b * L + r) * a.ldg + h * D;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        rk[16 * nt + lo] = f2bf(dk[nt][i]);
+        rv[16 * nt + lo] = f2bf(dv[nt][i]);
+      }
+    }
+  }
+  __syncthreads();
+  // dQ image -> bf16 rows, 8 d-values (16 B) per thread
+  for (int i = threadIdx.x; i < L * (D / 8); i += nthr) {
+    const int r = i >> 3, c = (i & 7) * 8;
+    const float4 x0 = *(const float4*)(dQs + r * DQS + c), x1 = *(const float4*)(dQs + r * DQS + c + 4);
+    *(uint4*)(a.dq + ((int64_t)b * L + r) * a.ldg + h * D + c) =
+        make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w), pack2(x1.x, x1.y), pack2(x1.z, x1.w));
+  }
+}
+
 }  // namespace
 
+int g_bwd_fused = 1;  // rk_attn_set_bwd_fused
+
 RK_API int rk_attn_max_len() { return LMAX; }
+
+// 1 (default): one fused dQ/dK/dV kernel; 0: the dQ and dK/dV kernels (A/B, ROCKET_ATTN_BWD=split)
+RK_API int rk_attn_set_bwd_fused(int on) {
+  g_bwd_fused = on != 0;
+  return 0;
+}
 
 // waves per block (4 or 8) of the forward, dQ and dK/dV kernels (A/B switch: ROCKET_ATTN_WAVES)
 RK_API int rk_attn_set_waves(int fwd, int bwd_q, int bwd_kv) {
@@ -401,6 +562,11 @@ RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, cons
   a.lse = (float*)lse; a.delta = delta;
   a.ld = ld; a.ldo = ldo; a.ldg = ldg; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);
+  if (g_bwd_fused) {
+    if ((uintptr_t)dq & 15 || ldg % 8) return (int)hipErrorInvalidValue;  // 16-byte dQ row stores
+    attn_bwd_fused_kernel<<<grid, 64 * ((L + 15) / 16), 0, s>>>(a);
+    return (int)hipGetLastError();
+  }
   if (g_waves[1] == 82) attn_bwd_q_kernel<512, 4><<<grid, 512, 0, s>>>(a);
   else if (g_waves[1] == 8) attn_bwd_q_kernel<512><<<grid, 512, 0, s>>>(a);
   else attn_bwd_q_kernel<256><<<grid, 256, 0, s>>>(a);

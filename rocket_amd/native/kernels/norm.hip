@@ -65,15 +65,30 @@ template <> struct V8<float> {
   }
 };
 
-// reduce per-thread [8] accumulators over the BN_RG row groups of the block into red[64]
-__device__ __forceinline__ void reduce_rowgroups(const float* v, float (*lds)[BN_CT + 1], float* out) {
-  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+// reduce per-thread [8] accumulators over the BN_RG row groups of the block into out[64]: the 8
+// row groups of a wave (lanes sharing lane & 7) by xor-shuffles, then the BN_T / 64 wave rows
+// through LDS, written as whole 32-byte channel runs (no bank conflicts; the round-2 version
+// parked every thread's 8 values in a [BN_RG][65] image: 2-way conflicts on every store, 31 %
+// SQ_LDS_BANK_CONFLICT on the BatchNorm reductions).  Fixed order: deterministic.
+constexpr int BN_WV = BN_T / 64;  // waves per block
+__device__ __forceinline__ void reduce_rowgroups(const float* v, float (*lds)[BN_CT], float* out) {
+  float w[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) lds[rg][cg * 8 + k] = v[k];
+  for (int k = 0; k < 8; ++k) {
+    float t = v[k] + __shfl_xor(v[k], 8, 64);
+    t += __shfl_xor(t, 16, 64);
+    w[k] = t + __shfl_xor(t, 32, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < 8) {  // lane == channel group cg
+    *(float4*)&lds[wv][lane * 8] = make_float4(w[0], w[1], w[2], w[3]);
+    *(float4*)&lds[wv][lane * 8 + 4] = make_float4(w[4], w[5], w[6], w[7]);
+  }
   __syncthreads();
   if (threadIdx.x < BN_CT) {
     float s = 0.f;
-    for (int g = 0; g < BN_RG; ++g) s += lds[g][threadIdx.x];
+#pragma unroll
+    for (int g = 0; g < BN_WV; ++g) s += lds[g][threadIdx.x];
     out[threadIdx.x] = s;
   }
   __syncthreads();
@@ -169,7 +184,7 @@ struct BnStatsArgs {
 // one tensor streamed: BN_US rows (16 B each) in flight per thread
 template <typename T>
 __global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
-  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ __attribute__((aligned(16))) float lds[BN_WV][BN_CT];
   __shared__ float s1[BN_CT], s2[BN_CT];
   __shared__ int flag;
   const T* x = (const T*)a.x;
@@ -237,7 +252,7 @@ __global__ void __launch_bounds__(BN_T) bn_stats_kernel(BnStatsArgs a) {
 // p + S1/n, var = S2/n - (S1/n)^2).  "Rows" of this launch are the slices.
 __global__ void __launch_bounds__(BN_T) bn_finalize_kernel(BnStatsArgs a, const float* __restrict__ tp, int ntiles,
                                                            int tile_rows) {
-  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ __attribute__((aligned(16))) float lds[BN_WV][BN_CT];
   __shared__ float s1[BN_CT], s2[BN_CT];
   __shared__ int flag;
   const int c0 = blockIdx.x * BN_CT;
@@ -312,7 +327,7 @@ __global__ void __launch_bounds__(BN_T) bn_finalize_kernel(BnStatsArgs a, const 
 template <typename T>
 __global__ void __launch_bounds__(BN_T) colsum_acc_kernel(const T* __restrict__ x, int64_t R, int C, int rpb,
                                                           float* part, unsigned* counters, float* out) {
-  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ __attribute__((aligned(16))) float lds[BN_WV][BN_CT];
   __shared__ float s1[BN_CT], s2[BN_CT];
   __shared__ int flag;
   const int c0 = blockIdx.x * BN_CT;
@@ -354,7 +369,7 @@ __global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const uint16_t* _
                                                                const uint16_t* __restrict__ z, uint16_t* __restrict__ dz,
                                                                int64_t R, int C, int rpb, float* part,
                                                                unsigned* counters, float* out) {
-  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ __attribute__((aligned(16))) float lds[BN_WV][BN_CT];
   __shared__ float s1[BN_CT], s2[BN_CT];
   __shared__ int flag;
   const int c0 = blockIdx.x * BN_CT;
@@ -462,7 +477,7 @@ struct BnBwdArgs {
 
 template <typename T, typename TO>
 __global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
-  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ __attribute__((aligned(16))) float lds[BN_WV][BN_CT];
   __shared__ float s1[BN_CT], s2[BN_CT];
   __shared__ int flag;
   const TO* dy = (const TO*)a.dy;
@@ -528,7 +543,7 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_reduce_kernel(BnBwdArgs a) {
 // bn_bwd_reduce's result from per-tile partials (sum dy', sum dy'*xhat) written by the stride-1
 // conv dgrad that produced dy' (conv.hip store_tile_lds<BNB>): "rows" of this launch are the tiles.
 __global__ void __launch_bounds__(BN_T) bn_bwd_finalize_kernel(BnBwdArgs a, const float* __restrict__ tp, int ntiles) {
-  __shared__ float lds[BN_RG][BN_CT + 1];
+  __shared__ __attribute__((aligned(16))) float lds[BN_WV][BN_CT];
   __shared__ float s1[BN_CT], s2[BN_CT];
   __shared__ int flag;
   const int c0 = blockIdx.x * BN_CT;
@@ -780,12 +795,9 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c = (j * 64 + lane) * 4;
-    if (c < C) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        sm[(w * 2) * C + c + k] = ag[j][k];
-        sm[(w * 2 + 1) * C + c + k] = ab[j][k];
-      }
+    if (c < C) {  // 16-byte stores: consecutive lanes fill whole bank rows (C % 4 == 0)
+      *(float4*)&sm[(w * 2) * C + c] = make_float4(ag[j][0], ag[j][1], ag[j][2], ag[j][3]);
+      *(float4*)&sm[(w * 2 + 1) * C + c] = make_float4(ab[j][0], ab[j][1], ab[j][2], ab[j][3]);
     }
   }
   __syncthreads();

@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-  tests/kernels/test_iconv.py tests/gpu/test_models.py \
+  tests/kernels/test_iconv.py tests/kernels/test_norm.py tests/gpu/test_models.py \
   > gpurun_out/r3_b_tests.log 2>&1 || { tail -40 gpurun_out/r3_b_tests.log; exit 1; }
 tail -3 gpurun_out/r3_b_tests.log
 timeout -k 10 120 python bench/graph_branch_probe.py > gpurun_out/r3_branch_probe.json 2>gpurun_out/r3_branch_probe.err || exit 1

@@ -118,10 +118,16 @@ def test_fused_add_layernorm():
     assert _rel(ln.weight.grad, w.grad) < 3e-2 and _rel(ln.bias.grad, b.grad) < 3e-2
 
 
+@pytest.mark.parametrize("bwd", ["fused", "split"])
 @pytest.mark.parametrize("B,L,H", [(2, 197, 12), (3, 50, 4), (1, 224, 2), (2, 17, 3)])
-def test_fused_attention_qkv(B, L, H):
-    """Fused MFMA attention (fwd + dQ/dK/dV) vs fp32 softmax attention on the same bf16 inputs."""
-    from rocket_amd.ops.activation import attention_qkv
+def test_fused_attention_qkv(B, L, H, bwd):
+    """Fused MFMA attention (fwd + dQ/dK/dV) vs fp32 softmax attention on the same bf16 inputs, with
+    the one-kernel backward (dQ reduced over key-tile waves in LDS) and the two-kernel backward."""
+    from rocket_amd.ops import _lib
+    from rocket_amd.ops.activation import _attn_lib, attention_qkv
+
+    _attn_lib()
+    _lib.kernels().rk_attn_set_bwd_fused(int(bwd == "fused"))
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -138,6 +144,7 @@ def test_fused_attention_qkv(B, L, H):
     assert o.shape == (B, L, H * D)
     assert _rel(o, ref) < 1.5e-2, _rel(o, ref)
     gq, gr = qkv.grad.view(B, L, 3, H * D), ref_in.grad.view(B, L, 3, H * D)
+    _lib.kernels().rk_attn_set_bwd_fused(1)
     for i, name in enumerate("qkv"):
         assert _rel(gq[:, :, i], gr[:, :, i]) < 3e-2, (name, _rel(gq[:, :, i], gr[:, :, i]))
 
