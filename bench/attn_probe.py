@@ -55,6 +55,15 @@ def main():
     rec = {"fwd_us": round(timed(fwd), 1)}
     lib.rk_attn_set_bwd_fused(1)
     rec["bwd_fused_us"] = round(timed(bwd), 1)
+    # phase stamps of the fused kernel (delta doubles as the stamp buffer: 4 floats per block)
+    stamps = torch.zeros(B * H * 4, device=dev)
+    lib.rk_attn_set_stamps(stamps.data_ptr())
+    bwd()
+    torch.cuda.synchronize()
+    lib.rk_attn_set_stamps(None)
+    st = stamps.view(-1, 4).median(0).values / 100.0  # 100 MHz ticks -> us
+    rec["fused_phase_us"] = {"staged": round(float(st[1]), 2), "loop_done": round(float(st[2]), 2),
+                             "end": round(float(st[3]), 2)}
     lib.rk_attn_set_bwd_fused(0)
     rec["bwd_split_us"] = round(timed(bwd), 1)
     lib.rk_attn_set_bwd_fused(1)

@@ -59,6 +59,7 @@ struct AttnArgs {
   uint16_t* dv;
   float* lse;          // [B*H][L], log2 domain
   float* delta;        // [B*H][L]
+  float* stamps;       // fused backward diagnostics: [B*H][4] phase times, or null (rk_attn_set_stamps)
   int ld, ldo, ldg;
   int L, H;
   float scale;         // softmax scale (1/sqrt(D))
@@ -107,6 +108,14 @@ __device__ __forceinline__ uint2 tr4(const uint16_t* img, int r0, int c0, int lo
 __device__ __forceinline__ bf16x8 tr_operand(const uint16_t* img, int r0a, int r0b, int c0, int lo) {
   const uint2 a = tr4(img, r0a, c0, lo), b = tr4(img, r0b, c0, lo);
   return __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
+}
+
+// transposed read of the fused backward's [key][32-query] dS chunk image (64-B rows): the 16-lane
+// group gets keys r0..r0+3, queries c0..c0+15; lane lo receives query c0 + lo, element j = key r0 + j
+__device__ __forceinline__ uint2 tr4dsc(const uint16_t* img, int r0, int c0, int lo) {
+  const uint16_t* p = img + (r0 + (lo >> 2)) * 32 + c0 + 4 * (lo & 3);
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+  return __builtin_bit_cast(uint2, v);
 }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
@@ -360,36 +369,41 @@ __global__ void __launch_bounds__(NTH, MINW) attn_bwd_kv_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------- backward: fused dQ, dK, dV
-// One block per (head, batch) with ONE WAVE PER 16-KEY TILE (ntile <= 14 waves): S = Q K^T and
-// dP = dO V^T are computed once (the split kernels above compute both twice), with the key on the
-// lane as in attn_bwd_kv, so dV = P^T dO and dK = dS^T Q accumulate in the wave's registers.
-// dQ = dS K sums over ALL key tiles, i.e. over waves: each wave parks its dS chunk (16 keys x 32
-// queries, bf16) in a private 1 KiB LDS image [key][query], reads it back transposed
-// (ds_read_b64_tr_b16: query on the lane, 4 keys per lane = the A operand of a 16x16x16 MFMA) and
-// multiplies by its key tile's K^T fragments (registers, loaded once), adding the 32 x 64 result
-// into an f32 dQ image in LDS (ds_add).  delta = rowsum(dO * O) is formed while dO is staged.
-// LDS: Q, dO images 2 x 28 KiB + dQ 224 x 68 f32 (59.5 KiB) + lse / delta + 14 x 1 KiB.
-constexpr int DQS = D + 4;  // dQ image row stride (f32): rows 4 apart land 16 banks apart
+// One block per (head, batch) with ONE WAVE PER 16-KEY TILE (ntile <= 14 waves); Q, dO and K are
+// staged once (swizzled row images).  The queries are walked in 32-row chunks; per chunk:
+//  A (every wave, its key tile): S = Q K^T and dP = dO V^T with the key on the lane (computed
+//    ONCE; the split kernels compute both twice), P and dS; dV += P^T dO and dK += dS^T Q stay in
+//    the wave's registers; dS goes to the chunk's shared [key][32-query] bf16 image;
+//  B (one barrier later, waves 0..7): one 16-query x 16-d tile of dQ each = dS_chunk K over all
+//    keys (A operand = the dS image read transposed: query on the lane; B = K image read
+//    transposed), complete in one wave -> stored straight to dQ (no cross-wave reduction).
+// The dS image is double-buffered, so a chunk costs one barrier.  delta = rowsum(dO * O) is
+// formed while dO is staged.  LDS: 3 x 28 KiB images + 2 x 14 KiB dS chunks + lse / delta.
+// (A first version reduced dQ over the key-tile waves with LDS float atomics: 5x slower than the
+// split kernels, its chunk loop ~20 us per iteration; bench/attn_probe.py phase stamps.)
 constexpr int FUSED_MAXW = LMAX / 16;
-
-typedef short s16x4b __attribute__((ext_vector_type(4)));
+constexpr int DSC = 32;  // queries per chunk
 
 __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Qs[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Gs[LMAX * RS];
-  __shared__ __attribute__((aligned(16))) float dQs[LMAX * DQS];
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t dSs[2][LMAX * DSC];  // [key][query of the chunk]
   __shared__ float lse_s[LMAX], del_s[LMAX];
-  __shared__ __attribute__((aligned(16))) uint16_t dSs[FUSED_MAXW][16 * 32];
   const int b = blockIdx.z, h = blockIdx.y;
   const int nthr = blockDim.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
   const int L = a.L;
   const int ntile = (L + 15) / 16;
   const int64_t bh = (int64_t)b * a.H + h;
-  // stage Q and dO (swizzled row images), delta = rowsum(dO * O) per query, lse; clear dQ
+  // diagnostics (rk_attn_set_stamps): thread 0 stamps s_memrealtime at phase boundaries into
+  // stamps[block * 4 + 1..3] (staged, chunk loop done, end; bench/attn_probe.py)
+  float* stamp = (a.stamps != nullptr && threadIdx.x == 0) ? a.stamps + (int64_t)bh * 4 : nullptr;
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   for (int i = threadIdx.x; i < LMAX * (D / 8); i += nthr) {  // 8 consecutive threads = one row
     const int r = i >> 3, ch = i & 7;
     *(bf16x8*)(Qs + eoff(r, ch)) = gload_row(a.q, a.ld, b, L, r, h, ch * 8);
+    *(bf16x8*)(Ks + eoff(r, ch)) = gload_row(a.k, a.ld, b, L, r, h, ch * 8);
     const bf16x8 gv = gload_row(a.dout, a.ldo, b, L, r, h, ch * 8);
     const bf16x8 ov = gload_row(a.o, a.ldo, b, L, r, h, ch * 8);
     *(bf16x8*)(Gs + eoff(r, ch)) = gv;
@@ -408,33 +422,53 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
       lse_s[r] = r < L ? a.lse[bh * L + r] : 0.f;
     }
   }
-  for (int i = threadIdx.x; i < LMAX * DQS / 4; i += nthr) *(float4*)(dQs + 4 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  // the dS rows of a key tile without a wave (odd ntile: the last 32-key step's upper half) are
+  // read by the dQ products: keep them zero (uninitialised LDS could hold NaN patterns)
+  for (int i = threadIdx.x; i < 2 * LMAX * DSC / 8; i += nthr) *(uint4*)(&dSs[0][0] + 8 * i) = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
+  if (stamp) stamp[1] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
 
   const float sl = a.scale * LOG2E;
-  const int kt = w;  // this wave's key tile (every wave of the block has one: blockDim = 64 * ntile)
-  const int k0 = 16 * kt;
-  bf16x8 kb[2], vb[2];  // B operands of S = Q K^T / dP = dO V^T: n = key k0 + lo, k = d
+  const int k0 = 16 * w;  // this wave's key tile (blockDim = 64 * ntile: every wave has one)
+  bf16x8 kb[2], vb[2];    // B operands of S = Q K^T / dP = dO V^T: n = key k0 + lo, k = d
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    kb[ks] = gload_row(a.k, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
+    kb[ks] = frag(Ks, k0 + lo, 4 * ks + hi);
     vb[ks] = gload_row(a.v, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
   }
-  // K^T fragments of the dQ MFMA (16x16x16 B operand): B[k = key 4hi + j][n = d 16nt + lo]
-  s16x4b kt4[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = k0 + 4 * hi + j;
-      kt4[nt][j] = r < L ? (short)a.k[((int64_t)b * L + r) * a.ld + h * D + 16 * nt + lo] : (short)0;
-    }
   f32x4 dk[4], dv[4];  // C[row = key 4hi + i][col = d 16nt + lo]
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) dk[nt] = dv[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint16_t* dsw = dSs[w];
+  const int nkey32 = (ntile + 1) / 2;  // 32-key k-steps of the dQ products
+  // phase B of chunk kc (reads dS buffer kc & 1): the chunk's 8 dQ tiles (16 queries qh x 16 d nt)
+  // = sum over keys of dS[q][k] K[k][d], tile t on wave t % nwaves (fewer than 8 waves when L <= 112)
+  auto phase_b = [&](int kc) {
+    const uint16_t* dsc = dSs[kc & 1];
+    for (int t = w; t < 8; t += nthr / 64) {
+      const int qh = t >> 2, nt = t & 3;
+      if (32 * kc + 16 * qh >= L) continue;  // wave-uniform
+      f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+      for (int kq = 0; kq < nkey32; ++kq) {
+        // A: row = query 16qh + lo, k = keys 32kq + {4hi + j, 16 + 4hi + j} (transposed reads of the
+        // [key][query] image); B: k = the same keys, n = d 16nt + lo (transposed reads of K)
+        const uint2 a0 = tr4dsc(dsc, 32 * kq + 4 * hi, 16 * qh, lo), a1 = tr4dsc(dsc, 32 * kq + 16 + 4 * hi, 16 * qh, lo);
+        const bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(a0.x, a0.y, a1.x, a1.y));
+        dq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            av, tr_operand(Ks, 32 * kq + 4 * hi, 32 * kq + 16 + 4 * hi, 16 * nt, lo), dq, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // C[row = query 4hi + i][col = d lo]
+        const int r = 32 * kc + 16 * qh + 4 * hi + i;
+        if (r < L) a.dq[((int64_t)b * L + r) * a.ldg + h * D + 16 * nt + lo] = f2bf(dq[i]);
+      }
+    }
+  };
+  int nchunks = 0;
   for (int ks = 0; ks < NKS; ++ks) {
     if (32 * ks >= 16 * ntile) break;  // uniform
+    nchunks = ks + 1;
+    uint16_t* dsc = dSs[ks & 1];
+    // ---- A: this wave's key tile x the chunk's 32 queries
     f32x4 p2[2], ds2[2];  // query tiles 2ks, 2ks+1: C[row = query 16qt + 4hi + i][col = key lo]
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -456,9 +490,14 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
         ds2[u][i] = p * (dp[i] - del_s[qi]) * a.scale;
       }
     }
-    // A operands: row = key lo, k = queries {32ks + 4hi + i, 32ks + 16 + 4hi + i}
-    const bf16x8 pa = pack_operand(p2[0], p2[1]);
+    const bf16x8 pa = pack_operand(p2[0], p2[1]);  // A: row = key lo, k = the chunk's queries
     const bf16x8 sa = pack_operand(ds2[0], ds2[1]);
+    // dS -> the chunk image first (the barrier below waits for it): row = key k0 + lo, 4
+    // consecutive queries 16u + 4hi .. +3
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      *(uint2*)(dsc + (k0 + lo) * DSC + 16 * u + 4 * hi) =
+          make_uint2(pack2(ds2[u][0], ds2[u][1]), pack2(ds2[u][2], ds2[u][3]));
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       dv[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
@@ -466,29 +505,13 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
       dk[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
           sa, tr_operand(Qs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dk[nt], 0, 0, 0);
     }
-    // dQ[32 queries][64 d] += dS[queries][this tile's keys] K[keys][d]: dS -> [key][query] image
-    // (row = key lo, 64 B), then transposed reads give query-on-lane A operands
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      *(uint2*)(dsw + lo * 32 + 16 * u + 4 * hi) = make_uint2(pack2(ds2[u][0], ds2[u][1]), pack2(ds2[u][2], ds2[u][3]));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's image writes landed (wave-private)
-#pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      // lane lo: query 32ks + 16qh + lo, element j = key 4hi + j
-      const uint16_t* p = dsw + (4 * hi + (lo >> 2)) * 32 + 16 * qh + 4 * (lo & 3);
-      const s16x4 av = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
-      const s16x4b aq = __builtin_bit_cast(s16x4b, av);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const f32x4 c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(aq, kt4[nt], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {  // C[row = query 4hi + i][col = d lo]
-          const int q = 32 * ks + 16 * qh + 4 * hi + i;
-          atomicAdd(dQs + q * DQS + 16 * nt + lo, c[i]);
-        }
-      }
-    }
+    // ---- B of the PREVIOUS chunk in the same barrier interval (its buffer was completed before
+    // the previous barrier; the next chunk's A rewrites it only after the barrier below)
+    if (ks > 0) phase_b(ks - 1);
+    __syncthreads();  // chunk ks's dS rows of every key tile are in
   }
+  if (nchunks > 0) phase_b(nchunks - 1);
+  if (stamp) stamp[2] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = k0 + 4 * hi + i;
@@ -502,25 +525,26 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
       }
     }
   }
-  __syncthreads();
-  // dQ image -> bf16 rows, 8 d-values (16 B) per thread
-  for (int i = threadIdx.x; i < L * (D / 8); i += nthr) {
-    const int r = i >> 3, c = (i & 7) * 8;
-    const float4 x0 = *(const float4*)(dQs + r * DQS + c), x1 = *(const float4*)(dQs + r * DQS + c + 4);
-    *(uint4*)(a.dq + ((int64_t)b * L + r) * a.ldg + h * D + c) =
-        make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w), pack2(x1.x, x1.y), pack2(x1.z, x1.w));
-  }
+  if (stamp) stamp[3] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
 }
 
 }  // namespace
 
-int g_bwd_fused = 1;  // rk_attn_set_bwd_fused
+int g_bwd_fused = 1;         // rk_attn_set_bwd_fused
+float* g_stamps = nullptr;   // rk_attn_set_stamps
 
 RK_API int rk_attn_max_len() { return LMAX; }
 
 // 1 (default): one fused dQ/dK/dV kernel; 0: the dQ and dK/dV kernels (A/B, ROCKET_ATTN_BWD=split)
 RK_API int rk_attn_set_bwd_fused(int on) {
   g_bwd_fused = on != 0;
+  return 0;
+}
+
+// diagnostics: the fused backward writes per-block phase stamps ([B*H][4] f32, 100 MHz ticks)
+// into `p` on its following launches; null turns them off
+RK_API int rk_attn_set_stamps(float* p) {
+  g_stamps = p;
   return 0;
 }
 
@@ -559,14 +583,14 @@ RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, cons
   a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v;
   a.o = (const uint16_t*)o; a.dout = (const uint16_t*)dout;
   a.dq = (uint16_t*)dq; a.dk = (uint16_t*)dk; a.dv = (uint16_t*)dv;
-  a.lse = (float*)lse; a.delta = delta;
+  a.lse = (float*)lse; a.delta = delta; a.stamps = g_stamps;
   a.ld = ld; a.ldo = ldo; a.ldg = ldg; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);
   if (g_bwd_fused) {
-    if ((uintptr_t)dq & 15 || ldg % 8) return (int)hipErrorInvalidValue;  // 16-byte dQ row stores
     attn_bwd_fused_kernel<<<grid, 64 * ((L + 15) / 16), 0, s>>>(a);
     return (int)hipGetLastError();
   }
+  if (delta == nullptr) return (int)hipErrorInvalidValue;  // the split kernels pass delta between them
   if (g_waves[1] == 82) attn_bwd_q_kernel<512, 4><<<grid, 512, 0, s>>>(a);
   else if (g_waves[1] == 8) attn_bwd_q_kernel<512><<<grid, 512, 0, s>>>(a);
   else attn_bwd_q_kernel<256><<<grid, 256, 0, s>>>(a);

@@ -94,6 +94,7 @@ KERNEL_SIGS = {
     "rk_attn_max_len": (c_int, []),
     "rk_attn_set_waves": (c_int, [c_int, c_int, c_int]),
     "rk_attn_set_bwd_fused": (c_int, [c_int]),
+    "rk_attn_set_stamps": (c_int, [c_void_p]),
     "rk_spin": (c_int, [ctypes.c_double, c_int, c_void_p, c_void_p]),
     "rk_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_float,
                             c_void_p]),

@@ -135,7 +135,7 @@ class _AttnQKV(torch.autograd.Function):
         if dout.dtype != qkv.dtype:
             dout = dout.to(qkv.dtype)
         dqkv = torch.empty_like(qkv)
-        delta = torch.empty(B * heads, L, dtype=torch.float32, device=qkv.device)
+        delta = torch.empty(B * heads, L, dtype=torch.float32, device=qkv.device)  # (split backward)
         base, gbase, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
         _lib.check(lib.rk_attn_bwd(base, base + HD * es, base + 2 * HD * es, C3, out.data_ptr(), dout.data_ptr(), HD,
                                    lse.data_ptr(), delta.data_ptr(), gbase, gbase + HD * es, gbase + 2 * HD * es, C3,
