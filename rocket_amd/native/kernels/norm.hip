@@ -54,6 +54,24 @@ template <> struct V8<uint16_t> {
     *(uint4*)p = u;
   }
 };
+template <> struct V8<f16_t> {
+  static __device__ __forceinline__ void load(const f16_t* p, float* v) {
+    const uint4 u = *(const uint4*)p;
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = h2f((uint16_t)(w[k] & 0xffffu));
+      v[2 * k + 1] = h2f((uint16_t)(w[k] >> 16));
+    }
+  }
+  static __device__ __forceinline__ void store(f16_t* p, const float* v) {
+    uint4 u;
+    uint32_t* w = (uint32_t*)&u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2h(v[2 * k]) | ((uint32_t)f2h(v[2 * k + 1]) << 16);
+    *(uint4*)p = u;
+  }
+};
 template <> struct V8<float> {
   static __device__ __forceinline__ void load(const float* p, float* v) {
     const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
@@ -735,19 +753,22 @@ __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const T* __restrict__ x, c
   }
 }
 
-template <typename T, typename TO, int NV>
+// NP = 2: block partials of dgamma / dbeta; NP = 3: also the column sums of the added branch's
+// gradient (dres) — the bias gradient of the linear layer that produced the branch (ViT proj /
+// fc2), so that layer's backward needs no column-sum pass over its output gradient.
+template <typename T, typename TO, int NV, int NP>
 __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
                                                       const float* __restrict__ g, const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                       const T* __restrict__ dsum, TO* __restrict__ dres,
                                                       float* part, int64_t rows, int C, int rows_per_block) {
-  extern __shared__ float sm[];  // [LN_W][2][C]
+  extern __shared__ float sm[];  // [LN_W][NP][C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float ag[NV][4], ab[NV][4];
+  float ag[NV][4], ab[NV][4], ar[NV][4];
 #pragma unroll
   for (int j = 0; j < NV; ++j)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) ag[j][k] = ab[j][k] = 0.f;
+    for (int k = 0; k < 4; ++k) ag[j][k] = ab[j][k] = ar[j][k] = 0.f;
   const int64_t rb = (int64_t)blockIdx.x * rows_per_block;
   const int64_t re = min(rows, rb + rows_per_block);
   for (int64_t row = rb + w; row < re; row += LN_W) {
@@ -788,6 +809,10 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
         }
         st4<T>(dx + row * C + c, o);
         if (dres) st4<TO>(dres + row * C + c, o);  // gradient of the added branch
+        if (NP == 3) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) ar[j][k] += o[k];
+        }
       }
     }
   }
@@ -796,16 +821,17 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
   for (int j = 0; j < NV; ++j) {
     const int c = (j * 64 + lane) * 4;
     if (c < C) {  // 16-byte stores: consecutive lanes fill whole bank rows (C % 4 == 0)
-      *(float4*)&sm[(w * 2) * C + c] = make_float4(ag[j][0], ag[j][1], ag[j][2], ag[j][3]);
-      *(float4*)&sm[(w * 2 + 1) * C + c] = make_float4(ab[j][0], ab[j][1], ab[j][2], ab[j][3]);
+      *(float4*)&sm[(w * NP) * C + c] = make_float4(ag[j][0], ag[j][1], ag[j][2], ag[j][3]);
+      *(float4*)&sm[(w * NP + 1) * C + c] = make_float4(ab[j][0], ab[j][1], ab[j][2], ab[j][3]);
+      if (NP == 3) *(float4*)&sm[(w * NP + 2) * C + c] = make_float4(ar[j][0], ar[j][1], ar[j][2], ar[j][3]);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * C; i += LN_T) {
+  for (int i = threadIdx.x; i < NP * C; i += LN_T) {
     float t = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < LN_W; ++ww) t += sm[ww * 2 * C + i];
-    part[(int64_t)blockIdx.x * 2 * C + i] = t;
+    for (int ww = 0; ww < LN_W; ++ww) t += sm[ww * NP * C + i];
+    part[(int64_t)blockIdx.x * NP * C + i] = t;
   }
 }
 
@@ -813,7 +839,7 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
 // Block: 64 columns x 16 row-slices; each thread strides its slice with 4 loads in flight.
 constexpr int CS_T = 1024;
 __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ part, int nrows, int C2,
-                                                      float* dgamma, float* dbeta, int C) {
+                                                      float* dgamma, float* dbeta, int C, float* dthird = nullptr) {
   __shared__ float red[CS_T / 64][65];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int sl = threadIdx.x >> 6, nsl = CS_T / 64;
@@ -834,8 +860,10 @@ __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ 
     for (int k = 0; k < CS_T / 64; ++k) u += red[k][threadIdx.x];
     if (col < C) {
       if (dgamma) dgamma[col] += u;
-    } else if (dbeta) {
-      dbeta[col - C] += u;
+    } else if (col < 2 * C) {
+      if (dbeta) dbeta[col - C] += u;
+    } else if (dthird) {
+      dthird[col - 2 * C] += u;
     }
   }
 }
@@ -982,6 +1010,9 @@ RK_API int rk_bn_relu_maxpool(int dt, const void* x, const float* scale, const f
   if (dt == BF16)
     bn_relu_maxpool_kernel<uint16_t><<<g, MP_T, 0, s>>>((const uint16_t*)x, scale, shift, (uint16_t*)y,
                                                          (uint8_t*)code, N, H, W, C, OH, OW);
+  else if (dt == F16)
+    bn_relu_maxpool_kernel<f16_t><<<g, MP_T, 0, s>>>((const f16_t*)x, scale, shift, (f16_t*)y, (uint8_t*)code, N, H,
+                                                      W, C, OH, OW);
   else
     bn_relu_maxpool_kernel<float><<<g, MP_T, 0, s>>>((const float*)x, scale, shift, (float*)y, (uint8_t*)code, N, H,
                                                       W, C, OH, OW);
@@ -997,6 +1028,9 @@ RK_API int rk_maxpool_bwd(int dt, const void* dy, const void* code, void* dx, in
   if (dt == BF16)
     maxpool_bwd_kernel<uint16_t><<<g, MP_T, 0, s>>>((const uint16_t*)dy, (const uint8_t*)code, (uint16_t*)dx, N, H,
                                                      W, C, OH, OW);
+  else if (dt == F16)
+    maxpool_bwd_kernel<f16_t><<<g, MP_T, 0, s>>>((const f16_t*)dy, (const uint8_t*)code, (f16_t*)dx, N, H, W, C,
+                                                  OH, OW);
   else
     maxpool_bwd_kernel<float><<<g, MP_T, 0, s>>>((const float*)dy, (const uint8_t*)code, (float*)dx, N, H, W, C,
                                                   OH, OW);
@@ -1013,6 +1047,8 @@ RK_API int rk_bn_stats(int dt, const void* x, int64_t R, int C, const float* gam
   dim3 grid((C + BN_CT - 1) / BN_CT, rb);
   if (dt == BF16)
     bn_stats_kernel<uint16_t><<<grid, BN_T, 0, s>>>(a);
+  else if (dt == F16)
+    bn_stats_kernel<f16_t><<<grid, BN_T, 0, s>>>(a);
   else
     bn_stats_kernel<float><<<grid, BN_T, 0, s>>>(a);
   return (int)hipGetLastError();
@@ -1086,7 +1122,9 @@ RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const fl
   const int rpb = bn_elem_rows(R, C, &grid);
 #define RK_BA(T, TO) bn_apply_kernel<T, TO><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y, \
                                                             relu ? (uint8_t*)mask : nullptr, R, C, relu, rpb)
-  if (dt == BF16 && dto == BF16) RK_BA(uint16_t, uint16_t);
+  if (dt == F16 && dto == F16) RK_BA(f16_t, f16_t);
+  else if (dt == F16 && dto == F32) RK_BA(f16_t, float);
+  else if (dt == BF16 && dto == BF16) RK_BA(uint16_t, uint16_t);
   else if (dt == BF16) RK_BA(uint16_t, float);
   else if (dto == BF16) RK_BA(float, uint16_t);
   else RK_BA(float, float);
@@ -1112,7 +1150,9 @@ RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void*
                                                    (T*)dx,                                                         \
                                                    (TO*)dres, R, C, erpb);                                         \
   } while (0)
-  if (dt == BF16 && dto == BF16) RK_BB(uint16_t, uint16_t);
+  if (dt == F16 && dto == F16) RK_BB(f16_t, f16_t);
+  else if (dt == F16 && dto == F32) RK_BB(f16_t, float);
+  else if (dt == BF16 && dto == BF16) RK_BB(uint16_t, uint16_t);
   else if (dt == BF16) RK_BB(uint16_t, float);
   else if (dto == BF16) RK_BB(float, uint16_t);
   else RK_BB(float, float);
@@ -1143,7 +1183,9 @@ RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, co
 #define RK_BP(T, TO)                                                                                      \
   bn_bwd_apply_kernel<T, TO><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x, nullptr, coef, (T*)dx, (TO*)dres, R, C, \
                                                  erpb)
-  if (dt == BF16 && dto == BF16) RK_BP(uint16_t, uint16_t);
+  if (dt == F16 && dto == F16) RK_BP(f16_t, f16_t);
+  else if (dt == F16 && dto == F32) RK_BP(f16_t, float);
+  else if (dt == BF16 && dto == BF16) RK_BP(uint16_t, uint16_t);
   else if (dt == BF16) RK_BP(uint16_t, float);
   else if (dto == BF16) RK_BP(float, uint16_t);
   else RK_BP(float, float);
@@ -1178,22 +1220,28 @@ constexpr int LN_BWD_RPB = 16;  // rows per block (4 per wave): ~1600 blocks for
 
 RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
   const int64_t rpb = LN_BWD_RPB;
-  return ((rows + rpb - 1) / rpb) * 2 * C;
+  return ((rows + rpb - 1) / rpb) * 3 * C;  // up to three column partials per block (rk_ln_bwd)
 }
 
 // LayerNorm backward; dgamma/dbeta accumulated (+=). dt: x/dx dtype, dto: dy dtype.
 // dsum (dtype dt) / dres (dtype dto) may be null: dx = LN_bwd(dy) [+ dsum], dres = dx
+// dres_sum (f32 [C], optional, needs dres): += column sums of dres (the added branch's bias gradient)
 RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float* g, const float* mean,
                      const float* rstd, void* dx, const void* dsum, void* dres, float* dgamma, float* dbeta,
-                     int64_t rows, int C, float* ws, unsigned* counter, hipStream_t s) {
-  if (C % 4 || C > 64 * 4 * LN_MAXV) return (int)hipErrorInvalidValue;
+                     float* dres_sum, int64_t rows, int C, float* ws, unsigned* counter, hipStream_t s) {
+  if (C % 4 || C > 64 * 4 * LN_MAXV || (dres_sum && !dres)) return (int)hipErrorInvalidValue;
   const int rpb = LN_BWD_RPB;
   const int grid = (int)((rows + rpb - 1) / rpb);
   const int nv = (C + 255) / 256;
-  const size_t smem = (size_t)LN_W * 2 * C * sizeof(float);
-#define RK_LB(T, TO, NV) \
-  ln_bwd_kernel<T, TO, NV><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx, (const T*)dsum, \
-                                                    (TO*)dres, ws, rows, C, rpb)
+  const int np = dres_sum ? 3 : 2;
+  const size_t smem = (size_t)LN_W * np * C * sizeof(float);
+#define RK_LB(T, TO, NV)                                                                                               \
+  if (np == 3)                                                                                                         \
+    ln_bwd_kernel<T, TO, NV, 3><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx,             \
+                                                         (const T*)dsum, (TO*)dres, ws, rows, C, rpb);                 \
+  else                                                                                                                 \
+    ln_bwd_kernel<T, TO, NV, 2><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx,             \
+                                                         (const T*)dsum, (TO*)dres, ws, rows, C, rpb)
 #define RK_LBN(T, TO)                 \
   if (nv <= 1) RK_LB(T, TO, 1);       \
   else if (nv <= 2) RK_LB(T, TO, 2);  \
@@ -1207,7 +1255,8 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
   else { RK_LBN(float, float) }
 #undef RK_LBN
 #undef RK_LB
-  if (dgamma || dbeta) colsum_kernel<<<(2 * C + 63) / 64, CS_T, 0, s>>>(ws, grid, 2 * C, dgamma, dbeta, C);
+  if (dgamma || dbeta || dres_sum)
+    colsum_kernel<<<(np * C + 63) / 64, CS_T, 0, s>>>(ws, grid, np * C, dgamma, dbeta, C, dres_sum);
   (void)counter;
   return (int)hipGetLastError();
 }

@@ -32,6 +32,11 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+// IEEE half (fp16 autocast): storage type _Float16, widened to f32 for math
+typedef _Float16 f16_t;
+__device__ __forceinline__ float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+
 template <typename T> struct Ld;
 template <> struct Ld<float> {
   static __device__ __forceinline__ float get(const float* p, int64_t i) { return p[i]; }
@@ -40,6 +45,10 @@ template <> struct Ld<float> {
 template <> struct Ld<uint16_t> {
   static __device__ __forceinline__ float get(const uint16_t* p, int64_t i) { return bf2f(p[i]); }
   static __device__ __forceinline__ void put(uint16_t* p, int64_t i, float v) { p[i] = f2bf(v); }
+};
+template <> struct Ld<f16_t> {
+  static __device__ __forceinline__ float get(const f16_t* p, int64_t i) { return (float)p[i]; }
+  static __device__ __forceinline__ void put(f16_t* p, int64_t i, float v) { p[i] = (f16_t)v; }
 };
 
 // erf for the GELU kernels and epilogues: Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16

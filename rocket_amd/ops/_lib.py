@@ -115,7 +115,7 @@ KERNEL_SIGS = {
     "rk_p2p_clear_error": (c_int, [c_void_p]),
     "rk_p2p_error_ptr": (c_void_p, [c_void_p]),
     "rk_p2p_destroy": (c_int, [c_void_p]),
-    "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 10 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
+    "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 11 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
 }
 
 

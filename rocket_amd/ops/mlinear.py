@@ -40,6 +40,8 @@ from rocket_amd.ops.mgemm import mgemm, pick_split
 #   native         every product on mgemm (forward, K-major dgrad, split-K wgrad + fused bias grad);
 #   hybrid         mgemm where it won the isolated per-shape probe (bench/mgemm_probe.py): all
 #                  wgrads, the <= 2048-wide dgrads and the K = 3072 forward; the library elsewhere.
+#   libw           forward / dgrad on the library, every weight gradient on mgemm (split-K with the
+#                  bias gradient from the same launch: no K-split batched GEMM + slab sums + colsum)
 MODE = os.environ.get("ROCKET_VIT_GEMM", "lib")
 _TILE_WIDE_FWD, _TILE_DEFAULT = 4, 0
 
@@ -49,11 +51,11 @@ def _fwd_tile(N: int) -> int:
 
 
 def _lib_fwd(K: int) -> bool:
-    return MODE == "lib" or (MODE == "hybrid" and K < 2048)
+    return MODE in ("lib", "libw") or (MODE == "hybrid" and K < 2048)
 
 
 def _lib_dgrad(N_in: int) -> bool:
-    return MODE == "lib" or (MODE == "hybrid" and N_in > 2048)
+    return MODE in ("lib", "libw") or (MODE == "hybrid" and N_in > 2048)
 
 
 def _ok(x: torch.Tensor, N: int, K: int) -> bool:
@@ -115,9 +117,33 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
     return (dw if need_w else None), db
 
 
+BIAS_LINK_HITS = 0  # bias gradients taken from a consuming add-LayerNorm (tests)
+
+
+def _bias_from_link(link, dy: torch.Tensor, bias) -> tuple:
+    """(handled, db): the bias gradient the consuming add-LayerNorm already formed (BiasLink), put
+    into a persistent ``bias.grad`` (db None) or returned; handled False -> compute it here."""
+    db = link.take(dy) if link is not None else None
+    if db is None:
+        return False, None
+    global BIAS_LINK_HITS
+    BIAS_LINK_HITS += 1
+    if _direct(bias):
+        bias.grad.add_(db)
+        grad_ready(bias)
+        return True, None
+    return True, db
+
+
+def _new_link(bias):
+    from rocket_amd.ops.norm import BiasLink
+
+    return BiasLink(bias) if (bias is not None and bias.requires_grad and torch.is_grad_enabled()) else None
+
+
 class _MLinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, w16, b16):
+    def forward(ctx, x, weight, bias, w16, b16, link=None):
         shape = x.shape
         K = shape[-1]
         N = w16.shape[0]
@@ -126,6 +152,7 @@ class _MLinearFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w16)
         ctx.params = (weight, bias)
         ctx.shape = shape
+        ctx.link = link
         return y.reshape(*shape[:-1], N)
 
     @staticmethod
@@ -137,9 +164,14 @@ class _MLinearFn(torch.autograd.Function):
         dx = _linear_dgrad(dy2, w16).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
         need_b = bias is not None and ctx.needs_input_grad[2]
         dw = db = None
+        link, ctx.link = ctx.link, None
+        if need_b:
+            done, db = _bias_from_link(link, dy, bias)
+            need_b = not done
         if ctx.needs_input_grad[1] or need_b:
-            dw, db = _wgrad(dy2, x2, weight, bias, ctx.needs_input_grad[1], need_b)
-        return dx, dw, db, None, None
+            dw, db_ = _wgrad(dy2, x2, weight, bias, ctx.needs_input_grad[1], need_b)
+            db = db_ if need_b else db
+        return dx, dw, db, None, None, None
 
 
 def _gelu_fwd(z: torch.Tensor) -> torch.Tensor:
@@ -181,7 +213,7 @@ class _MMlpFn(torch.autograd.Function):
     MFMAs of every block instead of overlapping them)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, w1_16, b1_16, w2_16, b2_16):
+    def forward(ctx, x, w1, b1, w2, b2, w1_16, b1_16, w2_16, b2_16, link=None):
         shape = x.shape
         K = shape[-1]
         N = w2_16.shape[0]
@@ -192,6 +224,7 @@ class _MMlpFn(torch.autograd.Function):
         ctx.save_for_backward(x2, z, h, w1_16, w2_16)
         ctx.params = (w1, b1, w2, b2)
         ctx.shape = shape
+        ctx.link = link
         return y.reshape(*shape[:-1], N)
 
     @staticmethod
@@ -209,10 +242,17 @@ class _MMlpFn(torch.autograd.Function):
             need_b1 = False
         else:
             dz = _gelu_bwd(_linear_dgrad(dy2, w2_16), z)
-        dw2, db2 = _wgrad(dy2, h, w2, b2, g[3], b2 is not None and g[4])
+        need_b2 = b2 is not None and g[4]
+        link, ctx.link = ctx.link, None
+        db2 = None
+        if need_b2:
+            done, db2 = _bias_from_link(link, dy, b2)
+            need_b2 = not done
+        dw2, db2_ = _wgrad(dy2, h, w2, b2, g[3], need_b2)
+        db2 = db2_ if need_b2 else db2
         dx = _linear_dgrad(dz, w1_16).reshape(ctx.shape) if g[0] else None
         dw1, db1_ = _wgrad(dz, x2, w1, b1, g[1], need_b1)
-        return dx, dw1, (db1 if db1_ is None else db1_), dw2, db2, None, None, None, None
+        return dx, dw1, (db1 if db1_ is None else db1_), dw2, db2, None, None, None, None, None
 
 
 def _native(module: nn.Linear, x: torch.Tensor) -> bool:
@@ -228,7 +268,11 @@ class MLinear(nn.Linear):
         if _native(self, x) and self.bias is not None:
             w16 = _bf16_copy(self, "_w16", self.weight)
             b16 = _bf16_copy(self, "_b16", self.bias)
-            return _MLinearFn.apply(x, self.weight, self.bias, w16, b16)
+            link = _new_link(self.bias)
+            y = _MLinearFn.apply(x, self.weight, self.bias, w16, b16, link)
+            if link is not None:
+                y._rocket_bias_link = link  # a consuming add-LayerNorm may form the bias gradient
+            return y
         return super().forward(x)
 
 
@@ -245,7 +289,11 @@ class MMlp(nn.Module):
         if _native(self.fc1, x) and _ok(x, self.fc2.out_features, self.fc2.in_features) and \
                 self.fc2.weight.is_contiguous() and self.fc1.bias is not None and self.fc2.bias is not None:
             f1, f2 = self.fc1, self.fc2
-            return _MMlpFn.apply(x, f1.weight, f1.bias, f2.weight, f2.bias, _bf16_copy(f1, "_w16", f1.weight),
-                                 _bf16_copy(f1, "_b16", f1.bias), _bf16_copy(f2, "_w16", f2.weight),
-                                 _bf16_copy(f2, "_b16", f2.bias))
+            link = _new_link(f2.bias)
+            y = _MMlpFn.apply(x, f1.weight, f1.bias, f2.weight, f2.bias, _bf16_copy(f1, "_w16", f1.weight),
+                              _bf16_copy(f1, "_b16", f1.bias), _bf16_copy(f2, "_w16", f2.weight),
+                              _bf16_copy(f2, "_b16", f2.bias), link)
+            if link is not None:
+                y._rocket_bias_link = link  # a consuming add-LayerNorm may form fc2's bias gradient
+            return y
         return self.fc2(F.gelu(self.fc1(x)))

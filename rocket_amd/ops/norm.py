@@ -275,22 +275,54 @@ class _LN(torch.autograd.Function):
         counter = _lib.Workspace.get(dev).counter("ln_bwd")
         w = weight.detach() if weight is not None else None
         _lib.check(lib.rk_ln_bwd(_dt(x), _dt(dy), dy.data_ptr(), x.data_ptr(), _lib.ptr(w), mean.data_ptr(),
-                                 rstd.data_ptr(), dx.data_ptr(), None, None, _lib.ptr(dgamma), _lib.ptr(dbeta), rows,
-                                 C, ws.data_ptr(), counter, _lib.stream_ptr(dev)), "rk_ln_bwd")
+                                 rstd.data_ptr(), dx.data_ptr(), None, None, _lib.ptr(dgamma), _lib.ptr(dbeta), None,
+                                 rows, C, ws.data_ptr(), counter, _lib.stream_ptr(dev)), "rk_ln_bwd")
         g = _finish(params, bufs, direct) if params else []
         gw = g[0] if weight is not None else None
         gb = g[-1] if bias is not None else None
         return dx, gw, gb, None, None
 
 
+class BiasLink:
+    """Hand-off between a linear layer whose output ``r`` feeds ONLY an add-LayerNorm and that
+    LayerNorm: the LN backward already streams dr (= the linear's output gradient), so it also
+    forms dr's column sums — the linear's bias gradient — into ``db``; the linear's backward uses
+    them when its incoming gradient is exactly that dr (``dr_ptr``), instead of a column-sum pass
+    over its output gradient.  Lives on the autograd graph (both ctxs), like :class:`BwdLink`."""
+
+    __slots__ = ("bias", "db", "dr_ptr")
+
+    def __init__(self, bias):
+        self.bias = bias
+        self.db = None
+        self.dr_ptr = None
+
+    def take(self, dy: torch.Tensor):
+        """The finished bias gradient for incoming gradient ``dy``, or None (compute it yourself)."""
+        db, self.db = self.db, None
+        ok = db is not None and dy.data_ptr() == self.dr_ptr
+        self.dr_ptr = None
+        return db if ok else None
+
+
+def attach_bias_link(y: torch.Tensor, bias) -> "BiasLink | None":
+    """Tag a linear layer's output with a :class:`BiasLink` (bias that needs a gradient only)."""
+    if bias is None or not bias.requires_grad or not torch.is_grad_enabled():
+        return None
+    link = BiasLink(bias)
+    y._rocket_bias_link = link
+    return link
+
+
 class _AddLN(torch.autograd.Function):
     """(s, y) = (x + r, LayerNorm(x + r)): the pre-norm transformer's residual add fused into its LN.
 
     Backward: dx = LN_bwd(dy) + ds (the residual stream's own gradient) and dr = dx, both written
-    by the same kernel — no separate add / cast / gradient-accumulation passes."""
+    by the same kernel — no separate add / cast / gradient-accumulation passes; with a
+    :class:`BiasLink` on r, the same kernel also sums dr's columns (r's producer's bias gradient)."""
 
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps, out_dtype):
+    def forward(ctx, x, r, weight, bias, eps, out_dtype, link=None):
         lib = _lib.kernels()
         x = x.contiguous()
         r = r.contiguous()
@@ -308,6 +340,7 @@ class _AddLN(torch.autograd.Function):
                                  _lib.stream_ptr(dev)), "rk_ln_fwd(add)")
         ctx.params = (weight, bias)
         ctx.r_dtype = r.dtype
+        ctx.link = link
         ctx.save_for_backward(ssum, mean, rstd)
         return ssum, y
 
@@ -334,14 +367,18 @@ class _AddLN(torch.autograd.Function):
         ws = torch.empty(int(lib.rk_ln_workspace(rows, C)), dtype=torch.float32, device=dev)
         counter = _lib.Workspace.get(dev).counter("ln_bwd")
         w = weight.detach() if weight is not None else None
+        link, ctx.link = ctx.link, None
+        rsum = torch.zeros(C, dtype=torch.float32, device=dev) if link is not None else None
         _lib.check(lib.rk_ln_bwd(_dt(ssum), _dt(dy), dy.data_ptr(), ssum.data_ptr(), _lib.ptr(w), mean.data_ptr(),
                                  rstd.data_ptr(), dx.data_ptr(), _lib.ptr(ds), dr.data_ptr(), _lib.ptr(dgamma),
-                                 _lib.ptr(dbeta), rows, C, ws.data_ptr(), counter, _lib.stream_ptr(dev)),
-                   "rk_ln_bwd(add)")
+                                 _lib.ptr(dbeta), _lib.ptr(rsum), rows, C, ws.data_ptr(), counter,
+                                 _lib.stream_ptr(dev)), "rk_ln_bwd(add)")
+        if link is not None:
+            link.db, link.dr_ptr = rsum, dr.data_ptr()
         g = _finish(params, bufs, direct) if params else []
         gw = g[0] if weight is not None else None
         gb = g[-1] if bias is not None else None
-        return dx, dr, gw, gb, None, None
+        return dx, dr, gw, gb, None, None, None
 
 
 class FusedLayerNorm(nn.LayerNorm):
@@ -358,9 +395,10 @@ class FusedLayerNorm(nn.LayerNorm):
         if (_ops.fused_enabled() and x.is_cuda and len(self.normalized_shape) == 1 and C % 4 == 0 and C <= 4096
                 and x.dtype in (torch.float32, torch.bfloat16) and r.shape == x.shape):
             out_dtype = torch.bfloat16 if (torch.is_autocast_enabled("cuda") or x.dtype == torch.bfloat16) else x.dtype
+            link = getattr(r, "_rocket_bias_link", None)
             if r.dtype != out_dtype:
-                r = r.to(out_dtype)
-            return _AddLN.apply(x, r, self.weight, self.bias, self.eps, out_dtype)
+                r, link = r.to(out_dtype), None  # the producer then sees a different gradient tensor
+            return _AddLN.apply(x, r, self.weight, self.bias, self.eps, out_dtype, link)
         s = x + r
         return s, self(s)
 

@@ -183,3 +183,47 @@ def test_batchnorm_relu_maxpool(dtype, shape):
     assert _rel(x.grad, xr.grad) < gtol
     assert _rel(bn.weight.grad, w.grad) < gtol
     assert _rel(bn.bias.grad, b.grad) < gtol
+
+
+@pytest.mark.parametrize("mlp", [False, True])
+def test_add_ln_forms_branch_bias_grad(mlp):
+    """A linear branch (MLinear / MMlp) feeding a fused add-LayerNorm: the LN backward forms the
+    branch's bias gradient (column sums of dr, BiasLink) and the linear skips its own pass; all
+    gradients equal the stock-torch composition."""
+    import rocket_amd.ops as ops
+    import rocket_amd.ops.mlinear as ml
+    from rocket_amd.ops.norm import FusedLayerNorm
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1)
+    C = 128
+    branch = (ml.MMlp(C, 4 * C) if mlp else ml.MLinear(C, C)).to(dev)
+    ln = FusedLayerNorm(C).to(dev)
+    with torch.no_grad():
+        for p in list(branch.parameters()) + list(ln.parameters()):
+            p.add_(torch.randn_like(p) * 0.1)
+    x0 = torch.randn(4, 50, C, device=dev)
+    h0 = torch.randn(4, 50, C, device=dev)
+    gy = torch.randn(4, 50, C, device=dev)
+    gs = torch.randn(4, 50, C, device=dev)
+    grads = []
+    for fused in (True, False):
+        ops.set_fused(fused)
+        try:
+            for p in list(branch.parameters()) + list(ln.parameters()):
+                p.grad = None
+            hits = ml.BIAS_LINK_HITS
+            x, h = x0.clone().requires_grad_(), h0.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                s, y = ln.add_forward(x, branch(h))
+            ((y.float() * gy).sum() + (s.float() * gs).sum()).backward()
+            torch.cuda.synchronize()
+            grads.append(([p.grad.float().clone() for p in branch.parameters()], h.grad.float(), x.grad.float(),
+                          ml.BIAS_LINK_HITS - hits))
+        finally:
+            ops.set_fused(True)
+    (gn, hn, xn, hits), (gt, ht, xt, _) = grads
+    assert hits == 1
+    for a, b in zip(gn, gt):
+        assert _rel(a, b) < 3e-2, _rel(a, b)
+    assert _rel(hn, ht) < 3e-2 and _rel(xn, xt) < 3e-2
