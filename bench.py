@@ -221,7 +221,10 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "step_ms_p50": round(p50, 4),
+            # host enqueue interval (GPU-paced once the device queue is full) and the unpaced host
+            # cost of issuing one step from an empty queue (runtime/profiling.py StepTimer)
             "host_ms_p50": round(summ.get("host_ms_p50", 0.0), 4),
+            "host_issue_ms": round(summ.get("host_issue_ms", 0.0), 4),
             "step_ms_max": round(summ.get("step_ms_max", 0.0), 4),  # rank 0, worst timing group
             "step_ms_max_at": summ.get("step_ms_max_at"),
             "higher_is_better": True,

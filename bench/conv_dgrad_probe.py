@@ -34,7 +34,7 @@ def case(N, C, H, Co, k, stride):
     st = _lib.stream_ptr(dy.device)
 
     def nat():
-        _lib.check(lib.rk_conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 1, 0, N, H, H, C, Co, k, k, stride,
+        _lib.check(lib.rk_conv_dgrad(1, dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 1, 0, N, H, H, C, Co, k, k, stride,
                                      pad, OH, OH, st), "dgrad")
 
     def ref():

@@ -1,4 +1,4 @@
-// Implicit-GEMM convolutions (NHWC bf16, f32 accumulation) on the MFMA GEMM core (mgemm_core.h)
+// Implicit-GEMM convolutions (NHWC bf16 or fp16, f32 accumulation) on the MFMA GEMM core (mgemm_core.h)
 // for the ResNet configs (reference anchor examples/mnist.py:47-48).
 //
 // Tensors are channels-last: X [N][H][W][C], weights [Cout][R][S][Cin] (the memory order of a
@@ -224,7 +224,7 @@ __device__ __forceinline__ void tile_bn_stats(const MArgs& g, const ConvGeom& cg
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float v = ok ? bf2f(f2bf(acc[i][j][e])) : 0.f;
+        const float v = ok ? round16(acc[i][j][e], g.c_dt) : 0.f;
         s1[j][e] += v;
         s2[j][e] = __builtin_fmaf(v, v, s2[j][e]);
       }
@@ -312,25 +312,25 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
         const uint32_t po[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          v[2 * w] += __uint_as_float(po[w] << 16);
-          v[2 * w + 1] += __uint_as_float(po[w] & 0xffff0000u);
+          v[2 * w] += lo16(po[w], g.c_dt);
+          v[2 * w + 1] += hi16(po[w], g.c_dt);
         }
       }
-      uint16_t hv[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) hv[e] = ((mb >> e) & 1u) ? f2bf(v[e]) : (uint16_t)0;
+      for (int e = 0; e < 8; ++e) v[e] = ((mb >> e) & 1u) ? v[e] : 0.f;
+      const uint32_t pk[4] = {pack16(v[0], v[1], g.c_dt), pack16(v[2], v[3], g.c_dt), pack16(v[4], v[5], g.c_dt),
+                              pack16(v[6], v[7], g.c_dt)};
       if constexpr (BNB) {
         const uint32_t px[4] = {xz.x, xz.y, xz.z, xz.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float x = __uint_as_float((e & 1) ? (px[e >> 1] & 0xffff0000u) : (px[e >> 1] << 16));
-          const float rr = bf2f(hv[e]);
+          const float x = (e & 1) ? hi16(px[e >> 1], g.c_dt) : lo16(px[e >> 1], g.c_dt);
+          const float rr = (e & 1) ? hi16(pk[e >> 1], g.c_dt) : lo16(pk[e >> 1], g.c_dt);
           s1[e] += rr;
           s2[e] = __builtin_fmaf(rr, (x - mu[e]) * is[e], s2[e]);
         }
       }
-      *(uint4*)dst = make_uint4((uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16),
-                                (uint32_t)hv[4] | ((uint32_t)hv[5] << 16), (uint32_t)hv[6] | ((uint32_t)hv[7] << 16));
+      *(uint4*)dst = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     }
   }
   if constexpr (BNB) {
@@ -365,6 +365,17 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
   }
 }
 
+// 16x16x32 MFMA on 16-bit operands held as raw bits: bf16 or (H) fp16
+template <bool H>
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (H) {
+    typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  } else {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+}
+
 // dX row of sub-grid pixel m of a strided-dgrad parity class
 struct ClsRow {
   int GH, GW, H, W, py, px;
@@ -375,7 +386,8 @@ struct ClsRow {
   }
 };
 
-template <int MODE, int BM, int BN, int WM, int WN>
+// H: fp16 operands (MFMA f16; storage / rounding by g.c_dt), else bf16
+template <int MODE, int BM, int BN, int WM, int WN, bool H>
 __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MArgs g, const ConvGeom cg0) {
   constexpr int BK = 64, NS = 2, NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -479,9 +491,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
   f32x4 racc[FR];
 #pragma unroll
   for (int i = 0; i < FR; ++i) racc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ones;
+  bf16x8 ones;  // 1.0 in the operand format
 #pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  for (int e = 0; e < 8; ++e) ones[e] = __builtin_bit_cast(__bf16, (uint16_t)(H ? 0x3C00u : 0x3F80u));
 
   if (nt > 0) issue(0);
   for (int t = 0; t < nt; ++t) {
@@ -502,11 +514,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16<H>(bfr[j], af[i], acc[i][j]);
       if (want_rows) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          if (i % WN == wn) racc[i / WN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], racc[i / WN], 0, 0, 0);
+          if (i % WN == wn) racc[i / WN] = mfma16<H>(ones, af[i], racc[i / WN]);
       }
     }
   }
@@ -565,22 +577,27 @@ int conv_tiles(const MArgs& g, const ConvGeom& cg, int bm, int bn) {
   return ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn);
 }
 
-template <int MODE>
-int launch_conv(const MArgs& g, ConvGeom cg, hipStream_t s) {
+template <int MODE, bool H>
+int launch_conv_t(const MArgs& g, ConvGeom cg, hipStream_t s) {
   // (the forward's wave row slice is 64 pixels in every variant: the BatchNorm partials rely on it)
   // 64-wide GEMM side (Cout / Cin = 64 layers): a 64-wide tile with 4 waves instead of half an
   // empty 128-wide one; everything else 128 x 128 with 8 waves
   if (MODE != kConvWgrad && g.N <= 64) {
     const int tiles = conv_tiles<MODE>(g, cg, 128, 64);
-    conv_kernel<MODE, 128, 64, 2, 2><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+    conv_kernel<MODE, 128, 64, 2, 2, H><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
   } else if (MODE == kConvWgrad && g.M <= 64) {
     const int tiles = ((g.M + 63) / 64) * ((g.N + 127) / 128);
-    conv_kernel<MODE, 64, 128, 2, 2><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+    conv_kernel<MODE, 64, 128, 2, 2, H><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
   } else {
     const int tiles = conv_tiles<MODE>(g, cg, 128, 128);
-    conv_kernel<MODE, 128, 128, 2, 4><<<tiles * g.splitk, 512, 0, s>>>(g, cg);
+    conv_kernel<MODE, 128, 128, 2, 4, H><<<tiles * g.splitk, 512, 0, s>>>(g, cg);
   }
   return (int)hipGetLastError();
+}
+// operand dtype dt: BF16 or F16 (anything else is refused by the entry points)
+template <int MODE>
+int launch_conv(const MArgs& g, ConvGeom cg, int dt, hipStream_t s) {
+  return dt == F16 ? launch_conv_t<MODE, true>(g, cg, s) : launch_conv_t<MODE, false>(g, cg, s);
 }
 
 ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stride, int pad, int taps_c) {
@@ -611,35 +628,41 @@ int g_lds_epi = 1;  // rk_conv_set_lds_epi
 
 }  // namespace
 
-// Y[N*OH*OW][Cout] (bf16 or f32) = conv(X, W) (+ bias[Cout]).  Cin % 64 == 0, Cout % 8 == 0.
+// Operand dtype `dt` (every entry point below): BF16 or F16 — X, W, dY and the 16-bit outputs all
+// in that format (MFMA bf16 / f16, f32 accumulation).
+static bool dt_ok(int dt) { return dt == BF16 || dt == F16; }
+
+// Y[N*OH*OW][Cout] (dt or f32) = conv(X, W) (+ bias[Cout]).  Cin % 64 == 0, Cout % 8 == 0.
 // bnpart (optional): f32 [ceil(N*OH*OW / 64)][2][Cout] per 64-pixel slice (sum, sum of squares)
 // BatchNorm partials for rk_bn_finalize.
-RK_API int rk_conv_fwd(const void* x, const void* w, void* y, int y_dt, const float* bias, int N, int H, int W, int Cin,
-                       int Cout, int R, int S, int stride, int pad, int OH, int OW, float* bnpart, hipStream_t s) {
+RK_API int rk_conv_fwd(int dt, const void* x, const void* w, void* y, int y_dt, const float* bias, int N, int H, int W,
+                       int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, float* bnpart,
+                       hipStream_t s) {
+  if (!dt_ok(dt) || (y_dt != F32 && y_dt != dt)) return (int)hipErrorInvalidValue;
   if (Cin % 64 || Cout % 8 || !aligned16(x) || !aligned16(w) || !aligned16(y)) return (int)hipErrorInvalidValue;
   if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW, K = R * S * Cin;
   MArgs g = margs(x, 0, w, K, y, y_dt, Cout, M, Cout, K);
   g.bias = bias;
-  g.lds_epi = g_lds_epi && y_dt == BF16 && bias == nullptr;
+  g.lds_epi = g_lds_epi && y_dt != F32 && bias == nullptr;
   ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
   cg.bnpart = bnpart;
-  return launch_conv<kConvFwd>(g, cg, s);
+  return launch_conv<kConvFwd>(g, cg, dt, s);
 }
 
-// Stem conv on a channel-padded image: X8 [N][H][W][8] bf16 (image channels + zeros), W8
-// [Cout][Kp] bf16 with the taps' 8 channels in (r, s, c) order and Kp = R*S*8 rounded up to 64
-// (zero pad columns).  Otherwise as rk_conv_fwd (bf16 Y, BatchNorm partials).
-RK_API int rk_conv_fwd_c8(const void* x8, const void* w8, void* y, int N, int H, int W, int Cout, int R, int S,
-                          int stride, int pad, int OH, int OW, float* bnpart, hipStream_t s) {
-  if (Cout % 8 || !aligned16(x8) || !aligned16(w8) || !aligned16(y) || R * S > 4096) return (int)hipErrorInvalidValue;
+// Stem conv on a channel-padded image: X8 [N][H][W][8] (image channels + zeros), W8 [Cout][Kp]
+// with the taps' 8 channels in (r, s, c) order and Kp = R*S*8 rounded up to 64 (zero pad
+// columns).  Otherwise as rk_conv_fwd (Y in dt, BatchNorm partials).
+RK_API int rk_conv_fwd_c8(int dt, const void* x8, const void* w8, void* y, int N, int H, int W, int Cout, int R,
+                          int S, int stride, int pad, int OH, int OW, float* bnpart, hipStream_t s) {
+  if (!dt_ok(dt) || Cout % 8 || !aligned16(x8) || !aligned16(w8) || !aligned16(y) || R * S > 4096) return (int)hipErrorInvalidValue;
   if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW, Kp = (R * S * 8 + 63) / 64 * 64;
-  MArgs g = margs(x8, 0, w8, Kp, y, BF16, Cout, M, Cout, Kp);
+  MArgs g = margs(x8, 0, w8, Kp, y, dt, Cout, M, Cout, Kp);
   g.lds_epi = g_lds_epi;
   ConvGeom cg = geom(N, H, W, 8, OH, OW, R, S, stride, pad, 8);
   cg.bnpart = bnpart;
-  return launch_conv<kConvFwdC8>(g, cg, s);
+  return launch_conv<kConvFwdC8>(g, cg, dt, s);
 }
 
 // Image [N][C][H][W] in any memory layout (element (n, c, pixel) at n*sn + c*sc + pixel*sp; C <= 8,
@@ -683,16 +706,16 @@ RK_API int rk_conv_set_lds_epi(int on) {
 // backward reduction: dX' = relu-mask * dX (+ old dX) is stored (bf16) and part (f32
 // [ceil(N*H*W / 128)][2][Cin]) receives per-128-pixel (sum dX', sum dX' * (x - mean) * invstd) for
 // rk_bn_bwd_partials.  mask may be null (BatchNorm without ReLU).
-RK_API int rk_conv_dgrad_bn(const void* dy, const void* w, void* dx, int accumulate, int N, int H, int W, int Cin,
-                            int Cout, int R, int S, int pad, const void* bn_x, const void* bn_mask, const float* mean,
-                            const float* invstd, float* part, hipStream_t s) {
-  if (Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx) || !aligned16(bn_x) || !part ||
+RK_API int rk_conv_dgrad_bn(int dt, const void* dy, const void* w, void* dx, int accumulate, int N, int H, int W,
+                            int Cin, int Cout, int R, int S, int pad, const void* bn_x, const void* bn_mask,
+                            const float* mean, const float* invstd, float* part, hipStream_t s) {
+  if (!dt_ok(dt) || Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx) || !aligned16(bn_x) || !part ||
       !aligned16(mean) || !aligned16(invstd) || !aligned16(part))
     return (int)hipErrorInvalidValue;
   const int OH = H + 2 * pad - R + 1, OW = W + 2 * pad - S + 1;
   if (OH <= 0 || OW <= 0) return (int)hipErrorInvalidValue;
   const int M = N * H * W, K = R * S * Cout;
-  MArgs g = margs(dy, 0, w, (int64_t)R * S * Cin, dx, BF16, Cin, M, Cin, K);
+  MArgs g = margs(dy, 0, w, (int64_t)R * S * Cin, dx, dt, Cin, M, Cin, K);
   g.accumulate = accumulate;
   ConvGeom cg = geom(N, OH, OW, Cout, H, W, R, S, 1, pad, Cout);
   cg.w_tap_stride = Cin;
@@ -702,22 +725,23 @@ RK_API int rk_conv_dgrad_bn(const void* dy, const void* w, void* dx, int accumul
   cg.bnb_mean = mean;
   cg.bnb_invstd = invstd;
   cg.bnb_part = part;
-  return launch_conv<kConvDgrad>(g, cg, s);
+  return launch_conv<kConvDgrad>(g, cg, dt, s);
 }
 
-RK_API int rk_conv_dgrad(const void* dy, const void* w, void* dx, int dx_dt, int accumulate, int N, int H, int W,
-                         int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, hipStream_t s) {
+RK_API int rk_conv_dgrad(int dt, const void* dy, const void* w, void* dx, int dx_dt, int accumulate, int N, int H,
+                         int W, int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, hipStream_t s) {
+  if (!dt_ok(dt) || (dx_dt != F32 && dx_dt != dt)) return (int)hipErrorInvalidValue;
   if ((stride != 1 && stride != 2) || Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx))
     return (int)hipErrorInvalidValue;
   if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
   const int M = N * H * W, K = R * S * Cout;
   MArgs g = margs(dy, 0, w, (int64_t)R * S * Cin, dx, dx_dt, Cin, M, Cin, K);
   g.accumulate = accumulate;
-  g.lds_epi = g_lds_epi && dx_dt == BF16;
+  g.lds_epi = g_lds_epi && dx_dt != F32;
   ConvGeom cg = geom(N, OH, OW, Cout, H, W, R, S, stride, pad, Cout);
   cg.w_tap_stride = Cin;
   cg.w_co_stride = (int64_t)R * S * Cin;
-  if (stride == 1) return launch_conv<kConvDgrad>(g, cg, s);
+  if (stride == 1) return launch_conv<kConvDgrad>(g, cg, dt, s);
   cg.dx_h = H;
   cg.dx_w = W;
   cg.ncls = 0;
@@ -740,21 +764,21 @@ RK_API int rk_conv_dgrad(const void* dy, const void* w, void* dx, int dx_dt, int
   // a 1x1 kernel (pad 0) leaves three classes without taps: class (0, 0)'s tiles zero them (a
   // tile launch per zero class measured ~3x slower than the whole GEMM)
   if (R == 1 && S == 1 && pad == 0) {
-    if (cg.ncls != 1 || dx_dt != BF16) return (int)hipErrorInvalidValue;
+    if (cg.ncls != 1 || dx_dt == F32) return (int)hipErrorInvalidValue;
     cg.zero_nb = 1;
   } else if (cg.ncls != 4) {
     return (int)hipErrorInvalidValue;  // every class must have taps (or be zeroed by its neighbour)
   }
-  return launch_conv<kConvDgradS>(g, cg, s);
+  return launch_conv<kConvDgradS>(g, cg, dt, s);
 }
 
 // dW[Cout][R*S*Cin] f32 (+)= dY^T (*) X; split-K over the N*OH*OW pixels into `slab`
 // (splitk*Cout*R*S*Cin floats) + one combine launch.  Cin % 8 == 0, Cout % 8 == 0.
 // db (optional, f32 [Cout]) += column sums of dY (the bias gradient) from the same launch.
-RK_API int rk_conv_wgrad(const void* dy, const void* x, float* dw, int accumulate, float* db, int N, int H, int W,
-                         int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, int splitk, float* slab,
-                         hipStream_t s) {
-  if (Cin % 8 || Cout % 8 || !aligned16(dy) || !aligned16(x)) return (int)hipErrorInvalidValue;
+RK_API int rk_conv_wgrad(int dt, const void* dy, const void* x, float* dw, int accumulate, float* db, int N, int H,
+                         int W, int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, int splitk,
+                         float* slab, hipStream_t s) {
+  if (!dt_ok(dt) || Cin % 8 || Cout % 8 || !aligned16(dy) || !aligned16(x)) return (int)hipErrorInvalidValue;
   const int P = N * OH * OW, Ncol = R * S * Cin;
   MArgs g = margs(dy, Cout, x, 0, dw, F32, Ncol, Cout, Ncol, P);
   g.rowsum = db;
@@ -767,7 +791,7 @@ RK_API int rk_conv_wgrad(const void* dy, const void* x, float* dw, int accumulat
   g.k_per_split = kps;
   g.slab = slab;
   ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
-  int rc = launch_conv<kConvWgrad>(g, cg, s);
+  int rc = launch_conv<kConvWgrad>(g, cg, dt, s);
   if (rc || splitk == 1) return rc;
   launch_mgemm_reduce(slab, splitk, Cout, Ncol, nullptr, dw, F32, Ncol, accumulate, s);
   return (int)hipGetLastError();

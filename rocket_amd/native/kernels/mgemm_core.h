@@ -209,9 +209,8 @@ __device__ __forceinline__ void store_tile(const MArgs& g, f32x4 (&acc)[FM][FN],
       float v[4] = {acc[i][j][0] + bias.x, acc[i][j][1] + bias.y, acc[i][j][2] + bias.z, acc[i][j][3] + bias.w};
       if (g.epi == kGelu || g.epi == kRelu) {
         if (g.c_pre) {
-          if (g.c_dt == BF16)
-            *(uint2*)((uint16_t*)g.c_pre + off) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                                                             (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+          if (g.c_dt != F32)
+            *(uint2*)((uint16_t*)g.c_pre + off) = make_uint2(pack16(v[0], v[1], g.c_dt), pack16(v[2], v[3], g.c_dt));
           else
             *(float4*)((float*)g.c_pre + off) = make_float4(v[0], v[1], v[2], v[3]);
         }
@@ -219,22 +218,21 @@ __device__ __forceinline__ void store_tile(const MArgs& g, f32x4 (&acc)[FM][FN],
         for (int e = 0; e < 4; ++e) v[e] = g.epi == kGelu ? gelu_f(v[e]) : fmaxf(v[e], 0.f);
       } else if (g.epi == kMulGeluGrad || g.epi == kMulReluGrad) {
         const uint2 z = PRE ? side[i][j] : *(const uint2*)(g.aux + off);
-        const float zz[4] = {__uint_as_float(z.x << 16), __uint_as_float(z.x & 0xffff0000u), __uint_as_float(z.y << 16),
-                             __uint_as_float(z.y & 0xffff0000u)};
+        const int adt = g.c_dt == F16 ? F16 : BF16;  // aux is 16-bit, same format as a 16-bit C
+        const float zz[4] = {lo16(z.x, adt), hi16(z.x, adt), lo16(z.y, adt), hi16(z.y, adt)};
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = g.epi == kMulGeluGrad ? v[e] * gelu_grad(zz[e]) : (zz[e] > 0.f ? v[e] : 0.f);
       }
-      if (g.c_dt == BF16) {
+      if (g.c_dt != F32) {
         uint16_t* c = (uint16_t*)g.c + off;
         if (g.accumulate) {
           const uint2 o = PRE ? side[i][j] : *(const uint2*)c;
-          v[0] += __uint_as_float(o.x << 16);
-          v[1] += __uint_as_float(o.x & 0xffff0000u);
-          v[2] += __uint_as_float(o.y << 16);
-          v[3] += __uint_as_float(o.y & 0xffff0000u);
+          v[0] += lo16(o.x, g.c_dt);
+          v[1] += hi16(o.x, g.c_dt);
+          v[2] += lo16(o.y, g.c_dt);
+          v[3] += hi16(o.y, g.c_dt);
         }
-        *(uint2*)c = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                                (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+        *(uint2*)c = make_uint2(pack16(v[0], v[1], g.c_dt), pack16(v[2], v[3], g.c_dt));
       } else {
         float* c = (float*)g.c + off;
         if (g.accumulate) {
@@ -247,7 +245,7 @@ __device__ __forceinline__ void store_tile(const MArgs& g, f32x4 (&acc)[FM][FN],
   }
 }
 
-// C[m][n] (+)= sum_s slab[s][m][n] + bias[n]  (f32 or bf16 C; N % 4 == 0).  G consecutive lanes share
+// C[m][n] (+)= sum_s slab[s][m][n] + bias[n]  (f32, bf16 or f16 C; N % 4 == 0).  G consecutive lanes share
 // one output float4, lane g summing the slabs s = g, g + G, ... (four loads in flight), combined by
 // xor-shuffles: small outputs with many splits (ResNet wgrads: 9k float4 x 32 splits) get G-fold more
 // loads in flight instead of a long serial slab loop per thread.  Fixed order: deterministic.
@@ -290,15 +288,14 @@ __global__ void __launch_bounds__(256) mgemm_reduce(const float* __restrict__ sl
       v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
     }
     const int64_t off = (int64_t)m * ldc + n;
-    if (c_dt == BF16) {
+    if (c_dt != F32) {
       uint16_t* o = (uint16_t*)c + off;
       if (accumulate) {
         const uint2 p = *(const uint2*)o;
-        v.x += __uint_as_float(p.x << 16); v.y += __uint_as_float(p.x & 0xffff0000u);
-        v.z += __uint_as_float(p.y << 16); v.w += __uint_as_float(p.y & 0xffff0000u);
+        v.x += lo16(p.x, c_dt); v.y += hi16(p.x, c_dt);
+        v.z += lo16(p.y, c_dt); v.w += hi16(p.y, c_dt);
       }
-      *(uint2*)o = make_uint2((uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
-                              (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+      *(uint2*)o = make_uint2(pack16(v.x, v.y, c_dt), pack16(v.z, v.w, c_dt));
     } else {
       float* o = (float*)c + off;
       if (accumulate) {

@@ -1085,7 +1085,7 @@ static int bn_elem_rows(int64_t R, int C, int* grid) {
   return (int)per;
 }
 
-// out[c] += sum_r x[r][c]  (x: [R][C], dt 0 f32 / 1 bf16, C % 8 == 0); ws: rk_bn_workspace(R, C)
+// out[c] += sum_r x[r][c]  (x: [R][C], dt f32 / bf16 / f16, C % 8 == 0); ws: rk_bn_workspace(R, C)
 // floats, counters: rk_bn_counters(C) zeroed uints (self-resetting)
 RK_API int rk_colsum_acc(int dt, const void* x, int64_t R, int C, float* out, float* ws, unsigned* counters,
                          hipStream_t s) {
@@ -1095,6 +1095,8 @@ RK_API int rk_colsum_acc(int dt, const void* x, int64_t R, int C, float* out, fl
   dim3 grid((C + BN_CT - 1) / BN_CT, rb);
   if (dt == BF16)
     colsum_acc_kernel<uint16_t><<<grid, BN_T, 0, s>>>((const uint16_t*)x, R, C, rpb, ws, counters, out);
+  else if (dt == F16)
+    colsum_acc_kernel<f16_t><<<grid, BN_T, 0, s>>>((const f16_t*)x, R, C, rpb, ws, counters, out);
   else
     colsum_acc_kernel<float><<<grid, BN_T, 0, s>>>((const float*)x, R, C, rpb, ws, counters, out);
   return (int)hipGetLastError();
@@ -1117,6 +1119,7 @@ RK_API int rk_gelu_bwd_colsum(const void* dh, const void* z, void* dz, int64_t R
 // null): the ReLU mask bits for rk_bn_bwd.
 RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const float* scale, const float* shift, void* y,
                        void* mask, int64_t R, int C, int relu, hipStream_t s) {
+  if (dto == F16 && dt != F16) return (int)hipErrorInvalidValue;  // f16 variants: (f16, f16), (f16, f32)
   if (C % 8 || C > 8 * BN_T || R <= 0) return (int)hipErrorInvalidValue;
   int grid;
   const int rpb = bn_elem_rows(R, C, &grid);
@@ -1137,6 +1140,7 @@ RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const fl
 RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void* mask, int64_t R, int C,
                      const float* mean, const float* invstd, const float* scale, float* dgamma, float* dbeta, void* dx,
                      void* dres, float* ws, float* coef /*[3C]*/, unsigned* counters, hipStream_t s) {
+  if (dto == F16 && dt != F16) return (int)hipErrorInvalidValue;  // f16 variants: (f16, f16), (f16, f32)
   if (C % 8 || C > 8 * BN_T || R <= 0) return (int)hipErrorInvalidValue;
   BnBwdArgs a{dy, x, (const uint8_t*)mask, R, C, 0, mean, invstd, ws, counters, dgamma, dbeta, scale, coef};
   const int rb = bn_grid_rows(R, C, &a.rpb);
@@ -1169,6 +1173,7 @@ RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, co
                               int C, const float* mean, const float* invstd, const float* scale, float* dgamma,
                               float* dbeta, void* dx, void* dres, float* ws, float* coef, unsigned* counters,
                               hipStream_t s) {
+  if (dto == F16 && dt != F16) return (int)hipErrorInvalidValue;  // f16 variants: (f16, f16), (f16, f32)
   if (C % 8 || C > 8 * BN_T || R <= 0 || ntiles <= 0) return (int)hipErrorInvalidValue;
   BnBwdArgs a{dy, x, nullptr, R, C, 0, mean, invstd, ws, counters, dgamma, dbeta, scale, coef};
   int rpb_rows;
@@ -1195,6 +1200,7 @@ RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, co
 
 RK_API int rk_ln_fwd(int dt, int dto, const void* x, const void* res, void* sum_out, const float* g, const float* b,
                      void* y, float* mean, float* rstd, int64_t rows, int C, float eps, hipStream_t s) {
+  if (dt == F16 || dto == F16) return (int)hipErrorInvalidValue;  // LayerNorm: f32 / bf16 only
   if (C % 4 || C > 64 * 4 * LN_MAXV) return (int)hipErrorInvalidValue;
   const int grid = (int)((rows + LN_W - 1) / LN_W);
   const int nv = (C + 255) / 256;
@@ -1229,6 +1235,7 @@ RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
 RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float* g, const float* mean,
                      const float* rstd, void* dx, const void* dsum, void* dres, float* dgamma, float* dbeta,
                      float* dres_sum, int64_t rows, int C, float* ws, unsigned* counter, hipStream_t s) {
+  if (dt == F16 || dto == F16) return (int)hipErrorInvalidValue;  // LayerNorm: f32 / bf16 only
   if (C % 4 || C > 64 * 4 * LN_MAXV || (dres_sum && !dres)) return (int)hipErrorInvalidValue;
   const int rpb = LN_BWD_RPB;
   const int grid = (int)((rows + rpb - 1) / rpb);

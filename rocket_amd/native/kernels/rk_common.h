@@ -37,6 +37,19 @@ typedef _Float16 f16_t;
 __device__ __forceinline__ float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
 __device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 
+// 16-bit storage chosen at run time (dt = BF16 / F16; wave-uniform, so the branch is free):
+// pack two f32 into one 32-bit word, widen its low / high element, round an f32 to the storage type
+__device__ __forceinline__ uint32_t pack16(float a, float b, int dt) {
+  return dt == F16 ? (uint32_t)f2h(a) | ((uint32_t)f2h(b) << 16) : (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+__device__ __forceinline__ float lo16(uint32_t w, int dt) {
+  return dt == F16 ? h2f((uint16_t)(w & 0xffffu)) : __uint_as_float(w << 16);
+}
+__device__ __forceinline__ float hi16(uint32_t w, int dt) {
+  return dt == F16 ? h2f((uint16_t)(w >> 16)) : __uint_as_float(w & 0xffff0000u);
+}
+__device__ __forceinline__ float round16(float v, int dt) { return dt == F16 ? h2f(f2h(v)) : bf2f(f2bf(v)); }
+
 template <typename T> struct Ld;
 template <> struct Ld<float> {
   static __device__ __forceinline__ float get(const float* p, int64_t i) { return p[i]; }

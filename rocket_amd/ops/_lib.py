@@ -41,16 +41,16 @@ KERNEL_SIGS = {
     "rk_mgemm": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p,
                          c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "rk_slab_acc": (c_int, [c_void_p, c_int, c_int, c_int64, c_void_p, c_int, c_void_p]),
-    "rk_conv_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 11 + [c_void_p, c_void_p]),
-    "rk_conv_fwd_c8": (c_int, [c_void_p, c_void_p, c_void_p] + [c_int] * 10 + [c_void_p, c_void_p]),
+    "rk_conv_fwd": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 11 + [c_void_p, c_void_p]),
+    "rk_conv_fwd_c8": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p] + [c_int] * 10 + [c_void_p, c_void_p]),
     "rk_pad_c8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_int64, c_void_p]),
     "rk_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_int64, c_int] + [c_void_p] * 9 + [c_float, c_float, c_void_p,
                                                                                             c_void_p, c_void_p]),
     "rk_conv_set_lds_epi": (c_int, [c_int]),
-    "rk_conv_dgrad_bn": (c_int, [c_void_p] * 3 + [c_int] * 9 + [c_void_p] * 6),
+    "rk_conv_dgrad_bn": (c_int, [c_int] + [c_void_p] * 3 + [c_int] * 9 + [c_void_p] * 6),
     "rk_bn_bwd_partials": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_int] + [c_void_p] * 11),
-    "rk_conv_dgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_int] * 11 + [c_void_p]),
-    "rk_conv_wgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p, c_void_p]),
+    "rk_conv_dgrad": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_int] * 11 + [c_void_p]),
+    "rk_conv_wgrad": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p, c_void_p]),
     "rk_conv_pool_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 7 + [c_void_p]),
     "rk_conv_pool_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
     "rk_conv_pool_dgrad": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int] + [c_int] * 7 + [c_void_p]),

@@ -1,12 +1,13 @@
-"""Channels-last bf16 convolutions on the native implicit-GEMM MFMA kernels (``native/kernels/conv.hip``).
+"""Channels-last bf16 / fp16 convolutions on the native implicit-GEMM MFMA kernels (``native/kernels/conv.hip``).
 
 :class:`IConv2d` is ``nn.Conv2d`` (same parameters / state_dict) whose forward, input gradient and
-weight gradient under bf16 autocast on a HIP device each run as one implicit-GEMM launch (plus the
+weight gradient under bf16 or fp16 autocast on a HIP device each run as one implicit-GEMM launch
+(MFMA bf16 / f16 by the autocast dtype, f32 accumulation; plus the
 split-K combine of the weight gradient) — no im2col buffer, no MIOpen solution search, no
 ``SubTensorOp`` casts:
 
 * forward: gathered NHWC activations x channels_last weights (read as a bf16 copy a fused
-  optimizer keeps current: dense bf16 shadow, ``_bf16_copy``);
+  optimizer keeps current: dense bf16 shadow, ``_bf16_copy``; fp16: a per-forward cast);
 * dgrad: dY gathered with the flipped taps x the weights read K-major per tap; stride 2 as the
   four parity classes of dX pixels (each a stride-1 gather over its taps) in one launch;
 * wgrad: dY x gathered X, split-K over the pixels into f32 slabs, accumulated straight into a
@@ -29,7 +30,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops import _lib
-from rocket_amd.ops.linear import _bf16_copy, _direct, grad_ready, native_route
+from rocket_amd.ops.linear import _direct, _lowp_copy, grad_ready, native_route
 from rocket_amd.ops.mgemm import _slab
 
 MODE = os.environ.get("ROCKET_CONV", "native")
@@ -53,10 +54,18 @@ def _kernels():
     return lib
 
 
-def _cl(t: torch.Tensor) -> torch.Tensor:
-    if t.dtype != torch.bfloat16:
-        t = t.to(torch.bfloat16)
+_LOWP = (torch.bfloat16, torch.float16)
+
+
+def _cl(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    if t.dtype != dtype:
+        t = t.to(dtype)
     return t.contiguous(memory_format=torch.channels_last)
+
+
+def _dt(t: torch.Tensor) -> int:
+    """conv.hip operand dtype code (BF16 = 1, F16 = 2)."""
+    return 2 if t.dtype == torch.float16 else 1
 
 
 def _wgrad_split(cout: int, ncol: int, pixels: int) -> int:
@@ -93,8 +102,9 @@ def _conv_fwd(xc: torch.Tensor, w16: torch.Tensor, stride: int, pad: int, bnpart
     Co, _, R, S = w16.shape
     OH = (H + 2 * pad - R) // stride + 1
     OW = (W + 2 * pad - S) // stride + 1
-    y = torch.empty((N, Co, OH, OW), dtype=torch.bfloat16, device=xc.device, memory_format=torch.channels_last)
-    _lib.check(_kernels().rk_conv_fwd(xc.data_ptr(), w16.data_ptr(), y.data_ptr(), 1, None, N, H, W, C, Co, R, S,
+    y = torch.empty((N, Co, OH, OW), dtype=xc.dtype, device=xc.device, memory_format=torch.channels_last)
+    _lib.check(_kernels().rk_conv_fwd(_dt(xc), xc.data_ptr(), w16.data_ptr(), y.data_ptr(), _dt(xc), None, N, H, W, C,
+                                      Co, R, S,
                                            stride, pad, OH, OW, _lib.ptr(bnpart), _lib.stream_ptr(xc.device)),
                "rk_conv_fwd")
     return y
@@ -113,7 +123,7 @@ def _bn_src(x: torch.Tensor, stride: int):
     if link is None or link.src is None or stride != 1:
         return None
     z = link.src[0]
-    if z.shape != x.shape or z.dtype != torch.bfloat16 or not z.is_contiguous(memory_format=torch.channels_last):
+    if z.shape != x.shape or z.dtype not in _LOWP or not z.is_contiguous(memory_format=torch.channels_last):
         return None
     return link
 
@@ -124,14 +134,15 @@ def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | No
     the epilogue also applies its ReLU mask and writes its backward reduction partials, handed to
     the BatchNorm's backward through the link (``norm.BwdLink.done``)."""
     N, C, H, W, Co, R, S, stride, pad, OH, OW = geo
-    if bn is not None and bn.src is not None and stride == 1 and Co % 64 == 0 and C % 8 == 0:
+    if (bn is not None and bn.src is not None and stride == 1 and Co % 64 == 0 and C % 8 == 0
+            and bn.src[0].dtype == dyc.dtype):
         z, mask, stats = bn.src
         acc = dx is not None
         if dx is None:
-            dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
+            dx = torch.empty((N, C, H, W), dtype=dyc.dtype, device=dyc.device, memory_format=torch.channels_last)
         ntiles = -(-(N * H * W) // 128)  # one partial row per 128-pixel dgrad tile
         part = torch.empty(ntiles * 2 * C, dtype=torch.float32, device=dyc.device)
-        _lib.check(_lib.kernels().rk_conv_dgrad_bn(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), int(acc), N, H, W, C,
+        _lib.check(_lib.kernels().rk_conv_dgrad_bn(_dt(dyc), dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), int(acc), N, H, W, C,
                                                    Co, R, S, pad, z.data_ptr(), _lib.ptr(mask), stats[0].data_ptr(),
                                                    stats[1].data_ptr(), part.data_ptr(), _lib.stream_ptr(dyc.device)),
                    "rk_conv_dgrad_bn")
@@ -140,8 +151,8 @@ def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | No
     if (stride == 1 or (stride == 2 and SDGRAD == "native" and _sdgrad_ok(R, S, pad))) and Co % 64 == 0:
         acc = dx is not None
         if dx is None:
-            dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
-        _lib.check(_kernels().rk_conv_dgrad(dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), 1, int(acc), N, H, W,
+            dx = torch.empty((N, C, H, W), dtype=dyc.dtype, device=dyc.device, memory_format=torch.channels_last)
+        _lib.check(_kernels().rk_conv_dgrad(_dt(dyc), dyc.data_ptr(), w16.data_ptr(), dx.data_ptr(), _dt(dx), int(acc), N, H, W,
                                                 C, Co, R, S, stride, pad, OH, OW, _lib.stream_ptr(dyc.device)),
                    "rk_conv_dgrad")
         return dx
@@ -159,7 +170,7 @@ def _conv_wgrad(dyc: torch.Tensor, xc: torch.Tensor, weight: torch.Tensor, geo):
     P, ncol = N * OH * OW, R * S * C
     split = _wgrad_split(Co, ncol, P)
     slab = _slab(dyc.device, split * Co * ncol) if split > 1 else None
-    _lib.check(_lib.kernels().rk_conv_wgrad(dyc.data_ptr(), xc.data_ptr(), target.data_ptr(), int(direct), None, N, H,
+    _lib.check(_lib.kernels().rk_conv_wgrad(_dt(xc), dyc.data_ptr(), xc.data_ptr(), target.data_ptr(), int(direct), None, N, H,
                                             W, C, Co, R, S, stride, pad, OH, OW, split, _lib.ptr(slab),
                                             _lib.stream_ptr(dyc.device)), "rk_conv_wgrad")
     if direct:
@@ -171,7 +182,7 @@ def _conv_wgrad(dyc: torch.Tensor, xc: torch.Tensor, weight: torch.Tensor, geo):
 class _IConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, w16, stride: int, pad: int, bnpart, bn=None):
-        xc = _cl(x)
+        xc = _cl(x, w16.dtype)
         y = _conv_fwd(xc, w16, stride, pad, bnpart)
         ctx.save_for_backward(xc, w16)
         ctx.weight = weight
@@ -182,7 +193,7 @@ class _IConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         xc, w16 = ctx.saved_tensors
-        dyc = _cl(dy)
+        dyc = _cl(dy, xc.dtype)
         dx = _conv_dgrad(dyc, w16, ctx.geo, None, ctx.bn) if ctx.needs_input_grad[0] else None
         dw = _conv_wgrad(dyc, xc, ctx.weight, ctx.geo) if ctx.needs_input_grad[1] else None
         ctx.bn = None
@@ -200,7 +211,7 @@ class _EntryFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wa, wa16, sa, pa, parta, wb, wb16, sb, pb, partb, bn=None):
         ctx.bn = bn  # conv_a's dgrad is the last write of dx: it finishes x's BatchNorm reduction
-        xc = _cl(x)
+        xc = _cl(x, wa16.dtype)
         ya = _conv_fwd(xc, wa16, sa, pa, parta)
         yb = _conv_fwd(xc, wb16, sb, pb, partb) if wb is not None else xc.view_as(xc)
         ctx.save_for_backward(xc, wa16, wb16 if wb is not None else None)
@@ -215,8 +226,8 @@ class _EntryFn(torch.autograd.Function):
         geo_a, geo_b = ctx.geo
         need = ctx.needs_input_grad
         dx = None
-        gac = _cl(ga) if ga is not None else None
-        gbc = _cl(gb) if gb is not None else None
+        gac = _cl(ga, xc.dtype) if ga is not None else None
+        gbc = _cl(gb, xc.dtype) if gb is not None else None
         if need[0]:
             if gbc is not None:
                 # shortcut first: downsample dgrad into a fresh dx / the identity's gradient as dx
@@ -231,12 +242,12 @@ class _EntryFn(torch.autograd.Function):
         return dx, dwa, None, None, None, None, dwb, None, None, None, None, None
 
 
-def _stem_weight(weight: torch.Tensor) -> torch.Tensor:
-    """[Cout][Cin][R][S] fp32 -> bf16 [Cout][Kp], taps' 8 (zero-padded) channels in (r, s, c)
+def _stem_weight(weight: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """[Cout][Cin][R][S] fp32 -> bf16 / fp16 [Cout][Kp], taps' 8 (zero-padded) channels in (r, s, c)
     order, K padded to whole 64-deep k-tiles."""
     co, ci, R, S = weight.shape
     kp = -(-(R * S * 8) // 64) * 64
-    w8 = torch.zeros(co, kp, dtype=torch.bfloat16, device=weight.device)
+    w8 = torch.zeros(co, kp, dtype=dtype, device=weight.device)
     with torch.no_grad():
         w8[:, : R * S * 8].view(co, R, S, 8)[..., :ci].copy_(weight.detach().permute(0, 2, 3, 1))
     return w8
@@ -253,16 +264,17 @@ class _StemFn(torch.autograd.Function):
         dev = x.device
         s = _lib.stream_ptr(dev)
         lib = _kernels()
-        xc = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+        cdt = torch.get_autocast_dtype("cuda")
+        xc = x if x.dtype == cdt else x.to(cdt)
         sn, sc, sh, sw = xc.stride()
         if not (sh == W * sw and (sw == 1 or sw == C)):  # pixels must be evenly strided (NCHW or NHWC)
             xc = xc.contiguous(memory_format=torch.channels_last)
             sn, sc, sh, sw = xc.stride()
-        x8 = torch.empty((N, H, W, 8), dtype=torch.bfloat16, device=dev)
+        x8 = torch.empty((N, H, W, 8), dtype=cdt, device=dev)
         _lib.check(lib.rk_pad_c8(xc.data_ptr(), x8.data_ptr(), N, C, H, W, sn, sc, sw, s), "rk_pad_c8")
-        w8 = _stem_weight(weight)
-        y = torch.empty((N, co, OH, OW), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
-        _lib.check(lib.rk_conv_fwd_c8(x8.data_ptr(), w8.data_ptr(), y.data_ptr(), N, H, W, co, R, S, stride, pad, OH,
+        w8 = _stem_weight(weight, cdt)
+        y = torch.empty((N, co, OH, OW), dtype=cdt, device=dev, memory_format=torch.channels_last)
+        _lib.check(lib.rk_conv_fwd_c8(_dt(x8), x8.data_ptr(), w8.data_ptr(), y.data_ptr(), N, H, W, co, R, S, stride, pad, OH,
                                       OW, _lib.ptr(bnpart), s), "rk_conv_fwd_c8")
         ctx.save_for_backward(x8)
         ctx.weight = weight
@@ -276,13 +288,13 @@ class _StemFn(torch.autograd.Function):
         N, C8, H, W, co, R, S, stride, pad, OH, OW = ctx.geo
         if not ctx.needs_input_grad[1]:
             return None, None, None, None, None
-        dyc = _cl(dy)
+        dyc = _cl(dy, x8.dtype)
         dev = dy.device
         P, ncol = N * OH * OW, R * S * C8
         t8 = torch.empty(co, ncol, dtype=torch.float32, device=dev)
         split = _wgrad_split(co, ncol, P)
         slab = _slab(dev, split * co * ncol) if split > 1 else None
-        _lib.check(_lib.kernels().rk_conv_wgrad(dyc.data_ptr(), x8.data_ptr(), t8.data_ptr(), 0, None, N, H, W, C8, co,
+        _lib.check(_lib.kernels().rk_conv_wgrad(_dt(x8), dyc.data_ptr(), x8.data_ptr(), t8.data_ptr(), 0, None, N, H, W, C8, co,
                                                 R, S, stride, pad, OH, OW, split, _lib.ptr(slab),
                                                 _lib.stream_ptr(dev)), "rk_conv_wgrad(stem)")
         g = t8.view(co, R, S, C8)[..., : weight.shape[1]].permute(0, 3, 1, 2)  # [Cout][Cin][R][S] view
@@ -294,7 +306,7 @@ class _StemFn(torch.autograd.Function):
 
 
 def stem_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
-    return (MODE == "native" and x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") == torch.bfloat16
+    return (MODE == "native" and x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") in _LOWP
             and conv.groups == 1 and conv.dilation == (1, 1) and conv.bias is None and conv.in_channels <= 8
             and conv.out_channels % 8 == 0 and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
             and isinstance(conv.padding[0], int) and conv.weight.dtype == torch.float32 and x.dim() == 4
@@ -302,7 +314,7 @@ def stem_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 
 
 def native_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
-    return (MODE == "native" and x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") == torch.bfloat16
+    return (MODE == "native" and x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") in _LOWP
             and conv.groups == 1 and conv.dilation == (1, 1) and conv.bias is None
             and conv.in_channels % 64 == 0 and conv.out_channels % 8 == 0 and conv.stride[0] == conv.stride[1]
             and conv.padding[0] == conv.padding[1] and isinstance(conv.padding[0], int)
@@ -320,11 +332,11 @@ class IConv2d(nn.Conv2d):
     emit_bn_stats = False
 
     def _prep(self, x):
-        """(bf16 weight copy, BN partials buffer or None) for a native forward."""
+        """(16-bit weight copy in the autocast dtype, BN partials buffer or None) for a native forward."""
         if not self.weight.is_contiguous(memory_format=torch.channels_last):
             with torch.no_grad():
                 self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
-        w16 = _bf16_copy(self, "_w16", self.weight)
+        w16 = _lowp_copy(self, "_w16", self.weight, torch.get_autocast_dtype("cuda"))
         part = None
         if self.emit_bn_stats:
             N, _, H, W = x.shape

@@ -310,6 +310,22 @@ def _bf16_copy(module, name: str, p: torch.Tensor):
     return buf
 
 
+def _lowp_copy(module, name: str, p: torch.Tensor, dtype: torch.dtype):
+    """16-bit copy of parameter ``p`` in the autocast compute dtype: the optimizer-maintained bf16
+    shadow (:func:`_bf16_copy`), or for fp16 a per-forward cast into a persistent buffer (the fused
+    optimizers' shadows are bf16 only)."""
+    if dtype == torch.bfloat16:
+        return _bf16_copy(module, name, p)
+    key = name + "_f16"
+    buf = getattr(module, key, None)
+    if buf is None or buf.shape != p.shape or buf.device != p.device or buf.stride() != p.stride():
+        buf = torch.empty_like(p, dtype=dtype)
+        setattr(module, key, buf)
+    with torch.no_grad():
+        buf.copy_(p)
+    return buf
+
+
 class LibLinear(torch.nn.Linear):
     """``nn.Linear`` (same parameters / state_dict) for the large projections that stay on the
     library GEMM: under bf16 autocast on a HIP device the bias gradient is one column-sum launch

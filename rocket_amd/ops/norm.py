@@ -206,7 +206,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
     def _fused_ok(self, x, residual) -> bool:
         return (
             _ops.fused_enabled() and x.is_cuda and self.training and x.dim() in (2, 4) and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
-            and x.dtype in (torch.float32, torch.bfloat16) and self.momentum is not None
+            and x.dtype in (torch.float32, torch.bfloat16, torch.float16) and self.momentum is not None
             and (residual is None or residual.shape == x.shape)
             and (not self.maxpool or (residual is None and x.dim() == 4 and 256 % (x.shape[1] // 8) == 0))
         )
@@ -219,7 +219,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
             if partials is not None and not (x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
                                              and partials[0].numel() == 2 * partials[1] * x.shape[1]):
                 partials = None
-            box = BwdLink() if (BWD_FUSE and not self.maxpool and x.dim() == 4 and x.dtype == torch.bfloat16) else None
+            box = (BwdLink() if (BWD_FUSE and not self.maxpool and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16))
+                   else None)
             y = _BNAct.apply(x, self.weight, self.bias, residual,
                              self.running_mean if self.track_running_stats else None,
                              self.running_var if self.track_running_stats else None,

@@ -106,7 +106,7 @@ def test_conv_dgrad_accumulate(k, stride):
     dy = torch.randn(N, Co, OH, OH, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     base = torch.randn(N, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     dx = base.clone()
-    _lib.check(_lib.kernels().rk_conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 1, 1, N, H, W, C, Co, k, k,
+    _lib.check(_lib.kernels().rk_conv_dgrad(1, dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 1, 1, N, H, W, C, Co, k, k,
                                             stride, pad, OH, OH, _lib.stream_ptr(dy.device)), "rk_conv_dgrad")
     want = base.float() + torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), stride=stride, padding=pad)
     assert _rel(dx, want) < 1e-2
