@@ -192,9 +192,28 @@ def main() -> int:
         destroy_process_group_after_launch=False,
         cpu=args.cpu,
     )
+    step_trace = None
+    if os.environ.get("ROCKET_LENET_TRACE") and args.model == "lenet" and on_gpu and fused:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
+        from lenet_timeline import StepTrace
+
+        step_trace = StepTrace(args.batch)  # installed before capture: every replay stamps
+    prof_path = os.environ.get("ROCKET_BENCH_PROFILE")  # host-side cProfile of the run (diagnostics)
+    prof = None
+    if prof_path:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     launcher.launch()
     wall = time.perf_counter() - t0
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(f"{prof_path}.{ctx.rank}")
+    if step_trace is not None:
+        with open(os.environ["ROCKET_LENET_TRACE"], "w") as fh:
+            json.dump(step_trace.report(), fh)
 
     elapsed = timer.elapsed
     summ = timer.summary()
@@ -230,7 +249,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
-            "dtype": "bf16" if (args.mp == "bf16" and on_gpu) else "fp32",
+            "dtype": args.mp if (args.mp in ("bf16", "fp16") and on_gpu) else "fp32",
             "data": f"synthetic (random {'x'.join(map(str, in_shape))} images / {classes}-class labels resident in "
             f"{'HBM' if on_gpu else 'host memory'}, "
             "random-init weights)",

@@ -99,5 +99,43 @@ def main():
                       "dgrad_done": [round(sum(w["dgrad_done_us"][i] for w in waves) / n, 2) for i in range(16)]}))
 
 
+class StepTrace:
+    """Phase stamps of the CAPTURED bench step (``ROCKET_LENET_TRACE=<file>`` in bench.py): the
+    stamp buffers are installed before the step is captured, so every replay of the graph writes
+    them and the last step's stamps remain.  All stamps share one clock (s_memrealtime, 100 MHz),
+    so the launches' spans and the gaps between them come out on one time axis."""
+
+    def __init__(self, batch: int):
+        from rocket_amd.ops import _lib
+
+        self.lib = _lib.kernels()
+        dev = torch.device("cuda", 0)
+        blocks = batch // 4
+        self.ftr = torch.zeros(blocks, 48, dtype=torch.int64, device=dev)
+        self.btr = torch.zeros(blocks, 48, dtype=torch.int64, device=dev)
+        self.wtr = torch.zeros(512, 4, dtype=torch.int64, device=dev)
+        self.lib.rk_lenet_set_trace(self.ftr.data_ptr(), self.btr.data_ptr())
+        self.lib.rk_mlp3_set_trace(self.wtr.data_ptr())
+
+    def report(self) -> dict:
+        torch.cuda.synchronize()
+        self.lib.rk_lenet_set_trace(None, None)
+        self.lib.rk_mlp3_set_trace(None)
+        f, b = self.ftr.cpu().double(), self.btr.cpu().double()
+        w = self.wtr.cpu().double()
+        w = w[w[:, 0] > 0]
+        t0 = f[:, 0].min()
+        us = lambda v: round(float(v - t0) * 0.01, 2)  # noqa: E731
+        spans = {
+            "fwd": {"first_start": us(f[:, 0].min()), "median_end": us(f[:, 8].median()), "last_end": us(f[:, 8].max())},
+            "bwd": {"first_start": us(b[:, 0].min()), "median_end": us(b[:, 12].median()), "last_end": us(b[:, 12].max())},
+            "wgrad": {"first_start": us(w[:, 0].min()), "median_loads_done": us(w[:, 1][w[:, 1] > 0].median()),
+                      "median_end": us(w[:, 2].median()), "last_end": us(w[:, 2].max()), "blocks": int(w.shape[0])},
+        }
+        return {"kernel": "captured LeNet step (us from the forward's first block start)", "spans": spans,
+                "fwd_phases": summarize(self.ftr.cpu(), FWD, list(range(9))),
+                "bwd_phases": summarize(self.btr.cpu(), BWD, BWD_MARKS)}
+
+
 if __name__ == "__main__":
     main()

@@ -207,7 +207,7 @@ struct GatherCols {
 // per channel of its columns, the sum and sum of squares of its TM-row slice of the tile — one
 // register pass and a 16-lane xor-shuffle reduction, no LDS, no barrier.  The following BatchNorm
 // merges these (rk_bn_finalize, pivoted on slice 0's mean) instead of re-reading the activation.
-template <int BM, int BN, int WM, int WN, int FM, int FN>
+template <int BM, int BN, int WM, int WN, int FM, int FN, bool H>
 __device__ __forceinline__ void tile_bn_stats(const MArgs& g, const ConvGeom& cg, f32x4 (&acc)[FM][FN], int tm,
                                               int row0, int col0, int wm, int wn, int lane) {
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -224,7 +224,7 @@ __device__ __forceinline__ void tile_bn_stats(const MArgs& g, const ConvGeom& cg
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float v = ok ? round16(acc[i][j][e], g.c_dt) : 0.f;
+        const float v = ok ? round16t<H>(acc[i][j][e]) : 0.f;
         s1[j][e] += v;
         s2[j][e] = __builtin_fmaf(v, v, s2[j][e]);
       }
@@ -263,7 +263,7 @@ __device__ __forceinline__ void tile_bn_stats(const MArgs& g, const ConvGeom& cg
 // reads the BN input / mask byte of its chunks row-contiguously like the store, and the per-thread
 // sums are combined (xor-shuffles over the lanes sharing the chunk, then LDS over the waves) into one
 // [2][BN] partial row per 128-row tile.
-template <int BM, int BN, int WM, int WN, int FM, int FN, bool BNB, typename RowMap>
+template <int BM, int BN, int WM, int WN, int FM, int FN, bool BNB, bool H, typename RowMap>
 __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& cg, f32x4 (&acc)[FM][FN], char* smem,
                                                int row0, int col0, int tm, int wm, int wn, int lane,
                                                const RowMap& rowmap) {
@@ -312,20 +312,20 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
         const uint32_t po[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          v[2 * w] += lo16(po[w], g.c_dt);
-          v[2 * w + 1] += hi16(po[w], g.c_dt);
+          v[2 * w] += lo16t<H>(po[w]);
+          v[2 * w + 1] += hi16t<H>(po[w]);
         }
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = ((mb >> e) & 1u) ? v[e] : 0.f;
-      const uint32_t pk[4] = {pack16(v[0], v[1], g.c_dt), pack16(v[2], v[3], g.c_dt), pack16(v[4], v[5], g.c_dt),
-                              pack16(v[6], v[7], g.c_dt)};
+      const uint32_t pk[4] = {pack16t<H>(v[0], v[1]), pack16t<H>(v[2], v[3]), pack16t<H>(v[4], v[5]),
+                              pack16t<H>(v[6], v[7])};
       if constexpr (BNB) {
         const uint32_t px[4] = {xz.x, xz.y, xz.z, xz.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float x = (e & 1) ? hi16(px[e >> 1], g.c_dt) : lo16(px[e >> 1], g.c_dt);
-          const float rr = (e & 1) ? hi16(pk[e >> 1], g.c_dt) : lo16(pk[e >> 1], g.c_dt);
+          const float x = (e & 1) ? hi16t<H>(px[e >> 1]) : lo16t<H>(px[e >> 1]);
+          const float rr = (e & 1) ? hi16t<H>(pk[e >> 1]) : lo16t<H>(pk[e >> 1]);
           s1[e] += rr;
           s2[e] = __builtin_fmaf(rr, (x - mu[e]) * is[e], s2[e]);
         }
@@ -530,12 +530,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
     }
   }
   if constexpr (FWD) {
-    if (cg.bnpart != nullptr) tile_bn_stats<BM, BN, WM, WN, FM, FN>(g, cg, acc, tm, row0, col0, wm, wn, lane);
+    if (cg.bnpart != nullptr) tile_bn_stats<BM, BN, WM, WN, FM, FN, H>(g, cg, acc, tm, row0, col0, wm, wn, lane);
   }
   const uint2 nos[FM][FN] = {};
   if constexpr (MODE == kConvDgradS) {
     if (g.lds_epi)
-      store_tile_lds<BM, BN, WM, WN, FM, FN, false>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, crow);
+      store_tile_lds<BM, BN, WM, WN, FM, FN, false, H>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, crow);
     else
       store_tile<FM, FN, false, ClsRow>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split, crow);
     if (cg0.zero_nb && !g.accumulate) {  // classes without taps: zeros next to this tile's pixels
@@ -559,9 +559,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
       }
     }
   } else if (MODE == kConvDgrad && cg.bnb_x != nullptr) {
-    store_tile_lds<BM, BN, WM, WN, FM, FN, true>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, IdRow());
+    store_tile_lds<BM, BN, WM, WN, FM, FN, true, H>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, IdRow());
   } else if (MODE != kConvWgrad && g.lds_epi) {
-    store_tile_lds<BM, BN, WM, WN, FM, FN, false>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, IdRow());
+    store_tile_lds<BM, BN, WM, WN, FM, FN, false, H>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, IdRow());
   } else
     store_tile<FM, FN, false>(g, acc, nos, row0 + wm * TM, col0 + wn * TN, lane, split);
 }

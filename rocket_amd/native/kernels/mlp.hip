@@ -261,6 +261,7 @@ struct LossFin {
   int sync;
 };
 struct WgradArgs {
+  uint64_t* trace;  // optional phase stamps [blocks][4] (s_memrealtime): start, loads done, end
   WgradProb p[3];
   int nprob, M, tiles, nslab;
   SlabArgs sl;
@@ -351,6 +352,7 @@ __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, flo
   red[rg][cl] = acc;
   sf();
   __syncthreads();
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
   if (dst) {
     float t = 0.f;
 #pragma unroll
@@ -374,6 +376,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
                            const StepFill& sf);
 
 __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
   __shared__ float red[NW][32 * 32];
   __shared__ float rsum[NW][32];
   __shared__ rk_opt::AdamStep s_ks[kEpiGroups];
@@ -390,6 +393,7 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
     wgrad_tile(a, red, rsum, ks, sf);
   }
   if (a.epi.on) rk_opt::advance_step(a.epi.step, a.epi.counter, false, cur);
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
 }
 
 __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks,
@@ -466,6 +470,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
   }
   sf();
   __syncthreads();
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
   for (int q = 0; q < 32 * 32 / NT; ++q) {
     const int e = threadIdx.x + q * NT, r = e >> 5, c = e & 31;
@@ -488,6 +493,11 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
 }
 
 }  // namespace
+
+// Diagnostics: per-block phase stamps of the grouped weight-gradient launch ([blocks][4] u64, or
+// null = off): start, operands reduced (after the block's LDS barrier), end.
+static uint64_t* g_wgrad_trace = nullptr;
+RK_API void rk_mlp3_set_trace(void* tr) { g_wgrad_trace = (uint64_t*)tr; }
 
 // K0, N1, N2 must be multiples of 4 (16-byte weight rows); widths <= 512.
 RK_API int rk_mlp3_fwd(const void* x, int K0, const float* w1, const float* b1, int N1, const float* w2,
@@ -539,6 +549,7 @@ RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* cons
                               const WgradEpi* epi, hipStream_t s) {
   if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
   WgradArgs a{};
+  a.trace = g_wgrad_trace;
   a.nprob = nprob;
   a.M = M;
   int tiles = 0;

@@ -49,6 +49,11 @@ __device__ __forceinline__ float hi16(uint32_t w, int dt) {
   return dt == F16 ? h2f((uint16_t)(w >> 16)) : __uint_as_float(w & 0xffff0000u);
 }
 __device__ __forceinline__ float round16(float v, int dt) { return dt == F16 ? h2f(f2h(v)) : bf2f(f2bf(v)); }
+// the same with the format fixed at compile time (H: fp16, else bf16) for kernels templated on it
+template <bool H> __device__ __forceinline__ uint32_t pack16t(float a, float b) { return pack16(a, b, H ? F16 : BF16); }
+template <bool H> __device__ __forceinline__ float lo16t(uint32_t w) { return lo16(w, H ? F16 : BF16); }
+template <bool H> __device__ __forceinline__ float hi16t(uint32_t w) { return hi16(w, H ? F16 : BF16); }
+template <bool H> __device__ __forceinline__ float round16t(float v) { return round16(v, H ? F16 : BF16); }
 
 template <typename T> struct Ld;
 template <> struct Ld<float> {
