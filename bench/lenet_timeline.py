@@ -132,6 +132,16 @@ class StepTrace:
             "wgrad": {"first_start": us(w[:, 0].min()), "median_loads_done": us(w[:, 1][w[:, 1] > 0].median()),
                       "median_end": us(w[:, 2].median()), "last_end": us(w[:, 2].max()), "blocks": int(w.shape[0])},
         }
+        wall = self.wtr.cpu().double()
+        groups = {"fc3 tiles": (0, 3), "fc2 tiles": (3, 15), "fc1 tiles": (15, 67), "slab cols": (67, 108),
+                  "loss": (108, 109)}
+        wg = {}
+        for name, (lo, hi) in groups.items():
+            g = wall[lo:hi]
+            if g.shape[0] and float(g[:, 0].min()) > 0:
+                wg[name] = {"median_start": us(g[:, 0].median()), "median_reduced": us(g[:, 1].median()),
+                            "median_end": us(g[:, 2].median()), "last_end": us(g[:, 2].max())}
+        spans["wgrad_groups"] = wg
         return {"kernel": "captured LeNet step (us from the forward's first block start)", "spans": spans,
                 "fwd_phases": summarize(self.ftr.cpu(), FWD, list(range(9))),
                 "bwd_phases": summarize(self.btr.cpu(), BWD, BWD_MARKS)}

@@ -217,12 +217,11 @@ struct ClsFwd {  // classifier operands of the fused forward
 };
 
 template <bool MLP>
-__global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__ x, const float* __restrict__ w1,
-                                                       const float* __restrict__ b1, const float* __restrict__ w2,
-                                                       const float* __restrict__ b2, uint16_t* __restrict__ a1g,
-                                                       uint8_t* __restrict__ code1, uint16_t* __restrict__ a2g,
-                                                       uint8_t* __restrict__ code2, int N, ClsFwd cf) {
-  __shared__ __attribute__((aligned(16))) FwdSmem sm;
+__device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ x, const float* __restrict__ w1,
+                                         const float* __restrict__ b1, const float* __restrict__ w2,
+                                         const float* __restrict__ b2, uint16_t* __restrict__ a1g,
+                                         uint8_t* __restrict__ code1, uint16_t* __restrict__ a2g,
+                                         uint8_t* __restrict__ code2, int N, ClsFwd cf) {
   RK_TR(cf.trace, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // conv B operands: the fused path loads the prep kernel's fragments first thing (one 16-byte
@@ -568,6 +567,16 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
   }
 }
 
+template <bool MLP>
+__global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__ x, const float* __restrict__ w1,
+                                                       const float* __restrict__ b1, const float* __restrict__ w2,
+                                                       const float* __restrict__ b2, uint16_t* __restrict__ a1g,
+                                                       uint8_t* __restrict__ code1, uint16_t* __restrict__ a2g,
+                                                       uint8_t* __restrict__ code2, int N, ClsFwd cf) {
+  __shared__ __attribute__((aligned(16))) FwdSmem sm;
+  fwd_body<MLP>(sm, x, w1, b1, w2, b2, a1g, code1, a2g, code2, N, cf);
+}
+
 // ------------------------------------------------------------------------------ backward
 // Output-owned decomposition (no LDS float atomics on shared addresses):
 //  phase A  stage 4 samples; expand the pooled conv2 gradient into a dense, zero-ringed
@@ -644,14 +653,11 @@ struct ClsBwd {
 };
 
 template <bool MLP>
-__global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__ x, const uint16_t* __restrict__ a1g,
-                                                       const uint8_t* __restrict__ code1g,
-                                                       const uint16_t* __restrict__ da2g,
-                                                       const uint8_t* __restrict__ code2g,
-                                                       const float* __restrict__ w2, float* __restrict__ dw1,
-                                                       float* __restrict__ db1, float* __restrict__ dw2,
-                                                       float* __restrict__ db2, int N, int rounds, ClsBwd cb) {
-  __shared__ __attribute__((aligned(16))) BwdSmem sm;
+__device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ x, const uint16_t* __restrict__ a1g,
+                                         const uint8_t* __restrict__ code1g, const uint16_t* __restrict__ da2g,
+                                         const uint8_t* __restrict__ code2g, const float* __restrict__ w2,
+                                         float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dw2,
+                                         float* __restrict__ db2, int N, int rounds, ClsBwd cb) {
   RK_TR(cb.trace, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int hi = lane >> 4, lo = lane & 15;
@@ -1197,6 +1203,39 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
   }
 }
 
+template <bool MLP>
+__global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__ x, const uint16_t* __restrict__ a1g,
+                                                       const uint8_t* __restrict__ code1g, const uint16_t* __restrict__ da2g,
+                                                       const uint8_t* __restrict__ code2g, const float* __restrict__ w2,
+                                                       float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dw2,
+                                                       float* __restrict__ db2, int N, int rounds, ClsBwd cb) {
+  __shared__ __attribute__((aligned(16))) BwdSmem sm;
+  bwd_body<MLP>(sm, x, a1g, code1g, da2g, code2g, w2, dw1, db1, dw2, db2, N, rounds, cb);
+}
+
+// ------------------------------------------------------------------------------ whole step
+// Forward + fused cross-entropy + backward of the block's 4 samples in ONE launch: nothing in the
+// backward of a sample depends on another block (the cross-entropy's mean count is derived from the
+// targets alone, every block counts them), so the forward -> backward kernel boundary (a dependent
+// dispatch, ~3.4 us of idle GPU per step, profiles/r3_lenet_step_timeline.json) is not needed.  The
+// two phases share the LDS (union); the backward reads the forward's global outputs (a1, codes,
+// logits, ReLU masks) back from this block's own stores, which the barrier orders (workgroup scope:
+// one CU, coherent L1).
+union TrainSmem {
+  FwdSmem f;
+  BwdSmem b;
+};
+
+__global__ void __launch_bounds__(NTHR) lenet_train_kernel(const float* __restrict__ x, const float* __restrict__ b1,
+                                                          const float* __restrict__ b2, uint16_t* __restrict__ a1g,
+                                                          uint8_t* __restrict__ code1, uint8_t* __restrict__ code2,
+                                                          int N, ClsFwd cf, ClsBwd cb) {
+  __shared__ __attribute__((aligned(16))) TrainSmem sm;
+  fwd_body<true>(sm.f, x, nullptr, b1, nullptr, b2, a1g, code1, nullptr, code2, N, cf);
+  __syncthreads();  // LDS reuse + this block's global stores visible to all its waves
+  bwd_body<true>(sm.b, x, a1g, code1, nullptr, code2, nullptr, nullptr, nullptr, nullptr, nullptr, N, 1, cb);
+}
+
 }  // namespace
 
 RK_API int rk_lenet_conv_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
@@ -1270,17 +1309,8 @@ struct LenetCE {  // host-side description of the fused cross-entropy (see ClsBw
   int defer_loss;  // 1: rk_mlp3_wgrad_loss finalises the loss (no last-block ticket in this launch)
 };
 
-// The conv weight/bias gradients are NOT accumulated here: each block writes its totals to
-// slab[block][rk_lenet_slab_width()] (N/4 rows), which rk_mlp3_wgrad then sums into dw1/db1/dw2/db2.
-RK_API int rk_lenet_slab_width() { return SLABW; }
-RK_API int rk_lenet_slab_cols() { return SLABN; }
-
-RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const void* code2, const float* w2,
-                        const void* frag, const float* dy, const void* h1T, const void* h2T, void* dyT, void* d2T,
-                        void* d1T, float* slab, int N, int rounds, const LenetCE* ce, hipStream_t s) {
-  rounds = 1;  // the fused kernel handles one group of SPB samples per block (argument kept for ABI)
-  if (N % 8 || N > 65536 || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;  // float4 image loads
-  if (!slab) return (int)hipErrorInvalidValue;
+static ClsBwd cls_bwd(const void* frag, const float* dy, const void* h1T, const void* h2T, void* dyT, void* d2T,
+                      void* d1T, float* slab, const LenetCE* ce) {
   ClsBwd cb{};
   cb.trace = g_bwd_trace;
   cb.slab = slab;
@@ -1308,8 +1338,39 @@ RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const
     cb.sync = ce->sync;
     cb.defer_loss = ce->defer_loss;
   }
+  return cb;
+}
+
+// The conv weight/bias gradients are NOT accumulated here: each block writes its totals to
+// slab[block][rk_lenet_slab_width()] (N/4 rows), which rk_mlp3_wgrad then sums into dw1/db1/dw2/db2.
+RK_API int rk_lenet_slab_width() { return SLABW; }
+RK_API int rk_lenet_slab_cols() { return SLABN; }
+
+RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const void* code2, const float* w2,
+                        const void* frag, const float* dy, const void* h1T, const void* h2T, void* dyT, void* d2T,
+                        void* d1T, float* slab, int N, int rounds, const LenetCE* ce, hipStream_t s) {
+  rounds = 1;  // the fused kernel handles one group of SPB samples per block (argument kept for ABI)
+  if (N % 8 || N > 65536 || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;  // float4 image loads
+  if (!slab) return (int)hipErrorInvalidValue;
+  const ClsBwd cb = cls_bwd(frag, dy, h1T, h2T, dyT, d2T, d1T, slab, ce);
   lenet_conv_bwd<true><<<N / (SPB * rounds), NTHR, 0, s>>>(x, (const uint16_t*)a1, (const uint8_t*)code1, nullptr,
                                                            (const uint8_t*)code2, w2, nullptr, nullptr, nullptr,
                                                            nullptr, N, rounds, cb);
   return (int)hipGetLastError();
 }
+
+// Whole fused LeNet training step of the batch but the weight gradients, in ONE launch
+// (lenet_train_kernel): the rk_lenet_fwd outputs (logits, a1, codes, transposed activations) and
+// the rk_lenet_bwd outputs (transposed gradients, conv-gradient slab, loss partials) for a
+// softmax cross-entropy on `ce` (required; its d(logits) scale is ce->grad_scale).
+RK_API int rk_lenet_train(const float* x, const float* b1, const float* b2, const void* frag, const float* fb1,
+                          const float* fb2, const float* fb3, void* a1, void* code1, void* code2, void* a2T, void* h1T,
+                          void* h2T, float* logits, void* dyT, void* d2T, void* d1T, float* slab, int N,
+                          const LenetCE* ce, hipStream_t s) {
+  if (N % 8 || N > 65536 || ((uintptr_t)x & 15) || !slab || !ce || ce->logits != logits) return (int)hipErrorInvalidValue;
+  const ClsFwd cf{(const bf16x8*)frag, fb1, fb2, fb3, (uint16_t*)a2T, (uint16_t*)h1T, (uint16_t*)h2T, logits, g_fwd_trace};
+  const ClsBwd cb = cls_bwd(frag, nullptr, h1T, h2T, dyT, d2T, d1T, slab, ce);
+  lenet_train_kernel<<<N / SPB, NTHR, 0, s>>>(x, b1, b2, (uint16_t*)a1, (uint8_t*)code1, (uint8_t*)code2, N, cf, cb);
+  return (int)hipGetLastError();
+}
+

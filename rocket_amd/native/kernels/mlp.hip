@@ -262,6 +262,7 @@ struct LossFin {
 };
 struct WgradArgs {
   uint64_t* trace;  // optional phase stamps [blocks][4] (s_memrealtime): start, loads done, end
+  float gscale;     // every produced gradient is scaled by this (the upstream gradient factor)
   WgradProb p[3];
   int nprob, M, tiles, nslab;
   SlabArgs sl;
@@ -357,6 +358,7 @@ __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, flo
     float t = 0.f;
 #pragma unroll
     for (int g = 0; g < NW; ++g) t += red[g][threadIdx.x];
+    t *= a.gscale;
     if (ks) rk_opt::epi_apply(a.rsl[di], ks[a.rsl[di].group], c - s.bound[di], ee, old + t, a.epi.zero_grads);
     else *dst = old + t;
   }
@@ -477,6 +479,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[w][e];
+    v *= a.gscale;
     if (n0 + r < P.N && k0 + c < P.K) {
       const int64_t i = (int64_t)(n0 + r) * P.K + k0 + c;
       if (ks) rk_opt::epi_apply(a.rdw[pi], ks[a.rdw[pi].group], i, ew[q], dw_old[q] + v, a.epi.zero_grads);
@@ -487,6 +490,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += rsum[w][threadIdx.x];
+    v *= a.gscale;
     if (ks) rk_opt::epi_apply(a.rdb[pi], ks[a.rdb[pi].group], n0 + threadIdx.x, eb, db_old + v, a.epi.zero_grads);
     else P.db[n0 + threadIdx.x] = db_old + v;
   }
@@ -543,13 +547,16 @@ struct WgradEpi {
 // loss (may be null): also finalise a batch loss from per-block partials (see LossFin).
 // epi (may be null): apply the Adam/AdamW update to every produced gradient element (the step's
 // optimizer launch is then skipped by the caller).  Every dW/db/slab destination needs a record.
+// gscale: factor on every produced gradient (1 unless the backward inputs were formed for a unit
+// upstream gradient, e.g. by the fused LeNet step kernel ahead of the loss scaling).
 RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* const* xT, float* const* dw,
                               float* const* db, const int* Ns, const int* Ks, int M, const float* slab, int slab_rows,
                               int slab_width, float* const* slab_dst, const int* slab_bound, const LossFin* loss,
-                              const WgradEpi* epi, hipStream_t s) {
+                              const WgradEpi* epi, float gscale, hipStream_t s) {
   if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
   WgradArgs a{};
   a.trace = g_wgrad_trace;
+  a.gscale = gscale;
   a.nprob = nprob;
   a.M = M;
   int tiles = 0;
@@ -615,5 +622,5 @@ RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT
                          const int* Ns, const int* Ks, int M, const float* slab, int slab_rows, int slab_width,
                          float* const* slab_dst, const int* slab_bound, hipStream_t s) {
   return rk_mlp3_wgrad_loss(nprob, dT, xT, dw, db, Ns, Ks, M, slab, slab_rows, slab_width, slab_dst, slab_bound,
-                            nullptr, nullptr, s);
+                            nullptr, nullptr, 1.f, s);
 }

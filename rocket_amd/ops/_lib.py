@@ -71,7 +71,8 @@ KERNEL_SIGS = {
     "rk_mlp3_wgrad": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                               c_int, c_void_p, c_void_p, c_void_p]),
     "rk_mlp3_wgrad_loss": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p]),
+    "rk_lenet_train": (c_int, [c_void_p] * 18 + [c_int, c_void_p, c_void_p]),
     "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_int, c_void_p]),
     "rk_amp_check": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
@@ -97,6 +98,8 @@ KERNEL_SIGS = {
     "rk_attn_set_bwd_fused": (c_int, [c_int]),
     "rk_attn_set_stamps": (c_int, [c_void_p]),
     "rk_spin": (c_int, [ctypes.c_double, c_int, c_void_p, c_void_p]),
+    "rk_gap_write": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p]),
+    "rk_gap_stamp": (c_int, [c_int, c_void_p, c_void_p]),
     "rk_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_float,
                             c_void_p]),
     "rk_attn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,

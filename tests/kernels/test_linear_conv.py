@@ -187,6 +187,77 @@ def test_lenet_fused_cross_entropy(N):
     y2.backward(torch.zeros_like(y2))
 
 
+@pytest.mark.parametrize("N", [1024, 4096])
+def test_lenet_speculative_step_matches(N):
+    """Speculative whole step (forward launch also runs the cross-entropy backward,
+    rk_lenet_train; the weight-gradient launch applies the loss's gradient scale) vs the
+    forward / backward launches: the same bf16 contract and an exact power-of-two scale, so
+    loss, gradients and the Loss-capsule bookkeeping agree to fp32 round-off."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.lenet import fuse_cross_entropy, lenet_forward
+
+    torch.manual_seed(6)
+    net = LeNet(fused=False).cuda()
+    ref = LeNet(fused=False).cuda()
+    ref.load_state_dict(net.state_dict())
+    x = torch.rand(N, 1, 28, 28, device="cuda")
+    t = torch.randint(0, 10, (N,), device="cuda")
+    t[::5] = -100
+    outs = []
+    for m, target in ((net, t), (ref, None)):
+        acc = torch.full((1,), 0.25, device="cuda")
+        ring = torch.zeros(4, device="cuda")
+        slot = torch.zeros(1, dtype=torch.int64, device="cuda")
+        y = lenet_forward(x, m.conv1, m.conv2, m.fc1, m.fc2, m.fc3, target)
+        assert (getattr(y.grad_fn, "spec", None) is not None) == (target is not None)
+        loss, dummy = fuse_cross_entropy(y, t, 0.5, (acc, ring, slot, 2.0, 1))
+        torch.autograd.backward([y], [dummy])
+        torch.cuda.synchronize()
+        outs.append((y.detach().clone(), float(loss), float(ring[0]), int(slot)))
+    (y1, l1, r1, s1), (y2, l2, r2, s2) = outs
+    assert torch.equal(y1, y2)
+    assert abs(l1 - l2) <= 1e-6 * abs(l2) and abs(r1 - r2) <= 1e-6 * abs(r2) and s1 == s2 == 1
+    for (name, p), pr in zip(net.named_parameters(), ref.parameters()):
+        assert _rel(p.grad, pr.grad) < 1e-5, (name, _rel(p.grad, pr.grad))
+
+
+def test_lenet_speculation_dropped_for_other_losses():
+    """A forward that speculated but whose backward gets an ordinary d(logits) runs the regular
+    backward (same gradients as without speculation); two such misses pause speculation, a fused
+    cross-entropy resumes it."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.lenet import lenet_forward
+
+    torch.manual_seed(7)
+    net = LeNet(fused=False).cuda()
+    ref = LeNet(fused=False).cuda()
+    ref.load_state_dict(net.state_dict())
+    x = torch.rand(512, 1, 28, 28, device="cuda")
+    t = torch.randint(0, 10, (512,), device="cuda")
+    g = torch.randn(512, 10, device="cuda")
+    for _ in range(2):
+        y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3, t)
+        assert y.grad_fn.spec is not None
+        y.backward(g)
+    yr = lenet_forward(x, ref.conv1, ref.conv2, ref.fc1, ref.fc2, ref.fc3)
+    yr.backward(g)
+    yr = lenet_forward(x, ref.conv1, ref.conv2, ref.fc1, ref.fc2, ref.fc3)
+    yr.backward(g)
+    for (name, p), pr in zip(net.named_parameters(), ref.parameters()):
+        assert torch.equal(p.grad, pr.grad), name
+    frags = net.conv1._rocket_fragments
+    assert not frags.spec_ok
+    y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3, t)
+    assert y.grad_fn.spec is None
+    from rocket_amd.ops.lenet import fuse_cross_entropy
+
+    _, dummy = fuse_cross_entropy(y, t, 1.0)
+    torch.autograd.backward([y], [dummy])
+    assert frags.spec_ok
+    y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3, t)
+    assert y.grad_fn.spec is not None
+
+
 @pytest.mark.parametrize("N", [1024, 256])
 def test_lenet_fused_backward_deterministic(N):
     """The fused backward has no float atomics (per-block gradient slab rows, reduced in a fixed
