@@ -113,14 +113,17 @@ class StepTrace:
         blocks = batch // 4
         self.ftr = torch.zeros(blocks, 48, dtype=torch.int64, device=dev)
         self.btr = torch.zeros(blocks, 48, dtype=torch.int64, device=dev)
-        self.wtr = torch.zeros(512, 4, dtype=torch.int64, device=dev)
+        self.wtr = torch.zeros(512, 8, dtype=torch.int64, device=dev)
         self.lib.rk_lenet_set_trace(self.ftr.data_ptr(), self.btr.data_ptr())
         self.lib.rk_mlp3_set_trace(self.wtr.data_ptr())
+        self.gtr = torch.zeros(4096, 2, dtype=torch.int64, device=dev)
+        self.lib.rk_gather_set_trace(self.gtr.data_ptr())
 
     def report(self) -> dict:
         torch.cuda.synchronize()
         self.lib.rk_lenet_set_trace(None, None)
         self.lib.rk_mlp3_set_trace(None)
+        self.lib.rk_gather_set_trace(None)
         f, b = self.ftr.cpu().double(), self.btr.cpu().double()
         w = self.wtr.cpu().double()
         w = w[w[:, 0] > 0]
@@ -141,7 +144,15 @@ class StepTrace:
             if g.shape[0] and float(g[:, 0].min()) > 0:
                 wg[name] = {"median_start": us(g[:, 0].median()), "median_reduced": us(g[:, 1].median()),
                             "median_end": us(g[:, 2].median()), "last_end": us(g[:, 2].max())}
+                if float(g[:, 3].min()) > 0:
+                    wg[name]["median_old_loaded"] = us(g[:, 3].median())
+                    wg[name]["median_loop_done"] = us(g[:, 4].median())
         spans["wgrad_groups"] = wg
+        g = self.gtr.cpu().double()
+        g = g[g[:, 0] > 0]
+        if g.shape[0]:  # the NEXT batch's gather (issued one ahead, before this step's launches)
+            spans["next_batch_gather"] = {"first_start": us(g[:, 0].min()), "last_end": us(g[:, 1].max()),
+                                          "blocks": int(g.shape[0])}
         return {"kernel": "captured LeNet step (us from the forward's first block start)", "spans": spans,
                 "fwd_phases": summarize(self.ftr.cpu(), FWD, list(range(9))),
                 "bwd_phases": summarize(self.btr.cpu(), BWD, BWD_MARKS)}

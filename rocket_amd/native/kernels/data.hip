@@ -10,6 +10,8 @@
 //                   and graph-capturable (the ring slot lives in device memory).
 #include "rk_common.h"
 
+#include <hip/hip_ext.h>
+
 namespace {
 
 constexpr int kMaxGather = 4;
@@ -20,6 +22,7 @@ struct GatherArgs {
   int64_t row_bytes[kMaxGather];
   int64_t src_rows[kMaxGather];
   int ntensors;
+  uint64_t* trace;  // diagnostics: [blocks][2] start / end stamps (s_memrealtime), or null
 };
 
 // grid: x = row blocks (kRowsPerBlock rows each), y = tensor.  One wave copies one row; each lane
@@ -49,6 +52,8 @@ __global__ void __launch_bounds__(kThreads) gather_rows_kernel(GatherArgs a, con
   const int t = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  uint64_t* tr = a.trace ? a.trace + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 : nullptr;
+  if (tr && threadIdx.x == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
   if (r >= nrows) return;
   int64_t s = idx[r];
   s = s < 0 ? s + a.src_rows[t] : s;
@@ -63,6 +68,7 @@ __global__ void __launch_bounds__(kThreads) gather_rows_kernel(GatherArgs a, con
   } else {
     copy_row(src, dst, (int)rb, lane);
   }
+  if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
 }
 
 __global__ void loss_accum_kernel(const float* __restrict__ loss, float* acc, float* ring, int64_t* slot,
@@ -79,6 +85,11 @@ __global__ void loss_accum_kernel(const float* __restrict__ loss, float* acc, fl
 
 }  // namespace
 
+thread_local int g_gather_any_order = 0;
+static uint64_t* g_gather_trace = nullptr;
+// diagnostics: block start / end stamps of every following gather launch ([blocks][2] u64), or null
+RK_API void rk_gather_set_trace(void* tr) { g_gather_trace = (uint64_t*)tr; }
+
 // srcs/dsts: arrays of device pointers (host memory), row_bytes/src_rows per tensor.
 RK_API int rk_gather_rows(int ntensors, const void* const* srcs, void* const* dsts, const int64_t* row_bytes,
                           const int64_t* src_rows, const int64_t* idx, int64_t nrows, hipStream_t s) {
@@ -93,10 +104,27 @@ RK_API int rk_gather_rows(int ntensors, const void* const* srcs, void* const* ds
     if (row_bytes[i] > ((int64_t)1 << 34) || src_rows[i] <= 0) return (int)hipErrorInvalidValue;
   }
   a.ntensors = ntensors;
+  a.trace = g_gather_trace;
   dim3 grid((unsigned)((nrows + kRowsPerBlock - 1) / kRowsPerBlock), (unsigned)ntensors);
+  if (g_gather_any_order) {
+    // AQL barrier bit clear: the gather may start while the previous packet on the stream (the
+    // last kernel of the step before) still runs; see rk_gather_rows_any_order
+    g_gather_any_order = 0;
+    void* args[] = {&a, &idx, &nrows};
+    return (int)hipExtLaunchKernel((const void*)gather_rows_kernel, grid, dim3(kThreads), args, 0, s, nullptr, nullptr,
+                                   hipExtAnyOrderLaunch);
+  }
   gather_rows_kernel<<<grid, kThreads, 0, s>>>(a, idx, nrows);
   return (int)hipGetLastError();
 }
+
+// The NEXT rk_gather_rows on this thread is launched with hipExtAnyOrderLaunch: it does not wait
+// for the previous packet on its stream to complete (every packet before that one has completed:
+// that packet's own barrier bit waited for them).  Only for a gather whose destination and index
+// table no in-flight packet touches — a device loader's ring slot, gathered one batch ahead
+// (runtime/data.py DeviceLoader): it then overlaps the previous step's tail kernel instead of
+// adding its own dispatch to the step's dependency chain.
+RK_API void rk_gather_rows_any_order() { g_gather_any_order = 1; }
 
 RK_API int rk_loss_accum(const float* loss, float* acc, float* ring, int64_t* slot, int ring_size, float scale,
                          int sync, hipStream_t s) {

@@ -5,6 +5,8 @@
 // footprint, used to tell whether two graph branches / streams actually run concurrently.
 #include "rk_common.h"
 
+#include <hip/hip_ext.h>
+
 using rk::f32x4;
 
 namespace {
@@ -45,6 +47,14 @@ __global__ void __launch_bounds__(256) gap_write_kernel(f32x4* __restrict__ buf,
 __global__ void __launch_bounds__(64) gap_stamp_kernel(uint64_t* __restrict__ trace) {
   if (threadIdx.x == 0) trace[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 }
+// the same stamp from a LeNet-step-shaped workgroup: 1024 threads and `lds` bytes of dynamic LDS
+__global__ void __launch_bounds__(1024) gap_stamp_big_kernel(uint64_t* __restrict__ trace) {
+  extern __shared__ char dyn[];
+  if (threadIdx.x == 0) {
+    trace[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    dyn[0] = 0;
+  }
+}
 }  // namespace
 
 RK_API int rk_gap_write(void* buf, int64_t bytes_per_block, int blocks, int nt, void* trace, hipStream_t s) {
@@ -53,8 +63,22 @@ RK_API int rk_gap_write(void* buf, int64_t bytes_per_block, int blocks, int nt, 
   return (int)hipGetLastError();
 }
 
-RK_API int rk_gap_stamp(int blocks, void* trace, hipStream_t s) {
-  if (blocks < 1) return (int)hipErrorInvalidValue;
-  gap_stamp_kernel<<<blocks, 64, 0, s>>>((uint64_t*)trace);
+// any_order: launched with hipExtAnyOrderLaunch (AQL barrier bit clear: may start before the
+// previous packet on the stream completes)
+RK_API int rk_gap_stamp_big(int blocks, void* trace, int lds, hipStream_t s) {
+  if (blocks < 1 || lds < 0 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (lds > 64 * 1024) hipFuncSetAttribute((const void*)gap_stamp_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  gap_stamp_big_kernel<<<blocks, 1024, lds, s>>>((uint64_t*)trace);
   return (int)hipGetLastError();
+}
+
+RK_API int rk_gap_stamp(int blocks, void* trace, int any_order, hipStream_t s) {
+  if (blocks < 1) return (int)hipErrorInvalidValue;
+  if (!any_order) {
+    gap_stamp_kernel<<<blocks, 64, 0, s>>>((uint64_t*)trace);
+    return (int)hipGetLastError();
+  }
+  void* args[] = {&trace};
+  return (int)hipExtLaunchKernel((const void*)gap_stamp_kernel, dim3(blocks), dim3(64), args, 0, s, nullptr, nullptr,
+                                 hipExtAnyOrderLaunch);
 }

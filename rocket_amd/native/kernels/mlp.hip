@@ -261,7 +261,7 @@ struct LossFin {
   int sync;
 };
 struct WgradArgs {
-  uint64_t* trace;  // optional phase stamps [blocks][4] (s_memrealtime): start, loads done, end
+  uint64_t* trace;  // optional phase stamps [blocks][8] (s_memrealtime): start, reduced, end, tile: old values in, main loop done
   float gscale;     // every produced gradient is scaled by this (the upstream gradient factor)
   WgradProb p[3];
   int nprob, M, tiles, nslab;
@@ -353,7 +353,7 @@ __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, flo
   red[rg][cl] = acc;
   sf();
   __syncthreads();
-  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
   if (dst) {
     float t = 0.f;
 #pragma unroll
@@ -378,7 +378,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
                            const StepFill& sf);
 
 __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
-  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8] = __builtin_amdgcn_s_memrealtime();
   __shared__ float red[NW][32 * 32];
   __shared__ float rsum[NW][32];
   __shared__ rk_opt::AdamStep s_ks[kEpiGroups];
@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
     wgrad_tile(a, red, rsum, ks, sf);
   }
   if (a.epi.on) rk_opt::advance_step(a.epi.step, a.epi.counter, false, cur);
-  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
 }
 
 __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks,
@@ -421,6 +421,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     dw_old[q] = in ? P.dw[(int64_t)(n0 + r) * P.K + k0 + c] : 0.f;
     if (ks && in) ew[q] = rk_opt::epi_fetch(a.rdw[pi], (int64_t)(n0 + r) * P.K + k0 + c);
   }
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime() + (uint64_t)(dw_old[0] == 12345.f);
   const bool has_db = k0 == 0 && P.db && threadIdx.x < 32 && n0 + (int)threadIdx.x < P.N;
   const float db_old = has_db ? P.db[n0 + threadIdx.x] : 0.f;
   if (ks && has_db) eb = rk_opt::epi_fetch(a.rdb[pi], n0 + threadIdx.x);
@@ -453,6 +454,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
       }
     }
   }
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memrealtime() + (uint64_t)(acc[0][0][0] == 12345.f);
   // reduce the 8 waves' partial tiles in LDS; C element (row 16i + 4hi + r, col 16j + lo)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -472,7 +474,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
   }
   sf();
   __syncthreads();
-  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
   for (int q = 0; q < 32 * 32 / NT; ++q) {
     const int e = threadIdx.x + q * NT, r = e >> 5, c = e & 31;
@@ -498,8 +500,9 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
 
 }  // namespace
 
-// Diagnostics: per-block phase stamps of the grouped weight-gradient launch ([blocks][4] u64, or
-// null = off): start, operands reduced (after the block's LDS barrier), end.
+// Diagnostics: per-block phase stamps of the grouped weight-gradient launch ([blocks][8] u64, or
+// null = off): start, operands reduced (after the block's LDS barrier), end; tiles also: old values
+// loaded, main loop done.
 static uint64_t* g_wgrad_trace = nullptr;
 RK_API void rk_mlp3_set_trace(void* tr) { g_wgrad_trace = (uint64_t*)tr; }
 

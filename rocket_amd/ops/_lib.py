@@ -99,7 +99,10 @@ KERNEL_SIGS = {
     "rk_attn_set_stamps": (c_int, [c_void_p]),
     "rk_spin": (c_int, [ctypes.c_double, c_int, c_void_p, c_void_p]),
     "rk_gap_write": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p]),
-    "rk_gap_stamp": (c_int, [c_int, c_void_p, c_void_p]),
+    "rk_gap_stamp": (c_int, [c_int, c_void_p, c_int, c_void_p]),
+    "rk_gather_rows_any_order": (None, []),
+    "rk_gather_set_trace": (None, [c_void_p]),
+    "rk_gap_stamp_big": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "rk_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_float,
                             c_void_p]),
     "rk_attn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,

@@ -57,13 +57,19 @@ class RowGather:
                           (ctypes.c_int64 * k)(*[s.shape[0] for s in srcs]))
             self._k = k
             self._fn = _lib.kernels().rk_gather_rows
+            self._any = _lib.kernels().rk_gather_rows_any_order
             self._dev = outs[0].device
 
-    def __call__(self, idx: torch.Tensor):
+    def __call__(self, idx: torch.Tensor, any_order: bool = False):
+        """``any_order``: launch without waiting for the stream's previous packet (see
+        ``rk_gather_rows_any_order``) — only when nothing in flight reads the destination or writes
+        ``idx``."""
         if not self.native:
             for s, o in zip(self.srcs, self.outs):
                 torch.index_select(s, 0, idx, out=o)
             return self.outs
+        if any_order:
+            self._any()
         code = self._fn(self._k, *self._args, idx.data_ptr(), idx.numel(), _lib.stream_ptr(self._dev))
         if code:
             _lib.check(code, "rk_gather_rows")

@@ -392,6 +392,13 @@ class DeviceLoader(_LoaderBase):
     #: 55 us step) the cross-queue event wait costs more than the overlap saves (17.3M -> 13.7M
     #: samples/s measured on 1x MI355X).
     PREFETCH = os.environ.get("ROCKET_PREFETCH", "0") == "1"
+    #: ROCKET_GATHER_ANY_ORDER=0 disables: batch gathers are launched without the AQL barrier bit, so
+    #: a gather overlaps the tail kernel of the step queued before it instead of adding a dependent
+    #: dispatch to the chain.  Safe because the loader gathers one batch ahead into a ring slot that
+    #: no in-flight step reads (the slot's last reader is RING - 1 steps back, and every packet but
+    #: the immediately preceding one has completed when the gather starts), and because the first
+    #: gather after an index-table upload keeps the barrier (it reads the uploaded table).
+    ANY_ORDER = os.environ.get("ROCKET_GATHER_ANY_ORDER", "1") != "0"
 
     def __init__(
         self,
@@ -425,6 +432,7 @@ class DeviceLoader(_LoaderBase):
         self.device = dataset.device
         self._rings: dict = {}
         self._ring_pos: dict = {}
+        self._fresh_table = True  # the next gather reads a just-uploaded index table
 
     def index_table(self) -> List[torch.Tensor]:
         batches = self.batch_sampler.local_batches()
@@ -457,7 +465,10 @@ class DeviceLoader(_LoaderBase):
         self._ring_pos[n] = (k + 1) % self.RING
         bufs, gather = ring[k]
         if not self.PREFETCH or torch.cuda.is_current_stream_capturing():
-            gather(idx)
+            any_order = (self.ANY_ORDER and not self._fresh_table and self.RING >= 3
+                         and not torch.cuda.is_current_stream_capturing())
+            self._fresh_table = False
+            gather(idx, any_order=any_order)
             return bufs
         compute = torch.cuda.current_stream(self.device)
         side = self._side_stream()
@@ -489,6 +500,7 @@ class DeviceLoader(_LoaderBase):
 
     def _batches(self):
         table = self.index_table()
+        self._fresh_table = True
         if table and self.PREFETCH and self.device.type == "cuda":
             self._side_stream()
             self._idx_ready = torch.cuda.Event()
