@@ -66,6 +66,7 @@ class Looper(Dispatcher):
     def set(self, attrs: Attributes | None = None) -> None:
         if not self._active(attrs):
             return
+        self._link_deferred_batches()
         Dispatcher.set(self, attrs=attrs)
         self._repeats = self._user_defined_repeats
         if self._repeats is None:
@@ -76,6 +77,23 @@ class Looper(Dispatcher):
             )
         if attrs.looper is None:
             attrs.looper = Attributes(repeats=self._repeats, state=Attributes(), terminate=False, tag=self._tag)
+
+    def _link_deferred_batches(self) -> None:
+        """A device-resident Dataset whose batches go straight to a Module whose model gathers its
+        own rows (``consumes_pending_rows``, e.g. the fused LeNet step) hands them over deferred:
+        the gather then happens inside the model's step kernel (runtime/data.py PendingRows) instead
+        of as a launch of its own.  Only for that adjacency in a training loop; everything else
+        gets gathered batches."""
+        from rocket_amd.core.dataset import Dataset
+        from rocket_amd.core.module import Module
+        from rocket_amd.runtime.data import DeviceLoader
+
+        caps = self._capsules
+        for i, c in enumerate(caps):
+            if isinstance(c, Dataset) and isinstance(c._dataloader, DeviceLoader):
+                nxt = caps[i + 1] if i + 1 < len(caps) else None
+                c._dataloader.defer = bool(self._grad_enabled and isinstance(nxt, Module)
+                                           and getattr(nxt, "_gathers_rows", False))
 
     def reset(self, attrs: Attributes | None = None) -> None:
         if not self._active(attrs):

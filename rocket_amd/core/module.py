@@ -32,6 +32,7 @@ import torch
 from rocket_amd.core.attributes import Attributes
 from rocket_amd.core.capsule import Capsule
 from rocket_amd.core.dispatcher import Dispatcher
+from rocket_amd.runtime.data import materialize_batch
 
 
 class Module(Dispatcher):
@@ -48,6 +49,7 @@ class Module(Dispatcher):
         self._capture = capture
         self._warmup = warmup
         self._graphs = None
+        self._gathers_rows = False  # the model gathers deferred loader batches itself (PendingRows)
 
     @property
     def module(self) -> torch.nn.Module:
@@ -65,6 +67,7 @@ class Module(Dispatcher):
         else:
             self._module = engine.prepare_model(self._module, device_placement=engine.device_placement)
         Dispatcher.setup(self, attrs)
+        self._gathers_rows = bool(getattr(engine.unwrap_model(self._module), "consumes_pending_rows", False))
         if self._capture and engine.device.type == "cuda":
             from rocket_amd.runtime.graphs import StepGraphs
 
@@ -73,6 +76,8 @@ class Module(Dispatcher):
     def launch(self, attrs: Attributes | None = None) -> None:
         if attrs is None or attrs.batch is None:
             return
+        if not self._gathers_rows:  # a deferred device-loader batch the model does not gather itself
+            materialize_batch(attrs.batch)
         train = torch.is_grad_enabled()
         if self._module.training != train:  # a recursive .train() costs ~20 us per iteration
             self._module.train(train)

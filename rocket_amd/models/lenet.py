@@ -63,10 +63,22 @@ class LeNet(nn.Module):
         x = F.relu(self.fc2(x))
         return self.fc3(x)
 
+    #: the fused training step gathers a deferred device-loader batch itself (runtime/data.py
+    #: PendingRows; the Looper defers the gather of batches this model consumes)
+    consumes_pending_rows = True
+
+    def _whole_fused(self, x: torch.Tensor) -> bool:
+        return self.use_fused(x) and x.shape[0] % 8 == 0 and self.fc3.out_features == 10
+
     def forward(self, batch):
+        from rocket_amd.runtime.data import materialize_batch
+
         if isinstance(batch, torch.Tensor):
+            materialize_batch(batch)
             return self.logits(batch)
         img, label = batch[0], batch[1]
+        if not self._whole_fused(img):  # only the whole-step fused path gathers a deferred batch
+            materialize_batch(batch)
         return (img, label, self.logits(img, label))
 
 

@@ -9,6 +9,7 @@
 //                   acc = 0.  One single-thread launch instead of five elementwise kernels,
 //                   and graph-capturable (the ring slot lives in device memory).
 #include "rk_common.h"
+#include "rows_common.h"
 
 #include <hip/hip_ext.h>
 
@@ -47,6 +48,8 @@ __device__ __forceinline__ void copy_row(const V* __restrict__ src, V* __restric
   }
 }
 
+__device__ __forceinline__ void copy_one(const GatherArgs& a, int t, int64_t s, int64_t r, int lane);
+
 __global__ void __launch_bounds__(kThreads) gather_rows_kernel(GatherArgs a, const int64_t* __restrict__ idx,
                                                                int64_t nrows) {
   const int t = blockIdx.y;
@@ -54,8 +57,18 @@ __global__ void __launch_bounds__(kThreads) gather_rows_kernel(GatherArgs a, con
   const int64_t r = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
   uint64_t* tr = a.trace ? a.trace + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 : nullptr;
   if (tr && threadIdx.x == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
-  if (r >= nrows) return;
-  int64_t s = idx[r];
+  if (r < nrows) copy_one(a, t, idx[r], r, lane);
+  if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+}
+
+// rows[i] = table[cursor' + i] for the next batch, cursor' = meta[0] + n_cur (stored back);
+// meta = {cursor, table length}.  One block.
+__global__ void __launch_bounds__(256) rows_next_kernel(const int64_t* __restrict__ table, int64_t* meta,
+                                                        int64_t* __restrict__ rows, int n_cur, int bs) {
+  rows_next_block(table, meta, rows, n_cur, bs);
+}
+
+__device__ __forceinline__ void copy_one(const GatherArgs& a, int t, int64_t s, int64_t r, int lane) {
   s = s < 0 ? s + a.src_rows[t] : s;
   s = s < 0 ? 0 : (s >= a.src_rows[t] ? a.src_rows[t] - 1 : s);
   const int64_t rb = a.row_bytes[t];
@@ -68,7 +81,6 @@ __global__ void __launch_bounds__(kThreads) gather_rows_kernel(GatherArgs a, con
   } else {
     copy_row(src, dst, (int)rb, lane);
   }
-  if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
 }
 
 __global__ void loss_accum_kernel(const float* __restrict__ loss, float* acc, float* ring, int64_t* slot,
@@ -91,8 +103,8 @@ static uint64_t* g_gather_trace = nullptr;
 RK_API void rk_gather_set_trace(void* tr) { g_gather_trace = (uint64_t*)tr; }
 
 // srcs/dsts: arrays of device pointers (host memory), row_bytes/src_rows per tensor.
-RK_API int rk_gather_rows(int ntensors, const void* const* srcs, void* const* dsts, const int64_t* row_bytes,
-                          const int64_t* src_rows, const int64_t* idx, int64_t nrows, hipStream_t s) {
+static int gather_launch(int ntensors, const void* const* srcs, void* const* dsts, const int64_t* row_bytes,
+                         const int64_t* src_rows, const int64_t* idx, int64_t nrows, hipStream_t s) {
   if (ntensors <= 0 || nrows <= 0) return 0;
   if (ntensors > kMaxGather) return (int)hipErrorInvalidValue;
   GatherArgs a{};
@@ -115,6 +127,20 @@ RK_API int rk_gather_rows(int ntensors, const void* const* srcs, void* const* ds
                                    hipExtAnyOrderLaunch);
   }
   gather_rows_kernel<<<grid, kThreads, 0, s>>>(a, idx, nrows);
+  return (int)hipGetLastError();
+}
+
+RK_API int rk_gather_rows(int ntensors, const void* const* srcs, void* const* dsts, const int64_t* row_bytes,
+                          const int64_t* src_rows, const int64_t* idx, int64_t nrows, hipStream_t s) {
+  return gather_launch(ntensors, srcs, dsts, row_bytes, src_rows, idx, nrows, s);
+}
+
+// Deferred device-loader batches (runtime/data.py PendingRows): advance the epoch cursor past the
+// current batch (n_cur rows) and stage the next batch's row indices (up to bs) into `rows`, which
+// the next batch's consumer reads.  meta = {cursor, table length} (device).  Graph-capturable.
+RK_API int rk_rows_next(const int64_t* table, int64_t* meta, int64_t* rows, int n_cur, int bs, hipStream_t s) {
+  if (!table || !meta || !rows || n_cur < 0 || bs < 1) return (int)hipErrorInvalidValue;
+  rows_next_kernel<<<1, 256, 0, s>>>(table, meta, rows, n_cur, bs);
   return (int)hipGetLastError();
 }
 

@@ -193,6 +193,17 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
   return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
 }
 
+// Fused batch gather (a deferred device-loader batch, runtime/data.py PendingRows): sample n of
+// the batch is dataset row rows[n] (staged by the previous step's tail / the loader); the step
+// kernel reads the image / label rows through it and writes them into the batch buffers (x, ydst)
+// for every later reader.  rows == null: x / the targets ARE the batch.
+struct RowSrc {
+  const int64_t* rows;
+  const float* xsrc;    // dataset images [rows][784]
+  const int64_t* ysrc;  // dataset labels [rows]
+  int64_t* ydst;        // the batch's label buffer [N]
+};
+
 // ------------------------------------------------------------------------------ forward
 constexpr int A1CL = Q1 * Q1 * 8;  // channel-last conv1 output: [pixel][8 channels], 6 used
 
@@ -221,7 +232,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
                                          const float* __restrict__ b1, const float* __restrict__ w2,
                                          const float* __restrict__ b2, uint16_t* __restrict__ a1g,
                                          uint8_t* __restrict__ code1, uint16_t* __restrict__ a2g,
-                                         uint8_t* __restrict__ code2, int N, ClsFwd cf) {
+                                         uint8_t* __restrict__ code2, int N, ClsFwd cf, const RowSrc& rs) {
   RK_TR(cf.trace, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // conv B operands: the fused path loads the prep kernel's fragments first thing (one 16-byte
@@ -248,9 +259,16 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
   // zero-slot elements are written by the other threads (disjoint addresses: no ordering needed)
   {
     static_assert(64 * WPS >= IMG * IMG / 4, "one vector per thread");
-    const float4* xs = (const float4*)(x + (int64_t)nc * IMG * IMG);
+    // fused gather: the sample's dataset row through the epoch table (two dependent loads), and
+    // the row is written back into the batch buffer for the backward phase and later readers
+    const int64_t srow = rs.rows ? rs.rows[nc] : (int64_t)nc;
+    const float4* xs = (const float4*)((rs.rows ? rs.xsrc : x) + srow * IMG * IMG);
     float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (st < IMG * IMG / 4) v4 = xs[st];
+    if (st < IMG * IMG / 4) {
+      v4 = xs[st];
+      if (rs.rows && live) ((float4*)(const_cast<float*>(x) + (int64_t)n * IMG * IMG))[st] = v4;
+    }
+    if (rs.rows && live && st == IMG * IMG / 4) rs.ydst[n] = rs.ysrc[srow];
     for (int b = st; b < 4 * IMGS + IMG * 5 + 8; b += 64 * WPS) {  // border / zero-slot elements
       int bi;
       if (b < 4 * IMGS) {  // rows 0, 1, 30, 31
@@ -574,7 +592,7 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
                                                        uint8_t* __restrict__ code1, uint16_t* __restrict__ a2g,
                                                        uint8_t* __restrict__ code2, int N, ClsFwd cf) {
   __shared__ __attribute__((aligned(16))) FwdSmem sm;
-  fwd_body<MLP>(sm, x, w1, b1, w2, b2, a1g, code1, a2g, code2, N, cf);
+  fwd_body<MLP>(sm, x, w1, b1, w2, b2, a1g, code1, a2g, code2, N, cf, RowSrc{});
 }
 
 // ------------------------------------------------------------------------------ backward
@@ -620,7 +638,7 @@ struct BwdSmem {
   float dyf[SPB][F3];               // fused CE: fp32 d(logits) of the block's samples
   float red[NTHR / 64];
   float lossp[SPB];
-  float cecnt[NTHR / 64];  // fused CE: valid-target count per wave (waves 1..15)
+  float cecnt[NTHR / 64];  // fused CE: [0] the block's valid-target count
   int flag;
 };
 static_assert(sizeof(((BwdSmem*)nullptr)->dc2) >= (NTHR / 64) * 2 * 256 * sizeof(float),
@@ -639,7 +657,7 @@ struct ClsBwd {
   const int64_t* target;
   int64_t ignore_index;
   float grad_scale;
-  float* partials;                  // [gridDim.x]
+  float* partials;                  // [2][gridDim.x]: loss sums, valid-target counts
   unsigned* counter;
   float* loss_out;                  // [2]: loss, nvalid
   int defer_loss;                   // 1: store block partials + nvalid only; the wgrad launch finalises
@@ -650,6 +668,8 @@ struct ClsBwd {
   int sync;
   uint64_t* trace;                  // optional phase timeline [blocks][kTraceStride]
   float* slab;                      // [blocks][SLABW] conv weight/bias gradient partials
+  const int64_t* row_table;         // fused gather: target of sample i = row_labels[row_table[i]]
+  const int64_t* row_labels;
 };
 
 template <bool MLP>
@@ -685,7 +705,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
 
   if (MLP)
     for (int i = threadIdx.x; i < H1P; i += NTHR) sm.zrow[i] = 0;
-  if (MLP && cb.ce && threadIdx.x == 0) sm.lossp[0] = 0.f;
+  if (MLP && cb.ce && threadIdx.x == 0) sm.lossp[0] = sm.cecnt[0] = 0.f;
   // fused path: the classifier dgrad B fragments and ReLU masks are loaded now, so the chain below
   // runs on registers and LDS only (each was one global round trip after a barrier)
   bf16x8 fb3, fb2[3], fb1[2][4];
@@ -717,17 +737,17 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
   for (int rd = 0; rd < nrounds; ++rd) {
     const int nbase = (blockIdx.x * rounds + rd) * SPB;
     // fused cross-entropy operands, issued ahead of the conv staging loads (in-order vmcnt):
-    // wave 0 holds one logit per lane (lane = 16 * sample + class); in round 0 waves 1..15 count
-    // the batch's valid targets (mean reduction; every block counts them itself)
+    // wave 0 holds one logit per lane (lane = 16 * sample + class).  The mean's 1/(valid targets)
+    // is NOT applied here: d(logits) is scaled by 1/N only, every block reports its own valid
+    // count, and the weight-gradient launch (which sums the counts) applies N / count to the
+    // gradients and divides the loss — no block reads the whole batch's targets.
     int64_t ce_t = 0;
-    float ce_x = 0.f, ce_cnt = 0.f;
+    float ce_x = 0.f;
     if (MLP && cb.ce) {
       if (wave == 0) {
         const int n = nbase + (lane >> 4), o = lane & 15;
-        ce_t = cb.target[n];
+        ce_t = cb.row_table ? cb.row_labels[cb.row_table[n]] : cb.target[n];
         ce_x = cb.logits[(int64_t)n * F3 + (o < F3 ? o : 0)];
-      } else if (rd == 0) {
-        for (int i = threadIdx.x - 64; i < N; i += NTHR - 64) ce_cnt += cb.target[i] != cb.ignore_index ? 1.f : 0.f;
       }
     }
     if constexpr (MLP) lds_barrier();
@@ -818,21 +838,22 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
           }
           if (oc) sm.dyf[sl][o] = valid ? e / se - ((int64_t)o == ce_t ? 1.f : 0.f) : 0.f;
           float li = (o == 0 && valid) ? mx + __logf(se) - xt : 0.f;  // lanes 0/16/32/48: a sample's loss
+          float ci = (o == 0 && valid) ? 1.f : 0.f;
           li += __shfl_xor(li, 16, 64);
           li += __shfl_xor(li, 32, 64);
-          if (lane == 0) sm.lossp[0] += li;  // block running sum over rounds (LDS: no live register)
-        } else if (rd == 0) {
-#pragma unroll
-          for (int k = 32; k >= 1; k >>= 1) ce_cnt += __shfl_xor(ce_cnt, k, 64);
-          if (lane == 0) sm.cecnt[wave] = ce_cnt;
+          ci += __shfl_xor(ci, 16, 64);
+          ci += __shfl_xor(ci, 32, 64);
+          if (lane == 0) {  // block running sums over rounds (LDS: no live register)
+            sm.lossp[0] += li;
+            sm.cecnt[0] += ci;
+          }
         }
         lds_barrier();
         RK_TR(cb.trace, 3);
         if (threadIdx.x < SPB * DYP || (threadIdx.x >= 256 && threadIdx.x < 256 + F3)) {
-          float nv = 0.f;
-#pragma unroll
-          for (int w = 1; w < NTHR / 64; ++w) nv += sm.cecnt[w];
-          const float sc = nv > 0.f ? cb.grad_scale / nv : 0.f;
+          // pre-normalised by the batch size (keeps the gradients' magnitudes, and so their bf16
+          // rounding, those of the mean); the weight-gradient launch applies N / (valid count)
+          const float sc = cb.grad_scale / (float)N;
           if (threadIdx.x < SPB * DYP) {
             const int sl = threadIdx.x / DYP, o = threadIdx.x % DYP;
             sm.dyl[sl][o] = f2bf(o < F3 ? sc * sm.dyf[sl][o] : 0.f);
@@ -1164,24 +1185,27 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
   RK_TR(cb.trace, 11);
   }
   if constexpr (MLP) {
-    if (cb.ce && cb.defer_loss) {  // partials + valid count; the next (wgrad) launch reduces them
+    if (cb.ce && cb.defer_loss) {  // loss / valid-count partials; the next (wgrad) launch reduces them
       if (threadIdx.x == 0) {
         cb.partials[blockIdx.x] = sm.lossp[0];
-        if (blockIdx.x == 0) {
-          float nv = 0.f;
-          for (int w = 1; w < NTHR / 64; ++w) nv += sm.cecnt[w];
-          cb.loss_out[1] = nv;
-        }
+        cb.partials[gridDim.x + blockIdx.x] = sm.cecnt[0];
       }
     } else if (cb.ce) {  // batch loss: block partials -> last block -> loss + Loss-capsule bookkeeping
-      if (threadIdx.x == 0) st_sc1(cb.partials + blockIdx.x, sm.lossp[0]);
+      // (this path is only for unit-scale callers: the gradients it leaves are unnormalised)
+      if (threadIdx.x == 0) {
+        st_sc1(cb.partials + blockIdx.x, sm.lossp[0]);
+        st_sc1(cb.partials + gridDim.x + blockIdx.x, sm.cecnt[0]);
+      }
       if (last_block_arrived(cb.counter, &sm.flag)) {
-        float t = 0.f;
-        for (int i = threadIdx.x; i < (int)gridDim.x; i += NTHR) t += ld_sc1(cb.partials + i);
+        float t = 0.f, c = 0.f;
+        for (int i = threadIdx.x; i < (int)gridDim.x; i += NTHR) {
+          t += ld_sc1(cb.partials + i);
+          c += ld_sc1(cb.partials + gridDim.x + i);
+        }
         t = block_sum(t, sm.red);
+        c = block_sum(c, sm.red);
         if (threadIdx.x == 0) {
-          float nv = 0.f;
-          for (int w = 1; w < NTHR / 64; ++w) nv += sm.cecnt[w];
+          const float nv = c;
           const float l = nv > 0.f ? t / nv : NAN;
           cb.loss_out[0] = l;
           cb.loss_out[1] = nv;
@@ -1229,10 +1253,14 @@ union TrainSmem {
 __global__ void __launch_bounds__(NTHR) lenet_train_kernel(const float* __restrict__ x, const float* __restrict__ b1,
                                                           const float* __restrict__ b2, uint16_t* __restrict__ a1g,
                                                           uint8_t* __restrict__ code1, uint8_t* __restrict__ code2,
-                                                          int N, ClsFwd cf, ClsBwd cb) {
+                                                          int N, ClsFwd cf, ClsBwd cb, RowSrc rs) {
   __shared__ __attribute__((aligned(16))) TrainSmem sm;
-  fwd_body<true>(sm.f, x, nullptr, b1, nullptr, b2, a1g, code1, nullptr, code2, N, cf);
+  fwd_body<true>(sm.f, x, nullptr, b1, nullptr, b2, a1g, code1, nullptr, code2, N, cf, rs);
   __syncthreads();  // LDS reuse + this block's global stores visible to all its waves
+  if (rs.rows) {  // the block's targets through the rows (as its own label stores, which it just made)
+    cb.row_table = rs.rows;
+    cb.row_labels = rs.ysrc;
+  }
   bwd_body<true>(sm.b, x, a1g, code1, nullptr, code2, nullptr, nullptr, nullptr, nullptr, nullptr, N, 1, cb);
 }
 
@@ -1362,15 +1390,18 @@ RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const
 // Whole fused LeNet training step of the batch but the weight gradients, in ONE launch
 // (lenet_train_kernel): the rk_lenet_fwd outputs (logits, a1, codes, transposed activations) and
 // the rk_lenet_bwd outputs (transposed gradients, conv-gradient slab, loss partials) for a
-// softmax cross-entropy on `ce` (required; its d(logits) scale is ce->grad_scale).
+// softmax cross-entropy on `ce` (required; its d(logits) scale is ce->grad_scale).  rows (may be
+// null): the batch is gathered by this launch (RowSrc): x / ce->target are the batch buffers it fills.
 RK_API int rk_lenet_train(const float* x, const float* b1, const float* b2, const void* frag, const float* fb1,
                           const float* fb2, const float* fb3, void* a1, void* code1, void* code2, void* a2T, void* h1T,
                           void* h2T, float* logits, void* dyT, void* d2T, void* d1T, float* slab, int N,
-                          const LenetCE* ce, hipStream_t s) {
+                          const LenetCE* ce, const RowSrc* rows, hipStream_t s) {
   if (N % 8 || N > 65536 || ((uintptr_t)x & 15) || !slab || !ce || ce->logits != logits) return (int)hipErrorInvalidValue;
+  const RowSrc rs = rows ? *rows : RowSrc{};
+  if (rs.rows && (!rs.xsrc || !rs.ysrc || !rs.ydst || ((uintptr_t)rs.xsrc & 15))) return (int)hipErrorInvalidValue;
   const ClsFwd cf{(const bf16x8*)frag, fb1, fb2, fb3, (uint16_t*)a2T, (uint16_t*)h1T, (uint16_t*)h2T, logits, g_fwd_trace};
   const ClsBwd cb = cls_bwd(frag, nullptr, h1T, h2T, dyT, d2T, d1T, slab, ce);
-  lenet_train_kernel<<<N / SPB, NTHR, 0, s>>>(x, b1, b2, (uint16_t*)a1, (uint8_t*)code1, (uint8_t*)code2, N, cf, cb);
+  lenet_train_kernel<<<N / SPB, NTHR, 0, s>>>(x, b1, b2, (uint16_t*)a1, (uint8_t*)code1, (uint8_t*)code2, N, cf, cb, rs);
   return (int)hipGetLastError();
 }
 

@@ -18,6 +18,7 @@
 //
 // Everything is branch-free in the load paths (clamped addresses + selects).
 #include "optim_common.h"
+#include "rows_common.h"
 
 using namespace rk;
 
@@ -263,6 +264,17 @@ struct LossFin {
 struct WgradArgs {
   uint64_t* trace;  // optional phase stamps [blocks][8] (s_memrealtime): start, reduced, end, tile: old values in, main loop done
   float gscale;     // every produced gradient is scaled by this (the upstream gradient factor)
+  // normalisation by a count the backward left unapplied (the fused LeNet cross-entropy's mean,
+  // pre-scaled by 1 / M): gradients are also scaled by M / sum(cnt_parts[0..ncnt)), and the loss
+  // block divides by that sum
+  const float* cnt_parts;
+  int ncnt;
+  // deferred loader batch consumed by this step (runtime/data.py PendingRows): one extra block
+  // advances the epoch cursor and stages the next batch's rows (rows_common.h), or null
+  const int64_t* rn_table;
+  int64_t* rn_meta;
+  int64_t* rn_rows;
+  int rn_cur, rn_bs, has_rows;
   WgradProb p[3];
   int nprob, M, tiles, nslab;
   SlabArgs sl;
@@ -273,17 +285,59 @@ struct WgradArgs {
   rk_opt::TensorRec rdw[3], rdb[3], rsl[4];
 };
 
-__device__ void loss_fin_block(const LossFin& f, float (*red)[32 * 32]) {
+
+
+// one slab block: 64 columns x all rows; 8 row groups per block, 8 independent loads per thread
+// in flight, LDS reduce over the groups, one plain RMW per column (sole owner: deterministic)
+constexpr int kEpiGroups = 4;  // param groups the epilogue precomputes step constants for
+
+// per-group Adam constants of this launch's step, written to LDS before the caller's barrier
+struct StepFill {
+  const WgradArgs* a;
+  float cur;
+  rk_opt::AdamStep* s_ks;
+  float cpart;   // this thread's share of the count partials (loaded at kernel start)
+  float* s_cnt;  // [NW] per-wave count sums
+  __device__ __forceinline__ void operator()() const {
+    if (a->epi.on && threadIdx.x < kEpiGroups)
+      s_ks[threadIdx.x] = rk_opt::adam_step(a->epi.hyper[threadIdx.x < a->epi.on ? threadIdx.x : 0], cur + 1.f);
+    if (a->cnt_parts) {
+      const float c = wave_sum(cpart);
+      if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = c;
+    }
+  }
+  // after the caller's barrier: the gradient factor (gscale / count when normalising)
+  __device__ __forceinline__ float count() const {
+    float n = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) n += s_cnt[w];
+    return n;
+  }
+  __device__ __forceinline__ float gs() const {
+    if (!a->cnt_parts) return a->gscale;
+    const float n = count();  // the backward pre-scaled by 1 / M (the batch): apply M / count
+    return n > 0.f ? a->gscale * ((float)a->M / n) : 0.f;
+  }
+};
+
+__device__ void loss_fin_block(const LossFin& f, float (*red)[32 * 32], const StepFill& sf) {
   float t = 0.f;
   for (int i = threadIdx.x; i < f.nparts; i += NT) t += f.partials[i];
 #pragma unroll
   for (int k = 32; k >= 1; k >>= 1) t += __shfl_xor(t, k, 64);
   if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = t;
+  sf();
   __syncthreads();
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int w = 0; w < NT / 64; ++w) s += red[0][w];  // fixed order: deterministic
-    const float nv = f.loss_out[1];
+    float nv;
+    if (sf.a->cnt_parts) {
+      nv = sf.count();
+      f.loss_out[1] = nv;
+    } else {
+      nv = f.loss_out[1];
+    }
     const float l = nv > 0.f ? s / nv : NAN;
     f.loss_out[0] = l;
     if (f.acc) {
@@ -298,21 +352,6 @@ __device__ void loss_fin_block(const LossFin& f, float (*red)[32 * 32]) {
     }
   }
 }
-
-// one slab block: 64 columns x all rows; 8 row groups per block, 8 independent loads per thread
-// in flight, LDS reduce over the groups, one plain RMW per column (sole owner: deterministic)
-constexpr int kEpiGroups = 4;  // param groups the epilogue precomputes step constants for
-
-// per-group Adam constants of this launch's step, written to LDS before the caller's barrier
-struct StepFill {
-  const WgradArgs* a;
-  float cur;
-  rk_opt::AdamStep* s_ks;
-  __device__ __forceinline__ void operator()() const {
-    if (a->epi.on && threadIdx.x < kEpiGroups)
-      s_ks[threadIdx.x] = rk_opt::adam_step(a->epi.hyper[threadIdx.x < a->epi.on ? threadIdx.x : 0], cur + 1.f);
-  }
-};
 
 __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, float (*red)[32 * 32],
                                                   const rk_opt::AdamStep* ks, const StepFill& sf) {
@@ -358,7 +397,7 @@ __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, flo
     float t = 0.f;
 #pragma unroll
     for (int g = 0; g < NW; ++g) t += red[g][threadIdx.x];
-    t *= a.gscale;
+    t *= sf.gs();
     if (ks) rk_opt::epi_apply(a.rsl[di], ks[a.rsl[di].group], c - s.bound[di], ee, old + t, a.epi.zero_grads);
     else *dst = old + t;
   }
@@ -382,15 +421,22 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   __shared__ float red[NW][32 * 32];
   __shared__ float rsum[NW][32];
   __shared__ rk_opt::AdamStep s_ks[kEpiGroups];
+  __shared__ float s_cnt[NW];
   // optimizer epilogue: the step counter is loaded now but consumed only where each block type
   // already synchronises (its LDS reduction), so its memory round trip overlaps the gradient loads
-  // instead of preceding them
+  // instead of preceding them; likewise the count partials of a normalising launch
   const float cur = a.epi.on ? a.epi.step[0] : 0.f;
-  const StepFill sf{&a, cur, s_ks};
+  float cpart = 0.f;
+  if (a.cnt_parts)
+    for (int i = threadIdx.x; i < a.ncnt; i += NT) cpart += a.cnt_parts[i];
+  const StepFill sf{&a, cur, s_ks, cpart, s_cnt};
   const rk_opt::AdamStep* ks = a.epi.on ? s_ks : nullptr;
-  if ((int)blockIdx.x >= a.tiles) {
+  if (a.has_rows && (int)blockIdx.x == (int)gridDim.x - 1) {
+    // the step's batch cursor (no gradient work; still takes the optimizer step's ticket below)
+    rows_next_block(a.rn_table, a.rn_meta, a.rn_rows, a.rn_cur, a.rn_bs);
+  } else if ((int)blockIdx.x >= a.tiles) {
     if ((int)blockIdx.x - a.tiles < a.nslab) slab_reduce_block(a, blockIdx.x - a.tiles, red, ks, sf);
-    else loss_fin_block(a.lf, red);
+    else loss_fin_block(a.lf, red, sf);
   } else {
     wgrad_tile(a, red, rsum, ks, sf);
   }
@@ -475,13 +521,14 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
   sf();
   __syncthreads();
   if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+  const float gsc = sf.gs();
 #pragma unroll
   for (int q = 0; q < 32 * 32 / NT; ++q) {
     const int e = threadIdx.x + q * NT, r = e >> 5, c = e & 31;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[w][e];
-    v *= a.gscale;
+    v *= gsc;
     if (n0 + r < P.N && k0 + c < P.K) {
       const int64_t i = (int64_t)(n0 + r) * P.K + k0 + c;
       if (ks) rk_opt::epi_apply(a.rdw[pi], ks[a.rdw[pi].group], i, ew[q], dw_old[q] + v, a.epi.zero_grads);
@@ -492,13 +539,29 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += rsum[w][threadIdx.x];
-    v *= a.gscale;
+    v *= gsc;
     if (ks) rk_opt::epi_apply(a.rdb[pi], ks[a.rdb[pi].group], n0 + threadIdx.x, eb, db_old + v, a.epi.zero_grads);
     else P.db[n0 + threadIdx.x] = db_old + v;
   }
 }
 
 }  // namespace
+
+// The NEXT rk_mlp3_wgrad_loss on this thread also advances a deferred loader batch's cursor and
+// stages the next batch's rows (one extra block; rows_common.h): the step that consumed the batch
+// ends with its cursor step instead of a launch of its own.
+struct RowsReq {
+  const int64_t* table;
+  int64_t* meta;
+  int64_t* rows;
+  int n_cur, bs;
+};
+static thread_local RowsReq g_rows{};
+RK_API int rk_mlp3_set_rows(const int64_t* table, int64_t* meta, int64_t* rows, int n_cur, int bs) {
+  if (!table || !meta || !rows || n_cur < 0 || bs < 1) return (int)hipErrorInvalidValue;
+  g_rows = RowsReq{table, meta, rows, n_cur, bs};
+  return 0;
+}
 
 // Diagnostics: per-block phase stamps of the grouped weight-gradient launch ([blocks][8] u64, or
 // null = off): start, operands reduced (after the block's LDS barrier), end; tiles also: old values
@@ -552,14 +615,22 @@ struct WgradEpi {
 // optimizer launch is then skipped by the caller).  Every dW/db/slab destination needs a record.
 // gscale: factor on every produced gradient (1 unless the backward inputs were formed for a unit
 // upstream gradient, e.g. by the fused LeNet step kernel ahead of the loss scaling).
+// norm_by_count: the backward scaled by 1 / M instead of the loss's 1 / (valid count) and stored
+// per-block valid counts after its loss partials (loss->partials[nparts ..]): gradients are scaled
+// by M / their sum, the loss divided by it.
 RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* const* xT, float* const* dw,
                               float* const* db, const int* Ns, const int* Ks, int M, const float* slab, int slab_rows,
                               int slab_width, float* const* slab_dst, const int* slab_bound, const LossFin* loss,
-                              const WgradEpi* epi, float gscale, hipStream_t s) {
+                              const WgradEpi* epi, float gscale, int norm_by_count, hipStream_t s) {
   if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
   WgradArgs a{};
   a.trace = g_wgrad_trace;
   a.gscale = gscale;
+  if (norm_by_count) {  // count partials follow the loss partials: partials[nparts .. 2 nparts)
+    if (!loss) return (int)hipErrorInvalidValue;
+    a.cnt_parts = loss->partials + loss->nparts;
+    a.ncnt = loss->nparts;
+  }
   a.nprob = nprob;
   a.M = M;
   int tiles = 0;
@@ -617,6 +688,16 @@ RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* cons
       if ((float*)a.rsl[i].g != slab_dst[i] || a.rsl[i].group >= epi->ngroups) return (int)hipErrorInvalidValue;
     }
   }
+  if (g_rows.table) {  // consumes the staged rows request (rk_mlp3_set_rows)
+    a.rn_table = g_rows.table;
+    a.rn_meta = g_rows.meta;
+    a.rn_rows = g_rows.rows;
+    a.rn_cur = g_rows.n_cur;
+    a.rn_bs = g_rows.bs;
+    a.has_rows = 1;
+    extra += 1;
+    g_rows = RowsReq{};
+  }
   mlp3_wgrad_kernel<<<tiles + extra, NT, 0, s>>>(a);
   return (int)hipGetLastError();
 }
@@ -625,5 +706,5 @@ RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT
                          const int* Ns, const int* Ks, int M, const float* slab, int slab_rows, int slab_width,
                          float* const* slab_dst, const int* slab_bound, hipStream_t s) {
   return rk_mlp3_wgrad_loss(nprob, dT, xT, dw, db, Ns, Ks, M, slab, slab_rows, slab_width, slab_dst, slab_bound,
-                            nullptr, nullptr, 1.f, s);
+                            nullptr, nullptr, 1.f, 0, s);
 }

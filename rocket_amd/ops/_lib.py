@@ -71,8 +71,8 @@ KERNEL_SIGS = {
     "rk_mlp3_wgrad": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                               c_int, c_void_p, c_void_p, c_void_p]),
     "rk_mlp3_wgrad_loss": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p]),
-    "rk_lenet_train": (c_int, [c_void_p] * 18 + [c_int, c_void_p, c_void_p]),
+                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p]),
+    "rk_lenet_train": (c_int, [c_void_p] * 18 + [c_int, c_void_p, c_void_p, c_void_p]),
     "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_int, c_void_p]),
     "rk_amp_check": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
@@ -102,6 +102,8 @@ KERNEL_SIGS = {
     "rk_gap_stamp": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "rk_gather_rows_any_order": (None, []),
     "rk_gather_set_trace": (None, [c_void_p]),
+    "rk_rows_next": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "rk_mlp3_set_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
     "rk_gap_stamp_big": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "rk_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_float,
                             c_void_p]),

@@ -263,6 +263,34 @@ class _LenetCE(ctypes.Structure):
                 ("sync", ctypes.c_int), ("defer_loss", ctypes.c_int)]
 
 
+class _RowSrc(ctypes.Structure):
+    """Mirror of ``struct RowSrc`` (lenet_conv.hip): the batch gathered by the step kernel itself."""
+
+    _fields_ = [("rows", ctypes.c_void_p), ("xsrc", ctypes.c_void_p), ("ysrc", ctypes.c_void_p),
+                ("ydst", ctypes.c_void_p)]
+
+
+def _claim_rows(x, target):
+    """The deferred device-loader batch ``(x, target)`` (runtime/data.py PendingRows), claimed for
+    the step kernel to gather itself: ``(_RowSrc, record)``; None when the batch is an ordinary one
+    (or not exactly these two buffers: then it is gathered now).  The weight-gradient launch of the
+    step performs the record's cursor advance."""
+    from rocket_amd.runtime.data import pending_rows
+
+    p = pending_rows((x, target))
+    if p is None:
+        return None
+    ok = (len(p.bufs) == 2 and p.bufs[0] is x and p.bufs[1] is target and p.n == x.shape[0]
+          and p.loader.dataset.tensors[0].dtype == torch.float32
+          and p.loader.dataset.tensors[1].dtype == torch.int64
+          and tuple(p.loader.dataset.tensors[0].shape[1:]) == (1, 28, 28))
+    if not ok:
+        p.materialize()
+        return None
+    (xs, ys), rows = p.claim()
+    return _RowSrc(rows.data_ptr(), xs.data_ptr(), ys.data_ptr(), target.data_ptr()), p
+
+
 class _LossFin(ctypes.Structure):
     """Mirror of ``struct LossFin`` (mlp.hip): the batch loss finalised by the wgrad launch from the
     backward's per-block partials (no last-block ticket at the tail of the backward)."""
@@ -352,22 +380,32 @@ class _LeNetFused(torch.autograd.Function):
                 and target.device == dev):
             dyT, d2T, d1T = torch.empty(10, N, **bf), torch.empty(84, N, **bf), torch.empty(120, N, **bf)
             slab = torch.empty(N // 4, int(lib.rk_lenet_slab_width()), dtype=torch.float32, device=dev)
-            partials = torch.empty(N // 4, dtype=torch.float32, device=dev)
+            partials = torch.empty(2 * (N // 4), dtype=torch.float32, device=dev)  # loss sums, valid counts
             loss_out = torch.empty(2, dtype=torch.float32, device=dev)
             ce = _LenetCE(logits.data_ptr(), target.data_ptr(), -100, 1.0, partials.data_ptr(),
                           _lib.Workspace.get(dev).counter("lenet_ce"), loss_out.data_ptr(), None, None, None, 0,
                           0.0, 0, 1)
+            claimed = _claim_rows(x, target)  # a deferred loader batch: this launch gathers it
+            rows = claimed[0] if claimed is not None else None
+            ctx.rows_pend = claimed[1] if claimed is not None else None
             _lib.check(lib.rk_lenet_train(x.data_ptr(), cw[1].data_ptr(), cw[3].data_ptr(), frag.data_ptr(),
                                           cw[5].data_ptr(), cw[7].data_ptr(), cw[9].data_ptr(), a1.data_ptr(),
                                           c1.data_ptr(), c2.data_ptr(), a2T.data_ptr(), h1T.data_ptr(), h2T.data_ptr(),
                                           logits.data_ptr(), dyT.data_ptr(), d2T.data_ptr(), d1T.data_ptr(),
-                                          slab.data_ptr(), N, ctypes.byref(ce), stream), "rk_lenet_train")
+                                          slab.data_ptr(), N, ctypes.byref(ce),
+                                          ctypes.byref(rows) if rows is not None else None, stream),
+                       "rk_lenet_train")
             ctx.spec = (target, target._version, dyT, d2T, d1T, slab, partials, loss_out)
         else:
+            from rocket_amd.runtime.data import materialize_batch
+
+            materialize_batch((x, target) if target is not None else x)  # a deferred loader batch: gather it now
             _lib.check(lib.rk_lenet_fwd(x.data_ptr(), cw[0].data_ptr(), cw[1].data_ptr(), cw[2].data_ptr(),
                                         cw[3].data_ptr(), frag.data_ptr(), cw[5].data_ptr(), cw[7].data_ptr(),
                                         cw[9].data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(), a2T.data_ptr(),
                                         h1T.data_ptr(), h2T.data_ptr(), logits.data_ptr(), N, stream), "rk_lenet_fwd")
+        if ctx.spec is None:
+            ctx.rows_pend = None
         ctx.params = (w1, b1, w2, b2, f1w, f1b, f2w, f2b, f3w, f3b)
         ctx.frags = frags
         ctx.save_for_backward(x, a1, c1, c2, a2T, h1T, h2T, frag, cw[2], logits)
@@ -409,7 +447,7 @@ class _LeNetFused(torch.autograd.Function):
             acc_scale, sync = 0.0, 0
             if accum is not None:
                 acc, ring, slot, acc_scale, sync = accum
-            partials = torch.empty(N // 4, dtype=torch.float32, device=dev)
+            partials = torch.empty(2 * (N // 4), dtype=torch.float32, device=dev)  # loss sums, valid counts
             keep = (partials, target)
             ce = _LenetCE(logits.data_ptr(), target.data_ptr(), -100, float(grad_scale), partials.data_ptr(),
                           _lib.Workspace.get(dev).counter("lenet_ce"), loss_out.data_ptr(), _lib.ptr(acc),
@@ -446,13 +484,18 @@ class _LeNetFused(torch.autograd.Function):
         assert sum(sizes) == int(lib.rk_lenet_slab_cols()), "fused LeNet expects conv1 6x1x5x5 / conv2 16x6x5x5"
         bounds = (ctypes.c_int * 5)(0, sizes[0], sizes[0] + sizes[1], sizes[0] + sizes[1] + sizes[2], sum(sizes))
         epi, opt = _optimizer_epilogue(params, direct)
+        pend, ctx.rows_pend = getattr(ctx, "rows_pend", None), None
+        if pend is not None and not pend.advanced:  # the step's batch cursor, as one more block of this launch
+            _lib.check(lib.rk_mlp3_set_rows(*pend.advance_args()), "rk_mlp3_set_rows")
+            pend.mark_advanced()
         _lib.check(lib.rk_mlp3_wgrad_loss(3, P(*[q[0].data_ptr() for q in probs]), P(*[q[1].data_ptr() for q in probs]),
                                           P(*[q[2].data_ptr() for q in probs]), P(*[q[3].data_ptr() for q in probs]),
                                           I(*[q[4] for q in probs]), I(*[q[5] for q in probs]), N, slab.data_ptr(),
                                           N // 4, slab.shape[1],
                                           (ctypes.c_void_p * 4)(*[bufs[i].data_ptr() for i in range(4)]), bounds,
                                           ctypes.byref(fin) if fin is not None else None,
-                                          ctypes.byref(epi) if epi is not None else None, float(gscale), stream),
+                                          ctypes.byref(epi) if epi is not None else None, float(gscale),
+                                          int(fin is not None), stream),
                    "rk_mlp3_wgrad_loss")
         if opt is not None:
             opt.epilogue_done = True  # the optimizer's own launch for this step is skipped

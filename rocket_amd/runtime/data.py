@@ -341,6 +341,88 @@ def mark_ring(sets: List[tuple]) -> None:
             b._rocket_ring = (sets, k, j)
 
 
+class PendingRows:
+    """A device-loader batch whose rows are not gathered yet (:class:`DeviceLoader` deferred mode).
+
+    Attached to each of the batch's buffers as ``_rocket_pending``.  The batch's dataset rows are
+    staged on the device in the loader's persistent ``rows`` buffer (indices ``rows[0:n]``), and
+    after the batch an epoch cursor (``meta = {cursor, table length}``) is advanced and the NEXT
+    batch's rows staged (``rk_rows_next``) — all device-side, so a captured step that consumes
+    the batch consumes the next one on every replay.  Exactly one of:
+
+    * :meth:`materialize` — a gather launch fills the buffers from ``rows``, then the advance;
+    * :meth:`claim` — a consumer whose own kernels read the rows (the fused LeNet step kernel) takes
+      over: they write the rows into the buffers (for every later reader), and the step's last
+      kernel performs the advance (:meth:`advance_args`, then :meth:`mark_advanced`).
+
+    ``done`` flips when the batch was gathered or claimed (at capture time: by the captured step).
+    A claimed batch whose advance never ran is advanced by the loader before the next batch.
+    """
+
+    __slots__ = ("loader", "bufs", "gather", "n", "done", "advanced")
+
+    def __init__(self, loader, bufs, gather, n):
+        self.loader, self.bufs, self.gather, self.n = loader, bufs, gather, n
+        self.done = self.advanced = False
+
+    def advance_args(self):
+        """(table, meta, rows, n, batch size) pointers for ``rk_rows_next`` / ``rk_mlp3_set_rows``."""
+        ld = self.loader
+        return ld._table.data_ptr(), ld._meta.data_ptr(), ld._rows.data_ptr(), self.n, ld._rows.numel()
+
+    def mark_advanced(self) -> None:
+        self.advanced = True
+
+    def advance(self) -> None:
+        """The advance as a launch of its own (a claimed batch whose step did not do it)."""
+        if self.advanced:
+            return
+        self.advanced = True
+        from rocket_amd.ops import _lib
+
+        _lib.check(_lib.kernels().rk_rows_next(*self.advance_args(), _lib.stream_ptr(self.loader.device)),
+                   "rk_rows_next")
+
+    def materialize(self) -> None:
+        if self.done:
+            return
+        self.done = True
+        self.gather(self.loader._rows[: self.n])
+        self.advance()
+
+    def claim(self):
+        """((image source, label source), staged rows) for a consumer that gathers the rows itself."""
+        self.done = True
+        return self.loader.dataset.tensors, self.loader._rows
+
+    def rebind(self, bufs) -> "PendingRows":
+        """The same pending batch on another ring slot's buffers (graph variant capture)."""
+        gather = next((g for b, g in self.loader._rings.get(self.n, []) if b[0] is bufs[0]), None)
+        return PendingRows(self.loader, bufs, gather, self.n)
+
+
+def pending_rows(batch) -> Optional[PendingRows]:
+    """The not-yet-gathered :class:`PendingRows` of a batch (tensor / tuple / list / dict), or None."""
+    if isinstance(batch, torch.Tensor):
+        p = getattr(batch, "_rocket_pending", None)
+        return p if (p is not None and not p.done and any(b is batch for b in p.bufs)) else None
+    if isinstance(batch, dict):
+        batch = list(batch.values())
+    if isinstance(batch, (list, tuple)):
+        for b in batch:
+            p = pending_rows(b)
+            if p is not None:
+                return p
+    return None
+
+
+def materialize_batch(batch) -> None:
+    """Gather a deferred device-loader batch now (no-op for ordinary batches)."""
+    p = pending_rows(batch)
+    if p is not None:
+        p.materialize()
+
+
 class DeviceTensorDataset(torch.utils.data.Dataset):
     """A dataset of aligned tensors resident on one device (typically HBM).
 
@@ -399,6 +481,11 @@ class DeviceLoader(_LoaderBase):
     #: the immediately preceding one has completed when the gather starts), and because the first
     #: gather after an index-table upload keeps the barrier (it reads the uploaded table).
     ANY_ORDER = os.environ.get("ROCKET_GATHER_ANY_ORDER", "1") != "0"
+    #: deferred mode (``defer = True``, set by the Looper when the consumer of the batches is a
+    #: model that gathers its own rows, see :class:`PendingRows`): batches are yielded as ring
+    #: slots still to be filled, and the row indices live in a persistent device table read through
+    #: a device-side cursor.  ROCKET_DEFER_GATHER=0 disables it.
+    DEFER = os.environ.get("ROCKET_DEFER_GATHER", "1") != "0"
 
     def __init__(
         self,
@@ -433,6 +520,9 @@ class DeviceLoader(_LoaderBase):
         self._rings: dict = {}
         self._ring_pos: dict = {}
         self._fresh_table = True  # the next gather reads a just-uploaded index table
+        self.defer = False
+        self._table = self._meta = self._rows = None
+        self._last_pending: Optional[PendingRows] = None
 
     def index_table(self) -> List[torch.Tensor]:
         batches = self.batch_sampler.local_batches()
@@ -491,6 +581,87 @@ class DeviceLoader(_LoaderBase):
         compute.wait_event(done)
         return bufs
 
+    def _deferred(self, n: int):
+        """Deferred mode: the next ring slot, tagged with its :class:`PendingRows`.  A previous
+        batch nobody gathered (consumed neither by a claiming model nor by a materialising reader)
+        is gathered first, so the device cursor stays in step with the batches handed out."""
+        last = self._last_pending
+        if last is not None:
+            if not last.done:
+                last.materialize()
+            elif not last.advanced:
+                last.advance()  # claimed, but the consuming step's advance never ran
+        bufs, gather = self._slot(n)
+        p = PendingRows(self, bufs, gather, n)
+        for b in bufs:
+            b._rocket_pending = p
+        self._last_pending = p
+        return bufs
+
+    def _slot(self, n: int):
+        from rocket_amd.ops.data import RowGather
+
+        ring = self._rings.get(n)
+        if ring is None:
+            tensors = self.dataset.tensors
+            ring = []
+            for _ in range(self.RING):
+                bufs = tuple(torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device) for t in tensors)
+                ring.append((bufs, RowGather([t.contiguous() for t in tensors], bufs)))
+            mark_ring([bufs for bufs, _ in ring])
+            self._rings[n] = ring
+        k = self._ring_pos.get(n, 0)
+        self._ring_pos[n] = (k + 1) % self.RING
+        return ring[k]
+
+    def _upload_table(self, batches) -> int:
+        """Deferred mode: this epoch's row order into the persistent device table, cursor 0 and the
+        first batch's rows staged (host-to-device copies, ordered before the epoch's first step)."""
+        flat = [i for b in batches for i in b]
+        self._ensure_table()
+        if len(flat) > self._table.numel():
+            raise RuntimeError("deferred device loader: epoch row table larger than its capacity")
+        host = torch.tensor(flat + [0, len(flat)], dtype=torch.int64).pin_memory()
+        if flat:
+            self._table[: len(flat)].copy_(host[: len(flat)], non_blocking=True)
+            k = min(len(flat), self._rows.numel())
+            self._rows[:k].copy_(host[:k], non_blocking=True)
+        self._meta.copy_(host[len(flat):], non_blocking=True)
+        self._table_host = host  # pinned source alive until the copies ran
+        return len(flat)
+
+    def _ensure_table(self) -> None:
+        """Allocate the persistent row table, cursor and staged rows once: captured steps keep their
+        addresses, so a loader and its ``with_skip`` copies (a resumed epoch) must share them."""
+        if self._table is None:
+            cap = len(self.dataset) + 2 * self.total_batch_size  # even_batches may repeat a few rows
+            self._table = torch.zeros(cap, dtype=torch.int64, device=self.device)
+            self._meta = torch.zeros(2, dtype=torch.int64, device=self.device)  # cursor, table length
+            self._rows = torch.zeros(self.batch_size, dtype=torch.int64, device=self.device)
+
+    def __iter__(self):
+        if not (self.defer and self.DEFER and self.device.type == "cuda"):
+            yield from super().__iter__()
+            return
+        # deferred: no gather one batch ahead (the consumer gathers each batch in its own step)
+        self._begin()
+        self.set_epoch(self.iteration)
+        batches = self.batch_sampler.local_batches()
+        self._upload_table(batches)
+        self._last_pending = None
+        for i, b in enumerate(batches):
+            if i == len(batches) - 1:
+                self.end_of_dataloader = True
+            yield self._deferred(len(b))
+        last = self._last_pending
+        if last is not None:
+            if not last.done:
+                last.materialize()
+            elif not last.advanced:
+                last.advance()
+        self.iteration += 1
+        self._end()
+
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
@@ -512,6 +683,10 @@ class DeviceLoader(_LoaderBase):
         out = DeviceLoader(self.dataset, skip=num_batches, **self._ctor)
         out.set_epoch(self.iteration)
         out._rings, out._ring_pos = self._rings, self._ring_pos  # same buffers -> same captured graphs
+        out.defer = self.defer
+        if self.device.type == "cuda":
+            self._ensure_table()
+        out._table, out._meta, out._rows = self._table, self._meta, self._rows
         return out
 
 

@@ -144,7 +144,7 @@ def _rebuild(batch, it):
 
 
 class _Captured:
-    __slots__ = ("graphs", "static_in", "persistent", "out", "sync", "host_sync_buffers")
+    __slots__ = ("graphs", "static_in", "persistent", "out", "sync", "host_sync_buffers", "rows_in_graph")
 
     def __init__(self):
         self.graphs: list = []   # [_Part A] or [A, B] (B after the host-side gradient reduction)
@@ -153,6 +153,7 @@ class _Captured:
         self.out = None
         self.sync = False
         self.host_sync_buffers = False
+        self.rows_in_graph = False  # the step gathers its deferred loader batch itself (PendingRows)
 
 
 class StepGraphs:
@@ -354,8 +355,37 @@ class StepGraphs:
             if fn is not None:
                 fn(attrs)
 
+    @staticmethod
+    def _bind_pending(attrs: Attributes, tens: List[torch.Tensor], run: bool):
+        """The deferred-batch record the captured step sees: this iteration's own (``run``), or the
+        same pending batch rebound to the ring slot of a variant captured ahead (``tens`` = that
+        slot's buffers), temporarily attached to them.  Returns (record, [(buffer, old attr)])."""
+        from rocket_amd.runtime.data import pending_rows
+
+        p = pending_rows(attrs.batch)
+        if p is None or run:
+            return p, []
+        tag = next((getattr(t, "_rocket_ring", None) for t in tens if getattr(t, "_rocket_ring", None)), None)
+        if tag is None:
+            return None, []
+        bufs = tag[0][tag[1]]
+        q = p.rebind(bufs)
+        restore = [(b, getattr(b, "_rocket_pending", None)) for b in bufs]
+        for b in bufs:
+            b._rocket_pending = q
+        return q, restore
+
     def _capture(self, attrs: Attributes, tens: List[torch.Tensor], run: bool = True) -> _Captured:
         """Capture the micro-step for inputs ``tens``; ``run``: also replay it for this iteration."""
+        pend, restore = self._bind_pending(attrs, tens, run)
+        try:
+            v = self._capture_inner(attrs, tens, run, pend)
+        finally:
+            for b, old in restore:
+                b._rocket_pending = old
+        return v
+
+    def _capture_inner(self, attrs: Attributes, tens: List[torch.Tensor], run: bool, pend) -> _Captured:
         engine = self.mod._accelerator
         v = _Captured()
         v.sync = engine.sync_gradients
@@ -402,6 +432,9 @@ class StepGraphs:
         if self._dev is None:
             self._dev = engine.device
         v.out = cap.batch
+        # the captured step gathered its deferred batch (claimed by the model's kernels or gathered
+        # by a captured cursor-mode launch): every replay gathers the batch of its iteration
+        v.rows_in_graph = pend is not None and pend.done
         self.captures += 1
         self.parts = max(self.parts, len(v.graphs))
         logger.info(f"captured HIP graph(s) for sync={v.sync} ({len(v.graphs)} part(s))")
@@ -427,6 +460,14 @@ class StepGraphs:
             host(attrs)
 
     def _replay(self, v: _Captured, attrs: Attributes, tens: List[torch.Tensor]) -> None:
+        from rocket_amd.runtime.data import pending_rows
+
+        pend = pending_rows(attrs.batch)
+        if pend is not None:
+            if v.rows_in_graph:
+                pend.done = pend.advanced = True  # the replay below gathers it and advances the cursor
+            else:
+                pend.materialize()
         for dst, src, keep in zip(v.static_in, tens, v.persistent):
             if not keep:
                 dst.copy_(src, non_blocking=True)

@@ -45,9 +45,10 @@ def test_resume_with_fused_optimizer_state(tmp_path):
     torch.manual_seed(1)  # different init: everything must come from the checkpoint
     res = LeNet()
     _tree(tmp_path / "c", data, res, FusedAdamW(res.parameters(), lr=1e-3), epochs=2).resume(str(ck)).launch()
-    # The fused conv backward accumulates weight gradients with global f32 atomics, so two runs of
-    # the same step differ in the last bits; Adam turns such differences on near-zero gradients into
-    # up to ~lr-sized weight deltas per step.  Resume is exact if the bulk agrees tightly and no
+    # The resumed run's first steps are eager (plain loss kernel -> d(logits) -> backward) where
+    # the uninterrupted run replays the captured fused-cross-entropy step: the same math with a
+    # different bf16 rounding of d(logits), and Adam turns such differences on near-zero gradients
+    # into up to ~lr-sized weight deltas per step.  Resume is exact if the bulk agrees tightly and no
     # element drifts further than a few Adam steps (a wrong restore is off by O(0.1) everywhere).
     for a, b in zip(ref.parameters(), res.parameters()):
         d = (a - b).abs()
