@@ -37,7 +37,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--cfgs", default="0", help="conv pipelines to A/B (rk_conv_set_cfg), e.g. 0,1,2,3")
+    ap.add_argument("--check", action="store_true", help="compare every pipeline's outputs with pipeline 0's")
     a = ap.parse_args()
+    cfgs = [int(c) for c in a.cfgs.split(",")]
     from rocket_amd import models
     from rocket_amd.ops import iconv
 
@@ -68,19 +71,36 @@ def main():
         OH, OW = geo[-2], geo[-1]
         dy = torch.randn(N, co, OH, OW, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
         flops = 2.0 * N * OH * OW * co * C * r * r
-        t = {
-            "fwd": timed(lambda: iconv._conv_fwd(xc, w16, st, pad, None)),
-            "dgrad": timed(lambda: iconv._conv_dgrad(dy, w16, geo, None)),
-            "wgrad": timed(lambda: iconv._conv_wgrad(dy, xc, w, geo)),
+        lib = iconv._kernels()
+        fns = {
+            "fwd": lambda: iconv._conv_fwd(xc, w16, st, pad, None),
+            "dgrad": lambda: iconv._conv_dgrad(dy, w16, geo, None),
+            "wgrad": lambda: iconv._conv_wgrad(dy, xc, w, geo),
         }
         rec = dict(x=list(xs), cout=co, k=r, stride=st, count=cnt)
-        for d, ms in t.items():
-            rec[f"{d}_us"] = round(ms * 1e3, 1)
-            rec[f"{d}_tf"] = round(flops / (ms * 1e-3) / 1e12, 1)
-            total[d] += ms * cnt
+        ref = {}
+        for rep in range(2):  # interleaved rounds (one process): the second round is reported
+            for c in cfgs:
+                lib.rk_conv_set_cfg(c)
+                for d, fn in fns.items():
+                    ms = timed(fn)
+                    if rep == 1:
+                        rec[f"{d}_us_c{c}"] = round(ms * 1e3, 1)
+                        rec[f"{d}_tf_c{c}"] = round(flops / (ms * 1e-3) / 1e12, 1)
+                        total[(c, d)] += ms * cnt
+                    if a.check and rep == 0:
+                        out = fn()
+                        out = out[0] if isinstance(out, tuple) else out
+                        if c == cfgs[0]:
+                            ref[d] = out.float().clone()
+                        else:
+                            err = (out.float() - ref[d]).abs().max().item() / (ref[d].abs().max().item() + 1e-6)
+                            rec[f"{d}_relerr_c{c}"] = err
+        lib.rk_conv_set_cfg(cfgs[0])
         print(json.dumps(rec), flush=True)
-    print(json.dumps({"total_ms_per_step": {d: round(v, 3) for d, v in total.items()},
-                      "sum_ms": round(sum(total.values()), 3)}), flush=True)
+    for c in cfgs:
+        print(json.dumps({"cfg": c, "total_ms_per_step": {d: round(total[(c, d)], 3) for d in ("fwd", "dgrad", "wgrad")},
+                          "sum_ms": round(sum(total[(c, d)] for d in ("fwd", "dgrad", "wgrad")), 3)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -81,16 +81,16 @@ __device__ __forceinline__ void split_pixel(int m, const ConvGeom& cg, int& n, i
 }
 
 // Gathered row-image operand (forward / dgrad A): rows are grid pixels, k runs over (r, s, c).
-template <int R, int NW, int MODE>
+template <int R, int BK, int NW, int MODE>
 struct GatherRows {
-  static constexpr int BK = 64, NI = R * BK / (512 * NW);
+  static constexpr int NI = R * BK / (512 * NW), CPR = BK / 8;
   int nb[NI], h0[NI], w0[NI], coff[NI];
   bool mok[NI];
   __device__ __forceinline__ void init(const ConvGeom& cg, int row0, int M, int wid, int lane) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int q = (wid * NI + i) * 64 + lane;
-      const int r = q >> 3, c = q & 7;
+      const int r = q / CPR, c = q % CPR;
       const int m = row0 + r;
       mok[i] = m < M;
       const int mm = mok[i] ? m : 0;
@@ -126,16 +126,16 @@ struct GatherRows {
 // zero channels, one 16-byte chunk per pixel): a 64-deep k-tile spans 8 taps, so every chunk of a
 // row is its own tap, (k0 / 8 + chunk).  K = R*S*8 is padded to whole k-tiles: taps >= R*S (and
 // pixels outside the image) come from the zero page, the weights' pad columns are zero.
-template <int R, int NW>
+template <int R, int BK, int NW>
 struct GatherRowsC8 {
-  static constexpr int BK = 64, NI = R * BK / (512 * NW);
+  static constexpr int NI = R * BK / (512 * NW), CPR = BK / 8;
   int pix[NI], h0[NI], w0[NI], j[NI];
   bool mok[NI];
   __device__ __forceinline__ void init(const ConvGeom& cg, int row0, int M, int wid, int lane) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int q = (wid * NI + i) * 64 + lane;
-      const int r = q >> 3, c = q & 7;
+      const int r = q / CPR, c = q % CPR;
       const int m = row0 + r;
       mok[i] = m < M;
       const int mm = mok[i] ? m : 0;
@@ -165,9 +165,9 @@ struct GatherRowsC8 {
 };
 
 // Gathered K-major operand (wgrad B): k rows are output pixels, columns are (r, s, ci) chunks.
-template <int R, int NW>
+template <int R, int BK, int NW>
 struct GatherCols {
-  static constexpr int BK = 64, NI = R * BK / (512 * NW), CPR = R / 8;
+  static constexpr int NI = R * BK / (512 * NW), CPR = R / 8;
   int krow[NI], tr[NI], ts[NI], ci[NI];
   bool cok[NI];
   __device__ __forceinline__ void init(const ConvGeom& cg, int col0, int Ncols, int wid, int lane) {
@@ -387,9 +387,11 @@ struct ClsRow {
 };
 
 // H: fp16 operands (MFMA f16; storage / rounding by g.c_dt), else bf16
-template <int MODE, int BM, int BN, int WM, int WN, bool H>
-__global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MArgs g, const ConvGeom cg0) {
-  constexpr int BK = 64, NS = 2, NW = WM * WN;
+// BK x NS: k-tile depth x LDS ring slots (NS - 1 k-tiles in flight while one is consumed); OCC:
+// resident blocks per CU the register budget is sized for
+template <int MODE, int BM, int BN, int WM, int WN, bool H, int BK = 64, int NS = 2, int OCC = 2>
+__global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(MArgs g, const ConvGeom cg0) {
+  constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16, KK = BK / 32;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
@@ -397,6 +399,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
   constexpr bool FWD = MODE == kConvFwd || MODE == kConvFwdC8;
   constexpr bool AK = MODE == kConvWgrad;   // A K-major (dY read pixel-major)
   constexpr bool BKM = !FWD;                // B K-major (dgrad: W per tap; wgrad: gathered X)
+  constexpr int NL = (BM + BN) * BK / (512 * NW);  // LDS-DMA instructions per wave per k-tile
+  static_assert(NS * STAGE_BYTES >= (BM / WM) * (BN + 4) * 4, "the LDS epilogue image fits in the ring");
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE_BYTES];
 
   int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -440,12 +444,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // operand stagers per mode
-  GatherRows<BM, NW, MODE == kConvFwd ? kConvFwd : kConvDgrad> ga;  // fwd/dgrad A
-  GatherRowsC8<BM, NW> ga8;                                            // stem fwd A (C = 8)
+  GatherRows<BM, BK, NW, MODE == kConvFwd ? kConvFwd : kConvDgrad> ga;  // fwd/dgrad A
+  GatherRowsC8<BM, BK, NW> ga8;                                            // stem fwd A (C = 8)
   Stager<BM, BK, true, NW> sa_k;                                      // wgrad A (dY K-major)
   Stager<BN, BK, false, NW> sb_row;                                    // fwd B (W rows)
   Stager<BN, BK, true, NW> sb_k;                                       // dgrad B (W per tap)
-  GatherCols<BN, NW> gb;                                               // wgrad B
+  GatherCols<BN, BK, NW> gb;                                           // wgrad B
   if constexpr (MODE == kConvWgrad) {
     sa_k.init(g.lda, row0, g.M, wid, lane);
     gb.init(cg, col0, g.N, wid, lane);
@@ -495,12 +499,18 @@ __global__ void __launch_bounds__(64 * WM * WN, 2 * WM * WN / 4) conv_kernel(MAr
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = __builtin_bit_cast(__bf16, (uint16_t)(H ? 0x3C00u : 0x3F80u));
 
-  if (nt > 0) issue(0);
+  // prologue: NS - 1 k-tiles in flight
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nt) issue(t);
   for (int t = 0; t < nt; ++t) {
-    wait_vm(0);
+    // tile t has landed once at most the tiles issued after it (up to t + NS - 2) are outstanding
+    wait_vm((min(nt - 1, t + NS - 2) - t) * NL);
+    // every wave's share of tile t is in LDS and every wave has consumed tile t - 1: refill its
+    // slot with tile t + NS - 1
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 1 < nt) issue(t + 1);
+    if (t + NS - 1 < nt) issue(t + NS - 1);
     const char* As = smem + (t % NS) * STAGE_BYTES;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -577,22 +587,39 @@ int conv_tiles(const MArgs& g, const ConvGeom& cg, int bm, int bn) {
   return ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn);
 }
 
-template <int MODE, bool H>
-int launch_conv_t(const MArgs& g, ConvGeom cg, hipStream_t s) {
+int g_conv_cfg = 0;  // rk_conv_set_cfg: k-tile pipeline of the bf16 kernels
+
+template <int MODE, bool H, int BK, int NS, int OCC, int WN128 = 4>
+int launch_conv_p(const MArgs& g, const ConvGeom& cg, hipStream_t s) {
   // (the forward's wave row slice is 64 pixels in every variant: the BatchNorm partials rely on it)
   // 64-wide GEMM side (Cout / Cin = 64 layers): a 64-wide tile with 4 waves instead of half an
   // empty 128-wide one; everything else 128 x 128 with 8 waves
   if (MODE != kConvWgrad && g.N <= 64) {
     const int tiles = conv_tiles<MODE>(g, cg, 128, 64);
-    conv_kernel<MODE, 128, 64, 2, 2, H><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+    conv_kernel<MODE, 128, 64, 2, 2, H, BK, NS, OCC><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
   } else if (MODE == kConvWgrad && g.M <= 64) {
     const int tiles = ((g.M + 63) / 64) * ((g.N + 127) / 128);
-    conv_kernel<MODE, 64, 128, 2, 2, H><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+    conv_kernel<MODE, 64, 128, 2, 2, H, BK, NS, OCC><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
   } else {
     const int tiles = conv_tiles<MODE>(g, cg, 128, 128);
-    conv_kernel<MODE, 128, 128, 2, 4, H><<<tiles * g.splitk, 512, 0, s>>>(g, cg);
+    conv_kernel<MODE, 128, 128, 2, WN128, H, BK, NS, OCC><<<tiles * g.splitk, 128 * WN128, 0, s>>>(g, cg);
   }
   return (int)hipGetLastError();
+}
+
+template <int MODE, bool H>
+int launch_conv_t(const MArgs& g, ConvGeom cg, hipStream_t s) {
+  if constexpr (!H) {
+    switch (g_conv_cfg) {
+      case 1: return launch_conv_p<MODE, H, 64, 3, 1>(g, cg, s);
+      case 2: return launch_conv_p<MODE, H, 32, 4, 2>(g, cg, s);
+      case 3: return launch_conv_p<MODE, H, 32, 3, 3>(g, cg, s);
+      case 4: return launch_conv_p<MODE, H, 64, 2, 2, 2>(g, cg, s);
+      case 5: return launch_conv_p<MODE, H, 32, 3, 3, 2>(g, cg, s);
+      default: break;
+    }
+  }
+  return launch_conv_p<MODE, H, 64, 2, 2>(g, cg, s);
 }
 // operand dtype dt: BF16 or F16 (anything else is refused by the entry points)
 template <int MODE>
@@ -699,6 +726,15 @@ RK_API int rk_pad_c8(const void* x, void* y, int N, int C, int H, int W, int64_t
 // chunks; 0: straight from the MFMA accumulator layout (A/B switch, ROCKET_CONV_LDS_EPI)
 RK_API int rk_conv_set_lds_epi(int on) {
   g_lds_epi = on != 0;
+  return 0;
+}
+
+// k-tile pipeline of the bf16 conv kernels: 0 = 64-deep k-tiles, 2-slot ring, 2 blocks/CU;
+// 1 = 64-deep, 3 slots, 1 block/CU; 2 = 32-deep, 4 slots, 2 blocks/CU; 3 = 32-deep, 3 slots, 3 blocks/CU;
+// 4 / 5 = 0 / 3 with 4-wave 128 x 128 tiles (64 x 64 per wave: half the LDS reads per MFMA)
+RK_API int rk_conv_set_cfg(int cfg) {
+  if (cfg < 0 || cfg > 5) return (int)hipErrorInvalidValue;
+  g_conv_cfg = cfg;
   return 0;
 }
 

@@ -47,6 +47,7 @@ KERNEL_SIGS = {
     "rk_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_int64, c_int] + [c_void_p] * 9 + [c_float, c_float, c_void_p,
                                                                                             c_void_p, c_void_p]),
     "rk_conv_set_lds_epi": (c_int, [c_int]),
+    "rk_conv_set_cfg": (c_int, [c_int]),
     "rk_mlp3_set_trace": (None, [c_void_p]),
     "rk_conv_dgrad_bn": (c_int, [c_int] + [c_void_p] * 3 + [c_int] * 9 + [c_void_p] * 6),
     "rk_bn_bwd_partials": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_int] + [c_void_p] * 11),

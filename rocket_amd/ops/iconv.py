@@ -42,6 +42,8 @@ N_SLOTS = 512  # resident 128x128 conv blocks (2 per CU)
 # bf16 conv outputs / input gradients stored through LDS in row-contiguous chunks (conv.hip
 # store_tile_lds); ROCKET_CONV_LDS_EPI=0 stores straight from the MFMA accumulator layout
 LDS_EPI = os.environ.get("ROCKET_CONV_LDS_EPI", "1") != "0"
+# k-tile pipeline of the bf16 conv kernels (conv.hip rk_conv_set_cfg)
+PIPE = int(os.environ.get("ROCKET_CONV_PIPE", "0"))
 _epi_set = False
 
 
@@ -50,6 +52,8 @@ def _kernels():
     lib = _lib.kernels()
     if not _epi_set:
         lib.rk_conv_set_lds_epi(int(LDS_EPI))
+        if lib.rk_conv_set_cfg(PIPE):
+            raise ValueError(f"ROCKET_CONV_PIPE={PIPE}: no such conv pipeline")
         _epi_set = True
     return lib
 
