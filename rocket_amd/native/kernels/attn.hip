@@ -81,12 +81,27 @@ __device__ __forceinline__ bf16x8 gload_row(const uint16_t* base, int ld, int b,
 // element offset of 8-element chunk ch of row r in a swizzled [LMAX][64] image (header comment)
 __device__ __forceinline__ int eoff(int r, int ch) { return r * RS + ((ch ^ (((r >> 1) & 3) << 1)) << 3); }
 
-// stage a head's tokens row-major into [LMAX][RS] (zero rows >= L)
+// stage a head's tokens of two tensors row-major into [LMAX][RS] images (zero rows >= L): every
+// thread issues all of its 16-byte loads before its first LDS write, so the block waits for one
+// memory round trip instead of one per loop iteration
 template <int NTH>
-__device__ __forceinline__ void stage_rows(uint16_t* dst, const uint16_t* src, int ld, int b, int L, int h) {
-  for (int i = threadIdx.x; i < LMAX * (D / 8); i += NTH) {
-    const int r = i >> 3, ch = i & 7;
-    *(bf16x8*)(dst + eoff(r, ch)) = gload_row(src, ld, b, L, r, h, ch * 8);
+__device__ __forceinline__ void stage_rows2(uint16_t* d0, const uint16_t* s0, int ld0, uint16_t* d1,
+                                            const uint16_t* s1, int ld1, int b, int L, int h) {
+  constexpr int N = LMAX * (D / 8), IT = (N + NTH - 1) / NTH;
+  bf16x8 v0[IT], v1[IT];
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    const int i = min((int)threadIdx.x + u * NTH, N - 1);
+    v0[u] = gload_row(s0, ld0, b, L, i >> 3, h, (i & 7) * 8);
+    v1[u] = gload_row(s1, ld1, b, L, i >> 3, h, (i & 7) * 8);
+  }
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    const int i = (int)threadIdx.x + u * NTH;
+    if (i < N) {
+      *(bf16x8*)(d0 + eoff(i >> 3, i & 7)) = v0[u];
+      *(bf16x8*)(d1 + eoff(i >> 3, i & 7)) = v1[u];
+    }
   }
 }
 
@@ -145,8 +160,10 @@ __global__ void __launch_bounds__(NTH, MINW) attn_fwd_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
   const int L = a.L;
   const int ntile = (L + 15) / 16;
-  stage_rows<NTH>(Ks, a.k, a.ld, b, L, h);
-  stage_rows<NTH>(Vs, a.v, a.ld, b, L, h);
+  bf16x8 qn[2];  // this wave's first query tile, loaded with the K/V staging
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) qn[ks] = gload_row(a.q, a.ld, b, L, 16 * w + lo, h, 32 * ks + 8 * hi);
+  stage_rows2<NTH>(Ks, a.k, a.ld, Vs, a.v, a.ld, b, L, h);
   __syncthreads();
 
   const float sl = a.scale * LOG2E;
@@ -155,7 +172,11 @@ __global__ void __launch_bounds__(NTH, MINW) attn_fwd_kernel(AttnArgs a) {
     const int q0 = 16 * qt;
     bf16x8 qb[2];  // B operand of S^T = K Q^T: n = query q0 + lo, k = d 32ks + 8hi + j
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qb[ks] = gload_row(a.q, a.ld, b, L, q0 + lo, h, 32 * ks + 8 * hi);
+    for (int ks = 0; ks < 2; ++ks) qb[ks] = qn[ks];
+    if (qt + NTH / 64 < ntile) {  // the next tile's Q: in flight under this tile's products
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) qn[ks] = gload_row(a.q, a.ld, b, L, q0 + 16 * (NTH / 64) + lo, h, 32 * ks + 8 * hi);
+    }
     f32x4 s[NT];
     float m = -INFINITY;
 #pragma unroll
@@ -219,8 +240,7 @@ __global__ void __launch_bounds__(NTH, MINW) attn_bwd_q_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
   const int L = a.L;
   const int ntile = (L + 15) / 16;
-  stage_rows<NTH>(Ks, a.k, a.ld, b, L, h);
-  stage_rows<NTH>(Vs, a.v, a.ld, b, L, h);
+  stage_rows2<NTH>(Ks, a.k, a.ld, Vs, a.v, a.ld, b, L, h);
   __syncthreads();
 
   const float sl = a.scale * LOG2E;
@@ -299,8 +319,7 @@ __global__ void __launch_bounds__(NTH, MINW) attn_bwd_kv_kernel(AttnArgs a) {
   const int L = a.L;
   const int ntile = (L + 15) / 16;
   const int64_t bh = (int64_t)b * a.H + h;
-  stage_rows<NTH>(Qs, a.q, a.ld, b, L, h);
-  stage_rows<NTH>(Gs, a.dout, a.ldo, b, L, h);
+  stage_rows2<NTH>(Qs, a.q, a.ld, Gs, a.dout, a.ldo, b, L, h);
   for (int i = threadIdx.x; i < LMAX; i += NTH) {
     lse_s[i] = i < L ? a.lse[bh * L + i] : 0.f;
     del_s[i] = i < L ? a.delta[bh * L + i] : 0.f;
@@ -400,26 +419,46 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
   // stamps[block * 4 + 1..3] (staged, chunk loop done, end; bench/attn_probe.py)
   float* stamp = (a.stamps != nullptr && threadIdx.x == 0) ? a.stamps + (int64_t)bh * 4 : nullptr;
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-  for (int i = threadIdx.x; i < LMAX * (D / 8); i += nthr) {  // 8 consecutive threads = one row
-    const int r = i >> 3, ch = i & 7;
-    *(bf16x8*)(Qs + eoff(r, ch)) = gload_row(a.q, a.ld, b, L, r, h, ch * 8);
-    *(bf16x8*)(Ks + eoff(r, ch)) = gload_row(a.k, a.ld, b, L, r, h, ch * 8);
-    const bf16x8 gv = gload_row(a.dout, a.ldo, b, L, r, h, ch * 8);
-    const bf16x8 ov = gload_row(a.o, a.ldo, b, L, r, h, ch * 8);
-    *(bf16x8*)(Gs + eoff(r, ch)) = gv;
-    const uint4 gu = __builtin_bit_cast(uint4, gv), ou = __builtin_bit_cast(uint4, ov);
-    const uint32_t gw[4] = {gu.x, gu.y, gu.z, gu.w}, ow[4] = {ou.x, ou.y, ou.z, ou.w};
-    float dot = 0.f;
+  // 8 consecutive threads = one row; a pass issues the 16-byte loads of SU rows-chunks per thread
+  // (Q, K, dO, O) before any LDS write: one memory round trip per pass (one pass at L = 197)
+  constexpr int SU = 3;
+  for (int i0 = threadIdx.x; i0 < LMAX * (D / 8); i0 += SU * nthr) {
+    bf16x8 qv[SU], kv[SU], gv[SU], ov[SU];
+    float lv[SU];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      dot += __uint_as_float(gw[e] << 16) * __uint_as_float(ow[e] << 16) +
-             __uint_as_float(gw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
-    dot += __shfl_xor(dot, 1, 64);
-    dot += __shfl_xor(dot, 2, 64);
-    dot += __shfl_xor(dot, 4, 64);
-    if (ch == 0) {
-      del_s[r] = dot;
-      lse_s[r] = r < L ? a.lse[bh * L + r] : 0.f;
+    for (int u = 0; u < SU; ++u) {
+      const int i = min(i0 + u * nthr, LMAX * (D / 8) - 1);
+      const int r = i >> 3, c = (i & 7) * 8;
+      lv[u] = a.lse[bh * L + min(r, L - 1)];
+      qv[u] = gload_row(a.q, a.ld, b, L, r, h, c);
+      kv[u] = gload_row(a.k, a.ld, b, L, r, h, c);
+      gv[u] = gload_row(a.dout, a.ldo, b, L, r, h, c);
+      ov[u] = gload_row(a.o, a.ldo, b, L, r, h, c);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int i = i0 + u * nthr;
+      const int r = i >> 3, ch = i & 7;
+      const bool in = i < LMAX * (D / 8);  // uniform per 8-thread row group (nthr % 64 == 0)
+      if (in) {
+        *(bf16x8*)(Qs + eoff(r, ch)) = qv[u];
+        *(bf16x8*)(Ks + eoff(r, ch)) = kv[u];
+        *(bf16x8*)(Gs + eoff(r, ch)) = gv[u];
+      }
+      const uint4 gu = __builtin_bit_cast(uint4, gv[u]), ou = __builtin_bit_cast(uint4, ov[u]);
+      const uint32_t gw[4] = {gu.x, gu.y, gu.z, gu.w}, ow[4] = {ou.x, ou.y, ou.z, ou.w};
+      float dot = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        dot += __uint_as_float(gw[e] << 16) * __uint_as_float(ow[e] << 16) +
+               __uint_as_float(gw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+      dot += __shfl_xor(dot, 1, 64);
+      dot += __shfl_xor(dot, 2, 64);
+      dot += __shfl_xor(dot, 4, 64);
+      if (in && ch == 0) {
+        del_s[r] = dot;
+        lse_s[r] = r < L ? lv[u] : 0.f;
+      }
     }
   }
   // the dS rows of a key tile without a wave (odd ntile: the last 32-key step's upper half) are

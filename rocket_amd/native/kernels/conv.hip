@@ -81,42 +81,57 @@ __device__ __forceinline__ void split_pixel(int m, const ConvGeom& cg, int& n, i
 }
 
 // Gathered row-image operand (forward / dgrad A): rows are grid pixels, k runs over (r, s, c).
+// A lane's rows are fixed for the whole block, only the k-tile's tap (r, s) and channel offset c0
+// change (wave-uniform): so the per-lane work of a k-tile is one pointer add of a scalar offset, a
+// bit test in the lane's precomputed tap-validity mask (R*S <= 32 taps, host-checked) and a select
+// — no per-k-tile multiplies, 64-bit index math or branches around the DMAs.
 template <int R, int BK, int NW, int MODE>
 struct GatherRows {
   static constexpr int NI = R * BK / (512 * NW), CPR = BK / 8;
-  int nb[NI], h0[NI], w0[NI], coff[NI];
-  bool mok[NI];
-  __device__ __forceinline__ void init(const ConvGeom& cg, int row0, int M, int wid, int lane) {
+  const char* p0[NI];  // the lane's chunk at tap (0, 0), c0 = 0 (may point outside x: never read then)
+  uint32_t vmask[NI];  // bit r*S + s: tap (r, s) inside the image, and the row inside M
+  __device__ __forceinline__ void init(const uint16_t* x, const ConvGeom& cg, int row0, int M, int wid, int lane) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int q = (wid * NI + i) * 64 + lane;
       const int r = q / CPR, c = q % CPR;
       const int m = row0 + r;
-      mok[i] = m < M;
-      const int mm = mok[i] ? m : 0;
+      const int mm = m < M ? m : 0;
       const int gw = mm % cg.GW, t = mm / cg.GW;
       const int gh = t % cg.GH, n = t / cg.GH;
-      nb[i] = n * cg.H;
+      int h0, w0;
       if (MODE == kConvFwd) {
-        h0[i] = gh * cg.stride - cg.pad;
-        w0[i] = gw * cg.stride - cg.pad;
+        h0 = gh * cg.stride - cg.pad;
+        w0 = gw * cg.stride - cg.pad;
       } else {  // dgrad (stride 1: hoff = woff = pad; strided: per parity class)
-        h0[i] = gh + cg.hoff;
-        w0[i] = gw + cg.woff;
+        h0 = gh + cg.hoff;
+        w0 = gw + cg.woff;
       }
-      coff[i] = (c ^ rswz<BK>(r)) * 8;
+      const int64_t e = ((int64_t)(n * cg.H + h0) * cg.W + w0) * cg.C + (c ^ rswz<BK>(r)) * 8;
+      p0[i] = (const char*)x + e * 2;
+      uint32_t v = 0;
+      if (m < M) {
+        for (int tr = 0; tr < cg.R; ++tr)
+          for (int ts = 0; ts < cg.S; ++ts) {
+            const int h = MODE == kConvFwd ? h0 + tr : h0 - tr;
+            const int w = MODE == kConvFwd ? w0 + ts : w0 - ts;
+            if ((unsigned)h < (unsigned)cg.H && (unsigned)w < (unsigned)cg.W) v |= 1u << (tr * cg.S + ts);
+          }
+      }
+      vmask[i] = v;
     }
   }
   // k-tile at tap (tr, ts), channel offset c0
-  __device__ __forceinline__ void issue(const uint16_t* x, const ConvGeom& cg, int tr, int ts, int c0, char* lds,
-                                        int wid, const char* zero) const {
+  __device__ __forceinline__ void issue(const ConvGeom& cg, int tr, int ts, int c0, char* lds, int wid,
+                                        const char* zero) const {
+    // wave-uniform byte offset of (tr, ts, c0) from tap (0, 0)
+    const int64_t tap_off = (int64_t)(tr * cg.W + ts) * cg.C;
+    const int64_t soff = ((MODE == kConvFwd ? tap_off : -tap_off) + c0) * 2;
+    const int bit = tr * cg.S + ts;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int h = MODE == kConvFwd ? h0[i] + tr : h0[i] - tr;
-      const int w = MODE == kConvFwd ? w0[i] + ts : w0[i] - ts;
-      const bool ok = mok[i] && (unsigned)h < (unsigned)cg.H && (unsigned)w < (unsigned)cg.W;
-      const int64_t e = ((int64_t)(nb[i] + h) * cg.W + w) * cg.C + c0 + coff[i];
-      const char* src = ok ? (const char*)(x + e) : zero;
+      const bool ok = (vmask[i] >> bit) & 1u;
+      const char* src = ok ? p0[i] + soff : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0, 0);
     }
   }
@@ -165,39 +180,82 @@ struct GatherRowsC8 {
 };
 
 // Gathered K-major operand (wgrad B): k rows are output pixels, columns are (r, s, ci) chunks.
+// A lane's column (tap, channel chunk) is fixed for the block and its k row moves by BK pixels per
+// k-tile (the tiles of a split are issued in order): the pixel's (n, oh, ow) digits, its window
+// position and its element offset are carried from k-tile to k-tile by mixed-radix increments with
+// wave-uniform deltas — adds, compares and selects only, no per-k-tile divisions or multiplies.
 template <int R, int BK, int NW>
 struct GatherCols {
   static constexpr int NI = R * BK / (512 * NW), CPR = R / 8;
-  int krow[NI], tr[NI], ts[NI], ci[NI];
+  int m[NI], oh[NI], ow[NI], hs[NI], ws[NI];  // pixel, its output row / col, window row / col + tap
+  int64_t e[NI];                              // element offset of the lane's chunk at that pixel
   bool cok[NI];
-  __device__ __forceinline__ void init(const ConvGeom& cg, int col0, int Ncols, int wid, int lane) {
+  // per-k-tile increments (wave-uniform): BK pixels = qn images + qh rows + qw columns
+  int qw, qh, qn;
+  int64_t d_w, d_wc, d_h, d_hc, d_n;
+  __device__ __forceinline__ void init(const ConvGeom& cg, int col0, int Ncols, int kb, int wid, int lane) {
+    const int st = cg.stride;
+    qw = BK % cg.GW;
+    qh = (BK / cg.GW) % cg.GH;
+    qn = BK / (cg.GW * cg.GH);
+    d_w = (int64_t)qw * st * cg.C;                              // ow += qw
+    d_wc = ((int64_t)st * cg.W - (int64_t)cg.GW * st) * cg.C;   // ow wraps: next output row
+    d_h = (int64_t)qh * st * cg.W * cg.C;                       // oh += qh
+    d_hc = ((int64_t)cg.H - (int64_t)cg.GH * st) * cg.W * cg.C; // oh wraps: next image
+    d_n = (int64_t)qn * cg.H * cg.W * cg.C;                     // n += qn
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int q = (wid * NI + i) * 64 + lane;
       const int k = q / CPR, c = q % CPR;
-      krow[i] = k;
       const int col = col0 + (c ^ kswz<R>(k)) * 8;
       cok[i] = col < Ncols;
       const int cc = cok[i] ? col : 0;
       const int tap = cc / cg.C;
-      ci[i] = cc - tap * cg.C;
-      tr[i] = tap / cg.S;
-      ts[i] = tap - tr[i] * cg.S;
+      const int ci = cc - tap * cg.C;
+      const int tr = tap / cg.S, ts = tap - tr * cg.S;
+      m[i] = kb + k;
+      int n, h, w;
+      split_pixel(m[i], cg, n, h, w);
+      oh[i] = h;
+      ow[i] = w;
+      hs[i] = h * st - cg.pad + tr;
+      ws[i] = w * st - cg.pad + ts;
+      e[i] = ((int64_t)(n * cg.H + hs[i]) * cg.W + ws[i]) * cg.C + ci;
     }
   }
-  __device__ __forceinline__ void issue(const uint16_t* x, const ConvGeom& cg, int k0, int kend, char* lds, int wid,
-                                        const char* zero) const {
+  // the current k-tile (rows m .. of every lane), then advance every lane's row by BK pixels
+  __device__ __forceinline__ void issue(const uint16_t* x, const ConvGeom& cg, int kend, char* lds, int wid,
+                                        const char* zero) {
+    const int st = cg.stride;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int m = k0 + krow[i];
-      int n, oh, ow;
-      split_pixel(min(m, kend - 1), cg, n, oh, ow);
-      const int h = oh * cg.stride - cg.pad + tr[i];
-      const int w = ow * cg.stride - cg.pad + ts[i];
-      const bool ok = cok[i] && m < kend && (unsigned)h < (unsigned)cg.H && (unsigned)w < (unsigned)cg.W;
-      const int64_t e = ((int64_t)(n * cg.H + h) * cg.W + w) * cg.C + ci[i];
-      const char* src = ok ? (const char*)(x + e) : zero;
+      const bool ok = cok[i] && m[i] < kend && (unsigned)hs[i] < (unsigned)cg.H && (unsigned)ws[i] < (unsigned)cg.W;
+      const char* src = ok ? (const char*)(x + e[i]) : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      m[i] += BK;
+      int w = ow[i] + qw, h = oh[i] + qh;
+      int64_t ee = e[i] + d_w + d_h + d_n;
+      int hh = hs[i] + qh * st, ww = ws[i] + qw * st;
+      if (w >= cg.GW) {  // column carry into the row digit
+        w -= cg.GW;
+        ++h;
+        ee += d_wc;
+        ww -= cg.GW * st;
+        hh += st;
+      }
+      if (h >= cg.GH) {  // row carry into the image digit
+        h -= cg.GH;
+        ee += d_hc;
+        hh -= cg.GH * st;
+      }
+      ow[i] = w;
+      oh[i] = h;
+      hs[i] = hh;
+      ws[i] = ww;
+      e[i] = ee;
     }
   }
 };
@@ -452,12 +510,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(M
   GatherCols<BN, BK, NW> gb;                                           // wgrad B
   if constexpr (MODE == kConvWgrad) {
     sa_k.init(g.lda, row0, g.M, wid, lane);
-    gb.init(cg, col0, g.N, wid, lane);
+    gb.init(cg, col0, g.N, kb, wid, lane);
   } else if constexpr (MODE == kConvFwdC8) {
     ga8.init(cg, row0, g.M, wid, lane);
     sb_row.init(g.ldb, col0, g.N, wid, lane);
   } else {
-    ga.init(cg, row0, g.M, wid, lane);
+    ga.init(g.a, cg, row0, g.M, wid, lane);
     if constexpr (MODE == kConvFwd) sb_row.init(g.ldb, col0, g.N, wid, lane);
     else sb_k.init(g.ldb, col0, g.N, wid, lane);
   }
@@ -468,14 +526,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(M
     if constexpr (MODE == kConvWgrad) {
       if (k0 + BK <= ke) sa_k.issue((const char*)g.a + (int64_t)k0 * g.lda * 2, buf, wid);
       else sa_k.issue_tail((const char*)g.a + (int64_t)k0 * g.lda * 2, buf, wid, lane, ke - k0, zero);
-      gb.issue(g.b, cg, k0, ke, buf + A_BYTES, wid, zero);
+      gb.issue(g.b, cg, ke, buf + A_BYTES, wid, zero);  // k-tiles are issued in order: its rows are k0..
     } else if constexpr (MODE == kConvFwdC8) {
       ga8.issue(g.a, cg, k0, buf, wid, zero);
       sb_row.issue((const char*)g.b + (int64_t)k0 * 2, buf + A_BYTES, wid);
     } else {
       const int tap = k0 / cg.taps_c, c0 = k0 - tap * cg.taps_c;
       const int tr = tap / cg.S, ts = tap - tr * cg.S;
-      ga.issue(g.a, cg, tr, ts, c0, buf, wid, zero);
+      ga.issue(cg, tr, ts, c0, buf, wid, zero);
       if constexpr (MODE == kConvFwd)
         sb_row.issue((const char*)g.b + (int64_t)k0 * 2, buf + A_BYTES, wid);
       else {  // W[co][tap][ci]: k-tile rows co = c0.., columns ci (strided: the class's tap (j, l))
@@ -659,14 +717,14 @@ int g_lds_epi = 1;  // rk_conv_set_lds_epi
 // in that format (MFMA bf16 / f16, f32 accumulation).
 static bool dt_ok(int dt) { return dt == BF16 || dt == F16; }
 
-// Y[N*OH*OW][Cout] (dt or f32) = conv(X, W) (+ bias[Cout]).  Cin % 64 == 0, Cout % 8 == 0.
+// Y[N*OH*OW][Cout] (dt or f32) = conv(X, W) (+ bias[Cout]).  Cin % 64 == 0, Cout % 8 == 0, R*S <= 32.
 // bnpart (optional): f32 [ceil(N*OH*OW / 64)][2][Cout] per 64-pixel slice (sum, sum of squares)
 // BatchNorm partials for rk_bn_finalize.
 RK_API int rk_conv_fwd(int dt, const void* x, const void* w, void* y, int y_dt, const float* bias, int N, int H, int W,
                        int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, float* bnpart,
                        hipStream_t s) {
   if (!dt_ok(dt) || (y_dt != F32 && y_dt != dt)) return (int)hipErrorInvalidValue;
-  if (Cin % 64 || Cout % 8 || !aligned16(x) || !aligned16(w) || !aligned16(y)) return (int)hipErrorInvalidValue;
+  if (Cin % 64 || Cout % 8 || R * S > 32 || !aligned16(x) || !aligned16(w) || !aligned16(y)) return (int)hipErrorInvalidValue;
   if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW, K = R * S * Cin;
   MArgs g = margs(x, 0, w, K, y, y_dt, Cout, M, Cout, K);
@@ -745,7 +803,7 @@ RK_API int rk_conv_set_cfg(int cfg) {
 RK_API int rk_conv_dgrad_bn(int dt, const void* dy, const void* w, void* dx, int accumulate, int N, int H, int W,
                             int Cin, int Cout, int R, int S, int pad, const void* bn_x, const void* bn_mask,
                             const float* mean, const float* invstd, float* part, hipStream_t s) {
-  if (!dt_ok(dt) || Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx) || !aligned16(bn_x) || !part ||
+  if (!dt_ok(dt) || Cout % 64 || Cin % 8 || R * S > 32 || !aligned16(dy) || !aligned16(w) || !aligned16(dx) || !aligned16(bn_x) || !part ||
       !aligned16(mean) || !aligned16(invstd) || !aligned16(part))
     return (int)hipErrorInvalidValue;
   const int OH = H + 2 * pad - R + 1, OW = W + 2 * pad - S + 1;
@@ -767,7 +825,7 @@ RK_API int rk_conv_dgrad_bn(int dt, const void* dy, const void* w, void* dx, int
 RK_API int rk_conv_dgrad(int dt, const void* dy, const void* w, void* dx, int dx_dt, int accumulate, int N, int H,
                          int W, int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, hipStream_t s) {
   if (!dt_ok(dt) || (dx_dt != F32 && dx_dt != dt)) return (int)hipErrorInvalidValue;
-  if ((stride != 1 && stride != 2) || Cout % 64 || Cin % 8 || !aligned16(dy) || !aligned16(w) || !aligned16(dx))
+  if ((stride != 1 && stride != 2) || Cout % 64 || Cin % 8 || R * S > 32 || !aligned16(dy) || !aligned16(w) || !aligned16(dx))
     return (int)hipErrorInvalidValue;
   if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
   const int M = N * H * W, K = R * S * Cout;

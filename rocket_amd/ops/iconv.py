@@ -321,6 +321,7 @@ def native_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     return (MODE == "native" and x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") in _LOWP
             and conv.groups == 1 and conv.dilation == (1, 1) and conv.bias is None
             and conv.in_channels % 64 == 0 and conv.out_channels % 8 == 0 and conv.stride[0] == conv.stride[1]
+            and conv.kernel_size[0] * conv.kernel_size[1] <= 32  # conv.hip gathers: tap-validity bit masks
             and conv.padding[0] == conv.padding[1] and isinstance(conv.padding[0], int)
             and conv.weight.dtype == torch.float32 and _lib.available())
 
