@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--cfgs", default="0", help="conv pipelines to A/B (rk_conv_set_cfg), e.g. 0,1,2,3")
     ap.add_argument("--check", action="store_true", help="compare every pipeline's outputs with pipeline 0's")
+    ap.add_argument("--only", default="", help="shapes to run, e.g. 'c128h16k3s1,c64h32k3s1' (Cin, H, kernel, stride)")
+    ap.add_argument("--dirs", default="fwd,dgrad,wgrad")
     a = ap.parse_args()
     cfgs = [int(c) for c in a.cfgs.split(",")]
     from rocket_amd import models
@@ -64,6 +66,8 @@ def main():
     total = collections.Counter()
     for (xs, co, r, st, pad), cnt in sorted(shapes.items(), key=lambda kv: -kv[1]):
         N, C, H, W = xs
+        if a.only and f"c{C}h{H}k{r}s{st}" not in a.only.split(","):
+            continue
         xc = torch.randn(xs, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
         w = torch.randn(co, C, r, r, device=dev).contiguous(memory_format=torch.channels_last)
         w16 = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -77,6 +81,7 @@ def main():
             "dgrad": lambda: iconv._conv_dgrad(dy, w16, geo, None),
             "wgrad": lambda: iconv._conv_wgrad(dy, xc, w, geo),
         }
+        fns = {d: f for d, f in fns.items() if d in a.dirs.split(",")}
         rec = dict(x=list(xs), cout=co, k=r, stride=st, count=cnt)
         ref = {}
         for rep in range(2):  # interleaved rounds (one process): the second round is reported
@@ -99,8 +104,8 @@ def main():
         lib.rk_conv_set_cfg(cfgs[0])
         print(json.dumps(rec), flush=True)
     for c in cfgs:
-        print(json.dumps({"cfg": c, "total_ms_per_step": {d: round(total[(c, d)], 3) for d in ("fwd", "dgrad", "wgrad")},
-                          "sum_ms": round(sum(total[(c, d)] for d in ("fwd", "dgrad", "wgrad")), 3)}), flush=True)
+        print(json.dumps({"cfg": c, "total_ms_per_step": {d: round(total[(c, d)], 3) for d in ("fwd", "dgrad", "wgrad") if d in a.dirs.split(",")},
+                          "sum_ms": round(sum(total[(c, d)] for d in a.dirs.split(",")), 3)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(NTH, MINW) attn_fwd_kernel(AttnArgs a) {
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        s[t][i] = exp2f(s[t][i] - m);  // masked / absent keys: exp2(-inf) = 0
+        s[t][i] = __builtin_amdgcn_exp2f(s[t][i] - m);  // masked / absent keys: exp2(-inf) = 0
         sum += s[t][i];
       }
     sum = red4_sum(sum);
@@ -408,7 +408,8 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
   __shared__ __attribute__((aligned(16))) uint16_t Gs[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t dSs[2][LMAX * DSC];  // [key][query of the chunk]
-  __shared__ float lse_s[LMAX], del_s[LMAX];
+  __shared__ __attribute__((aligned(16))) float lse_s[LMAX];
+  __shared__ __attribute__((aligned(16))) float del_s[LMAX];
   const int b = blockIdx.z, h = blockIdx.y;
   const int nthr = blockDim.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
@@ -419,6 +420,12 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
   // stamps[block * 4 + 1..3] (staged, chunk loop done, end; bench/attn_probe.py)
   float* stamp = (a.stamps != nullptr && threadIdx.x == 0) ? a.stamps + (int64_t)bh * 4 : nullptr;
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  const int k0 = 16 * w;  // this wave's key tile (blockDim = 64 * ntile: every wave has one)
+  // its V fragments, loaded with the staging (retired by the staging barrier: no memory wait in
+  // the chunk loop, whose only memory operations are then the dQ stores)
+  bf16x8 vb[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) vb[ks] = gload_row(a.v, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
   // 8 consecutive threads = one row; a pass issues the 16-byte loads of SU rows-chunks per thread
   // (Q, K, dO, O) before any LDS write: one memory round trip per pass (one pass at L = 197)
   constexpr int SU = 3;
@@ -468,13 +475,9 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
   if (stamp) stamp[1] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
 
   const float sl = a.scale * LOG2E;
-  const int k0 = 16 * w;  // this wave's key tile (blockDim = 64 * ntile: every wave has one)
-  bf16x8 kb[2], vb[2];    // B operands of S = Q K^T / dP = dO V^T: n = key k0 + lo, k = d
+  bf16x8 kb[2];  // B operands of S = Q K^T / dP = dO V^T: n = key k0 + lo, k = d
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    kb[ks] = frag(Ks, k0 + lo, 4 * ks + hi);
-    vb[ks] = gload_row(a.v, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
-  }
+  for (int ks = 0; ks < 2; ++ks) kb[ks] = frag(Ks, k0 + lo, 4 * ks + hi);
   f32x4 dk[4], dv[4];  // C[row = key 4hi + i][col = d 16nt + lo]
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) dk[nt] = dv[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -495,11 +498,11 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
         dq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
             av, tr_operand(Ks, 32 * kq + 4 * hi, 32 * kq + 16 + 4 * hi, 16 * nt, lo), dq, 0, 0, 0);
       }
+      const int r0 = 32 * kc + 16 * qh + 4 * hi;  // C[row = query r0 + i][col = d lo]
+      uint16_t* dqp = a.dq + ((int64_t)b * L + r0) * a.ldg + h * D + 16 * nt + lo;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {  // C[row = query 4hi + i][col = d lo]
-        const int r = 32 * kc + 16 * qh + 4 * hi + i;
-        if (r < L) a.dq[((int64_t)b * L + r) * a.ldg + h * D + 16 * nt + lo] = f2bf(dq[i]);
-      }
+      for (int i = 0; i < 4; ++i)
+        if (r0 + i < L) dqp[(int64_t)i * a.ldg] = f2bf(dq[i]);
     }
   };
   int nchunks = 0;
@@ -520,13 +523,17 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
           dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Gs, 16 * qt + lo, 4 * kk + hi), vb[kk], dp, 0, 0, 0);
         }
       }
+      // the 4 queries' lse / delta as one 16-byte LDS read each (entries >= L are zero), the exp
+      // unconditional and masked by a select: no branch, no per-element LDS round trip
+      const int q4 = 16 * qt + 4 * hi;
+      const f32x4 lq = *(const f32x4*)(lse_s + q4), dq4 = *(const f32x4*)(del_s + q4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int qi = 16 * qt + 4 * hi + i;
-        const bool ok = qi < L && k0 + lo < L;
-        const float p = ok ? exp2f(sv[i] * sl - lse_s[qi]) : 0.f;
+        const bool ok = q4 + i < L && k0 + lo < L;
+        const float e = __builtin_amdgcn_exp2f(sv[i] * sl - lq[i]);
+        const float p = ok ? e : 0.f;
         p2[u][i] = p;
-        ds2[u][i] = p * (dp[i] - del_s[qi]) * a.scale;
+        ds2[u][i] = p * (dp[i] - dq4[i]) * a.scale;
       }
     }
     const bf16x8 pa = pack_operand(p2[0], p2[1]);  // A: row = key lo, k = the chunk's queries
@@ -547,7 +554,12 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
     // ---- B of the PREVIOUS chunk in the same barrier interval (its buffer was completed before
     // the previous barrier; the next chunk's A rewrites it only after the barrier below)
     if (ks > 0) phase_b(ks - 1);
-    __syncthreads();  // chunk ks's dS rows of every key tile are in
+    // chunk ks's dS rows of every key tile are in: wait for this wave's LDS traffic only, then the
+    // raw barrier — __syncthreads() would also wait (vmcnt(0)) for the dQ stores just issued, a
+    // memory round trip per chunk that nothing here depends on
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
   if (nchunks > 0) phase_b(nchunks - 1);
   if (stamp) stamp[2] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);

@@ -23,6 +23,7 @@ columns dropped.  ``ROCKET_CONV=native`` (default) | ``lib``.
 
 from __future__ import annotations
 
+import functools
 import os
 
 import torch
@@ -72,6 +73,7 @@ def _dt(t: torch.Tensor) -> int:
     return 2 if t.dtype == torch.float16 else 1
 
 
+@functools.lru_cache(maxsize=None)
 def _wgrad_split(cout: int, ncol: int, pixels: int) -> int:
     """K-split of a conv weight gradient (few output tiles, long pixel reduction): minimise
     modelled time = waves of resident blocks x per-block MFMA time + the split-K slab traffic
