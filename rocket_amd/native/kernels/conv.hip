@@ -309,6 +309,14 @@ __device__ __forceinline__ void tile_bn_stats(const MArgs& g, const ConvGeom& cg
   }
 }
 
+// Block barrier for LDS hand-offs only: waits for this wave's LDS operations, not for the tile's
+// global stores already issued (__syncthreads() would drain vmcnt: a memory round trip per slice)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Row-coalesced bf16 tile store through LDS (plain / accumulate, no bias / activation / split-K):
 // the accumulators are parked in an f32 LDS image and every thread then moves 16-byte (8-channel)
 // row chunks, so a wave instruction covers whole row segments instead of the MFMA layout's 16 rows x
@@ -341,7 +349,7 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
   }
 #pragma unroll
   for (int h = 0; h < WM; ++h) {
-    __syncthreads();  // operand stages (h = 0) / the previous slice's image (h > 0) are dead
+    lds_barrier();  // operand stages (h = 0) / the previous slice's image (h > 0) are dead
     if (wm == h) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -349,7 +357,7 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
         for (int j = 0; j < FN; ++j)
           *(f32x4*)(img + (i * 16 + (lane & 15)) * LS + wn * TN + j * 16 + 4 * (lane >> 4)) = acc[i][j];
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int k = 0; k < TM * CPR / NT; ++k) {
       const int r = (k * NT + (int)threadIdx.x) / CPR;
@@ -402,7 +410,7 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
       }
     constexpr int NW = WM * WN;
     float* red = img;  // [NW][2][BN]
-    __syncthreads();   // the last slice's image is dead
+    lds_barrier();     // the last slice's image is dead
     const int w = (int)threadIdx.x >> 6;
     if (lane < CPR) {
 #pragma unroll
@@ -411,7 +419,7 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
         red[(w * 2 + 1) * BN + cc + e] = s2[e];
       }
     }
-    __syncthreads();
+    lds_barrier();
     for (int t = (int)threadIdx.x; t < 2 * BN; t += NT) {
       const int which = t / BN, c = t % BN;
       if (col0 + c >= g.N) continue;

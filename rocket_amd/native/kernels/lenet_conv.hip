@@ -947,7 +947,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
         *(uint2*)(sm.c1[sl] + e) = c1v;
       }
     }
-    __syncthreads();
+    lds_barrier();
     RK_TR(cb.trace, 7);
     for (int i = threadIdx.x; i < SPB * A2N; i += NTHR) {  // scatter the pooled gradients
       const int sl = i / A2N, e = i % A2N, co = e / 25, w = e % 25;
@@ -971,7 +971,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       sm.imgb[sl][0][IMGN + k] = zo;
       sm.imgb[sl][1][IMGN - 1 + k] = 0;
     }
-    __syncthreads();
+    lds_barrier();
     RK_TR(cb.trace, 8);
 
     // ---- phase B: conv2 dgrad (4 samples x 13 pixel tiles) and dW2 (10 column tiles), which
@@ -1087,7 +1087,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       }
     }
     RK_TRW(cb.trace, 32);  // per wave: dgrad tiles done
-    __syncthreads();
+    lds_barrier();
     RK_TR(cb.trace, 9);
 
     // ---- phase C: dW1 on all 16 waves (4 x 25 k-steps over the positions of the 14x14 pool grid);
@@ -1164,7 +1164,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 4; ++i) red1[wave][u][(4 * hi + i) * 16 + lo] = g1[u][i];
     }
-    __syncthreads();
+    lds_barrier();
     RK_TR(cb.trace, 10);
     for (int e = threadIdx.x; e < 2 * 256; e += NTHR) {  // column r = R1 (u = 1, lane 9) holds db1
       const int u = e >> 8, row = (e & 255) >> 4, col = 16 * u + (e & 15);
