@@ -347,6 +347,45 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
       is[e] = cg.bnb_invstd[n + e];
     }
   }
+  // side inputs of every chunk this thread stores (the BN input and ReLU-mask byte of BNB, the old
+  // output of an accumulate), all issued now: their memory latency overlaps the LDS image passes
+  // instead of stalling each chunk's store in turn
+  // (each optional input under ONE uniform branch around its whole loop: a per-element
+  // condition would make hipcc wait for every load separately)
+  constexpr int KI = TM * CPR / NT;
+  uint4 xz[WM][KI], old[WM][KI];
+  unsigned mbv[WM][KI];
+  int64_t offs[WM][KI];
+  int mrow[WM][KI];
+  const int ncl = min(col0 + cc, g.N - 8);
+#pragma unroll
+  for (int h = 0; h < WM; ++h)
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int r = (k * NT + (int)threadIdx.x) / CPR;
+      mrow[h][k] = min(row0 + h * TM + r, g.M - 1);
+      offs[h][k] = rowmap(mrow[h][k]) * g.ldc + ncl;
+      xz[h][k] = old[h][k] = make_uint4(0u, 0u, 0u, 0u);
+      mbv[h][k] = 0xFFu;
+    }
+  if constexpr (BNB) {
+#pragma unroll
+    for (int h = 0; h < WM; ++h)
+#pragma unroll
+      for (int k = 0; k < KI; ++k) xz[h][k] = *(const uint4*)(cg.bnb_x + offs[h][k]);
+    if (cg.bnb_mask) {
+#pragma unroll
+      for (int h = 0; h < WM; ++h)
+#pragma unroll
+        for (int k = 0; k < KI; ++k) mbv[h][k] = cg.bnb_mask[(int64_t)mrow[h][k] * (g.N >> 3) + (ncl >> 3)];
+    }
+  }
+  if (g.accumulate) {
+#pragma unroll
+    for (int h = 0; h < WM; ++h)
+#pragma unroll
+      for (int k = 0; k < KI; ++k) old[h][k] = *(const uint4*)((const uint16_t*)g.c + offs[h][k]);
+  }
 #pragma unroll
   for (int h = 0; h < WM; ++h) {
     lds_barrier();  // operand stages (h = 0) / the previous slice's image (h > 0) are dead
@@ -359,23 +398,17 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
     }
     lds_barrier();
 #pragma unroll
-    for (int k = 0; k < TM * CPR / NT; ++k) {
+    for (int k = 0; k < KI; ++k) {
       const int r = (k * NT + (int)threadIdx.x) / CPR;
       const int m = row0 + h * TM + r, n = col0 + cc;
       if (m >= g.M || n >= g.N) continue;  // N % 8 == 0: a chunk is all in or all out
       const int64_t off = rowmap(m) * g.ldc + n;
-      uint4 xz = make_uint4(0u, 0u, 0u, 0u);
-      unsigned mb = 0xFFu;
-      if constexpr (BNB) {
-        xz = *(const uint4*)(cg.bnb_x + off);
-        if (cg.bnb_mask) mb = cg.bnb_mask[(int64_t)m * (g.N >> 3) + (n >> 3)];
-      }
+      const unsigned mb = mbv[h][k];
       const f32x4 a = *(const f32x4*)(img + r * LS + cc), b = *(const f32x4*)(img + r * LS + cc + 4);
       float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
       uint16_t* dst = (uint16_t*)g.c + off;
       if (g.accumulate) {
-        const uint4 o = *(const uint4*)dst;
-        const uint32_t po[4] = {o.x, o.y, o.z, o.w};
+        const uint32_t po[4] = {old[h][k].x, old[h][k].y, old[h][k].z, old[h][k].w};
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
           v[2 * w] += lo16t<H>(po[w]);
@@ -387,7 +420,7 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
       const uint32_t pk[4] = {pack16t<H>(v[0], v[1]), pack16t<H>(v[2], v[3]), pack16t<H>(v[4], v[5]),
                               pack16t<H>(v[6], v[7])};
       if constexpr (BNB) {
-        const uint32_t px[4] = {xz.x, xz.y, xz.z, xz.w};
+        const uint32_t px[4] = {xz[h][k].x, xz[h][k].y, xz[h][k].z, xz[h][k].w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float x = (e & 1) ? hi16t<H>(px[e >> 1]) : lo16t<H>(px[e >> 1]);

@@ -432,7 +432,9 @@ __global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const uint16_t* _
 // (always valid) addresses keep 4 independent 16-byte loads in flight per tensor.
 // y = relu?(x*a + b + res?).  With ReLU the launch also writes the 1-bit mask [y > 0]
 // (mask[r][cv], bit k = channel 8cv + k): the backward reads 1 byte per 8 elements instead of y.
-template <typename T, typename TO>
+// RES: the residual input is a template flag, not a run-time test per element (a conditional load
+// in the unrolled row loop makes hipcc wait for each load on its own: vmcnt(0) per element)
+template <typename T, typename TO, bool RES>
 __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x, const TO* __restrict__ res,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
                                                         TO* __restrict__ y, uint8_t* __restrict__ mask, int64_t R,
@@ -454,7 +456,7 @@ __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x,
     for (int u = 0; u < BN_U; ++u) {
       const int64_t ru = min(r + u * RPP, r1 - 1);
       V8<T>::load(x + ru * C + c, v[u]);
-      if (res) V8<TO>::load(res + ru * C + c, q[u]);
+      if constexpr (RES) V8<TO>::load(res + ru * C + c, q[u]);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -462,7 +464,7 @@ __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x,
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float o = v[u][k] * A[k] + B[k];
-        if (res) o += q[u][k];
+        if constexpr (RES) o += q[u][k];
         if (relu) {
           o = fmaxf(o, 0.f);
           m |= (o > 0.f ? 1u : 0u) << k;
@@ -1123,8 +1125,15 @@ RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const fl
   if (C % 8 || C > 8 * BN_T || R <= 0) return (int)hipErrorInvalidValue;
   int grid;
   const int rpb = bn_elem_rows(R, C, &grid);
-#define RK_BA(T, TO) bn_apply_kernel<T, TO><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y, \
-                                                            relu ? (uint8_t*)mask : nullptr, R, C, relu, rpb)
+#define RK_BA(T, TO)                                                                                            \
+  do {                                                                                                          \
+    if (res)                                                                                                    \
+      bn_apply_kernel<T, TO, true><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y,    \
+                                                         relu ? (uint8_t*)mask : nullptr, R, C, relu, rpb);    \
+    else                                                                                                        \
+      bn_apply_kernel<T, TO, false><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y,   \
+                                                          relu ? (uint8_t*)mask : nullptr, R, C, relu, rpb);   \
+  } while (0)
   if (dt == F16 && dto == F16) RK_BA(f16_t, f16_t);
   else if (dt == F16 && dto == F32) RK_BA(f16_t, float);
   else if (dt == BF16 && dto == BF16) RK_BA(uint16_t, uint16_t);
