@@ -42,6 +42,8 @@ from rocket_amd.ops.mgemm import mgemm, pick_split
 #                  wgrads, the <= 2048-wide dgrads and the K = 3072 forward; the library elsewhere.
 #   libw           forward / dgrad on the library, every weight gradient on mgemm (split-K with the
 #                  bias gradient from the same launch: no K-split batched GEMM + slab sums + colsum)
+#   libd           forward / wgrad on the library, every input gradient (K-major weight read, no
+#                  transpose) on mgemm
 MODE = os.environ.get("ROCKET_VIT_GEMM", "lib")
 _TILE_WIDE_FWD, _TILE_DEFAULT = 4, 0
 
@@ -51,7 +53,7 @@ def _fwd_tile(N: int) -> int:
 
 
 def _lib_fwd(K: int) -> bool:
-    return MODE in ("lib", "libw") or (MODE == "hybrid" and K < 2048)
+    return MODE in ("lib", "libw", "libd") or (MODE == "hybrid" and K < 2048)
 
 
 def _lib_dgrad(N_in: int) -> bool:
@@ -80,13 +82,17 @@ def _linear_fwd(x2: torch.Tensor, w16: torch.Tensor, bias: torch.Tensor, b16: to
     return y
 
 
-def _linear_dgrad(dy2: torch.Tensor, w16: torch.Tensor) -> torch.Tensor:
+def _linear_dgrad(dy2: torch.Tensor, w16: torch.Tensor, gelu_of: torch.Tensor | None = None) -> torch.Tensor:
+    """dx = dy W (bf16); with ``gelu_of`` = z (native route only) the epilogue also multiplies by
+    gelu'(z): the input gradient of a GELU whose input z fed this layer, in the same launch."""
     M, N = dy2.shape
     K = w16.shape[1]
     if _lib_dgrad(K):
+        assert gelu_of is None
         return dy2 @ w16
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy2.device)
-    mgemm(dy2, w16, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, b_kmaj=True, tile=_TILE_DEFAULT)
+    mgemm(dy2, w16, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, b_kmaj=True, tile=_TILE_DEFAULT,
+          aux=gelu_of, epi="none" if gelu_of is None else "mul_gelu_grad")
     return dx
 
 
@@ -96,7 +102,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
     engine provides them (returns None for those), else returned as new tensors."""
     M, N = dy.shape
     K = x.shape[1]
-    if MODE == "lib":
+    if MODE in ("lib", "libd"):
         return lib_param_grads(dy, x, weight, bias, need_w, need_b)
     direct = (not need_w or _direct(weight)) and (not need_b or _direct(bias))
     if direct:
@@ -240,6 +246,9 @@ class _MMlpFn(torch.autograd.Function):
             # GELU backward and fc1's bias gradient in one pass over the [tokens, hidden] gradient
             dz, db1 = _gelu_bwd_bias(_linear_dgrad(dy2, w2_16), z, b1)
             need_b1 = False
+        elif not _lib_dgrad(z.shape[1]):
+            # native fc2 input gradient with gelu'(z) in its epilogue: dz straight out of the GEMM
+            dz = _linear_dgrad(dy2, w2_16, gelu_of=z)
         else:
             dz = _gelu_bwd(_linear_dgrad(dy2, w2_16), z)
         need_b2 = b2 is not None and g[4]
