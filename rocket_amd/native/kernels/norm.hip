@@ -865,7 +865,7 @@ __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ 
     } else if (col < 2 * C) {
       if (dbeta) dbeta[col - C] += u;
     } else if (dthird) {
-      dthird[col - 2 * C] += u;
+      dthird[col - 2 * C] = u;  // written, not accumulated: the caller needs no zeroed buffer
     }
   }
 }
@@ -1240,7 +1240,8 @@ RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
 
 // LayerNorm backward; dgamma/dbeta accumulated (+=). dt: x/dx dtype, dto: dy dtype.
 // dsum (dtype dt) / dres (dtype dto) may be null: dx = LN_bwd(dy) [+ dsum], dres = dx
-// dres_sum (f32 [C], optional, needs dres): += column sums of dres (the added branch's bias gradient)
+// dres_sum (f32 [C], optional, needs dres): = column sums of dres (the added branch's bias gradient;
+// written, not accumulated)
 RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float* g, const float* mean,
                      const float* rstd, void* dx, const void* dsum, void* dres, float* dgamma, float* dbeta,
                      float* dres_sum, int64_t rows, int C, float* ws, unsigned* counter, hipStream_t s) {

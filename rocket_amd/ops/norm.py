@@ -369,7 +369,7 @@ class _AddLN(torch.autograd.Function):
         counter = _lib.Workspace.get(dev).counter("ln_bwd")
         w = weight.detach() if weight is not None else None
         link, ctx.link = ctx.link, None
-        rsum = torch.zeros(C, dtype=torch.float32, device=dev) if link is not None else None
+        rsum = torch.empty(C, dtype=torch.float32, device=dev) if link is not None else None  # written by the kernel
         _lib.check(lib.rk_ln_bwd(_dt(ssum), _dt(dy), dy.data_ptr(), ssum.data_ptr(), _lib.ptr(w), mean.data_ptr(),
                                  rstd.data_ptr(), dx.data_ptr(), _lib.ptr(ds), dr.data_ptr(), _lib.ptr(dgamma),
                                  _lib.ptr(dbeta), _lib.ptr(rsum), rows, C, ws.data_ptr(), counter,
