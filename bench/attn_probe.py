@@ -64,6 +64,16 @@ def main():
     st = stamps.view(-1, 4).median(0).values / 100.0  # 100 MHz ticks -> us
     rec["fused_phase_us"] = {"staged": round(float(st[1]), 2), "loop_done": round(float(st[2]), 2),
                              "end": round(float(st[3]), 2)}
+    lib.rk_attn_set_bwd_fused(2)
+    rec["bwd_stream_us"] = round(timed(bwd), 1)
+    stamps.zero_()
+    lib.rk_attn_set_stamps(stamps.data_ptr())
+    bwd()
+    torch.cuda.synchronize()
+    lib.rk_attn_set_stamps(None)
+    st = stamps.view(-1, 4).median(0).values / 100.0
+    rec["stream_phase_us"] = {"staged": round(float(st[1]), 2), "loop_done": round(float(st[2]), 2),
+                              "end": round(float(st[3]), 2)}
     lib.rk_attn_set_bwd_fused(0)
     rec["bwd_split_us"] = round(timed(bwd), 1)
     lib.rk_attn_set_bwd_fused(1)

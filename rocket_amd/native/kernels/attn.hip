@@ -67,6 +67,7 @@ struct AttnArgs {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ bf16x8 ld16(const uint16_t* p) { return *(const bf16x8*)p; }
 __device__ __forceinline__ bf16x8 zero8() { return bf16x8{}; }
@@ -579,6 +580,218 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
   if (stamp) stamp[3] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
 }
 
+
+// ------------------------------------------------ backward: fused dQ, dK, dV, streamed queries
+// As attn_bwd_fused_kernel (one block per (head, batch), a wave per 16-key tile, 32-query chunks,
+// dS through a double-buffered image, the previous chunk's dQ in the same barrier interval), but
+// only K is staged whole: the chunk's Q / dO / O rows (3 x 4 KiB) arrive by LDS-DMA into a 2-slot
+// ring, issued one chunk ahead by waves 0..11 (one 1-KiB piece each, source-side swizzle so the
+// lane-linear DMA image matches eoff), so the loads of chunk ks+1 run under chunk ks's products
+// instead of a whole-block staging phase in front of them.  delta = rowsum(dO * O) of the chunk's
+// rows is formed by every wave from the slot (32 rows x 64 d), then shuffled to the lanes that
+// need it.  Every dQ store is issued (rows >= L go to a sink), so the number of VMEM operations a
+// wave issues after its DMA piece is known (nst) and the end-of-chunk wait is vmcnt(nst): the
+// stores are never waited for.  All LDS is one array (hipcc otherwise waits vmcnt(0) before LDS
+// reads next to an LDS-DMA destination).
+__device__ __attribute__((aligned(16))) uint4 g_attn_zero[1];
+__device__ uint16_t g_attn_sink[64];
+
+constexpr int SB_K = 0;                          // K image [LMAX][64], eoff-swizzled
+constexpr int SB_Q = SB_K + LMAX * RS * 2;       // Q ring: 2 slots x [32][64]
+constexpr int SB_G = SB_Q + 2 * DSC * RS * 2;    // dO ring
+constexpr int SB_O = SB_G + 2 * DSC * RS * 2;    // O ring (delta only)
+constexpr int SB_S = SB_O + 2 * DSC * RS * 2;    // dS: 2 x [LMAX][32]
+constexpr int SB_L = SB_S + 2 * LMAX * DSC * 2;  // lse [LMAX] f32
+constexpr int SB_END = SB_L + LMAX * 4;
+
+__global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_stream_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[SB_END];
+  uint16_t* Ks = (uint16_t*)(smem + SB_K);
+  float* lse_s = (float*)(smem + SB_L);
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
+  const int nthr = blockDim.x;
+  const int L = a.L;
+  const int ntile = (L + 15) / 16;
+  const int nchunks = (ntile + 1) / 2;
+  const int64_t bh = (int64_t)b * a.H + h;
+  float* stamp = (a.stamps != nullptr && threadIdx.x == 0) ? a.stamps + (int64_t)bh * 4 : nullptr;
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  const int k0 = 16 * w;
+
+  // a chunk is 12 pieces of 1 KiB (tensor pc / 4: Q, dO, O; rows 8 (pc % 4) .. + 7), piece pc on
+  // wave pc % nw (one each at L = 197, up to 12 on a 1-wave block)
+  const int nw = nthr / 64;
+  const bool stager = w < 12;
+  const int srow0 = lane >> 3;
+  auto stage_chunk = [&](int c, int slot) {
+    for (int pc = w; pc < 12; pc += nw) {
+      const int tsel = pc >> 2, piece = pc & 3;
+      const int srow = 8 * piece + srow0;
+      const int lch = (lane & 7) ^ (((srow >> 1) & 3) << 1);  // logical chunk landing at this lane's slot
+      const uint16_t* sbase = tsel == 0 ? a.q : tsel == 1 ? a.dout : a.o;
+      const int sld = tsel == 0 ? a.ld : a.ldo;
+      const int sbyte = (tsel == 0 ? SB_Q : tsel == 1 ? SB_G : SB_O) + piece * 1024;
+      const int r = 32 * c + srow;
+      const char* src = r < L ? (const char*)(sbase + ((int64_t)b * L + r) * sld + h * D + lch * 8)
+                              : (const char*)g_attn_zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(smem + sbyte + slot * DSC * RS * 2), 16, 0, 0);
+    }
+  };
+  stage_chunk(0, 0);  // in flight under the K staging
+  bf16x8 vb[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) vb[ks] = gload_row(a.v, a.ld, b, L, k0 + lo, h, 32 * ks + 8 * hi);
+  {  // K image + lse, every load issued before the first LDS write
+    constexpr int N = LMAX * (D / 8), SU = 3;
+    for (int i0 = threadIdx.x; i0 < N; i0 += SU * nthr) {
+      bf16x8 kv[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = min(i0 + u * nthr, N - 1);
+        kv[u] = gload_row(a.k, a.ld, b, L, i >> 3, h, (i & 7) * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = i0 + u * nthr;
+        if (i < N) *(bf16x8*)(Ks + eoff(i >> 3, i & 7)) = kv[u];
+      }
+    }
+    for (int r = threadIdx.x; r < LMAX; r += nthr) lse_s[r] = r < L ? a.lse[bh * L + r] : 0.f;
+  }
+  {  // dS rows of key tiles without a wave stay zero (read by the dQ products)
+    uint16_t* d0 = (uint16_t*)(smem + SB_S);
+    for (int i = threadIdx.x; i < 2 * LMAX * DSC / 8; i += nthr) *(uint4*)(d0 + 8 * i) = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();  // K, lse, dS zeros and chunk 0's DMA (every wave waited vmcnt(0) here)
+  if (stamp) stamp[1] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
+
+  const float sl = a.scale * LOG2E;
+  bf16x8 kb[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) kb[ks] = frag(Ks, k0 + lo, 4 * ks + hi);
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) dk[nt] = dv[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nkey32 = (ntile + 1) / 2;
+  // phase B of chunk kc: the chunk's 8 dQ tiles, tile t on wave t % nw; returns the number of VMEM
+  // stores this wave issued (wave-uniform)
+  auto phase_b = [&](int kc) -> int {
+    int nst = 0;
+    const uint16_t* dsc = (const uint16_t*)(smem + SB_S) + (kc & 1) * LMAX * DSC;
+    for (int t = w; t < 8; t += nw) {
+    const int qh = t >> 2, nt = t & 3;
+    if (32 * kc + 16 * qh >= L) continue;  // wave-uniform
+    f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+    for (int kq = 0; kq < nkey32; ++kq) {
+      const uint2 a0 = tr4dsc(dsc, 32 * kq + 4 * hi, 16 * qh, lo), a1 = tr4dsc(dsc, 32 * kq + 16 + 4 * hi, 16 * qh, lo);
+      const bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(a0.x, a0.y, a1.x, a1.y));
+      dq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+          av, tr_operand(Ks, 32 * kq + 4 * hi, 32 * kq + 16 + 4 * hi, 16 * nt, lo), dq, 0, 0, 0);
+    }
+    const int r0 = 32 * kc + 16 * qh + 4 * hi;
+    uint16_t* dqp = a.dq + ((int64_t)b * L + r0) * a.ldg + h * D + 16 * nt + lo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // every store issued (rows >= L into the sink): a known count
+      uint16_t* p = r0 + i < L ? dqp + (int64_t)i * a.ldg : g_attn_sink + lane;
+      *p = f2bf(dq[i]);
+    }
+    nst += 4;
+    }
+    return nst;
+  };
+  for (int ks = 0; ks < nchunks; ++ks) {
+    const int slot = ks & 1;
+    const bool ahead = ks + 1 < nchunks;
+    if (ahead) stage_chunk(ks + 1, slot ^ 1);  // that slot was last read before the previous barrier
+    const uint16_t* Qc = (const uint16_t*)(smem + SB_Q) + slot * DSC * RS;
+    const uint16_t* Gc = (const uint16_t*)(smem + SB_G) + slot * DSC * RS;
+    const uint16_t* Oc = (const uint16_t*)(smem + SB_O) + slot * DSC * RS;
+    uint16_t* dsc = (uint16_t*)(smem + SB_S) + slot * LMAX * DSC;
+    // delta of the chunk's rows: lane = row (lane & 31), d half (lane >> 5)
+    float dl;
+    {
+      const int r = lane & 31, hf = lane >> 5;
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint4 gu = __builtin_bit_cast(uint4, frag(Gc, r, 4 * hf + j));
+        const uint4 ou = __builtin_bit_cast(uint4, frag(Oc, r, 4 * hf + j));
+        const uint32_t gw[4] = {gu.x, gu.y, gu.z, gu.w}, ow[4] = {ou.x, ou.y, ou.z, ou.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          t += __uint_as_float(gw[e] << 16) * __uint_as_float(ow[e] << 16) +
+               __uint_as_float(gw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+      }
+      dl = t + __shfl_xor(t, 32, 64);
+    }
+    f32x4 p2[2], ds2[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qt = 2 * ks + u;
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      if (qt < ntile) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Qc, 16 * u + lo, 4 * kk + hi), kb[kk], sv, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Gc, 16 * u + lo, 4 * kk + hi), vb[kk], dp, 0, 0, 0);
+        }
+      }
+      const int q4 = 16 * qt + 4 * hi;
+      const f32x4 lq = *(const f32x4*)(lse_s + q4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float dqi = __shfl(dl, 16 * u + 4 * hi + i, 64);
+        const bool ok = q4 + i < L && k0 + lo < L;
+        const float e = __builtin_amdgcn_exp2f(sv[i] * sl - lq[i]);
+        const float p = ok ? e : 0.f;
+        p2[u][i] = p;
+        ds2[u][i] = p * (dp[i] - dqi) * a.scale;
+      }
+    }
+    const bf16x8 pa = pack_operand(p2[0], p2[1]);
+    const bf16x8 sa = pack_operand(ds2[0], ds2[1]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      *(uint2*)(dsc + (k0 + lo) * DSC + 16 * u + 4 * hi) =
+          make_uint2(pack2(ds2[u][0], ds2[u][1]), pack2(ds2[u][2], ds2[u][3]));
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      dv[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_operand(Gc, 4 * hi, 16 + 4 * hi, 16 * nt, lo), dv[nt],
+                                                       0, 0, 0);
+      dk[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_operand(Qc, 4 * hi, 16 + 4 * hi, 16 * nt, lo), dk[nt],
+                                                       0, 0, 0);
+    }
+    const int nst = ks > 0 ? phase_b(ks - 1) : 0;
+    // this wave's DMA piece of chunk ks+1 has landed once at most the nst dQ stores issued after it
+    // are outstanding; then LDS traffic, then the raw barrier (no wait for the stores themselves)
+    if (ahead && stager) {
+      if (nst == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (nst == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (0 stores; or many: wait for all)
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (nchunks > 0) phase_b(nchunks - 1);
+  if (stamp) stamp[2] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = k0 + 4 * hi + i;
+    if (r < L) {
+      uint16_t* rk = a.dk + ((int64_t)b * L + r) * a.ldg + h * D;
+      uint16_t* rv = a.dv + ((int64_t)b * L + r) * a.ldg + h * D;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        rk[16 * nt + lo] = f2bf(dk[nt][i]);
+        rv[16 * nt + lo] = f2bf(dv[nt][i]);
+      }
+    }
+  }
+  if (stamp) stamp[3] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
+}
+
 }  // namespace
 
 int g_bwd_fused = 1;         // rk_attn_set_bwd_fused
@@ -586,9 +799,11 @@ float* g_stamps = nullptr;   // rk_attn_set_stamps
 
 RK_API int rk_attn_max_len() { return LMAX; }
 
-// 1 (default): one fused dQ/dK/dV kernel; 0: the dQ and dK/dV kernels (A/B, ROCKET_ATTN_BWD=split)
-RK_API int rk_attn_set_bwd_fused(int on) {
-  g_bwd_fused = on != 0;
+// 2: the fused kernel with streamed query chunks (attn_bwd_stream_kernel); 1 (default): one fused
+// dQ/dK/dV kernel with whole-head staging; 0: the dQ and dK/dV kernels (A/B, ROCKET_ATTN_BWD)
+RK_API int rk_attn_set_bwd_fused(int mode) {
+  if (mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  g_bwd_fused = mode;
   return 0;
 }
 
@@ -637,6 +852,10 @@ RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, cons
   a.lse = (float*)lse; a.delta = delta; a.stamps = g_stamps;
   a.ld = ld; a.ldo = ldo; a.ldg = ldg; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);
+  if (g_bwd_fused == 2) {
+    attn_bwd_stream_kernel<<<grid, 64 * ((L + 15) / 16), 0, s>>>(a);
+    return (int)hipGetLastError();
+  }
   if (g_bwd_fused) {
     attn_bwd_fused_kernel<<<grid, 64 * ((L + 15) / 16), 0, s>>>(a);
     return (int)hipGetLastError();

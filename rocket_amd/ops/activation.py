@@ -93,8 +93,11 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
 # register-bounded to 128 VGPRs so two blocks share a CU; profiles/r2_attn_waves_ab.txt)
 ATTN_WAVES = tuple(int(v) for v in os.environ.get("ROCKET_ATTN_WAVES", "8,82,82").split(","))
 # backward: "fused" (default: one kernel per (batch, head), S / dP computed once, one wave per key
-# tile, dQ reduced in LDS) or "split" (the dQ and dK/dV kernels, each recomputing S and dP)
+# tile, dQ from the per-chunk dS image), "stream" (the same with only K staged whole and the query
+# chunks' Q / dO / O streamed by LDS-DMA one chunk ahead) or "split" (the dQ and dK/dV kernels,
+# each recomputing S and dP)
 ATTN_BWD = os.environ.get("ROCKET_ATTN_BWD", "fused")
+_BWD_MODES = {"split": 0, "fused": 1, "stream": 2}
 _waves_set = False
 
 
@@ -103,7 +106,7 @@ def _attn_lib():
     lib = _lib.kernels()
     if not _waves_set:
         _lib.check(lib.rk_attn_set_waves(*ATTN_WAVES), "rk_attn_set_waves")
-        _lib.check(lib.rk_attn_set_bwd_fused(int(ATTN_BWD != "split")), "rk_attn_set_bwd_fused")
+        _lib.check(lib.rk_attn_set_bwd_fused(_BWD_MODES[ATTN_BWD]), "rk_attn_set_bwd_fused")
         _waves_set = True
     return lib
 

@@ -118,8 +118,8 @@ def test_fused_add_layernorm():
     assert _rel(ln.weight.grad, w.grad) < 3e-2 and _rel(ln.bias.grad, b.grad) < 3e-2
 
 
-@pytest.mark.parametrize("bwd", ["fused", "split"])
-@pytest.mark.parametrize("B,L,H", [(2, 197, 12), (3, 50, 4), (1, 224, 2), (2, 17, 3)])
+@pytest.mark.parametrize("bwd", ["fused", "stream", "split"])
+@pytest.mark.parametrize("B,L,H", [(2, 197, 12), (3, 50, 4), (1, 224, 2), (2, 17, 3), (2, 208, 2)])
 def test_fused_attention_qkv(B, L, H, bwd):
     """Fused MFMA attention (fwd + dQ/dK/dV) vs fp32 softmax attention on the same bf16 inputs, with
     the one-kernel backward (dQ reduced over key-tile waves in LDS) and the two-kernel backward."""
@@ -127,7 +127,7 @@ def test_fused_attention_qkv(B, L, H, bwd):
     from rocket_amd.ops.activation import _attn_lib, attention_qkv
 
     _attn_lib()
-    _lib.kernels().rk_attn_set_bwd_fused(int(bwd == "fused"))
+    _lib.kernels().rk_attn_set_bwd_fused({"split": 0, "fused": 1, "stream": 2}[bwd])
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
