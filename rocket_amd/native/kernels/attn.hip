@@ -593,6 +593,31 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
 // wave issues after its DMA piece is known (nst) and the end-of-chunk wait is vmcnt(nst): the
 // stores are never waited for.  All LDS is one array (hipcc otherwise waits vmcnt(0) before LDS
 // reads next to an LDS-DMA destination).
+// Transpose reads as inline asm: the ds_read_tr16_b64 intrinsic carries no alias information, so
+// after an LDS-DMA into the same array hipcc puts s_waitcnt vmcnt(0) in front of it (the DMA of
+// the next chunk would then be waited for mid-chunk).  The caller waits lgkmcnt(0) + sched_barrier
+// before using the results (hipcc does not track inline-asm LDS reads).
+__device__ __forceinline__ uint2 tr_raw(const uint16_t* p) {
+  uint2 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(const lds_void*)p));
+  return v;
+}
+__device__ __forceinline__ uint2 tr4_raw(const uint16_t* img, int r0, int c0, int lo) {
+  const int c = c0 + 4 * (lo & 3);
+  return tr_raw(img + eoff(r0 + (lo >> 2), c >> 3) + (c & 7));
+}
+__device__ __forceinline__ bf16x8 tr_operand_raw(const uint16_t* img, int r0a, int r0b, int c0, int lo) {
+  const uint2 a = tr4_raw(img, r0a, c0, lo), b = tr4_raw(img, r0b, c0, lo);
+  return __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
+}
+__device__ __forceinline__ uint2 tr4dsc_raw(const uint16_t* img, int r0, int c0, int lo) {
+  return tr_raw(img + (r0 + (lo >> 2)) * 32 + c0 + 4 * (lo & 3));
+}
+__device__ __forceinline__ void lds_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __attribute__((aligned(16))) uint4 g_attn_zero[1];
 __device__ uint16_t g_attn_sink[64];
 
@@ -609,7 +634,8 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_stream_kernel(AttnAr
   uint16_t* Ks = (uint16_t*)(smem + SB_K);
   float* lse_s = (float*)(smem + SB_L);
   const int b = blockIdx.z, h = blockIdx.y;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
+  const int lane = threadIdx.x & 63, lo = lane & 15, hi = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar) wave index
   const int nthr = blockDim.x;
   const int L = a.L;
   const int ntile = (L + 15) / 16;
@@ -624,13 +650,16 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_stream_kernel(AttnAr
   const int nw = nthr / 64;
   const bool stager = w < 12;
   const int srow0 = lane >> 3;
+  // per-tensor sources (kernel arguments read once, outside the chunk loop)
+  const uint16_t* const srcs[3] = {a.q, a.dout, a.o};
+  const int lds_[3] = {a.ld, a.ldo, a.ldo};
   auto stage_chunk = [&](int c, int slot) {
-    for (int pc = w; pc < 12; pc += nw) {
+    for (int pc = w; pc < 12; pc += nw) {  // scalar loop
       const int tsel = pc >> 2, piece = pc & 3;
       const int srow = 8 * piece + srow0;
       const int lch = (lane & 7) ^ (((srow >> 1) & 3) << 1);  // logical chunk landing at this lane's slot
-      const uint16_t* sbase = tsel == 0 ? a.q : tsel == 1 ? a.dout : a.o;
-      const int sld = tsel == 0 ? a.ld : a.ldo;
+      const uint16_t* sbase = tsel == 0 ? srcs[0] : tsel == 1 ? srcs[1] : srcs[2];
+      const int sld = tsel == 0 ? lds_[0] : lds_[1];
       const int sbyte = (tsel == 0 ? SB_Q : tsel == 1 ? SB_G : SB_O) + piece * 1024;
       const int r = 32 * c + srow;
       const char* src = r < L ? (const char*)(sbase + ((int64_t)b * L + r) * sld + h * D + lch * 8)
@@ -684,10 +713,11 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_stream_kernel(AttnAr
     if (32 * kc + 16 * qh >= L) continue;  // wave-uniform
     f32x4 dq = {0.f, 0.f, 0.f, 0.f};
     for (int kq = 0; kq < nkey32; ++kq) {
-      const uint2 a0 = tr4dsc(dsc, 32 * kq + 4 * hi, 16 * qh, lo), a1 = tr4dsc(dsc, 32 * kq + 16 + 4 * hi, 16 * qh, lo);
+      const uint2 a0 = tr4dsc_raw(dsc, 32 * kq + 4 * hi, 16 * qh, lo), a1 = tr4dsc_raw(dsc, 32 * kq + 16 + 4 * hi, 16 * qh, lo);
+      const bf16x8 bv = tr_operand_raw(Ks, 32 * kq + 4 * hi, 32 * kq + 16 + 4 * hi, 16 * nt, lo);
+      lds_wait();
       const bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(a0.x, a0.y, a1.x, a1.y));
-      dq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-          av, tr_operand(Ks, 32 * kq + 4 * hi, 32 * kq + 16 + 4 * hi, 16 * nt, lo), dq, 0, 0, 0);
+      dq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, dq, 0, 0, 0);
     }
     const int r0 = 32 * kc + 16 * qh + 4 * hi;
     uint16_t* dqp = a.dq + ((int64_t)b * L + r0) * a.ldg + h * D + 16 * nt + lo;
@@ -751,16 +781,28 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_stream_kernel(AttnAr
     }
     const bf16x8 pa = pack_operand(p2[0], p2[1]);
     const bf16x8 sa = pack_operand(ds2[0], ds2[1]);
+    {  // dS row of this lane's key, 4 queries per u, as inline-asm LDS stores (a plain store after an
+       // LDS-DMA into the same array gets a vmcnt(0) wait from hipcc; the barrier's lgkmcnt(0)
+       // retires these)
+      const uint32_t da = (uint32_t)(uintptr_t)(lds_void*)(dsc + (k0 + lo) * DSC + 4 * hi);
+      const uint2 v0 = make_uint2(pack2(ds2[0][0], ds2[0][1]), pack2(ds2[0][2], ds2[0][3]));
+      const uint2 v1 = make_uint2(pack2(ds2[1][0], ds2[1][1]), pack2(ds2[1][2], ds2[1][3]));
+      asm volatile("ds_write_b64 %0, %1\n\tds_write_b64 %0, %2 offset:32" ::"v"(da), "v"(v0), "v"(v1) : "memory");
+    }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-      *(uint2*)(dsc + (k0 + lo) * DSC + 16 * u + 4 * hi) =
-          make_uint2(pack2(ds2[u][0], ds2[u][1]), pack2(ds2[u][2], ds2[u][3]));
+    for (int hh = 0; hh < 2; ++hh) {  // two d-halves: 8 transpose reads in flight, then 4 MFMAs
+      bf16x8 gv[2], qv[2];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      dv[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_operand(Gc, 4 * hi, 16 + 4 * hi, 16 * nt, lo), dv[nt],
-                                                       0, 0, 0);
-      dk[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_operand(Qc, 4 * hi, 16 + 4 * hi, 16 * nt, lo), dk[nt],
-                                                       0, 0, 0);
+      for (int j = 0; j < 2; ++j) {
+        gv[j] = tr_operand_raw(Gc, 4 * hi, 16 + 4 * hi, 16 * (2 * hh + j), lo);
+        qv[j] = tr_operand_raw(Qc, 4 * hi, 16 + 4 * hi, 16 * (2 * hh + j), lo);
+      }
+      lds_wait();
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        dv[2 * hh + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, gv[j], dv[2 * hh + j], 0, 0, 0);
+        dk[2 * hh + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, qv[j], dk[2 * hh + j], 0, 0, 0);
+      }
     }
     const int nst = ks > 0 ? phase_b(ks - 1) : 0;
     // this wave's DMA piece of chunk ks+1 has landed once at most the nst dQ stores issued after it
