@@ -128,8 +128,9 @@ __device__ __forceinline__ bf16x8 tr_operand(const uint16_t* img, int r0a, int r
 
 // transposed read of the fused backward's [key][32-query] dS chunk image (64-B rows): the 16-lane
 // group gets keys r0..r0+3, queries c0..c0+15; lane lo receives query c0 + lo, element j = key r0 + j
+template <int P = 32>  // row pitch (elements)
 __device__ __forceinline__ uint2 tr4dsc(const uint16_t* img, int r0, int c0, int lo) {
-  const uint16_t* p = img + (r0 + (lo >> 2)) * 32 + c0 + 4 * (lo & 3);
+  const uint16_t* p = img + (r0 + (lo >> 2)) * P + c0 + 4 * (lo & 3);
   const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
   return __builtin_bit_cast(uint2, v);
 }
@@ -403,12 +404,15 @@ __global__ void __launch_bounds__(NTH, MINW) attn_bwd_kv_kernel(AttnArgs a) {
 // split kernels, its chunk loop ~20 us per iteration; bench/attn_probe.py phase stamps.)
 constexpr int FUSED_MAXW = LMAX / 16;
 constexpr int DSC = 32;  // queries per chunk
+// dS image row pitch (elements): 96-byte rows put the 8 rows x 32 bytes of a transpose-read half
+// wave on disjoint banks (64-byte rows: 2-way) and halve the store conflicts (8-way -> 4-way)
+constexpr int DSP = 48;
 
 __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Qs[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Gs[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t dSs[2][LMAX * DSC];  // [key][query of the chunk]
+  __shared__ __attribute__((aligned(16))) uint16_t dSs[2][LMAX * DSP];  // [key][query of the chunk]
   __shared__ __attribute__((aligned(16))) float lse_s[LMAX];
   __shared__ __attribute__((aligned(16))) float del_s[LMAX];
   const int b = blockIdx.z, h = blockIdx.y;
@@ -471,7 +475,7 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
   }
   // the dS rows of a key tile without a wave (odd ntile: the last 32-key step's upper half) are
   // read by the dQ products: keep them zero (uninitialised LDS could hold NaN patterns)
-  for (int i = threadIdx.x; i < 2 * LMAX * DSC / 8; i += nthr) *(uint4*)(&dSs[0][0] + 8 * i) = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = threadIdx.x; i < 2 * LMAX * DSP / 8; i += nthr) *(uint4*)(&dSs[0][0] + 8 * i) = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   if (stamp) stamp[1] = (float)(__builtin_amdgcn_s_memrealtime() - t_start);
 
@@ -494,7 +498,7 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
       for (int kq = 0; kq < nkey32; ++kq) {
         // A: row = query 16qh + lo, k = keys 32kq + {4hi + j, 16 + 4hi + j} (transposed reads of the
         // [key][query] image); B: k = the same keys, n = d 16nt + lo (transposed reads of K)
-        const uint2 a0 = tr4dsc(dsc, 32 * kq + 4 * hi, 16 * qh, lo), a1 = tr4dsc(dsc, 32 * kq + 16 + 4 * hi, 16 * qh, lo);
+        const uint2 a0 = tr4dsc<DSP>(dsc, 32 * kq + 4 * hi, 16 * qh, lo), a1 = tr4dsc<DSP>(dsc, 32 * kq + 16 + 4 * hi, 16 * qh, lo);
         const bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(a0.x, a0.y, a1.x, a1.y));
         dq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
             av, tr_operand(Ks, 32 * kq + 4 * hi, 32 * kq + 16 + 4 * hi, 16 * nt, lo), dq, 0, 0, 0);
@@ -543,7 +547,7 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
     // consecutive queries 16u + 4hi .. +3
 #pragma unroll
     for (int u = 0; u < 2; ++u)
-      *(uint2*)(dsc + (k0 + lo) * DSC + 16 * u + 4 * hi) =
+      *(uint2*)(dsc + (k0 + lo) * DSP + 16 * u + 4 * hi) =
           make_uint2(pack2(ds2[u][0], ds2[u][1]), pack2(ds2[u][2], ds2[u][3]));
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
