@@ -73,6 +73,11 @@ def _dt(t: torch.Tensor) -> int:
     return 2 if t.dtype == torch.float16 else 1
 
 
+# modelled per-CU rate of the wgrad kernel (ROCKET_WGRAD_RATE_CU: the split-K choice's GEMM-vs-slab
+# trade-off; 3.5e12 = ~0.9 PF/s over 256 CUs)
+WGRAD_RATE_CU = float(os.environ.get("ROCKET_WGRAD_RATE_CU", "3.5e12"))
+
+
 @functools.lru_cache(maxsize=None)
 def _wgrad_split(cout: int, ncol: int, pixels: int) -> int:
     """K-split of a conv weight gradient (few output tiles, long pixel reduction): minimise
@@ -80,7 +85,7 @@ def _wgrad_split(cout: int, ncol: int, pixels: int) -> int:
     (each split writes one f32 [Cout][R*S*Cin] slab that the combine launch re-reads)."""
     bm, per_cu = (64, 3) if cout <= 64 else (128, 2)
     tiles = -(-cout // bm) * -(-ncol // 128)
-    rate_cu = 3.5e12  # sustained bf16 FLOP/s per CU of this kernel (~0.9 PF/s over 256 CUs)
+    rate_cu = WGRAD_RATE_CU  # sustained bf16 FLOP/s per CU of this kernel
     best, arg = None, 1
     for s in range(1, 257):
         if s > 1 and pixels // s < 256:
