@@ -266,6 +266,9 @@ RK_API int rk_gemm(const void* a, int a_dt, int64_t lda, int a_trans, const void
                    void* c_pre, const float* bias, int act, int accumulate, float* rowsum, int M, int N, int K,
                    int splitk, int cfg, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
+  // operands are bf16 or f32 (anything else would be read with the wrong element size)
+  auto dt_ok = [](int d) { return d == F32 || d == BF16; };
+  if (!dt_ok(a_dt) || !dt_ok(b_dt) || !dt_ok(c_dt)) return (int)hipErrorInvalidValue;
   GemmArgs g;
   g.a = a; g.a_mask = a_mask; g.b = b; g.c = c; g.c_pre = c_pre; g.bias = bias; g.rowsum = rowsum;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ld_mask = ld_mask;

@@ -758,10 +758,25 @@ int launch_pp(const MArgs& g, int a_kmaj, int b_kmaj, hipStream_t s) {
 constexpr int kTileBK[] = {32, 64, 64, 64, 64, 32};
 
 // dst[i] (+)= sum_s part[s][i]: the combine of a library split-K weight gradient (strided-batched
-// partial products, bf16 or f32) straight into the fp32 weight.grad — one pass instead of a
+// partial products, bf16 / fp16 or f32) straight into the fp32 weight.grad — one pass instead of a
 // reduction launch, a temporary and an accumulation launch.  8 elements per thread, all split
-// loads issued before the first add.
-template <bool BF>
+// loads issued before the first add.  DT: 0 f32, 1 bf16, 2 fp16 (the _lib dtype codes).
+template <int DT>
+__device__ __forceinline__ void slab_add16(float (&acc)[8], const uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if constexpr (DT == 1) {
+      acc[2 * k] += __uint_as_float(w[k] << 16);
+      acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+    } else {
+      acc[2 * k] += h2f((uint16_t)(w[k] & 0xffffu));
+      acc[2 * k + 1] += h2f((uint16_t)(w[k] >> 16));
+    }
+  }
+}
+
+template <int DT>
 __global__ void __launch_bounds__(256) slab_acc_kernel(const void* __restrict__ part, int splits, int64_t count,
                                                        float* __restrict__ dst, int accumulate) {
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
@@ -777,19 +792,12 @@ __global__ void __launch_bounds__(256) slab_acc_kernel(const void* __restrict__ 
   }
   int s = 0;
   for (; s + 4 <= splits; s += 4) {
-    if constexpr (BF) {
+    if constexpr (DT != 0) {
       uint4 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) v[u] = *(const uint4*)((const uint16_t*)part + (int64_t)(s + u) * count + i);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          acc[2 * k] += __uint_as_float(w[k] << 16);
-          acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
-        }
-      }
+      for (int u = 0; u < 4; ++u) slab_add16<DT>(acc, v[u]);
     } else {
       float4 v[4][2];
 #pragma unroll
@@ -806,14 +814,8 @@ __global__ void __launch_bounds__(256) slab_acc_kernel(const void* __restrict__ 
     }
   }
   for (; s < splits; ++s) {
-    if constexpr (BF) {
-      const uint4 v = *(const uint4*)((const uint16_t*)part + (int64_t)s * count + i);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        acc[2 * k] += __uint_as_float(w[k] << 16);
-        acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
-      }
+    if constexpr (DT != 0) {
+      slab_add16<DT>(acc, *(const uint4*)((const uint16_t*)part + (int64_t)s * count + i));
     } else {
       const float* p = (const float*)part + (int64_t)s * count + i;
       const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
@@ -827,15 +829,17 @@ __global__ void __launch_bounds__(256) slab_acc_kernel(const void* __restrict__ 
 
 }  // namespace
 
-// dst[count] (+)= sum over `splits` partial arrays part[s][count] (dt 0 f32 / 1 bf16); count % 8 == 0,
+// dst[count] (+)= sum over `splits` partial arrays part[s][count] (dt 0 f32 / 1 bf16 / 2 fp16); count % 8 == 0,
 // 16-byte aligned pointers.
 RK_API int rk_slab_acc(const void* part, int dt, int splits, int64_t count, float* dst, int accumulate,
                        hipStream_t s) {
   if (count <= 0) return 0;
-  if (count % 8 || splits < 1 || ((uintptr_t)part | (uintptr_t)dst) % 16) return (int)hipErrorInvalidValue;
+  if (count % 8 || splits < 1 || dt < 0 || dt > 2 || ((uintptr_t)part | (uintptr_t)dst) % 16)
+    return (int)hipErrorInvalidValue;
   const int64_t blocks = (count / 8 + 255) / 256;
-  if (dt == 1) slab_acc_kernel<true><<<(unsigned)blocks, 256, 0, s>>>(part, splits, count, dst, accumulate);
-  else slab_acc_kernel<false><<<(unsigned)blocks, 256, 0, s>>>(part, splits, count, dst, accumulate);
+  if (dt == 1) slab_acc_kernel<1><<<(unsigned)blocks, 256, 0, s>>>(part, splits, count, dst, accumulate);
+  else if (dt == 2) slab_acc_kernel<2><<<(unsigned)blocks, 256, 0, s>>>(part, splits, count, dst, accumulate);
+  else slab_acc_kernel<0><<<(unsigned)blocks, 256, 0, s>>>(part, splits, count, dst, accumulate);
   return (int)hipGetLastError();
 }
 

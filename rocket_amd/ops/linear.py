@@ -163,6 +163,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         out_dtype = torch.bfloat16 if (_autocast_on() or x.dtype == torch.bfloat16) else torch.float32
     if weight.dtype != torch.float32 and weight.dtype != torch.bfloat16:
         weight = weight.float()
+    if x.dtype != torch.float32 and x.dtype != torch.bfloat16:  # the kernel reads bf16 / f32 operands
+        x = x.float()
     return _Linear.apply(x, weight, bias, act, out_dtype)
 
 

@@ -224,7 +224,7 @@ def test_lib_direct_grads_split(monkeypatch, f32, direct):
     assert _rel(m.bias.grad, want_b) < 1e-4
 
 
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("splits", [1, 3, 4, 9])
 def test_slab_acc(dt, splits):
     from rocket_amd.ops import _lib
@@ -238,6 +238,31 @@ def test_slab_acc(dt, splits):
     _lib.check(_lib.kernels().rk_slab_acc(part.data_ptr(), _lib.dtype_code(part), splits, dst.numel(),
                                           dst.data_ptr(), 0, _lib.stream_ptr(dst.device)), "rk_slab_acc")
     torch.testing.assert_close(dst, part.float().sum(0), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("direct", [False, True])
+def test_lib_linear_fp16_split(direct):
+    """LibLinear (ViT head / patch-embed path) under fp16 autocast with a split-K weight gradient:
+    the fp16 partial products are combined by rk_slab_acc's fp16 path (it used to read them as
+    fp32 - an out-of-bounds read that faulted the fp16 ViT bench)."""
+    from rocket_amd.ops.linear import LibLinear, _wgrad_splits
+
+    torch.manual_seed(7)
+    m = LibLinear(384, 768).cuda()
+    if direct:
+        for p in m.parameters():
+            p.grad = torch.full_like(p, 0.5)
+            p._rocket_direct_grad = True
+    x = _r(8192, 384)
+    g = _r(8192, 768)
+    assert _wgrad_splits(8192, 768, 384) > 1
+    with torch.autocast("cuda", dtype=torch.float16):
+        y = m(x)
+    assert y.dtype == torch.float16
+    y.backward(g)
+    base = 0.5 if direct else 0.0
+    assert _rel(m.weight.grad, base + g.float().t() @ x.float()) < 5e-3
+    assert _rel(m.bias.grad, base + g.float().sum(0)) < 1e-3
 
 
 @pytest.mark.parametrize("M,N", [(25216, 3072), (300, 136)])
