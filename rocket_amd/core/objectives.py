@@ -204,9 +204,13 @@ class Optimizer(Capsule):
 
     # ---------------------------------------------------- HIP-graph protocol
     def graph_supported(self) -> bool:
-        # fp16 steps are not captured: the scaler reports skipped steps through a host copy
+        # fp16: only the device-resident scaler is capturable (check + unscale-in-update + scale
+        # rule are device launches); torch's GradScaler reads found_inf on the host
+        from rocket_amd.runtime.amp import FusedGradScaler
+
+        scaler = self._accelerator.scaler
         return (hasattr(self._optimizer, "fused_zero_ok") and self._optimizer.fused_zero_ok()
-                and self._accelerator.scaler is None)
+                and (scaler is None or isinstance(scaler, FusedGradScaler)))
 
     def graph_token(self):
         return self._optimizer.optimizer.version
@@ -239,12 +243,21 @@ class Optimizer(Capsule):
             if getattr(inner, "epilogue_done", False):
                 inner.epilogue_done = False  # the gradient producer applied this step's update
                 return
+            scaler = self._accelerator.scaler
+            if scaler is not None:
+                scaler.step_device(inner, zero_grads=True)  # flag check + scaled update, in-graph
+                return
             inner.launch(zero_grads=True)
 
     def graph_host(self, attrs: Attributes) -> None:
         inner = self._optimizer.optimizer
         if getattr(inner, "epilogue_armed", False):
             inner.epilogue_armed = False
+        scaler = self._accelerator.scaler
+        if scaler is not None and self._accelerator.sync_gradients:
+            # the skipped-step flag of the replayed update: copied behind it, read only if asked
+            scaler.record_last()
+            self._optimizer.step_was_skipped_lazy()
         self.post(attrs)
 
     def destroy(self, attrs: Attributes | None = None) -> None:

@@ -17,7 +17,8 @@ two launches with no host synchronisation:
 
 Whether a step was skipped is only needed by the LR scheduler wrapper (accelerate does not step
 the scheduler after a skipped optimizer step); that value is copied to pinned memory behind the
-update and read lazily.  Optimizers that are not fused fall back to the torch primitives on the
+update and read lazily.  The two launches are graph-capturable (``step_device``): fp16 steps are
+captured like bf16 ones, the flag copy being enqueued after each replay.  Optimizers that are not fused fall back to the torch primitives on the
 same device state.  ``state_dict`` uses ``torch.amp.GradScaler``'s format (``scaler.pt``
 checkpoints are interchangeable).
 """
@@ -105,6 +106,23 @@ class FusedGradScaler:
         self._update_host_side()
         self._record_last()
         return out
+
+    def step_device(self, optimizer, zero_grads: bool = False) -> None:
+        """The device part of a fused scaled step (flag check + update with in-kernel unscale and
+        scale rule): graph-capturable; ``record_last`` after the replay publishes the skip flag."""
+        if id(optimizer) not in self._unscaled:
+            optimizer.amp_check(self.state)
+        else:
+            self.state[INV] = 1.0
+        optimizer.amp = self.state
+        try:
+            optimizer.launch(zero_grads=zero_grads)
+        finally:
+            optimizer.amp = None
+        self._unscaled.clear()
+
+    def record_last(self) -> None:
+        self._record_last()
 
     def _update_host_side(self) -> None:
         """The scale update for a step that did not run through the fused optimizer kernel."""

@@ -85,6 +85,10 @@ class EngineOptimizer:
             self._skip_lazy = False
         return self._skipped
 
+    def step_was_skipped_lazy(self) -> None:
+        """A scaled update ran on the device (e.g. in a replayed graph): resolve the flag on demand."""
+        self._skip_lazy = True
+
     @step_was_skipped.setter
     def step_was_skipped(self, v: bool) -> None:
         self._skipped, self._skip_lazy = bool(v), False

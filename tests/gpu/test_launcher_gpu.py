@@ -102,3 +102,53 @@ def test_eval_looper_meter_on_fused_lenet(tmp_path):
         logging_dir=str(tmp_path), mixed_precision="bf16", num_epochs=2, destroy_process_group_after_launch=False,
     ).launch()
     assert sum(seen) == 2000  # 1000 eval samples per epoch (last batch 232)
+
+
+def test_fp16_step_is_captured_and_matches_eager(tmp_path):
+    """fp16 steps with the device-resident scaler replay as graphs (flag check + scaled update
+    in-graph, the skip flag copied after each replay for the LR scheduler) and give the eager
+    run's weights, loss scale and learning rate."""
+    from rocket_amd.ops.optim import FusedSGD
+
+    class Mlp(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.net = torch.nn.Sequential(torch.nn.Flatten(), torch.nn.Linear(784, 128), torch.nn.ReLU(),
+                                           torch.nn.Linear(128, 10))
+
+        def forward(self, batch):
+            return (batch[0], batch[1], self.net(batch[0]))
+
+    class Grab(rocket.Capsule):  # keeps the engine's scaler for after the launch
+        def __init__(self):
+            super().__init__(statefull=False)
+
+        def setup(self, attrs=None):
+            super().setup(attrs)
+            held["scaler"] = self._accelerator.scaler
+
+    held = {}
+    data = _data(2048)
+    runs = {}
+    for capture in (False, True):
+        torch.manual_seed(0)
+        net = Mlp().cuda()
+        opt = FusedSGD(net.parameters(), lr=0.05, momentum=0.9)
+        sched = torch.optim.lr_scheduler.StepLR(opt, 3, gamma=0.5)
+        mod = rocket.Module(net, [rocket.Loss(CrossEntropy()), rocket.Optimizer(opt), rocket.Scheduler(sched)],
+                            capture=capture, warmup=2)
+        launcher = rocket.Launcher(
+            [rocket.Looper([rocket.Dataset(rocket.DeviceTensorDataset(*data), batch_size=256), mod, Grab()],
+                           progress=False)],
+            logging_dir=str(tmp_path / str(capture)), num_epochs=1, mixed_precision="fp16",
+            destroy_process_group_after_launch=False)
+        launcher.launch()
+        scale = held["scaler"].get_scale()
+        runs[capture] = ([p.detach().clone() for p in net.parameters()], sched.get_last_lr()[0], scale,
+                         mod._graphs)
+    g = runs[True][3]
+    assert g is not None and g.captures >= 1 and g.replays >= 3, (g.disabled_reason, g.captures, g.replays)
+    assert runs[True][1] == runs[False][1] < 0.05  # same skipped steps -> same scheduler steps
+    assert runs[True][2] == runs[False][2]
+    for a, b in zip(runs[False][0], runs[True][0]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
