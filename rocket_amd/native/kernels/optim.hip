@@ -12,7 +12,8 @@
 // Optional bf16 shadows: a tensor record may carry an index map (int32 [n][2], -1 = none) and a
 // bf16 buffer; every updated element is also written, rounded to bf16, to buf[map[i][0]] and
 // buf[map[i][1]] — or, with the map pointer 1 ("dense"), to buf[i] (a bf16 copy of the weights
-// that GEMMs read directly instead of casting the fp32 master every forward).  A kernel that consumes the weights as pre-arranged bf16 MFMA fragments (the
+// that GEMMs read directly instead of casting the fp32 master every forward; map pointer 2: the
+// same as an fp16 copy, for fp16 autocast).  A kernel that consumes the weights as pre-arranged bf16 MFMA fragments (the
 // fused LeNet's fragment table) then needs no per-step re-layout launch.
 //
 // Optional AMP (fp16 dynamic loss scaling, all on the device): rk_amp_check flags non-finite
@@ -40,7 +41,7 @@ struct Map4 {
   int4 a, b;
 };
 __device__ __forceinline__ Map4 shadow_map4(const TensorRec& tr, int64_t i) {
-  if (tr.shadow_map <= kDenseShadow) return Map4{};
+  if (tr.shadow_map <= kDenseShadowF16) return Map4{};
   const int4* m = (const int4*)((const int2*)tr.shadow_map + i);
   return Map4{m[0], m[1]};
 }
@@ -51,6 +52,11 @@ __device__ __forceinline__ void shadow_store4(const TensorRec& tr, int64_t i, co
   if (tr.shadow_map == kDenseShadow) {
     *(uint2*)(buf + i) = make_uint2((uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
                                     (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+    return;
+  }
+  if (tr.shadow_map == kDenseShadowF16) {
+    *(uint2*)(buf + i) = make_uint2((uint32_t)f2h(v.x) | ((uint32_t)f2h(v.y) << 16),
+                                    (uint32_t)f2h(v.z) | ((uint32_t)f2h(v.w) << 16));
     return;
   }
   const int idx[8] = {mp.a.x, mp.a.y, mp.a.z, mp.a.w, mp.b.x, mp.b.y, mp.b.z, mp.b.w};

@@ -7,13 +7,15 @@
 namespace rk_opt {
 
 using rk::f2bf;
+using rk::f2h;
 
 struct TensorRec {  // 8 x int64: a parameter tensor as the update kernels see it
   int64_t p, g, s0, s1, n, group;
-  int64_t shadow_map, shadow_buf;  // int32 [n][2] (or 1 = dense) / bf16 buffer, or 0
+  int64_t shadow_map, shadow_buf;  // int32 [n][2] (or 1 = dense bf16, 2 = dense fp16) / buffer, or 0
 };
 
-constexpr int64_t kDenseShadow = 1;
+constexpr int64_t kDenseShadow = 1;     // buffer laid out like p, bf16
+constexpr int64_t kDenseShadowF16 = 2;  // buffer laid out like p, fp16 (fp16 autocast compute copies)
 
 struct AdamHyper {  // 8 floats per group
   float lr, beta1, beta2, eps, wd, decoupled, maximize, pad;
@@ -21,6 +23,10 @@ struct AdamHyper {  // 8 floats per group
 
 __device__ __forceinline__ void shadow_store(const TensorRec& tr, int64_t i, float v) {
   uint16_t* buf = (uint16_t*)tr.shadow_buf;
+  if (tr.shadow_map == kDenseShadowF16) {
+    buf[i] = f2h(v);
+    return;
+  }
   const uint16_t b = f2bf(v);
   if (tr.shadow_map == kDenseShadow) {
     buf[i] = b;
@@ -139,7 +145,7 @@ __device__ __forceinline__ EpiElem epi_fetch(const TensorRec& tr, int64_t i) {
   e.p = ((const float*)tr.p)[i];
   e.m = ((const float*)tr.s0)[i];
   e.v = ((const float*)tr.s1)[i];
-  e.map = tr.shadow_map > kDenseShadow ? ((const int2*)tr.shadow_map)[i] : make_int2(-1, -1);
+  e.map = tr.shadow_map > kDenseShadowF16 ? ((const int2*)tr.shadow_map)[i] : make_int2(-1, -1);
   return e;
 }
 __device__ __forceinline__ void epi_apply(const TensorRec& tr, const AdamStep& k, int64_t i, EpiElem e, float g,
@@ -151,6 +157,8 @@ __device__ __forceinline__ void epi_apply(const TensorRec& tr, const AdamStep& k
   ((float*)tr.g)[i] = zero_grads ? 0.f : g;
   if (tr.shadow_map == kDenseShadow) {
     ((uint16_t*)tr.shadow_buf)[i] = f2bf(e.p);
+  } else if (tr.shadow_map == kDenseShadowF16) {
+    ((uint16_t*)tr.shadow_buf)[i] = f2h(e.p);
   } else if (tr.shadow_map) {
     const uint16_t b = f2bf(e.p);
     if (e.map.x >= 0) ((uint16_t*)tr.shadow_buf)[e.map.x] = b;

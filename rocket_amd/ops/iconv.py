@@ -7,7 +7,7 @@ split-K combine of the weight gradient) — no im2col buffer, no MIOpen solution
 ``SubTensorOp`` casts:
 
 * forward: gathered NHWC activations x channels_last weights (read as a bf16 copy a fused
-  optimizer keeps current: dense bf16 shadow, ``_bf16_copy``; fp16: a per-forward cast);
+  optimizer keeps current: dense bf16 / fp16 shadow, ``_lowp_copy``);
 * dgrad: dY gathered with the flipped taps x the weights read K-major per tap; stride 2 as the
   four parity classes of dX pixels (each a stride-1 gather over its taps) in one launch;
 * wgrad: dY x gathered X, split-K over the pixels into f32 slabs, accumulated straight into a

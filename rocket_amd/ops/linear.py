@@ -295,16 +295,21 @@ def lib_param_grads(dy2: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, b
     return dw, db
 
 
-def _bf16_copy(module, name: str, p: torch.Tensor):
-    """bf16 copy of parameter ``p``, registered as its dense bf16 shadow: a fused optimizer keeps
-    it current while updating ``p`` (no per-forward cast).  Re-cast here whenever ``p`` was written
-    by anything else (its autograd version moved) or no fused optimizer maintains it."""
+def _shadow_copy(module, name: str, p: torch.Tensor, dtype: torch.dtype):
+    """16-bit (bf16 / fp16) copy of parameter ``p``, registered as its dense shadow: a fused
+    optimizer keeps it current while updating ``p`` (no per-forward cast).  Re-cast here whenever
+    ``p`` was written by anything else (its autograd version moved), no fused optimizer maintains
+    it, or the parameter's registered shadow is another buffer (autocast dtype switched)."""
     buf = getattr(module, name, None)
-    if buf is None or buf.shape != p.shape or buf.device != p.device or buf.stride() != p.stride():
-        buf = torch.empty_like(p, dtype=torch.bfloat16)
+    if (buf is None or buf.dtype != dtype or buf.shape != p.shape or buf.device != p.device
+            or buf.stride() != p.stride()):
+        buf = torch.empty_like(p, dtype=dtype)
         setattr(module, name, buf)
         setattr(module, name + "_version", None)
+    sh = getattr(p, "_rocket_bf16_shadow", None)
+    if sh is None or sh[1] is not buf:
         p._rocket_bf16_shadow = (None, buf)
+        setattr(module, name + "_version", None)  # the optimizer maintained another buffer so far
     if not (getattr(p, "_rocket_shadow_live", False) and getattr(module, name + "_version") == p._version):
         with torch.no_grad():
             buf.copy_(p)
@@ -312,20 +317,15 @@ def _bf16_copy(module, name: str, p: torch.Tensor):
     return buf
 
 
+def _bf16_copy(module, name: str, p: torch.Tensor):
+    """bf16 copy of ``p`` maintained by the fused optimizer (:func:`_shadow_copy`)."""
+    return _shadow_copy(module, name, p, torch.bfloat16)
+
+
 def _lowp_copy(module, name: str, p: torch.Tensor, dtype: torch.dtype):
-    """16-bit copy of parameter ``p`` in the autocast compute dtype: the optimizer-maintained bf16
-    shadow (:func:`_bf16_copy`), or for fp16 a per-forward cast into a persistent buffer (the fused
-    optimizers' shadows are bf16 only)."""
-    if dtype == torch.bfloat16:
-        return _bf16_copy(module, name, p)
-    key = name + "_f16"
-    buf = getattr(module, key, None)
-    if buf is None or buf.shape != p.shape or buf.device != p.device or buf.stride() != p.stride():
-        buf = torch.empty_like(p, dtype=dtype)
-        setattr(module, key, buf)
-    with torch.no_grad():
-        buf.copy_(p)
-    return buf
+    """16-bit copy of parameter ``p`` in the autocast compute dtype, optimizer-maintained in both
+    cases (dense bf16 or dense fp16 shadow); the fp16 copy lives under ``name + "_f16"``."""
+    return _shadow_copy(module, name if dtype == torch.bfloat16 else name + "_f16", p, dtype)
 
 
 class LibLinear(torch.nn.Linear):
@@ -341,9 +341,10 @@ class LibLinear(torch.nn.Linear):
                 and torch.is_grad_enabled()):
             cdtype = torch.get_autocast_dtype("cuda")
             w16 = b16 = None
-            if cdtype == torch.bfloat16 and self.weight.dtype == torch.float32 and self.weight.is_contiguous():
-                w16 = _bf16_copy(self, "_w16", self.weight)
-                b16 = _bf16_copy(self, "_b16", self.bias)
+            if (cdtype in (torch.bfloat16, torch.float16) and self.weight.dtype == torch.float32
+                    and self.weight.is_contiguous()):
+                w16 = _lowp_copy(self, "_w16", self.weight, cdtype)
+                b16 = _lowp_copy(self, "_b16", self.bias, cdtype)
             return _LibLinear.apply(x, self.weight, self.bias, cdtype, w16, b16)
         return super().forward(x)
 

@@ -149,11 +149,15 @@ class _FusedBase(torch.optim.Optimizer):
 
         A consumer registers ``p._rocket_bf16_shadow = (index int32 [numel, 2], bf16 buffer)``;
         every update then also writes bf16(p[i]) to ``buffer[index[i, 0/1]]`` (-1 = skip).  With
-        ``index = None`` the shadow is dense: ``buffer`` is a bf16 tensor laid out like ``p``."""
+        ``index = None`` the shadow is dense: ``buffer`` is a bf16 (or fp16) tensor laid out like ``p``."""
         sh = getattr(p, "_rocket_bf16_shadow", None)
         if sh is None:
             return (0, 0)
         idx, buf = sh
+        if idx is None and buf.dtype == torch.float16:  # dense fp16 copy (fp16 autocast compute)
+            if buf.shape != p.shape or buf.stride() != p.stride() or buf.device != p.device:
+                raise RuntimeError("dense fp16 shadow: buffer must have the parameter's shape, layout and device")
+            return (2, buf.data_ptr())
         if buf.dtype != torch.bfloat16 or buf.device != p.device:
             raise RuntimeError("bf16 shadow: expected a bf16 buffer on the parameter's device")
         if idx is None:

@@ -175,3 +175,33 @@ def test_optimizer_maintains_dense_bf16_weight_copy():
     with torch.autocast("cuda", dtype=torch.bfloat16):
         ref = torch.nn.functional.linear(x, lin.weight, lin.bias)
         assert torch.equal(lin(x), ref)
+
+
+@pytest.mark.parametrize("kind", ["adamw", "sgd"])
+def test_optimizer_maintains_dense_fp16_weight_copy(kind):
+    """fp16 autocast: LibLinear's fp16 weight copy is a dense fp16 shadow (map pointer 2) that the
+    fused update writes; switching the autocast dtype re-registers the bf16 one, never a stale copy."""
+    from rocket_amd.ops.linear import LibLinear
+    from rocket_amd.ops.optim import FusedAdamW, FusedSGD
+
+    torch.manual_seed(7)
+    lin = LibLinear(64, 48).cuda()
+    opt = FusedAdamW(lin.parameters(), lr=1e-2) if kind == "adamw" else FusedSGD(lin.parameters(), lr=1e-2,
+                                                                                 momentum=0.9)
+    x = torch.randn(32, 64, device="cuda")
+    for dt in (torch.float16, torch.float16, torch.bfloat16, torch.float16):
+        with torch.autocast("cuda", dtype=dt):
+            y = lin(x)
+        y.float().square().mean().backward()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+    torch.cuda.synchronize()
+    assert torch.equal(lin._w16_f16, lin.weight.detach().to(torch.float16))
+    assert torch.equal(lin._b16_f16, lin.bias.detach().to(torch.float16))
+    assert lin._w16_f16_version == lin.weight._version
+    with torch.autocast("cuda", dtype=torch.float16):
+        ref = torch.nn.functional.linear(x, lin.weight, lin.bias)
+        assert torch.equal(lin(x), ref)
+    with torch.autocast("cuda", dtype=torch.bfloat16):  # the bf16 copy was re-cast, not stale
+        ref = torch.nn.functional.linear(x, lin.weight, lin.bias)
+        assert torch.equal(lin(x), ref)
