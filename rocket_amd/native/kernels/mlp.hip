@@ -622,6 +622,10 @@ RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* cons
                               float* const* db, const int* Ns, const int* Ks, int M, const float* slab, int slab_rows,
                               int slab_width, float* const* slab_dst, const int* slab_bound, const LossFin* loss,
                               const WgradEpi* epi, float gscale, int norm_by_count, hipStream_t s) {
+  // the staged rows request (rk_mlp3_set_rows) belongs to THIS call whatever happens: taken and
+  // cleared first, so an argument error below cannot leave it attached to a later launch
+  const RowsReq rows_req = g_rows;
+  g_rows = RowsReq{};
   if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
   WgradArgs a{};
   a.trace = g_wgrad_trace;
@@ -688,15 +692,14 @@ RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* cons
       if ((float*)a.rsl[i].g != slab_dst[i] || a.rsl[i].group >= epi->ngroups) return (int)hipErrorInvalidValue;
     }
   }
-  if (g_rows.table) {  // consumes the staged rows request (rk_mlp3_set_rows)
-    a.rn_table = g_rows.table;
-    a.rn_meta = g_rows.meta;
-    a.rn_rows = g_rows.rows;
-    a.rn_cur = g_rows.n_cur;
-    a.rn_bs = g_rows.bs;
+  if (rows_req.table) {  // the staged rows request: one more block of this launch
+    a.rn_table = rows_req.table;
+    a.rn_meta = rows_req.meta;
+    a.rn_rows = rows_req.rows;
+    a.rn_cur = rows_req.n_cur;
+    a.rn_bs = rows_req.bs;
     a.has_rows = 1;
     extra += 1;
-    g_rows = RowsReq{};
   }
   mlp3_wgrad_kernel<<<tiles + extra, NT, 0, s>>>(a);
   return (int)hipGetLastError();

@@ -485,9 +485,9 @@ class _LeNetFused(torch.autograd.Function):
         bounds = (ctypes.c_int * 5)(0, sizes[0], sizes[0] + sizes[1], sizes[0] + sizes[1] + sizes[2], sum(sizes))
         epi, opt = _optimizer_epilogue(params, direct)
         pend, ctx.rows_pend = getattr(ctx, "rows_pend", None), None
-        if pend is not None and not pend.advanced:  # the step's batch cursor, as one more block of this launch
+        rows_staged = pend is not None and not pend.advanced
+        if rows_staged:  # the step's batch cursor, as one more block of this launch
             _lib.check(lib.rk_mlp3_set_rows(*pend.advance_args()), "rk_mlp3_set_rows")
-            pend.mark_advanced()
         _lib.check(lib.rk_mlp3_wgrad_loss(3, P(*[q[0].data_ptr() for q in probs]), P(*[q[1].data_ptr() for q in probs]),
                                           P(*[q[2].data_ptr() for q in probs]), P(*[q[3].data_ptr() for q in probs]),
                                           I(*[q[4] for q in probs]), I(*[q[5] for q in probs]), N, slab.data_ptr(),
@@ -497,6 +497,8 @@ class _LeNetFused(torch.autograd.Function):
                                           ctypes.byref(epi) if epi is not None else None, float(gscale),
                                           int(fin is not None), stream),
                    "rk_mlp3_wgrad_loss")
+        if rows_staged:
+            pend.mark_advanced()  # only once the launch that advances the cursor was accepted
         if opt is not None:
             opt.epilogue_done = True  # the optimizer's own launch for this step is skipped
         del keep  # partials: read by the wgrad launch (stream-ordered before any reuse)

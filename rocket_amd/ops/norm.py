@@ -288,21 +288,28 @@ class BiasLink:
     """Hand-off between a linear layer whose output ``r`` feeds ONLY an add-LayerNorm and that
     LayerNorm: the LN backward already streams dr (= the linear's output gradient), so it also
     forms dr's column sums — the linear's bias gradient — into ``db``; the linear's backward uses
-    them when its incoming gradient is exactly that dr (``dr_ptr``), instead of a column-sum pass
+    them when its incoming gradient is exactly that dr, unmodified (:meth:`take`), instead of a column-sum pass
     over its output gradient.  Lives on the autograd graph (both ctxs), like :class:`BwdLink`."""
 
-    __slots__ = ("bias", "db", "dr_ptr")
+    __slots__ = ("bias", "db", "dr", "dr_ver")
 
     def __init__(self, bias):
         self.bias = bias
         self.db = None
-        self.dr_ptr = None
+        self.dr = None  # the LN's dr (held: its storage cannot be recycled under another tensor)
+        self.dr_ver = None
 
     def take(self, dy: torch.Tensor):
-        """The finished bias gradient for incoming gradient ``dy``, or None (compute it yourself)."""
-        db, self.db = self.db, None
-        ok = db is not None and dy.data_ptr() == self.dr_ptr
-        self.dr_ptr = None
+        """The finished bias gradient for incoming gradient ``dy``, or None (compute it yourself).
+
+        ``dy`` must BE the LN's dr, unmodified: same storage, same shape, and the same version
+        counter value.  When the linear's output also feeds another op, autograd's input buffer may
+        sum that op's gradient into dr in place before handing it over (same pointer, bumped
+        ``_version``): then the link's column sums miss that contribution and are refused."""
+        db, dr, ver = self.db, self.dr, self.dr_ver
+        self.db = self.dr = self.dr_ver = None
+        ok = (db is not None and dr is not None and dy.data_ptr() == dr.data_ptr()
+              and dy.numel() == dr.numel() and dy._version == ver)
         return db if ok else None
 
 
@@ -375,7 +382,7 @@ class _AddLN(torch.autograd.Function):
                                  _lib.ptr(dbeta), _lib.ptr(rsum), rows, C, ws.data_ptr(), counter,
                                  _lib.stream_ptr(dev)), "rk_ln_bwd(add)")
         if link is not None:
-            link.db, link.dr_ptr = rsum, dr.data_ptr()
+            link.db, link.dr, link.dr_ver = rsum, dr, dr._version
         g = _finish(params, bufs, direct) if params else []
         gw = g[0] if weight is not None else None
         gb = g[-1] if bias is not None else None

@@ -145,6 +145,9 @@ class DataParallel(nn.Module):
         self._p2p = self._make_p2p()
         # native transport: per-bucket all-reduce on a side stream, one join before the optimizer
         self._native = None
+        # set (on every rank together) when an overlapped capture failed: captured sync steps then
+        # use two graphs with the host-issued reduction between them (runtime/graphs.py)
+        self.force_split = False
         if self._p2p is None and hasattr(self.comm, "make_reducer"):
             self._native = self.comm.make_reducer([b.flat for b in self.buckets])
 
@@ -276,7 +279,7 @@ class DataParallel(nn.Module):
           captured): two graphs with the host-issued bucket all-reduce between them."""
         if self._p2p is not None:
             return "inline"
-        if self._native is not None:
+        if self._native is not None and not self.force_split:
             return "overlap"
         return "split"
 

@@ -196,6 +196,12 @@ class P2PComm:
     def _reduce(self, t: torch.Tensor, scale: float) -> None:
         """``t <- scale * sum_ranks(t)`` for any dtype / size: fp32 staging in cap-sized chunks
         (integers and bytes below 2^24 are exact in fp32)."""
+        if not t.is_contiguous():
+            # reshape would return a copy: reduce a contiguous copy and write it back
+            tmp = t.contiguous()
+            self._reduce(tmp, scale)
+            t.copy_(tmp)
+            return
         flat = t.reshape(-1)
         f32 = flat if (flat.dtype == torch.float32 and flat.is_contiguous()) else flat.to(torch.float32)
         for off in range(0, f32.numel(), self.ar.cap):

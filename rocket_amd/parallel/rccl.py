@@ -7,8 +7,11 @@ caller's current HIP stream — graph-capturable, no ProcessGroupNCCL bookkeepin
 complete bucket is all-reduced on a dedicated high-priority HIP stream fenced by events, and
 the compute stream waits for all buckets once at the end of backward.
 
-Opt-in: ``Engine(comm="native")`` or ``ROCKET_NATIVE_COMM=1``; the default reducer transport
-is torch.distributed's RCCL process group.
+This is the engine's default data-parallel transport on GPUs (``Engine(comm="torch")`` or
+``ROCKET_NATIVE_COMM=0`` selects torch.distributed's RCCL process group instead).  Creation is
+agreed over the host group: if any rank fails, every rank falls back to the torch group together
+(``runtime/engine.py`` ``_dp_comm``); a failed overlapped capture likewise drops every rank to the
+two-graph ``split`` mode (``runtime/graphs.py``).
 """
 
 from __future__ import annotations
@@ -40,10 +43,16 @@ class RcclComm:
         self.device = device or ctx.device
         uid = None
         if self.rank == 0:
-            buf = ctypes.create_string_buffer(self.rt.rkr_unique_id_bytes())
-            check(self.rt.rkr_unique_id(buf), "ncclGetUniqueId")
-            uid = buf.raw
+            try:
+                buf = ctypes.create_string_buffer(self.rt.rkr_unique_id_bytes())
+                check(self.rt.rkr_unique_id(buf), "ncclGetUniqueId")
+                uid = buf.raw
+            except Exception:
+                uid = None  # still broadcast: the peers must not wait for an id that never comes
         uid = _comm.broadcast_object(uid, src=0)
+        # every rank enters ncclCommInitRank (a blocking collective bootstrap) or none does
+        if not _comm.all_ranks_agree(uid is not None):
+            raise RuntimeError("ncclGetUniqueId failed on rank 0")
         h = ctypes.c_void_p()
         idbuf = ctypes.create_string_buffer(uid, len(uid))
         check(self.rt.rkr_comm_init(ctypes.byref(h), self.world, self.rank, idbuf, self.device.index or 0),

@@ -82,11 +82,11 @@ class FusedGradScaler:
         unscaled = id(optimizer) in self._unscaled
         if isinstance(optimizer, _FusedBase) and not args and not kwargs:
             if not optimizer.prepare():
-                # no gradient to update: torch still runs the scale update on the (clear) flag,
-                # and this step's skip state and the unscaled set must not leak into the next
-                self._update_host_side()
-                self._record_last()
-                return None
+                # no gradient to update: torch.amp.GradScaler.step asserts here ("No inf checks
+                # were recorded for this optimizer") without touching the scale or the growth
+                # tracker; same here, after dropping this step's unscaled mark
+                self._unscaled.discard(id(optimizer))
+                raise AssertionError("No inf checks were recorded for this optimizer.")
             if not unscaled:
                 optimizer.amp_check(self.state)
             else:  # unscaled in place (and checked) already: unscale by 1 this time; the last

@@ -156,6 +156,20 @@ def all_gather_object(obj: Any) -> List[Any]:
     return out
 
 
+def all_ranks_agree(ok: bool) -> bool:
+    """True only when ``ok`` holds on EVERY rank (host gloo group; no device involvement).
+
+    Used wherever a rank-local outcome (a communicator init, a graph capture) picks between two
+    code paths that issue different collectives: all ranks must take the same branch or they
+    desynchronise and hang."""
+    ctx = context()
+    if not ctx.distributed:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctx.host_group)
+    return bool(t.item())
+
+
 def barrier() -> None:
     ctx = context()
     if ctx.distributed:

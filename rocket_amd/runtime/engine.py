@@ -359,12 +359,22 @@ class Engine:
         if self._native_comm is None:
             from rocket_amd.parallel.rccl import RcclComm
 
+            comm, err = None, None
             try:
-                self._native_comm = RcclComm(self.device)
-            except Exception as e:  # every rank takes the same branch: ncclCommInitRank is collective
-                logger.warning(f"native RCCL communicator unavailable ({e}); using the torch.distributed group")
+                comm = RcclComm(self.device)
+            except Exception as e:
+                err = e
+            # a failure can be rank-local (hipSetDevice, an allocation, a watchdog): the ranks agree
+            # over the host group, and ALL fall back together if any rank failed — a rank that fell
+            # back alone would issue different collectives from its peers and hang them
+            if not _comm.all_ranks_agree(err is None):
+                if comm is not None:
+                    comm.close()
+                logger.warning(f"native RCCL communicator unavailable on some rank ({err or 'peer failed'}); "
+                               "every rank uses the torch.distributed group")
                 self.comm_backend = "torch"
                 return None
+            self._native_comm = comm
         return self._native_comm
 
     def grad_owner(self, p):

@@ -378,14 +378,40 @@ class StepGraphs:
     def _capture(self, attrs: Attributes, tens: List[torch.Tensor], run: bool = True) -> _Captured:
         """Capture the micro-step for inputs ``tens``; ``run``: also replay it for this iteration."""
         pend, restore = self._bind_pending(attrs, tens, run)
+        rep = self._replica()
+        engine = self.mod._accelerator
+        # an overlapped step captures RCCL calls: a capture error may be rank-local, so the ranks
+        # agree on the outcome BEFORE anything runs, and all drop to split mode together
+        agree = (rep is not None and engine.sync_gradients and rep.capture_mode == "overlap"
+                 and engine.num_processes > 1)
         try:
-            v = self._capture_inner(attrs, tens, run, pend)
+            err = None
+            try:
+                v = self._capture_inner(attrs, tens, pend)
+            except Exception as e:
+                if not agree:
+                    raise
+                err, v = e, None
+            if agree:
+                from rocket_amd.runtime import comm as _comm
+
+                if not _comm.all_ranks_agree(err is None):
+                    logger.warning(f"overlapped capture failed on some rank ({err or 'peer failed'}); "
+                                   "every rank captures sync steps in split mode")
+                    rep.force_split = True
+                    torch.cuda.synchronize()
+                    v = self._capture_inner(attrs, tens, pend)
         finally:
             for b, old in restore:
                 b._rocket_pending = old
+        if run:
+            # the captured work has not run yet: replay it for this iteration
+            self._run(v, rep if len(v.graphs) > 1 else None)
+            attrs.batch = v.out
+            self._host(attrs)
         return v
 
-    def _capture_inner(self, attrs: Attributes, tens: List[torch.Tensor], run: bool, pend) -> _Captured:
+    def _capture_inner(self, attrs: Attributes, tens: List[torch.Tensor], pend) -> _Captured:
         engine = self.mod._accelerator
         v = _Captured()
         v.sync = engine.sync_gradients
@@ -437,13 +463,7 @@ class StepGraphs:
         v.rows_in_graph = pend is not None and pend.done
         self.captures += 1
         self.parts = max(self.parts, len(v.graphs))
-        logger.info(f"captured HIP graph(s) for sync={v.sync} ({len(v.graphs)} part(s))")
-        if not run:
-            return v
-        # the captured work has not run yet: replay it for this iteration
-        self._run(v, rep if split else None)
-        attrs.batch = v.out
-        self._host(attrs)
+        logger.info(f"captured HIP graph(s) for sync={v.sync} ({len(v.graphs)} part(s), mode={mode})")
         return v
 
     # ------------------------------------------------------------------ replay

@@ -227,3 +227,44 @@ def test_add_ln_forms_branch_bias_grad(mlp):
     for a, b in zip(gn, gt):
         assert _rel(a, b) < 3e-2, _rel(a, b)
     assert _rel(hn, ht) < 3e-2 and _rel(xn, xt) < 3e-2
+
+
+def test_bias_link_refused_with_second_consumer():
+    """The linear's output feeds the add-LayerNorm AND another op: the incoming gradient is dr plus
+    that op's gradient, so the LN's column sums of dr are not the bias gradient.  The link must be
+    refused (no hit) and the bias gradient must still equal the stock-torch composition."""
+    import rocket_amd.ops as ops
+    import rocket_amd.ops.mlinear as ml
+    from rocket_amd.ops.norm import FusedLayerNorm
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(2)
+    C = 128
+    branch = ml.MLinear(C, C).to(dev)
+    ln = FusedLayerNorm(C).to(dev)
+    x0 = torch.randn(4, 50, C, device=dev)
+    h0 = torch.randn(4, 50, C, device=dev)
+    gy = torch.randn(4, 50, C, device=dev)
+    gs = torch.randn(4, 50, C, device=dev)
+    gz = torch.randn(4, 50, C, device=dev)
+    grads = []
+    for fused in (True, False):
+        ops.set_fused(fused)
+        try:
+            for p in list(branch.parameters()) + list(ln.parameters()):
+                p.grad = None
+            hits = ml.BIAS_LINK_HITS
+            x, h = x0.clone().requires_grad_(), h0.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                r = branch(h)
+                s, y = ln.add_forward(x, r)
+                z = r.float() * 3.0  # second consumer of the linear's output
+            ((y.float() * gy).sum() + (s.float() * gs).sum() + (z * gz).sum()).backward()
+            torch.cuda.synchronize()
+            grads.append(([p.grad.float().clone() for p in branch.parameters()], ml.BIAS_LINK_HITS - hits))
+        finally:
+            ops.set_fused(True)
+    (gn, hits), (gt, _) = grads
+    assert hits == 0
+    for a, b in zip(gn, gt):
+        assert _rel(a, b) < 3e-2, _rel(a, b)
