@@ -88,6 +88,53 @@ def _spawn(n: int) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _weight_checksum(net) -> list:
+    """Two float64 sums over every parameter (plain and position-weighted): equal on every rank iff
+    the replicas ended identical (DP applies the same averaged update everywhere)."""
+    s0 = torch.zeros((), dtype=torch.float64, device=next(net.parameters()).device)
+    s1 = torch.zeros_like(s0)
+    off = 0
+    for p in net.parameters():
+        v = p.detach().reshape(-1).to(torch.float64)
+        w = (torch.arange(v.numel(), device=v.device, dtype=torch.float64) + off).remainder_(97.0)
+        s0 += v.sum()
+        s1 += (v * w).sum()
+        off += v.numel()
+    return [s0.item(), s1.item()]
+
+
+def _dp_record(mod, net, ctx, comm) -> dict:
+    """What ran: the data-parallel transport and capture mode, bucket sizes, how many ranks the
+    communicator spans, the capture counters, and whether the replicas ended bit-identical
+    (cross-rank weight checksums, compared on every rank)."""
+    from rocket_amd.parallel.ddp import DataParallel
+
+    rep = getattr(mod, "_module", None)
+    rec = {"world": ctx.world_size, "backend": ctx.backend}
+    if isinstance(rep, DataParallel):
+        c = rep.comm
+        if rep._p2p is not None:
+            transport = "p2p-xgmi"
+        elif rep._native is not None:
+            transport = "native-rccl"
+        else:
+            transport = "torch-" + str(ctx.backend)
+        rec.update(transport=transport, capture_mode=rep.capture_mode,
+                   bucket_mb=[round(b.flat.numel() * b.flat.element_size() / 2**20, 4) for b in rep.buckets],
+                   comm_ranks=int(getattr(c, "world", ctx.world_size)))
+    else:
+        rec.update(transport="none", capture_mode=None, bucket_mb=[], comm_ranks=1)
+    g = getattr(mod, "_graphs", None)
+    if g is not None:
+        rec["graph"] = {"captures": g.captures, "replays": g.replays, "parts": g.parts,
+                        "launch_lists": g.launch_lists}
+    sums = _weight_checksum(net)
+    parts = comm.all_gather_object(sums) if ctx.world_size > 1 else [sums]
+    rec["weight_checksum"] = sums
+    rec["replicas_identical"] = all(p == parts[0] for p in parts)
+    return rec
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -172,7 +219,7 @@ def main() -> int:
             rocket.Looper(
                 [
                     rocket.Dataset(data, batch_size=args.batch, shuffle=True, drop_last=True),
-                    rocket.Module(
+                    mod := rocket.Module(
                         net,
                         [rocket.Loss(CrossEntropy(fused=fused)), rocket.Optimizer(opt), rocket.Scheduler(sched)],
                         # every model's step is captured and replayed (ResNet-18: host 3.9 -> 0.56 ms/step,
@@ -217,6 +264,7 @@ def main() -> int:
 
     elapsed = timer.elapsed
     summ = timer.summary()
+    dp = _dp_record(mod, net, ctx, comm)
     stats = torch.tensor([elapsed, summ.get("step_ms_p50", 0.0)], dtype=torch.float64)
     if world > 1:
         parts = comm.all_gather_object(stats.tolist())
@@ -265,6 +313,7 @@ def main() -> int:
                 if fused else "torch-eager",
             },
             "wall_s": round(wall, 2),
+            "dp": dp,
         }
         print(json.dumps(rec), flush=True)
     comm.shutdown()

@@ -146,3 +146,65 @@ def test_overlapped_bucket_reduce_is_a_parallel_branch(monkeypatch):
     torch.cuda.synchronize()
     for p, e in zip(params, eager):
         torch.testing.assert_close(p.detach(), e, rtol=1e-5, atol=1e-6)
+
+
+def test_native_rccl_reducer_graph_structure(monkeypatch):
+    """The REAL native reducer (``parallel/rccl.py`` NativeReducer over an RcclComm, world 1 on the
+    single-GPU box) captured with forward/backward and the optimizer: the RCCL nodes it leaves in
+    the graph sit on branches parallel to backward work and precede the optimizer."""
+    monkeypatch.setenv("ROCKET_P2P", "0")
+    from rocket_amd.ops.optim import FusedSGD
+    from rocket_amd.parallel.ddp import DataParallel
+    from rocket_amd.parallel.rccl import RcclComm
+    from rocket_amd.runtime import comm as rcomm
+    from rocket_amd.runtime.native import describe_graph
+
+    rcomm.init()
+    dev = torch.device("cuda", 0)
+    comm = RcclComm(dev)
+    try:
+        torch.manual_seed(0)
+        layers = []
+        for _ in range(6):
+            layers += [torch.nn.Linear(256, 256), torch.nn.ReLU()]
+        net = torch.nn.Sequential(*layers, torch.nn.Linear(256, 10)).to(dev)
+        dp = DataParallel(net, comm=comm, first_bucket_mb=0.2, bucket_cap_mb=0.5)
+        assert dp.capture_mode == "overlap" and dp._native is not None and len(dp.buckets) >= 4
+        opt = FusedSGD(net.parameters(), lr=0.01, momentum=0.9)
+        x = torch.randn(64, 256, device=dev)
+
+        def step():
+            dp(x).square().mean().backward()
+            opt.launch(zero_grads=True)
+
+        dp(x).square().mean().backward()
+        assert opt.prepare()
+        opt.launch(zero_grads=True)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            step()
+        nodes, edges = describe_graph(g)
+        anc = _ancestors(len(nodes), edges)
+        opt_nodes = [i for i, (t, name) in enumerate(nodes) if "sgd_mt" in name]
+        assert len(opt_nodes) == 1, nodes
+        o = opt_nodes[0]
+        red = [i for i, (t, name) in enumerate(nodes) if "nccl" in name.lower() or "rccl" in name.lower()]
+        print(f"captured graph: {len(nodes)} nodes, {len(red)} RCCL nodes: {[nodes[i] for i in red][:4]}")
+        if not red:
+            pytest.skip("RCCL emits no graph node for a world-1 all-reduce (nothing to place)")
+        kern = [i for i, (t, _) in enumerate(nodes) if t == 0 and i not in red and i != o]
+        for r in red:
+            assert r in anc[o], "optimizer must wait for every bucket's RCCL all-reduce"
+        first = min(red, key=lambda r: len(anc[r]))
+        concurrent = [k for k in kern if k not in anc[first] and first not in anc[k]]
+        assert concurrent, "RCCL all-reduce is serialised with the rest of backward"
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
