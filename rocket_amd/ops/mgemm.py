@@ -26,6 +26,9 @@ EPI = {"none": 0, "relu": 1, "gelu": 2, "mul_gelu_grad": 3, "mul_relu_grad": 4}
 TILES = {0: (128, 128, 2, 0.85), 4: (128, 128, 2, 0.85), 5: (128, 128, 2, 0.8), 6: (256, 256, 1, 1.0),
          7: (256, 128, 1, 0.9), 8: (256, 256, 1, 1.0), 9: (256, 128, 1, 0.9)}
 N_CU = 256
+# tile ids >= XTILE select the macro-tile kernels of native/kernels/xgemm.hip (config = id - XTILE)
+XTILE = 20
+XTILES = {20: (256, 256, 1, 1.0), 21: (256, 256, 1, 1.0), 22: (320, 256, 1, 1.0), 23: (256, 128, 1, 0.9)}
 
 
 def _cost(M: int, N: int, K: int, tile: int, splitk: int = 1) -> float:
@@ -85,10 +88,11 @@ def mgemm(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, *, M: int, N: int, 
         tile = pick_tile(M, N, K // max(splitk, 1))
     slab = _slab(c.device, splitk * M * N) if splitk > 1 else None
     lib = _lib.kernels()
+    fn, name, t = (lib.rk_xgemm, "rk_xgemm", tile - XTILE) if tile >= XTILE else (lib.rk_mgemm, "rk_mgemm", tile)
     _lib.check(
-        lib.rk_mgemm(a.data_ptr(), lda, int(a_kmaj), b.data_ptr(), ldb, int(b_kmaj), c.data_ptr(), _lib.dtype_code(c),
+        fn(a.data_ptr(), lda, int(a_kmaj), b.data_ptr(), ldb, int(b_kmaj), c.data_ptr(), _lib.dtype_code(c),
                      ldc, _lib.ptr(c_pre), _lib.ptr(bias), _lib.ptr(aux), EPI[epi], int(accumulate), _lib.ptr(rowsum),
-                     M, N, K, splitk, tile, _lib.ptr(slab), _lib.stream_ptr(c.device)),
-        "rk_mgemm",
+                     M, N, K, splitk, t, _lib.ptr(slab), _lib.stream_ptr(c.device)),
+        name,
     )
     return c
