@@ -1,6 +1,6 @@
 // Elementwise / row-wise activation kernels for the transformer path (ViT-B/16):
 //
-//   gelu_fwd     y = gelu(x) (erf form; erf to 1.5e-7, rk_common.h), bf16/f32 in/out, 4 elements per access.
+//   gelu_fwd     y = gelu(x) (erf form; erf to 1.5e-7, rk_common.h), bf16/fp16/f32 in/out, 4 elements per access.
 //   gelu_bwd     dx = dy * gelu'(x), recomputed from the saved pre-activation (no extra tensor).
 //   softmax_fwd  y = softmax(x * scale) over rows of length L (attention scores), one wave per
 //                row, values held in registers (L <= 1024): one read, one write.
@@ -31,6 +31,20 @@ template <> struct V4<uint16_t> {
     uint2 u;
     u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *(uint2*)p = u;
+  }
+};
+
+template <> struct V4<f16_t> {  // IEEE half (fp16 autocast)
+  static __device__ __forceinline__ void load(const f16_t* p, float* v) {
+    const uint2 u = *(const uint2*)p;
+    v[0] = h2f((uint16_t)(u.x & 0xffffu)); v[1] = h2f((uint16_t)(u.x >> 16));
+    v[2] = h2f((uint16_t)(u.y & 0xffffu)); v[3] = h2f((uint16_t)(u.y >> 16));
+  }
+  static __device__ __forceinline__ void store(f16_t* p, const float* v) {
+    uint2 u;
+    u.x = (uint32_t)f2h(v[0]) | ((uint32_t)f2h(v[1]) << 16);
+    u.y = (uint32_t)f2h(v[2]) | ((uint32_t)f2h(v[3]) << 16);
     *(uint2*)p = u;
   }
 };
@@ -122,24 +136,26 @@ int egrid(int64_t n) {
 
 }  // namespace
 
+// element type per dtype code (F32 / BF16 / F16), for the two-type elementwise dispatches below
+#define RK_ACT_T(dt, T0, ...)                                     \
+  do {                                                            \
+    if ((dt) == BF16) { typedef uint16_t T0; __VA_ARGS__ }        \
+    else if ((dt) == F16) { typedef f16_t T0; __VA_ARGS__ }       \
+    else { typedef float T0; __VA_ARGS__ }                        \
+  } while (0)
+
 RK_API int rk_gelu_fwd(int dti, int dto, const void* x, void* y, int64_t n, hipStream_t s) {
-  if (n % 4) return (int)hipErrorInvalidValue;
+  if (n % 4 || dti < 0 || dti > 2 || dto < 0 || dto > 2) return (int)hipErrorInvalidValue;
   const int g = egrid(n / 4);
-  if (dti == BF16 && dto == BF16) gelu_fwd_kernel<uint16_t, uint16_t><<<g, T, 0, s>>>((const uint16_t*)x, (uint16_t*)y, n);
-  else if (dti == BF16) gelu_fwd_kernel<uint16_t, float><<<g, T, 0, s>>>((const uint16_t*)x, (float*)y, n);
-  else if (dto == BF16) gelu_fwd_kernel<float, uint16_t><<<g, T, 0, s>>>((const float*)x, (uint16_t*)y, n);
-  else gelu_fwd_kernel<float, float><<<g, T, 0, s>>>((const float*)x, (float*)y, n);
+  RK_ACT_T(dti, TI, RK_ACT_T(dto, TO, gelu_fwd_kernel<TI, TO><<<g, T, 0, s>>>((const TI*)x, (TO*)y, n);););
   return (int)hipGetLastError();
 }
 
 // dti: dtype of x / dx; dtg: dtype of dy
 RK_API int rk_gelu_bwd(int dti, int dtg, const void* dy, const void* x, void* dx, int64_t n, hipStream_t s) {
-  if (n % 4) return (int)hipErrorInvalidValue;
+  if (n % 4 || dti < 0 || dti > 2 || dtg < 0 || dtg > 2) return (int)hipErrorInvalidValue;
   const int g = egrid(n / 4);
-  if (dti == BF16 && dtg == BF16) gelu_bwd_kernel<uint16_t, uint16_t><<<g, T, 0, s>>>((const uint16_t*)dy, (const uint16_t*)x, (uint16_t*)dx, n);
-  else if (dti == BF16) gelu_bwd_kernel<uint16_t, float><<<g, T, 0, s>>>((const float*)dy, (const uint16_t*)x, (uint16_t*)dx, n);
-  else if (dtg == BF16) gelu_bwd_kernel<float, uint16_t><<<g, T, 0, s>>>((const uint16_t*)dy, (const float*)x, (float*)dx, n);
-  else gelu_bwd_kernel<float, float><<<g, T, 0, s>>>((const float*)dy, (const float*)x, (float*)dx, n);
+  RK_ACT_T(dti, TI, RK_ACT_T(dtg, TG, gelu_bwd_kernel<TI, TG><<<g, T, 0, s>>>((const TG*)dy, (const TI*)x, (TI*)dx, n);););
   return (int)hipGetLastError();
 }
 

@@ -135,13 +135,30 @@ __device__ __forceinline__ uint2 tr4dsc(const uint16_t* img, int r0, int c0, int
   return __builtin_bit_cast(uint2, v);
 }
 
+// 16-bit element format of a kernel instance: H = fp16 (autocast fp16), else bf16.  Operands
+// travel as bf16x8 bit patterns either way; only the MFMA opcode and the conversions differ.
+template <bool H = false>
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  return pack16t<H>(a, b);
 }
-// accumulators of tiles t0 (k 0..3) and t1 (k 4..7) -> one bf16x8 operand
+template <bool H = false>
+__device__ __forceinline__ uint16_t cvt16(float a) {
+  return H ? f2h(a) : f2bf(a);
+}
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+template <bool H = false>
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (H)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// accumulators of tiles t0 (k 0..3) and t1 (k 4..7) -> one 16-bit x 8 operand
+template <bool H = false>
 __device__ __forceinline__ bf16x8 pack_operand(const f32x4& x, const f32x4& y) {
-  return __builtin_bit_cast(bf16x8, make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(y[0], y[1]),
-                                               pack2(y[2], y[3])));
+  return __builtin_bit_cast(bf16x8, make_uint4(pack2<H>(x[0], x[1]), pack2<H>(x[2], x[3]), pack2<H>(y[0], y[1]),
+                                               pack2<H>(y[2], y[3])));
 }
 
 __device__ __forceinline__ float red4_max(float v) {  // over the 4 lanes sharing lo (hi = 0..3)
@@ -154,7 +171,7 @@ __device__ __forceinline__ float red4_sum(float v) {
 }
 
 // --------------------------------------------------------------------------------- forward
-template <int NTH, int MINW = 1>  // MINW: minimum waves per SIMD (launch_bounds)
+template <int NTH, int MINW = 1, bool H = false>  // MINW: minimum waves per SIMD (launch_bounds)
 __global__ void __launch_bounds__(NTH, MINW) attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[LMAX * RS];
@@ -188,8 +205,7 @@ __global__ void __launch_bounds__(NTH, MINW) attn_fwd_kernel(AttnArgs a) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Ks, 16 * t + lo, 4 * ks + hi), qb[ks], acc,
-                                                        0, 0, 0);
+          acc = mfma16<H>(frag(Ks, 16 * t + lo, 4 * ks + hi), qb[ks], acc);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {  // C[row = key 16t + 4hi + i][col = query lo]
           s[t][i] = 16 * t + 4 * hi + i < L ? acc[i] * sl : -INFINITY;
@@ -213,11 +229,11 @@ __global__ void __launch_bounds__(NTH, MINW) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       if (32 * ks < 16 * ntile) {  // uniform
-        const bf16x8 pb = pack_operand(s[2 * ks], s[2 * ks + 1]);
+        const bf16x8 pb = pack_operand<H>(s[2 * ks], s[2 * ks + 1]);
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
-          o[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              tr_operand(Vs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), pb, o[nt], 0, 0, 0);
+          o[nt] = mfma16<H>(
+              tr_operand(Vs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), pb, o[nt]);
       }
     }
     const int r = q0 + lo;
@@ -226,8 +242,8 @@ __global__ void __launch_bounds__(NTH, MINW) attn_fwd_kernel(AttnArgs a) {
       uint16_t* orow = a.out + ((int64_t)b * L + r) * a.ldo + h * D;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
-        *(uint2*)(orow + 16 * nt + 4 * hi) = make_uint2(pack2(o[nt][0] * inv, o[nt][1] * inv),
-                                                        pack2(o[nt][2] * inv, o[nt][3] * inv));
+        *(uint2*)(orow + 16 * nt + 4 * hi) = make_uint2(pack2<H>(o[nt][0] * inv, o[nt][1] * inv),
+                                                        pack2<H>(o[nt][2] * inv, o[nt][3] * inv));
       if (hi == 0) a.lse[bh * L + r] = m + log2f(sum);
     }
   }
@@ -408,6 +424,7 @@ constexpr int DSC = 32;  // queries per chunk
 // wave on disjoint banks (64-byte rows: 2-way) and halve the store conflicts (8-way -> 4-way)
 constexpr int DSP = 48;
 
+template <bool H = false>
 __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Qs[LMAX * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Gs[LMAX * RS];
@@ -462,8 +479,7 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
       float dot = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        dot += __uint_as_float(gw[e] << 16) * __uint_as_float(ow[e] << 16) +
-               __uint_as_float(gw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+        dot += lo16t<H>(gw[e]) * lo16t<H>(ow[e]) + hi16t<H>(gw[e]) * hi16t<H>(ow[e]);
       dot += __shfl_xor(dot, 1, 64);
       dot += __shfl_xor(dot, 2, 64);
       dot += __shfl_xor(dot, 4, 64);
@@ -500,14 +516,14 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
         // [key][query] image); B: k = the same keys, n = d 16nt + lo (transposed reads of K)
         const uint2 a0 = tr4dsc<DSP>(dsc, 32 * kq + 4 * hi, 16 * qh, lo), a1 = tr4dsc<DSP>(dsc, 32 * kq + 16 + 4 * hi, 16 * qh, lo);
         const bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(a0.x, a0.y, a1.x, a1.y));
-        dq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            av, tr_operand(Ks, 32 * kq + 4 * hi, 32 * kq + 16 + 4 * hi, 16 * nt, lo), dq, 0, 0, 0);
+        dq = mfma16<H>(
+            av, tr_operand(Ks, 32 * kq + 4 * hi, 32 * kq + 16 + 4 * hi, 16 * nt, lo), dq);
       }
       const int r0 = 32 * kc + 16 * qh + 4 * hi;  // C[row = query r0 + i][col = d lo]
       uint16_t* dqp = a.dq + ((int64_t)b * L + r0) * a.ldg + h * D + 16 * nt + lo;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (r0 + i < L) dqp[(int64_t)i * a.ldg] = f2bf(dq[i]);
+        if (r0 + i < L) dqp[(int64_t)i * a.ldg] = cvt16<H>(dq[i]);
     }
   };
   int nchunks = 0;
@@ -524,8 +540,8 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
       if (qt < ntile) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Qs, 16 * qt + lo, 4 * kk + hi), kb[kk], sv, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(Gs, 16 * qt + lo, 4 * kk + hi), vb[kk], dp, 0, 0, 0);
+          sv = mfma16<H>(frag(Qs, 16 * qt + lo, 4 * kk + hi), kb[kk], sv);
+          dp = mfma16<H>(frag(Gs, 16 * qt + lo, 4 * kk + hi), vb[kk], dp);
         }
       }
       // the 4 queries' lse / delta as one 16-byte LDS read each (entries >= L are zero), the exp
@@ -541,20 +557,20 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
         ds2[u][i] = p * (dp[i] - dq4[i]) * a.scale;
       }
     }
-    const bf16x8 pa = pack_operand(p2[0], p2[1]);  // A: row = key lo, k = the chunk's queries
-    const bf16x8 sa = pack_operand(ds2[0], ds2[1]);
+    const bf16x8 pa = pack_operand<H>(p2[0], p2[1]);  // A: row = key lo, k = the chunk's queries
+    const bf16x8 sa = pack_operand<H>(ds2[0], ds2[1]);
     // dS -> the chunk image first (the barrier below waits for it): row = key k0 + lo, 4
     // consecutive queries 16u + 4hi .. +3
 #pragma unroll
     for (int u = 0; u < 2; ++u)
       *(uint2*)(dsc + (k0 + lo) * DSP + 16 * u + 4 * hi) =
-          make_uint2(pack2(ds2[u][0], ds2[u][1]), pack2(ds2[u][2], ds2[u][3]));
+          make_uint2(pack2<H>(ds2[u][0], ds2[u][1]), pack2<H>(ds2[u][2], ds2[u][3]));
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      dv[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-          pa, tr_operand(Gs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dv[nt], 0, 0, 0);
-      dk[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-          sa, tr_operand(Qs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dk[nt], 0, 0, 0);
+      dv[nt] = mfma16<H>(
+          pa, tr_operand(Gs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dv[nt]);
+      dk[nt] = mfma16<H>(
+          sa, tr_operand(Qs, 32 * ks + 4 * hi, 32 * ks + 16 + 4 * hi, 16 * nt, lo), dk[nt]);
     }
     // ---- B of the PREVIOUS chunk in the same barrier interval (its buffer was completed before
     // the previous barrier; the next chunk's A rewrites it only after the barrier below)
@@ -576,8 +592,8 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
       uint16_t* rv = a.dv + ((int64_t)b * L + r) * a.ldg + h * D;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        rk[16 * nt + lo] = f2bf(dk[nt][i]);
-        rv[16 * nt + lo] = f2bf(dv[nt][i]);
+        rk[16 * nt + lo] = cvt16<H>(dk[nt][i]);
+        rv[16 * nt + lo] = cvt16<H>(dv[nt][i]);
       }
     }
   }
@@ -870,26 +886,33 @@ RK_API int rk_attn_set_waves(int fwd, int bwd_q, int bwd_kv) {
   return 0;
 }
 
-// q/k/v: bf16 token-major (row stride ld elements), out: [B*L][ldo] with head h at column h*64;
-// lse: [B*H][L] f32.  head dim 64, L <= 224.
-RK_API int rk_attn_fwd(const void* q, const void* k, const void* v, int ld, void* out, int ldo, float* lse, int B,
-                       int L, int H, float scale, hipStream_t s) {
+// q/k/v: 16-bit token-major (row stride ld elements; h = 1: fp16, 0: bf16), out: [B*L][ldo] with
+// head h at column h*64; lse: [B*H][L] f32.  head dim 64, L <= 224.
+RK_API int rk_attn_fwd16(int hf, const void* q, const void* k, const void* v, int ld, void* out, int ldo, float* lse,
+                         int B, int L, int H, float scale, hipStream_t s) {
   if (L < 1 || L > LMAX || B < 1 || H < 1) return (int)hipErrorInvalidValue;
   AttnArgs a{};
   a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v;
   a.out = (uint16_t*)out; a.lse = lse; a.ld = ld; a.ldo = ldo; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);  // one block per (batch, head)
-  if (g_waves[0] == 82) attn_fwd_kernel<512, 4><<<grid, 512, 0, s>>>(a);
+  if (hf) {
+    if (g_waves[0] != 82) return (int)hipErrorInvalidValue;  // fp16: the default configuration only
+    attn_fwd_kernel<512, 4, true><<<grid, 512, 0, s>>>(a);
+  } else if (g_waves[0] == 82) attn_fwd_kernel<512, 4><<<grid, 512, 0, s>>>(a);
   else if (g_waves[0] == 8) attn_fwd_kernel<512><<<grid, 512, 0, s>>>(a);
   else attn_fwd_kernel<256><<<grid, 256, 0, s>>>(a);
   return (int)hipGetLastError();
 }
+RK_API int rk_attn_fwd(const void* q, const void* k, const void* v, int ld, void* out, int ldo, float* lse, int B,
+                       int L, int H, float scale, hipStream_t s) {
+  return rk_attn_fwd16(0, q, k, v, ld, out, ldo, lse, B, L, H, scale, s);
+}
 
 // gradients dq/dk/dv written token-major with row stride ldg (e.g. into one [B*L][3*H*64] buffer);
-// delta: [B*H][L] f32 scratch.
-RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, const void* o, const void* dout, int ldo,
-                       const float* lse, float* delta, void* dq, void* dk, void* dv, int ldg, int B, int L, int H,
-                       float scale, hipStream_t s) {
+// delta: [B*H][L] f32 scratch.  fp16 (hf = 1): the fused backward only.
+RK_API int rk_attn_bwd16(int hf, const void* q, const void* k, const void* v, int ld, const void* o, const void* dout,
+                         int ldo, const float* lse, float* delta, void* dq, void* dk, void* dv, int ldg, int B, int L,
+                         int H, float scale, hipStream_t s) {
   if (L < 1 || L > LMAX || B < 1 || H < 1) return (int)hipErrorInvalidValue;
   AttnArgs a{};
   a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v;
@@ -898,6 +921,11 @@ RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, cons
   a.lse = (float*)lse; a.delta = delta; a.stamps = g_stamps;
   a.ld = ld; a.ldo = ldo; a.ldg = ldg; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);
+  if (hf) {
+    if (g_bwd_fused != 1) return (int)hipErrorInvalidValue;
+    attn_bwd_fused_kernel<true><<<grid, 64 * ((L + 15) / 16), 0, s>>>(a);
+    return (int)hipGetLastError();
+  }
   if (g_bwd_fused == 2) {
     attn_bwd_stream_kernel<<<grid, 64 * ((L + 15) / 16), 0, s>>>(a);
     return (int)hipGetLastError();
@@ -914,4 +942,9 @@ RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, cons
   else if (g_waves[2] == 8) attn_bwd_kv_kernel<512><<<grid, 512, 0, s>>>(a);
   else attn_bwd_kv_kernel<256><<<grid, 256, 0, s>>>(a);
   return (int)hipGetLastError();
+}
+RK_API int rk_attn_bwd(const void* q, const void* k, const void* v, int ld, const void* o, const void* dout, int ldo,
+                       const float* lse, float* delta, void* dq, void* dk, void* dv, int ldg, int B, int L, int H,
+                       float scale, hipStream_t s) {
+  return rk_attn_bwd16(0, q, k, v, ld, o, dout, ldo, lse, delta, dq, dk, dv, ldg, B, L, H, scale, s);
 }

@@ -689,6 +689,20 @@ __device__ __forceinline__ void st4<uint16_t>(uint16_t* p, const float* v) {
   *(uint2*)p = u;
 }
 
+template <>
+__device__ __forceinline__ void ld4<f16_t>(const f16_t* p, float* v) {
+  const uint2 u = *(const uint2*)p;
+  v[0] = h2f((uint16_t)(u.x & 0xffffu)); v[1] = h2f((uint16_t)(u.x >> 16));
+  v[2] = h2f((uint16_t)(u.y & 0xffffu)); v[3] = h2f((uint16_t)(u.y >> 16));
+}
+template <>
+__device__ __forceinline__ void st4<f16_t>(f16_t* p, const float* v) {
+  uint2 u;
+  u.x = (uint32_t)f2h(v[0]) | ((uint32_t)f2h(v[1]) << 16);
+  u.y = (uint32_t)f2h(v[2]) | ((uint32_t)f2h(v[3]) << 16);
+  *(uint2*)p = u;
+}
+
 template <typename T, typename TO, int NV>
 __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const T* __restrict__ x, const TO* __restrict__ res,
                                                       T* __restrict__ sum_out, const float* __restrict__ g,
@@ -1209,7 +1223,7 @@ RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, co
 
 RK_API int rk_ln_fwd(int dt, int dto, const void* x, const void* res, void* sum_out, const float* g, const float* b,
                      void* y, float* mean, float* rstd, int64_t rows, int C, float eps, hipStream_t s) {
-  if (dt == F16 || dto == F16) return (int)hipErrorInvalidValue;  // LayerNorm: f32 / bf16 only
+  if ((dt == F16 && dto == BF16) || (dt == BF16 && dto == F16)) return (int)hipErrorInvalidValue;
   if (C % 4 || C > 64 * 4 * LN_MAXV) return (int)hipErrorInvalidValue;
   const int grid = (int)((rows + LN_W - 1) / LN_W);
   const int nv = (C + 255) / 256;
@@ -1223,6 +1237,9 @@ RK_API int rk_ln_fwd(int dt, int dto, const void* x, const void* res, void* sum_
   else if (nv <= 8) RK_LF(T, TO, 8);  \
   else RK_LF(T, TO, 16);
   if (dt == BF16 && dto == BF16) { RK_LFN(uint16_t, uint16_t) }
+  else if (dt == F16 && dto == F16) { RK_LFN(f16_t, f16_t) }
+  else if (dt == F16) { RK_LFN(f16_t, float) }
+  else if (dto == F16) { RK_LFN(float, f16_t) }
   else if (dt == BF16) { RK_LFN(uint16_t, float) }
   else if (dto == BF16) { RK_LFN(float, uint16_t) }
   else { RK_LFN(float, float) }
@@ -1245,7 +1262,7 @@ RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
 RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float* g, const float* mean,
                      const float* rstd, void* dx, const void* dsum, void* dres, float* dgamma, float* dbeta,
                      float* dres_sum, int64_t rows, int C, float* ws, unsigned* counter, hipStream_t s) {
-  if (dt == F16 || dto == F16) return (int)hipErrorInvalidValue;  // LayerNorm: f32 / bf16 only
+  if ((dt == F16 && dto == BF16) || (dt == BF16 && dto == F16)) return (int)hipErrorInvalidValue;
   if (C % 4 || C > 64 * 4 * LN_MAXV || (dres_sum && !dres)) return (int)hipErrorInvalidValue;
   const int rpb = LN_BWD_RPB;
   const int grid = (int)((rows + rpb - 1) / rpb);
@@ -1267,6 +1284,9 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
   else if (nv <= 8) RK_LB(T, TO, 8);  \
   else RK_LB(T, TO, 16);
   if (dt == BF16 && dto == BF16) { RK_LBN(uint16_t, uint16_t) }
+  else if (dt == F16 && dto == F16) { RK_LBN(f16_t, f16_t) }
+  else if (dt == F16) { RK_LBN(f16_t, float) }
+  else if (dto == F16) { RK_LBN(float, f16_t) }
   else if (dt == BF16) { RK_LBN(uint16_t, float) }
   else if (dto == BF16) { RK_LBN(float, uint16_t) }
   else { RK_LBN(float, float) }

@@ -112,6 +112,10 @@ KERNEL_SIGS = {
                             c_void_p]),
     "rk_attn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p]),
+    "rk_attn_fwd16": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                              c_float, c_void_p]),
+    "rk_attn_bwd16": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p]),
     "rk_gelu_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_gelu_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_softmax_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p]),

@@ -44,7 +44,8 @@ class _Gelu(torch.autograd.Function):
 
 
 def gelu(x: torch.Tensor) -> torch.Tensor:
-    if _ops.fused_enabled() and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.numel() % 4 == 0:
+    if (_ops.fused_enabled() and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16, torch.float16)
+            and x.numel() % 4 == 0):
         return _Gelu.apply(x)
     return F.gelu(x)
 
@@ -121,8 +122,10 @@ class _AttnQKV(torch.autograd.Function):
         out = torch.empty(B, L, HD, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(B * heads, L, dtype=torch.float32, device=qkv.device)
         base, es = qkv.data_ptr(), qkv.element_size()
-        _lib.check(lib.rk_attn_fwd(base, base + HD * es, base + 2 * HD * es, C3, out.data_ptr(), HD, lse.data_ptr(),
-                                   B, L, heads, float(scale), _lib.stream_ptr(qkv.device)), "rk_attn_fwd")
+        hf = int(qkv.dtype == torch.float16)
+        _lib.check(lib.rk_attn_fwd16(hf, base, base + HD * es, base + 2 * HD * es, C3, out.data_ptr(), HD,
+                                     lse.data_ptr(), B, L, heads, float(scale), _lib.stream_ptr(qkv.device)),
+                   "rk_attn_fwd16")
         ctx.cfg = (heads, scale)
         ctx.save_for_backward(qkv, out, lse)
         return out
@@ -140,9 +143,10 @@ class _AttnQKV(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(B * heads, L, dtype=torch.float32, device=qkv.device)  # (split backward)
         base, gbase, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
-        _lib.check(lib.rk_attn_bwd(base, base + HD * es, base + 2 * HD * es, C3, out.data_ptr(), dout.data_ptr(), HD,
-                                   lse.data_ptr(), delta.data_ptr(), gbase, gbase + HD * es, gbase + 2 * HD * es, C3,
-                                   B, L, heads, float(scale), _lib.stream_ptr(qkv.device)), "rk_attn_bwd")
+        _lib.check(lib.rk_attn_bwd16(int(qkv.dtype == torch.float16), base, base + HD * es, base + 2 * HD * es, C3,
+                                     out.data_ptr(), dout.data_ptr(), HD, lse.data_ptr(), delta.data_ptr(), gbase,
+                                     gbase + HD * es, gbase + 2 * HD * es, C3, B, L, heads, float(scale),
+                                     _lib.stream_ptr(qkv.device)), "rk_attn_bwd16")
         return dqkv, None, None
 
 
@@ -151,7 +155,9 @@ def attention_qkv(qkv: torch.Tensor, heads: int, scale: float | None = None) -> 
     B, L, C3 = qkv.shape
     D = C3 // (3 * heads)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
-    if (_ops.fused_enabled() and qkv.is_cuda and qkv.dtype == torch.bfloat16 and D == 64
+    # fp16: the default kernel configuration only (8-wave forward, fused backward)
+    f16_ok = qkv.dtype == torch.float16 and ATTN_WAVES[0] == 82 and ATTN_BWD == "fused"
+    if (_ops.fused_enabled() and qkv.is_cuda and (qkv.dtype == torch.bfloat16 or f16_ok) and D == 64
             and L <= _lib.kernels().rk_attn_max_len()):
         return _AttnQKV.apply(qkv, heads, scale)
     t = qkv.view(B, L, 3, heads, D).permute(2, 0, 3, 1, 4)

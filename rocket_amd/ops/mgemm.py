@@ -28,7 +28,7 @@ TILES = {0: (128, 128, 2, 0.85), 4: (128, 128, 2, 0.85), 5: (128, 128, 2, 0.8), 
 N_CU = 256
 # tile ids >= XTILE select the macro-tile kernels of native/kernels/xgemm.hip (config = id - XTILE)
 XTILE = 20
-XTILES = {20: (256, 256, 1, 1.0), 21: (256, 256, 1, 1.0), 22: (320, 256, 1, 1.0), 23: (256, 128, 1, 0.9)}
+XTILES = {20: (256, 256, 1, 1.0), 21: (256, 128, 1, 0.9)}  # + 16: fp16 operands
 
 
 def _cost(M: int, N: int, K: int, tile: int, splitk: int = 1) -> float:

@@ -29,7 +29,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops import _lib
-from rocket_amd.ops.linear import native_route, _bf16_copy, _direct, grad_ready, lib_param_grads
+from rocket_amd.ops.linear import native_route, _bf16_copy, _direct, _lowp_copy, grad_ready, lib_param_grads
 from rocket_amd.ops.mgemm import mgemm, pick_split
 
 # Which engine runs each product.  ROCKET_VIT_GEMM:
@@ -44,12 +44,43 @@ from rocket_amd.ops.mgemm import mgemm, pick_split
 #                  bias gradient from the same launch: no K-split batched GEMM + slab sums + colsum)
 #   libd           forward / wgrad on the library, every input gradient (K-major weight read, no
 #                  transpose) on mgemm
+#   x              every product on the macro-tile kernels of native/kernels/xgemm.hip (persistent
+#                  256x256 / 256x128 tiles, buffer-load LDS-DMA ring; forward + bias, K-major-weight
+#                  dgrad, split-K wgrad with the bias gradient from the same launch); the only route
+#                  with fp16 operands (the GELU runs as its own streaming kernel)
 MODE = os.environ.get("ROCKET_VIT_GEMM", "lib")
 _TILE_WIDE_FWD, _TILE_DEFAULT = 4, 0
 
 
 def _fwd_tile(N: int) -> int:
     return _TILE_WIDE_FWD if N >= 2048 else _TILE_DEFAULT
+
+
+def _x_tile(M: int, N: int, dtype: torch.dtype, splitk: int = 1) -> int:
+    """xgemm config for an M x N output: the 256x256 tile unless the 256x128 one leaves fewer CU
+    rounds (wave quantisation over the persistent grid); + 16 for fp16 operands."""
+    from rocket_amd.ops.mgemm import N_CU, XTILE
+
+    def rounds(bm, bn):
+        return -(-(-(-M // bm) * -(-N // bn) * splitk) // N_CU)
+
+    t = XTILE if rounds(256, 256) * 2 <= rounds(256, 128) * 1.25 else XTILE + 1
+    return t + (16 if dtype == torch.float16 else 0)
+
+
+def _x_split(M: int, N: int, K: int) -> int:
+    """K splits of an xgemm wgrad (long K, few tiles): fill the CUs, each split a whole number of
+    32-deep units, priced with the f32 slab each split writes and the combine reads."""
+    from rocket_amd.ops.mgemm import N_CU
+
+    tiles = -(-M // 256) * -(-N // 256)
+    best = None
+    for s in range(1, 33):
+        rounds = -(-(tiles * s) // N_CU)
+        cost = rounds * (K / s) + 0.08 * (s - 1) * K / 8
+        if best is None or cost < best[0]:
+            best = (cost, s)
+    return best[1]
 
 
 def _lib_fwd(K: int) -> bool:
@@ -61,20 +92,30 @@ def _lib_dgrad(N_in: int) -> bool:
 
 
 def _ok(x: torch.Tensor, N: int, K: int) -> bool:
-    # features % 8 (16-byte rows); the token count is free (the wgrad reads tokens as k-rows)
+    # features % 8 (16-byte rows); the token count is free (the wgrad reads tokens as k-rows);
+    # xgemm: row-layout operands move in 32-deep k-units (features % 32)
+    if MODE == "x" and (K % 32 or N % 32):
+        return False
     return x.is_cuda and K % 8 == 0 and N % 8 == 0 and _lib.available()
 
 
-def _as_bf16_2d(t: torch.Tensor, K: int) -> torch.Tensor:
+def _as_16_2d(t: torch.Tensor, K: int, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
     t = t.reshape(-1, K)
-    if t.dtype != torch.bfloat16:
-        t = t.to(torch.bfloat16)
+    if t.dtype != dtype:
+        t = t.to(dtype)
     return t if t.is_contiguous() else t.contiguous()
+
+
+_as_bf16_2d = _as_16_2d
 
 
 def _linear_fwd(x2: torch.Tensor, w16: torch.Tensor, bias: torch.Tensor, b16: torch.Tensor) -> torch.Tensor:
     M, K = x2.shape
     N = w16.shape[0]
+    if MODE == "x":
+        y = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
+        mgemm(x2, w16, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, tile=_x_tile(M, N, x2.dtype))
+        return y
     if _lib_fwd(K):
         return torch.addmm(b16, x2, w16.t())
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
@@ -87,6 +128,11 @@ def _linear_dgrad(dy2: torch.Tensor, w16: torch.Tensor, gelu_of: torch.Tensor | 
     gelu'(z): the input gradient of a GELU whose input z fed this layer, in the same launch."""
     M, N = dy2.shape
     K = w16.shape[1]
+    if MODE == "x":
+        assert gelu_of is None
+        dx = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
+        mgemm(dy2, w16, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, b_kmaj=True, tile=_x_tile(M, K, dy2.dtype))
+        return dx
     if _lib_dgrad(K):
         assert gelu_of is None
         return dy2 @ w16
@@ -111,7 +157,11 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
     else:
         dw = torch.empty(N, K, dtype=torch.float32, device=dy.device)
         db = torch.zeros(N, dtype=torch.float32, device=dy.device) if need_b else None
-    tile, split = pick_split(N, K, M)
+    if MODE == "x":
+        split = _x_split(N, K, M)
+        tile = _x_tile(N, K, dy.dtype, split)
+    else:
+        tile, split = pick_split(N, K, M)
     mgemm(dy, x, dw, M=N, N=K, K=M, lda=N, ldb=K, ldc=K, a_kmaj=True, b_kmaj=True, rowsum=db,
           accumulate=direct and need_w, splitk=split, tile=tile)
     if direct:
@@ -153,7 +203,7 @@ class _MLinearFn(torch.autograd.Function):
         shape = x.shape
         K = shape[-1]
         N = w16.shape[0]
-        x2 = _as_bf16_2d(x, K)
+        x2 = _as_16_2d(x, K, w16.dtype)
         y = _linear_fwd(x2, w16, bias, b16)
         ctx.save_for_backward(x2, w16)
         ctx.params = (weight, bias)
@@ -166,7 +216,7 @@ class _MLinearFn(torch.autograd.Function):
         x2, w16 = ctx.saved_tensors
         weight, bias = ctx.params
         N = w16.shape[0]
-        dy2 = _as_bf16_2d(dy, N)
+        dy2 = _as_16_2d(dy, N, w16.dtype)
         dx = _linear_dgrad(dy2, w16).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
         need_b = bias is not None and ctx.needs_input_grad[2]
         dw = db = None
@@ -182,15 +232,16 @@ class _MLinearFn(torch.autograd.Function):
 
 def _gelu_fwd(z: torch.Tensor) -> torch.Tensor:
     h = torch.empty_like(z)
-    _lib.check(_lib.kernels().rk_gelu_fwd(1, 1, z.data_ptr(), h.data_ptr(), z.numel(),
+    dt = _lib.dtype_code(z)
+    _lib.check(_lib.kernels().rk_gelu_fwd(dt, dt, z.data_ptr(), h.data_ptr(), z.numel(),
                                           _lib.stream_ptr(z.device)), "rk_gelu_fwd")
     return h
 
 
 def _gelu_bwd(dh: torch.Tensor, z: torch.Tensor) -> torch.Tensor:
     dz = torch.empty_like(z)
-    _lib.check(_lib.kernels().rk_gelu_bwd(1, 1, dh.data_ptr(), z.data_ptr(), dz.data_ptr(),
-                                          z.numel(), _lib.stream_ptr(z.device)), "rk_gelu_bwd")
+    _lib.check(_lib.kernels().rk_gelu_bwd(_lib.dtype_code(z), _lib.dtype_code(dh), dh.data_ptr(), z.data_ptr(),
+                                          dz.data_ptr(), z.numel(), _lib.stream_ptr(z.device)), "rk_gelu_bwd")
     return dz
 
 
@@ -223,7 +274,7 @@ class _MMlpFn(torch.autograd.Function):
         shape = x.shape
         K = shape[-1]
         N = w2_16.shape[0]
-        x2 = _as_bf16_2d(x, K)
+        x2 = _as_16_2d(x, K, w1_16.dtype)
         z = _linear_fwd(x2, w1_16, b1, b1_16)
         h = _gelu_fwd(z)
         y = _linear_fwd(h, w2_16, b2, b2_16)
@@ -238,11 +289,15 @@ class _MMlpFn(torch.autograd.Function):
         x2, z, h, w1_16, w2_16 = ctx.saved_tensors
         w1, b1, w2, b2 = ctx.params
         N = w2_16.shape[0]
-        dy2 = _as_bf16_2d(dy, N)
+        dy2 = _as_16_2d(dy, N, w2_16.dtype)
         g = ctx.needs_input_grad
         need_b1 = b1 is not None and g[2]
         db1 = None
-        if MODE == "lib" and need_b1:
+        if MODE == "x":
+            # dz = gelu'(z) * (dy W2) by the streaming kernel; fc1's bias gradient comes out of
+            # its wgrad launch (row sums of dz)
+            dz = _gelu_bwd(_linear_dgrad(dy2, w2_16), z)
+        elif MODE == "lib" and need_b1:
             # GELU backward and fc1's bias gradient in one pass over the [tokens, hidden] gradient
             dz, db1 = _gelu_bwd_bias(_linear_dgrad(dy2, w2_16), z, b1)
             need_b1 = False
@@ -264,8 +319,13 @@ class _MMlpFn(torch.autograd.Function):
         return dx, dw1, (db1 if db1_ is None else db1_), dw2, db2, None, None, None, None, None
 
 
+def _cdtype() -> torch.dtype:
+    return torch.get_autocast_dtype("cuda")
+
+
 def _native(module: nn.Linear, x: torch.Tensor) -> bool:
-    return (x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") == torch.bfloat16
+    dt = _cdtype()
+    return (x.is_cuda and native_route() and (dt == torch.bfloat16 or (dt == torch.float16 and MODE == "x"))
             and module.weight.dtype == torch.float32 and module.weight.is_contiguous()
             and _ok(x, module.out_features, module.in_features))
 
@@ -275,8 +335,9 @@ class MLinear(nn.Linear):
 
     def forward(self, x):
         if _native(self, x) and self.bias is not None:
-            w16 = _bf16_copy(self, "_w16", self.weight)
-            b16 = _bf16_copy(self, "_b16", self.bias)
+            dt = _cdtype()
+            w16 = _lowp_copy(self, "_w16", self.weight, dt)
+            b16 = _lowp_copy(self, "_b16", self.bias, dt)
             link = _new_link(self.bias)
             y = _MLinearFn.apply(x, self.weight, self.bias, w16, b16, link)
             if link is not None:
@@ -298,10 +359,11 @@ class MMlp(nn.Module):
         if _native(self.fc1, x) and _ok(x, self.fc2.out_features, self.fc2.in_features) and \
                 self.fc2.weight.is_contiguous() and self.fc1.bias is not None and self.fc2.bias is not None:
             f1, f2 = self.fc1, self.fc2
+            dt = _cdtype()
             link = _new_link(f2.bias)
-            y = _MMlpFn.apply(x, f1.weight, f1.bias, f2.weight, f2.bias, _bf16_copy(f1, "_w16", f1.weight),
-                              _bf16_copy(f1, "_b16", f1.bias), _bf16_copy(f2, "_w16", f2.weight),
-                              _bf16_copy(f2, "_b16", f2.bias), link)
+            y = _MMlpFn.apply(x, f1.weight, f1.bias, f2.weight, f2.bias, _lowp_copy(f1, "_w16", f1.weight, dt),
+                              _lowp_copy(f1, "_b16", f1.bias, dt), _lowp_copy(f2, "_w16", f2.weight, dt),
+                              _lowp_copy(f2, "_b16", f2.bias, dt), link)
             if link is not None:
                 y._rocket_bias_link = link  # a consuming add-LayerNorm may form fc2's bias gradient
             return y

@@ -389,8 +389,17 @@ class _AddLN(torch.autograd.Function):
         return dx, dr, gw, gb, None, None, None
 
 
+def _ln_out_dtype(x: torch.Tensor) -> torch.dtype:
+    """LayerNorm output dtype: the autocast compute dtype (bf16 or fp16: the output feeds a GEMM),
+    else the input's 16-bit dtype, else fp32."""
+    if torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return x.dtype
+
+
 class FusedLayerNorm(nn.LayerNorm):
-    """``LayerNorm`` over the last dim; under autocast the output is bf16 (it feeds a GEMM).
+    """``LayerNorm`` over the last dim; under autocast the output is in the autocast dtype (it
+    feeds a GEMM).
 
     ``add_forward(x, r)`` returns ``(x + r, LN(x + r))`` with the residual add fused (pre-norm
     transformer blocks); ``r=None`` is a plain LN that passes ``x`` through.
@@ -401,8 +410,10 @@ class FusedLayerNorm(nn.LayerNorm):
             return x, self(x)
         C = x.shape[-1]
         if (_ops.fused_enabled() and x.is_cuda and len(self.normalized_shape) == 1 and C % 4 == 0 and C <= 4096
-                and x.dtype in (torch.float32, torch.bfloat16) and r.shape == x.shape):
-            out_dtype = torch.bfloat16 if (torch.is_autocast_enabled("cuda") or x.dtype == torch.bfloat16) else x.dtype
+                and x.dtype in (torch.float32, torch.bfloat16, torch.float16) and r.shape == x.shape):
+            out_dtype = _ln_out_dtype(x)
+            if {x.dtype, out_dtype} == {torch.bfloat16, torch.float16}:
+                x = x.to(out_dtype)
             link = getattr(r, "_rocket_bias_link", None)
             if r.dtype != out_dtype:
                 r, link = r.to(out_dtype), None  # the producer then sees a different gradient tensor
@@ -413,8 +424,10 @@ class FusedLayerNorm(nn.LayerNorm):
     def forward(self, x):
         C = x.shape[-1]
         if (_ops.fused_enabled() and x.is_cuda and len(self.normalized_shape) == 1 and C % 4 == 0 and C <= 4096
-                and x.dtype in (torch.float32, torch.bfloat16)):
-            out_dtype = torch.bfloat16 if (torch.is_autocast_enabled("cuda") or x.dtype == torch.bfloat16) else x.dtype
+                and x.dtype in (torch.float32, torch.bfloat16, torch.float16)):
+            out_dtype = _ln_out_dtype(x)
+            if {x.dtype, out_dtype} == {torch.bfloat16, torch.float16}:
+                x = x.to(out_dtype)
             return _LN.apply(x, self.weight, self.bias, self.eps, out_dtype)
         if x.is_cuda and _ops.fused_enabled():
             _lib.kernels()
