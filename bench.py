@@ -311,6 +311,8 @@ def main() -> int:
                 "parallelism": f"dp{world}",
                 "impl": ("fused-hip" + ("" if args.no_graph else "+hipgraph"))
                 if fused else "torch-eager",
+                **({"gemm_route": __import__("rocket_amd.ops.mlinear", fromlist=["MODE"]).MODE}
+                   if args.model == "vit_b16" and fused else {}),
             },
             "wall_s": round(wall, 2),
             "dp": dp,
