@@ -16,6 +16,7 @@ import argparse
 import concurrent.futures as cf
 import glob
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -49,6 +50,14 @@ def _compile(cmd, out) -> str:
     return out
 
 
+def _included_sources(src) -> list:
+    """Sources a translation unit textually includes (e.g. lenet_conv_h.hip: #include "lenet_conv.hip")."""
+    d = os.path.dirname(src)
+    with open(src) as f:
+        names = re.findall(r'^\s*#\s*include\s+"([^"]+\.(?:hip|cpp))"', f.read(), flags=re.M)
+    return [os.path.join(d, n) for n in names if os.path.exists(os.path.join(d, n))]
+
+
 def _build_lib(sources, headers, target, extra_compile, extra_link, force, jobs, language_hip=True) -> bool:
     os.makedirs(OBJDIR, exist_ok=True)
     hipcc = _hipcc()
@@ -57,7 +66,8 @@ def _build_lib(sources, headers, target, extra_compile, extra_link, force, jobs,
     for src in sources:
         obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
         objs.append(obj)
-        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_time):
+        src_time = _newest([src] + _included_sources(src))
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(src_time, hdr_time):
             flags = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"-I{os.path.dirname(src)}"]
             if language_hip:
                 flags += [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]

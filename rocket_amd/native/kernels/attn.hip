@@ -420,9 +420,23 @@ __global__ void __launch_bounds__(NTH, MINW) attn_bwd_kv_kernel(AttnArgs a) {
 // split kernels, its chunk loop ~20 us per iteration; bench/attn_probe.py phase stamps.)
 constexpr int FUSED_MAXW = LMAX / 16;
 constexpr int DSC = 32;  // queries per chunk
-// dS image row pitch (elements): 96-byte rows put the 8 rows x 32 bytes of a transpose-read half
-// wave on disjoint banks (64-byte rows: 2-way) and halve the store conflicts (8-way -> 4-way)
-constexpr int DSP = 48;
+// dS image: 64-byte rows [key][32 queries], the 8-byte query groups (4 queries) XOR-swizzled per
+// row, g -> g ^ dsw(row) with dsw = row bits {2, 1} in place and bit 3 moved to bit 0.  Both
+// accesses are then conflict-free (tools/lds_banks.py): the writer's 16 lanes (16 consecutive
+// key rows, one group) cover 32 distinct banks because dsw is a bijection over the 8 rows of a
+// parity, and a transpose-read half wave (8 consecutive rows x 4 groups) puts rows r and r + 4
+// (the same 16-dword segment of the 256-byte bank row) into opposite 4-group halves via bit 2.
+// (The unswizzled 96-byte pitch it replaces: 4-way store conflicts, 37 % of the kernel's LDS cycles.)
+constexpr int DSP = 32;
+__device__ __forceinline__ int dsw(int row) { return (row & 6) | ((row >> 3) & 1); }
+// element offset of query group g (queries 4g..4g+3) of key row `row`
+__device__ __forceinline__ int dsoff(int row, int g) { return row * DSP + 4 * (g ^ dsw(row)); }
+__device__ __forceinline__ uint2 tr4dsz(const uint16_t* img, int r0, int c0, int lo) {
+  const int row = r0 + (lo >> 2);
+  const uint16_t* p = img + dsoff(row, (c0 >> 2) + (lo & 3));
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+  return __builtin_bit_cast(uint2, v);
+}
 
 template <bool H = false>
 __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArgs a) {
@@ -514,7 +528,7 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
       for (int kq = 0; kq < nkey32; ++kq) {
         // A: row = query 16qh + lo, k = keys 32kq + {4hi + j, 16 + 4hi + j} (transposed reads of the
         // [key][query] image); B: k = the same keys, n = d 16nt + lo (transposed reads of K)
-        const uint2 a0 = tr4dsc<DSP>(dsc, 32 * kq + 4 * hi, 16 * qh, lo), a1 = tr4dsc<DSP>(dsc, 32 * kq + 16 + 4 * hi, 16 * qh, lo);
+        const uint2 a0 = tr4dsz(dsc, 32 * kq + 4 * hi, 16 * qh, lo), a1 = tr4dsz(dsc, 32 * kq + 16 + 4 * hi, 16 * qh, lo);
         const bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(a0.x, a0.y, a1.x, a1.y));
         dq = mfma16<H>(
             av, tr_operand(Ks, 32 * kq + 4 * hi, 32 * kq + 16 + 4 * hi, 16 * nt, lo), dq);
@@ -563,7 +577,7 @@ __global__ void __launch_bounds__(64 * FUSED_MAXW) attn_bwd_fused_kernel(AttnArg
     // consecutive queries 16u + 4hi .. +3
 #pragma unroll
     for (int u = 0; u < 2; ++u)
-      *(uint2*)(dsc + (k0 + lo) * DSP + 16 * u + 4 * hi) =
+      *(uint2*)(dsc + dsoff(k0 + lo, 4 * u + hi)) =
           make_uint2(pack2<H>(ds2[u][0], ds2[u][1]), pack2<H>(ds2[u][2], ds2[u][3]));
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -896,8 +910,9 @@ RK_API int rk_attn_fwd16(int hf, const void* q, const void* k, const void* v, in
   a.out = (uint16_t*)out; a.lse = lse; a.ld = ld; a.ldo = ldo; a.L = L; a.H = H; a.scale = scale;
   dim3 grid(1, H, B);  // one block per (batch, head)
   if (hf) {
-    if (g_waves[0] != 82) return (int)hipErrorInvalidValue;  // fp16: the default configuration only
-    attn_fwd_kernel<512, 4, true><<<grid, 512, 0, s>>>(a);
+    if (g_waves[0] == 82) attn_fwd_kernel<512, 4, true><<<grid, 512, 0, s>>>(a);
+    else if (g_waves[0] == 8) attn_fwd_kernel<512, 1, true><<<grid, 512, 0, s>>>(a);
+    else attn_fwd_kernel<256, 1, true><<<grid, 256, 0, s>>>(a);
   } else if (g_waves[0] == 82) attn_fwd_kernel<512, 4><<<grid, 512, 0, s>>>(a);
   else if (g_waves[0] == 8) attn_fwd_kernel<512><<<grid, 512, 0, s>>>(a);
   else attn_fwd_kernel<256><<<grid, 256, 0, s>>>(a);

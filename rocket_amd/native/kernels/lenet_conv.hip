@@ -23,7 +23,31 @@
 
 using namespace rk;
 
+// 16-bit format of every activation / fragment / weight-gradient operand: bf16 (default) or, when
+// this file is compiled with RK_LENET_H = 1 (the *_h.hip wrapper TU), IEEE fp16 for autocast fp16;
+// the fp16 build's entry points carry an "_h" suffix.
+#ifndef RK_LENET_H
+#define RK_LENET_H 0
+#endif
+#if RK_LENET_H
+#define RKL_NAME(n) n##_h
+#else
+#define RKL_NAME(n) n
+#endif
+
 namespace {
+
+constexpr bool kH16 = RK_LENET_H;
+__device__ __forceinline__ uint16_t c16(float v) { return kH16 ? f2h(v) : f2bf(v); }
+__device__ __forceinline__ float d16(uint16_t v) { return kH16 ? h2f(v) : bf2f(v); }
+__device__ __forceinline__ __bf16 e16(float v) { return __builtin_bit_cast(__bf16, c16(v)); }
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+  if constexpr (kH16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 
 constexpr int IMG = 28, PADI = 32, C1 = 6, KS = 5, Q1 = 14, C2 = 16, Q2 = 5;
 constexpr int A1N = C1 * Q1 * Q1;  // 1176 conv1 pooled outputs per sample
@@ -31,8 +55,6 @@ constexpr int A2N = C2 * Q2 * Q2;  // 400
 constexpr int R1 = KS * KS;        // 25  conv1 reduction
 constexpr int R2 = C1 * KS * KS;   // 150 conv2 reduction
 constexpr int K1P = KS * 6;        // 30: conv1 reduction with kw padded to 6 (fused path: pair reads)
-
-__device__ __forceinline__ __bf16 tobf(float v) { return (__bf16)v; }
 
 // Optional phase timeline (diagnostics): thread 0 of every block stamps s_memrealtime (100 MHz)
 // at phase boundaries into trace[block][0..15]; RK_TRW stamps lane 0 of EVERY wave into
@@ -136,7 +158,7 @@ __global__ void __launch_bounds__(64) lenet_prep_kernel(const float* __restrict_
         const int kk = 2 * (f - OFF_D2) + (hi >> 1), co = 8 * (hi & 1) + j;
         if (kk < R1 && lo < C1) x = cw2[(co * C1 + lo) * R1 + kk];
       }
-      v[j] = (__bf16)x;
+      v[j] = e16(x);
     }
     frag[f * 64 + lane] = v;
     return;
@@ -154,7 +176,7 @@ __global__ void __launch_bounds__(64) lenet_prep_kernel(const float* __restrict_
     const int a = bwd ? 32 * ks + 8 * hi + j : 16 * tile + lo;  // output-feature row of W
     const int b = bwd ? 16 * tile + lo : 32 * ks + 8 * hi + j;  // input-feature column of W
     const bool ok = a < nout && b < nin;
-    v[j] = (__bf16)(ok ? W[a * nin + b] : 0.f);
+    v[j] = e16(ok ? W[a * nin + b] : 0.f);
   }
   frag[f * 64 + lane] = v;
 }
@@ -172,7 +194,7 @@ __device__ __forceinline__ f32x4 cls_tile(const uint16_t* act, int stride, const
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(row + 32 * ks + 8 * hi), b[ks], acc, 0, 0, 0);
+    acc = mfma16(*(const bf16x8*)(row + 32 * ks + 8 * hi), b[ks], acc);
   return acc;
 }
 
@@ -185,12 +207,12 @@ __device__ __forceinline__ f32x4 cls_tile_pre(const uint16_t* act, int stride, c
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(row + 32 * ks + 8 * hi), b[ks], acc, 0, 0, 0);
+    acc = mfma16(*(const bf16x8*)(row + 32 * ks + 8 * hi), b[ks], acc);
   return acc;
 }
 
 __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-  return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
+  return make_uint2((uint32_t)c16(a) | ((uint32_t)c16(b) << 16), (uint32_t)c16(c) | ((uint32_t)c16(d) << 16));
 }
 
 // Fused batch gather (a deferred device-loader batch, runtime/data.py PendingRows): sample n of
@@ -289,7 +311,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint16_t u = f2bf(live ? vv[j] : 0.f);
+        const uint16_t u = c16(live ? vv[j] : 0.f);
         img0[i + j] = u;
         img1[i + j - 1] = u;
       }
@@ -309,7 +331,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
     if constexpr (!MLP) {
       const bool ok = lo < C1 && r < R1;
       const float v = w1[ok ? lo * R1 + r : 0];
-      bw1[j] = tobf(ok ? v : 0.f);
+      bw1[j] = e16(ok ? v : 0.f);
     }
     koff1[j] = r < R1 ? (r / KS) * IMGS + (r % KS) : -100000;
   }
@@ -382,7 +404,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       }
       f32x4 acc[U1];
 #pragma unroll
-      for (int u = 0; u < U1; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bw1, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      for (int u = 0; u < U1; ++u) acc[u] = mfma16(a[u], bw1, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int u = 0; u < U1; ++u) {
         if (t0 + u * WPS >= 49) break;  // wave-uniform
@@ -396,7 +418,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
         }
         m += bias1;
         const bool on = m > 0.f;
-        const uint16_t v = f2bf(on ? m : 0.f);
+        const uint16_t v = c16(on ? m : 0.f);
         a1[o + u * ostep] = v;
         c1[o + u * ostep] = on ? (uint8_t)arg : 0xFF;
         a1cl[oc + u * cstep] = lo < C1 ? v : (uint16_t)0;
@@ -418,7 +440,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       }
       f32x4 acc[U1];
 #pragma unroll
-      for (int u = 0; u < U1; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bw1, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      for (int u = 0; u < U1; ++u) acc[u] = mfma16(a[u], bw1, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int u = 0; u < U1; ++u) {
         const int t = t0 + u * WPS;
@@ -434,7 +456,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
         m += bias1;
         const bool on = m > 0.f;
         const int o = lo < C1 ? lo * (Q1 * Q1) + 4 * t + hi : A1N + 4;
-        const uint16_t v = f2bf(on ? m : 0.f);
+        const uint16_t v = c16(on ? m : 0.f);
         a1[o] = v;
         c1[o] = on ? (uint8_t)arg : 0xFF;
         sm.a1cl[slot][lo < 8 ? (4 * t + hi) * 8 + lo : A1CL + 8] = lo < C1 ? v : (uint16_t)0;
@@ -459,7 +481,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
         const int kk = 4 * s + hi;
         const bool ok = kk < R1 && j < C1;
         const float v = w2[ok ? (lo * C1 + j) * R1 + kk : 0];
-        bw2[s][j] = tobf(ok ? v : 0.f);
+        bw2[s][j] = e16(ok ? v : 0.f);
       }
   }
   lds_barrier();
@@ -493,7 +515,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       for (int u = 0; u < 2; ++u) {
         const int kk = 4 * s + hi;
         const int px = (wvalid[u] && kk < R1) ? pos[u] + (kk / KS) * Q1 + (kk % KS) : Q1 * Q1;  // Q1*Q1 -> zero pixel
-        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(acl + px * 8), bw2[s], acc[u], 0, 0, 0);
+        acc[u] = mfma16(*(const bf16x8*)(acl + px * 8), bw2[s], acc[u]);
       }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -511,7 +533,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       m += bias2;
       const bool on = m > 0.f;
       const int o = wq < Q2 * Q2 ? lo * (Q2 * Q2) + wq : (MLP ? A2TRASH : A2N);  // flatten order (C, H, W)
-      sm.a2[slot][o] = f2bf(on ? m : 0.f);
+      sm.a2[slot][o] = c16(on ? m : 0.f);
       sm.c2[slot][o] = on ? (uint8_t)arg : 0xFF;
     }
   }
@@ -545,7 +567,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           v[i] = col < F1 ? fmaxf(acc[i] + bb, 0.f) : 0.f;
-          sm.h1[i][col] = f2bf(v[i]);
+          sm.h1[i][col] = c16(v[i]);
         }
         if (col < F1) *(uint2*)(cf.h1T + (int64_t)col * N + n0) = pack4(v[0], v[1], v[2], v[3]);
       }
@@ -566,7 +588,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           v[i] = col < F2 ? fmaxf(acc[i] + bb, 0.f) : 0.f;
-          sm.h2[i][col] = f2bf(v[i]);
+          sm.h2[i][col] = c16(v[i]);
         }
         if (col < F2) *(uint2*)(cf.h2T + (int64_t)col * N + n0) = pack4(v[0], v[1], v[2], v[3]);
       }
@@ -697,7 +719,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       const int kk = 2 * s + (h >> 1), co = 8 * (h & 1) + j;
       const bool ok = kk < R1 && c < C1;
       const float f = w2[ok ? (co * C1 + c) * R1 + kk : 0];
-      v[j] = tobf(ok ? f : 0.f);
+      v[j] = e16(ok ? f : 0.f);
     }
     sm.wfr[i] = v;
   }
@@ -790,7 +812,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       const int r = e / IMGS - 2, c = e % IMGS - 2;
       const bool in = n < N && r >= 0 && r < IMG && c >= 0 && c < IMG;
       const float v = x[(int64_t)(n < N ? n : 0) * IMG * IMG + (in ? r * IMG + c : 0)];
-      const uint16_t u = f2bf(in ? v : 0.f);
+      const uint16_t u = c16(in ? v : 0.f);
       sm.imgb[sl][0][e] = u;
       if (e > 0) sm.imgb[sl][1][e - 1] = u;
     }
@@ -856,7 +878,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
           const float sc = cb.grad_scale / (float)N;
           if (threadIdx.x < SPB * DYP) {
             const int sl = threadIdx.x / DYP, o = threadIdx.x % DYP;
-            sm.dyl[sl][o] = f2bf(o < F3 ? sc * sm.dyf[sl][o] : 0.f);
+            sm.dyl[sl][o] = c16(o < F3 ? sc * sm.dyf[sl][o] : 0.f);
           } else {
             const int o = threadIdx.x - 256;
             *(uint2*)(cb.dyT + (int64_t)o * N + nbase) =
@@ -867,7 +889,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       } else {
         if (threadIdx.x < SPB * DYP) {
           const int sl = threadIdx.x / DYP, o = threadIdx.x % DYP;
-          sm.dyl[sl][o] = f2bf(o < F3 ? cb.dy[(int64_t)(nbase + sl) * F3 + o] : 0.f);
+          sm.dyl[sl][o] = c16(o < F3 ? cb.dy[(int64_t)(nbase + sl) * F3 + o] : 0.f);
         } else if (threadIdx.x >= 256 && threadIdx.x < 256 + F3) {
           const int o = threadIdx.x - 256;
           const float* d = cb.dy + (int64_t)nbase * F3 + o;
@@ -882,12 +904,12 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
         if (hi == 0) {
           const int col = 16 * wave + lo;
           const uint2 m = mk2;
-          const float mk[4] = {bf2f(m.x & 0xffff), bf2f(m.x >> 16), bf2f(m.y & 0xffff), bf2f(m.y >> 16)};
+          const float mk[4] = {d16(m.x & 0xffff), d16(m.x >> 16), d16(m.y & 0xffff), d16(m.y >> 16)};
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             v[i] = (col < F2 && mk[i] > 0.f) ? acc[i] : 0.f;
-            sm.d2l[i][col] = f2bf(v[i]);
+            sm.d2l[i][col] = c16(v[i]);
           }
           if (col < F2) *(uint2*)(cb.d2T + (int64_t)col * N + nbase) = pack4(v[0], v[1], v[2], v[3]);
         }
@@ -899,12 +921,12 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
         if (hi == 0) {
           const int col = 16 * wave + lo;
           const uint2 m = mk1;
-          const float mk[4] = {bf2f(m.x & 0xffff), bf2f(m.x >> 16), bf2f(m.y & 0xffff), bf2f(m.y >> 16)};
+          const float mk[4] = {d16(m.x & 0xffff), d16(m.x >> 16), d16(m.y & 0xffff), d16(m.y >> 16)};
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             v[i] = (col < F1 && mk[i] > 0.f) ? acc[i] : 0.f;
-            sm.d1l[i][col] = f2bf(v[i]);
+            sm.d1l[i][col] = c16(v[i]);
           }
           if (col < F1) *(uint2*)(cb.d1T + (int64_t)col * N + nbase) = pack4(v[0], v[1], v[2], v[3]);
         }
@@ -918,7 +940,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
           const f32x4 acc = cls_tile_pre<4>(&sm.d1l[0][0], H1P, sm.zrow, fb1[u], lane);
           if (hi == 0) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) sm.da2[i][16 * t + lo] = f2bf(acc[i]);
+            for (int i = 0; i < 4; ++i) sm.da2[i][16 * t + lo] = c16(acc[i]);
           }
         }
       }
@@ -930,7 +952,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
         const float vv[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const uint16_t u = f2bf(vv[j]);
+          const uint16_t u = c16(vv[j]);
           sm.imgb[sl][0][i + j] = u;
           sm.imgb[sl][1][i + j - 1] = u;
         }
@@ -962,9 +984,9 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     }
     if (threadIdx.x < SPB * 8) {
       const int sl = threadIdx.x >> 3, k = threadIdx.x & 7;
-      // zero pair at [0..1], bf16 ones pair at [2..3]: the B operand of the "ones column" whose
+      // zero pair at [0..1], 16-bit ones pair at [2..3]: the B operand of the "ones column" whose
       // MFMA output is the bias gradient (row sums of the A operand)
-      const uint16_t zo = (k == 2 || k == 3) ? (uint16_t)0x3F80 : (uint16_t)0;
+      const uint16_t zo = (k == 2 || k == 3) ? (uint16_t)(kH16 ? 0x3C00 : 0x3F80) : (uint16_t)0;  // 16-bit 1.0
       sm.a1[sl][A1N + k] = zo;
       sm.a1o[sl][A1N - 1 + k] = 0;
       sm.c1[sl][A1N + k] = 0xFE;
@@ -1020,7 +1042,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
           b_nxt = ld_b(i + 1);
         }
         __builtin_amdgcn_sched_barrier(0);
-        g2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_cur, __builtin_bit_cast(bf16x8, b_cur), g2, 0, 0, 0);
+        g2 = mfma16(a_cur, __builtin_bit_cast(bf16x8, b_cur), g2);
         a_cur = a_nxt;
         b_cur = b_nxt;
       }
@@ -1071,8 +1093,8 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
           for (int q = 0; q < CH; ++q) {
             const int s = c * CH + q;
             if (s < K2P) {
-              if constexpr (MLP) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(abuf[c & 1][q], wr[s], acc, 0, 0, 0);
-              else acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(abuf[c & 1][q], sm.wfr[s * 64 + lane], acc, 0, 0, 0);
+              if constexpr (MLP) acc = mfma16(abuf[c & 1][q], wr[s], acc);
+              else acc = mfma16(abuf[c & 1][q], sm.wfr[s * 64 + lane], acc);
             }
           }
         }
@@ -1121,7 +1143,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
         const uint32_t ca = sm.c1[sl][ia], cb = sm.c1[sl][ib];
         // windows past the grid have an all-zero A; clamp them to a valid window for B
         const int pa = pos1(min(wa, Q1 * Q1 - 1), 0), pb = pos1(min(wb, Q1 * Q1 - 1), 0);
-        const uint32_t ab = f2bf(da), bb = f2bf(dbv);
+        const uint32_t ab = c16(da), bb = c16(dbv);
         const uint4 aw = make_uint4((ca == 0 ? ab : 0u) | (ca == 1 ? ab << 16 : 0u),
                                     (ca == 2 ? ab : 0u) | (ca == 3 ? ab << 16 : 0u),
                                     (cb == 0 ? bb : 0u) | (cb == 1 ? bb << 16 : 0u),
@@ -1134,7 +1156,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
                                      *(const uint32_t*)(ib0 + pa * pm[u] + cst[u][1]),
                                      *(const uint32_t*)(ib0 + pb * pm[u] + cst[u][2]),
                                      *(const uint32_t*)(ib0 + pb * pm[u] + cst[u][3]));
-          g1[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, w), g1[u], 0, 0, 0);
+          g1[u] = mfma16(a, __builtin_bit_cast(bf16x8, w), g1[u]);
         }
       }
     }
@@ -1266,7 +1288,7 @@ __global__ void __launch_bounds__(NTHR) lenet_train_kernel(const float* __restri
 
 }  // namespace
 
-RK_API int rk_lenet_conv_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+RK_API int RKL_NAME(rk_lenet_conv_fwd)(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                              void* a1, void* code1, void* a2, void* code2, int N, hipStream_t s) {
   if ((uintptr_t)x & 15) return (int)hipErrorInvalidValue;  // float4 image loads
   const int grid = (N + SPB - 1) / SPB;
@@ -1276,25 +1298,33 @@ RK_API int rk_lenet_conv_fwd(const float* x, const float* w1, const float* b1, c
 }
 
 // fc + conv weights (fp32 masters) -> bf16 MFMA fragment table (NFRAG x 64 x 16 B)
-RK_API int rk_lenet_prep(const float* fc1w, const float* fc2w, const float* fc3w, const float* conv1w,
+RK_API int RKL_NAME(rk_lenet_prep)(const float* fc1w, const float* fc2w, const float* fc3w, const float* conv1w,
                          const float* conv2w, void* frag, hipStream_t s) {
   lenet_prep_kernel<<<NFRAG, 64, 0, s>>>(fc1w, fc2w, fc3w, conv1w, conv2w, (bf16x8*)frag);
   return (int)hipGetLastError();
 }
 
+#if !RK_LENET_H
 RK_API int rk_lenet_frag_bytes() { return NFRAG * 64 * 16; }
+#endif
 
 // Whole LeNet forward (conv stack + classifier) for N % 8 == 0: logits [N][10] fp32, plus the
 // saved state of the fused backward (a1, codes) and the transposed activations of the wgrads.
 // Diagnostics: phase timelines of the fused launches ([blocks][48] u64 each, or null = off).
-static uint64_t* g_fwd_trace = nullptr;
-static uint64_t* g_bwd_trace = nullptr;
+// (one pair of pointers, shared by the bf16 and fp16 builds of this file)
+#if RK_LENET_H
+extern uint64_t* g_fwd_trace;
+extern uint64_t* g_bwd_trace;
+#else
+uint64_t* g_fwd_trace = nullptr;
+uint64_t* g_bwd_trace = nullptr;
 RK_API void rk_lenet_set_trace(void* fwd, void* bwd) {
   g_fwd_trace = (uint64_t*)fwd;
   g_bwd_trace = (uint64_t*)bwd;
 }
+#endif
 
-RK_API int rk_lenet_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+RK_API int RKL_NAME(rk_lenet_fwd)(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                         const void* frag, const float* fb1, const float* fb2, const float* fb3, void* a1,
                         void* code1, void* code2, void* a2T, void* h1T, void* h2T, float* logits, int N,
                         hipStream_t s) {
@@ -1307,7 +1337,7 @@ RK_API int rk_lenet_fwd(const float* x, const float* w1, const float* b1, const 
 
 // Gradients are ACCUMULATED (atomics) into dw1/db1/dw2/db2 (zeroed or persistent f32 buffers).
 // `rounds`: samples groups of 4 processed per block (more rounds -> fewer global atomics).
-RK_API int rk_lenet_conv_bwd(const float* x, const void* a1, const void* code1, const void* da2, const void* code2,
+RK_API int RKL_NAME(rk_lenet_conv_bwd)(const float* x, const void* a1, const void* code1, const void* da2, const void* code2,
                              const float* w2, float* dw1, float* db1, float* dw2, float* db2, int N, int rounds,
                              hipStream_t s) {
   if (rounds < 1) rounds = 1;
@@ -1371,10 +1401,12 @@ static ClsBwd cls_bwd(const void* frag, const float* dy, const void* h1T, const 
 
 // The conv weight/bias gradients are NOT accumulated here: each block writes its totals to
 // slab[block][rk_lenet_slab_width()] (N/4 rows), which rk_mlp3_wgrad then sums into dw1/db1/dw2/db2.
+#if !RK_LENET_H
 RK_API int rk_lenet_slab_width() { return SLABW; }
 RK_API int rk_lenet_slab_cols() { return SLABN; }
+#endif
 
-RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const void* code2, const float* w2,
+RK_API int RKL_NAME(rk_lenet_bwd)(const float* x, const void* a1, const void* code1, const void* code2, const float* w2,
                         const void* frag, const float* dy, const void* h1T, const void* h2T, void* dyT, void* d2T,
                         void* d1T, float* slab, int N, int rounds, const LenetCE* ce, hipStream_t s) {
   rounds = 1;  // the fused kernel handles one group of SPB samples per block (argument kept for ABI)
@@ -1392,7 +1424,7 @@ RK_API int rk_lenet_bwd(const float* x, const void* a1, const void* code1, const
 // the rk_lenet_bwd outputs (transposed gradients, conv-gradient slab, loss partials) for a
 // softmax cross-entropy on `ce` (required; its d(logits) scale is ce->grad_scale).  rows (may be
 // null): the batch is gathered by this launch (RowSrc): x / ce->target are the batch buffers it fills.
-RK_API int rk_lenet_train(const float* x, const float* b1, const float* b2, const void* frag, const float* fb1,
+RK_API int RKL_NAME(rk_lenet_train)(const float* x, const float* b1, const float* b2, const void* frag, const float* fb1,
                           const float* fb2, const float* fb3, void* a1, void* code1, void* code2, void* a2T, void* h1T,
                           void* h2T, float* logits, void* dyT, void* d2T, void* d1T, float* slab, int N,
                           const LenetCE* ce, const RowSrc* rows, hipStream_t s) {

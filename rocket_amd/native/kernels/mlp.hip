@@ -22,7 +22,31 @@
 
 using namespace rk;
 
+// 16-bit format of every activation / fragment / weight-gradient operand: bf16 (default) or, when
+// this file is compiled with RK_LENET_H = 1 (the *_h.hip wrapper TU), IEEE fp16 for autocast fp16;
+// the fp16 build's entry points carry an "_h" suffix.
+#ifndef RK_LENET_H
+#define RK_LENET_H 0
+#endif
+#if RK_LENET_H
+#define RKL_NAME(n) n##_h
+#else
+#define RKL_NAME(n) n
+#endif
+
 namespace {
+
+constexpr bool kH16 = RK_LENET_H;
+__device__ __forceinline__ uint16_t c16(float v) { return kH16 ? f2h(v) : f2bf(v); }
+__device__ __forceinline__ float d16(uint16_t v) { return kH16 ? h2f(v) : bf2f(v); }
+__device__ __forceinline__ __bf16 e16(float v) { return __builtin_bit_cast(__bf16, c16(v)); }
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+  if constexpr (kH16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 
 constexpr int ROWS = 16;
 constexpr int MAXK = 512;
@@ -40,10 +64,10 @@ __device__ __forceinline__ bf16x8 wfrag_fwd(const float* W, int N, int K, int nt
   const float4 v1 = *(const float4*)(W + (int64_t)nc * K + kb);
   const bool oa = n < N && k0 < K, ob = n < N && k0 + 4 < K;
   bf16x8 b;
-  b[0] = (__bf16)(oa ? v0.x : 0.f); b[1] = (__bf16)(oa ? v0.y : 0.f);
-  b[2] = (__bf16)(oa ? v0.z : 0.f); b[3] = (__bf16)(oa ? v0.w : 0.f);
-  b[4] = (__bf16)(ob ? v1.x : 0.f); b[5] = (__bf16)(ob ? v1.y : 0.f);
-  b[6] = (__bf16)(ob ? v1.z : 0.f); b[7] = (__bf16)(ob ? v1.w : 0.f);
+  b[0] = e16(oa ? v0.x : 0.f); b[1] = e16(oa ? v0.y : 0.f);
+  b[2] = e16(oa ? v0.z : 0.f); b[3] = e16(oa ? v0.w : 0.f);
+  b[4] = e16(ob ? v1.x : 0.f); b[5] = e16(ob ? v1.y : 0.f);
+  b[6] = e16(ob ? v1.z : 0.f); b[7] = e16(ob ? v1.w : 0.f);
   return b;
 }
 
@@ -56,7 +80,7 @@ __device__ __forceinline__ bf16x8 wfrag_bwd(const float* W, int N, int K, int ct
   for (int j = 0; j < 8; ++j) {
     const int n = n0 + j;
     const float v = W[(int64_t)(n < N ? n : N - 1) * K + cc];
-    b[j] = (__bf16)((c < K && n < N) ? v : 0.f);
+    b[j] = e16((c < K && n < N) ? v : 0.f);
   }
   return b;
 }
@@ -78,7 +102,7 @@ __device__ __forceinline__ void layer_fwd(const uint16_t* in, int K, const float
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) bf[ks] = wfrag_fwd(W, N, K, nt, ks, lane);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(in, ks, lane), bf[ks], acc, 0, 0, 0);
+      for (int ks = 0; ks < KS; ++ks) acc = mfma16(afrag(in, ks, lane), bf[ks], acc);
     } else {  // generic widths: prefetch 4 k-steps at a time
       for (int k0 = 0; k0 < (K + 31) / 32; k0 += 4) {
         bf16x8 bf[4];
@@ -87,7 +111,7 @@ __device__ __forceinline__ void layer_fwd(const uint16_t* in, int K, const float
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (k0 + q < (K + 31) / 32)  // uniform; never read LDS columns past the staged width
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(in, k0 + q, lane), bf[q], acc, 0, 0, 0);
+            acc = mfma16(afrag(in, k0 + q, lane), bf[q], acc);
       }
     }
     const int col = nt * 16 + (lane & 15);
@@ -98,7 +122,7 @@ __device__ __forceinline__ void layer_fwd(const uint16_t* in, int K, const float
       float v = acc[i] + bias;
       if (relu) v = fmaxf(v, 0.f);
       if (col < N) {
-        if (out) out[r * LDSW + col] = f2bf(v);
+        if (out) out[r * LDSW + col] = c16(v);
         if (gout_f32 && row0 + r < M) gout_f32[(row0 + r) * N + col] = v;
       }
     }
@@ -118,7 +142,7 @@ __device__ __forceinline__ void layer_dgrad(const uint16_t* in, int N, const flo
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) bf[ks] = wfrag_bwd(W, N, K, ct, ks, lane);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(in, ks, lane), bf[ks], acc, 0, 0, 0);
+      for (int ks = 0; ks < KS; ++ks) acc = mfma16(afrag(in, ks, lane), bf[ks], acc);
     } else {
       for (int k0 = 0; k0 < (N + 31) / 32; k0 += 4) {
         bf16x8 bf[4];
@@ -127,7 +151,7 @@ __device__ __forceinline__ void layer_dgrad(const uint16_t* in, int N, const flo
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (k0 + q < (N + 31) / 32)
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(in, k0 + q, lane), bf[q], acc, 0, 0, 0);
+            acc = mfma16(afrag(in, k0 + q, lane), bf[q], acc);
       }
     }
     const int col = ct * 16 + (lane & 15);
@@ -137,12 +161,12 @@ __device__ __forceinline__ void layer_dgrad(const uint16_t* in, int N, const flo
       const bool rin = row0 + r < M;
       float v = acc[i];
       if (maskT) {
-        const float mv = bf2f(maskT[(int64_t)(col < K ? col : 0) * M + (rin ? row0 + r : 0)]);
+        const float mv = d16(maskT[(int64_t)(col < K ? col : 0) * M + (rin ? row0 + r : 0)]);
         v = mv > 0.f ? v : 0.f;
       }
       if (col < K) {
-        if (out) out[r * LDSW + col] = f2bf(v);
-        if (gout_rows && rin) gout_rows[(row0 + r) * K + col] = f2bf(v);
+        if (out) out[r * LDSW + col] = c16(v);
+        if (gout_rows && rin) gout_rows[(row0 + r) * K + col] = c16(v);
       }
     }
   }
@@ -161,8 +185,8 @@ __device__ void stage_rows(uint16_t* dst, const void* src, int src_f32, int K, i
     const int r = i / Kp, c = i % Kp;
     const bool ok = c < K && row0 + r < M;
     const int64_t o = ok ? (row0 + r) * K + c : 0;
-    const float v = src_f32 ? ((const float*)src)[o] : bf2f(((const uint16_t*)src)[o]);
-    dst[r * LDSW + c] = f2bf(ok ? v : 0.f);
+    const float v = src_f32 ? ((const float*)src)[o] : d16(((const uint16_t*)src)[o]);
+    dst[r * LDSW + c] = c16(ok ? v : 0.f);
   }
 }
 
@@ -493,10 +517,15 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     for (int s = 0; s < 4; ++s) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
+        // (the fragment's elements via its dwords: a per-element __bf16 -> uint16_t bit_cast of
+        // the vector's lanes miscompiles under -O3 to element 0 eight times)
+        const uint4 aw = __builtin_bit_cast(uint4, af[s][i]);
+        const uint32_t awd[4] = {aw.x, aw.y, aw.z, aw.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) rs[i] += (float)af[s][i][j];
+        for (int j = 0; j < 4; ++j)
+          rs[i] += d16((uint16_t)(awd[j] & 0xffffu)) + d16((uint16_t)(awd[j] >> 16));
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bf[s][j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[s][i], bf[s][j], acc[i][j]);
       }
     }
   }
@@ -557,7 +586,7 @@ struct RowsReq {
   int n_cur, bs;
 };
 static thread_local RowsReq g_rows{};
-RK_API int rk_mlp3_set_rows(const int64_t* table, int64_t* meta, int64_t* rows, int n_cur, int bs) {
+RK_API int RKL_NAME(rk_mlp3_set_rows)(const int64_t* table, int64_t* meta, int64_t* rows, int n_cur, int bs) {
   if (!table || !meta || !rows || n_cur < 0 || bs < 1) return (int)hipErrorInvalidValue;
   g_rows = RowsReq{table, meta, rows, n_cur, bs};
   return 0;
@@ -566,11 +595,15 @@ RK_API int rk_mlp3_set_rows(const int64_t* table, int64_t* meta, int64_t* rows, 
 // Diagnostics: per-block phase stamps of the grouped weight-gradient launch ([blocks][8] u64, or
 // null = off): start, operands reduced (after the block's LDS barrier), end; tiles also: old values
 // loaded, main loop done.
-static uint64_t* g_wgrad_trace = nullptr;
+#if RK_LENET_H
+extern uint64_t* g_wgrad_trace;
+#else
+uint64_t* g_wgrad_trace = nullptr;
 RK_API void rk_mlp3_set_trace(void* tr) { g_wgrad_trace = (uint64_t*)tr; }
+#endif
 
 // K0, N1, N2 must be multiples of 4 (16-byte weight rows); widths <= 512.
-RK_API int rk_mlp3_fwd(const void* x, int K0, const float* w1, const float* b1, int N1, const float* w2,
+RK_API int RKL_NAME(rk_mlp3_fwd)(const void* x, int K0, const float* w1, const float* b1, int N1, const float* w2,
                        const float* b2, int N2, const float* w3, const float* b3, int N3, void* xT, void* h1T,
                        void* h2T, float* y, int M, hipStream_t s) {
   if (K0 > MAXK || N1 > MAXK || N2 > MAXK || N3 > MAXK) return (int)hipErrorInvalidValue;
@@ -584,7 +617,7 @@ RK_API int rk_mlp3_fwd(const void* x, int K0, const float* w1, const float* b1, 
   return (int)hipGetLastError();
 }
 
-RK_API int rk_mlp3_dgrad(const float* dy, int N3, const float* w3, int N2, const void* h2T, const float* w2, int N1,
+RK_API int RKL_NAME(rk_mlp3_dgrad)(const float* dy, int N3, const float* w3, int N2, const void* h2T, const float* w2, int N1,
                          const void* h1T, const float* w1, int K0, void* dyT, void* d2T, void* d1T, void* dx, int M,
                          hipStream_t s) {
   if (K0 > MAXK || N1 > MAXK || N2 > MAXK || N3 > MAXK) return (int)hipErrorInvalidValue;
@@ -618,7 +651,7 @@ struct WgradEpi {
 // norm_by_count: the backward scaled by 1 / M instead of the loss's 1 / (valid count) and stored
 // per-block valid counts after its loss partials (loss->partials[nparts ..]): gradients are scaled
 // by M / their sum, the loss divided by it.
-RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* const* xT, float* const* dw,
+RK_API int RKL_NAME(rk_mlp3_wgrad_loss)(int nprob, const void* const* dT, const void* const* xT, float* const* dw,
                               float* const* db, const int* Ns, const int* Ks, int M, const float* slab, int slab_rows,
                               int slab_width, float* const* slab_dst, const int* slab_bound, const LossFin* loss,
                               const WgradEpi* epi, float gscale, int norm_by_count, hipStream_t s) {
@@ -705,9 +738,9 @@ RK_API int rk_mlp3_wgrad_loss(int nprob, const void* const* dT, const void* cons
   return (int)hipGetLastError();
 }
 
-RK_API int rk_mlp3_wgrad(int nprob, const void* const* dT, const void* const* xT, float* const* dw, float* const* db,
+RK_API int RKL_NAME(rk_mlp3_wgrad)(int nprob, const void* const* dT, const void* const* xT, float* const* dw, float* const* db,
                          const int* Ns, const int* Ks, int M, const float* slab, int slab_rows, int slab_width,
                          float* const* slab_dst, const int* slab_bound, hipStream_t s) {
-  return rk_mlp3_wgrad_loss(nprob, dT, xT, dw, db, Ns, Ks, M, slab, slab_rows, slab_width, slab_dst, slab_bound,
+  return RKL_NAME(rk_mlp3_wgrad_loss)(nprob, dT, xT, dw, db, Ns, Ks, M, slab, slab_rows, slab_width, slab_dst, slab_bound,
                             nullptr, nullptr, 1.f, 0, s);
 }

@@ -383,8 +383,9 @@ __global__ void __launch_bounds__(BN_T) colsum_acc_kernel(const T* __restrict__ 
 // dz = dh * gelu'(z) (bf16 [R][C]) AND out[c] += sum_r dz[r][c]: the transformer MLP's GELU
 // backward fused with fc1's bias gradient, so the [tokens x hidden] gradient is read once instead of
 // twice.  Grid and two-level reduction as colsum_acc_kernel.
-__global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const uint16_t* __restrict__ dh,
-                                                               const uint16_t* __restrict__ z, uint16_t* __restrict__ dz,
+template <typename T>  // uint16_t: bf16, f16_t: fp16
+__global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const T* __restrict__ dh,
+                                                               const T* __restrict__ z, T* __restrict__ dz,
                                                                int64_t R, int C, int rpb, float* part,
                                                                unsigned* counters, float* out) {
   __shared__ __attribute__((aligned(16))) float lds[BN_WV][BN_CT];
@@ -399,23 +400,31 @@ __global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const uint16_t* _
   float acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  for (int64_t r = r0 + rg; r < r1; r += BN_U * BN_RG) {
+  // the block's rows as one wave-uniform base + 32-bit per-lane offsets (rpb * C < 2^31, host
+  // check): no 64-bit address arithmetic per row
+  const int64_t base = r0 * C;
+  const T* dhb = dh + base;
+  const T* zb = z + base;
+  T* dzb = dz + base;
+  const int nr = (int)(r1 - r0);
+  for (int r = rg; r < nr; r += BN_U * BN_RG) {
     float g[BN_U][8], v[BN_U][8];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
-      const int64_t off = min(r + u * BN_RG, r1 - 1) * C + (cok ? c : 0);
-      V8<uint16_t>::load(dh + off, g[u]);
-      V8<uint16_t>::load(z + off, v[u]);
+      // byte offset: base (SGPR) + zero-extended 32-bit VGPR offset = the saddr load form
+      const uint32_t off = ((uint32_t)min(r + u * BN_RG, nr - 1) * (uint32_t)C + (uint32_t)(cok ? c : 0)) * 2u;
+      V8<T>::load((const T*)((const char*)dhb + off), g[u]);
+      V8<T>::load((const T*)((const char*)zb + off), v[u]);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
-      const bool ok = r + u * BN_RG < r1 && cok;
+      const bool ok = r + u * BN_RG < nr && cok;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         v[u][k] = g[u][k] * gelu_grad(v[u][k]);
         acc[k] += ok ? v[u][k] : 0.f;
       }
-      if (ok) V8<uint16_t>::store(dz + (r + u * BN_RG) * C + c, v[u]);
+      if (ok) V8<T>::store((T*)((char*)dzb + ((uint32_t)(r + u * BN_RG) * (uint32_t)C + c) * 2u), v[u]);
     }
   }
   reduce_rowgroups(acc, lds, s1);
@@ -769,93 +778,152 @@ __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const T* __restrict__ x, c
   }
 }
 
+// a 4-element group kept as loaded (16-bit: 2 registers instead of 4) until its use
+template <typename T> struct Raw4 {
+  uint2 u;
+  __device__ __forceinline__ void load(const T* p) { u = *(const uint2*)p; }
+  __device__ __forceinline__ void get(float* v) const { ld4<T>((const T*)&u, v); }
+};
+template <> struct Raw4<float> {
+  float4 u;
+  __device__ __forceinline__ void load(const float* p) { u = *(const float4*)p; }
+  __device__ __forceinline__ void get(float* v) const { v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; }
+};
+
 // NP = 2: block partials of dgamma / dbeta; NP = 3: also the column sums of the added branch's
 // gradient (dres) — the bias gradient of the linear layer that produced the branch (ViT proj /
 // fc2), so that layer's backward needs no column-sum pass over its output gradient.
+// Streaming design: the row reductions run on the DPP network (no LDS instructions), gamma is held
+// in registers, loads stay packed until used, and the block's column partials meet in ONE [NP][C]
+// LDS image through LDS float atomics (9 KB at C = 768 instead of 36: ~7 blocks per CU resident
+// instead of 4, so ~1.75x the rows in flight).
 template <typename T, typename TO, int NV, int NP>
 __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
                                                       const float* __restrict__ g, const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                       const T* __restrict__ dsum, TO* __restrict__ dres,
                                                       float* part, int64_t rows, int C, int rows_per_block) {
-  extern __shared__ float sm[];  // [LN_W][NP][C]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float ag[NV][4], ab[NV][4], ar[NV][4];
+  extern __shared__ float sm[];  // [NP][C]
+  // w (so each row index and row pointer) is wave-uniform: the row bases live in SGPRs and every
+  // lane addresses all five tensors with the same small column offset
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int i = threadIdx.x; i < NP * C; i += LN_T) sm[i] = 0.f;
+  float ag[NV][4], ab[NV][4], ar[NV][4], gm[NV][4];
 #pragma unroll
-  for (int j = 0; j < NV; ++j)
+  for (int j = 0; j < NV; ++j) {
+    const int c = (j * 64 + lane) * 4;
+    if (g && c < C) ld4<float>(g + c, gm[j]);
+    else gm[j][0] = gm[j][1] = gm[j][2] = gm[j][3] = 1.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) ag[j][k] = ab[j][k] = ar[j][k] = 0.f;
+  }
   const int64_t rb = (int64_t)blockIdx.x * rows_per_block;
   const int64_t re = min(rows, rb + rows_per_block);
+  // software prefetch: the next row's loads are in flight while this row is reduced and stored
+  Raw4<T> xr[NV], sr[NV], xn[NV], sn[NV];
+  Raw4<TO> dr[NV], dn[NV];
+  auto fetch = [&](int64_t row, Raw4<T> (&xa)[NV], Raw4<TO> (&da)[NV], Raw4<T> (&sa)[NV]) {
+    const T* xrow = x + row * C;
+    const TO* dyrow = dy + row * C;
+    const T* dsrow = dsum ? dsum + row * C : nullptr;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (j * 64 + lane) * 4;
+      const int cc = c < C ? c : 0;
+      xa[j].load(xrow + cc);
+      da[j].load(dyrow + cc);
+      if (dsum) sa[j].load(dsrow + cc);
+    }
+  };
+  constexpr bool PF = NV <= 4;  // wide rows (C > 1024): no room for a second row's registers
+  if (PF && rb + w < re) fetch(rb + w, xr, dr, sr);
   for (int64_t row = rb + w; row < re; row += LN_W) {
     const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[NV][4], gy[NV][4], ds[NV][4];
+    if (!PF) fetch(row, xr, dr, sr);
+    else if (row + LN_W < re) fetch(row + LN_W, xn, dn, sn);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int c = (j * 64 + lane) * 4;
       if (c < C) {
         float xv[4], dv[4];
-        ld4<T>(x + row * C + c, xv);
-        ld4<TO>(dy + row * C + c, dv);
-        if (dsum) ld4<T>(dsum + row * C + c, ds[j]);  // in flight with x / dy, not after the reductions
+        xr[j].get(xv);
+        dr[j].get(dv);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          xh[j][k] = (xv[k] - mean) * rstd;
-          gy[j][k] = dv[k] * (g ? g[c + k] : 1.f);
-          s1 += gy[j][k];
-          s2 += gy[j][k] * xh[j][k];
-          ag[j][k] += dv[k] * xh[j][k];
+          const float xh = (xv[k] - mean) * rstd;
+          const float gy = dv[k] * gm[j][k];
+          s1 += gy;
+          s2 += gy * xh;
+          ag[j][k] += dv[k] * xh;
           ab[j][k] += dv[k];
         }
       }
     }
-    s1 = wave_sum(s1) / C;
-    s2 = wave_sum(s2) / C;
+    s1 = wave_sum_dpp(s1) / C;
+    s2 = wave_sum_dpp(s2) / C;
+    T* dxrow = dx + row * C;
+    TO* dresrow = dres ? dres + row * C : nullptr;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int c = (j * 64 + lane) * 4;
       if (c < C) {
-        float o[4];
+        float xv[4], dv[4], o[4];
+        xr[j].get(xv);
+        dr[j].get(dv);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = rstd * (gy[j][k] - s1 - xh[j][k] * s2);
+        for (int k = 0; k < 4; ++k) o[k] = rstd * (dv[k] * gm[j][k] - s1 - (xv[k] - mean) * rstd * s2);
         if (dsum) {  // the residual stream's own gradient joins here (fused add-norm)
+          float ds[4];
+          sr[j].get(ds);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) o[k] += ds[j][k];
+          for (int k = 0; k < 4; ++k) o[k] += ds[k];
         }
-        st4<T>(dx + row * C + c, o);
-        if (dres) st4<TO>(dres + row * C + c, o);  // gradient of the added branch
+        st4<T>(dxrow + c, o);
+        if (dres) st4<TO>(dresrow + c, o);  // gradient of the added branch
         if (NP == 3) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) ar[j][k] += o[k];
         }
       }
     }
+    if (PF) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        xr[j] = xn[j];
+        dr[j] = dn[j];
+        sr[j] = sn[j];
+      }
+    }
   }
-  // block partial of dgamma/dbeta
+  // the image is k-major per partial (column 4q + k at k * C/4 + q): consecutive lanes add to
+  // consecutive words (conflict-free); colsum_kernel undoes the permutation (perm_q = C/4)
+  __syncthreads();  // the zeroed image
+  const int Q = C / 4;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const int c = (j * 64 + lane) * 4;
-    if (c < C) {  // 16-byte stores: consecutive lanes fill whole bank rows (C % 4 == 0)
-      *(float4*)&sm[(w * NP) * C + c] = make_float4(ag[j][0], ag[j][1], ag[j][2], ag[j][3]);
-      *(float4*)&sm[(w * NP + 1) * C + c] = make_float4(ab[j][0], ab[j][1], ab[j][2], ab[j][3]);
-      if (NP == 3) *(float4*)&sm[(w * NP + 2) * C + c] = make_float4(ar[j][0], ar[j][1], ar[j][2], ar[j][3]);
+    const int q = j * 64 + lane;
+    if (q < Q) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        atomicAdd(&sm[k * Q + q], ag[j][k]);
+        atomicAdd(&sm[C + k * Q + q], ab[j][k]);
+        if (NP == 3) atomicAdd(&sm[2 * C + k * Q + q], ar[j][k]);
+      }
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < NP * C; i += LN_T) {
-    float t = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < LN_W; ++ww) t += sm[ww * NP * C + i];
-    part[(int64_t)blockIdx.x * NP * C + i] = t;
-  }
+  for (int i = threadIdx.x; i < NP * C; i += LN_T) part[(int64_t)blockIdx.x * NP * C + i] = sm[i];
 }
 
 // column sums of the [nrows][2C] block partials -> dgamma (first C) / dbeta (last C), accumulated.
 // Block: 64 columns x 16 row-slices; each thread strides its slice with 4 loads in flight.
+// perm_q > 0: each C-wide section of a partial row is stored k-major (position k * perm_q + q holds
+// column 4q + k, ln_bwd_kernel's image).
 constexpr int CS_T = 1024;
 __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ part, int nrows, int C2,
-                                                      float* dgamma, float* dbeta, int C, float* dthird = nullptr) {
+                                                      float* dgamma, float* dbeta, int C, float* dthird = nullptr,
+                                                      int perm_q = 0) {
   __shared__ float red[CS_T / 64][65];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int sl = threadIdx.x >> 6, nsl = CS_T / 64;
@@ -874,12 +942,15 @@ __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ 
     float u = 0.f;
 #pragma unroll
     for (int k = 0; k < CS_T / 64; ++k) u += red[k][threadIdx.x];
-    if (col < C) {
-      if (dgamma) dgamma[col] += u;
-    } else if (col < 2 * C) {
-      if (dbeta) dbeta[col - C] += u;
+    const int sec = col / C;
+    int oc = col - sec * C;
+    if (perm_q > 0) oc = 4 * (oc % perm_q) + oc / perm_q;
+    if (sec == 0) {
+      if (dgamma) dgamma[oc] += u;
+    } else if (sec == 1) {
+      if (dbeta) dbeta[oc] += u;
     } else if (dthird) {
-      dthird[col - 2 * C] = u;  // written, not accumulated: the caller needs no zeroed buffer
+      dthird[oc] = u;  // written, not accumulated: the caller needs no zeroed buffer
     }
   }
 }
@@ -1118,17 +1189,26 @@ RK_API int rk_colsum_acc(int dt, const void* x, int64_t R, int C, float* out, fl
   return (int)hipGetLastError();
 }
 
-// dz = dh * gelu'(z) and out[c] += sum_r dz[r][c] (all bf16 [R][C] except out; C % 8 == 0); ws /
-// counters as rk_colsum_acc
-RK_API int rk_gelu_bwd_colsum(const void* dh, const void* z, void* dz, int64_t R, int C, float* out, float* ws,
-                              unsigned* counters, hipStream_t s) {
-  if (C % 8 || R <= 0) return (int)hipErrorInvalidValue;
+// dz = dh * gelu'(z) and out[c] += sum_r dz[r][c] (all 16-bit [R][C] of dtype dt, bf16 or fp16,
+// except out; C % 8 == 0); ws / counters as rk_colsum_acc
+RK_API int rk_gelu_bwd_colsum16(int dt, const void* dh, const void* z, void* dz, int64_t R, int C, float* out,
+                                float* ws, unsigned* counters, hipStream_t s) {
+  if (C % 8 || R <= 0 || (dt != BF16 && dt != F16)) return (int)hipErrorInvalidValue;
   int rpb;
   const int rb = bn_grid_rows(R, C, &rpb);
+  if ((int64_t)rpb * C * 2 >= (1ll << 32)) return (int)hipErrorInvalidValue;
   dim3 grid((C + BN_CT - 1) / BN_CT, rb);
-  gelu_bwd_colsum_kernel<<<grid, BN_T, 0, s>>>((const uint16_t*)dh, (const uint16_t*)z, (uint16_t*)dz, R, C, rpb, ws,
-                                               counters, out);
+  if (dt == F16)
+    gelu_bwd_colsum_kernel<f16_t><<<grid, BN_T, 0, s>>>((const f16_t*)dh, (const f16_t*)z, (f16_t*)dz, R, C, rpb, ws,
+                                                        counters, out);
+  else
+    gelu_bwd_colsum_kernel<uint16_t><<<grid, BN_T, 0, s>>>((const uint16_t*)dh, (const uint16_t*)z, (uint16_t*)dz, R, C,
+                                                           rpb, ws, counters, out);
   return (int)hipGetLastError();
+}
+RK_API int rk_gelu_bwd_colsum(const void* dh, const void* z, void* dz, int64_t R, int C, float* out, float* ws,
+                              unsigned* counters, hipStream_t s) {
+  return rk_gelu_bwd_colsum16(BF16, dh, z, dz, R, C, out, ws, counters, s);
 }
 
 // y = relu?(x*scale + shift + res?); dt: x dtype, dto: y/res dtype.  mask (uint8 [R][C/8], may be
@@ -1248,10 +1328,28 @@ RK_API int rk_ln_fwd(int dt, int dto, const void* x, const void* res, void* sum_
   return (int)hipGetLastError();
 }
 
-constexpr int LN_BWD_RPB = 16;  // rows per block (4 per wave): ~1600 blocks for ViT's 25k rows
+// Rows per block of ln_bwd_kernel: ONE round of blocks over the chip (3 resident per CU at its
+// ~150 VGPRs), each wave walking rows with the next row's loads in flight; at least 16 rows.
+int ln_num_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cus[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+int ln_bwd_rpb(int64_t rows) {
+  const int64_t slots = (int64_t)ln_num_cus() * 3;
+  int64_t rpb = (rows + slots - 1) / slots;
+  rpb = (rpb + LN_W - 1) / LN_W * LN_W;
+  return (int)std::max<int64_t>(16, std::min<int64_t>(rpb, 1 << 20));
+}
 
 RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
-  const int64_t rpb = LN_BWD_RPB;
+  const int64_t rpb = ln_bwd_rpb(rows);
   return ((rows + rpb - 1) / rpb) * 3 * C;  // up to three column partials per block (rk_ln_bwd)
 }
 
@@ -1264,11 +1362,11 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
                      float* dres_sum, int64_t rows, int C, float* ws, unsigned* counter, hipStream_t s) {
   if ((dt == F16 && dto == BF16) || (dt == BF16 && dto == F16)) return (int)hipErrorInvalidValue;
   if (C % 4 || C > 64 * 4 * LN_MAXV || (dres_sum && !dres)) return (int)hipErrorInvalidValue;
-  const int rpb = LN_BWD_RPB;
+  const int rpb = ln_bwd_rpb(rows);
   const int grid = (int)((rows + rpb - 1) / rpb);
   const int nv = (C + 255) / 256;
   const int np = dres_sum ? 3 : 2;
-  const size_t smem = (size_t)LN_W * np * C * sizeof(float);
+  const size_t smem = (size_t)np * C * sizeof(float);
 #define RK_LB(T, TO, NV)                                                                                               \
   if (np == 3)                                                                                                         \
     ln_bwd_kernel<T, TO, NV, 3><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx,             \
@@ -1293,7 +1391,7 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
 #undef RK_LBN
 #undef RK_LB
   if (dgamma || dbeta || dres_sum)
-    colsum_kernel<<<(np * C + 63) / 64, CS_T, 0, s>>>(ws, grid, np * C, dgamma, dbeta, C, dres_sum);
+    colsum_kernel<<<(np * C + 63) / 64, CS_T, 0, s>>>(ws, grid, np * C, dgamma, dbeta, C, dres_sum, C / 4);
   (void)counter;
   return (int)hipGetLastError();
 }

@@ -74,7 +74,7 @@ template <> struct Ld<f16_t> {
 // e^{-u^2} is shared with gelu'.  Returns erf(u) given e = exp(-u*u).
 __device__ __forceinline__ float erf_as(float u, float e) {
   const float a = fabsf(u);
-  const float t = __frcp_rn(__builtin_fmaf(0.3275911f, a, 1.f));
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f, a, 1.f));  // v_rcp_f32 (1 ulp), not an IEEE divide
   float p = __builtin_fmaf(1.061405429f, t, -1.453152027f);
   p = __builtin_fmaf(p, t, 1.421413741f);
   p = __builtin_fmaf(p, t, -0.284496736f);
@@ -96,6 +96,25 @@ __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
   return v;
+}
+// The same sum on the DPP network (no LDS traffic: __shfl_xor lowers to ds_bpermute, an LDS
+// instruction that queues behind and bank-conflicts with the kernel's own LDS work): butterflies
+// inside each 16-lane row, then the four row sums read out through SGPRs.  All 64 lanes must be
+// active; the result is wave-uniform.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  int t = __builtin_bit_cast(int, v);
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0xb1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]
+  t = __builtin_bit_cast(int, v);
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x4e, 0xf, 0xf, false));  // quad_perm [2,3,0,1]
+  t = __builtin_bit_cast(int, v);
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  t = __builtin_bit_cast(int, v);
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x140, 0xf, 0xf, false));  // row_mirror
+  t = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 48)));
 }
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

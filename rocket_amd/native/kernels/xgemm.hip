@@ -15,7 +15,16 @@ int xg_num_cus() {
   return cus[dev];
 }
 
+int g_dbg = 0;  // rk_xgemm_set_dbg
+
 }  // namespace
+
+// Diagnostics only (timing what each part of the main loop costs; results are garbage): bit 0
+// skips the LDS-DMA, 1 the barrier, 2 the fragment reads, 3 the MFMAs.
+RK_API int rk_xgemm_set_dbg(int bits) {
+  g_dbg = bits;
+  return 0;
+}
 
 // Configs (block tile, waves; one persistent block per CU, 4-slot ring of 32-deep k-units):
 //   0: 256 x 256, 8 waves (2 x 4), 128 x 64 per wave   (128 KiB LDS)
@@ -45,6 +54,7 @@ RK_API int rk_xgemm(const void* a, int64_t lda, int a_kmaj, const void* b, int64
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.c_dt = c_dt; g.epi = epi; g.accumulate = accumulate;
   g.lds_epi = 0;
+  g.dbg = g_dbg;
   if (splitk < 1) splitk = 1;
   const int kq = 32;  // split boundaries on whole units
   const int kps = ((K + kq - 1) / kq + splitk - 1) / splitk * kq;

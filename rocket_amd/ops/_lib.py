@@ -42,6 +42,7 @@ KERNEL_SIGS = {
                          c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "rk_xgemm": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p,
                          c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "rk_xgemm_set_dbg": (c_int, [c_int]),
     "rk_slab_acc": (c_int, [c_void_p, c_int, c_int, c_int64, c_void_p, c_int, c_void_p]),
     "rk_conv_fwd": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 11 + [c_void_p, c_void_p]),
     "rk_conv_fwd_c8": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p] + [c_int] * 10 + [c_void_p, c_void_p]),
@@ -91,6 +92,8 @@ KERNEL_SIGS = {
     "rk_bn_relu_maxpool": (c_int, [c_int] + [c_void_p] * 5 + [c_int] * 6 + [c_void_p]),
     "rk_maxpool_bwd": (c_int, [c_int] + [c_void_p] * 3 + [c_int] * 6 + [c_void_p]),
     "rk_colsum_acc": (c_int, [c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rk_gelu_bwd_colsum16": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]),
     "rk_gelu_bwd_colsum": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),
     "rk_bn_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int] + [c_void_p] * 11),
@@ -133,6 +136,11 @@ KERNEL_SIGS = {
     "rk_p2p_destroy": (c_int, [c_void_p]),
     "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 11 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
 }
+
+# fp16 builds of the fused LeNet kernels (lenet_conv_h.hip / mlp_h.hip): same signatures
+KERNEL_SIGS.update({n + "_h": KERNEL_SIGS[n] for n in (
+    "rk_lenet_conv_fwd", "rk_lenet_conv_bwd", "rk_lenet_prep", "rk_lenet_fwd", "rk_lenet_bwd", "rk_lenet_train",
+    "rk_mlp3_fwd", "rk_mlp3_dgrad", "rk_mlp3_wgrad", "rk_mlp3_wgrad_loss", "rk_mlp3_set_rows")})
 
 
 class NativeError(RuntimeError):

@@ -156,7 +156,7 @@ def attention_qkv(qkv: torch.Tensor, heads: int, scale: float | None = None) -> 
     D = C3 // (3 * heads)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     # fp16: the default kernel configuration only (8-wave forward, fused backward)
-    f16_ok = qkv.dtype == torch.float16 and ATTN_WAVES[0] == 82 and ATTN_BWD == "fused"
+    f16_ok = qkv.dtype == torch.float16 and ATTN_BWD == "fused"  # fp16 backward: the fused kernel
     if (_ops.fused_enabled() and qkv.is_cuda and (qkv.dtype == torch.bfloat16 or f16_ok) and D == 64
             and L <= _lib.kernels().rk_attn_max_len()):
         return _AttnQKV.apply(qkv, heads, scale)

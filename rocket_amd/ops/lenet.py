@@ -26,6 +26,19 @@ from rocket_amd.ops import _lib
 from rocket_amd.ops.linear import _direct, gemm, grad_ready
 
 
+def half_mode(device) -> bool:
+    """True under fp16 autocast on ``device``: the fused LeNet then runs its fp16 kernel build
+    (``*_h`` entries of lenet_conv_h.hip / mlp_h.hip: fp16 activations, fragments and MFMA
+    operands, fp32 accumulation), otherwise bf16."""
+    dt = device.type if isinstance(device, torch.device) else str(device)
+    return torch.is_autocast_enabled(dt) and torch.get_autocast_dtype(dt) == torch.float16
+
+
+def _k(lib, name: str, half: bool):
+    """The bf16 or fp16 build of a fused-LeNet entry point."""
+    return getattr(lib, name + "_h" if half else name)
+
+
 def _grad_targets(params: Sequence[torch.nn.Parameter], device):
     """Return (buffers, direct): persistent grads, or one zeroed flat buffer split per param."""
     if all(_direct(p) for p in params):
@@ -48,21 +61,23 @@ def _finish(params, bufs, direct):
 
 class _LeNetFeatures(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, half=False):
         lib = _lib.kernels()
         x = x.contiguous().float()
         N = x.shape[0]
         assert tuple(x.shape[1:]) == (1, 28, 28), "lenet_features expects [N,1,28,28]"
         dev = x.device
-        a1 = torch.empty(N, 1176, dtype=torch.bfloat16, device=dev)
+        dt = torch.float16 if half else torch.bfloat16
+        a1 = torch.empty(N, 1176, dtype=dt, device=dev)
         c1 = torch.empty(N, 1176, dtype=torch.uint8, device=dev)
-        a2 = torch.empty(N, 400, dtype=torch.bfloat16, device=dev)
+        a2 = torch.empty(N, 400, dtype=dt, device=dev)
         c2 = torch.empty(N, 400, dtype=torch.uint8, device=dev)
         w1c, b1c, w2c, b2c = (t.detach().float().contiguous() for t in (w1, b1, w2, b2))
-        _lib.check(lib.rk_lenet_conv_fwd(x.data_ptr(), w1c.data_ptr(), b1c.data_ptr(), w2c.data_ptr(), b2c.data_ptr(),
+        _lib.check(_k(lib, "rk_lenet_conv_fwd", half)(x.data_ptr(), w1c.data_ptr(), b1c.data_ptr(), w2c.data_ptr(), b2c.data_ptr(),
                                          a1.data_ptr(), c1.data_ptr(), a2.data_ptr(), c2.data_ptr(), N,
                                          _lib.stream_ptr(dev)), "rk_lenet_conv_fwd")
         ctx.params = (w1, b1, w2, b2)
+        ctx.half = half
         ctx.save_for_backward(x, a1, c1, c2, w2c)
         return a2
 
@@ -72,19 +87,19 @@ class _LeNetFeatures(torch.autograd.Function):
         x, a1, c1, c2, w2c = ctx.saved_tensors
         N = x.shape[0]
         da2 = da2.contiguous()
-        if da2.dtype != torch.bfloat16:
-            da2 = da2.to(torch.bfloat16)
+        if da2.dtype != a1.dtype:
+            da2 = da2.to(a1.dtype)
         params = ctx.params
         bufs, direct = _grad_targets(params, x.device)
         rounds = max(1, N // 2048)
-        _lib.check(lib.rk_lenet_conv_bwd(x.data_ptr(), a1.data_ptr(), c1.data_ptr(), da2.data_ptr(), c2.data_ptr(),
+        _lib.check(_k(lib, "rk_lenet_conv_bwd", ctx.half)(x.data_ptr(), a1.data_ptr(), c1.data_ptr(), da2.data_ptr(), c2.data_ptr(),
                                          w2c.data_ptr(), bufs[0].data_ptr(), bufs[1].data_ptr(), bufs[2].data_ptr(),
                                          bufs[3].data_ptr(), N, rounds, _lib.stream_ptr(x.device)), "rk_lenet_conv_bwd")
-        return (None, *_finish(params, bufs, direct))
+        return (None, *_finish(params, bufs, direct), None)
 
 
 def lenet_features(x, w1, b1, w2, b2):
-    return _LeNetFeatures.apply(x, w1, b1, w2, b2)
+    return _LeNetFeatures.apply(x, w1, b1, w2, b2, half_mode(x.device))
 
 
 class _MLPHead(torch.autograd.Function):
@@ -92,22 +107,24 @@ class _MLPHead(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, w3, b3):
         lib = _lib.kernels()
         x = x.contiguous()
-        if x.dtype != torch.bfloat16:
+        half = x.dtype == torch.float16  # fp16 features (fp16 autocast) -> fp16 kernel build
+        if not half and x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
         M, K0 = x.shape
         N1, N2, N3 = w1.shape[0], w2.shape[0], w3.shape[0]
         dev = x.device
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        bf = dict(dtype=x.dtype, device=dev)
         xT = torch.empty(K0, M, **bf)
         h1T = torch.empty(N1, M, **bf)
         h2T = torch.empty(N2, M, **bf)
         y = torch.empty(M, N3, dtype=torch.float32, device=dev)
         ws = [t.detach().float().contiguous() for t in (w1, b1, w2, b2, w3, b3)]
-        _lib.check(lib.rk_mlp3_fwd(x.data_ptr(), K0, ws[0].data_ptr(), ws[1].data_ptr(), N1, ws[2].data_ptr(),
+        _lib.check(_k(lib, "rk_mlp3_fwd", half)(x.data_ptr(), K0, ws[0].data_ptr(), ws[1].data_ptr(), N1, ws[2].data_ptr(),
                                    ws[3].data_ptr(), N2, ws[4].data_ptr(), ws[5].data_ptr(), N3, xT.data_ptr(),
                                    h1T.data_ptr(), h2T.data_ptr(), y.data_ptr(), M, _lib.stream_ptr(dev)),
                    "rk_mlp3_fwd")
         ctx.params = (w1, b1, w2, b2, w3, b3)
+        ctx.half = half
         ctx.save_for_backward(xT, h1T, h2T, ws[0], ws[2], ws[4])
         return y
 
@@ -119,13 +136,14 @@ class _MLPHead(torch.autograd.Function):
         N1, N2, N3 = w1.shape[0], w2.shape[0], w3.shape[0]
         dev = xT.device
         dy = dy.contiguous().float()
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        half = ctx.half
+        bf = dict(dtype=xT.dtype, device=dev)
         dyT = torch.empty(N3, M, **bf)
         d2T = torch.empty(N2, M, **bf)
         d1T = torch.empty(N1, M, **bf)
         dx = torch.empty(M, K0, **bf) if ctx.needs_input_grad[0] else None
         stream = _lib.stream_ptr(dev)
-        _lib.check(lib.rk_mlp3_dgrad(dy.data_ptr(), N3, w3.data_ptr(), N2, h2T.data_ptr(), w2.data_ptr(), N1,
+        _lib.check(_k(lib, "rk_mlp3_dgrad", half)(dy.data_ptr(), N3, w3.data_ptr(), N2, h2T.data_ptr(), w2.data_ptr(), N1,
                                      h1T.data_ptr(), w1.data_ptr(), K0, dyT.data_ptr(), d2T.data_ptr(),
                                      d1T.data_ptr(), _lib.ptr(dx), M, stream), "rk_mlp3_dgrad")
         params = ctx.params
@@ -135,11 +153,13 @@ class _MLPHead(torch.autograd.Function):
         if M % 8 == 0:
             P = ctypes.c_void_p * 3
             I = ctypes.c_int * 3
-            _lib.check(lib.rk_mlp3_wgrad(3, P(*[p[0].data_ptr() for p in probs]), P(*[p[1].data_ptr() for p in probs]),
+            _lib.check(_k(lib, "rk_mlp3_wgrad", half)(3, P(*[p[0].data_ptr() for p in probs]), P(*[p[1].data_ptr() for p in probs]),
                                          P(*[p[2].data_ptr() for p in probs]), P(*[p[3].data_ptr() for p in probs]),
                                          I(*[p[4] for p in probs]), I(*[p[5] for p in probs]), M, None, 0, 0, None,
                                          None, stream), "rk_mlp3_wgrad")
         else:  # generic MFMA GEMM: dW[n][k] += sum_m dT[n][m] xT[k][m]
+            if half:
+                raise NotImplementedError("fused fp16 MLP head needs M % 8 == 0")
             for dT, inT, wbuf, bbuf, n_out, k_in in probs:
                 gemm(dT, inT, wbuf, M=n_out, N=k_in, K=M, lda=M, ldb=M, ldc=k_in, accumulate=True, rowsum=bbuf,
                      cfg=0)
@@ -220,9 +240,11 @@ class LeNetFragments:
     SPECULATE = os.environ.get("ROCKET_LENET_SPEC", "1") != "0"
     MAX_MISSES = 2
 
-    def __init__(self, device):
+    def __init__(self, device, half: bool = False):
         lib = _lib.kernels()
-        self.frag = torch.empty(int(lib.rk_lenet_frag_bytes()) // 2, dtype=torch.bfloat16, device=device)
+        self.half = half
+        self.frag = torch.empty(int(lib.rk_lenet_frag_bytes()) // 2, dtype=torch.float16 if half else torch.bfloat16,
+                                device=device)
         if LeNetFragments._maps_host is None:
             LeNetFragments._maps_host = _frag_index_maps()
         self.maps = [torch.from_numpy(m).to(device) for m in LeNetFragments._maps_host]
@@ -237,14 +259,16 @@ class LeNetFragments:
     def ensure(self, fc1w, fc2w, fc3w, conv1w, conv2w, stream) -> torch.Tensor:
         params = (fc1w, fc2w, fc3w, conv1w, conv2w)
         versions = tuple(p._version for p in params)
-        live = (self.params is not None and all(a is b for a, b in zip(params, self.params))
+        # the fp16 table is no optimizer shadow (fused optimizers maintain bf16 shadows only):
+        # it is rebuilt by every forward (one 282-block launch inside the step's graph)
+        live = (not self.half and self.params is not None and all(a is b for a, b in zip(params, self.params))
                 and versions == self.versions and all(getattr(p, "_rocket_shadow_live", False) for p in params))
         if not live:
             cw = [p.detach().float().contiguous() for p in params]
-            _lib.check(_lib.kernels().rk_lenet_prep(cw[0].data_ptr(), cw[1].data_ptr(), cw[2].data_ptr(),
+            _lib.check(_k(_lib.kernels(), "rk_lenet_prep", self.half)(cw[0].data_ptr(), cw[1].data_ptr(), cw[2].data_ptr(),
                                                     cw[3].data_ptr(), cw[4].data_ptr(), self.frag.data_ptr(), stream),
                        "rk_lenet_prep")
-            if self.params is None or not all(a is b for a, b in zip(params, self.params)):
+            if not self.half and (self.params is None or not all(a is b for a, b in zip(params, self.params))):
                 for p, m in zip(params, self.maps):
                     if p.dtype == torch.float32 and p.is_contiguous():
                         p._rocket_bf16_shadow = (m, self.frag)
@@ -357,6 +381,7 @@ class _LeNetFused(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, f1w, f1b, f2w, f2b, f3w, f3b, frags, target=None):
+        half = frags.half
         lib = _lib.kernels()
         x = x.contiguous().float()
         N = x.shape[0]
@@ -365,7 +390,7 @@ class _LeNetFused(torch.autograd.Function):
         stream = _lib.stream_ptr(dev)
         cw = [t.detach().float().contiguous() for t in (w1, b1, w2, b2, f1w, f1b, f2w, f2b, f3w, f3b)]
         frag = frags.ensure(f1w, f2w, f3w, w1, w2, stream)
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        bf = dict(dtype=torch.float16 if half else torch.bfloat16, device=dev)
         a1 = torch.empty(N, 1176, **bf)
         c1 = torch.empty(N, 1176, dtype=torch.uint8, device=dev)
         c2 = torch.empty(N, 400, dtype=torch.uint8, device=dev)
@@ -388,7 +413,7 @@ class _LeNetFused(torch.autograd.Function):
             claimed = _claim_rows(x, target)  # a deferred loader batch: this launch gathers it
             rows = claimed[0] if claimed is not None else None
             ctx.rows_pend = claimed[1] if claimed is not None else None
-            _lib.check(lib.rk_lenet_train(x.data_ptr(), cw[1].data_ptr(), cw[3].data_ptr(), frag.data_ptr(),
+            _lib.check(_k(lib, "rk_lenet_train", half)(x.data_ptr(), cw[1].data_ptr(), cw[3].data_ptr(), frag.data_ptr(),
                                           cw[5].data_ptr(), cw[7].data_ptr(), cw[9].data_ptr(), a1.data_ptr(),
                                           c1.data_ptr(), c2.data_ptr(), a2T.data_ptr(), h1T.data_ptr(), h2T.data_ptr(),
                                           logits.data_ptr(), dyT.data_ptr(), d2T.data_ptr(), d1T.data_ptr(),
@@ -400,7 +425,7 @@ class _LeNetFused(torch.autograd.Function):
             from rocket_amd.runtime.data import materialize_batch
 
             materialize_batch((x, target) if target is not None else x)  # a deferred loader batch: gather it now
-            _lib.check(lib.rk_lenet_fwd(x.data_ptr(), cw[0].data_ptr(), cw[1].data_ptr(), cw[2].data_ptr(),
+            _lib.check(_k(lib, "rk_lenet_fwd", half)(x.data_ptr(), cw[0].data_ptr(), cw[1].data_ptr(), cw[2].data_ptr(),
                                         cw[3].data_ptr(), frag.data_ptr(), cw[5].data_ptr(), cw[7].data_ptr(),
                                         cw[9].data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(), a2T.data_ptr(),
                                         h1T.data_ptr(), h2T.data_ptr(), logits.data_ptr(), N, stream), "rk_lenet_fwd")
@@ -458,13 +483,13 @@ class _LeNetFused(torch.autograd.Function):
             dy = logits  # unread
         else:
             dy = dlogits.contiguous().float()
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        bf = dict(dtype=a1.dtype, device=dev)
         dyT = torch.empty(10, N, **bf)
         d2T = torch.empty(84, N, **bf)
         d1T = torch.empty(120, N, **bf)
         # conv weight/bias gradients: one slab row per backward block, summed by the wgrad launch
         slab = torch.empty(N // 4, int(lib.rk_lenet_slab_width()), dtype=torch.float32, device=dev)
-        _lib.check(lib.rk_lenet_bwd(x.data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(), w2c.data_ptr(),
+        _lib.check(_k(lib, "rk_lenet_bwd", ctx.frags.half)(x.data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(), w2c.data_ptr(),
                                     frag.data_ptr(), dy.data_ptr(), h1T.data_ptr(), h2T.data_ptr(), dyT.data_ptr(),
                                     d2T.data_ptr(), d1T.data_ptr(), slab.data_ptr(), N, rounds,
                                     ctypes.byref(ce) if ce is not None else None, stream), "rk_lenet_bwd")
@@ -474,6 +499,7 @@ class _LeNetFused(torch.autograd.Function):
     def _wgrad(ctx, lib, N, dev, stream, dyT, d2T, d1T, a2T, h1T, h2T, slab, fin, gscale, keep):
         """The grouped weight-gradient launch (+ loss finalisation, + the armed optimizer's update)."""
         params = ctx.params
+        half = ctx.frags.half
         bufs, direct = _grad_targets(params, dev)
         probs = ((dyT, h2T, bufs[8], bufs[9], 10, 84), (d2T, h1T, bufs[6], bufs[7], 84, 120),
                  (d1T, a2T, bufs[4], bufs[5], 120, 400))
@@ -487,8 +513,8 @@ class _LeNetFused(torch.autograd.Function):
         pend, ctx.rows_pend = getattr(ctx, "rows_pend", None), None
         rows_staged = pend is not None and not pend.advanced
         if rows_staged:  # the step's batch cursor, as one more block of this launch
-            _lib.check(lib.rk_mlp3_set_rows(*pend.advance_args()), "rk_mlp3_set_rows")
-        _lib.check(lib.rk_mlp3_wgrad_loss(3, P(*[q[0].data_ptr() for q in probs]), P(*[q[1].data_ptr() for q in probs]),
+            _lib.check(_k(lib, "rk_mlp3_set_rows", half)(*pend.advance_args()), "rk_mlp3_set_rows")
+        _lib.check(_k(lib, "rk_mlp3_wgrad_loss", half)(3, P(*[q[0].data_ptr() for q in probs]), P(*[q[1].data_ptr() for q in probs]),
                                           P(*[q[2].data_ptr() for q in probs]), P(*[q[3].data_ptr() for q in probs]),
                                           I(*[q[4] for q in probs]), I(*[q[5] for q in probs]), N, slab.data_ptr(),
                                           N // 4, slab.shape[1],
@@ -507,10 +533,14 @@ class _LeNetFused(torch.autograd.Function):
 
 def lenet_forward(x, conv1, conv2, fc1, fc2, fc3, target=None):
     """Fused LeNet logits (N % 8 == 0).  The bf16 fragment table lives on ``conv1``
-    (:class:`LeNetFragments`), kept current by a fused optimizer between steps."""
-    frags = getattr(conv1, "_rocket_fragments", None)
+    (:class:`LeNetFragments`), kept current by a fused optimizer between steps; under fp16
+    autocast the fp16 kernel build runs with its own (per-forward) fp16 table."""
+    half = half_mode(x.device)
+    attr = "_rocket_fragments_h" if half else "_rocket_fragments"
+    frags = getattr(conv1, attr, None)
     if frags is None or frags.frag.device != x.device:
-        frags = conv1._rocket_fragments = LeNetFragments(x.device)
+        frags = LeNetFragments(x.device, half)
+        setattr(conv1, attr, frags)
     return _LeNetFused.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, fc1.weight, fc1.bias,
                              fc2.weight, fc2.bias, fc3.weight, fc3.bias, frags, target)
 

@@ -255,9 +255,12 @@ def _gelu_bwd_bias(dh: torch.Tensor, z: torch.Tensor, bias: torch.Tensor):
     lib = _lib.kernels()
     ws = torch.empty(int(lib.rk_bn_workspace(M, N)), dtype=torch.float32, device=z.device)
     nctr = int(lib.rk_bn_counters(N))
-    _lib.check(lib.rk_gelu_bwd_colsum(dh.data_ptr(), z.data_ptr(), dz.data_ptr(), M, N, target.data_ptr(),
-                                      ws.data_ptr(), _lib.Workspace.get(z.device).counter_array(f"bn{nctr}", nctr),
-                                      _lib.stream_ptr(z.device)), "rk_gelu_bwd_colsum")
+    if dh.dtype != z.dtype:
+        dh = dh.to(z.dtype)
+    _lib.check(lib.rk_gelu_bwd_colsum16(_lib.dtype_code(z), dh.data_ptr(), z.data_ptr(), dz.data_ptr(), M, N,
+                                        target.data_ptr(), ws.data_ptr(),
+                                        _lib.Workspace.get(z.device).counter_array(f"bn{nctr}", nctr),
+                                        _lib.stream_ptr(z.device)), "rk_gelu_bwd_colsum16")
     if direct:
         grad_ready(bias)
         return dz, None
@@ -325,7 +328,9 @@ def _cdtype() -> torch.dtype:
 
 def _native(module: nn.Linear, x: torch.Tensor) -> bool:
     dt = _cdtype()
-    return (x.is_cuda and native_route() and (dt == torch.bfloat16 or (dt == torch.float16 and MODE == "x"))
+    # fp16: the library routes (hipBLASLt fp16 GEMMs beside the fp16 attention / LayerNorm / GELU
+    # kernels) and the xgemm route; the mgemm routes are bf16-only
+    return (x.is_cuda and native_route() and (dt == torch.bfloat16 or (dt == torch.float16 and MODE in ("x", "lib")))
             and module.weight.dtype == torch.float32 and module.weight.is_contiguous()
             and _ok(x, module.out_features, module.in_features))
 

@@ -161,3 +161,101 @@ def test_resnet18_fp16_step_has_no_miopen_kernels():
     assert any("conv_kernel" in n for n in names), names  # the trace saw the native convs
     bad = [n for n in names if any(t in n.lower() for t in ("miopen", "igemm", "naive_conv", "batchnorm"))]
     assert not bad, bad
+
+
+def _h(t):
+    return t.to(H16).float()
+
+
+def _ref_lenet_h(x, net):
+    """fp32 math on fp16-rounded operands, activations rounded to fp16 between layers (the fp16 AMP
+    contract of the fused LeNet's fp16 kernel build)."""
+    h = _h(F.max_pool2d(F.relu(F.conv2d(_h(x), _h(net.conv1.weight), net.conv1.bias, padding=2)), 2))
+    h = F.max_pool2d(F.relu(F.conv2d(h, _h(net.conv2.weight), net.conv2.bias)), 2)
+    a2 = _h(h.flatten(1))
+    h1 = _h(F.relu(F.linear(a2, _h(net.fc1.weight), net.fc1.bias)))
+    h2 = _h(F.relu(F.linear(h1, _h(net.fc2.weight), net.fc2.bias)))
+    return a2, F.linear(h2, _h(net.fc3.weight), net.fc3.bias)
+
+
+@pytest.mark.parametrize("N", [1024, 64])
+def test_lenet_whole_fused_fp16(N):
+    """The fp16 build of the whole-network LeNet kernels (selected by fp16 autocast) vs the fp32
+    reference of the fp16 contract; activations, fragments and d(activations) are fp16."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.lenet import lenet_forward
+
+    torch.manual_seed(2)
+    net = LeNet(fused=False).cuda()
+    ref = LeNet(fused=False).cuda()
+    ref.load_state_dict(net.state_dict())
+    x = torch.rand(N, 1, 28, 28, device="cuda")
+    with torch.autocast("cuda", dtype=H16):
+        y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3)
+    fr = net.conv1._rocket_fragments_h
+    assert fr.frag.dtype == H16 and getattr(net.conv1, "_rocket_fragments", None) is None
+    _, yr = _ref_lenet_h(x, ref)
+    assert y.dtype == torch.float32
+    assert _rel(y, yr) < 2e-3, _rel(y, yr)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    for (name, p), pr in zip(net.named_parameters(), ref.parameters()):
+        assert _rel(p.grad, pr.grad) < 1e-2, (name, _rel(p.grad, pr.grad))
+
+
+def test_lenet_blocks_fp16():
+    """lenet_features + mlp_head under fp16 autocast: fp16 feature map, fp16 MLP kernel build."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.lenet import lenet_features, mlp_head
+
+    torch.manual_seed(1)
+    net = LeNet(fused=False).cuda()
+    ref = LeNet(fused=False).cuda()
+    ref.load_state_dict(net.state_dict())
+    x = torch.rand(256, 1, 28, 28, device="cuda")
+    with torch.autocast("cuda", dtype=H16):
+        a2 = lenet_features(x, net.conv1.weight, net.conv1.bias, net.conv2.weight, net.conv2.bias)
+        y = mlp_head(a2, [net.fc1, net.fc2, net.fc3])
+    assert a2.dtype == H16
+    a2r, yr = _ref_lenet_h(x, ref)
+    assert _rel(a2, a2r) < 2e-3 and _rel(y, yr) < 2e-3, (_rel(a2, a2r), _rel(y, yr))
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    for (name, p), pr in zip(net.named_parameters(), ref.parameters()):
+        assert _rel(p.grad, pr.grad) < 1e-2, (name, _rel(p.grad, pr.grad))
+
+
+def test_lenet_fp16_training_steps_track_fp32():
+    """Engine-free fp16 training loop on the fused LeNet (speculative whole-step path, fused
+    cross-entropy, fp16 fragment table re-prepped each forward after in-place weight updates):
+    the loss trajectory follows the fp32 PyTorch model's."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.lenet import fuse_cross_entropy, lenet_forward
+
+    torch.manual_seed(4)
+    net = LeNet(fused=False).cuda()
+    ref = LeNet(fused=False).cuda()
+    ref.load_state_dict(net.state_dict())
+    o1 = torch.optim.SGD(net.parameters(), lr=0.05)
+    o2 = torch.optim.SGD(ref.parameters(), lr=0.05)
+    x = torch.rand(512, 1, 28, 28, device="cuda")
+    t = torch.randint(0, 10, (512,), device="cuda")
+    l1, l2 = [], []
+    for _ in range(8):
+        with torch.autocast("cuda", dtype=H16):
+            y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3, t)
+        loss, dummy = fuse_cross_entropy(y, t, 1.0)
+        torch.autograd.backward([y], [dummy])
+        o1.step()
+        o1.zero_grad()
+        lr_ = F.cross_entropy(ref.logits(x), t)
+        lr_.backward()
+        o2.step()
+        o2.zero_grad()
+        l1.append(float(loss))
+        l2.append(float(lr_))
+    assert l1[-1] < l1[0]
+    for a, b in zip(l1, l2):
+        assert abs(a - b) < 1e-2 * abs(b), (l1, l2)
