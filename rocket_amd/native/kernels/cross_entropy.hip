@@ -229,7 +229,8 @@ RK_API int rk_ce_fwd(const void* logits, int dtype, const int64_t* target, int N
                      float smoothing, float* partials, unsigned* counter, float* out, int mean, hipStream_t s) {
   if (N <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   return (int)(dtype == BF16 ? launch_fwd<uint16_t>(logits, target, N, C, ignore_index, smoothing, partials, counter, out, mean, s)
-                             : launch_fwd<float>(logits, target, N, C, ignore_index, smoothing, partials, counter, out, mean, s));
+               : dtype == F16 ? launch_fwd<f16_t>(logits, target, N, C, ignore_index, smoothing, partials, counter, out, mean, s)
+                              : launch_fwd<float>(logits, target, N, C, ignore_index, smoothing, partials, counter, out, mean, s));
 }
 
 RK_API int rk_ce_bwd(const void* logits, int dtype, const int64_t* target, void* dlogits, int N, int C,
@@ -237,7 +238,8 @@ RK_API int rk_ce_bwd(const void* logits, int dtype, const int64_t* target, void*
                      hipStream_t s) {
   if (N <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   return (int)(dtype == BF16 ? launch_bwd<uint16_t>(logits, target, dlogits, N, C, ignore_index, smoothing, grad_out, stats, mean, s)
-                             : launch_bwd<float>(logits, target, dlogits, N, C, ignore_index, smoothing, grad_out, stats, mean, s));
+               : dtype == F16 ? launch_bwd<f16_t>(logits, target, dlogits, N, C, ignore_index, smoothing, grad_out, stats, mean, s)
+                              : launch_bwd<float>(logits, target, dlogits, N, C, ignore_index, smoothing, grad_out, stats, mean, s));
 }
 
 RK_API int rk_ce_train(const void* logits, int dtype, const int64_t* target, void* dlogits, int N, int C,
@@ -253,6 +255,8 @@ RK_API int rk_ce_train(const void* logits, int dtype, const int64_t* target, voi
                                                                smoothing, grad_scale, partials, counter, out, mean, la)
   if (dtype == BF16) {
     if (wave) RK_CT(uint16_t, true); else RK_CT(uint16_t, false);
+  } else if (dtype == F16) {
+    if (wave) RK_CT(f16_t, true); else RK_CT(f16_t, false);
   } else {
     if (wave) RK_CT(float, true); else RK_CT(float, false);
   }

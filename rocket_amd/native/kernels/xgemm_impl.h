@@ -133,6 +133,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm_pkernel(MArgs g, int64_
   constexpr int NL = SA::NI + SB::NI;
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
+  const int dbg = g.dbg;  // diagnostics bits, read once (rk_xgemm_set_dbg)
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
   const int total = ntiles * g.splitk;
@@ -190,7 +191,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm_pkernel(MArgs g, int64_
     const int64_t bo = BKM ? ((int64_t)k0 * g.ldb + iss.c0) * 2 : ((int64_t)iss.c0 * g.ldb + k0) * 2;
     const int64_t a_end = AK ? (int64_t)iss.ke * g.lda * 2 : a_bytes;
     const int64_t b_end = BKM ? (int64_t)iss.ke * g.ldb * 2 : b_bytes;
-    if (!(g.dbg & 1)) {
+    if (!(dbg & 1)) {
       sa.issue((const char*)g.a + ao, a_end - ao, buf, wid);
       sb.issue((const char*)g.b + bo, b_end - bo, buf + A_BYTES, wid);
     }
@@ -206,7 +207,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm_pkernel(MArgs g, int64_
   rb.init(wn * TN, lane);
   bf16x8 A0[FM], B0[FN], A1[FM], B1[FN];
   auto read = [&](bf16x8 (&A)[FM], bf16x8 (&B)[FN], int u) {
-    if (g.dbg & 4) return;
+    if (dbg & 4) return;
     const char* As = smem + (u & (NS - 1)) * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -216,7 +217,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm_pkernel(MArgs g, int64_
   };
   XItem cur = place(0);  // compute cursor (the item being consumed)
   auto mma = [&](const bf16x8 (&A)[FM], const bf16x8 (&B)[FN]) {
-    if (g.dbg & 8) return;
+    if (dbg & 8) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -309,7 +310,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm_pkernel(MArgs g, int64_
   };
 
   auto sync = [&]() {
-    if (g.dbg & 2) return;
+    if (dbg & 2) return;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();

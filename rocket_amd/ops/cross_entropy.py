@@ -62,7 +62,7 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int 
         or target.dim() != 1
         or target.dtype.is_floating_point
         or reduction not in ("mean", "sum")
-        or logits.dtype not in (torch.float32, torch.bfloat16)
+        or logits.dtype not in (torch.float32, torch.bfloat16, torch.float16)
     ):
         return F.cross_entropy(logits.float(), target, ignore_index=ignore_index,
                                label_smoothing=label_smoothing, reduction=reduction)
@@ -78,7 +78,7 @@ def ce_train(logits: torch.Tensor, target: torch.Tensor, grad_scale: float, accu
     same launch.  Returns ``(loss[0-d], dlogits)`` or ``None`` when the case is not covered.
     """
     if (logits.device.type != "cuda" or logits.dim() != 2 or target.dim() != 1 or target.dtype.is_floating_point
-            or reduction not in ("mean", "sum") or logits.dtype not in (torch.float32, torch.bfloat16)
+            or reduction not in ("mean", "sum") or logits.dtype not in (torch.float32, torch.bfloat16, torch.float16)
             or logits.shape[0] > 65536):
         return None
     lib = _lib.kernels()

@@ -88,10 +88,10 @@ def test_vit_fp16_step_is_native():
     """A small ViT training step under fp16 autocast on the default (library-GEMM) route: the
     attention, LayerNorm, GELU and GELU-backward/bias-gradient passes are the native fp16 kernels
     (no torch softmax / GELU / fp16 copy kernels in the trace), and the loss is finite."""
-    import torch.nn.functional as F
     from torch.profiler import ProfilerActivity, profile
 
     from rocket_amd.models.vit import VisionTransformer
+    from rocket_amd.ops.cross_entropy import cross_entropy
     from rocket_amd.ops.optim import FusedAdamW
 
     torch.manual_seed(0)
@@ -102,7 +102,7 @@ def test_vit_fp16_step_is_native():
 
     def step():
         with torch.autocast("cuda", dtype=torch.float16):
-            loss = F.cross_entropy(net.logits(x).float(), y)
+            loss = cross_entropy(net.logits(x), y)  # the native loss kernel (as the Loss capsule)
         loss.backward()
         opt.step()
         opt.zero_grad(set_to_none=False)
