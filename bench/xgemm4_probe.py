@@ -55,6 +55,10 @@ def main():
             ms = timeit(fn)
             rec[tag] = {"ms": round(ms, 4), "tflops": round(flop / ms / 1e9, 1)}
         rec["x4_vs_lib"] = round(rec["lib"]["ms"] / rec["x4"]["ms"], 3)
+        for bits in (1, 2, 3):  # diagnostics: no in-loop DMA / no barrier / neither (garbage results)
+            lib.rk_xgemm4_set_dbg(bits)
+            rec[f"x4_dbg{bits}"] = round(flop / timeit(x4) / 1e9, 1)
+        lib.rk_xgemm4_set_dbg(0)
         print(json.dumps(rec), flush=True)
         out.write(json.dumps(rec) + "\n")
 

@@ -42,7 +42,7 @@ struct Map4 {
 };
 __device__ __forceinline__ Map4 shadow_map4(const TensorRec& tr, int64_t i) {
   if (tr.shadow_map <= kDenseShadowF16) return Map4{};
-  const int4* m = (const int4*)((const int2*)tr.shadow_map + i);
+  const int4* m = (const int4*)(shadow_map_ptr(tr.shadow_map) + i);
   return Map4{m[0], m[1]};
 }
 // four consecutive elements (i % 4 == 0, 16-byte aligned parameter rows): dense shadows take one
@@ -63,7 +63,7 @@ __device__ __forceinline__ void shadow_store4(const TensorRec& tr, int64_t i, co
   const float val[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const uint16_t b = f2bf(val[e]);
+    const uint16_t b = shadow_cvt(tr.shadow_map, val[e]);
     if (idx[2 * e] >= 0) buf[idx[2 * e]] = b;
     if (idx[2 * e + 1] >= 0) buf[idx[2 * e + 1]] = b;
   }

@@ -16,6 +16,10 @@ struct TensorRec {  // 8 x int64: a parameter tensor as the update kernels see i
 
 constexpr int64_t kDenseShadow = 1;     // buffer laid out like p, bf16
 constexpr int64_t kDenseShadowF16 = 2;  // buffer laid out like p, fp16 (fp16 autocast compute copies)
+// index-mapped shadows: the map pointer (16-byte aligned) with bit 0 set = the buffer is fp16
+// (e.g. the fused LeNet's fp16 fragment table), clear = bf16
+__device__ __forceinline__ const int2* shadow_map_ptr(int64_t m) { return (const int2*)(m & ~(int64_t)1); }
+__device__ __forceinline__ uint16_t shadow_cvt(int64_t m, float v) { return (m & 1) ? f2h(v) : f2bf(v); }
 
 struct AdamHyper {  // 8 floats per group
   float lr, beta1, beta2, eps, wd, decoupled, maximize, pad;
@@ -27,12 +31,12 @@ __device__ __forceinline__ void shadow_store(const TensorRec& tr, int64_t i, flo
     buf[i] = f2h(v);
     return;
   }
-  const uint16_t b = f2bf(v);
   if (tr.shadow_map == kDenseShadow) {
-    buf[i] = b;
+    buf[i] = f2bf(v);
     return;
   }
-  const int2 m = ((const int2*)tr.shadow_map)[i];
+  const uint16_t b = shadow_cvt(tr.shadow_map, v);
+  const int2 m = shadow_map_ptr(tr.shadow_map)[i];
   if (m.x >= 0) buf[m.x] = b;
   if (m.y >= 0) buf[m.y] = b;
 }
@@ -145,7 +149,7 @@ __device__ __forceinline__ EpiElem epi_fetch(const TensorRec& tr, int64_t i) {
   e.p = ((const float*)tr.p)[i];
   e.m = ((const float*)tr.s0)[i];
   e.v = ((const float*)tr.s1)[i];
-  e.map = tr.shadow_map > kDenseShadowF16 ? ((const int2*)tr.shadow_map)[i] : make_int2(-1, -1);
+  e.map = tr.shadow_map > kDenseShadowF16 ? shadow_map_ptr(tr.shadow_map)[i] : make_int2(-1, -1);
   return e;
 }
 __device__ __forceinline__ void epi_apply(const TensorRec& tr, const AdamStep& k, int64_t i, EpiElem e, float g,
@@ -160,7 +164,7 @@ __device__ __forceinline__ void epi_apply(const TensorRec& tr, const AdamStep& k
   } else if (tr.shadow_map == kDenseShadowF16) {
     ((uint16_t*)tr.shadow_buf)[i] = f2h(e.p);
   } else if (tr.shadow_map) {
-    const uint16_t b = f2bf(e.p);
+    const uint16_t b = shadow_cvt(tr.shadow_map, e.p);
     if (e.map.x >= 0) ((uint16_t*)tr.shadow_buf)[e.map.x] = b;
     if (e.map.y >= 0) ((uint16_t*)tr.shadow_buf)[e.map.y] = b;
   }

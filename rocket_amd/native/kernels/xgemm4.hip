@@ -57,7 +57,7 @@ __device__ __forceinline__ void x4_dma(const char* base, int64_t bytes, int64_t 
 __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                           const uint16_t* __restrict__ B, int64_t ldb, void* C,
                                                           int64_t ldc, int c_dt, const float* __restrict__ bias,
-                                                          int M, int N, int K) {
+                                                          int M, int N, int K, int dbg) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * X4_STAGE];
   const int tiles_n = (N + X4_BN - 1) / X4_BN;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -159,9 +159,9 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
     if (t + 1 < T) __builtin_amdgcn_s_waitcnt(kWaitAll0);
     else __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(dbg & 2)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < T) dma(t + 2);  // into tile t's stage
+    if (t + 2 < T && !(dbg & 1)) dma(t + 2);  // into tile t's stage
     // sub 1: MFMAs on half 1, reads of half 0 of tile t+1
     __builtin_amdgcn_s_setprio(1);
     mma(A1, B1, t + 1 < T, A0, B0, addr(arow, t + 1, 0), addr(brow, t + 1, 0));
@@ -196,6 +196,11 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
 
 // C[M][N] = A[M][K] B[N][K]^T (+ bias[N]); bf16 operands (rows 16-byte aligned), K % 64 == 0,
 // N % 4 == 0; C f32 / bf16 / fp16 (c_dt).
+int g_x4_dbg = 0;
+RK_API int rk_xgemm4_set_dbg(int bits) {  // diagnostics: bit 0 no in-loop DMA, bit 1 no barrier
+  g_x4_dbg = bits;
+  return 0;
+}
 RK_API int rk_xgemm4(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int c_dt,
                      const float* bias, int M, int N, int K, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
@@ -204,6 +209,7 @@ RK_API int rk_xgemm4(const void* a, int64_t lda, const void* b, int64_t ldb, voi
   // per-lane + per-instruction DMA offsets stay below 2^31 (256 rows of the operand)
   if ((int64_t)256 * lda * 2 >= (1ll << 31) || (int64_t)256 * ldb * 2 >= (1ll << 31)) return (int)hipErrorInvalidValue;
   const int tiles = ((M + X4_BM - 1) / X4_BM) * ((N + X4_BN - 1) / X4_BN);
-  xgemm4_kernel<<<tiles, X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc, c_dt, bias, M, N, K);
+  xgemm4_kernel<<<tiles, X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc, c_dt, bias, M, N, K,
+                                        g_x4_dbg);
   return (int)hipGetLastError();
 }

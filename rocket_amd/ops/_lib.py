@@ -43,6 +43,7 @@ KERNEL_SIGS = {
     "rk_xgemm": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p, c_int, c_int64, c_void_p, c_void_p,
                          c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "rk_xgemm_set_dbg": (c_int, [c_int]),
+    "rk_xgemm4_set_dbg": (c_int, [c_int]),
     "rk_xgemm4": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_int, c_int, c_int,
                           c_void_p]),
     "rk_slab_acc": (c_int, [c_void_p, c_int, c_int, c_int64, c_void_p, c_int, c_void_p]),

@@ -226,7 +226,8 @@ def _frag_index_maps():
 
 
 class LeNetFragments:
-    """Persistent bf16 MFMA fragment table of a fused LeNet (one per model).
+    """Persistent 16-bit MFMA fragment table of a fused LeNet (one per model and precision: bf16,
+    or fp16 under fp16 autocast).
 
     The table is rebuilt by the ``lenet_prep`` launch only when needed.  It is registered as the
     bf16 shadow of the five weight tensors (``_rocket_bf16_shadow``), so a fused optimizer
@@ -259,20 +260,23 @@ class LeNetFragments:
     def ensure(self, fc1w, fc2w, fc3w, conv1w, conv2w, stream) -> torch.Tensor:
         params = (fc1w, fc2w, fc3w, conv1w, conv2w)
         versions = tuple(p._version for p in params)
-        # the fp16 table is no optimizer shadow (fused optimizers maintain bf16 shadows only):
-        # it is rebuilt by every forward (one 282-block launch inside the step's graph)
-        live = (not self.half and self.params is not None and all(a is b for a, b in zip(params, self.params))
-                and versions == self.versions and all(getattr(p, "_rocket_shadow_live", False) for p in params))
+        # live: the table is the registered shadow of all five weights (a table of the other
+        # precision may have registered itself since) and a fused optimizer keeps it current
+        live = (self.params is not None and all(a is b for a, b in zip(params, self.params))
+                and versions == self.versions
+                and all(getattr(p, "_rocket_shadow_live", False)
+                        and getattr(p, "_rocket_bf16_shadow", (None, None))[1] is self.frag for p in params))
         if not live:
             cw = [p.detach().float().contiguous() for p in params]
             _lib.check(_k(_lib.kernels(), "rk_lenet_prep", self.half)(cw[0].data_ptr(), cw[1].data_ptr(), cw[2].data_ptr(),
                                                     cw[3].data_ptr(), cw[4].data_ptr(), self.frag.data_ptr(), stream),
                        "rk_lenet_prep")
-            if not self.half and (self.params is None or not all(a is b for a, b in zip(params, self.params))):
-                for p, m in zip(params, self.maps):
-                    if p.dtype == torch.float32 and p.is_contiguous():
-                        p._rocket_bf16_shadow = (m, self.frag)
-                self.params = params
+            for p, m in zip(params, self.maps):
+                if p.dtype == torch.float32 and p.is_contiguous() and \
+                        getattr(p, "_rocket_bf16_shadow", (None, None))[1] is not self.frag:
+                    p._rocket_bf16_shadow = (m, self.frag)  # the fp16 table: an fp16 mapped shadow
+                    p._rocket_shadow_live = False  # until a fused optimizer prepares with it
+            self.params = params
             self.versions = versions
         return self.frag
 

@@ -158,9 +158,11 @@ class _FusedBase(torch.optim.Optimizer):
             if buf.shape != p.shape or buf.stride() != p.stride() or buf.device != p.device:
                 raise RuntimeError("dense fp16 shadow: buffer must have the parameter's shape, layout and device")
             return (2, buf.data_ptr())
-        if buf.dtype != torch.bfloat16 or buf.device != p.device:
-            raise RuntimeError("bf16 shadow: expected a bf16 buffer on the parameter's device")
+        if buf.dtype not in (torch.bfloat16, torch.float16) or buf.device != p.device:
+            raise RuntimeError("shadow: expected a bf16 / fp16 buffer on the parameter's device")
         if idx is None:
+            if buf.dtype != torch.bfloat16:
+                raise RuntimeError("dense shadow: unexpected dtype")
             if buf.shape != p.shape or buf.stride() != p.stride():
                 raise RuntimeError("dense bf16 shadow: buffer must have the parameter's shape and layout")
             return (1, buf.data_ptr())
@@ -170,7 +172,8 @@ class _FusedBase(torch.optim.Optimizer):
             # the kernel fetches 4 elements' entries as two 16-byte loads: keep an aligned copy
             idx = idx.contiguous().clone()
             p._rocket_bf16_shadow = (idx, buf)
-        return (idx.data_ptr(), buf.data_ptr())
+        # bit 0 of the (16-byte aligned) map pointer: fp16 buffer (optim_common.h shadow_cvt)
+        return (idx.data_ptr() | int(buf.dtype == torch.float16), buf.data_ptr())
 
     # --------------------------------------------------------- device side
     def amp_check(self, amp: torch.Tensor) -> None:

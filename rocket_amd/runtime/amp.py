@@ -42,7 +42,12 @@ class FusedGradScaler:
         self._growth_interval = int(growth_interval)
         self.state = torch.tensor([init_scale, 1.0 / init_scale, 0.0, 0.0, growth_factor, backoff_factor,
                                    float(growth_interval), 0.0], dtype=torch.float32, device=self.device)
-        self._last_host = torch.zeros(1, dtype=torch.float32, pin_memory=self.device.type == "cuda")
+        # the skip flag of recent steps: a small ring of pinned copies + their events, so a caller can
+        # hold the handle of step k while step k+1 records its own (EngineScheduler speculation)
+        pin = self.device.type == "cuda"
+        self._ring = [torch.zeros(1, dtype=torch.float32, pin_memory=pin) for _ in range(4)]
+        self._ring_i = 0
+        self._last_host = self._ring[0]
         self._last_event = None
         self._unscaled = set()  # id(optimizer) unscaled this step (clip_grad_norm_ path)
 
@@ -139,10 +144,27 @@ class FusedGradScaler:
 
     def _record_last(self) -> None:
         self._unscaled.clear()
+        self._ring_i = (self._ring_i + 1) % len(self._ring)
+        self._last_host = self._ring[self._ring_i]
         self._last_host.copy_(self.state[LAST : LAST + 1], non_blocking=True)
+        self._last_event = None
         if self.device.type == "cuda":
             self._last_event = torch.cuda.Event()
             self._last_event.record()
+
+    def last_handle(self):
+        """(pinned flag copy, event) of the last recorded step: resolve with :func:`handle_skipped`."""
+        return (self._last_host, self._last_event)
+
+    @staticmethod
+    def handle_ready(h) -> bool:
+        return h[1] is None or h[1].query()
+
+    @staticmethod
+    def handle_skipped(h) -> bool:
+        if h[1] is not None:
+            h[1].synchronize()
+        return bool(h[0][0] != 0)
 
     def update(self, new_scale=None) -> None:
         """The scale update already ran on the device; ``new_scale`` overrides it."""

@@ -75,19 +75,24 @@ class EngineOptimizer:
         self.engine = engine
         self._skipped = False
         self._skip_lazy = False  # fp16 fused scaler: the flag lives on the device until asked for
+        self._lazy_handle = None  # (pinned copy, event) of that flag (FusedGradScaler.last_handle)
 
     @property
     def step_was_skipped(self) -> bool:
         """accelerate's ``step_was_skipped``.  With the device-resident scaler it is read back only
         here (waiting for that step's update), not on every step."""
         if self._skip_lazy:
-            self._skipped = self.engine.scaler.last_step_skipped()
+            h = self._lazy_handle
+            self._skipped = (FusedGradScaler.handle_skipped(h) if h is not None
+                             else self.engine.scaler.last_step_skipped())
             self._skip_lazy = False
         return self._skipped
 
     def step_was_skipped_lazy(self) -> None:
         """A scaled update ran on the device (e.g. in a replayed graph): resolve the flag on demand."""
         self._skip_lazy = True
+        scaler = self.engine.scaler
+        self._lazy_handle = scaler.last_handle() if isinstance(scaler, FusedGradScaler) else None
 
     @step_was_skipped.setter
     def step_was_skipped(self, v: bool) -> None:
@@ -125,7 +130,7 @@ class EngineOptimizer:
         scaler = self.engine.scaler
         if isinstance(scaler, FusedGradScaler):
             out = scaler.step(self.optimizer, closure) if closure else scaler.step(self.optimizer)
-            self._skip_lazy = True
+            self.step_was_skipped_lazy()
             return out
         if scaler is not None:
             scale_before = scaler.get_scale()
@@ -152,7 +157,7 @@ class EngineOptimizer:
         if self.fused_zero_ok():
             if isinstance(self.engine.scaler, FusedGradScaler):
                 self.engine.scaler.step(self.optimizer, zero_grads=True)
-                self._skip_lazy = True
+                self.step_was_skipped_lazy()
                 return
             self.step_was_skipped = False
             if self.optimizer.prepare():
@@ -172,30 +177,73 @@ class EngineScheduler:
     accumulation micro-steps it only advances ``_step_count``.
     """
 
+    #: fp16 device-resident scaler: instead of waiting for the step's skip flag (a host sync per
+    #: step, which serialises host issue and device work), step the scheduler assuming "not
+    #: skipped" and verify at the next scheduler step (that flag has landed by then); a wrong guess
+    #: (an inf/NaN step) restores the scheduler and the param-group hyperparameters.  The one update
+    #: already issued in between used the speculated hyperparameters; set ROCKET_SCHED_SPECULATE=0
+    #: for the exact (synchronising) form.
+    SPECULATE = os.environ.get("ROCKET_SCHED_SPECULATE", "1") != "0"
+
     def __init__(self, scheduler, optimizers: List[EngineOptimizer], engine: "Engine"):
         self.scheduler = scheduler
         self.optimizers = optimizers
         self.engine = engine
+        self._pending = None  # (flag handles, snapshot) of a speculated step
+        self.mispredicted = 0
 
-    def step(self, *args, **kwargs):
-        if not self.engine.sync_gradients:
-            self.scheduler._step_count += 1
+    def _groups(self):
+        return [g for o in self.optimizers for g in o.optimizer.param_groups]
+
+    def _snapshot(self):
+        sd = {k: (list(v) if isinstance(v, list) else v) for k, v in self.scheduler.state_dict().items()}
+        return sd, [{k: v for k, v in g.items() if k != "params"} for g in self._groups()]
+
+    def _resolve(self) -> None:
+        p, self._pending = self._pending, None
+        if p is None:
             return
-        if any(o.step_was_skipped for o in self.optimizers):
-            return
+        handles, (sd, groups) = p
+        if any(FusedGradScaler.handle_skipped(h) for h in handles):
+            self.mispredicted += 1
+            self.scheduler.load_state_dict(sd)
+            for g, saved in zip(self._groups(), groups):
+                g.update(saved)
+
+    def _do_step(self, *args, **kwargs) -> None:
         for _ in range(self.engine.num_processes):
             total = getattr(self.scheduler, "total_steps", None)
             if total is not None and self.scheduler._step_count > total:
                 continue
             self.scheduler.step(*args, **kwargs)
 
+    def step(self, *args, **kwargs):
+        if not self.engine.sync_gradients:
+            self.scheduler._step_count += 1
+            return
+        self._resolve()
+        if self.SPECULATE:
+            lazy = [o for o in self.optimizers if o._skip_lazy and o._lazy_handle is not None]
+            handles = [o._lazy_handle for o in lazy]
+            if lazy and len(lazy) == len(self.optimizers) and not all(FusedGradScaler.handle_ready(h) for h in handles):
+                snap = self._snapshot()
+                self._do_step(*args, **kwargs)
+                self._pending = (handles, snap)
+                return
+        if any(o.step_was_skipped for o in self.optimizers):
+            return
+        self._do_step(*args, **kwargs)
+
     def get_last_lr(self):
+        self._resolve()
         return self.scheduler.get_last_lr()
 
     def state_dict(self):
+        self._resolve()
         return self.scheduler.state_dict()
 
     def load_state_dict(self, sd):
+        self._pending = None
         self.scheduler.load_state_dict(sd)
 
     def __getattr__(self, name):
