@@ -55,7 +55,12 @@ def main():
             ms = timeit(fn)
             rec[tag] = {"ms": round(ms, 4), "tflops": round(flop / ms / 1e9, 1)}
         rec["x4_vs_lib"] = round(rec["lib"]["ms"] / rec["x4"]["ms"], 3)
-        for bits in (1, 2, 3):  # diagnostics: no in-loop DMA / no barrier / neither (garbage results)
+        for bits in (8, 4, 12, 16, 17, 1):  # variant R (4) / no in-loop DMA (1) / + no barrier (2): garbage results
+            if bits in (4, 16):
+                lib.rk_xgemm4_set_dbg(bits)
+                x4()
+                torch.cuda.synchronize()
+                rec[f"x4_{bits}_rel_err"] = round(((y.float() - ref).abs().max() / ref.abs().max()).item(), 5)
             lib.rk_xgemm4_set_dbg(bits)
             rec[f"x4_dbg{bits}"] = round(flop / timeit(x4) / 1e9, 1)
         lib.rk_xgemm4_set_dbg(0)

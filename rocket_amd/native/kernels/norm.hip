@@ -794,20 +794,19 @@ template <> struct Raw4<float> {
 // gradient (dres) — the bias gradient of the linear layer that produced the branch (ViT proj /
 // fc2), so that layer's backward needs no column-sum pass over its output gradient.
 // Streaming design: the row reductions run on the DPP network (no LDS instructions), gamma is held
-// in registers, loads stay packed until used, and the block's column partials meet in ONE [NP][C]
-// LDS image through LDS float atomics (9 KB at C = 768 instead of 36: ~7 blocks per CU resident
-// instead of 4, so ~1.75x the rows in flight).
+// in registers, loads stay packed until used and the next row's loads are in flight while a row is
+// reduced and stored.
 template <typename T, typename TO, int NV, int NP>
 __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
                                                       const float* __restrict__ g, const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                       const T* __restrict__ dsum, TO* __restrict__ dres,
-                                                      float* part, int64_t rows, int C, int rows_per_block) {
-  extern __shared__ float sm[];  // [NP][C]
+                                                      float* part, int64_t rows, int C, int rows_per_block,
+                                                      int use_pf) {
+  extern __shared__ float sm[];  // [LN_W][NP][C]
   // w (so each row index and row pointer) is wave-uniform: the row bases live in SGPRs and every
   // lane addresses all five tensors with the same small column offset
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int i = threadIdx.x; i < NP * C; i += LN_T) sm[i] = 0.f;
   float ag[NV][4], ab[NV][4], ar[NV][4], gm[NV][4];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
@@ -835,7 +834,8 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
       if (dsum) sa[j].load(dsrow + cc);
     }
   };
-  constexpr bool PF = NV <= 4;  // wide rows (C > 1024): no room for a second row's registers
+  // wide rows (C > 1024): no room for a second row's registers
+  const bool PF = NV <= 4 && use_pf;
   if (PF && rb + w < re) fetch(rb + w, xr, dr, sr);
   for (int64_t row = rb + w; row < re; row += LN_W) {
     const float mean = mean_in[row], rstd = rstd_in[row];
@@ -896,24 +896,26 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
       }
     }
   }
-  // the image is k-major per partial (column 4q + k at k * C/4 + q): consecutive lanes add to
-  // consecutive words (conflict-free); colsum_kernel undoes the permutation (perm_q = C/4)
-  __syncthreads();  // the zeroed image
-  const int Q = C / 4;
+  // block partial: every wave parks its column partials in its own LDS image (16-byte stores,
+  // consecutive lanes: whole bank rows), then each thread sums the 4 waves' values of its columns
+  // (per-wave images instead of LDS atomics into one: the atomics' per-block cost measured higher
+  // than the 4x LDS footprint, bench/ln_probe.py)
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const int q = j * 64 + lane;
-    if (q < Q) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        atomicAdd(&sm[k * Q + q], ag[j][k]);
-        atomicAdd(&sm[C + k * Q + q], ab[j][k]);
-        if (NP == 3) atomicAdd(&sm[2 * C + k * Q + q], ar[j][k]);
-      }
+    const int c = (j * 64 + lane) * 4;
+    if (c < C) {
+      *(float4*)&sm[(w * NP) * C + c] = make_float4(ag[j][0], ag[j][1], ag[j][2], ag[j][3]);
+      *(float4*)&sm[(w * NP + 1) * C + c] = make_float4(ab[j][0], ab[j][1], ab[j][2], ab[j][3]);
+      if (NP == 3) *(float4*)&sm[(w * NP + 2) * C + c] = make_float4(ar[j][0], ar[j][1], ar[j][2], ar[j][3]);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < NP * C; i += LN_T) part[(int64_t)blockIdx.x * NP * C + i] = sm[i];
+  for (int i = threadIdx.x; i < NP * C; i += LN_T) {
+    float t = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < LN_W; ++ww) t += sm[ww * NP * C + i];
+    part[(int64_t)blockIdx.x * NP * C + i] = t;
+  }
 }
 
 // column sums of the [nrows][2C] block partials -> dgamma (first C) / dbeta (last C), accumulated.
@@ -1341,7 +1343,17 @@ int ln_num_cus() {
   }
   return cus[dev];
 }
+int g_ln_rpb = 64;  // rk_ln_set_bwd_cfg: rows per block (0 = one round of blocks over the chip);
+                    // 64: 5.1 TB/s on ViT's 25216 x 768 (bench/ln_probe.py; 16: 4.3, one round: 4.7)
+int g_ln_pf = 1;    // next-row prefetch in ln_bwd_kernel
+RK_API int rk_ln_set_bwd_cfg(int rpb, int pf) {
+  if (rpb < 0 || (rpb > 0 && rpb % LN_W)) return (int)hipErrorInvalidValue;
+  g_ln_rpb = rpb;
+  g_ln_pf = pf != 0;
+  return 0;
+}
 int ln_bwd_rpb(int64_t rows) {
+  if (g_ln_rpb > 0) return g_ln_rpb;
   const int64_t slots = (int64_t)ln_num_cus() * 3;
   int64_t rpb = (rows + slots - 1) / slots;
   rpb = (rpb + LN_W - 1) / LN_W * LN_W;
@@ -1366,14 +1378,14 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
   const int grid = (int)((rows + rpb - 1) / rpb);
   const int nv = (C + 255) / 256;
   const int np = dres_sum ? 3 : 2;
-  const size_t smem = (size_t)np * C * sizeof(float);
+  const size_t smem = (size_t)LN_W * np * C * sizeof(float);
 #define RK_LB(T, TO, NV)                                                                                               \
   if (np == 3)                                                                                                         \
     ln_bwd_kernel<T, TO, NV, 3><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx,             \
-                                                         (const T*)dsum, (TO*)dres, ws, rows, C, rpb);                 \
+                                                         (const T*)dsum, (TO*)dres, ws, rows, C, rpb, g_ln_pf);      \
   else                                                                                                                 \
     ln_bwd_kernel<T, TO, NV, 2><<<grid, LN_T, smem, s>>>((const TO*)dy, (const T*)x, g, mean, rstd, (T*)dx,             \
-                                                         (const T*)dsum, (TO*)dres, ws, rows, C, rpb)
+                                                         (const T*)dsum, (TO*)dres, ws, rows, C, rpb, g_ln_pf)
 #define RK_LBN(T, TO)                 \
   if (nv <= 1) RK_LB(T, TO, 1);       \
   else if (nv <= 2) RK_LB(T, TO, 2);  \
@@ -1391,7 +1403,7 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
 #undef RK_LBN
 #undef RK_LB
   if (dgamma || dbeta || dres_sum)
-    colsum_kernel<<<(np * C + 63) / 64, CS_T, 0, s>>>(ws, grid, np * C, dgamma, dbeta, C, dres_sum, C / 4);
+    colsum_kernel<<<(np * C + 63) / 64, CS_T, 0, s>>>(ws, grid, np * C, dgamma, dbeta, C, dres_sum);
   (void)counter;
   return (int)hipGetLastError();
 }

@@ -27,6 +27,19 @@ using namespace rk;
 
 namespace {
 
+// Tile order: the linear id (after the XCD remap: the ids of one XCD are consecutive) walks the
+// tile grid in groups of GH tile-rows, column by column inside a group, so the 32 tiles an XCD
+// runs at once form a GH x (32/GH) block: GH A-panels and 32/GH B-panels per k-step through that
+// XCD's L2 instead of 1-2 A-panels and 16-32 B-panels (a row-major walk over a wide grid).
+__device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, int gh, int& tm, int& tn) {
+  const int per = gh * tiles_n;
+  const int g = t / per, first = g * gh;
+  const int h = min(tiles_m - first, gh);
+  const int r = t - g * per;
+  tm = first + r % h;
+  tn = r / h;
+}
+
 constexpr int X4_BM = 256, X4_BN = 256, X4_BK = 64, X4_NT = 256;
 constexpr int X4_ROWB = X4_BK * 2;                 // 128-byte image rows
 constexpr int X4_OPB = X4_BM * X4_ROWB;            // 32 KiB per operand per stage
@@ -35,6 +48,10 @@ constexpr int X4_NI = X4_OPB / (1024 * 4);         // 8 DMA instructions per ope
 
 __device__ __forceinline__ void mfma_a(f32x4& c, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+// the same with C = 0: starts an accumulation (no zeroing of the accumulator registers needed)
+__device__ __forceinline__ void mfma_a0(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -61,7 +78,10 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
   __shared__ __attribute__((aligned(1024))) char smem[2 * X4_STAGE];
   const int tiles_n = (N + X4_BN - 1) / X4_BN;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int r0 = (tile / tiles_n) * X4_BM, c0 = (tile % tiles_n) * X4_BN;
+  int tm, tn;
+  if (dbg & 8) { tm = tile / tiles_n; tn = tile % tiles_n; }  // row-major walk (diagnostics)
+  else grouped_tile(tile, (M + X4_BM - 1) / X4_BM, tiles_n, 4, tm, tn);
+  const int r0 = tm * X4_BM, c0 = tn * X4_BN;
   const int lane = threadIdx.x & 63, lo = lane & 15, hi = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -192,6 +212,323 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
   }
 }
 
+// Variant R: the same 4-wave 256x256 tile on 32-deep k-units in a 4-slot LDS ring (4 x 32 KiB):
+// per unit u (64 MFMAs per wave): wait for unit u+1 (units u+2, u+3 stay in flight: vmcnt(16)),
+// ONE barrier, DMA of unit u+4 into unit u's slot, then the MFMAs on u's registers interleaved
+// with the fragment reads of u+1.  Three units (~3k MFMA cycles, 96 KiB in flight) hide each DMA
+// instead of one 64-deep tile (~2k, 64 KiB), at one barrier per 64 MFMAs.  Image rows are 64 B, chunk c of row r at
+// c ^ rswz<32>(r) (mgemm_core.h; conflict-free ds_read_b128).
+constexpr int XR_BK = 32, XR_ROWB = 64, XR_OPB = 256 * XR_ROWB, XR_SLOT = 2 * XR_OPB, XR_NS = 4;
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// 16 rows x 64 B per 1-KiB instruction; wave w stages rows 64w .. 64w+63 (4 instructions)
+__device__ __forceinline__ void xr_dma(const char* base, int64_t bytes, int64_t ld2, char* lds, int w, uint32_t voff) {
+  const int n = (int)(bytes < 0 ? 0 : (bytes > 0x7fffffff ? 0x7fffffff : bytes));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, n, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row0 = 64 * w + 16 * i;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + row0 * XR_ROWB), 16, voff + (uint32_t)(row0 * ld2),
+                                             0, 0, 0);
+  }
+}
+#endif
+
+__global__ void __launch_bounds__(X4_NT, 1) xgemm4r_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                           const uint16_t* __restrict__ B, int64_t ldb, void* C,
+                                                           int64_t ldc, int c_dt, const float* __restrict__ bias,
+                                                           int M, int N, int K, int dbg) {
+  __shared__ __attribute__((aligned(1024))) char smem[XR_NS * XR_SLOT];
+  const int tiles_n = (N + X4_BN - 1) / X4_BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  if (dbg & 8) { tm = tile / tiles_n; tn = tile % tiles_n; }  // row-major walk (diagnostics)
+  else grouped_tile(tile, (M + X4_BM - 1) / X4_BM, tiles_n, 4, tm, tn);
+  const int r0 = tm * X4_BM, c0 = tn * X4_BN;
+  const int lane = threadIdx.x & 63, lo = lane & 15, hi = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int U = K / XR_BK;
+
+  // DMA lane pattern: image row (lane >> 2) of the 16-row piece, chunk (lane & 3) holds source
+  // chunk (lane & 3) ^ rswz<32>(row); rswz reads row bits 2..3 = lane bits 4..5: one pattern
+  const int prow = lane >> 2;
+  const uint32_t va = (uint32_t)(prow * lda * 2 + (((lane & 3) ^ rswz<32>(prow)) * 16));
+  const uint32_t vb = (uint32_t)(prow * ldb * 2 + (((lane & 3) ^ rswz<32>(prow)) * 16));
+  const char* abase = (const char*)A + (int64_t)r0 * lda * 2;
+  const char* bbase = (const char*)B + (int64_t)c0 * ldb * 2;
+  const int64_t abytes = ((int64_t)M - r0) * lda * 2, bbytes = ((int64_t)N - c0) * ldb * 2;
+  auto dma = [&](int u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    char* st = smem + (u & (XR_NS - 1)) * XR_SLOT;
+    xr_dma(abase + u * XR_ROWB, abytes - u * XR_ROWB, lda * 2, st, w, va);
+    xr_dma(bbase + u * XR_ROWB, bbytes - u * XR_ROWB, ldb * 2, st + XR_OPB, w, vb);
+#endif
+  };
+  // fragment i: image row 128 wm + 16 i + lo (rows 16 apart: immediate offsets of i * 1024)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const lds_void*)smem;
+  const uint32_t ch = (uint32_t)((hi ^ rswz<32>(lo)) * 16);
+  const uint32_t arow = lds0 + (uint32_t)((128 * wm + lo) * XR_ROWB) + ch;
+  const uint32_t brow = lds0 + (uint32_t)(XR_OPB + (128 * wn + lo) * XR_ROWB) + ch;
+#define XR_RD(dst, a, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(a), "i"(off))
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto rd_pair = [&](bf16x8 (&Na)[8], bf16x8 (&Nb)[8], uint32_t aa, uint32_t ab, int i) {
+    switch (i) {
+      case 0: XR_RD(Na[0], aa, 0); XR_RD(Nb[0], ab, 0); break;
+      case 1: XR_RD(Na[1], aa, 1024); XR_RD(Nb[1], ab, 1024); break;
+      case 2: XR_RD(Na[2], aa, 2048); XR_RD(Nb[2], ab, 2048); break;
+      case 3: XR_RD(Na[3], aa, 3072); XR_RD(Nb[3], ab, 3072); break;
+      case 4: XR_RD(Na[4], aa, 4096); XR_RD(Nb[4], ab, 4096); break;
+      case 5: XR_RD(Na[5], aa, 5120); XR_RD(Nb[5], ab, 5120); break;
+      case 6: XR_RD(Na[6], aa, 6144); XR_RD(Nb[6], ab, 6144); break;
+      default: XR_RD(Na[7], aa, 7168); XR_RD(Nb[7], ab, 7168); break;
+    }
+  };
+  auto mma = [&](const bf16x8 (&Ra)[8], const bf16x8 (&Rb)[8], bool rd, bf16x8 (&Na)[8], bf16x8 (&Nb)[8],
+                 uint32_t aa, uint32_t ab) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (rd) rd_pair(Na, Nb, aa, ab, i);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mfma_a(acc[i][j], Rb[j], Ra[i]);
+    }
+  };
+  auto slot = [&](int u) { return (uint32_t)((u & (XR_NS - 1)) * XR_SLOT); };
+  constexpr int kWaitLgkm0 = 0xC07F;
+  bf16x8 A0[8], B0[8], A1[8], B1[8];
+  if (U > 0) {
+#pragma unroll
+    for (int u = 0; u < XR_NS; ++u)
+      if (u < U) dma(u);
+    // unit 0 landed (units 1..3 may be in flight: 8 instructions each)
+    if (U >= 4) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (U == 3) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (U == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rd_pair(A0, B0, arow + slot(0), brow + slot(0), i);
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+  }
+  // one unit: [wait unit u+1 (u+2, u+3 in flight) + barrier] -> DMA u+4 into u's slot (u's
+  // fragments are already in registers: every wave finished reading the slot before this
+  // barrier) -> MFMAs(u) || reads(u+1).  DMA(u+4) is waited for at the top of unit u+3.
+#define XR_UNIT(u, CA, CB, NA, NB)                                                          \
+  do {                                                                                      \
+    const int u_ = (u);                                                                     \
+    if (u_ + 3 < U) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");                       \
+    else if (u_ + 2 < U) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                  \
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                   \
+    if (!(dbg & 2)) __builtin_amdgcn_s_barrier();                                           \
+    asm volatile("" ::: "memory");                                                          \
+    if (u_ + 4 < U && !(dbg & 1)) dma(u_ + 4);                                              \
+    __builtin_amdgcn_s_setprio(1);                                                          \
+    mma(CA, CB, u_ + 1 < U, NA, NB, arow + slot(u_ + 1), brow + slot(u_ + 1));              \
+    __builtin_amdgcn_s_setprio(0);                                                          \
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);                                                 \
+  } while (0)
+  int u = 0;
+  for (; u + 1 < U; u += 2) {
+    XR_UNIT(u, A0, B0, A1, B1);
+    XR_UNIT(u + 1, A1, B1, A0, B0);
+  }
+  if (u < U) XR_UNIT(u, A0, B0, A1, B1);
+#undef XR_UNIT
+#undef XR_RD
+
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 7" ::: "memory");
+  const int mb = r0 + 128 * wm, nb = c0 + 128 * wn;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = nb + 16 * j + 4 * hi;
+    const bool nok = n < N;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (bias && nok) bv = *(const float4*)(bias + n);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mb + 16 * i + lo;
+      if (!nok || m >= M) continue;
+      const float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
+                  v3 = acc[i][j][3] + bv.w;
+      if (c_dt == F32) *(float4*)((float*)C + (int64_t)m * ldc + n) = make_float4(v0, v1, v2, v3);
+      else *(uint2*)((uint16_t*)C + (int64_t)m * ldc + n) = make_uint2(pack16(v0, v1, c_dt), pack16(v2, v3, c_dt));
+    }
+  }
+}
+
+// Variant P: variant R made persistent (grid = one block per CU; block b walks tiles pos, pos + G,
+// ... in the grouped order) with ONE unit stream across its tiles: the DMAs of the next tile's
+// first units are in flight while the current tile's last units and its epilogue run, so there is
+// no pipeline fill or drain per tile (ViT's K = 768 products are only 24 units deep).  The
+// epilogue's stores join the vmcnt queue; the first wait after it allows for them.
+__global__ void __launch_bounds__(X4_NT, 1) xgemm4p_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                           const uint16_t* __restrict__ B, int64_t ldb, void* C,
+                                                           int64_t ldc, int c_dt, const float* __restrict__ bias,
+                                                           int M, int N, int K, int dbg) {
+  __shared__ __attribute__((aligned(1024))) char smem[XR_NS * XR_SLOT];
+  const int tiles_m = (M + X4_BM - 1) / X4_BM, tiles_n = (N + X4_BN - 1) / X4_BN;
+  const int total = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int pos = xcd_remap(blockIdx.x, G);
+  const int my = pos < total ? (total - pos + G - 1) / G : 0;
+  const int U = K / XR_BK;
+  const int S = my * U;  // units in this block's stream
+  const int lane = threadIdx.x & 63, lo = lane & 15, hi = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+
+  const int prow = lane >> 2;
+  const uint32_t va = (uint32_t)(prow * lda * 2 + (((lane & 3) ^ rswz<32>(prow)) * 16));
+  const uint32_t vb = (uint32_t)(prow * ldb * 2 + (((lane & 3) ^ rswz<32>(prow)) * 16));
+  // issue cursor (tile of the next DMA, its unit) and compute cursor (tile being multiplied)
+  int iss_i = 0, iss_u = 0;
+  const char *ia = nullptr, *ib = nullptr;
+  int64_t ia_n = 0, ib_n = 0;
+  auto iss_tile = [&](int i) {
+    int tm, tn;
+    grouped_tile(pos + i * G, tiles_m, tiles_n, 4, tm, tn);
+    ia = (const char*)A + (int64_t)tm * X4_BM * lda * 2;
+    ib = (const char*)B + (int64_t)tn * X4_BN * ldb * 2;
+    ia_n = ((int64_t)M - tm * X4_BM) * lda * 2;
+    ib_n = ((int64_t)N - tn * X4_BN) * ldb * 2;
+  };
+  if (my > 0) iss_tile(0);
+  auto dma_next = [&](int q) {  // global unit q of the stream
+#if defined(__HIP_DEVICE_COMPILE__)
+    char* st = smem + (q & (XR_NS - 1)) * XR_SLOT;
+    if (!(dbg & 1)) {
+      xr_dma(ia + iss_u * XR_ROWB, ia_n - iss_u * XR_ROWB, lda * 2, st, w, va);
+      xr_dma(ib + iss_u * XR_ROWB, ib_n - iss_u * XR_ROWB, ldb * 2, st + XR_OPB, w, vb);
+    }
+#endif
+    if (++iss_u == U) {
+      iss_u = 0;
+      if (++iss_i < my) iss_tile(iss_i);
+    }
+  };
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const lds_void*)smem;
+  const uint32_t ch = (uint32_t)((hi ^ rswz<32>(lo)) * 16);
+  const uint32_t arow = lds0 + (uint32_t)((128 * wm + lo) * XR_ROWB) + ch;
+  const uint32_t brow = lds0 + (uint32_t)(XR_OPB + (128 * wn + lo) * XR_ROWB) + ch;
+#define XP_RD(dst, a, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(a), "i"(off))
+  // accumulators: defined by the first unit of every tile (MFMAs with C = 0), so the epilogue
+  // never writes them (a zeroing assignment inside the persistent loop made the allocator move them
+  // out of the accumulator registers: hundreds of spills)
+  f32x4 acc[8][8];
+  auto rd_pair = [&](bf16x8 (&Na)[8], bf16x8 (&Nb)[8], uint32_t aa, uint32_t ab, int i) {
+    switch (i) {
+      case 0: XP_RD(Na[0], aa, 0); XP_RD(Nb[0], ab, 0); break;
+      case 1: XP_RD(Na[1], aa, 1024); XP_RD(Nb[1], ab, 1024); break;
+      case 2: XP_RD(Na[2], aa, 2048); XP_RD(Nb[2], ab, 2048); break;
+      case 3: XP_RD(Na[3], aa, 3072); XP_RD(Nb[3], ab, 3072); break;
+      case 4: XP_RD(Na[4], aa, 4096); XP_RD(Nb[4], ab, 4096); break;
+      case 5: XP_RD(Na[5], aa, 5120); XP_RD(Nb[5], ab, 5120); break;
+      case 6: XP_RD(Na[6], aa, 6144); XP_RD(Nb[6], ab, 6144); break;
+      default: XP_RD(Na[7], aa, 7168); XP_RD(Nb[7], ab, 7168); break;
+    }
+  };
+  // the next unit's 16 fragment reads go out first (asm: the compiler adds no waits; they land
+  // under the 64 MFMAs), then the MFMAs, starting a tile's accumulation with C = 0 in its first unit
+  auto mma = [&](const bf16x8 (&Ra)[8], const bf16x8 (&Rb)[8], bool rd, bf16x8 (&Na)[8], bf16x8 (&Nb)[8],
+                 uint32_t aa, uint32_t ab, bool first) {
+    if (rd) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rd_pair(Na, Nb, aa, ab, i);
+    }
+    if (first) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mfma_a0(acc[i][j], Rb[j], Ra[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mfma_a(acc[i][j], Rb[j], Ra[i]);
+    }
+  };
+  auto slot = [&](int q) { return (uint32_t)((q & (XR_NS - 1)) * XR_SLOT); };
+  constexpr int kWaitLgkm0 = 0xC07F;
+  int cur_i = 0;
+  auto epilogue = [&]() {
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 7" ::: "memory");
+    int tm, tn;
+    grouped_tile(pos + cur_i * G, tiles_m, tiles_n, 4, tm, tn);
+    const int mb = tm * X4_BM + 128 * wm, nb = tn * X4_BN + 128 * wn;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = nb + 16 * j + 4 * hi;
+      const bool nok = n < N;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (bias && nok) bv = *(const float4*)(bias + n);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = mb + 16 * i + lo;
+        const float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
+                    v3 = acc[i][j][3] + bv.w;
+        if (!nok || m >= M) continue;
+        *(uint2*)((uint16_t*)C + (int64_t)m * ldc + n) = make_uint2(pack16(v0, v1, c_dt), pack16(v2, v3, c_dt));
+      }
+      // one column of fragments at a time: the accumulator reads of the next column are not
+      // hoisted (the next tile's first fragments are live in arch VGPRs meanwhile)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  bf16x8 A0[8], B0[8], A1[8], B1[8];
+  if (S > 0) {
+#pragma unroll
+    for (int q = 0; q < XR_NS; ++q)
+      if (q < S) dma_next(q);
+    if (S >= 4) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (S == 3) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (S == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rd_pair(A0, B0, arow + slot(0), brow + slot(0), i);
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+  }
+  // after an epilogue its (many) stores sit behind the DMAs in the vmcnt queue: the first wait
+  // then saturates at 63 (it may also wait for a few of the oldest stores)
+  bool after_epi = false;
+#define XP_UNIT(q, u, CA, CB, NA, NB, EPI)                                                 \
+  do {                                                                                     \
+    const int q_ = (q);                                                                    \
+    if (after_epi) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");                       \
+    if (q_ + 3 < S) { if (!after_epi) asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); } \
+    else if (q_ + 2 < S) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                 \
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                  \
+    after_epi = false;                                                                     \
+    if (!(dbg & 2)) __builtin_amdgcn_s_barrier();                                          \
+    asm volatile("" ::: "memory");                                                         \
+    if (q_ + 4 < S) dma_next(q_ + 4);                                                      \
+    __builtin_amdgcn_s_setprio(1);                                                         \
+    mma(CA, CB, q_ + 1 < S, NA, NB, arow + slot(q_ + 1), brow + slot(q_ + 1), (u) == 0);   \
+    __builtin_amdgcn_s_setprio(0);                                                         \
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);                                                \
+    if (EPI && (u) == U - 1) {                                                             \
+      epilogue();                                                                          \
+      ++cur_i;                                                                             \
+      after_epi = true;                                                                    \
+    }                                                                                      \
+  } while (0)
+  // U is even for every supported K (K % 64 == 0): units pair up inside a tile
+  for (int q = 0; q < S; q += 2) {
+    const int u = q % U;
+    XP_UNIT(q, u, A0, B0, A1, B1, false);  // u is even: never a tile's last unit
+    XP_UNIT(q + 1, u + 1, A1, B1, A0, B0, true);
+  }
+#undef XP_UNIT
+#undef XP_RD
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 }  // namespace
 
 // C[M][N] = A[M][K] B[N][K]^T (+ bias[N]); bf16 operands (rows 16-byte aligned), K % 64 == 0,
@@ -209,6 +546,21 @@ RK_API int rk_xgemm4(const void* a, int64_t lda, const void* b, int64_t ldb, voi
   // per-lane + per-instruction DMA offsets stay below 2^31 (256 rows of the operand)
   if ((int64_t)256 * lda * 2 >= (1ll << 31) || (int64_t)256 * ldb * 2 >= (1ll << 31)) return (int)hipErrorInvalidValue;
   const int tiles = ((M + X4_BM - 1) / X4_BM) * ((N + X4_BN - 1) / X4_BN);
+  if (g_x4_dbg & 16) {  // variant P (persistent R): one block per CU
+    static int ncu = 0;
+    if (ncu <= 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    }
+    xgemm4p_kernel<<<std::min(tiles, ncu), X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc,
+                                                          c_dt, bias, M, N, K, g_x4_dbg);
+    return (int)hipGetLastError();
+  }
+  if (g_x4_dbg & 4) {  // variant R (32-deep units, 4-slot ring); K % 32 suffices
+    xgemm4r_kernel<<<tiles, X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc, c_dt, bias, M, N,
+                                           K, g_x4_dbg);
+    return (int)hipGetLastError();
+  }
   xgemm4_kernel<<<tiles, X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc, c_dt, bias, M, N, K,
                                         g_x4_dbg);
   return (int)hipGetLastError();

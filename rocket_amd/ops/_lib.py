@@ -102,6 +102,7 @@ KERNEL_SIGS = {
     "rk_bn_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int] + [c_void_p] * 11),
     "rk_ln_fwd": (c_int, [c_int, c_int] + [c_void_p] * 8 + [c_int64, c_int, c_float, c_void_p]),
     "rk_ln_workspace": (c_int64, [c_int64, c_int]),
+    "rk_ln_set_bwd_cfg": (c_int, [c_int, c_int]),
     "rk_attn_max_len": (c_int, []),
     "rk_attn_set_waves": (c_int, [c_int, c_int, c_int]),
     "rk_attn_set_bwd_fused": (c_int, [c_int]),

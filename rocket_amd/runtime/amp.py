@@ -46,6 +46,7 @@ class FusedGradScaler:
         # hold the handle of step k while step k+1 records its own (EngineScheduler speculation)
         pin = self.device.type == "cuda"
         self._ring = [torch.zeros(1, dtype=torch.float32, pin_memory=pin) for _ in range(4)]
+        self._ring_ev = [torch.cuda.Event() for _ in range(4)] if pin else [None] * 4  # reused: no per-step event
         self._ring_i = 0
         self._last_host = self._ring[0]
         self._last_event = None
@@ -147,9 +148,8 @@ class FusedGradScaler:
         self._ring_i = (self._ring_i + 1) % len(self._ring)
         self._last_host = self._ring[self._ring_i]
         self._last_host.copy_(self.state[LAST : LAST + 1], non_blocking=True)
-        self._last_event = None
-        if self.device.type == "cuda":
-            self._last_event = torch.cuda.Event()
+        self._last_event = self._ring_ev[self._ring_i]
+        if self._last_event is not None:
             self._last_event.record()
 
     def last_handle(self):
