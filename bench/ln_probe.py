@@ -40,7 +40,7 @@ def main():
         def run():
             _lib.check(lib.rk_ln_bwd(0, 1, dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                      dx.data_ptr(), dsum.data_ptr(), dres.data_ptr(), dgam.data_ptr(), dbet.data_ptr(),
-                                     dsb.data_ptr(), R, C, ws.data_ptr(), ctr, _lib.stream_ptr(dev)), "rk_ln_bwd")
+                                     dsb.data_ptr(), None, R, C, ws.data_ptr(), ctr, _lib.stream_ptr(dev)), "rk_ln_bwd")
 
         ms = timeit(run)
         print(json.dumps({"rpb": rpb, "prefetch": pf, "us": round(ms * 1e3, 1), "TB/s": round(nbytes / ms / 1e9, 2)}),

@@ -117,11 +117,16 @@ class Loss(Capsule):
         engine = self._accelerator
         sync_here = engine.sync_gradients and not attrs.graph_split
         fused = getattr(self._objective, "loss_and_grad", None)
-        if fused is not None and engine.scaler is None:
+        scaler = engine.scaler
+        dev_scale = getattr(scaler, "scale_tensor", None) if scaler is not None else None
+        if fused is not None and (scaler is None or dev_scale is not None):
             # objective supplies loss AND d(outputs) in one launch, with the loss bookkeeping folded
-            # in: backward starts directly from the outputs (no loss node, no seed fill)
+            # in: backward starts directly from the outputs (no loss node, no seed fill); under the
+            # device fp16 scaler the kernel also multiplies d(outputs) by the loss scale
             scale = 1.0 / engine.gradient_accumulation_steps
-            res = fused(attrs.batch, scale, (self._acc, self._ring, self._slot, scale, sync_here))
+            acc = (self._acc, self._ring, self._slot, scale, sync_here)
+            res = (fused(attrs.batch, scale, acc, dev_scale=dev_scale) if dev_scale is not None
+                   else fused(attrs.batch, scale, acc))
             if res is not None:
                 _, outs, grads = res
                 torch.autograd.backward(outs, grads)

@@ -102,18 +102,23 @@ class CrossEntropy(nn.Module):
         return F.cross_entropy(logits.float(), target)
 
 
-    def loss_and_grad(self, batch, grad_scale: float, accum=None):
+    def loss_and_grad(self, batch, grad_scale: float, accum=None, dev_scale=None):
         """Training-step fast path (used by the Loss capsule under graph capture): loss and
-        d(logits) in one launch.  Returns ``(loss, outputs, output_grads)`` or None."""
+        d(logits) in one launch.  Returns ``(loss, outputs, output_grads)`` or None.  ``dev_scale``:
+        the fp16 loss scale (1-element device tensor) d(logits) is multiplied by; only the fused
+        LeNet backward takes one (None is returned for other logits)."""
         logits, target = batch[2], batch[1]
         if self._fused is False or logits.device.type != "cuda":
             return None
         from rocket_amd.ops.cross_entropy import ce_train
         from rocket_amd.ops.lenet import fuse_cross_entropy
 
-        fused = fuse_cross_entropy(logits, target, grad_scale, accum)  # CE inside the LeNet backward launch
+        # CE inside the LeNet backward launch
+        fused = fuse_cross_entropy(logits, target, grad_scale, accum, dev_scale=dev_scale)
         if fused is not None:
             return fused[0], [logits], [fused[1]]
+        if dev_scale is not None:
+            return None
         res = ce_train(logits, target, grad_scale, accum)
         if res is None:
             return None

@@ -525,7 +525,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(M
   if (MODE == kConvDgradS && lin >= ntiles) return;  // this class has fewer tiles than the largest
   const int split = lin / ntiles;
   const int tile = lin % ntiles;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  int tm, tn;
+  grouped_tile(tile, tiles_m, tiles_n, g.tgroup, tm, tn);
   const int row0 = tm * BM, col0 = tn * BN;
   const int kb = split * g.k_per_split;
   const int ke = min(g.K, kb + g.k_per_split);
@@ -739,12 +740,15 @@ ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stri
   return cg;
 }
 
+int g_tile_group = 4;  // rk_conv_set_tile_group: tile-rows per group of the conv tile walk (1: row-major)
+
 MArgs margs(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int c_dt, int64_t ldc, int M, int N,
             int K) {
   MArgs g = {};
   g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.M = M; g.N = N; g.K = K; g.c_dt = c_dt;
   g.splitk = 1; g.k_per_split = K;
+  g.tgroup = g_tile_group;
   return g;
 }
 
@@ -823,6 +827,10 @@ RK_API int rk_pad_c8(const void* x, void* y, int N, int C, int H, int W, int64_t
 // classes of dX pixels as four stride-1 gathers in one launch (classes without taps store zeros).
 // 1 (default): bf16 forward / input-gradient tiles are stored through LDS in row-contiguous 16-byte
 // chunks; 0: straight from the MFMA accumulator layout (A/B switch, ROCKET_CONV_LDS_EPI)
+RK_API int rk_conv_set_tile_group(int gh) {
+  g_tile_group = gh < 1 ? 1 : gh;
+  return 0;
+}
 RK_API int rk_conv_set_lds_epi(int on) {
   g_lds_epi = on != 0;
   return 0;

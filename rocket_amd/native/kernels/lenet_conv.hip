@@ -692,6 +692,7 @@ struct ClsBwd {
   float* slab;                      // [blocks][SLABW] conv weight/bias gradient partials
   const int64_t* row_table;         // fused gather: target of sample i = row_labels[row_table[i]]
   const int64_t* row_labels;
+  const float* gscale_dev;          // optional device factor on d(logits) (the fp16 loss scale)
 };
 
 template <bool MLP>
@@ -875,7 +876,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
         if (threadIdx.x < SPB * DYP || (threadIdx.x >= 256 && threadIdx.x < 256 + F3)) {
           // pre-normalised by the batch size (keeps the gradients' magnitudes, and so their bf16
           // rounding, those of the mean); the weight-gradient launch applies N / (valid count)
-          const float sc = cb.grad_scale / (float)N;
+          const float sc = cb.grad_scale / (float)N * (cb.gscale_dev ? *cb.gscale_dev : 1.f);
           if (threadIdx.x < SPB * DYP) {
             const int sl = threadIdx.x / DYP, o = threadIdx.x % DYP;
             sm.dyl[sl][o] = c16(o < F3 ? sc * sm.dyf[sl][o] : 0.f);
@@ -1365,6 +1366,7 @@ struct LenetCE {  // host-side description of the fused cross-entropy (see ClsBw
   float acc_scale;
   int sync;
   int defer_loss;  // 1: rk_mlp3_wgrad_loss finalises the loss (no last-block ticket in this launch)
+  const float* gscale_dev;  // nullable: d(logits) also scaled by *gscale_dev (device loss scale)
 };
 
 static ClsBwd cls_bwd(const void* frag, const float* dy, const void* h1T, const void* h2T, void* dyT, void* d2T,
@@ -1395,6 +1397,7 @@ static ClsBwd cls_bwd(const void* frag, const float* dy, const void* h1T, const 
     cb.acc_scale = ce->acc_scale;
     cb.sync = ce->sync;
     cb.defer_loss = ce->defer_loss;
+    cb.gscale_dev = ce->gscale_dev;
   }
   return cb;
 }

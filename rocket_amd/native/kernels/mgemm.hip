@@ -53,7 +53,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) mgemm_kernel(
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int split = lin / ntiles;
   const int tile = lin % ntiles;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  int tm, tn;
+  grouped_tile(tile, tiles_m, tiles_n, g.tgroup, tm, tn);
   const int row0 = tm * BM, col0 = tn * BN;
   const int kb = split * g.k_per_split;
   const int ke = min(g.K, kb + g.k_per_split);
@@ -871,6 +872,9 @@ RK_API int rk_mgemm(const void* a, int64_t lda, int a_kmaj, const void* b, int64
   g.aux = (const uint16_t*)aux; g.rowsum = rowsum; g.slab = slab;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.c_dt = c_dt; g.epi = epi; g.accumulate = accumulate;
+  g.lds_epi = 0;
+  g.tgroup = 4;  // grouped tile walk (rk_common.h)
+  g.dbg = 0;
   if (splitk < 1) splitk = 1;
   const int kq = 64;  // split boundaries on 64 (a multiple of every config's BK)
   int kps = ((K + kq - 1) / kq + splitk - 1) / splitk * kq;

@@ -34,6 +34,7 @@ struct MArgs {
   int accumulate;
   int splitk, k_per_split;
   int lds_epi;  // conv.hip: bf16 tile stored through LDS in row-contiguous 16-byte chunks
+  int tgroup;   // grouped tile walk (rk_common.h grouped_tile): tile-rows per group, <= 1 row-major
   int dbg;      // xgemm.hip diagnostics (rk_xgemm_set_dbg): bit 0 no DMA, 1 no barrier, 2 no ds_read, 3 no MFMA
 };
 

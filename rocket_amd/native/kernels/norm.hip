@@ -925,7 +925,7 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
 constexpr int CS_T = 1024;
 __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ part, int nrows, int C2,
                                                       float* dgamma, float* dbeta, int C, float* dthird = nullptr,
-                                                      int perm_q = 0) {
+                                                      int perm_q = 0, float* dthird_acc = nullptr) {
   __shared__ float red[CS_T / 64][65];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int sl = threadIdx.x >> 6, nsl = CS_T / 64;
@@ -953,6 +953,7 @@ __global__ void __launch_bounds__(CS_T) colsum_kernel(const float* __restrict__ 
       if (dbeta) dbeta[oc] += u;
     } else if (dthird) {
       dthird[oc] = u;  // written, not accumulated: the caller needs no zeroed buffer
+      if (dthird_acc) dthird_acc[oc] += u;
     }
   }
 }
@@ -1368,12 +1369,14 @@ RK_API int64_t rk_ln_workspace(int64_t rows, int C) {
 // LayerNorm backward; dgamma/dbeta accumulated (+=). dt: x/dx dtype, dto: dy dtype.
 // dsum (dtype dt) / dres (dtype dto) may be null: dx = LN_bwd(dy) [+ dsum], dres = dx
 // dres_sum (f32 [C], optional, needs dres): = column sums of dres (the added branch's bias gradient;
-// written, not accumulated)
+// written, not accumulated); dres_acc (f32 [C], optional, needs dres_sum): += the same sums (that
+// bias's persistent gradient, so its producer needs no add launch)
 RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float* g, const float* mean,
                      const float* rstd, void* dx, const void* dsum, void* dres, float* dgamma, float* dbeta,
-                     float* dres_sum, int64_t rows, int C, float* ws, unsigned* counter, hipStream_t s) {
+                     float* dres_sum, float* dres_acc, int64_t rows, int C, float* ws, unsigned* counter,
+                     hipStream_t s) {
   if ((dt == F16 && dto == BF16) || (dt == BF16 && dto == F16)) return (int)hipErrorInvalidValue;
-  if (C % 4 || C > 64 * 4 * LN_MAXV || (dres_sum && !dres)) return (int)hipErrorInvalidValue;
+  if (C % 4 || C > 64 * 4 * LN_MAXV || (dres_sum && !dres) || (dres_acc && !dres_sum)) return (int)hipErrorInvalidValue;
   const int rpb = ln_bwd_rpb(rows);
   const int grid = (int)((rows + rpb - 1) / rpb);
   const int nv = (C + 255) / 256;
@@ -1403,7 +1406,7 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
 #undef RK_LBN
 #undef RK_LB
   if (dgamma || dbeta || dres_sum)
-    colsum_kernel<<<(np * C + 63) / 64, CS_T, 0, s>>>(ws, grid, np * C, dgamma, dbeta, C, dres_sum);
+    colsum_kernel<<<(np * C + 63) / 64, CS_T, 0, s>>>(ws, grid, np * C, dgamma, dbeta, C, dres_sum, 0, dres_acc);
   (void)counter;
   return (int)hipGetLastError();
 }

@@ -25,6 +25,8 @@
 // Memory: each block streams one chunk of J*1024 elements (J float4 per thread per array):
 // params/grads/exp_avg/exp_avg_sq read once, written once.  J = 4 (4096-element chunks) for big
 // models; J = 1 for small ones (LeNet's 61,706 parameters: 4x the blocks, one load round trip).
+#include <cstring>
+
 #include "optim_common.h"
 
 using namespace rk;
@@ -280,3 +282,21 @@ RK_API int rk_optim_mt(int kind, int gdtype, const void* tensors, const void* bl
 #undef RK_OPT_LAUNCH_J
   return (int)hipGetLastError();
 }
+
+// Host-mapped (coherent) memory for device-published values the host polls with plain loads (the
+// fp16 scaler's skip-flag ring, AmpSlot kAmpHost).  Returns the host address; *dev gets the
+// device address to hand to kernels.  nullptr on failure.
+RK_API void* rk_host_mapped_alloc(int64_t bytes, void** dev) {
+  void* h = nullptr;
+  if (hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+  memset(h, 0, (size_t)bytes);
+  if (hipHostGetDevicePointer(dev, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    return nullptr;
+  }
+  return h;
+}
+RK_API void rk_host_mapped_free(void* h) {
+  if (h) (void)hipHostFree(h);
+}
+

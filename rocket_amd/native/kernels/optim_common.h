@@ -54,8 +54,13 @@ __device__ __forceinline__ float read_step(const float* step) {
 // Device-resident dynamic loss scaling (fp16 AMP; torch.amp.GradScaler semantics):
 //   amp[0] scale, amp[1] 1/scale, amp[2] found_inf (set by rk_amp_check, consumed + cleared here),
 //   amp[3] growth tracker, amp[4] growth factor, amp[5] backoff factor, amp[6] growth interval,
-//   amp[7] found_inf of the last step (read back by the host only when it must know).
-enum AmpSlot { kAmpScale = 0, kAmpInv, kAmpFound, kAmpTracker, kAmpGrowth, kAmpBackoff, kAmpInterval, kAmpLast };
+//   amp[7] found_inf of the last step, amp[8] number of updates so far (uint32 bits),
+//   amp[10..11] 0 or the device address of a host-mapped int32 ring[kAmpRing]: update number n
+//   publishes (n << 1) | found_inf into ring[n % kAmpRing] (one 4-byte store, so the host reads a
+//   step's skip flag with a plain load: no copy, no event on the stream).
+enum AmpSlot { kAmpScale = 0, kAmpInv, kAmpFound, kAmpTracker, kAmpGrowth, kAmpBackoff, kAmpInterval, kAmpLast,
+               kAmpSeq, kAmpHost = 10, kAmpSlots = 12 };
+constexpr int kAmpRing = 64;
 
 // torch._amp_update_scale_, executed by the optimizer launch's last block
 __device__ __forceinline__ void amp_update(float* amp) {
@@ -78,6 +83,13 @@ __device__ __forceinline__ void amp_update(float* amp) {
   amp[kAmpInv] = 1.f / scale;
   amp[kAmpLast] = found;
   amp[kAmpFound] = 0.f;  // every block has read it: each took its ticket after its first read
+  const uint32_t seq = __float_as_uint(amp[kAmpSeq]) + 1u;
+  amp[kAmpSeq] = __uint_as_float(seq);
+  const uint64_t ring = *reinterpret_cast<const uint64_t*>(amp + kAmpHost);
+  if (ring) {  // system-scope (write-through) vector store into host memory
+    int* e = reinterpret_cast<int*>(ring) + (seq % kAmpRing);
+    __hip_atomic_store(e, (int)((seq << 1) | (found != 0.f ? 1u : 0u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 __device__ __forceinline__ void advance_step(float* step, unsigned* counter, bool skip, float cur,

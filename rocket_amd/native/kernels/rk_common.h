@@ -174,4 +174,22 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
+// Grouped tile walk: linear tile id t (after xcd_remap the ids an XCD runs at once are
+// consecutive) -> (tm, tn) in groups of gh tile-rows, column by column inside a group, so an
+// XCD's concurrent tiles form a gh-row block sharing few A- and B-panels in its L2.  gh <= 1: the
+// row-major walk.  A bijection for any tiles_m (the last group is shorter).
+__device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, int gh, int& tm, int& tn) {
+  if (gh <= 1) {
+    tm = t / tiles_n;
+    tn = t - tm * tiles_n;
+    return;
+  }
+  const int per = gh * tiles_n;
+  const int g = t / per, first = g * gh;
+  const int h = min(tiles_m - first, gh);
+  const int r = t - g * per;
+  tm = first + r % h;
+  tn = r / h;
+}
+
 }  // namespace rk

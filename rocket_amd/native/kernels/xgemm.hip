@@ -54,6 +54,7 @@ RK_API int rk_xgemm(const void* a, int64_t lda, int a_kmaj, const void* b, int64
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.c_dt = c_dt; g.epi = epi; g.accumulate = accumulate;
   g.lds_epi = 0;
+  g.tgroup = 1;  // (the persistent walk places tiles itself)
   g.dbg = g_dbg;
   if (splitk < 1) splitk = 1;
   const int kq = 32;  // split boundaries on whole units

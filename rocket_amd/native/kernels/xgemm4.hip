@@ -27,19 +27,6 @@ using namespace rk;
 
 namespace {
 
-// Tile order: the linear id (after the XCD remap: the ids of one XCD are consecutive) walks the
-// tile grid in groups of GH tile-rows, column by column inside a group, so the 32 tiles an XCD
-// runs at once form a GH x (32/GH) block: GH A-panels and 32/GH B-panels per k-step through that
-// XCD's L2 instead of 1-2 A-panels and 16-32 B-panels (a row-major walk over a wide grid).
-__device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, int gh, int& tm, int& tn) {
-  const int per = gh * tiles_n;
-  const int g = t / per, first = g * gh;
-  const int h = min(tiles_m - first, gh);
-  const int r = t - g * per;
-  tm = first + r % h;
-  tn = r / h;
-}
-
 constexpr int X4_BM = 256, X4_BN = 256, X4_BK = 64, X4_NT = 256;
 constexpr int X4_ROWB = X4_BK * 2;                 // 128-byte image rows
 constexpr int X4_OPB = X4_BM * X4_ROWB;            // 32 KiB per operand per stage

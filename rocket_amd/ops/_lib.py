@@ -53,6 +53,7 @@ KERNEL_SIGS = {
     "rk_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_int64, c_int] + [c_void_p] * 9 + [c_float, c_float, c_void_p,
                                                                                             c_void_p, c_void_p]),
     "rk_conv_set_lds_epi": (c_int, [c_int]),
+    "rk_conv_set_tile_group": (c_int, [c_int]),
     "rk_conv_set_cfg": (c_int, [c_int]),
     "rk_mlp3_set_trace": (None, [c_void_p]),
     "rk_conv_dgrad_bn": (c_int, [c_int] + [c_void_p] * 3 + [c_int] * 9 + [c_void_p] * 6),
@@ -83,6 +84,8 @@ KERNEL_SIGS = {
     "rk_optim_mt": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_int, c_void_p]),
     "rk_amp_check": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "rk_host_mapped_alloc": (c_void_p, [c_int64, c_void_p]),
+    "rk_host_mapped_free": (None, [c_void_p]),
     "rk_optim_chunk_for": (c_int, [c_int64]),
     "rk_gather_rows": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "rk_loss_accum": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_int, c_void_p]),
@@ -138,7 +141,7 @@ KERNEL_SIGS = {
     "rk_p2p_clear_error": (c_int, [c_void_p]),
     "rk_p2p_error_ptr": (c_void_p, [c_void_p]),
     "rk_p2p_destroy": (c_int, [c_void_p]),
-    "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 11 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
+    "rk_ln_bwd": (c_int, [c_int, c_int] + [c_void_p] * 12 + [c_int64, c_int, c_void_p, c_void_p, c_void_p]),
 }
 
 # fp16 builds of the fused LeNet kernels (lenet_conv_h.hip / mlp_h.hip): same signatures

@@ -45,6 +45,10 @@ N_SLOTS = 512  # resident 128x128 conv blocks (2 per CU)
 LDS_EPI = os.environ.get("ROCKET_CONV_LDS_EPI", "1") != "0"
 # k-tile pipeline of the bf16 conv kernels (conv.hip rk_conv_set_cfg)
 PIPE = int(os.environ.get("ROCKET_CONV_PIPE", "0"))
+# tile walk of the conv kernels: tile-rows per group (rk_common.h grouped_tile; 1 = row-major).
+# Grouped walks (4 tile-rows) measured neutral-to-slower on ResNet-50/18 (activation panels already
+# fit L2): profiles/r4_conv_tile_group_ab.md
+TILE_GROUP = int(os.environ.get("ROCKET_CONV_TILE_GROUP", "1"))
 _epi_set = False
 
 
@@ -55,6 +59,7 @@ def _kernels():
         lib.rk_conv_set_lds_epi(int(LDS_EPI))
         if lib.rk_conv_set_cfg(PIPE):
             raise ValueError(f"ROCKET_CONV_PIPE={PIPE}: no such conv pipeline")
+        lib.rk_conv_set_tile_group(TILE_GROUP)
         _epi_set = True
     return lib
 

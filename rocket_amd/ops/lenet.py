@@ -252,6 +252,9 @@ class LeNetFragments:
         self.versions = None
         self.params = None
         self.spec_misses = 0
+        # the device loss scale (fp16 AMP) the last fused cross-entropy multiplied d(logits) by;
+        # the speculative forward launch applies the same one
+        self.dev_scale = None
 
     @property
     def spec_ok(self) -> bool:
@@ -288,7 +291,7 @@ class _LenetCE(ctypes.Structure):
                 ("grad_scale", ctypes.c_float), ("partials", ctypes.c_void_p), ("counter", ctypes.c_void_p),
                 ("loss_out", ctypes.c_void_p), ("acc", ctypes.c_void_p), ("ring", ctypes.c_void_p),
                 ("slot", ctypes.c_void_p), ("ring_size", ctypes.c_int), ("acc_scale", ctypes.c_float),
-                ("sync", ctypes.c_int), ("defer_loss", ctypes.c_int)]
+                ("sync", ctypes.c_int), ("defer_loss", ctypes.c_int), ("gscale_dev", ctypes.c_void_p)]
 
 
 class _RowSrc(ctypes.Structure):
@@ -358,10 +361,10 @@ def _optimizer_epilogue(params, direct):
     return epi, opt
 
 
-def _spec_matches(spec, target) -> bool:
+def _spec_matches(spec, target, dev_scale=None) -> bool:
     t, ver = spec[0], spec[1]
     return (target.data_ptr() == t.data_ptr() and target.shape == t.shape and target.dtype == t.dtype
-            and target._version == ver)
+            and target._version == ver and spec[8] is dev_scale)
 
 
 class _LeNetFused(torch.autograd.Function):
@@ -411,9 +414,10 @@ class _LeNetFused(torch.autograd.Function):
             slab = torch.empty(N // 4, int(lib.rk_lenet_slab_width()), dtype=torch.float32, device=dev)
             partials = torch.empty(2 * (N // 4), dtype=torch.float32, device=dev)  # loss sums, valid counts
             loss_out = torch.empty(2, dtype=torch.float32, device=dev)
+            dscale = frags.dev_scale
             ce = _LenetCE(logits.data_ptr(), target.data_ptr(), -100, 1.0, partials.data_ptr(),
                           _lib.Workspace.get(dev).counter("lenet_ce"), loss_out.data_ptr(), None, None, None, 0,
-                          0.0, 0, 1)
+                          0.0, 0, 1, _lib.ptr(dscale))
             claimed = _claim_rows(x, target)  # a deferred loader batch: this launch gathers it
             rows = claimed[0] if claimed is not None else None
             ctx.rows_pend = claimed[1] if claimed is not None else None
@@ -424,7 +428,7 @@ class _LeNetFused(torch.autograd.Function):
                                           slab.data_ptr(), N, ctypes.byref(ce),
                                           ctypes.byref(rows) if rows is not None else None, stream),
                        "rk_lenet_train")
-            ctx.spec = (target, target._version, dyT, d2T, d1T, slab, partials, loss_out)
+            ctx.spec = (target, target._version, dyT, d2T, d1T, slab, partials, loss_out, dscale)
         else:
             from rocket_amd.runtime.data import materialize_batch
 
@@ -452,11 +456,12 @@ class _LeNetFused(torch.autograd.Function):
         ce, keep, fin = None, None, None
         spec, ctx.spec = ctx.spec, None
         gscale = 1.0
-        if ctx.ce_spec is not None and spec is not None and _spec_matches(spec, ctx.ce_spec[0]):
+        if ctx.ce_spec is not None and spec is not None and _spec_matches(spec, ctx.ce_spec[0], ctx.ce_spec[4]):
             # the forward launch already ran this loss's backward for a unit upstream gradient
-            target, grad_scale, accum, loss_out = ctx.ce_spec
+            # (times the same device loss scale)
+            target, grad_scale, accum, loss_out, _ = ctx.ce_spec
             ctx.ce_spec = None
-            _, _, dyT, d2T, d1T, slab, partials, _ = spec
+            _, _, dyT, d2T, d1T, slab, partials, _, _ = spec
             acc = ring = slot = None
             acc_scale, sync = 0.0, 0
             if accum is not None:
@@ -470,7 +475,7 @@ class _LeNetFused(torch.autograd.Function):
         if spec is not None:
             ctx.frags.spec_misses += 1  # the loss was not the fused cross-entropy on those targets
         if ctx.ce_spec is not None:
-            target, grad_scale, accum, loss_out = ctx.ce_spec
+            target, grad_scale, accum, loss_out, dev_scale = ctx.ce_spec
             ctx.ce_spec = None
             acc = ring = slot = None
             acc_scale, sync = 0.0, 0
@@ -481,7 +486,7 @@ class _LeNetFused(torch.autograd.Function):
             ce = _LenetCE(logits.data_ptr(), target.data_ptr(), -100, float(grad_scale), partials.data_ptr(),
                           _lib.Workspace.get(dev).counter("lenet_ce"), loss_out.data_ptr(), _lib.ptr(acc),
                           _lib.ptr(ring), _lib.ptr(slot), ring.numel() if ring is not None else 0, float(acc_scale),
-                          int(sync), 1)
+                          int(sync), 1, _lib.ptr(dev_scale))
             fin = _LossFin(partials.data_ptr(), N // 4, loss_out.data_ptr(), _lib.ptr(acc), _lib.ptr(ring),
                            _lib.ptr(slot), ring.numel() if ring is not None else 0, float(acc_scale), int(sync))
             dy = logits  # unread
@@ -549,25 +554,29 @@ def lenet_forward(x, conv1, conv2, fc1, fc2, fc3, target=None):
                              fc2.weight, fc2.bias, fc3.weight, fc3.bias, frags, target)
 
 
-def fuse_cross_entropy(logits, target, grad_scale: float, accum=None):
+def fuse_cross_entropy(logits, target, grad_scale: float, accum=None, dev_scale=None):
     """Attach a mean cross-entropy (ignore_index -100) to fused-LeNet ``logits`` so the backward
     launch computes loss and d(logits) in-kernel.  Returns ``(loss[0-d], dummy_grad)`` to pass to
     ``torch.autograd.backward([logits], [dummy_grad])``, or None if ``logits`` is not a fused-LeNet
-    output (or ``N > 65536``).  ``accum`` as in :func:`rocket_amd.ops.cross_entropy.ce_train`."""
+    output (or ``N > 65536``).  ``accum`` as in :func:`rocket_amd.ops.cross_entropy.ce_train`.
+    ``dev_scale``: optional 1-element fp32 device tensor (the fp16 loss scale) that d(logits) is
+    multiplied by in-kernel, as ``scaler.scale(loss).backward()`` would (the loss stays unscaled)."""
     fn = logits.grad_fn
     if (fn is None or type(fn).__name__ != "_LeNetFusedBackward" or logits.dim() != 2 or logits.shape[0] > 65536
             or target.dim() != 1 or target.dtype.is_floating_point):
         return None
     target = target.contiguous().to(torch.int64)
     spec = getattr(fn, "spec", None)
-    if spec is not None and _spec_matches(spec, target):
+    frags = getattr(fn, "frags", None)
+    if frags is not None:
+        frags.dev_scale = dev_scale  # the next speculative forward scales d(logits) the same way
+    if spec is not None and _spec_matches(spec, target, dev_scale):
         loss_out = spec[7]  # the speculative forward launch already wrote this loss's partials
     else:
         loss_out = torch.empty(2, dtype=torch.float32, device=logits.device)
-        frags = getattr(fn, "frags", None)
         if frags is not None:
             frags.spec_misses = 0  # the fused loss is in use: speculate on the next forward
-    fn.ce_spec = (target, float(grad_scale), accum, loss_out)
+    fn.ce_spec = (target, float(grad_scale), accum, loss_out, dev_scale)
     # the incoming gradient is never read (the kernel derives d(logits) itself): no fill launch
     return loss_out[0], torch.empty((), dtype=logits.dtype, device=logits.device).expand_as(logits)
 

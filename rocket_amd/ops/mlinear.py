@@ -179,11 +179,15 @@ BIAS_LINK_HITS = 0  # bias gradients taken from a consuming add-LayerNorm (tests
 def _bias_from_link(link, dy: torch.Tensor, bias) -> tuple:
     """(handled, db): the bias gradient the consuming add-LayerNorm already formed (BiasLink), put
     into a persistent ``bias.grad`` (db None) or returned; handled False -> compute it here."""
+    applied = link is not None and link.applied
     db = link.take(dy) if link is not None else None
     if db is None:
         return False, None
     global BIAS_LINK_HITS
     BIAS_LINK_HITS += 1
+    if applied:  # the LN kernel added db into the persistent bias.grad already
+        grad_ready(bias)
+        return True, None
     if _direct(bias):
         bias.grad.add_(db)
         grad_ready(bias)

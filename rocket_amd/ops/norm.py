@@ -28,6 +28,7 @@ import os
 import rocket_amd.ops as _ops
 from rocket_amd.ops import _lib
 from rocket_amd.ops.lenet import _finish, _grad_targets
+from rocket_amd.ops.linear import _direct
 
 
 # ROCKET_BN_BWD_FUSE (default 1): a BatchNorm whose output feeds a stride-1 native conv leaves its
@@ -277,7 +278,7 @@ class _LN(torch.autograd.Function):
         w = weight.detach() if weight is not None else None
         _lib.check(lib.rk_ln_bwd(_dt(x), _dt(dy), dy.data_ptr(), x.data_ptr(), _lib.ptr(w), mean.data_ptr(),
                                  rstd.data_ptr(), dx.data_ptr(), None, None, _lib.ptr(dgamma), _lib.ptr(dbeta), None,
-                                 rows, C, ws.data_ptr(), counter, _lib.stream_ptr(dev)), "rk_ln_bwd")
+                                 None, rows, C, ws.data_ptr(), counter, _lib.stream_ptr(dev)), "rk_ln_bwd")
         g = _finish(params, bufs, direct) if params else []
         gw = g[0] if weight is not None else None
         gb = g[-1] if bias is not None else None
@@ -291,13 +292,14 @@ class BiasLink:
     them when its incoming gradient is exactly that dr, unmodified (:meth:`take`), instead of a column-sum pass
     over its output gradient.  Lives on the autograd graph (both ctxs), like :class:`BwdLink`."""
 
-    __slots__ = ("bias", "db", "dr", "dr_ver")
+    __slots__ = ("bias", "db", "dr", "dr_ver", "applied")
 
     def __init__(self, bias):
         self.bias = bias
         self.db = None
         self.dr = None  # the LN's dr (held: its storage cannot be recycled under another tensor)
         self.dr_ver = None
+        self.applied = False  # the LN kernel already added db into the persistent bias.grad
 
     def take(self, dy: torch.Tensor):
         """The finished bias gradient for incoming gradient ``dy``, or None (compute it yourself).
@@ -306,10 +308,13 @@ class BiasLink:
         counter value.  When the linear's output also feeds another op, autograd's input buffer may
         sum that op's gradient into dr in place before handing it over (same pointer, bumped
         ``_version``): then the link's column sums miss that contribution and are refused."""
-        db, dr, ver = self.db, self.dr, self.dr_ver
+        db, dr, ver, applied = self.db, self.dr, self.dr_ver, self.applied
         self.db = self.dr = self.dr_ver = None
+        self.applied = False
         ok = (db is not None and dr is not None and dy.data_ptr() == dr.data_ptr()
               and dy.numel() == dr.numel() and dy._version == ver)
+        if applied and not ok:
+            self.bias.grad.sub_(db)  # refused: back out what the LN kernel already added
         return db if ok else None
 
 
@@ -377,12 +382,16 @@ class _AddLN(torch.autograd.Function):
         w = weight.detach() if weight is not None else None
         link, ctx.link = ctx.link, None
         rsum = torch.empty(C, dtype=torch.float32, device=dev) if link is not None else None  # written by the kernel
+        # a persistent fp32 bias.grad takes the sums in the same launch (the linear then only
+        # confirms the hand-off, or backs the sums out again if it refuses it: BiasLink.take)
+        acc = (link.bias.grad if link is not None and _direct(link.bias) and link.bias.grad.dtype == torch.float32
+               else None)
         _lib.check(lib.rk_ln_bwd(_dt(ssum), _dt(dy), dy.data_ptr(), ssum.data_ptr(), _lib.ptr(w), mean.data_ptr(),
                                  rstd.data_ptr(), dx.data_ptr(), _lib.ptr(ds), dr.data_ptr(), _lib.ptr(dgamma),
-                                 _lib.ptr(dbeta), _lib.ptr(rsum), rows, C, ws.data_ptr(), counter,
+                                 _lib.ptr(dbeta), _lib.ptr(rsum), _lib.ptr(acc), rows, C, ws.data_ptr(), counter,
                                  _lib.stream_ptr(dev)), "rk_ln_bwd(add)")
         if link is not None:
-            link.db, link.dr, link.dr_ver = rsum, dr, dr._version
+            link.db, link.dr, link.dr_ver, link.applied = rsum, dr, dr._version, acc is not None
         g = _finish(params, bufs, direct) if params else []
         gw = g[0] if weight is not None else None
         gb = g[-1] if bias is not None else None

@@ -205,7 +205,7 @@ class _FusedBase(torch.optim.Optimizer):
             return None
         # a private AmpSlot block: unscale by grad_scale, skip on found_inf; GradScaler.update()
         # (host side) keeps owning the scale, so growth/backoff here are inert
-        amp = torch.zeros(8, dtype=torch.float32, device=self._device)
+        amp = torch.zeros(12, dtype=torch.float32, device=self._device)  # optim_common.h kAmpSlots
         amp[1] = 1.0
         amp[6] = float("inf")
         if gs is not None:  # torch hands over the scale itself (its fused kernels divide by it)

@@ -53,7 +53,7 @@ class P2PAllReduce:
         # fault guard: an identity loss-scaling block (optim_common.h AmpSlot: scale 1, growth and
         # backoff 1) handed to the fused optimizers of the replicated model.  A timed-out launch
         # raises its found flag, so the update that would consume un-reduced gradients is skipped.
-        self.fault = torch.tensor([1.0, 1.0, 0.0, 0.0, 1.0, 1.0, float("inf"), 0.0], device=device)
+        self.fault = torch.tensor([1.0, 1.0, 0.0, 0.0, 1.0, 1.0, float("inf"), 0.0] + [0.0] * 4, device=device)  # kAmpSlots
         self._scaler_state = None
         self._set_skip()
 

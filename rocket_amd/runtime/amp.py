@@ -16,9 +16,11 @@ two launches with no host synchronisation:
    rule of ``torch._amp_update_scale_`` and clears the flag.
 
 Whether a step was skipped is only needed by the LR scheduler wrapper (accelerate does not step
-the scheduler after a skipped optimizer step); that value is copied to pinned memory behind the
-update and read lazily.  The two launches are graph-capturable (``step_device``): fp16 steps are
-captured like bf16 ones, the flag copy being enqueued after each replay.  Optimizers that are not fused fall back to the torch primitives on the
+the scheduler after a skipped optimizer step); the update's last block publishes it into a
+host-mapped ring (``(n << 1) | skipped`` at slot ``n % 64`` for update number ``n``), which the host
+reads lazily with a plain load — no copy and no event on the stream (those cost the launch-bound
+fp16 LeNet step ~40 us of host time).  The two launches are graph-capturable (``step_device``):
+fp16 steps are captured like bf16 ones.  Optimizers that are not fused fall back to the torch primitives on the
 same device state.  ``state_dict`` uses ``torch.amp.GradScaler``'s format (``scaler.pt``
 checkpoints are interchangeable).
 """
@@ -27,9 +29,14 @@ from __future__ import annotations
 
 from typing import Optional
 
+import ctypes
+
 import torch
 
-SCALE, INV, FOUND, TRACKER, GROWTH, BACKOFF, INTERVAL, LAST = range(8)
+SCALE, INV, FOUND, TRACKER, GROWTH, BACKOFF, INTERVAL, LAST, SEQ = range(9)
+HOST = 10   # slots 10..11: device address of the host-mapped flag ring (int64 bits)
+SLOTS = 12  # optim_common.h kAmpSlots
+RING = 64   # optim_common.h kAmpRing
 
 
 class FusedGradScaler:
@@ -40,17 +47,42 @@ class FusedGradScaler:
         self._growth_factor = float(growth_factor)
         self._backoff_factor = float(backoff_factor)
         self._growth_interval = int(growth_interval)
-        self.state = torch.tensor([init_scale, 1.0 / init_scale, 0.0, 0.0, growth_factor, backoff_factor,
-                                   float(growth_interval), 0.0], dtype=torch.float32, device=self.device)
-        # the skip flag of recent steps: a small ring of pinned copies + their events, so a caller can
-        # hold the handle of step k while step k+1 records its own (EngineScheduler speculation)
-        pin = self.device.type == "cuda"
-        self._ring = [torch.zeros(1, dtype=torch.float32, pin_memory=pin) for _ in range(4)]
-        self._ring_ev = [torch.cuda.Event() for _ in range(4)] if pin else [None] * 4  # reused: no per-step event
-        self._ring_i = 0
-        self._last_host = self._ring[0]
-        self._last_event = None
+        self.state = torch.zeros(SLOTS, dtype=torch.float32, device=self.device)
+        self.state[:8].copy_(torch.tensor([init_scale, 1.0 / init_scale, 0.0, 0.0, growth_factor, backoff_factor,
+                                           float(growth_interval), 0.0]))
+        # the live scale as a fixed 1-element view (state is only ever updated in place): kernels
+        # that fold the loss scale into the gradient they seed read it from here
+        self.scale_tensor = self.state[SCALE : SCALE + 1] if enabled else None
+        # the skip flags of recent updates (a caller may hold the handle of update n while n+1
+        # publishes its own: EngineScheduler speculation): host-mapped on a HIP device, written by
+        # the update kernel; plain host memory elsewhere
+        self._ring_h = None
+        if self.device.type == "cuda":
+            from rocket_amd.ops import _lib
+
+            lib = _lib.kernels()
+            dev = ctypes.c_void_p()
+            with torch.cuda.device(self.device):
+                h = lib.rk_host_mapped_alloc(RING * 4, ctypes.byref(dev))
+            if not h:
+                raise RuntimeError("FusedGradScaler: rk_host_mapped_alloc failed")
+            self._ring_h = h
+            self._free = lib.rk_host_mapped_free
+            self._ring = (ctypes.c_int32 * RING).from_address(h)
+            self.state.view(torch.int64)[HOST // 2] = int(dev.value)
+        else:
+            self._ring = (ctypes.c_int32 * RING)()
+        self._seq = 0  # updates launched (host count; the device counts its own in state[SEQ])
         self._unscaled = set()  # id(optimizer) unscaled this step (clip_grad_norm_ path)
+
+    def __del__(self):
+        h, self._ring_h = getattr(self, "_ring_h", None), None
+        if h:
+            try:
+                torch.cuda.synchronize(self.device)  # no update may still write the ring
+                self._free(h)
+            except Exception:
+                pass
 
     # ------------------------------------------------------------------ API
     def is_enabled(self) -> bool:
@@ -110,7 +142,7 @@ class FusedGradScaler:
         skip = bool(self.state[FOUND].item())
         out = None if skip else optimizer.step(*args, **kwargs)
         self._update_host_side()
-        self._record_last()
+        self._record_last(host_flag=skip)
         return out
 
     def step_device(self, optimizer, zero_grads: bool = False) -> None:
@@ -143,28 +175,45 @@ class FusedGradScaler:
         self.state[LAST] = self.state[FOUND]
         self.state[FOUND] = 0.0
 
-    def _record_last(self) -> None:
+    def _record_last(self, host_flag=None) -> None:
+        """One update was launched (its kernel publishes the flag), or ran host side (``host_flag``:
+        its skip flag, published here, and the device count advanced to match)."""
         self._unscaled.clear()
-        self._ring_i = (self._ring_i + 1) % len(self._ring)
-        self._last_host = self._ring[self._ring_i]
-        self._last_host.copy_(self.state[LAST : LAST + 1], non_blocking=True)
-        self._last_event = self._ring_ev[self._ring_i]
-        if self._last_event is not None:
-            self._last_event.record()
+        self._seq += 1
+        if host_flag is not None:
+            u = ((self._seq << 1) | int(bool(host_flag))) & 0xFFFFFFFF  # as the kernel stores it
+            self._ring[self._seq % RING] = u - (1 << 32) if u >= (1 << 31) else u
+            self.state.view(torch.int32)[SEQ] += 1
+
+    def _entry(self, seq: int):
+        """The published skip flag of update ``seq``, or None (not yet written / overwritten)."""
+        u = self._ring[seq % RING] & 0xFFFFFFFF
+        return bool(u & 1) if (u >> 1) == (seq & 0x7FFFFFFF) else None
+
+    def _resolve(self, seq: int) -> bool:
+        f = self._entry(seq)
+        if f is not None:
+            return f
+        torch.cuda.synchronize(self.device)  # the update is enqueued: wait for it
+        f = self._entry(seq)
+        if f is not None:
+            return f
+        # the host and device counts disagree (an update ran outside record_last, or this handle
+        # is over RING updates old): realign on the device's count, answer with its latest flag
+        self._seq = int(self.state.view(torch.int32)[SEQ].item())
+        return bool(self.state[LAST].item() != 0)
 
     def last_handle(self):
-        """(pinned flag copy, event) of the last recorded step: resolve with :func:`handle_skipped`."""
-        return (self._last_host, self._last_event)
+        """Handle of the last launched update's skip flag: resolve with :func:`handle_skipped`."""
+        return (self, self._seq)
 
     @staticmethod
     def handle_ready(h) -> bool:
-        return h[1] is None or h[1].query()
+        return h[1] == 0 or h[0]._entry(h[1]) is not None
 
     @staticmethod
     def handle_skipped(h) -> bool:
-        if h[1] is not None:
-            h[1].synchronize()
-        return bool(h[0][0] != 0)
+        return False if h[1] == 0 else h[0]._resolve(h[1])
 
     def update(self, new_scale=None) -> None:
         """The scale update already ran on the device; ``new_scale`` overrides it."""
@@ -174,10 +223,8 @@ class FusedGradScaler:
             self.state[INV] = 1.0 / v
 
     def last_step_skipped(self) -> bool:
-        """Whether the last scaled step found inf/NaN gradients (waits for that step only)."""
-        if self._last_event is not None:
-            self._last_event.synchronize()
-        return bool(self._last_host[0] != 0)
+        """Whether the last scaled step found inf/NaN gradients (waits only if it has not run yet)."""
+        return self.handle_skipped(self.last_handle())
 
     def get_scale(self) -> float:
         return float(self.state[SCALE].item()) if self._enabled else 1.0
@@ -206,8 +253,8 @@ class FusedGradScaler:
         self._backoff_factor = float(sd["backoff_factor"])
         self._growth_interval = int(sd["growth_interval"])
         s = float(sd["scale"])
-        self.state.copy_(torch.tensor([s, 1.0 / s, 0.0, float(sd.get("_growth_tracker", 0)), self._growth_factor,
-                                       self._backoff_factor, float(self._growth_interval), 0.0]))
+        self.state[:8].copy_(torch.tensor([s, 1.0 / s, 0.0, float(sd.get("_growth_tracker", 0)), self._growth_factor,
+                                           self._backoff_factor, float(self._growth_interval), 0.0]))
 
 
 def make_scaler(device) -> Optional[object]:

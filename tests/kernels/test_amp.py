@@ -96,3 +96,31 @@ def test_torch_gradscaler_protocol_with_fused_optimizer():
     # rsqrt); Adam amplifies them on near-zero second moments: same bound as test_ce_optim at 10x lr
     for a, b in zip(ref.parameters(), mine.parameters()):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
+
+
+def test_skip_flags_published_to_host_ring():
+    """Each fused update's last block publishes its own skip flag into the host-mapped ring: once
+    the updates ran, every handle is readable with a plain host load (no copy, no event), and
+    handles of earlier steps still resolve to THEIR step's flag after later steps ran."""
+    from rocket_amd.ops.optim import FusedAdamW
+    from rocket_amd.runtime.amp import SEQ, FusedGradScaler
+
+    net = _model()
+    opt = FusedAdamW(net.parameters(), lr=1e-3)
+    sc = FusedGradScaler("cuda", init_scale=1024.0)
+    x = torch.randn(16, 32, device="cuda")
+    handles = []
+    for step in range(6):
+        with torch.autocast("cuda", dtype=torch.float16):
+            loss = net(x).float().pow(2).mean()
+        sc.scale(loss).backward()
+        if step in (1, 4):
+            next(net.parameters()).grad[0, 0] = float("inf")
+        sc.step(opt)
+        sc.update()
+        opt.zero_grad()
+        handles.append(sc.last_handle())
+    torch.cuda.synchronize()
+    assert all(FusedGradScaler.handle_ready(h) for h in handles)
+    assert [FusedGradScaler.handle_skipped(h) for h in handles] == [False, True, False, False, True, False]
+    assert int(sc.state.view(torch.int32)[SEQ]) == 6

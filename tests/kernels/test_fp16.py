@@ -259,3 +259,38 @@ def test_lenet_fp16_training_steps_track_fp32():
     assert l1[-1] < l1[0]
     for a, b in zip(l1, l2):
         assert abs(a - b) < 1e-2 * abs(b), (l1, l2)
+
+
+def _lenet_step_grads(net, x, t, dev_scale, spec):
+    from rocket_amd.ops.lenet import fuse_cross_entropy, lenet_forward
+
+    for p in net.parameters():
+        p.grad = None
+    with torch.autocast("cuda", dtype=H16):
+        y = lenet_forward(x, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3, t if spec else None)
+    launched = y.grad_fn.spec  # the speculative whole-step launch (None: forward-only launch)
+    loss, dummy = fuse_cross_entropy(y, t, 1.0, dev_scale=dev_scale)
+    torch.autograd.backward([y], [dummy])
+    used_spec = launched is not None and launched[8] is dev_scale
+    return float(loss), [p.grad.clone() for p in net.parameters()], used_spec
+
+
+@pytest.mark.parametrize("spec", [True, False])
+def test_lenet_fused_ce_device_loss_scale(spec):
+    """The fp16 scaler's loss scale folded into the fused LeNet cross-entropy (device tensor, read
+    in-kernel): gradients are S x the unscaled ones, the reported loss is unscaled — in both the
+    speculative whole-step launch and the separate backward launch."""
+    from rocket_amd.models import LeNet
+
+    torch.manual_seed(5)
+    net = LeNet(fused=False).cuda()
+    x = torch.rand(256, 1, 28, 28, device="cuda")
+    t = torch.randint(0, 10, (256,), device="cuda")
+    S = torch.tensor([1024.0], device="cuda")
+    l0, g0, _ = _lenet_step_grads(net, x, t, None, spec)
+    _lenet_step_grads(net, x, t, S, spec)  # primes the speculative launch with the device scale
+    l1, g1, used = _lenet_step_grads(net, x, t, S, spec)
+    assert used == spec
+    assert abs(l1 - l0) < 1e-5 * abs(l0)
+    for (name, _), a, b in zip(net.named_parameters(), g1, g0):
+        assert _rel(a / 1024.0, b) < 1e-2, (name, _rel(a / 1024.0, b))

@@ -185,11 +185,25 @@ def test_batchnorm_relu_maxpool(dtype, shape):
     assert _rel(bn.bias.grad, b.grad) < gtol
 
 
+def _set_grads(params, direct):
+    """Fresh gradients: None, or persistent fp32 .grad buffers the kernels accumulate into (the
+    engine's direct-gradient mode), pre-filled so accumulation (not overwrite) is checked."""
+    for p in params:
+        if direct:
+            p.grad = torch.full(p.shape, 0.25, dtype=torch.float32, device=p.device)
+            p._rocket_direct_grad = True
+        else:
+            p.grad = None
+            p._rocket_direct_grad = False
+
+
+@pytest.mark.parametrize("direct", [False, True])
 @pytest.mark.parametrize("mlp", [False, True])
-def test_add_ln_forms_branch_bias_grad(mlp):
+def test_add_ln_forms_branch_bias_grad(mlp, direct):
     """A linear branch (MLinear / MMlp) feeding a fused add-LayerNorm: the LN backward forms the
     branch's bias gradient (column sums of dr, BiasLink) and the linear skips its own pass; all
-    gradients equal the stock-torch composition."""
+    gradients equal the stock-torch composition.  direct: persistent fp32 grads, where the LN
+    kernel adds the sums into bias.grad itself."""
     import rocket_amd.ops as ops
     import rocket_amd.ops.mlinear as ml
     from rocket_amd.ops.norm import FusedLayerNorm
@@ -210,8 +224,7 @@ def test_add_ln_forms_branch_bias_grad(mlp):
     for fused in (True, False):
         ops.set_fused(fused)
         try:
-            for p in list(branch.parameters()) + list(ln.parameters()):
-                p.grad = None
+            _set_grads(list(branch.parameters()) + list(ln.parameters()), direct)
             hits = ml.BIAS_LINK_HITS
             x, h = x0.clone().requires_grad_(), h0.clone().requires_grad_()
             with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -229,10 +242,12 @@ def test_add_ln_forms_branch_bias_grad(mlp):
     assert _rel(hn, ht) < 3e-2 and _rel(xn, xt) < 3e-2
 
 
-def test_bias_link_refused_with_second_consumer():
+@pytest.mark.parametrize("direct", [False, True])
+def test_bias_link_refused_with_second_consumer(direct):
     """The linear's output feeds the add-LayerNorm AND another op: the incoming gradient is dr plus
     that op's gradient, so the LN's column sums of dr are not the bias gradient.  The link must be
-    refused (no hit) and the bias gradient must still equal the stock-torch composition."""
+    refused (no hit) and the bias gradient must still equal the stock-torch composition (direct:
+    the sums the LN kernel already added into bias.grad are backed out)."""
     import rocket_amd.ops as ops
     import rocket_amd.ops.mlinear as ml
     from rocket_amd.ops.norm import FusedLayerNorm
@@ -251,8 +266,7 @@ def test_bias_link_refused_with_second_consumer():
     for fused in (True, False):
         ops.set_fused(fused)
         try:
-            for p in list(branch.parameters()) + list(ln.parameters()):
-                p.grad = None
+            _set_grads(list(branch.parameters()) + list(ln.parameters()), direct)
             hits = ml.BIAS_LINK_HITS
             x, h = x0.clone().requires_grad_(), h0.clone().requires_grad_()
             with torch.autocast("cuda", dtype=torch.bfloat16):

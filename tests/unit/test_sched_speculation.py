@@ -7,15 +7,19 @@ import torch
 from rocket_amd.runtime.engine import EngineOptimizer, EngineScheduler
 
 
-class _Ev:
-    def __init__(self):
-        self.done = False
+class _Flags:
+    """Stands in for FusedGradScaler's published skip flags (handle = (scaler, update number))."""
 
-    def query(self):
-        return self.done
+    def __init__(self, skipped: bool):
+        self.skipped = skipped
+        self.done = False  # published yet
 
-    def synchronize(self):
-        self.done = True
+    def _entry(self, seq):
+        return self.skipped if self.done else None
+
+    def _resolve(self, seq):
+        self.done = True  # (the real one waits for the update)
+        return self.skipped
 
 
 class _Eng:
@@ -25,7 +29,7 @@ class _Eng:
 
 
 def _flag(skipped: bool):
-    return (torch.tensor([1.0 if skipped else 0.0]), _Ev())
+    return (_Flags(skipped), 1)
 
 
 def test_speculated_step_kept_and_mispredicted_step_rolled_back():
@@ -53,7 +57,7 @@ def test_landed_flag_takes_the_exact_path():
     eo = EngineOptimizer(opt, _Eng())
     sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5), [eo], _Eng())
     h = _flag(True)
-    h[1].done = True
+    h[0].done = True
     eo._skip_lazy, eo._lazy_handle = True, h
     sch.step()  # flag available: the skipped step does not advance the schedule
     assert opt.param_groups[0]["lr"] == 1.0 and sch._pending is None
