@@ -233,7 +233,15 @@ class Optimizer(Capsule):
             # gradient launch) then applies the update itself; see _FusedBase.epilogue.
             inner.epilogue_armed = (engine.sync_gradients and engine.num_processes == 1 and engine.scaler is None
                                     and os.environ.get("ROCKET_OPT_EPILOGUE", "1") != "0")
-            if inner.epilogue_armed and not getattr(self, "_epi_tagged", False):
+            # under the device fp16 scaler the same producer can instead flag non-finite gradients
+            # itself (the step's separate check launch is then skipped; see _FusedBase.amp_checked):
+            # exact when its gradients are final and local ones are all there is (one replica)
+            from rocket_amd.runtime.amp import FusedGradScaler
+
+            inner.amp_fold_armed = (engine.sync_gradients and engine.num_processes == 1
+                                    and isinstance(engine.scaler, FusedGradScaler)
+                                    and os.environ.get("ROCKET_OPT_EPILOGUE", "1") != "0")
+            if (inner.epilogue_armed or inner.amp_fold_armed) and not getattr(self, "_epi_tagged", False):
                 for g in inner.param_groups:
                     for p in g["params"]:
                         p._rocket_optimizer = inner
@@ -258,6 +266,8 @@ class Optimizer(Capsule):
         inner = self._optimizer.optimizer
         if getattr(inner, "epilogue_armed", False):
             inner.epilogue_armed = False
+        if getattr(inner, "amp_fold_armed", False):
+            inner.amp_fold_armed = False
         scaler = self._accelerator.scaler
         if scaler is not None and self._accelerator.sync_gradients:
             # the skipped-step flag of the replayed update: copied behind it, read only if asked

@@ -307,7 +307,14 @@ struct WgradArgs {
   // optional optimizer epilogue: records of the 3 dW / 3 db / 4 slab destinations' parameters
   rk_opt::AdamEpi epi;
   rk_opt::TensorRec rdw[3], rdb[3], rsl[4];
+  // fp16 AMP (may be null): any non-finite gradient this launch writes sets *amp_found = 1 (the
+  // loss scaler's found-inf slot), so the step needs no separate check launch
+  float* amp_found;
 };
+
+__device__ __forceinline__ void flag_nonfinite(float* found, float v) {
+  if (found && !__builtin_isfinite(v)) *found = 1.f;  // same value from any lane: benign race
+}
 
 
 
@@ -424,6 +431,7 @@ __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, flo
     t *= sf.gs();
     if (ks) rk_opt::epi_apply(a.rsl[di], ks[a.rsl[di].group], c - s.bound[di], ee, old + t, a.epi.zero_grads);
     else *dst = old + t;
+    flag_nonfinite(a.amp_found, old + t);
   }
 }
 
@@ -562,6 +570,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
       const int64_t i = (int64_t)(n0 + r) * P.K + k0 + c;
       if (ks) rk_opt::epi_apply(a.rdw[pi], ks[a.rdw[pi].group], i, ew[q], dw_old[q] + v, a.epi.zero_grads);
       else P.dw[i] = dw_old[q] + v;
+      flag_nonfinite(a.amp_found, dw_old[q] + v);
     }
   }
   if (has_db) {
@@ -571,6 +580,7 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     v *= gsc;
     if (ks) rk_opt::epi_apply(a.rdb[pi], ks[a.rdb[pi].group], n0 + threadIdx.x, eb, db_old + v, a.epi.zero_grads);
     else P.db[n0 + threadIdx.x] = db_old + v;
+    flag_nonfinite(a.amp_found, db_old + v);
   }
 }
 
@@ -586,6 +596,12 @@ struct RowsReq {
   int n_cur, bs;
 };
 static thread_local RowsReq g_rows{};
+// Likewise the NEXT rk_mlp3_wgrad_loss flags non-finite gradients into *found (WgradArgs::amp_found).
+static thread_local float* g_amp_found = nullptr;
+RK_API int RKL_NAME(rk_mlp3_set_amp_found)(float* found) {
+  g_amp_found = found;
+  return 0;
+}
 RK_API int RKL_NAME(rk_mlp3_set_rows)(const int64_t* table, int64_t* meta, int64_t* rows, int n_cur, int bs) {
   if (!table || !meta || !rows || n_cur < 0 || bs < 1) return (int)hipErrorInvalidValue;
   g_rows = RowsReq{table, meta, rows, n_cur, bs};
@@ -659,10 +675,13 @@ RK_API int RKL_NAME(rk_mlp3_wgrad_loss)(int nprob, const void* const* dT, const 
   // cleared first, so an argument error below cannot leave it attached to a later launch
   const RowsReq rows_req = g_rows;
   g_rows = RowsReq{};
+  float* const amp_found = g_amp_found;
+  g_amp_found = nullptr;
   if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
   WgradArgs a{};
   a.trace = g_wgrad_trace;
   a.gscale = gscale;
+  a.amp_found = amp_found;
   if (norm_by_count) {  // count partials follow the loss partials: partials[nparts .. 2 nparts)
     if (!loss) return (int)hipErrorInvalidValue;
     a.cnt_parts = loss->partials + loss->nparts;

@@ -117,6 +117,7 @@ KERNEL_SIGS = {
     "rk_gather_set_trace": (None, [c_void_p]),
     "rk_rows_next": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "rk_mlp3_set_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
+    "rk_mlp3_set_amp_found": (c_int, [c_void_p]),
     "rk_gap_stamp_big": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "rk_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_float,
                             c_void_p]),
@@ -147,7 +148,8 @@ KERNEL_SIGS = {
 # fp16 builds of the fused LeNet kernels (lenet_conv_h.hip / mlp_h.hip): same signatures
 KERNEL_SIGS.update({n + "_h": KERNEL_SIGS[n] for n in (
     "rk_lenet_conv_fwd", "rk_lenet_conv_bwd", "rk_lenet_prep", "rk_lenet_fwd", "rk_lenet_bwd", "rk_lenet_train",
-    "rk_mlp3_fwd", "rk_mlp3_dgrad", "rk_mlp3_wgrad", "rk_mlp3_wgrad_loss", "rk_mlp3_set_rows")})
+    "rk_mlp3_fwd", "rk_mlp3_dgrad", "rk_mlp3_wgrad", "rk_mlp3_wgrad_loss", "rk_mlp3_set_rows",
+    "rk_mlp3_set_amp_found")})
 
 
 class NativeError(RuntimeError):

@@ -253,8 +253,10 @@ class LeNetFragments:
         self.params = None
         self.spec_misses = 0
         # the device loss scale (fp16 AMP) the last fused cross-entropy multiplied d(logits) by;
-        # the speculative forward launch applies the same one
+        # the speculative forward launch applies the same one (before any fused cross-entropy:
+        # the live fp16 scaler's, runtime/amp.py active_loss_scale)
         self.dev_scale = None
+        self.dev_scale_known = False
 
     @property
     def spec_ok(self) -> bool:
@@ -414,7 +416,12 @@ class _LeNetFused(torch.autograd.Function):
             slab = torch.empty(N // 4, int(lib.rk_lenet_slab_width()), dtype=torch.float32, device=dev)
             partials = torch.empty(2 * (N // 4), dtype=torch.float32, device=dev)  # loss sums, valid counts
             loss_out = torch.empty(2, dtype=torch.float32, device=dev)
-            dscale = frags.dev_scale
+            if frags.dev_scale_known:
+                dscale = frags.dev_scale
+            else:
+                from rocket_amd.runtime.amp import active_loss_scale
+
+                dscale = active_loss_scale(dev)
             ce = _LenetCE(logits.data_ptr(), target.data_ptr(), -100, 1.0, partials.data_ptr(),
                           _lib.Workspace.get(dev).counter("lenet_ce"), loss_out.data_ptr(), None, None, None, 0,
                           0.0, 0, 1, _lib.ptr(dscale))
@@ -453,13 +460,13 @@ class _LeNetFused(torch.autograd.Function):
         dev = x.device
         stream = _lib.stream_ptr(dev)
         rounds = 1  # one block per 4 samples (the kernel keeps no state across sample groups)
-        ce, keep, fin = None, None, None
+        ce, keep, fin, dev_scale = None, None, None, None
         spec, ctx.spec = ctx.spec, None
         gscale = 1.0
         if ctx.ce_spec is not None and spec is not None and _spec_matches(spec, ctx.ce_spec[0], ctx.ce_spec[4]):
             # the forward launch already ran this loss's backward for a unit upstream gradient
             # (times the same device loss scale)
-            target, grad_scale, accum, loss_out, _ = ctx.ce_spec
+            target, grad_scale, accum, loss_out, dev_scale = ctx.ce_spec
             ctx.ce_spec = None
             _, _, dyT, d2T, d1T, slab, partials, _, _ = spec
             acc = ring = slot = None
@@ -471,7 +478,8 @@ class _LeNetFused(torch.autograd.Function):
                            _lib.ptr(slot), ring.numel() if ring is not None else 0, float(acc_scale), int(sync))
             gscale = float(grad_scale)
             ctx.frags.spec_misses = 0
-            return _LeNetFused._wgrad(ctx, lib, N, dev, stream, dyT, d2T, d1T, a2T, h1T, h2T, slab, fin, gscale, keep)
+            return _LeNetFused._wgrad(ctx, lib, N, dev, stream, dyT, d2T, d1T, a2T, h1T, h2T, slab, fin, gscale, keep,
+                                      dev_scale)
         if spec is not None:
             ctx.frags.spec_misses += 1  # the loss was not the fused cross-entropy on those targets
         if ctx.ce_spec is not None:
@@ -502,11 +510,13 @@ class _LeNetFused(torch.autograd.Function):
                                     frag.data_ptr(), dy.data_ptr(), h1T.data_ptr(), h2T.data_ptr(), dyT.data_ptr(),
                                     d2T.data_ptr(), d1T.data_ptr(), slab.data_ptr(), N, rounds,
                                     ctypes.byref(ce) if ce is not None else None, stream), "rk_lenet_bwd")
-        return _LeNetFused._wgrad(ctx, lib, N, dev, stream, dyT, d2T, d1T, a2T, h1T, h2T, slab, fin, gscale, keep)
+        return _LeNetFused._wgrad(ctx, lib, N, dev, stream, dyT, d2T, d1T, a2T, h1T, h2T, slab, fin, gscale, keep,
+                                  dev_scale)
 
     @staticmethod
-    def _wgrad(ctx, lib, N, dev, stream, dyT, d2T, d1T, a2T, h1T, h2T, slab, fin, gscale, keep):
-        """The grouped weight-gradient launch (+ loss finalisation, + the armed optimizer's update)."""
+    def _wgrad(ctx, lib, N, dev, stream, dyT, d2T, d1T, a2T, h1T, h2T, slab, fin, gscale, keep, dev_scale=None):
+        """The grouped weight-gradient launch (+ loss finalisation, + the armed optimizer's update,
+        or under the device fp16 scaler the non-finite check of the gradients it writes)."""
         params = ctx.params
         half = ctx.frags.half
         bufs, direct = _grad_targets(params, dev)
@@ -519,6 +529,14 @@ class _LeNetFused(torch.autograd.Function):
         assert sum(sizes) == int(lib.rk_lenet_slab_cols()), "fused LeNet expects conv1 6x1x5x5 / conv2 16x6x5x5"
         bounds = (ctypes.c_int * 5)(0, sizes[0], sizes[0] + sizes[1], sizes[0] + sizes[1] + sizes[2], sum(sizes))
         epi, opt = _optimizer_epilogue(params, direct)
+        amp_opt = None
+        amp_state = getattr(dev_scale, "_rocket_amp_state", None) if dev_scale is not None else None
+        if epi is None and amp_state is not None and direct:
+            o = getattr(params[4], "_rocket_optimizer", None)
+            if o is not None and o.amp_fold_target(params):
+                amp_opt = o
+                found = amp_state[2:3]  # runtime/amp.py FOUND
+                _lib.check(_k(lib, "rk_mlp3_set_amp_found", half)(found.data_ptr()), "rk_mlp3_set_amp_found")
         pend, ctx.rows_pend = getattr(ctx, "rows_pend", None), None
         rows_staged = pend is not None and not pend.advanced
         if rows_staged:  # the step's batch cursor, as one more block of this launch
@@ -536,6 +554,8 @@ class _LeNetFused(torch.autograd.Function):
             pend.mark_advanced()  # only once the launch that advances the cursor was accepted
         if opt is not None:
             opt.epilogue_done = True  # the optimizer's own launch for this step is skipped
+        if amp_opt is not None:
+            amp_opt.amp_checked = True  # the scaler skips its check launch for this step
         del keep  # partials: read by the wgrad launch (stream-ordered before any reuse)
         return (None, *_finish(params, bufs, direct), None, None)
 
@@ -570,6 +590,7 @@ def fuse_cross_entropy(logits, target, grad_scale: float, accum=None, dev_scale=
     frags = getattr(fn, "frags", None)
     if frags is not None:
         frags.dev_scale = dev_scale  # the next speculative forward scales d(logits) the same way
+        frags.dev_scale_known = True
     if spec is not None and _spec_matches(spec, target, dev_scale):
         loss_out = spec[7]  # the speculative forward launch already wrote this loss's partials
     else:

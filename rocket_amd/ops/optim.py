@@ -268,6 +268,18 @@ class _FusedBase(torch.optim.Optimizer):
     # with ``epilogue(params)``, reports ``epilogue_done``, and the step's own launch is skipped.
     epilogue_armed = False
     epilogue_done = False
+    # fp16 AMP: a producer of ALL the active parameters' final (fp32) gradients may flag non-finite
+    # values into the scaler's found slot itself when armed (``amp_fold_target``); it then sets
+    # ``amp_checked`` and the scaler skips this step's check launch
+    amp_fold_armed = False
+    amp_checked = False
+
+    def amp_fold_target(self, params) -> bool:
+        """True when the fold is armed and ``params`` are exactly the active parameters (fp32 grads)."""
+        if not (self.amp_fold_armed and self._tables is not None and self._gdtype == 0):
+            return False
+        active = self._active()
+        return len(active) == len(params) and {id(p) for _, p in active} == {id(p) for p in params}
 
     def epilogue(self, params) -> Optional[tuple]:
         """``(ngroups, hyper_ptr, step_ptr, counter_ptr, records)`` when ``params`` are exactly this

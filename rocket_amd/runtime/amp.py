@@ -30,6 +30,7 @@ from __future__ import annotations
 from typing import Optional
 
 import ctypes
+import weakref
 
 import torch
 
@@ -37,6 +38,18 @@ SCALE, INV, FOUND, TRACKER, GROWTH, BACKOFF, INTERVAL, LAST, SEQ = range(9)
 HOST = 10   # slots 10..11: device address of the host-mapped flag ring (int64 bits)
 SLOTS = 12  # optim_common.h kAmpSlots
 RING = 64   # optim_common.h kAmpRing
+
+
+_ACTIVE = {}  # device -> weakref of the last enabled FusedGradScaler created on it
+
+
+def active_loss_scale(device) -> Optional[torch.Tensor]:
+    """The live loss-scale tensor of the last enabled FusedGradScaler on ``device`` (or None): what a
+    kernel that folds the loss scale into the gradient it seeds should assume before its loss says
+    otherwise (the fused LeNet's speculative whole-step launch)."""
+    ref = _ACTIVE.get(torch.device(device))
+    sc = ref() if ref is not None else None
+    return sc.scale_tensor if sc is not None else None
 
 
 class FusedGradScaler:
@@ -53,6 +66,11 @@ class FusedGradScaler:
         # the live scale as a fixed 1-element view (state is only ever updated in place): kernels
         # that fold the loss scale into the gradient they seed read it from here
         self.scale_tensor = self.state[SCALE : SCALE + 1] if enabled else None
+        if self.scale_tensor is not None:
+            self.scale_tensor._rocket_amp_state = self.state  # consumers that also flag found-inf
+            if self.device.type == "cuda":
+                idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+                _ACTIVE[torch.device("cuda", idx)] = weakref.ref(self)
         # the skip flags of recent updates (a caller may hold the handle of update n while n+1
         # publishes its own: EngineScheduler speculation): host-mapped on a HIP device, written by
         # the update kernel; plain host memory elsewhere
@@ -126,7 +144,8 @@ class FusedGradScaler:
                 self._unscaled.discard(id(optimizer))
                 raise AssertionError("No inf checks were recorded for this optimizer.")
             if not unscaled:
-                optimizer.amp_check(self.state)
+                if not self._producer_checked(optimizer):
+                    optimizer.amp_check(self.state)
             else:  # unscaled in place (and checked) already: unscale by 1 this time; the last
                 self.state[INV] = 1.0  # block restores 1/scale with the scale update
             optimizer.amp = self.state
@@ -149,7 +168,8 @@ class FusedGradScaler:
         """The device part of a fused scaled step (flag check + update with in-kernel unscale and
         scale rule): graph-capturable; ``record_last`` after the replay publishes the skip flag."""
         if id(optimizer) not in self._unscaled:
-            optimizer.amp_check(self.state)
+            if not self._producer_checked(optimizer):
+                optimizer.amp_check(self.state)
         else:
             self.state[INV] = 1.0
         optimizer.amp = self.state
@@ -158,6 +178,15 @@ class FusedGradScaler:
         finally:
             optimizer.amp = None
         self._unscaled.clear()
+
+    @staticmethod
+    def _producer_checked(optimizer) -> bool:
+        """The gradients' producer already flagged non-finite values into state[FOUND] (the fused
+        LeNet weight-gradient launch: _FusedBase.amp_fold_target); consumes the mark."""
+        done = getattr(optimizer, "amp_checked", False)
+        if done:
+            optimizer.amp_checked = False
+        return done
 
     def record_last(self) -> None:
         self._record_last()

@@ -294,3 +294,48 @@ def test_lenet_fused_ce_device_loss_scale(spec):
     assert abs(l1 - l0) < 1e-5 * abs(l0)
     for (name, _), a, b in zip(net.named_parameters(), g1, g0):
         assert _rel(a / 1024.0, b) < 1e-2, (name, _rel(a / 1024.0, b))
+
+
+def test_lenet_wgrad_flags_nonfinite_for_scaler():
+    """Under the device fp16 scaler the LeNet weight-gradient launch flags non-finite gradients
+    into the scaler's found slot itself (armed fold, persistent grads): the scaler skips its check
+    launch, a clean step updates, a poisoned (inf input) step is skipped with the weights kept."""
+    from rocket_amd.models import LeNet
+    from rocket_amd.ops.lenet import fuse_cross_entropy, lenet_forward
+    from rocket_amd.ops.optim import FusedAdamW
+    from rocket_amd.runtime.amp import FusedGradScaler
+
+    torch.manual_seed(6)
+    net = LeNet(fused=False).cuda()
+    params = list(net.parameters())
+    opt = FusedAdamW(params, lr=1e-3)
+    sc = FusedGradScaler("cuda", init_scale=1024.0)
+    for p in params:
+        p.grad = torch.zeros_like(p)
+        p._rocket_direct_grad = True
+        p._rocket_optimizer = opt
+    opt.prepare()
+    x = torch.rand(256, 1, 28, 28, device="cuda")
+    t = torch.randint(0, 10, (256,), device="cuda")
+    checks = []
+    orig = opt.amp_check
+    opt.amp_check = lambda amp: (checks.append(1), orig(amp))
+    skipped = []
+    for poison in (False, True):
+        xb = x.clone()
+        if poison:
+            xb[3, 0, 10, 10] = float("inf")
+        before = [p.detach().clone() for p in params]
+        opt.amp_fold_armed = True
+        with torch.autocast("cuda", dtype=H16):
+            y = lenet_forward(xb, net.conv1, net.conv2, net.fc1, net.fc2, net.fc3, t)
+        _, dummy = fuse_cross_entropy(y, t, 1.0, dev_scale=sc.scale_tensor)
+        torch.autograd.backward([y], [dummy])
+        assert opt.amp_checked  # the wgrad launch took the check over
+        sc.step(opt, zero_grads=True)
+        opt.amp_fold_armed = False
+        skipped.append(sc.last_step_skipped())
+        changed = any(not torch.equal(a, p.detach()) for a, p in zip(before, params))
+        assert changed != poison
+    assert skipped == [False, True] and not checks
+    assert sc.get_scale() == 512.0
