@@ -443,11 +443,24 @@ __global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const T* __restri
 // (mask[r][cv], bit k = channel 8cv + k): the backward reads 1 byte per 8 elements instead of y.
 // RES: the residual input is a template flag, not a run-time test per element (a conditional load
 // in the unrolled row loop makes hipcc wait for each load on its own: vmcnt(0) per element)
-template <typename T, typename TO, bool RES>
+// Addresses: the block's rows start at a wave-uniform (SGPR) base; each lane adds a 32-bit byte
+// offset (host check: rpb * C * 4 < 2^32), so every load / store is the saddr form with no 64-bit
+// address arithmetic per row (64-bit per-row index math left these passes instruction-bound at
+// ~3.6 TB/s, profiles/r3_pmc_resnet50.md).
+template <typename T>
+__device__ __forceinline__ T* at_b(T* base, uint32_t e) {
+  return (T*)((char*)base + e * (uint32_t)sizeof(T));
+}
+template <typename T>
+__device__ __forceinline__ const T* at_b(const T* base, uint32_t e) {
+  return (const T*)((const char*)base + e * (uint32_t)sizeof(T));
+}
+
+template <typename T, typename TO, bool RES, bool RELU>
 __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x, const TO* __restrict__ res,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
                                                         TO* __restrict__ y, uint8_t* __restrict__ mask, int64_t R,
-                                                        int C, int relu, int rpb) {
+                                                        int C, int rpb) {
   const int CV = C >> 3, RPP = BN_T / CV;
   if ((int)threadIdx.x >= RPP * CV) return;
   const int cv = threadIdx.x % CV, c = cv * 8;
@@ -458,14 +471,18 @@ __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x,
     B[k] = shift[c + k];
   }
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
-  const int64_t r1 = min(R, r0 + rpb);
-  for (int64_t r = r0 + threadIdx.x / CV; r < r1; r += BN_U * RPP) {
+  const int nr = (int)(min(R, r0 + rpb) - r0);
+  const T* xb = x + r0 * C;
+  const TO* qb = RES ? res + r0 * C : res;
+  TO* yb = y + r0 * C;
+  uint8_t* mb = mask ? mask + r0 * (C >> 3) : mask;
+  for (int r = threadIdx.x / CV; r < nr; r += BN_U * RPP) {
     float v[BN_U][8], q[BN_U][8];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
-      const int64_t ru = min(r + u * RPP, r1 - 1);
-      V8<T>::load(x + ru * C + c, v[u]);
-      if constexpr (RES) V8<TO>::load(res + ru * C + c, q[u]);
+      const uint32_t e = (uint32_t)min(r + u * RPP, nr - 1) * (uint32_t)C + (uint32_t)c;
+      V8<T>::load(at_b(xb, e), v[u]);
+      if constexpr (RES) V8<TO>::load(at_b(qb, e), q[u]);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -474,15 +491,16 @@ __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x,
       for (int k = 0; k < 8; ++k) {
         float o = v[u][k] * A[k] + B[k];
         if constexpr (RES) o += q[u][k];
-        if (relu) {
+        if constexpr (RELU) {
           o = fmaxf(o, 0.f);
           m |= (o > 0.f ? 1u : 0u) << k;
         }
         v[u][k] = o;
       }
-      if (r + u * RPP < r1) {
-        V8<TO>::store(y + (r + u * RPP) * C + c, v[u]);
-        if (mask) mask[(r + u * RPP) * CV + cv] = (uint8_t)m;
+      const int ru = r + u * RPP;
+      if (ru < nr) {
+        V8<TO>::store(at_b(yb, (uint32_t)ru * (uint32_t)C + (uint32_t)c), v[u]);
+        if (RELU && mb) mb[(uint32_t)ru * (uint32_t)CV + (uint32_t)cv] = (uint8_t)m;
       }
     }
   }
@@ -640,28 +658,36 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(const TO* __restrict
     S[k] = coef[2 * C + c + k];
   }
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
-  const int64_t r1 = min(R, r0 + rpb);
-  for (int64_t r = r0 + threadIdx.x / CV; r < r1; r += BN_U * RPP) {
+  const int nr = (int)(min(R, r0 + rpb) - r0);
+  const TO* gb = dy + r0 * C;
+  const T* xb = x + r0 * C;
+  T* dxb = dx + r0 * C;
+  TO* drb = dres ? dres + r0 * C : dres;
+  const uint8_t* mkb = mask ? mask + r0 * CV : mask;
+  for (int r = threadIdx.x / CV; r < nr; r += BN_U * RPP) {
     float g[BN_U][8], xv[BN_U][8];
     unsigned mb[BN_U];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
-      const int64_t ru = min(r + u * RPP, r1 - 1);
-      V8<TO>::load(dy + ru * C + c, g[u]);
-      V8<T>::load(x + ru * C + c, xv[u]);
-      mb[u] = mask ? mask[ru * CV + cv] : 0xFFu;
+      const uint32_t ru = (uint32_t)min(r + u * RPP, nr - 1);
+      const uint32_t e = ru * (uint32_t)C + (uint32_t)c;
+      V8<TO>::load(at_b(gb, e), g[u]);
+      V8<T>::load(at_b(xb, e), xv[u]);
+      mb[u] = mkb ? mkb[ru * (uint32_t)CV + (uint32_t)cv] : 0xFFu;
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
-      if (mask) {
+      if (mkb) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) g[u][k] = ((mb[u] >> k) & 1u) ? g[u][k] : 0.f;
       }
-      const bool ok = r + u * RPP < r1;
-      if (ok && dres) V8<TO>::store(dres + (r + u * RPP) * C + c, g[u]);
+      const int ru = r + u * RPP;
+      const bool ok = ru < nr;
+      const uint32_t e = (uint32_t)ru * (uint32_t)C + (uint32_t)c;
+      if (ok && drb) V8<TO>::store(at_b(drb, e), g[u]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) xv[u][k] = P[k] * g[u][k] + Q[k] * xv[u][k] + S[k];
-      if (ok) V8<T>::store(dx + (r + u * RPP) * C + c, xv[u]);
+      if (ok) V8<T>::store(at_b(dxb, e), xv[u]);
     }
   }
 }
@@ -1174,6 +1200,8 @@ static int bn_elem_rows(int64_t R, int C, int* grid) {
   *grid = (int)((R + per - 1) / per);
   return (int)per;
 }
+// the elementwise passes' per-block 32-bit byte offsets (at_b) must not wrap
+static bool bn_elem_ok(int rpb, int C) { return (int64_t)rpb * C * 4 < (1ll << 32); }
 
 // out[c] += sum_r x[r][c]  (x: [R][C], dt f32 / bf16 / f16, C % 8 == 0); ws: rk_bn_workspace(R, C)
 // floats, counters: rk_bn_counters(C) zeroed uints (self-resetting)
@@ -1222,14 +1250,20 @@ RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const fl
   if (C % 8 || C > 8 * BN_T || R <= 0) return (int)hipErrorInvalidValue;
   int grid;
   const int rpb = bn_elem_rows(R, C, &grid);
-#define RK_BA(T, TO)                                                                                            \
+  if (!bn_elem_ok(rpb, C)) return (int)hipErrorInvalidValue;
+#define RK_BA2(T, TO, RES)                                                                                      \
   do {                                                                                                          \
-    if (res)                                                                                                    \
-      bn_apply_kernel<T, TO, true><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y,    \
-                                                         relu ? (uint8_t*)mask : nullptr, R, C, relu, rpb);    \
+    if (relu)                                                                                                   \
+      bn_apply_kernel<T, TO, RES, true><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y, \
+                                                              (uint8_t*)mask, R, C, rpb);                       \
     else                                                                                                        \
-      bn_apply_kernel<T, TO, false><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y,   \
-                                                          relu ? (uint8_t*)mask : nullptr, R, C, relu, rpb);   \
+      bn_apply_kernel<T, TO, RES, false><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift,       \
+                                                               (TO*)y, nullptr, R, C, rpb);                     \
+  } while (0)
+#define RK_BA(T, TO)              \
+  do {                            \
+    if (res) RK_BA2(T, TO, true); \
+    else RK_BA2(T, TO, false);    \
   } while (0)
   if (dt == F16 && dto == F16) RK_BA(f16_t, f16_t);
   else if (dt == F16 && dto == F32) RK_BA(f16_t, float);
@@ -1238,6 +1272,7 @@ RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const fl
   else if (dto == BF16) RK_BA(float, uint16_t);
   else RK_BA(float, float);
 #undef RK_BA
+#undef RK_BA2
   return (int)hipGetLastError();
 }
 
@@ -1253,6 +1288,7 @@ RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void*
   dim3 grid((C + BN_CT - 1) / BN_CT, rb);
   int eg;
   const int erpb = bn_elem_rows(R, C, &eg);
+  if (!bn_elem_ok(erpb, C)) return (int)hipErrorInvalidValue;
 #define RK_BB(T, TO)                                                                                               \
   do {                                                                                                             \
     bn_bwd_reduce_kernel<T, TO><<<grid, BN_T, 0, s>>>(a);                                                          \
@@ -1291,6 +1327,7 @@ RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, co
   bn_bwd_finalize_kernel<<<grid, BN_T, 0, s>>>(a, tp, ntiles);
   int eg;
   const int erpb = bn_elem_rows(R, C, &eg);
+  if (!bn_elem_ok(erpb, C)) return (int)hipErrorInvalidValue;
 #define RK_BP(T, TO)                                                                                      \
   bn_bwd_apply_kernel<T, TO><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x, nullptr, coef, (T*)dx, (TO*)dres, R, C, \
                                                  erpb)
