@@ -152,3 +152,29 @@ def test_fp16_step_is_captured_and_matches_eager(tmp_path):
     assert runs[True][2] == runs[False][2]
     for a, b in zip(runs[False][0], runs[True][0]):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
+
+
+def test_fp16_fused_lenet_captured_steps(tmp_path):
+    """fp16 fused LeNet under the engine: captured steps run the speculative whole-step launch with
+    the device loss scale and take the non-finite check from the weight-gradient launch (no check
+    launch once captured), and end within Adam-rounding distance of the same run with capture off
+    (plain loss kernel, separate check launch every step)."""
+    from rocket_amd.ops.optim import FusedAdamW
+
+    data = _data(2048)
+    runs = {}
+    for capture in (False, True):
+        torch.manual_seed(0)
+        net = LeNet()
+        opt = FusedAdamW(net.parameters(), lr=1e-3)
+        checks = []
+        orig = opt.amp_check
+        opt.amp_check = lambda amp, _o=orig: (checks.append(1), _o(amp))
+        _tree(tmp_path / str(capture), data, net, opt, mp="fp16", capture=capture, epochs=2).launch()
+        runs[capture] = ([p.detach().clone() for p in net.parameters()], len(checks))
+    assert runs[False][1] == 2 * 2048 // 256  # eager: one check launch per optimizer step
+    assert runs[True][1] <= 2  # captured: only the eager warm-up steps launch it
+    for a, b in zip(runs[False][0], runs[True][0]):
+        d = (a - b).abs()
+        assert d.max().item() <= 2e-2, d.max().item()
+        assert (d > 1e-3).float().mean().item() < 0.05, (d > 1e-3).float().mean().item()
