@@ -23,7 +23,9 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops.iconv import IConv2d, conv_entry, stem_ok
+from rocket_amd.ops.linear import LibLinear, native_route
 from rocket_amd.ops.norm import BatchNormAct2d
+from rocket_amd.ops.pool import global_avg_pool
 
 
 def _conv(cin, cout, k, stride=1):
@@ -100,7 +102,10 @@ class ResNet(nn.Module):
                 cin = width * block.expansion
             stages.append(nn.Sequential(*blocks))
         self.layer1, self.layer2, self.layer3, self.layer4 = stages
-        self.fc = nn.Linear(cin, num_classes)
+        # nn.Linear on the library GEMM with an optimizer-kept 16-bit weight copy and a column-sum bias
+        # gradient straight into the fp32 grad (ops/linear.py LibLinear; plain nn.Linear when the
+        # class count is not a multiple of 8 or the fused kernels are off)
+        self.fc = LibLinear(cin, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
@@ -120,7 +125,10 @@ class ResNet(nn.Module):
             x = x.contiguous(memory_format=torch.channels_last)
         x = self.stem(x)  # ImageNet stem: the max-pool is inside its BatchNormAct2d
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        if native_route():
+            x = global_avg_pool(x)  # one pooling launch, one broadcast launch in the backward
+        else:
+            x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)
 
     def forward(self, batch):

@@ -435,6 +435,58 @@ __global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const T* __restri
   if ((threadIdx.x & 3) == 0 && cc < C) out[cc] += t1;
 }
 
+// Global average pool of a channels-last [N][HW][C] activation -> [N][C] (the ResNet head):
+// a thread owns 8 channels of one sample and walks its HW rows with 4 loads in flight, fp32 sums.
+template <typename T, typename TO>
+__global__ void __launch_bounds__(256) gap_fwd_kernel(const T* __restrict__ x, TO* __restrict__ out, int N, int HW,
+                                                      int C) {
+  const int CV = C >> 3;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)N * CV) return;
+  const int n = (int)(t / CV), cv = (int)(t - (int64_t)n * CV);
+  const T* p = x + (int64_t)n * HW * C + cv * 8;
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  int h = 0;
+  for (; h + 3 < HW; h += 4) {
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) V8<T>::load(p + (int64_t)(h + u) * C, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[u][k];
+  }
+  for (; h < HW; ++h) {
+    float v[8];
+    V8<T>::load(p + (int64_t)h * C, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += v[k];
+  }
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] *= inv;
+  V8<TO>::store(out + (int64_t)n * C + cv * 8, acc);
+}
+
+// its backward: dx[n][hw][c] = dy[n][c] / HW (a thread writes 8 channels of one pixel)
+template <typename TG, typename T>
+__global__ void __launch_bounds__(256) gap_bwd_kernel(const TG* __restrict__ dy, T* __restrict__ dx, int N, int HW,
+                                                      int C) {
+  const int CV = C >> 3;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)N * HW * CV) return;
+  const int64_t pix = t / CV;
+  const int cv = (int)(t - pix * CV), n = (int)(pix / HW);
+  float v[8];
+  V8<TG>::load(dy + (int64_t)n * C + cv * 8, v);
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] *= inv;
+  V8<T>::store(dx + pix * C + cv * 8, v);
+}
+
 // Elementwise passes: thread t owns channel vector cv = t % CV (CV = C/8 <= 256) for the whole
 // launch, so its per-channel coefficients live in registers (loaded once), and walks rows
 // r = r0 + t / CV, stepping by RPP = BN_T / CV rows; 4 rows per iteration with clamped
@@ -1205,6 +1257,39 @@ static bool bn_elem_ok(int rpb, int C) { return (int64_t)rpb * C * 4 < (1ll << 3
 
 // out[c] += sum_r x[r][c]  (x: [R][C], dt f32 / bf16 / f16, C % 8 == 0); ws: rk_bn_workspace(R, C)
 // floats, counters: rk_bn_counters(C) zeroed uints (self-resetting)
+// Global average pool (channels-last [N][HW][C] -> [N][C]) and its backward.  dt: x / dx dtype,
+// dto: out / dy dtype (F32, BF16 or F16; 16-bit pairs must match).  C % 8 == 0.
+RK_API int rk_gap_fwd(int dt, int dto, const void* x, void* out, int N, int HW, int C, hipStream_t s) {
+  if (C % 8 || N <= 0 || HW <= 0 || (dt != F32 && dto != F32 && dt != dto)) return (int)hipErrorInvalidValue;
+  const int64_t nt = (int64_t)N * (C / 8);
+  const int grid = (int)((nt + 255) / 256);
+#define RK_GF(T, TO) gap_fwd_kernel<T, TO><<<grid, 256, 0, s>>>((const T*)x, (TO*)out, N, HW, C)
+  if (dt == BF16 && dto == BF16) RK_GF(uint16_t, uint16_t);
+  else if (dt == F16 && dto == F16) RK_GF(f16_t, f16_t);
+  else if (dt == BF16) RK_GF(uint16_t, float);
+  else if (dt == F16) RK_GF(f16_t, float);
+  else if (dto == BF16) RK_GF(float, uint16_t);
+  else if (dto == F16) RK_GF(float, f16_t);
+  else RK_GF(float, float);
+#undef RK_GF
+  return (int)hipGetLastError();
+}
+RK_API int rk_gap_bwd(int dt, int dto, const void* dy, void* dx, int N, int HW, int C, hipStream_t s) {
+  if (C % 8 || N <= 0 || HW <= 0 || (dt != F32 && dto != F32 && dt != dto)) return (int)hipErrorInvalidValue;
+  const int64_t nt = (int64_t)N * HW * (C / 8);
+  const int grid = (int)((nt + 255) / 256);
+#define RK_GB(TG, T) gap_bwd_kernel<TG, T><<<grid, 256, 0, s>>>((const TG*)dy, (T*)dx, N, HW, C)
+  if (dt == BF16 && dto == BF16) RK_GB(uint16_t, uint16_t);
+  else if (dt == F16 && dto == F16) RK_GB(f16_t, f16_t);
+  else if (dt == BF16) RK_GB(float, uint16_t);
+  else if (dt == F16) RK_GB(float, f16_t);
+  else if (dto == BF16) RK_GB(uint16_t, float);
+  else if (dto == F16) RK_GB(f16_t, float);
+  else RK_GB(float, float);
+#undef RK_GB
+  return (int)hipGetLastError();
+}
+
 RK_API int rk_colsum_acc(int dt, const void* x, int64_t R, int C, float* out, float* ws, unsigned* counters,
                          hipStream_t s) {
   if (C % 8 || R <= 0) return (int)hipErrorInvalidValue;

@@ -85,6 +85,8 @@ KERNEL_SIGS = {
                             c_int, c_int, c_void_p]),
     "rk_amp_check": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "rk_host_mapped_alloc": (c_void_p, [c_int64, c_void_p]),
+    "rk_gap_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "rk_gap_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "rk_host_mapped_free": (None, [c_void_p]),
     "rk_optim_chunk_for": (c_int, [c_int64]),
     "rk_gather_rows": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),

@@ -359,7 +359,7 @@ class _PatchEmbedFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, w16, b16, k):
         B, C, H, W = x.shape
         gh, gw = H // k, W // k
-        p = x.to(torch.bfloat16).reshape(B, C, gh, k, gw, k).permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * k * k)
+        p = x.to(w16.dtype).reshape(B, C, gh, k, gw, k).permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * k * k)
         y = torch.addmm(b16, p, w16.reshape(w16.shape[0], -1).t())
         ctx.save_for_backward(p)
         ctx.params = (weight, bias)
@@ -371,8 +371,8 @@ class _PatchEmbedFn(torch.autograd.Function):
         weight, bias = ctx.params
         N = weight.shape[0]
         dy2 = dy.reshape(-1, N)
-        if dy2.dtype != torch.bfloat16:
-            dy2 = dy2.to(torch.bfloat16)
+        if dy2.dtype != p.dtype:
+            dy2 = dy2.to(p.dtype)
         dy2 = dy2.contiguous()
         w2 = _FlatParam(weight)
         dw, db = lib_param_grads(dy2, p, w2, bias, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
@@ -392,8 +392,8 @@ class _FlatParam:
 
 
 class PatchEmbed(torch.nn.Conv2d):
-    """``nn.Conv2d(C, D, k, stride=k)`` (same parameters / state_dict) whose forward under bf16
-    autocast on a HIP device returns the token matrix ``[B, (H/k)*(W/k), D]`` from one patchify
+    """``nn.Conv2d(C, D, k, stride=k)`` (same parameters / state_dict) whose forward under bf16 or
+    fp16 autocast on a HIP device returns the token matrix ``[B, (H/k)*(W/k), D]`` from one patchify
     copy + one library GEMM (:class:`_PatchEmbedFn`); elsewhere ``conv(x).flatten(2).transpose(1, 2)``."""
 
     def __init__(self, in_chans: int, dim: int, patch: int):
@@ -401,10 +401,11 @@ class PatchEmbed(torch.nn.Conv2d):
 
     def forward(self, x):
         k = self.kernel_size[0]
-        if (x.is_cuda and native_route() and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.dim() == 4
+        cdtype = torch.get_autocast_dtype("cuda") if x.is_cuda else None
+        if (x.is_cuda and native_route() and cdtype in (torch.bfloat16, torch.float16) and x.dim() == 4
                 and x.shape[2] % k == 0 and x.shape[3] % k == 0 and self.weight.is_contiguous()
                 and self.weight.dtype == torch.float32):
-            w16 = _bf16_copy(self, "_w16", self.weight)
-            b16 = _bf16_copy(self, "_b16", self.bias)
+            w16 = _lowp_copy(self, "_w16", self.weight, cdtype)
+            b16 = _lowp_copy(self, "_b16", self.bias, cdtype)
             return _PatchEmbedFn.apply(x, self.weight, self.bias, w16, b16, k)
         return super().forward(x).flatten(2).transpose(1, 2)

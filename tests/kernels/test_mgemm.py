@@ -280,9 +280,11 @@ def test_gelu_bwd_colsum(M, N):
     assert _rel(db, zr.grad.sum(0)) < 1e-4
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("direct", [False, True])
-def test_patch_embed_matches_conv(direct):
-    """ViT patch embedding as patchify + library GEMM vs an fp32 nn.Conv2d on the same bf16 weights."""
+def test_patch_embed_matches_conv(direct, dtype):
+    """ViT patch embedding as patchify + library GEMM vs an fp32 nn.Conv2d on the same 16-bit
+    weights (bf16 and fp16 autocast)."""
     from rocket_amd.ops.linear import PatchEmbed
 
     torch.manual_seed(8)
@@ -290,15 +292,16 @@ def test_patch_embed_matches_conv(direct):
     ref = torch.nn.Conv2d(3, 768, 16, stride=16).cuda()
     ref.load_state_dict(pe.state_dict())
     with torch.no_grad():
-        ref.weight.copy_(ref.weight.to(torch.bfloat16).float())
+        ref.weight.copy_(ref.weight.to(dtype).float())
     if direct:
         for p in pe.parameters():
             p.grad = torch.full_like(p, 0.25)
             p._rocket_direct_grad = True
-    x = torch.randn(4, 3, 224, 224, device="cuda").to(torch.bfloat16)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    x = torch.randn(4, 3, 224, 224, device="cuda").to(dtype)
+    with torch.autocast("cuda", dtype=dtype):
         y = pe(x)
-    assert y.shape == (4, 196, 768)
+    assert y.shape == (4, 196, 768) and y.dtype == dtype
+    assert type(y.grad_fn).__name__ == "_PatchEmbedFnBackward"
     g = _r(4, 196, 768)
     y.backward(g)
     yr = ref(x.float()).flatten(2).transpose(1, 2)
