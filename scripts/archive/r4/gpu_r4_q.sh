@@ -10,4 +10,4 @@ f=$(find gpurun_out/r4q_vit16 -name "*kernel_trace.csv" | head -1)
 python3 bench/summarize_trace.py $f --steps 5 --title "ViT-B/16 bs128 fp16 step (round 4), rocprofv3 kernel trace" > gpurun_out/r4_vit_b16_fp16_kernels.md
 rm -rf gpurun_out/r4q_vit16
 head -40 gpurun_out/r4_vit_b16_fp16_kernels.md
-bash scripts/gpu_r4_pmc.sh
+bash scripts/archive/r4/gpu_r4_pmc.sh
