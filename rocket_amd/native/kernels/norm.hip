@@ -487,6 +487,28 @@ __global__ void __launch_bounds__(256) gap_bwd_kernel(const TG* __restrict__ dy,
   V8<T>::store(dx + pix * C + cv * 8, v);
 }
 
+// ViT patchify: x [B][C][H][W] (f32 or 16-bit) -> patches [B * gh * gw][C * k * k] in a 16-bit dtype,
+// the im2col of a stride-k, kernel-k conv (a permutation: no duplication).  A thread moves 8
+// consecutive kx of one (patch, c, ky) row: one 32-/16-byte read, one 16-byte write.  k % 8 == 0.
+template <typename T, typename TO>
+__global__ void __launch_bounds__(256) patchify_kernel(const T* __restrict__ x, TO* __restrict__ out, int B, int C,
+                                                       int H, int W, int k) {
+  const int gh = H / k, gw = W / k, kk = k * k, row_len = C * kk;
+  const int64_t total = (int64_t)B * gh * gw * row_len / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int64_t e = t * 8;
+  const int64_t row = e / row_len;
+  const int col = (int)(e - row * row_len);
+  const int c = col / kk, r = col - c * kk, ky = r / k, kx = r - ky * k;
+  const int P = gh * gw;
+  const int b = (int)(row / P), pp = (int)(row - (int64_t)b * P);
+  const int py = pp / gw, px = pp - py * gw;
+  float v[8];
+  V8<T>::load(x + (((int64_t)b * C + c) * H + py * k + ky) * W + px * k + kx, v);
+  V8<TO>::store(out + e, v);
+}
+
 // Elementwise passes: thread t owns channel vector cv = t % CV (CV = C/8 <= 256) for the whole
 // launch, so its per-channel coefficients live in registers (loaded once), and walks rows
 // r = r0 + t / CV, stepping by RPP = BN_T / CV rows; 4 rows per iteration with clamped
@@ -1287,6 +1309,22 @@ RK_API int rk_gap_bwd(int dt, int dto, const void* dy, void* dx, int N, int HW, 
   else if (dto == F16) RK_GB(f16_t, float);
   else RK_GB(float, float);
 #undef RK_GB
+  return (int)hipGetLastError();
+}
+
+// ViT patchify (see patchify_kernel).  dt: x dtype (F32 / BF16 / F16), dto: out dtype (BF16 / F16).
+RK_API int rk_patchify(int dt, int dto, const void* x, void* out, int B, int C, int H, int W, int k, hipStream_t s) {
+  if (k <= 0 || k % 8 || H % k || W % k || B <= 0 || C <= 0 || (dto != BF16 && dto != F16) ||
+      (dt != F32 && dt != dto))
+    return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * (H / k) * (W / k) * C * k * k / 8;
+  const int grid = (int)((total + 255) / 256);
+#define RK_PF(T, TO) patchify_kernel<T, TO><<<grid, 256, 0, s>>>((const T*)x, (TO*)out, B, C, H, W, k)
+  if (dt == F32 && dto == BF16) RK_PF(float, uint16_t);
+  else if (dt == F32) RK_PF(float, f16_t);
+  else if (dto == BF16) RK_PF(uint16_t, uint16_t);
+  else RK_PF(f16_t, f16_t);
+#undef RK_PF
   return (int)hipGetLastError();
 }
 

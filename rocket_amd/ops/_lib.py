@@ -86,6 +86,7 @@ KERNEL_SIGS = {
     "rk_amp_check": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "rk_host_mapped_alloc": (c_void_p, [c_int64, c_void_p]),
     "rk_gap_fwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "rk_patchify": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "rk_gap_bwd": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "rk_host_mapped_free": (None, [c_void_p]),
     "rk_optim_chunk_for": (c_int, [c_int64]),

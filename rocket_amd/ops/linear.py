@@ -359,7 +359,14 @@ class _PatchEmbedFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, w16, b16, k):
         B, C, H, W = x.shape
         gh, gw = H // k, W // k
-        p = x.to(w16.dtype).reshape(B, C, gh, k, gw, k).permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * k * k)
+        if (k % 8 == 0 and x.dtype in (torch.float32, w16.dtype) and x.is_contiguous()
+                and w16.dtype in (torch.bfloat16, torch.float16)):
+            # one native pass: cast + im2col permutation (norm.hip rk_patchify)
+            p = torch.empty(B * gh * gw, C * k * k, dtype=w16.dtype, device=x.device)
+            _lib.check(_lib.kernels().rk_patchify(_lib.dtype_code(x), _lib.dtype_code(p), x.data_ptr(), p.data_ptr(),
+                                                  B, C, H, W, k, _lib.stream_ptr(x.device)), "rk_patchify")
+        else:
+            p = x.to(w16.dtype).reshape(B, C, gh, k, gw, k).permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * k * k)
         y = torch.addmm(b16, p, w16.reshape(w16.shape[0], -1).t())
         ctx.save_for_backward(p)
         ctx.params = (weight, bias)

@@ -280,6 +280,24 @@ def test_gelu_bwd_colsum(M, N):
     assert _rel(db, zr.grad.sum(0)) < 1e-4
 
 
+@pytest.mark.parametrize("src,dst", [(torch.float32, torch.bfloat16), (torch.float32, torch.float16),
+                                     (torch.bfloat16, torch.bfloat16), (torch.float16, torch.float16)])
+def test_patchify_kernel_is_the_im2col_permutation(src, dst):
+    """rk_patchify (cast + stride-k / kernel-k im2col in one pass) equals the torch permutation
+    bit for bit (same round-to-nearest-even cast)."""
+    from rocket_amd.ops import _lib
+
+    torch.manual_seed(9)
+    x = torch.randn(3, 3, 64, 48, device="cuda").to(src)
+    B, C, H, W = x.shape
+    k = 16
+    ref = x.to(dst).reshape(B, C, H // k, k, W // k, k).permute(0, 2, 4, 1, 3, 5).reshape(-1, C * k * k)
+    out = torch.empty_like(ref)
+    _lib.check(_lib.kernels().rk_patchify(_lib.dtype_code(x), _lib.dtype_code(out), x.data_ptr(), out.data_ptr(),
+                                          B, C, H, W, k, _lib.stream_ptr(x.device)), "rk_patchify")
+    assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("direct", [False, True])
 def test_patch_embed_matches_conv(direct, dtype):
