@@ -228,6 +228,9 @@ def wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, target: torch.Tensor, accumu
 def bias_grad_into(dy2: torch.Tensor, target: torch.Tensor) -> None:
     """target += column sums of dy2 [M, N] (fp32 target, e.g. a persistent ``bias.grad``)."""
     M, N = dy2.shape
+    if N % 8:  # the column-sum kernel reads 8 channels per thread; small heads (10 classes) reduce here
+        target.add_(dy2.float().sum(0))
+        return
     lib = _lib.kernels()
     ws = torch.empty(int(lib.rk_bn_workspace(M, N)), dtype=torch.float32, device=dy2.device)
     nctr = int(lib.rk_bn_counters(N))
@@ -337,8 +340,8 @@ class LibLinear(torch.nn.Linear):
     ``nn.Linear``."""
 
     def forward(self, x):
-        if (x.is_cuda and self.bias is not None and native_route() and self.out_features % 8 == 0
-                and torch.is_grad_enabled()):
+        if (x.is_cuda and self.bias is not None and native_route()
+                and (self.out_features * self.in_features) % 8 == 0 and torch.is_grad_enabled()):
             cdtype = torch.get_autocast_dtype("cuda")
             w16 = b16 = None
             if (cdtype in (torch.bfloat16, torch.float16) and self.weight.dtype == torch.float32

@@ -292,7 +292,7 @@ def test_lenet_fused_backward_deterministic(N):
             assert torch.equal(a, b), (name, float((a - b).abs().max()))
 
 
-@pytest.mark.parametrize("M,K,N", [(25216, 768, 2304), (100, 64, 24), (37, 16, 8)])
+@pytest.mark.parametrize("M,K,N", [(25216, 768, 2304), (100, 64, 24), (37, 16, 8), (256, 512, 10)])
 def test_lib_linear_bias_grad(M, K, N):
     """LibLinear under bf16 autocast: same output / input and weight gradients as nn.Linear, bias
     gradient from the column-sum kernel vs the fp32 row sum of d(out)."""
@@ -307,6 +307,7 @@ def test_lib_linear_bias_grad(M, K, N):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y = lin(x)
         yr = ref(x)
+    assert type(y.grad_fn).__name__ == "_LibLinearBackward"  # (N = 10: the ResNet-18 CIFAR head)
     y.backward(g)
     yr.backward(g)
     assert y.dtype == torch.bfloat16 and torch.equal(y, yr)
