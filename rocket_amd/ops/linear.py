@@ -221,6 +221,15 @@ def wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, target: torch.Tensor, accumu
         a, b = dy2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K)
         part = torch.bmm(a, b, out_dtype=torch.float32) if _WGRAD_F32 else torch.bmm(a, b)
     part = part.contiguous()
+    if (N * K) % 8 or target.data_ptr() % 16 or part.data_ptr() % 16:
+        # the combine kernel moves 8 floats per thread from 16-byte aligned rows; a small head's grad
+        # packed into a flat gradient bucket at an odd offset is summed here instead
+        red = (part if s == 1 else part.sum(0)).float().view_as(target)
+        if accumulate:
+            target.add_(red)
+        else:
+            target.copy_(red)
+        return
     _lib.check(_lib.kernels().rk_slab_acc(part.data_ptr(), _lib.dtype_code(part), s, N * K, target.data_ptr(),
                                           int(accumulate), _lib.stream_ptr(dy2.device)), "rk_slab_acc")
 
