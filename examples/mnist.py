@@ -83,6 +83,10 @@ def main() -> int:
     ap.add_argument("--logs", default="./logs")
     ap.add_argument("--resume", default=None)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--train-size", type=int, default=60000, help="synthetic training samples")
+    ap.add_argument("--test-size", type=int, default=10000, help="synthetic evaluation samples")
+    ap.add_argument("--save-every", type=int, default=50, help="Checkpointer cadence (iterations)")
+    ap.add_argument("--capture", type=int, default=None, help="HIP-graph capture of the train step (default: on GPUs)")
     args = ap.parse_args()
 
     from rocket_amd.runtime import comm
@@ -93,8 +97,8 @@ def main() -> int:
         xtr, ytr = load_mnist(args.data, True)
         xte, yte = load_mnist(args.data, False)
     else:
-        xtr, ytr = synthetic_mnist(60000, seed=0)
-        xte, yte = synthetic_mnist(10000, seed=1)
+        xtr, ytr = synthetic_mnist(args.train_size, seed=0)
+        xte, yte = synthetic_mnist(args.test_size, seed=1)
     # the whole dataset fits in HBM many times over: keep it resident, gather batches on-device
     train = rocket.DeviceTensorDataset(xtr.to(dev), ytr.to(dev))
     test = rocket.DeviceTensorDataset(xte.to(dev), yte.to(dev))
@@ -114,9 +118,9 @@ def main() -> int:
                 [
                     rocket.Dataset(train, batch_size=args.batch, shuffle=True),
                     rocket.Module(net, [rocket.Loss(CrossEntropy()), rocket.Optimizer(opt), rocket.Scheduler(sched)],
-                                  capture=dev.type == "cuda"),
+                                  capture=dev.type == "cuda" if args.capture is None else bool(args.capture)),
                     rocket.Tracker(backend="jsonl"),
-                    rocket.Checkpointer(save_every=50),
+                    rocket.Checkpointer(save_every=args.save_every),
                 ],
                 tag="train",
             ),

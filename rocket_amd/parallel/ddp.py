@@ -52,6 +52,12 @@ DEFAULT_FIRST_BUCKET_MB = 1.0
 SIDE_SLOTS = 16
 
 
+def _padded(n: int) -> int:
+    """Elements a parameter occupies in a flat buffer: rounded up to 4 (16 B of fp32); the pad
+    stays zero, so reducing the whole flat buffer is unaffected."""
+    return (n + 3) // 4 * 4
+
+
 class _Bucket:
     __slots__ = ("index", "params", "offsets", "flat", "pending", "work", "ready", "touched", "numel_params")
 
@@ -62,7 +68,7 @@ class _Bucket:
         n = 0
         for p in params:
             self.offsets.append(n)
-            n += p.numel()
+            n += _padded(p.numel())  # every grad view 16-byte aligned (native kernels store 16 B)
         self.numel_params = n
         self.flat = torch.zeros(n + extra, dtype=dtype, device=device)
         self.pending = len(params)

@@ -25,6 +25,12 @@ import torch
 from torch import nn
 
 
+def _padded(n: int) -> int:
+    """Elements a parameter occupies in a flat gradient buffer: rounded up to 4 (16 B of fp32),
+    so every view starts 16-byte aligned for the native kernels' vector stores."""
+    return (n + 3) // 4 * 4
+
+
 def _param_view(flat: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
     """A slice of ``flat`` shaped AND strided like ``p`` (channels-last weights get channels-last
     grads, so autograd accumulates in place instead of copying through a layout change)."""
@@ -55,7 +61,7 @@ class FlatGrads:
         self.params: List[nn.Parameter] = []
         self.views: List[torch.Tensor] = []
         for (dev, dtype), ps in groups.items():
-            n = sum(p.numel() for p in ps)
+            n = sum(_padded(p.numel()) for p in ps)
             flat = torch.zeros(n, dtype=dtype, device=dev)
             off = 0
             for p in ps:
@@ -65,7 +71,7 @@ class FlatGrads:
                         view.copy_(p.grad)
                 p.grad = view
                 p._rocket_direct_grad = True
-                off += p.numel()
+                off += _padded(p.numel())  # 16-byte aligned views (zero pad between them)
                 self.params.append(p)
                 self.views.append(view)
             self.buffers.append(flat)

@@ -143,8 +143,11 @@ class FusedGradScaler:
                 # tracker; same here, after dropping this step's unscaled mark
                 self._unscaled.discard(id(optimizer))
                 raise AssertionError("No inf checks were recorded for this optimizer.")
+            # consume the producer's mark on every step (also the unscale_ path), so a stale mark
+            # can never skip the check of a later step whose producer did not fold it
+            checked = self._producer_checked(optimizer)
             if not unscaled:
-                if not self._producer_checked(optimizer):
+                if not checked:
                     optimizer.amp_check(self.state)
             else:  # unscaled in place (and checked) already: unscale by 1 this time; the last
                 self.state[INV] = 1.0  # block restores 1/scale with the scale update
@@ -167,8 +170,9 @@ class FusedGradScaler:
     def step_device(self, optimizer, zero_grads: bool = False) -> None:
         """The device part of a fused scaled step (flag check + update with in-kernel unscale and
         scale rule): graph-capturable; ``record_last`` after the replay publishes the skip flag."""
+        checked = self._producer_checked(optimizer)  # consumed on every step (see step)
         if id(optimizer) not in self._unscaled:
-            if not self._producer_checked(optimizer):
+            if not checked:
                 optimizer.amp_check(self.state)
         else:
             self.state[INV] = 1.0

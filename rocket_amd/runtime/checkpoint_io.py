@@ -109,6 +109,10 @@ def _np_state_restore(st):
 def save_state(engine, output_dir: str) -> Path:
     out = Path(output_dir)
     out.mkdir(parents=True, exist_ok=True)
+    # settle speculated scheduler steps before anything is written: a rolled-back step must leave
+    # optimizer.bin (param-group lr) and scheduler.bin consistent
+    for sched in engine._schedulers:
+        sched._resolve()
     for i, model in enumerate(engine._models):
         st_save(_cpu_state_dict(engine.unwrap_model(model)), str(out / _suffixed("model", "safetensors", i)),
                 metadata={"format": "pt"})

@@ -111,6 +111,11 @@ class EngineOptimizer:
         return self.optimizer.defaults
 
     def state_dict(self):
+        # a speculated scheduler step may still hold this optimizer's param-group hyperparameters:
+        # settle it first, so the saved lr is the one accelerate would hold
+        for s in getattr(self.engine, "_schedulers", ()):
+            if any(o is self for o in s.optimizers):
+                s._resolve()
         return self.optimizer.state_dict()
 
     def load_state_dict(self, sd):
@@ -177,13 +182,13 @@ class EngineScheduler:
     accumulation micro-steps it only advances ``_step_count``.
     """
 
-    #: fp16 device-resident scaler: instead of waiting for the step's skip flag (a host sync per
-    #: step, which serialises host issue and device work), step the scheduler assuming "not
-    #: skipped" and verify at the next scheduler step (that flag has landed by then); a wrong guess
-    #: (an inf/NaN step) restores the scheduler and the param-group hyperparameters.  The one update
-    #: already issued in between used the speculated hyperparameters; set ROCKET_SCHED_SPECULATE=0
-    #: for the exact (synchronising) form.
-    SPECULATE = os.environ.get("ROCKET_SCHED_SPECULATE", "1") != "0"
+    #: Opt-in (ROCKET_SCHED_SPECULATE=1), fp16 device-resident scaler only: instead of waiting for
+    #: the step's skip flag (a host sync per step), step the scheduler assuming "not skipped" and
+    #: verify at the next scheduler step; a wrong guess (an inf/NaN step) restores the scheduler and
+    #: the param-group hyperparameters.  The one update issued in between then ran with the
+    #: speculated lr, which accelerate never does (it does not step the scheduler after a skipped
+    #: step), so the default is the exact form: the lr sequence matches accelerate's.
+    SPECULATE = os.environ.get("ROCKET_SCHED_SPECULATE", "0") == "1"
 
     def __init__(self, scheduler, optimizers: List[EngineOptimizer], engine: "Engine"):
         self.scheduler = scheduler

@@ -384,6 +384,7 @@ class StepGraphs:
         # agree on the outcome BEFORE anything runs, and all drop to split mode together
         agree = (rep is not None and engine.sync_gradients and rep.capture_mode == "overlap"
                  and engine.num_processes > 1)
+        side = self._side_effects(pend) if agree else None
         try:
             err = None
             try:
@@ -400,7 +401,18 @@ class StepGraphs:
                                    "every rank captures sync steps in split mode")
                     rep.force_split = True
                     torch.cuda.synchronize()
-                    v = self._capture_inner(attrs, tens, pend)
+                    # the discarded capture already claimed the pending batch and set the fused
+                    # optimizers' per-step flags: undo that, or the retried graph would skip the
+                    # batch gather and the cursor advance on every replay
+                    self._restore_side_effects(pend, side)
+                    err2 = None
+                    try:
+                        v = self._capture_inner(attrs, tens, pend)
+                    except Exception as e:
+                        err2, v = e, None
+                    if not _comm.all_ranks_agree(err2 is None):
+                        raise RuntimeError(f"split-mode graph capture failed on some rank ({err2 or 'peer failed'})") \
+                            from err2
         finally:
             for b, old in restore:
                 b._rocket_pending = old
@@ -410,6 +422,23 @@ class StepGraphs:
             attrs.batch = v.out
             self._host(attrs)
         return v
+
+    _OPT_FLAGS = ("amp_checked", "epilogue_done")
+
+    def _side_effects(self, pend):
+        """Host-side state a capture mutates (pending batch, fused-optimizer step flags, counters)."""
+        opts = [getattr(o, "optimizer", o) for o in getattr(self.mod._accelerator, "_optimizers", [])]
+        flags = [(o, {f: getattr(o, f) for f in self._OPT_FLAGS if hasattr(o, f)}) for o in opts]
+        return ((pend.done, pend.advanced) if pend is not None else None, flags, self.captures, self.parts,
+                self.launch_lists)
+
+    def _restore_side_effects(self, pend, side) -> None:
+        pstate, flags, self.captures, self.parts, self.launch_lists = side
+        if pend is not None:
+            pend.done, pend.advanced = pstate
+        for o, vals in flags:
+            for f, val in vals.items():
+                setattr(o, f, val)
 
     def _capture_inner(self, attrs: Attributes, tens: List[torch.Tensor], pend) -> _Captured:
         engine = self.mod._accelerator

@@ -1,6 +1,10 @@
-"""EngineScheduler under the fp16 device-resident scaler: the scheduler steps speculatively when
-the step's skip flag has not landed yet, and a mispredicted (skipped) step is rolled back when the
-flag is read (runtime/engine.py EngineScheduler.SPECULATE)."""
+"""EngineScheduler under the fp16 device-resident scaler.
+
+Default (exact form): a skipped step never advances the schedule, as in accelerate
+(``accelerate@1.14.0:scheduler.py:54-83``; reference ``rocket/core/scheduler.py:94-113``).
+Opt-in speculation (ROCKET_SCHED_SPECULATE=1, runtime/engine.py EngineScheduler.SPECULATE): the
+scheduler steps when the step's skip flag has not landed yet and a mispredicted (skipped) step is
+rolled back when the flag is read; checkpoints settle the speculation first."""
 
 import torch
 
@@ -37,6 +41,7 @@ def test_speculated_step_kept_and_mispredicted_step_rolled_back():
     opt = torch.optim.SGD([p], lr=1.0, momentum=0.9)
     eo = EngineOptimizer(opt, _Eng())
     sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5), [eo], _Eng())
+    sch.SPECULATE = True
 
     eo._skip_lazy, eo._lazy_handle = True, _flag(False)
     sch.step()  # flag not landed: speculate
@@ -61,3 +66,66 @@ def test_landed_flag_takes_the_exact_path():
     eo._skip_lazy, eo._lazy_handle = True, h
     sch.step()  # flag available: the skipped step does not advance the schedule
     assert opt.param_groups[0]["lr"] == 1.0 and sch._pending is None
+
+
+def test_exact_form_is_the_default():
+    assert EngineScheduler.SPECULATE is False
+
+
+def _run_lrs(skips, speculate):
+    """lr seen by every update of a run whose steps ``skips`` flags as inf/NaN-skipped."""
+    p = torch.nn.Parameter(torch.zeros(2))
+    opt = torch.optim.SGD([p], lr=1.0)
+    eo = EngineOptimizer(opt, _Eng())
+    sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5), [eo], _Eng())
+    sch.SPECULATE = speculate
+    seen = []
+    for sk in skips:
+        seen.append(opt.param_groups[0]["lr"])  # the lr this update runs with
+        eo._skip_lazy, eo._lazy_handle = True, _flag(sk)
+        sch.step()
+    sch.get_last_lr()
+    return seen, opt.param_groups[0]["lr"]
+
+
+def test_exact_lr_sequence_matches_accelerate_with_skipped_steps():
+    skips = [True, True, False, True, False, False, True, False]
+    # accelerate: the scheduler steps only after a non-skipped optimizer step
+    lr, want = 1.0, []
+    for sk in skips:
+        want.append(lr)
+        if not sk:
+            lr *= 0.5
+    seen, final = _run_lrs(skips, speculate=False)
+    assert seen == want and final == lr
+    # the speculative form differs exactly on the update that follows a skipped step
+    seen_spec, final_spec = _run_lrs(skips, speculate=True)
+    assert final_spec == lr and seen_spec != want
+
+
+def test_checkpoint_settles_a_mispredicted_speculation(tmp_path):
+    from rocket_amd.runtime import checkpoint_io
+
+    p = torch.nn.Parameter(torch.zeros(2))
+    opt = torch.optim.SGD([p], lr=1.0)
+
+    class _E(_Eng):
+        _models, _custom_objects, step, process_index = [], [], 0, 0
+
+    eng = _E()
+    eo = EngineOptimizer(opt, eng)
+    sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5), [eo], eng)
+    sch.SPECULATE = True
+    eng._optimizers, eng._schedulers = [eo], [sch]
+    eo._skip_lazy, eo._lazy_handle = True, _flag(True)
+    sch.step()  # speculated; the step was in fact skipped
+    assert opt.param_groups[0]["lr"] == 0.5
+    checkpoint_io.save_state(eng, str(tmp_path / "ck"))
+    osd = torch.load(tmp_path / "ck" / "optimizer.bin", weights_only=True)
+    ssd = torch.load(tmp_path / "ck" / "scheduler.bin", weights_only=True)
+    assert osd["param_groups"][0]["lr"] == 1.0 and ssd["last_epoch"] == 0
+
+    # and the optimizer's own state_dict settles it too
+    eo._skip_lazy, eo._lazy_handle = True, _flag(True)
+    sch.step()
+    assert eo.state_dict()["param_groups"][0]["lr"] == 1.0
