@@ -17,6 +17,9 @@ from rocket_amd.core.attributes import Attributes
 from rocket_amd.core.capsule import Capsule, Events
 
 
+_BASE_DISPATCH = Capsule.dispatch  # a child whose dispatch differs (override, spy) keeps going through it
+
+
 class Dispatcher(Capsule):
     def __init__(self, capsules: list[Capsule], priority: int = 1000) -> None:
         super().__init__(statefull=False, priority=priority)
@@ -24,6 +27,7 @@ class Dispatcher(Capsule):
         self.guard(capsules)
         # list.sort is stable: equal priorities keep insertion order
         self._capsules = sorted(capsules, key=lambda c: c._priority, reverse=True)
+        self._launch_handlers = None  # (children list, bound launch handlers) — see launch()
 
     def _fan_out(self, event: Events, attrs: Attributes | None) -> None:
         for capsule in self._capsules:
@@ -47,8 +51,16 @@ class Dispatcher(Capsule):
         self._fan_out(Events.RESET, attrs)
 
     def launch(self, attrs: Attributes | None = None) -> None:
-        Capsule.launch(self, attrs=attrs)
-        self._fan_out(Events.LAUNCH, attrs)
+        # the per-iteration event: the children's bound ``launch`` handlers, resolved once (a child
+        # that overrides ``dispatch`` keeps going through it), called in priority order — the same
+        # calls as ``_fan_out(Events.LAUNCH)`` without an enum lookup + getattr per child per step
+        hs = self._launch_handlers
+        if hs is None or hs[0] is not self._capsules:
+            hs = self._launch_handlers = (self._capsules, [
+                c.launch if type(c).dispatch is _BASE_DISPATCH else (lambda a, c=c: c.dispatch(Events.LAUNCH, a))
+                for c in self._capsules])
+        for h in hs[1]:
+            h(attrs)
 
     def accelerate(self, accelerator) -> None:
         Capsule.accelerate(self, accelerator)

@@ -114,20 +114,22 @@ class Looper(Dispatcher):
 
             bar = tqdm(total=self._repeats, desc=f"{_green(self._tag)} epoch={epoch}, grad={self._grad_enabled}")
         last = 0.0
-        for i in range(self._repeats):
-            attrs.batch = None
-            with torch.set_grad_enabled(self._grad_enabled):
+        # grad mode for the whole loop (the reference enters it per iteration, loop.py:217; the
+        # children see the same mode either way, and it is restored when the loop ends)
+        with torch.set_grad_enabled(self._grad_enabled):
+            for i in range(self._repeats):
+                attrs["batch"] = None
                 Dispatcher.launch(self, attrs)
-            if attrs.looper.terminate:
-                break
-            if bar is not None:
-                now = time.monotonic()
-                if now - last >= self._postfix_interval or i == self._repeats - 1:
-                    state = attrs.looper.state
-                    materialize(v for v in state.values())
-                    bar.set_postfix(state, refresh=False)
-                    last = now
-                bar.update(1)
+                if attrs.looper.terminate:
+                    break
+                if bar is not None:
+                    now = time.monotonic()
+                    if now - last >= self._postfix_interval or i == self._repeats - 1:
+                        state = attrs.looper.state
+                        materialize(v for v in state.values())
+                        bar.set_postfix(state, refresh=False)
+                        last = now
+                    bar.update(1)
         if bar is not None:
             bar.close()
         self._iter_idx = 0

@@ -56,13 +56,27 @@ __device__ __forceinline__ void x4_dma(const char* base, int64_t bytes, int64_t 
                                              voff[i & 1] + (uint32_t)(row0 * ld2), 0, 0, 0);
   }
 }
+// one of the X4_NI instructions of x4_dma (the spread schedule issues them between MFMAs)
+__device__ __forceinline__ void x4_dma1(const char* base, int64_t bytes, int64_t ld2, char* lds, int w,
+                                        const uint32_t (&voff)[2], int i) {
+  const int n = (int)(bytes < 0 ? 0 : (bytes > 0x7fffffff ? 0x7fffffff : bytes));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, n, 0x00020000);
+  const int row0 = 64 * w + 8 * i;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + row0 * X4_ROWB), 16, voff[i & 1] + (uint32_t)(row0 * ld2),
+                                           0, 0, 0);
+}
 #endif
 
+template <bool SPREAD>
 __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                           const uint16_t* __restrict__ B, int64_t ldb, void* C,
                                                           int64_t ldc, int c_dt, const float* __restrict__ bias,
-                                                          int M, int N, int K, int dbg) {
+                                                          int M, int N, int K, int dbg, uint64_t* trace) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * X4_STAGE];
+  // diagnostics (rk_xgemm4_set_trace): thread 0 stamps s_memrealtime (100 MHz) at block start,
+  // prologue done, main loop done, epilogue done, plus the tile id: trace[block][0..4]
+  uint64_t* const tr = trace ? trace + (int64_t)blockIdx.x * 8 : nullptr;
+  if (tr && threadIdx.x == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
   const int tiles_n = (N + X4_BN - 1) / X4_BN;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   int tm, tn;
@@ -157,6 +171,7 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
     X4_READ_ALL(A0, B0, addr(arow, 0, 0), addr(brow, 0, 0));
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
   }
+  if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
   for (int t = 0; t < T; ++t) {
     // sub 0: MFMAs on half 0 of tile t, reads of half 1 of tile t
     __builtin_amdgcn_s_setprio(1);
@@ -168,11 +183,53 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (!(dbg & 2)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < T && !(dbg & 1)) dma(t + 2);  // into tile t's stage
-    // sub 1: MFMAs on half 1, reads of half 0 of tile t+1
-    __builtin_amdgcn_s_setprio(1);
-    mma(A1, B1, t + 1 < T, A0, B0, addr(arow, t + 1, 0), addr(brow, t + 1, 0));
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!SPREAD) {
+      if (t + 2 < T && !(dbg & 1)) dma(t + 2);  // into tile t's stage
+      // sub 1: MFMAs on half 1, reads of half 0 of tile t+1
+      __builtin_amdgcn_s_setprio(1);
+      mma(A1, B1, t + 1 < T, A0, B0, addr(arow, t + 1, 0), addr(brow, t + 1, 0));
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+      // spread schedule (the library's): tile t+2's 16 DMA instructions go out one per 4 MFMAs of
+      // sub 1 instead of as one burst at the barrier, so they never queue ahead of a fragment read
+      const bool dm = t + 2 < T && !(dbg & 1);
+      const bool rd = t + 1 < T;
+      const uint32_t aa = addr(arow, t + 1, 0), ab = addr(brow, t + 1, 0);
+#if defined(__HIP_DEVICE_COMPILE__)
+      char* st = smem + (t & 1) * X4_STAGE;
+      const char* ga = abase + (t + 2) * X4_ROWB;
+      const char* gb = bbase + (t + 2) * X4_ROWB;
+      const int64_t na = abytes - (t + 2) * X4_ROWB, nb = bbytes - (t + 2) * X4_ROWB;
+#endif
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (rd) {
+          switch (i) {
+            case 0: X4_RD(A0[0], aa, 0); X4_RD(B0[0], ab, 0); break;
+            case 1: X4_RD(A0[1], aa, 2048); X4_RD(B0[1], ab, 2048); break;
+            case 2: X4_RD(A0[2], aa, 4096); X4_RD(B0[2], ab, 4096); break;
+            case 3: X4_RD(A0[3], aa, 6144); X4_RD(B0[3], ab, 6144); break;
+            case 4: X4_RD(A0[4], aa, 8192); X4_RD(B0[4], ab, 8192); break;
+            case 5: X4_RD(A0[5], aa, 10240); X4_RD(B0[5], ab, 10240); break;
+            case 6: X4_RD(A0[6], aa, 12288); X4_RD(B0[6], ab, 12288); break;
+            default: X4_RD(A0[7], aa, 14336); X4_RD(B0[7], ab, 14336); break;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          mfma_a(acc[i][j], B1[j], A1[i]);
+#if defined(__HIP_DEVICE_COMPILE__)
+          if (dm && (j & 3) == 3) {  // 2 per row i: A instructions in rows 0-3, B in rows 4-7
+            const int q = 2 * i + (j >> 2);
+            if (q < X4_NI) x4_dma1(ga, na, lda * 2, st, w, va, q);
+            else x4_dma1(gb, nb, ldb * 2, st + X4_OPB, w, vb, q - X4_NI);
+          }
+#endif
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 #undef X4_READ_ALL
@@ -180,6 +237,7 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
 
   // epilogue: lane holds D[n = 16 j + 4 hi + r][m = 16 i + lo]
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 7" ::: "memory");
+  if (tr && threadIdx.x == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
   const int mb = r0 + 128 * wm, nb = c0 + 128 * wn;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -196,6 +254,11 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
       if (c_dt == F32) *(float4*)((float*)C + (int64_t)m * ldc + n) = make_float4(v0, v1, v2, v3);
       else *(uint2*)((uint16_t*)C + (int64_t)m * ldc + n) = make_uint2(pack16(v0, v1, c_dt), pack16(v2, v3, c_dt));
     }
+  }
+  if (tr && threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tr[3] = __builtin_amdgcn_s_memrealtime();
+    tr[4] = (uint64_t)tile;
   }
 }
 
@@ -521,7 +584,12 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4p_kernel(const uint16_t* __res
 // C[M][N] = A[M][K] B[N][K]^T (+ bias[N]); bf16 operands (rows 16-byte aligned), K % 64 == 0,
 // N % 4 == 0; C f32 / bf16 / fp16 (c_dt).
 int g_x4_dbg = 0;
-RK_API int rk_xgemm4_set_dbg(int bits) {  // diagnostics: bit 0 no in-loop DMA, bit 1 no barrier
+uint64_t* g_x4_trace = nullptr;
+RK_API int rk_xgemm4_set_trace(void* tr) {  // diagnostics: per-block phase stamps [blocks][8] (or null)
+  g_x4_trace = (uint64_t*)tr;
+  return 0;
+}
+RK_API int rk_xgemm4_set_dbg(int bits) {  // diagnostics: bit 0 no in-loop DMA, bit 1 no barrier, bit 5 spread DMA
   g_x4_dbg = bits;
   return 0;
 }
@@ -548,7 +616,11 @@ RK_API int rk_xgemm4(const void* a, int64_t lda, const void* b, int64_t ldb, voi
                                            K, g_x4_dbg);
     return (int)hipGetLastError();
   }
-  xgemm4_kernel<<<tiles, X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc, c_dt, bias, M, N, K,
-                                        g_x4_dbg);
+  if (g_x4_dbg & 32)
+    xgemm4_kernel<true><<<tiles, X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc, c_dt, bias, M,
+                                                N, K, g_x4_dbg, g_x4_trace);
+  else
+    xgemm4_kernel<false><<<tiles, X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc, c_dt, bias, M,
+                                                 N, K, g_x4_dbg, g_x4_trace);
   return (int)hipGetLastError();
 }
