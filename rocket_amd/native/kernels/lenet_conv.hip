@@ -21,6 +21,8 @@
 // per element per block.
 #include "rk_common.h"
 
+#include <cstdlib>
+
 using namespace rk;
 
 // 16-bit format of every activation / fragment / weight-gradient operand: bf16 (default) or, when
@@ -224,20 +226,35 @@ struct RowSrc {
   const float* xsrc;    // dataset images [rows][784]
   const int64_t* ysrc;  // dataset labels [rows]
   int64_t* ydst;        // the batch's label buffer [N]
+  const int64_t* target;  // labels of a batch that is not gathered (rows == null); keep != 0 only
+  int keep;             // whole-step kernel: also stage the backward's inputs in KeepSmem (labels, dgrad fragments)
 };
 
 // ------------------------------------------------------------------------------ forward
 constexpr int A1CL = Q1 * Q1 * 8;  // channel-last conv1 output: [pixel][8 channels], 6 used
 
-struct FwdSmem {
+constexpr int K2P = 13;            // conv2-dgrad k-steps: (kh,kw,co) = 400 -> 416
+
+// The forward state the backward reuses.  Both phase layouts (FwdSmem, BwdSmem) START with it, so in
+// the whole-step kernel (TrainSmem, a union of the two) the backward finds the staged image, the
+// pooled conv1 output a1 and both argmax/ReLU code maps still in LDS: no global round trip (and no
+// global copy of a1 / codes at all, which also shrinks the dirty bytes the kernel boundary writes back).
+struct KeepSmem {
   uint16_t imgb[SPB][2][IMGN + 8];  // bf16 image, two copies for pair reads (see BwdSmem)
-  uint16_t a1cl[SPB][A1CL + 16];  // zero pixel at A1CL (8 zeros), trash lanes at A1CL+8
-  uint16_t a1[SPB][A1N + 8];  // zero slot at A1N, trash at A1N+4
-  uint8_t c1[SPB][A1N + 8];
-  uint16_t a2[SPB][A2P];  // data 0..399, zero pad 400..415, trash at A2TRASH
-  uint8_t c2[SPB][A2P];   // same row pitch as a2: the trash slot A2TRASH must stay inside the row
-  uint16_t h1[SPB][H1P];  // classifier activations (bf16), zero pads for the next layer's K
+  uint16_t a1[SPB][A1N + 8];        // fwd: zero slot at A1N, trash at A1N+4; bwd: zero / ones pairs there
+  uint8_t c1[SPB][A1N + 8];         // bwd: never-matching slot at A1N
+  uint8_t c2[SPB][A2P];             // same row pitch as a2: the trash slot A2TRASH must stay inside the row
+  uint16_t h1[SPB][H1P];            // classifier activations (bf16; the backward's ReLU masks), zero K pads
   uint16_t h2[SPB][H2P];
+  float logit[SPB][16];             // fp32 logits (the fused cross-entropy's input)
+  int64_t label[SPB];               // the samples' targets
+  bf16x8 wfr[K2P * 64];             // conv2-dgrad B fragments (loaded during the forward by the whole-step kernel)
+};
+
+struct FwdSmem {
+  KeepSmem k;
+  uint16_t a1cl[SPB][A1CL + 16];  // zero pixel at A1CL (8 zeros), trash lanes at A1CL+8
+  uint16_t a2[SPB][A2P];  // data 0..399, zero pad 400..415, trash at A2TRASH
   uint16_t zrow[A2P];
 };
 
@@ -271,10 +288,10 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
   const int n = blockIdx.x * SPB + slot;
   const bool live = n < N;
   const int nc = live ? n : 0;
-  uint16_t* img0 = sm.imgb[slot][0];
-  uint16_t* img1 = sm.imgb[slot][1];
-  uint16_t* a1 = sm.a1[slot];
-  uint8_t* c1 = sm.c1[slot];
+  uint16_t* img0 = sm.k.imgb[slot][0];
+  uint16_t* img1 = sm.k.imgb[slot][1];
+  uint16_t* a1 = sm.k.a1[slot];
+  uint8_t* c1 = sm.k.c1[slot];
 
   // the sample's 784 pixels as 196 float4 loads (one per thread), written at their padded
   // position (row stride IMGS, 2-pixel zero border) into both image copies; the 280 border /
@@ -288,9 +305,23 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
     float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (st < IMG * IMG / 4) {
       v4 = xs[st];
-      if (rs.rows && live) ((float4*)(const_cast<float*>(x) + (int64_t)n * IMG * IMG))[st] = v4;
+      // the batch buffer is only for later readers (the backward reuses the LDS image): streamed
+      // out non-temporally, so it does not sit dirty in L2 at the kernel boundary
+      if (rs.rows && live) {
+        f32x4* const xd = (f32x4*)(const_cast<float*>(x) + (int64_t)n * IMG * IMG) + st;
+        if (rs.keep & 2) *xd = f32x4{v4.x, v4.y, v4.z, v4.w};  // A/B knob ROCKET_LENET_X_PLAIN=1
+        else __builtin_nontemporal_store(f32x4{v4.x, v4.y, v4.z, v4.w}, xd);
+      }
     }
-    if (rs.rows && live && st == IMG * IMG / 4) rs.ydst[n] = rs.ysrc[srow];
+    if (st == IMG * IMG / 4 && (rs.rows || rs.keep)) {
+      const int64_t lab = rs.rows ? rs.ysrc[srow] : (rs.target ? rs.target[nc] : 0);
+      if (rs.rows && live) __builtin_nontemporal_store(lab, rs.ydst + n);
+      if (rs.keep) sm.k.label[slot] = lab;
+    }
+    if constexpr (MLP) {
+      if (rs.keep)  // the backward's conv2-dgrad fragments (its phase A then waits on no global load)
+        for (int i = threadIdx.x; i < K2P * 64; i += NTHR) sm.k.wfr[i] = cf.frag[OFF_D2 * 64 + i];
+    }
     for (int b = st; b < 4 * IMGS + IMG * 5 + 8; b += 64 * WPS) {  // border / zero-slot elements
       int bi;
       if (b < 4 * IMGS) {  // rows 0, 1, 30, 31
@@ -486,7 +517,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
   }
   lds_barrier();
   RK_TR(cf.trace, 3);
-  if (live) {
+  if (live && a1g) {  // (null in the whole-step kernel: its backward reads them from LDS)
     for (int i = st * 8; i < A1N; i += 64 * WPS * 8) {
       *(uint4*)(a1g + (int64_t)n * A1N + i) = *(const uint4*)(a1 + i);
       *(uint2*)(code1 + (int64_t)n * A1N + i) = *(const uint2*)(c1 + i);
@@ -534,7 +565,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       const bool on = m > 0.f;
       const int o = wq < Q2 * Q2 ? lo * (Q2 * Q2) + wq : (MLP ? A2TRASH : A2N);  // flatten order (C, H, W)
       sm.a2[slot][o] = c16(on ? m : 0.f);
-      sm.c2[slot][o] = on ? (uint8_t)arg : 0xFF;
+      sm.k.c2[slot][o] = on ? (uint8_t)arg : 0xFF;
     }
   }
   if constexpr (MLP) {  // fc2 / fc3 fragments (bw2 is dead now; fc1 hides their latency)
@@ -549,10 +580,10 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
   }
   lds_barrier();
   RK_TR(cf.trace, 5);
-  if (live) {
+  if (live && code2) {
     for (int i = st * 8; i < A2N; i += 64 * WPS * 8) {
       if (!MLP) *(uint4*)(a2g + (int64_t)n * A2N + i) = *(const uint4*)(sm.a2[slot] + i);
-      *(uint2*)(code2 + (int64_t)n * A2N + i) = *(const uint2*)(sm.c2[slot] + i);
+      *(uint2*)(code2 + (int64_t)n * A2N + i) = *(const uint2*)(sm.k.c2[slot] + i);
     }
   }
   if constexpr (MLP) {
@@ -567,7 +598,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           v[i] = col < F1 ? fmaxf(acc[i] + bb, 0.f) : 0.f;
-          sm.h1[i][col] = c16(v[i]);
+          sm.k.h1[i][col] = c16(v[i]);
         }
         if (col < F1) *(uint2*)(cf.h1T + (int64_t)col * N + n0) = pack4(v[0], v[1], v[2], v[3]);
       }
@@ -575,12 +606,12 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       for (int f = threadIdx.x - 512; f < F0; f += 512)
         *(uint2*)(cf.a2T + (int64_t)f * N + n0) = make_uint2(
             (uint32_t)sm.a2[0][f] | ((uint32_t)sm.a2[1][f] << 16), (uint32_t)sm.a2[2][f] | ((uint32_t)sm.a2[3][f] << 16));
-      if (threadIdx.x - 512 < SPB * 8) sm.h1[(threadIdx.x - 512) >> 3][128 + ((threadIdx.x - 512) & 7)] = 0;
+      if (threadIdx.x - 512 < SPB * 8) sm.k.h1[(threadIdx.x - 512) >> 3][128 + ((threadIdx.x - 512) & 7)] = 0;
     }
     lds_barrier();
     RK_TR(cf.trace, 6);
     if (wave < 6) {  // fc2: 6 n-tiles x 4 k-steps
-      const f32x4 acc = cls_tile_pre<4>(&sm.h1[0][0], H1P, sm.zrow, fr2, lane);
+      const f32x4 acc = cls_tile_pre<4>(&sm.k.h1[0][0], H1P, sm.zrow, fr2, lane);
       if (hi == 0) {
         const int col = 16 * wave + lo;
         const float bb = fbias2;
@@ -588,7 +619,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           v[i] = col < F2 ? fmaxf(acc[i] + bb, 0.f) : 0.f;
-          sm.h2[i][col] = c16(v[i]);
+          sm.k.h2[i][col] = c16(v[i]);
         }
         if (col < F2) *(uint2*)(cf.h2T + (int64_t)col * N + n0) = pack4(v[0], v[1], v[2], v[3]);
       }
@@ -596,11 +627,14 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
     lds_barrier();
     RK_TR(cf.trace, 7);
     if (wave == 0) {  // fc3: 1 n-tile x 3 k-steps -> fp32 logits
-      const f32x4 acc = cls_tile_pre<3>(&sm.h2[0][0], H2P, sm.zrow, fr3, lane);
+      const f32x4 acc = cls_tile_pre<3>(&sm.k.h2[0][0], H2P, sm.zrow, fr3, lane);
       if (hi == 0 && lo < F3) {
         const float bb = fbias3;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) cf.logits[(int64_t)(n0 + i) * F3 + lo] = acc[i] + bb;
+        for (int i = 0; i < 4; ++i) {
+          cf.logits[(int64_t)(n0 + i) * F3 + lo] = acc[i] + bb;
+          sm.k.logit[i][lo] = acc[i] + bb;
+        }
       }
     }
     RK_TR(cf.trace, 8);
@@ -632,25 +666,21 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
 constexpr int DC = 18;             // dConv2 image side: 10 + 2*4 zero ring
 constexpr int DCN = DC * DC * C2;  // 5184, channel-last [y][x][co]; zero pixel at DCN
 constexpr int DTS = 136;           // row stride of dConv2^T [co][position] (100 used, zero padded; 272 B: rows on distinct LDS slots)
-constexpr int K2P = 13;            // conv2-dgrad k-steps: (kh,kw,co) = 400 -> 416
 // fused path: per-block conv-gradient slab row [dW1 150 | db1 6 | dW2 2400 | db2 16] (+pad)
 constexpr int SL_W1 = 0, SL_B1 = SL_W1 + C1 * R1, SL_W2 = SL_B1 + C1, SL_B2 = SL_W2 + C2 * R2;
 constexpr int SLABN = SL_B2 + C2;  // 2572
 constexpr int SLABW = 2576;
 
 struct BwdSmem {
-  // bf16 image in two copies: [0][i] = img[i], [1][i] = img[i + 1], so any pair (x, x+1) is ONE
-  // aligned 4-byte read (copy x & 1 at x & ~1) — the dW1 B operand is 4 pair reads per fragment.
-  // Zero pair at [0][IMGZ].
-  uint16_t imgb[SPB][2][IMGN + 8];
+  // k.imgb: bf16 image in two copies: [0][i] = img[i], [1][i] = img[i + 1], so any pair (x, x+1) is
+  // ONE aligned 4-byte read (copy x & 1 at x & ~1) — the dW1 B operand is 4 pair reads per fragment.
+  // Zero pair at [0][IMGZ].  k.a1 (+ zero slot at A1N), k.c1 (+ never-matching slot at A1N), k.c2.
+  KeepSmem k;
   float dx2[SPB][A1N + 4];          // dL/d a1 (conv2 input gradient)
-  uint16_t a1[SPB][A1N + 8];        // + zero slot at A1N
   uint16_t a1o[SPB][A1N + 8];       // a1 shifted by one element (pair reads for the dW2 B operand)
-  uint8_t c1[SPB][A1N + 8];         // + never-matching slot at A1N
   uint16_t dc2[SPB][DCN + 16];      // dense channel-last dConv2 with zero ring; zero pixel at DCN
                                     // (after phase B: the 16 waves' dW1 partials [16][2][256] f32)
   uint16_t dcT[SPB][C2 * DTS];      // dConv2^T [co][p = 4*window + quadrant] (wgrad2 A operand)
-  bf16x8 wfr[K2P * 64];             // conv2-dgrad B fragments
   // fused classifier backward (MLP=true): gradients of the 4 samples as MFMA A rows
   uint16_t dyl[SPB][DYP];           // dlogits, K pad 10..39 zero
   uint16_t d2l[SPB][H2P];           // d(fc2 out) masked, pad 84..
@@ -695,7 +725,9 @@ struct ClsBwd {
   const float* gscale_dev;          // optional device factor on d(logits) (the fp16 loss scale)
 };
 
-template <bool MLP>
+// RES (whole-step kernel only): the forward of this block left the image, a1 and both code maps in
+// sm.k (KeepSmem), so phase A stages nothing from global memory and a1g / code1g / code2g are unused.
+template <bool MLP, bool RES = false>
 __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ x, const uint16_t* __restrict__ a1g,
                                          const uint8_t* __restrict__ code1g, const uint16_t* __restrict__ da2g,
                                          const uint8_t* __restrict__ code2g, const float* __restrict__ w2,
@@ -709,8 +741,10 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
   // consecutive k share (kh, kw) and step co by 1: gather offsets are base + j*DC*DC.
   // B operand B[k][col = ci] = w2[co][ci][kh][kw]: 13 k-steps, lanes lo < 6.
   // kept in LDS in fragment order (wfr[s*64 + lane]), one ds_read_b128 per k-step
-  if constexpr (MLP) {
-    for (int i = threadIdx.x; i < K2P * 64; i += NTHR) sm.wfr[i] = cb.frag[OFF_D2 * 64 + i];
+  if constexpr (RES) {
+    // staged by the forward (KeepSmem)
+  } else if constexpr (MLP) {
+    for (int i = threadIdx.x; i < K2P * 64; i += NTHR) sm.k.wfr[i] = cb.frag[OFF_D2 * 64 + i];
   } else
   for (int i = threadIdx.x; i < K2P * 64; i += NTHR) {
     const int s = i >> 6, l = i & 63, h = l >> 4, c = l & 15;
@@ -722,7 +756,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       const float f = w2[ok ? (co * C1 + c) * R1 + kk : 0];
       v[j] = e16(ok ? f : 0.f);
     }
-    sm.wfr[i] = v;
+    sm.k.wfr[i] = v;
   }
 
 
@@ -738,13 +772,21 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     if (wave < 6) {
       fb3 = cb.frag[(OFF_B3 + wave) * 64 + lane];
       const int col = 16 * wave + lo;
-      if (hi == 0) mk2 = *(const uint2*)(cb.h2T + (int64_t)(col < F2 ? col : 0) * N + nb);
+      if (RES) {
+        if (hi == 0)
+          mk2 = make_uint2((uint32_t)sm.k.h2[0][col] | ((uint32_t)sm.k.h2[1][col] << 16),
+                           (uint32_t)sm.k.h2[2][col] | ((uint32_t)sm.k.h2[3][col] << 16));
+      } else if (hi == 0) mk2 = *(const uint2*)(cb.h2T + (int64_t)(col < F2 ? col : 0) * N + nb);
     }
     if (wave < 8) {
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks) fb2[ks] = cb.frag[(OFF_B2 + wave * 3 + ks) * 64 + lane];
       const int col = 16 * wave + lo;
-      if (hi == 0) mk1 = *(const uint2*)(cb.h1T + (int64_t)(col < F1 ? col : 0) * N + nb);
+      if (RES) {
+        if (hi == 0)
+          mk1 = make_uint2((uint32_t)sm.k.h1[0][col] | ((uint32_t)sm.k.h1[1][col] << 16),
+                           (uint32_t)sm.k.h1[2][col] | ((uint32_t)sm.k.h1[3][col] << 16));
+      } else if (hi == 0) mk1 = *(const uint2*)(cb.h1T + (int64_t)(col < F1 ? col : 0) * N + nb);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -769,8 +811,13 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     if (MLP && cb.ce) {
       if (wave == 0) {
         const int n = nbase + (lane >> 4), o = lane & 15;
-        ce_t = cb.row_table ? cb.row_labels[cb.row_table[n]] : cb.target[n];
-        ce_x = cb.logits[(int64_t)n * F3 + (o < F3 ? o : 0)];
+        if constexpr (RES) {
+          ce_t = sm.k.label[lane >> 4];
+          ce_x = sm.k.logit[lane >> 4][o < F3 ? o : 0];
+        } else {
+          ce_t = cb.row_table ? cb.row_labels[cb.row_table[n]] : cb.target[n];
+          ce_x = cb.logits[(int64_t)n * F3 + (o < F3 ? o : 0)];
+        }
       }
     }
     if constexpr (MLP) lds_barrier();
@@ -782,7 +829,9 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
     uint4 a1v = make_uint4(0u, 0u, 0u, 0u);
     uint2 c1v = make_uint2(0u, 0u);
-    if constexpr (MLP) {
+    if constexpr (RES) {
+      // everything is in LDS already (the image border zeros and zero slots included)
+    } else if constexpr (MLP) {
       static_assert(SPB * IMG * IMG / 4 <= NTHR && SPB * (A1N / 8) <= NTHR, "one vector per thread");
       if (threadIdx.x < SPB * IMG * IMG / 4) {
         const int sl = threadIdx.x / (IMG * IMG / 4), v = threadIdx.x % (IMG * IMG / 4);
@@ -803,8 +852,8 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
           const int u = b - 4 * IMGS, c5 = u % 5;
           bi = (2 + u / 5) * IMGS + (c5 < 2 ? c5 : c5 + IMG);
         }
-        sm.imgb[sl][0][bi] = 0;
-        if (bi > 0) sm.imgb[sl][1][bi - 1] = 0;
+        sm.k.imgb[sl][0][bi] = 0;
+        if (bi > 0) sm.k.imgb[sl][1][bi - 1] = 0;
       }
     } else
     for (int i = threadIdx.x; i < SPB * IMGN; i += NTHR) {
@@ -814,22 +863,22 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       const bool in = n < N && r >= 0 && r < IMG && c >= 0 && c < IMG;
       const float v = x[(int64_t)(n < N ? n : 0) * IMG * IMG + (in ? r * IMG + c : 0)];
       const uint16_t u = c16(in ? v : 0.f);
-      sm.imgb[sl][0][e] = u;
-      if (e > 0) sm.imgb[sl][1][e - 1] = u;
+      sm.k.imgb[sl][0][e] = u;
+      if (e > 0) sm.k.imgb[sl][1][e - 1] = u;
     }
     if (!MLP)
     for (int i = threadIdx.x; i < SPB * (A1N / 8); i += NTHR) {
       const int sl = i / (A1N / 8), e = (i % (A1N / 8)) * 8;
       const int n = nbase + sl, nc = n < N ? n : 0;
       const uint4 v = *(const uint4*)(a1g + (int64_t)nc * A1N + e);
-      *(uint4*)(sm.a1[sl] + e) = v;
+      *(uint4*)(sm.k.a1[sl] + e) = v;
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {  // a1o[e - 1 + j] = a1[e + j]
         if (e + 2 * k > 0) sm.a1o[sl][e + 2 * k - 1] = (uint16_t)(w[k] & 0xffff);
         sm.a1o[sl][e + 2 * k] = (uint16_t)(w[k] >> 16);
       }
-      *(uint2*)(sm.c1[sl] + e) = *(const uint2*)(code1g + (int64_t)nc * A1N + e);
+      *(uint2*)(sm.k.c1[sl] + e) = *(const uint2*)(code1g + (int64_t)nc * A1N + e);
     }
     for (int i = threadIdx.x; i < SPB * (DCN + 16) / 8; i += NTHR) {  // zero dc2 (16-byte stores)
       const int sl = i / ((DCN + 16) / 8), e = (i % ((DCN + 16) / 8)) * 8;
@@ -945,6 +994,19 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
           }
         }
       }
+      if constexpr (RES) {
+        // a1o (a1 shifted by one element) from the LDS-resident a1
+        if (threadIdx.x < SPB * (A1N / 8)) {
+          const int sl = threadIdx.x / (A1N / 8), e = (threadIdx.x % (A1N / 8)) * 8;
+          const uint4 v = *(const uint4*)(sm.k.a1[sl] + e);
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {  // a1o[e - 1 + j] = a1[e + j]
+            if (e + 2 * k > 0) sm.a1o[sl][e + 2 * k - 1] = (uint16_t)(w[k] & 0xffff);
+            sm.a1o[sl][e + 2 * k] = (uint16_t)(w[k] >> 16);
+          }
+        }
+      } else {
       // the staged conv operands, loaded before the chain
       if (threadIdx.x < SPB * IMG * IMG / 4) {
         const int sl = threadIdx.x / (IMG * IMG / 4), p = 4 * (threadIdx.x % (IMG * IMG / 4));
@@ -954,20 +1016,21 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint16_t u = c16(vv[j]);
-          sm.imgb[sl][0][i + j] = u;
-          sm.imgb[sl][1][i + j - 1] = u;
+          sm.k.imgb[sl][0][i + j] = u;
+          sm.k.imgb[sl][1][i + j - 1] = u;
         }
       }
       if (threadIdx.x < SPB * (A1N / 8)) {
         const int sl = threadIdx.x / (A1N / 8), e = (threadIdx.x % (A1N / 8)) * 8;
-        *(uint4*)(sm.a1[sl] + e) = a1v;
+        *(uint4*)(sm.k.a1[sl] + e) = a1v;
         const uint32_t w[4] = {a1v.x, a1v.y, a1v.z, a1v.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {  // a1o[e - 1 + j] = a1[e + j]
           if (e + 2 * k > 0) sm.a1o[sl][e + 2 * k - 1] = (uint16_t)(w[k] & 0xffff);
           sm.a1o[sl][e + 2 * k] = (uint16_t)(w[k] >> 16);
         }
-        *(uint2*)(sm.c1[sl] + e) = c1v;
+        *(uint2*)(sm.k.c1[sl] + e) = c1v;
+      }
       }
     }
     lds_barrier();
@@ -976,7 +1039,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       const int sl = i / A2N, e = i % A2N, co = e / 25, w = e % 25;
       const int n = nbase + sl, nc = n < N ? n : 0;
       const uint16_t g = MLP ? sm.da2[sl][e] : da2g[(int64_t)nc * A2N + e];
-      const uint8_t cd = code2g[(int64_t)nc * A2N + e];
+      const uint8_t cd = RES ? sm.k.c2[sl][e] : code2g[(int64_t)nc * A2N + e];
       if (n < N && cd < 4) {
         const int rr = 2 * (w / Q2) + (cd >> 1), cc = 2 * (w % Q2) + (cd & 1);
         sm.dc2[sl][((rr + 4) * DC + cc + 4) * C2 + co] = g;
@@ -988,11 +1051,11 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       // zero pair at [0..1], 16-bit ones pair at [2..3]: the B operand of the "ones column" whose
       // MFMA output is the bias gradient (row sums of the A operand)
       const uint16_t zo = (k == 2 || k == 3) ? (uint16_t)(kH16 ? 0x3C00 : 0x3F80) : (uint16_t)0;  // 16-bit 1.0
-      sm.a1[sl][A1N + k] = zo;
+      sm.k.a1[sl][A1N + k] = zo;
       sm.a1o[sl][A1N - 1 + k] = 0;
-      sm.c1[sl][A1N + k] = 0xFE;
-      sm.imgb[sl][0][IMGN + k] = zo;
-      sm.imgb[sl][1][IMGN - 1 + k] = 0;
+      sm.k.c1[sl][A1N + k] = 0xFE;
+      sm.k.imgb[sl][0][IMGN + k] = zo;
+      sm.k.imgb[sl][1][IMGN - 1 + k] = 0;
     }
     lds_barrier();
     RK_TR(cb.trace, 8);
@@ -1010,7 +1073,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       const int cof = r < R2 ? (r / R1) * (Q1 * Q1) + ((r / KS) % KS) * Q1 + (r % KS) : -100000;
       // B element j of k-step ks at a1 offset (j<4 ? pa : pb) + ((j&3)>>1)*Q1 + (j&1): 4 pairs,
       // each one aligned 4-byte read from a1 (even x) or a1o (odd x), relative to sample 0's a1
-      constexpr int A1O = (int)(offsetof(BwdSmem, a1o) - offsetof(BwdSmem, a1)) / 2;
+      constexpr int A1O = (int)(offsetof(BwdSmem, a1o) - offsetof(BwdSmem, k.a1)) / 2;
       int pofs[4][4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
@@ -1021,7 +1084,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
           if (r == R2) x = A1N + 2;  // ones pair -> db2
           pofs[ks][k] = (x & 1) ? A1O + x - 1 : x;
         }
-      const uint16_t* a1b = &sm.a1[0][0];
+      const uint16_t* a1b = &sm.k.a1[0][0];
       // 16 k-steps (4 samples x 4), operands of step i + 1 read before step i's MFMA
       auto ld_a = [&](int i) {  // A[co = lo][p]
         return *(const bf16x8*)(sm.dcT[i >> 2] + lo * DTS + 32 * (i & 3) + 8 * hi);
@@ -1059,7 +1122,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       bf16x8 wr[MLP ? K2P : 1];
       if constexpr (MLP) {
 #pragma unroll
-        for (int s = 0; s < K2P; ++s) wr[s] = sm.wfr[s * 64 + lane];
+        for (int s = 0; s < K2P; ++s) wr[s] = sm.k.wfr[s * 64 + lane];
       }
       // pixel (ih, iw) reads dConv2 pixel (ih + 4 - kh, iw + 4 - kw), tap kk = 2s + hi/2; the pad
       // tap kk = 25 has zero weights, so it may read any finite pixel (clamped to tap 24)
@@ -1095,7 +1158,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
             const int s = c * CH + q;
             if (s < K2P) {
               if constexpr (MLP) acc = mfma16(abuf[c & 1][q], wr[s], acc);
-              else acc = mfma16(abuf[c & 1][q], sm.wfr[s * 64 + lane], acc);
+              else acc = mfma16(abuf[c & 1][q], sm.k.wfr[s * 64 + lane], acc);
             }
           }
         }
@@ -1141,7 +1204,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
         const bool va = lo < C1 && wa < Q1 * Q1, vb = lo < C1 && wb < Q1 * Q1;
         const int ia = va ? lo * 196 + wa : A1N, ib = vb ? lo * 196 + wb : A1N;
         const float da = sm.dx2[sl][va ? ia : 0], dbv = sm.dx2[sl][vb ? ib : 0];
-        const uint32_t ca = sm.c1[sl][ia], cb = sm.c1[sl][ib];
+        const uint32_t ca = sm.k.c1[sl][ia], cb = sm.k.c1[sl][ib];
         // windows past the grid have an all-zero A; clamp them to a valid window for B
         const int pa = pos1(min(wa, Q1 * Q1 - 1), 0), pb = pos1(min(wb, Q1 * Q1 - 1), 0);
         const uint32_t ab = c16(da), bb = c16(dbv);
@@ -1150,7 +1213,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
                                     (cb == 0 ? bb : 0u) | (cb == 1 ? bb << 16 : 0u),
                                     (cb == 2 ? bb : 0u) | (cb == 3 ? bb << 16 : 0u));
         const bf16x8 a = __builtin_bit_cast(bf16x8, aw);
-        const uint16_t* ib0 = &sm.imgb[sl][0][0];
+        const uint16_t* ib0 = &sm.k.imgb[sl][0][0];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const uint4 w = make_uint4(*(const uint32_t*)(ib0 + pa * pm[u] + cst[u][0]),
@@ -1265,9 +1328,9 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_bwd(const float* __restrict__
 // backward of a sample depends on another block (the cross-entropy's mean count is derived from the
 // targets alone, every block counts them), so the forward -> backward kernel boundary (a dependent
 // dispatch, ~3.4 us of idle GPU per step, profiles/r3_lenet_step_timeline.json) is not needed.  The
-// two phases share the LDS (union); the backward reads the forward's global outputs (a1, codes,
-// logits, ReLU masks) back from this block's own stores, which the barrier orders (workgroup scope:
-// one CU, coherent L1).
+// two phases share the LDS (union) except the KeepSmem prefix (image, a1, code maps), which the
+// backward reads in place; the forward's other outputs it needs (logits, ReLU masks) come back from
+// this block's own global stores, which the barrier orders (workgroup scope: one CU, coherent L1).
 union TrainSmem {
   FwdSmem f;
   BwdSmem b;
@@ -1278,13 +1341,16 @@ __global__ void __launch_bounds__(NTHR) lenet_train_kernel(const float* __restri
                                                           uint8_t* __restrict__ code1, uint8_t* __restrict__ code2,
                                                           int N, ClsFwd cf, ClsBwd cb, RowSrc rs) {
   __shared__ __attribute__((aligned(16))) TrainSmem sm;
-  fwd_body<true>(sm.f, x, nullptr, b1, nullptr, b2, a1g, code1, nullptr, code2, N, cf, rs);
+  // a1 / codes stay in LDS (sm.f.k == sm.b.k): no global copies (a regular backward after a missed
+  // speculation re-runs rk_lenet_fwd for them, ops/lenet.py)
+  fwd_body<true>(sm.f, x, nullptr, b1, nullptr, b2, nullptr, nullptr, nullptr, nullptr, N, cf, rs);
   __syncthreads();  // LDS reuse + this block's global stores visible to all its waves
   if (rs.rows) {  // the block's targets through the rows (as its own label stores, which it just made)
     cb.row_table = rs.rows;
     cb.row_labels = rs.ysrc;
   }
-  bwd_body<true>(sm.b, x, a1g, code1, nullptr, code2, nullptr, nullptr, nullptr, nullptr, nullptr, N, 1, cb);
+  bwd_body<true, true>(sm.b, x, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, N, 1,
+                       cb);
 }
 
 }  // namespace
@@ -1432,7 +1498,10 @@ RK_API int RKL_NAME(rk_lenet_train)(const float* x, const float* b1, const float
                           void* h2T, float* logits, void* dyT, void* d2T, void* d1T, float* slab, int N,
                           const LenetCE* ce, const RowSrc* rows, hipStream_t s) {
   if (N % 8 || N > 65536 || ((uintptr_t)x & 15) || !slab || !ce || ce->logits != logits) return (int)hipErrorInvalidValue;
-  const RowSrc rs = rows ? *rows : RowSrc{};
+  RowSrc rs = rows ? *rows : RowSrc{};
+  rs.target = ce->target;
+  static const int x_plain = getenv("ROCKET_LENET_X_PLAIN") ? atoi(getenv("ROCKET_LENET_X_PLAIN")) : 0;
+  rs.keep = 1 | (x_plain ? 2 : 0);
   if (rs.rows && (!rs.xsrc || !rs.ysrc || !rs.ydst || ((uintptr_t)rs.xsrc & 15))) return (int)hipErrorInvalidValue;
   const ClsFwd cf{(const bf16x8*)frag, fb1, fb2, fb3, (uint16_t*)a2T, (uint16_t*)h1T, (uint16_t*)h2T, logits, g_fwd_trace};
   const ClsBwd cb = cls_bwd(frag, nullptr, h1T, h2T, dyT, d2T, d1T, slab, ce);

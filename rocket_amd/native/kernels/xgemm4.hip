@@ -67,11 +67,26 @@ __device__ __forceinline__ void x4_dma1(const char* base, int64_t bytes, int64_t
 }
 #endif
 
+// Fused epilogues of the LDS-staged store path (16-bit C, N % 8 == 0).  The staged tile holds
+// t = round16(acc + bias), exactly what an unfused GEMM would have written, so the fused forms keep
+// the unfused numerics:
+//   X4_GELU      c_pre = t (the pre-activation, for the backward), C = round16(gelu(t))
+//   X4_MULGELU   C = round16(t * gelu'(aux)) (aux = the GELU's input z: the input gradient of a GELU
+//                that fed this layer), and colsum[n] += sum over the tile's rows of the f32 product
+//                (the bias gradient of the layer that produced z), one f32 atomic per column per wave
+enum X4EpiKind : int { X4_NONE = 0, X4_GELU = 1, X4_MULGELU = 2 };
+struct X4Epi {
+  void* c_pre;
+  const uint16_t* aux;
+  float* colsum;
+  int kind;
+};
+
 template <bool SPREAD>
 __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                           const uint16_t* __restrict__ B, int64_t ldb, void* C,
                                                           int64_t ldc, int c_dt, const float* __restrict__ bias,
-                                                          int M, int N, int K, int dbg, uint64_t* trace) {
+                                                          int M, int N, int K, int dbg, uint64_t* trace, X4Epi ep) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * X4_STAGE];
   // diagnostics (rk_xgemm4_set_trace): thread 0 stamps s_memrealtime (100 MHz) at block start,
   // prologue done, main loop done, epilogue done, plus the tile id: trace[block][0..4]
@@ -239,6 +254,93 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 7" ::: "memory");
   if (tr && threadIdx.x == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
   const int mb = r0 + 128 * wm, nb = c0 + 128 * wn;
+  if (SPREAD && c_dt != F32 && (N & 7) == 0 && (ldc & 7) == 0) {
+    // 16-bit C through LDS: each wave packs its 128 x 128 tile into its own 32 KiB of the (now idle)
+    // staging ring as 256-B rows, then stores whole rows 16 B per lane (4 rows = 8 full 128-B lines
+    // per instruction).  Writing the fragments straight out (8 B per lane, 32-B pieces of 16 rows per
+    // instruction) measured 15-16 us per 256 x 256 tile — as long as a K = 768 main loop.
+    // Row m_l's 16-B chunk c sits at slot c ^ (m_l & 15): the 16 rows a ds_write_b64 covers land in
+    // 16 different slots.
+    __builtin_amdgcn_s_barrier();  // every wave is done reading the last k-tile's stage
+    asm volatile("" ::: "memory");
+    char* const wb = smem + w * 32768;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = nb + 16 * j + 4 * hi;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (bias && n < N) bv = *(const float4*)(bias + n);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int ml = 16 * i + lo;
+        const int slot = (2 * j + (hi >> 1)) ^ lo;
+        *(uint2*)(wb + ml * 256 + slot * 16 + (hi & 1) * 8) =
+            make_uint2(pack16(acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, c_dt),
+                       pack16(acc[i][j][2] + bv.z, acc[i][j][3] + bv.w, c_dt));
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // own rows only: no barrier needed
+    asm volatile("" ::: "memory");
+    const int rl = lane >> 4, cc = lane & 15;
+    const int n = nb + 8 * cc;
+    if (ep.kind == X4_NONE) {
+#pragma unroll 8
+      for (int q = 0; q < 32; ++q) {
+        const int ml = 4 * q + rl;
+        const uint4 v = *(const uint4*)(wb + ml * 256 + ((cc ^ (ml & 15)) * 16));
+        const int m = mb + ml;
+        if (m < M && n < N) *(uint4*)((uint16_t*)C + (int64_t)m * ldc + n) = v;
+      }
+    } else if (ep.kind == X4_GELU) {
+#pragma unroll 4
+      for (int q = 0; q < 32; ++q) {
+        const int ml = 4 * q + rl;
+        const uint4 v = *(const uint4*)(wb + ml * 256 + ((cc ^ (ml & 15)) * 16));
+        const int m = mb + ml;
+        if (m < M && n < N) {
+          const int64_t off = (int64_t)m * ldc + n;
+          if (ep.c_pre) *(uint4*)((uint16_t*)ep.c_pre + off) = v;
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = pack16(gelu_f(lo16(w[e], c_dt)), gelu_f(hi16(w[e], c_dt)), c_dt);
+          *(uint4*)((uint16_t*)C + off) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    } else {  // X4_MULGELU
+      float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int q = 0; q < 32; ++q) {
+        const int ml = 4 * q + rl;
+        const int m = mb + ml;
+        const bool ok = m < M && n < N;
+        const int64_t off = (int64_t)(ok ? m : 0) * ldc + (ok ? n : 0);
+        const uint4 z = *(const uint4*)(ep.aux + off);  // (any in-range row when !ok: never used)
+        const uint4 v = *(const uint4*)(wb + ml * 256 + ((cc ^ (ml & 15)) * 16));
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w}, zw[4] = {z.x, z.y, z.z, z.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d0 = lo16(w[e], c_dt) * gelu_grad(lo16(zw[e], c_dt));
+          const float d1 = hi16(w[e], c_dt) * gelu_grad(hi16(zw[e], c_dt));
+          cs[2 * e] += ok ? d0 : 0.f;
+          cs[2 * e + 1] += ok ? d1 : 0.f;
+          o[e] = pack16(d0, d1, c_dt);
+        }
+        if (ok) *(uint4*)((uint16_t*)C + off) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      if (ep.colsum) {  // the 4 lanes of a column group (rl = 0..3): one atomic per column per wave
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          cs[e] += __shfl_xor(cs[e], 16, 64);
+          cs[e] += __shfl_xor(cs[e], 32, 64);
+        }
+        if (rl == 0 && n < N) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) atomicAdd(ep.colsum + n + e, cs[e]);
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int n = nb + 16 * j + 4 * hi;
@@ -254,6 +356,7 @@ __global__ void __launch_bounds__(X4_NT, 1) xgemm4_kernel(const uint16_t* __rest
       if (c_dt == F32) *(float4*)((float*)C + (int64_t)m * ldc + n) = make_float4(v0, v1, v2, v3);
       else *(uint2*)((uint16_t*)C + (int64_t)m * ldc + n) = make_uint2(pack16(v0, v1, c_dt), pack16(v2, v3, c_dt));
     }
+  }
   }
   if (tr && threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -593,8 +696,31 @@ RK_API int rk_xgemm4_set_dbg(int bits) {  // diagnostics: bit 0 no in-loop DMA, 
   g_x4_dbg = bits;
   return 0;
 }
+static int xgemm4_launch(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int c_dt,
+                         const float* bias, int M, int N, int K, X4Epi ep, hipStream_t s);
+
 RK_API int rk_xgemm4(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int c_dt,
                      const float* bias, int M, int N, int K, hipStream_t s) {
+  return xgemm4_launch(a, lda, b, ldb, c, ldc, c_dt, bias, M, N, K, X4Epi{nullptr, nullptr, nullptr, X4_NONE}, s);
+}
+
+// C[M][N] = epi(A[M][K] B[N][K]^T + bias) on the spread-DMA 256x256 kernel with the LDS-staged epilogue
+// (16-bit C, N % 8 == 0, ldc % 8 == 0): epi 0 none, 1 GELU (c_pre = pre-activation, may be null),
+// 2 multiply by gelu'(aux) (+ colsum[n] += column sums of the f32 product, colsum may be null).
+RK_API int rk_xgemm4_epi(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int c_dt,
+                         const float* bias, void* c_pre, const void* aux, float* colsum, int epi, int M, int N, int K,
+                         hipStream_t s) {
+  if (c_dt == F32 || N % 8 || ldc % 8 || epi < 0 || epi > 2 || (epi == X4_MULGELU && !aux)) return (int)hipErrorInvalidValue;
+  const int saved = g_x4_dbg;
+  g_x4_dbg = 32;  // the spread schedule (the fused epilogues live in its LDS-staged store path)
+  const int rc = xgemm4_launch(a, lda, b, ldb, c, ldc, c_dt, bias, M, N, K,
+                               X4Epi{c_pre, (const uint16_t*)aux, colsum, epi}, s);
+  g_x4_dbg = saved;
+  return rc;
+}
+
+static int xgemm4_launch(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int c_dt,
+                         const float* bias, int M, int N, int K, X4Epi ep, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0 || K % X4_BK || N % 4 || ((uintptr_t)a | (uintptr_t)b) % 16 || (lda * 2) % 16 || (ldb * 2) % 16)
     return (int)hipErrorInvalidValue;
@@ -618,9 +744,64 @@ RK_API int rk_xgemm4(const void* a, int64_t lda, const void* b, int64_t ldb, voi
   }
   if (g_x4_dbg & 32)
     xgemm4_kernel<true><<<tiles, X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc, c_dt, bias, M,
-                                                N, K, g_x4_dbg, g_x4_trace);
+                                                N, K, g_x4_dbg, g_x4_trace, ep);
   else
     xgemm4_kernel<false><<<tiles, X4_NT, 0, s>>>((const uint16_t*)a, lda, (const uint16_t*)b, ldb, c, ldc, c_dt, bias, M,
-                                                 N, K, g_x4_dbg, g_x4_trace);
+                                                 N, K, g_x4_dbg, g_x4_trace, ep);
+  return (int)hipGetLastError();
+}
+
+// 16-bit transpose dst[c][r] = src[r][c] (rows x cols, both dense): the transformer MLP's input-gradient
+// GEMM reads fc2's weight as the forward layout's B operand (K contiguous) from this copy.  64 x 64
+// tiles through LDS (row pitch 66 elements: the column reads hit 32 distinct banks), 16-byte global
+// reads, 4-byte global writes of row-contiguous pairs.
+namespace {
+__global__ void __launch_bounds__(256) transpose16_kernel(const uint16_t* __restrict__ src, int rows, int cols,
+                                                          uint16_t* __restrict__ dst) {
+  __shared__ uint16_t t[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  // load: 64 rows x 8 chunks of 8 elements; thread -> (row tid / 8 + 32 k, chunk tid % 8)
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int r = threadIdx.x / 8 + 32 * k, ch = threadIdx.x % 8;
+    const int gr = r0 + r, gc = c0 + 8 * ch;
+    uint16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (gr < rows && gc + 8 <= cols) {
+      const uint4 q = *(const uint4*)(src + (int64_t)gr * cols + gc);
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = (uint16_t)(w[e] & 0xffff);
+        v[2 * e + 1] = (uint16_t)(w[e] >> 16);
+      }
+    } else if (gr < rows) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (gc + e < cols) v[e] = src[(int64_t)gr * cols + gc + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[r][8 * ch + e] = v[e];
+  }
+  __syncthreads();
+  // store: dst row (c0 + c) holds src rows r0 .. r0+63 of column c; thread -> (c = tid / 4 .. , pair)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = threadIdx.x / 32 + 8 * k, rp = threadIdx.x % 32;  // rows 2 rp, 2 rp + 1
+    const int gc = c0 + c, gr = r0 + 2 * rp;
+    if (gc >= cols) continue;
+    if (gr + 1 < rows) {
+      *(uint32_t*)(dst + (int64_t)gc * rows + gr) = (uint32_t)t[2 * rp][c] | ((uint32_t)t[2 * rp + 1][c] << 16);
+    } else if (gr < rows) {
+      dst[(int64_t)gc * rows + gr] = t[2 * rp][c];
+    }
+  }
+}
+}  // namespace
+
+RK_API int rk_transpose16(const void* src, int rows, int cols, void* dst, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (((uintptr_t)src | (uintptr_t)dst) & 15 || cols % 8 || rows % 2) return (int)hipErrorInvalidValue;
+  const dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  transpose16_kernel<<<grid, 256, 0, s>>>((const uint16_t*)src, rows, cols, (uint16_t*)dst);
   return (int)hipGetLastError();
 }

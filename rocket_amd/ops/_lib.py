@@ -47,6 +47,9 @@ KERNEL_SIGS = {
     "rk_xgemm4_set_trace": (c_int, [c_void_p]),
     "rk_xgemm4": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_int, c_int, c_int,
                           c_void_p]),
+    "rk_xgemm4_epi": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "rk_transpose16": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "rk_slab_acc": (c_int, [c_void_p, c_int, c_int, c_int64, c_void_p, c_int, c_void_p]),
     "rk_conv_fwd": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 11 + [c_void_p, c_void_p]),
     "rk_conv_fwd_c8": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p] + [c_int] * 10 + [c_void_p, c_void_p]),

@@ -300,7 +300,7 @@ class _RowSrc(ctypes.Structure):
     """Mirror of ``struct RowSrc`` (lenet_conv.hip): the batch gathered by the step kernel itself."""
 
     _fields_ = [("rows", ctypes.c_void_p), ("xsrc", ctypes.c_void_p), ("ysrc", ctypes.c_void_p),
-                ("ydst", ctypes.c_void_p)]
+                ("ydst", ctypes.c_void_p), ("target", ctypes.c_void_p), ("keep", ctypes.c_int)]
 
 
 def _claim_rows(x, target):
@@ -482,6 +482,13 @@ class _LeNetFused(torch.autograd.Function):
                                       dev_scale)
         if spec is not None:
             ctx.frags.spec_misses += 1  # the loss was not the fused cross-entropy on those targets
+            # the whole-step launch kept a1 and the code maps in LDS (no global copies): the
+            # regular backward below needs them, so the forward launch recomputes them (same values)
+            cw = [p.detach().float().contiguous() for p in ctx.params]
+            _lib.check(_k(lib, "rk_lenet_fwd", ctx.frags.half)(
+                x.data_ptr(), cw[0].data_ptr(), cw[1].data_ptr(), cw[2].data_ptr(), cw[3].data_ptr(), frag.data_ptr(),
+                cw[5].data_ptr(), cw[7].data_ptr(), cw[9].data_ptr(), a1.data_ptr(), c1.data_ptr(), c2.data_ptr(),
+                a2T.data_ptr(), h1T.data_ptr(), h2T.data_ptr(), logits.data_ptr(), N, stream), "rk_lenet_fwd")
         if ctx.ce_spec is not None:
             target, grad_scale, accum, loss_out, dev_scale = ctx.ce_spec
             ctx.ce_spec = None

@@ -49,6 +49,13 @@ from rocket_amd.ops.mgemm import mgemm, pick_split
 #                  dgrad, split-K wgrad with the bias gradient from the same launch); the only route
 #                  with fp16 operands (the GELU runs as its own streaming kernel)
 MODE = os.environ.get("ROCKET_VIT_GEMM", "lib")
+# The transformer MLP's two GEMMs whose neighbours are streaming GELU passes run on the native 256x256
+# kernel (native/kernels/xgemm4.hip) with the GELU fused into their epilogues, beside any MODE:
+#   fc1 forward       z = x W1^T + b1 and h = gelu(z) from ONE launch (no gelu_fwd pass);
+#   fc2 input grad    dz = (dy W2) * gelu'(z) and db1 += colsum(dz) from ONE launch (no GELU-backward
+#                     + column-sum pass; W2 read through a per-step transposed bf16 copy).
+# ROCKET_VIT_X4_MLP=0 keeps them on the MODE's engine with separate GELU kernels.
+X4_MLP = os.environ.get("ROCKET_VIT_X4_MLP", "1") != "0"
 _TILE_WIDE_FWD, _TILE_DEFAULT = 4, 0
 
 
@@ -249,6 +256,47 @@ def _gelu_bwd(dh: torch.Tensor, z: torch.Tensor) -> torch.Tensor:
     return dz
 
 
+def _x4_ok(x2: torch.Tensor, K: int, N: int) -> bool:
+    """Shapes / dtype the fused-epilogue x4 kernel takes: bf16 operands, K % 64, N % 8."""
+    return X4_MLP and x2.dtype == torch.bfloat16 and K % 64 == 0 and N % 8 == 0 and x2.data_ptr() % 16 == 0
+
+
+def _x4_fwd_gelu(x2: torch.Tensor, w16: torch.Tensor, bias: torch.Tensor):
+    """(z, h = gelu(z)) of ``x2 @ w16^T + bias`` from one launch (rk_xgemm4_epi, GELU epilogue)."""
+    M, K = x2.shape
+    N = w16.shape[0]
+    z = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
+    h = torch.empty_like(z)
+    b = bias.detach().float().contiguous()
+    _lib.check(_lib.kernels().rk_xgemm4_epi(x2.data_ptr(), K, w16.data_ptr(), K, h.data_ptr(), N,
+                                            _lib.dtype_code(h), b.data_ptr(), z.data_ptr(), None, None, 1, M, N, K,
+                                            _lib.stream_ptr(x2.device)), "rk_xgemm4_epi")
+    return z, h
+
+
+def _x4_dgrad_gelu(dy2: torch.Tensor, w16: torch.Tensor, z: torch.Tensor, bias: torch.Tensor | None):
+    """dz = (dy2 @ w16) * gelu'(z) with the bias gradient of the layer that produced z (column sums
+    of dz) accumulated by the same launch; returns (dz, db) with db None when it went straight into
+    a persistent ``bias.grad`` (or when ``bias`` is None)."""
+    M, N = dy2.shape
+    K = w16.shape[1]  # dz columns
+    wt = torch.empty(K, N, dtype=w16.dtype, device=w16.device)  # w16^T: the forward layout's B operand
+    lib = _lib.kernels()
+    stream = _lib.stream_ptr(dy2.device)
+    _lib.check(lib.rk_transpose16(w16.data_ptr(), N, K, wt.data_ptr(), stream), "rk_transpose16")
+    dz = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
+    db = None
+    if bias is not None:
+        direct = _direct(bias)
+        db = bias.grad if direct else torch.zeros(K, dtype=torch.float32, device=dy2.device)
+    _lib.check(lib.rk_xgemm4_epi(dy2.data_ptr(), N, wt.data_ptr(), N, dz.data_ptr(), K, _lib.dtype_code(dz), None,
+                                 None, z.data_ptr(), _lib.ptr(db), 2, M, K, N, stream), "rk_xgemm4_epi")
+    if bias is not None and _direct(bias):
+        grad_ready(bias)
+        return dz, None
+    return dz, db
+
+
 def _gelu_bwd_bias(dh: torch.Tensor, z: torch.Tensor, bias: torch.Tensor):
     """(dz = dh * gelu'(z), column sums of dz added to the bias gradient) in one launch; returns
     (dz, db) with db None when it went straight into a persistent ``bias.grad``."""
@@ -282,8 +330,11 @@ class _MMlpFn(torch.autograd.Function):
         K = shape[-1]
         N = w2_16.shape[0]
         x2 = _as_16_2d(x, K, w1_16.dtype)
-        z = _linear_fwd(x2, w1_16, b1, b1_16)
-        h = _gelu_fwd(z)
+        if MODE != "x" and _x4_ok(x2, K, w1_16.shape[0]):
+            z, h = _x4_fwd_gelu(x2, w1_16, b1)  # GELU in the GEMM epilogue
+        else:
+            z = _linear_fwd(x2, w1_16, b1, b1_16)
+            h = _gelu_fwd(z)
         y = _linear_fwd(h, w2_16, b2, b2_16)
         ctx.save_for_backward(x2, z, h, w1_16, w2_16)
         ctx.params = (w1, b1, w2, b2)
@@ -304,6 +355,10 @@ class _MMlpFn(torch.autograd.Function):
             # dz = gelu'(z) * (dy W2) by the streaming kernel; fc1's bias gradient comes out of
             # its wgrad launch (row sums of dz)
             dz = _gelu_bwd(_linear_dgrad(dy2, w2_16), z)
+        elif MODE != "x" and _x4_ok(dy2, N, z.shape[1]) and z.dtype == torch.bfloat16:
+            # gelu'(z) and fc1's bias gradient in fc2's input-gradient GEMM epilogue
+            dz, db1 = _x4_dgrad_gelu(dy2, w2_16, z, b1 if need_b1 else None)
+            need_b1 = False
         elif MODE == "lib" and need_b1:
             # GELU backward and fc1's bias gradient in one pass over the [tokens, hidden] gradient
             dz, db1 = _gelu_bwd_bias(_linear_dgrad(dy2, w2_16), z, b1)
