@@ -76,20 +76,22 @@ class Dataset(Capsule):
 
     def launch(self, attrs: Attributes | None = None) -> None:
         Capsule.launch(self, attrs=attrs)
-        if attrs is None or attrs.batch is not None:
+        # (per-iteration path: the buffer's keys through dict methods, not the attribute hook)
+        if attrs is None or attrs.get("batch") is not None:
             return
         data = next(self._iterator, None) if self._iterator is not None else None
+        looper = attrs.get("looper")
         if data is None:
-            attrs.batch = None
-            if attrs.looper is not None:
-                attrs.looper.terminate = True
+            attrs["batch"] = None
+            if looper is not None:
+                looper["terminate"] = True
             return
         if getattr(self._active_dataloader, "device_resident", False):
-            attrs.batch = data  # device/host loaders already delivered the batch on the device
+            attrs["batch"] = data  # device/host loaders already delivered the batch on the device
         else:
-            attrs.batch = torch_move(data, self._accelerator.device)
-        if attrs.looper is not None:
-            attrs.looper.terminate = False
+            attrs["batch"] = torch_move(data, self._accelerator.device)
+        if looper is not None:
+            looper["terminate"] = False
         self._batch_idx += 1
 
     def destroy(self, attrs: Attributes | None = None) -> None:

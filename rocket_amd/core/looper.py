@@ -120,7 +120,7 @@ class Looper(Dispatcher):
             for i in range(self._repeats):
                 attrs["batch"] = None
                 Dispatcher.launch(self, attrs)
-                if attrs.looper.terminate:
+                if attrs["looper"]["terminate"]:
                     break
                 if bar is not None:
                     now = time.monotonic()

@@ -74,10 +74,10 @@ class Module(Dispatcher):
             self._graphs = StepGraphs(self, warmup=self._warmup)
 
     def launch(self, attrs: Attributes | None = None) -> None:
-        if attrs is None or attrs.batch is None:
+        if attrs is None or attrs.get("batch") is None:
             return
         if not self._gathers_rows:  # a deferred device-loader batch the model does not gather itself
-            materialize_batch(attrs.batch)
+            materialize_batch(attrs["batch"])
         train = torch.is_grad_enabled()
         if self._module.training != train:  # a recursive .train() costs ~20 us per iteration
             self._module.train(train)

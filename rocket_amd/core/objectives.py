@@ -151,10 +151,11 @@ class Loss(Capsule):
         value = LazyScalar(self._ring_views[self._slot_host])
         self._lap.append(weakref.ref(value))
         self._slot_host = (self._slot_host + 1) % self.RING
-        if attrs.tracker is not None:
-            attrs.tracker.scalars.append(Attributes(step=self._step, data={self._tag: value}))
-        if attrs.looper is not None:
-            attrs.looper.state.loss = value
+        tracker, looper = attrs.get("tracker"), attrs.get("looper")
+        if tracker is not None:
+            tracker.scalars.append(Attributes(step=self._step, data={self._tag: value}))
+        if looper is not None:
+            looper["state"]["loss"] = value
         self._step += 1
 
     def state_dict(self) -> dict:
@@ -196,10 +197,11 @@ class Optimizer(Capsule):
             return
         data = {f"{self._tag}.lr.{i}": g.get("lr") for i, g in enumerate(self._optimizer.param_groups)}
         if attrs is not None:
-            if attrs.tracker is not None:
-                attrs.tracker.scalars.append(Attributes(step=self._iter_idx, data=data))
-            if attrs.looper is not None:
-                attrs.looper.state.lr = list(data.values())
+            tracker, looper = attrs.get("tracker"), attrs.get("looper")
+            if tracker is not None:
+                tracker.scalars.append(Attributes(step=self._iter_idx, data=data))
+            if looper is not None:
+                looper["state"]["lr"] = list(data.values())
         self._iter_idx += 1
 
     def launch(self, attrs: Attributes | None = None) -> None:

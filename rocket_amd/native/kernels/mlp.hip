@@ -20,6 +20,8 @@
 #include "optim_common.h"
 #include "rows_common.h"
 
+#include <cstdlib>
+
 using namespace rk;
 
 // 16-bit format of every activation / fragment / weight-gradient operand: bf16 (default) or, when
@@ -445,12 +447,18 @@ __device__ __forceinline__ bf16x8 rowfrag(const uint16_t* T, int R, int M, int r
 }
 
 
+template <bool LDSV>
 __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks,
-                           const StepFill& sf);
+                           const StepFill& sf, char* stage);
 
+// LDSV: the tiles' operands arrive by LDS-DMA in whole 256-B row segments (16 KiB per wave: its 32 rows
+// of d^T and x^T over its 128 batch elements) and the MFMA fragments are read back from LDS, instead of
+// fragment-shaped global loads (16 rows x 64 B per instruction: half cache lines).  M % 512 == 0.
+template <bool LDSV>
 __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8] = __builtin_amdgcn_s_memrealtime();
-  __shared__ float red[NW][32 * 32];
+  __shared__ __attribute__((aligned(1024))) char stage[LDSV ? NW * 16384 : NW * 32 * 32 * 4];
+  float (*red)[32 * 32] = (float (*)[32 * 32])stage;  // (LDSV: reused once the staged operands are read)
   __shared__ float rsum[NW][32];
   __shared__ rk_opt::AdamStep s_ks[kEpiGroups];
   __shared__ float s_cnt[NW];
@@ -470,14 +478,15 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
     if ((int)blockIdx.x - a.tiles < a.nslab) slab_reduce_block(a, blockIdx.x - a.tiles, red, ks, sf);
     else loss_fin_block(a.lf, red, sf);
   } else {
-    wgrad_tile(a, red, rsum, ks, sf);
+    wgrad_tile<LDSV>(a, red, rsum, ks, sf, stage);
   }
   if (a.epi.on) rk_opt::advance_step(a.epi.step, a.epi.counter, false, cur);
   if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
 }
 
+template <bool LDSV>
 __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks,
-                           const StepFill& sf) {
+                           const StepFill& sf, char* stage) {
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < 3; ++i)
@@ -509,6 +518,48 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float rs[2] = {0.f, 0.f};
+  if constexpr (LDSV) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // wave region: [32 d rows][256 B] then [32 x rows][256 B]; row r's 16-B chunk c at c ^ (r & 15)
+    // (the 16 rows a ds_read_b128 lane group reads hit 16 different bank slots); the LDS-DMA image
+    // is lane-linear, so the swizzle is applied to each lane's SOURCE chunk
+    char* const wst = stage + wv * 16384;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {  // 16 x 1 KiB: 4 rows x 256 B each
+      const int r = 4 * (q & 7) + (lane >> 4), c = lane & 15;
+      const uint16_t* T = q < 8 ? P.dT : P.xT;
+      const int R = q < 8 ? P.N : P.K, r0 = q < 8 ? n0 : k0;
+      const int gr = min(r0 + r, R - 1);  // rows past the edge: any valid row (their outputs are not stored)
+      const uint16_t* src = T + (int64_t)gr * a.M + mb + 8 * (c ^ (r & 15));
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(wst + q * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      bf16x8 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ra = 16 * i + lo;
+        af[i] = *(const bf16x8*)(wst + ra * 256 + (((4 * s4 + hi) ^ (ra & 15)) * 16));
+        bf[i] = *(const bf16x8*)(wst + 8192 + ra * 256 + (((4 * s4 + hi) ^ (ra & 15)) * 16));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool rin = n0 + 16 * i + lo < P.N;  // clamped rows must not enter the row sums
+        const uint4 aw = __builtin_bit_cast(uint4, af[i]);
+        const uint32_t awd[4] = {aw.x, aw.y, aw.z, aw.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          rs[i] += rin ? d16((uint16_t)(awd[j] & 0xffffu)) + d16((uint16_t)(awd[j] >> 16)) : 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+      }
+    }
+    __syncthreads();  // every wave done with its staged operands: `red` (aliased) may be written
+#endif
+  } else
   for (int m = mb; m < me; m += 128) {  // four k-steps per iteration, all loads issued first
     bf16x8 af[4][2], bf[4][2];
 #pragma unroll
@@ -753,7 +804,11 @@ RK_API int RKL_NAME(rk_mlp3_wgrad_loss)(int nprob, const void* const* dT, const 
     a.has_rows = 1;
     extra += 1;
   }
-  mlp3_wgrad_kernel<<<tiles + extra, NT, 0, s>>>(a);
+  // LDS-staged tile operands (mlp3_wgrad_kernel<true>) when every wave's batch range is 128 rows;
+  // ROCKET_WGRAD_LDS=0 keeps the fragment-shaped global loads
+  static const int lds_env = getenv("ROCKET_WGRAD_LDS") ? atoi(getenv("ROCKET_WGRAD_LDS")) : 1;
+  if (lds_env && M == NW * 128) mlp3_wgrad_kernel<true><<<tiles + extra, NT, 0, s>>>(a);
+  else mlp3_wgrad_kernel<false><<<tiles + extra, NT, 0, s>>>(a);
   return (int)hipGetLastError();
 }
 

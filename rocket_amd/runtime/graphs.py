@@ -175,11 +175,13 @@ class StepGraphs:
         self._toks = None
         self._params = None  # parameter list for the version token (fixed once graphs exist)
         self._dev = None
+        self._bcache: dict = {}  # id(batch) -> (batch, tensors, signature, persistent key) of ring slots
         self.launch_lists = 0  # captured parts replayed as native launch lists
         self.launch_list_reason = None  # why a part kept hipGraphLaunch replay (first such part)
 
     def release(self) -> None:
         self.variants.clear()
+        self._bcache.clear()
         self.pool = None
         self.disabled_reason = self.disabled_reason or "released"
 
@@ -240,13 +242,21 @@ class StepGraphs:
         """Run the micro-step through a graph; False -> the caller runs it eagerly."""
         if self.disabled_reason is not None:
             return False
-        batch = attrs.batch
-        tens = _tensors(batch)
-        if not tens or any(t.device.type != "cuda" for t in tens):
-            return False
+        batch = attrs.get("batch")
+        ent = self._bcache.get(id(batch))
+        if ent is not None and ent[0] is batch:
+            # a loader ring slot seen before (the same tuple of persistent buffers: fixed shapes)
+            _, tens, bsig, pkey = ent
+        else:
+            tens = _tensors(batch)
+            if not tens or any(t.device.type != "cuda" for t in tens):
+                return False
+            bsig = _signature(batch)
+            pkey = tuple(t.data_ptr() if getattr(t, "_rocket_persistent", False) else 0 for t in tens)
+            if type(batch) is tuple and all(pkey) and len(self._bcache) < 64:
+                self._bcache[id(batch)] = (batch, tens, bsig, pkey)
         sync = self._predict_sync()
-        sig = (sync, _signature(batch))
-        pkey = tuple(t.data_ptr() if getattr(t, "_rocket_persistent", False) else 0 for t in tens)
+        sig = (sync, bsig)
         key = (sig, pkey)
         v = self.variants.get(key)
         if v is None:
@@ -511,7 +521,7 @@ class StepGraphs:
     def _replay(self, v: _Captured, attrs: Attributes, tens: List[torch.Tensor]) -> None:
         from rocket_amd.runtime.data import pending_rows
 
-        pend = pending_rows(attrs.batch)
+        pend = pending_rows(attrs.get("batch"))
         if pend is not None:
             if v.rows_in_graph:
                 pend.done = pend.advanced = True  # the replay below gathers it and advances the cursor
@@ -526,7 +536,7 @@ class StepGraphs:
         if rep is not None:
             rep.check_comm()  # P2P peer timeouts surface at the next step (one host load)
         self._run(v, rep if len(v.graphs) > 1 else None)
-        attrs.batch = v.out
+        attrs["batch"] = v.out
         self._host(attrs)
 
 
