@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from rocket_amd.ops.iconv import IConv2d, conv_entry, stem_ok
+from rocket_amd.ops.iconv import IConv2d, bn_relu_conv, conv_entry, stem_ok
 from rocket_amd.ops.linear import LibLinear, native_route
 from rocket_amd.ops.norm import BatchNormAct2d
 from rocket_amd.ops.pool import global_avg_pool
@@ -54,8 +54,8 @@ class BasicBlock(nn.Module):
         # conv1 and the shortcut as one node: x's two input gradients meet in conv1's dgrad epilogue
         y1, short = conv_entry(x, self.conv1, self.down[0] if self.down is not None else None)
         identity = short if self.down is None else self.down[1](short)
-        out = self.bn1(y1)
-        return self.bn2(self.conv2(out), residual=identity)
+        # conv2(relu(bn1(y1))): bn1 applied inside conv2's operand staging (ops/iconv.py bn_relu_conv)
+        return self.bn2(bn_relu_conv(self.bn1, self.conv2, y1), residual=identity)
 
 
 class Bottleneck(nn.Module):
@@ -77,9 +77,10 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         y1, short = conv_entry(x, self.conv1, self.down[0] if self.down is not None else None)
         identity = short if self.down is None else self.down[1](short)
-        out = self.bn1(y1)
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), residual=identity)
+        # bn1 / bn2 (+ ReLU) folded into conv2 / conv3 where the fold applies (stride-1 consumer)
+        out = bn_relu_conv(self.bn1, self.conv2, y1)
+        out = bn_relu_conv(self.bn2, self.conv3, out)
+        return self.bn3(out, residual=identity)
 
 
 class ResNet(nn.Module):

@@ -26,6 +26,8 @@ using namespace rk;
 
 namespace {
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
 enum ConvMode : int { kConvFwd = 0, kConvDgrad = 1, kConvWgrad = 2, kConvDgradS = 3, kConvFwdC8 = 4 };
 
 // Strided input gradient, one GEMM per parity class (py, px) of the dX pixels: pixel
@@ -60,6 +62,12 @@ struct ConvGeom {
   const float* bnb_mean;
   const float* bnb_invstd;
   float* bnb_part;
+  // BatchNorm-apply prologue (fwd A / wgrad B gather): the gathered tensor is a BatchNorm's INPUT z
+  // and the operand is relu(z*scale + shift) [2][C] (scale, shift), formed in registers between the
+  // load and the LDS write; padding chunks stay zero.  bnb_ss (BNB dgrad): the ReLU mask is
+  // recomputed from bnb_x the same way instead of read from bnb_mask.
+  const float* pro_ss;
+  const float* bnb_ss;
   int w_s;               // strided dgrad: the weight's full kernel width S (tap index r*S + s)
   int ncls;              // strided dgrad: parity classes in the launch
   int zero_nb;           // strided dgrad, 1x1 kernel: only class (0, 0) has taps; its tiles also zero
@@ -80,6 +88,25 @@ __device__ __forceinline__ void split_pixel(int m, const ConvGeom& cg, int& n, i
   n = nn;
 }
 
+// relu(z*scale + shift) of 8 16-bit channels (scale / shift: 8 f32 at sc / sc + C in LDS), or zero
+// for a padding chunk — the same fp32 expression (and rounding) as norm.hip bn_apply_kernel
+constexpr int kProMaxC = 512;  // channels of a prologue's scale / shift table (LDS, host-checked)
+template <bool H>
+__device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const float* sc, int C, bool ok) {
+  const f32x4 a0 = *(const f32x4*)sc, a1 = *(const f32x4*)(sc + 4);
+  const f32x4 b0 = *(const f32x4*)(sc + C), b1 = *(const f32x4*)(sc + C + 4);
+  const float a[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+  const float b[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  u32x4 o;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float lo = fmaxf(__builtin_fmaf(lo16t<H>(v[p]), a[2 * p], b[2 * p]), 0.f);
+    const float hi = fmaxf(__builtin_fmaf(hi16t<H>(v[p]), a[2 * p + 1], b[2 * p + 1]), 0.f);
+    o[p] = ok ? pack16t<H>(lo, hi) : 0u;
+  }
+  return o;
+}
+
 // Gathered row-image operand (forward / dgrad A): rows are grid pixels, k runs over (r, s, c).
 // A lane's rows are fixed for the whole block, only the k-tile's tap (r, s) and channel offset c0
 // change (wave-uniform): so the per-lane work of a k-tile is one pointer add of a scalar offset, a
@@ -90,6 +117,7 @@ struct GatherRows {
   static constexpr int NI = R * BK / (512 * NW), CPR = BK / 8;
   const char* p0[NI];  // the lane's chunk at tap (0, 0), c0 = 0 (may point outside x: never read then)
   uint32_t vmask[NI];  // bit r*S + s: tap (r, s) inside the image, and the row inside M
+  int chl[NI];         // the lane's channel offset within a k-tile (prologue scale / shift index)
   __device__ __forceinline__ void init(const uint16_t* x, const ConvGeom& cg, int row0, int M, int wid, int lane) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -107,7 +135,8 @@ struct GatherRows {
         h0 = gh + cg.hoff;
         w0 = gw + cg.woff;
       }
-      const int64_t e = ((int64_t)(n * cg.H + h0) * cg.W + w0) * cg.C + (c ^ rswz<BK>(r)) * 8;
+      chl[i] = (c ^ rswz<BK>(r)) * 8;
+      const int64_t e = ((int64_t)(n * cg.H + h0) * cg.W + w0) * cg.C + chl[i];
       p0[i] = (const char*)x + e * 2;
       uint32_t v = 0;
       if (m < M) {
@@ -134,6 +163,28 @@ struct GatherRows {
       const char* src = ok ? p0[i] + soff : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0, 0);
     }
+  }
+  // prologue form: the k-tile's chunks into registers (padding: the zero page, flagged in okm)
+  __device__ __forceinline__ void load(const ConvGeom& cg, int tr, int ts, int c0, const char* zero, u32x4 (&v)[NI],
+                                       uint32_t& okm) const {
+    const int64_t tap_off = (int64_t)(tr * cg.W + ts) * cg.C;
+    const int64_t soff = ((MODE == kConvFwd ? tap_off : -tap_off) + c0) * 2;
+    const int bit = tr * cg.S + ts;
+    okm = 0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const bool ok = (vmask[i] >> bit) & 1u;
+      okm |= (uint32_t)ok << i;
+      v[i] = *(const u32x4*)(ok ? p0[i] + soff : zero);
+    }
+  }
+  // ... transformed and written to the k-tile's LDS image (the DMA's lane-linear layout)
+  template <bool H>
+  __device__ __forceinline__ void put(char* lds, int wid, int lane, const u32x4 (&v)[NI], uint32_t okm,
+                                      const float* tab, int C, int c0) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      *(u32x4*)(lds + (wid * NI + i) * 1024 + lane * 16) = bn_relu8<H>(v[i], tab + c0 + chl[i], C, (okm >> i) & 1u);
   }
 };
 
@@ -190,6 +241,7 @@ struct GatherCols {
   int m[NI], oh[NI], ow[NI], hs[NI], ws[NI];  // pixel, its output row / col, window row / col + tap
   int64_t e[NI];                              // element offset of the lane's chunk at that pixel
   bool cok[NI];
+  int chn[NI];                                // the lane's channel (prologue scale / shift index)
   // per-k-tile increments (wave-uniform): BK pixels = qn images + qh rows + qw columns
   int qw, qh, qn;
   int64_t d_w, d_wc, d_h, d_hc, d_n;
@@ -212,6 +264,7 @@ struct GatherCols {
       const int cc = cok[i] ? col : 0;
       const int tap = cc / cg.C;
       const int ci = cc - tap * cg.C;
+      chn[i] = ci;
       const int tr = tap / cg.S, ts = tap - tr * cg.S;
       m[i] = kb + k;
       int n, h, w;
@@ -226,13 +279,36 @@ struct GatherCols {
   // the current k-tile (rows m .. of every lane), then advance every lane's row by BK pixels
   __device__ __forceinline__ void issue(const uint16_t* x, const ConvGeom& cg, int kend, char* lds, int wid,
                                         const char* zero) {
-    const int st = cg.stride;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const bool ok = cok[i] && m[i] < kend && (unsigned)hs[i] < (unsigned)cg.H && (unsigned)ws[i] < (unsigned)cg.W;
       const char* src = ok ? (const char*)(x + e[i]) : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + (wid * NI + i) * 1024), 16, 0, 0);
     }
+    advance(cg);
+  }
+  // prologue form of issue: the chunks into registers (zero page + okm flag for padding / tails)
+  __device__ __forceinline__ void load(const uint16_t* x, const ConvGeom& cg, int kend, const char* zero,
+                                       u32x4 (&v)[NI], uint32_t& okm) {
+    okm = 0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const bool ok = cok[i] && m[i] < kend && (unsigned)hs[i] < (unsigned)cg.H && (unsigned)ws[i] < (unsigned)cg.W;
+      okm |= (uint32_t)ok << i;
+      v[i] = *(const u32x4*)(ok ? (const char*)(x + e[i]) : zero);
+    }
+    advance(cg);
+  }
+  template <bool H>
+  __device__ __forceinline__ void put(char* lds, int wid, int lane, const u32x4 (&v)[NI], uint32_t okm,
+                                      const float* tab, int C) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      *(u32x4*)(lds + (wid * NI + i) * 1024 + lane * 16) = bn_relu8<H>(v[i], tab + chn[i], C, (okm >> i) & 1u);
+  }
+  // every lane's row moves on by BK pixels
+  __device__ __forceinline__ void advance(const ConvGeom& cg) {
+    const int st = cg.stride;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       m[i] += BK;
@@ -329,7 +405,7 @@ __device__ __forceinline__ void lds_barrier() {
 // reads the BN input / mask byte of its chunks row-contiguously like the store, and the per-thread
 // sums are combined (xor-shuffles over the lanes sharing the chunk, then LDS over the waves) into one
 // [2][BN] partial row per 128-row tile.
-template <int BM, int BN, int WM, int WN, int FM, int FN, bool BNB, bool H, typename RowMap>
+template <int BM, int BN, int WM, int WN, int FM, int FN, bool BNB, bool H, typename RowMap, bool BNX = false>
 __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& cg, f32x4 (&acc)[FM][FN], char* smem,
                                                int row0, int col0, int tm, int wm, int wn, int lane,
                                                const RowMap& rowmap) {
@@ -337,7 +413,7 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
   static_assert(TM * CPR % NT == 0 && NT % CPR == 0 && CPR <= 64, "whole chunk passes, fixed chunk column");
   float* img = (float*)smem;
   const int cc = ((int)threadIdx.x % CPR) * 8;  // this thread's chunk column (fixed: NT % CPR == 0)
-  float s1[8], s2[8], mu[8], is[8];
+  float s1[8], s2[8], mu[8], is[8], qa[BNX ? 8 : 1], qb[BNX ? 8 : 1];
   if constexpr (BNB) {
     const int n = min(col0 + cc, g.N - 8);
 #pragma unroll
@@ -345,6 +421,13 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
       s1[e] = s2[e] = 0.f;
       mu[e] = cg.bnb_mean[n + e];
       is[e] = cg.bnb_invstd[n + e];
+    }
+    if (BNX) {  // the mask is recomputed from the BN input: scale / shift of these channels
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        qa[e] = cg.bnb_ss[n + e];
+        qb[e] = cg.bnb_ss[g.N + n + e];
+      }
     }
   }
   // side inputs of every chunk this thread stores (the BN input and ReLU-mask byte of BNB, the old
@@ -403,7 +486,18 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
       const int m = row0 + h * TM + r, n = col0 + cc;
       if (m >= g.M || n >= g.N) continue;  // N % 8 == 0: a chunk is all in or all out
       const int64_t off = rowmap(m) * g.ldc + n;
-      const unsigned mb = mbv[h][k];
+      unsigned mb = mbv[h][k];
+      if constexpr (BNB) {
+        if constexpr (BNX) {  // [relu(x*scale + shift) > 0], the fp32 expression of the forward's prologue
+          const uint32_t px[4] = {xz[h][k].x, xz[h][k].y, xz[h][k].z, xz[h][k].w};
+          mb = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = (e & 1) ? hi16t<H>(px[e >> 1]) : lo16t<H>(px[e >> 1]);
+            mb |= (__builtin_fmaf(x, qa[e], qb[e]) > 0.f ? 1u : 0u) << e;
+          }
+        }
+      }
       const f32x4 a = *(const f32x4*)(img + r * LS + cc), b = *(const f32x4*)(img + r * LS + cc + 4);
       float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
       uint16_t* dst = (uint16_t*)g.c + off;
@@ -488,7 +582,10 @@ struct ClsRow {
 // H: fp16 operands (MFMA f16; storage / rounding by g.c_dt), else bf16
 // BK x NS: k-tile depth x LDS ring slots (NS - 1 k-tiles in flight while one is consumed); OCC:
 // resident blocks per CU the register budget is sized for
-template <int MODE, int BM, int BN, int WM, int WN, bool H, int BK = 64, int NS = 2, int OCC = 2>
+// PRO: BatchNorm-apply prologue on the gathered operand (forward A / wgrad B; ConvGeom::pro_ss):
+// that operand is loaded into registers one k-tile ahead (together with the other operand's DMA),
+// transformed after the current k-tile's MFMAs and written into the free ring slot with ds_write_b128
+template <int MODE, int BM, int BN, int WM, int WN, bool H, int BK = 64, int NS = 2, int OCC = 2, bool PRO = false>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(MArgs g, const ConvGeom cg0) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -500,7 +597,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(M
   constexpr bool BKM = !FWD;                // B K-major (dgrad: W per tap; wgrad: gathered X)
   constexpr int NL = (BM + BN) * BK / (512 * NW);  // LDS-DMA instructions per wave per k-tile
   static_assert(NS * STAGE_BYTES >= (BM / WM) * (BN + 4) * 4, "the LDS epilogue image fits in the ring");
+  // PRO on the stride-1 dgrad: its BatchNorm epilogue recomputes the ReLU mask (ConvGeom::bnb_ss)
+  static_assert(!PRO || ((MODE == kConvFwd || MODE == kConvWgrad || MODE == kConvDgrad) && NS == 2),
+                "prologue: fwd / wgrad / BNB dgrad, 2-slot ring");
+  constexpr bool PL = PRO && MODE != kConvDgrad;  // an operand goes through registers
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) float pro_tab[PL ? 2 * kProMaxC : 4];  // [scale C][shift C]
 
   int lin = xcd_remap(blockIdx.x, gridDim.x);
   ConvGeom cg = cg0;
@@ -562,20 +664,37 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(M
     else sb_k.init(g.ldb, col0, g.N, wid, lane);
   }
 
+  // prologue operand of the k-tile in flight (registers), its padding flags and channel offset
+  constexpr int PNI = MODE == kConvWgrad ? GatherCols<BN, BK, NW>::NI : GatherRows<BM, BK, NW, kConvFwd>::NI;
+  u32x4 pv[PNI];
+  uint32_t pok = 0;
+  int pc0 = 0;
+  if constexpr (PL) {
+    for (int i = (int)threadIdx.x; i < 2 * cg.C; i += 64 * NW) pro_tab[i] = cg.pro_ss[i];
+    __syncthreads();
+  }
   auto issue = [&](int t) {
     char* buf = smem + (t % NS) * STAGE_BYTES;
     const int k0 = kb + t * BK;
     if constexpr (MODE == kConvWgrad) {
+      // (prologue: the register loads first, so the DMAs after them are the only vm ops a wait for
+      // the registers has to let through)
+      if constexpr (PL) gb.load(g.b, cg, ke, zero, pv, pok);
       if (k0 + BK <= ke) sa_k.issue((const char*)g.a + (int64_t)k0 * g.lda * 2, buf, wid);
       else sa_k.issue_tail((const char*)g.a + (int64_t)k0 * g.lda * 2, buf, wid, lane, ke - k0, zero);
-      gb.issue(g.b, cg, ke, buf + A_BYTES, wid, zero);  // k-tiles are issued in order: its rows are k0..
+      if constexpr (!PL) gb.issue(g.b, cg, ke, buf + A_BYTES, wid, zero);  // k-tiles are issued in order: its rows are k0..
     } else if constexpr (MODE == kConvFwdC8) {
       ga8.issue(g.a, cg, k0, buf, wid, zero);
       sb_row.issue((const char*)g.b + (int64_t)k0 * 2, buf + A_BYTES, wid);
     } else {
       const int tap = k0 / cg.taps_c, c0 = k0 - tap * cg.taps_c;
       const int tr = tap / cg.S, ts = tap - tr * cg.S;
-      ga.issue(cg, tr, ts, c0, buf, wid, zero);
+      if constexpr (PL) {
+        ga.load(cg, tr, ts, c0, zero, pv, pok);
+        pc0 = c0;
+      } else {
+        ga.issue(cg, tr, ts, c0, buf, wid, zero);
+      }
       if constexpr (MODE == kConvFwd)
         sb_row.issue((const char*)g.b + (int64_t)k0 * 2, buf + A_BYTES, wid);
       else {  // W[co][tap][ci]: k-tile rows co = c0.., columns ci (strided: the class's tap (j, l))
@@ -599,13 +718,25 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(M
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = __builtin_bit_cast(__bf16, (uint16_t)(H ? 0x3C00u : 0x3F80u));
 
+  // PRO: the registers of k-tile t, transformed, into its slot
+  auto put = [&](int t) {
+    char* buf = smem + (t % NS) * STAGE_BYTES;
+    if constexpr (MODE == kConvWgrad) gb.template put<H>(buf + A_BYTES, wid, lane, pv, pok, pro_tab, cg.C);
+    else ga.template put<H>(buf, wid, lane, pv, pok, pro_tab, cg.C, pc0);
+  };
+
   // prologue: NS - 1 k-tiles in flight
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
     if (t < nt) issue(t);
+  if constexpr (PL) {
+    if (nt > 0) put(0);
+  }
   for (int t = 0; t < nt; ++t) {
     // tile t has landed once at most the tiles issued after it (up to t + NS - 2) are outstanding
-    wait_vm((min(nt - 1, t + NS - 2) - t) * NL);
+    // (PRO: its DMA'd operand; the register-staged one was written by put(t) — waited for here)
+    wait_vm(PL ? 0 : (min(nt - 1, t + NS - 2) - t) * NL);
+    if constexpr (PL) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // every wave's share of tile t is in LDS and every wave has consumed tile t - 1: refill its
     // slot with tile t + NS - 1
     __builtin_amdgcn_s_barrier();
@@ -630,6 +761,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(M
         for (int i = 0; i < FM; ++i)
           if (i % WN == wn) racc[i / WN] = mfma16<H>(ones, af[i], racc[i / WN]);
       }
+    }
+    if constexpr (PL) {
+      if (t + 1 < nt) put(t + 1);
     }
   }
   if (want_rows && lane < 16) {
@@ -669,7 +803,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(M
       }
     }
   } else if (MODE == kConvDgrad && cg.bnb_x != nullptr) {
-    store_tile_lds<BM, BN, WM, WN, FM, FN, true, H>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, IdRow());
+    store_tile_lds<BM, BN, WM, WN, FM, FN, true, H, IdRow, PRO>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, IdRow());
   } else if (MODE != kConvWgrad && g.lds_epi) {
     store_tile_lds<BM, BN, WM, WN, FM, FN, false, H>(g, cg, acc, smem, row0, col0, tm, wm, wn, lane, IdRow());
   } else
@@ -689,26 +823,29 @@ int conv_tiles(const MArgs& g, const ConvGeom& cg, int bm, int bn) {
 
 int g_conv_cfg = 0;  // rk_conv_set_cfg: k-tile pipeline of the bf16 kernels
 
-template <int MODE, bool H, int BK, int NS, int OCC, int WN128 = 4>
+template <int MODE, bool H, int BK, int NS, int OCC, int WN128 = 4, bool PRO = false>
 int launch_conv_p(const MArgs& g, const ConvGeom& cg, hipStream_t s) {
   // (the forward's wave row slice is 64 pixels in every variant: the BatchNorm partials rely on it)
   // 64-wide GEMM side (Cout / Cin = 64 layers): a 64-wide tile with 4 waves instead of half an
   // empty 128-wide one; everything else 128 x 128 with 8 waves
   if (MODE != kConvWgrad && g.N <= 64) {
     const int tiles = conv_tiles<MODE>(g, cg, 128, 64);
-    conv_kernel<MODE, 128, 64, 2, 2, H, BK, NS, OCC><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+    conv_kernel<MODE, 128, 64, 2, 2, H, BK, NS, OCC, PRO><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
   } else if (MODE == kConvWgrad && g.M <= 64) {
     const int tiles = ((g.M + 63) / 64) * ((g.N + 127) / 128);
-    conv_kernel<MODE, 64, 128, 2, 2, H, BK, NS, OCC><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+    conv_kernel<MODE, 64, 128, 2, 2, H, BK, NS, OCC, PRO><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
   } else {
     const int tiles = conv_tiles<MODE>(g, cg, 128, 128);
-    conv_kernel<MODE, 128, 128, 2, WN128, H, BK, NS, OCC><<<tiles * g.splitk, 128 * WN128, 0, s>>>(g, cg);
+    conv_kernel<MODE, 128, 128, 2, WN128, H, BK, NS, OCC, PRO><<<tiles * g.splitk, 128 * WN128, 0, s>>>(g, cg);
   }
   return (int)hipGetLastError();
 }
 
 template <int MODE, bool H>
 int launch_conv_t(const MArgs& g, ConvGeom cg, hipStream_t s) {
+  if constexpr (MODE == kConvFwd || MODE == kConvWgrad || MODE == kConvDgrad) {
+    if (cg.pro_ss || cg.bnb_ss) return launch_conv_p<MODE, H, 64, 2, 2, 4, true>(g, cg, s);  // the default pipeline only
+  }
   if constexpr (!H) {
     switch (g_conv_cfg) {
       case 1: return launch_conv_p<MODE, H, 64, 3, 1>(g, cg, s);
@@ -733,6 +870,7 @@ ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stri
   cg.R = R; cg.S = S; cg.stride = stride; cg.pad = pad; cg.taps_c = taps_c;
   cg.w_tap_stride = 0; cg.w_co_stride = 0; cg.bnpart = nullptr;
   cg.bnb_x = nullptr; cg.bnb_mask = nullptr; cg.bnb_mean = nullptr; cg.bnb_invstd = nullptr; cg.bnb_part = nullptr;
+  cg.pro_ss = nullptr; cg.bnb_ss = nullptr;
   cg.hoff = cg.woff = pad; cg.dx_h = cg.dx_w = 0; cg.w_s = S; cg.ncls = 0; cg.zero_nb = 0;
   cg.inv_gw = 1.f / (float)GW;
   cg.inv_gh = 1.f / (float)GH;
@@ -755,6 +893,14 @@ MArgs margs(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 int g_lds_epi = 1;  // rk_conv_set_lds_epi
+// rk_conv_set_bn_prologue: [2][C] scale / shift for the NEXT rk_conv_fwd / rk_conv_wgrad /
+// rk_conv_dgrad_bn call on this host thread (consumed by it)
+thread_local const float* g_pro_ss = nullptr;
+const float* take_pro() {
+  const float* p = g_pro_ss;
+  g_pro_ss = nullptr;
+  return p;
+}
 
 }  // namespace
 
@@ -768,7 +914,9 @@ static bool dt_ok(int dt) { return dt == BF16 || dt == F16; }
 RK_API int rk_conv_fwd(int dt, const void* x, const void* w, void* y, int y_dt, const float* bias, int N, int H, int W,
                        int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, float* bnpart,
                        hipStream_t s) {
+  const float* pro = take_pro();
   if (!dt_ok(dt) || (y_dt != F32 && y_dt != dt)) return (int)hipErrorInvalidValue;
+  if (pro && (Cin > kProMaxC || !aligned16(pro))) return (int)hipErrorInvalidValue;
   if (Cin % 64 || Cout % 8 || R * S > 32 || !aligned16(x) || !aligned16(w) || !aligned16(y)) return (int)hipErrorInvalidValue;
   if (OH != (H + 2 * pad - R) / stride + 1 || OW != (W + 2 * pad - S) / stride + 1) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW, K = R * S * Cin;
@@ -777,6 +925,7 @@ RK_API int rk_conv_fwd(int dt, const void* x, const void* w, void* y, int y_dt, 
   g.lds_epi = g_lds_epi && y_dt != F32 && bias == nullptr;
   ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
   cg.bnpart = bnpart;
+  cg.pro_ss = pro;
   return launch_conv<kConvFwd>(g, cg, dt, s);
 }
 
@@ -827,6 +976,13 @@ RK_API int rk_pad_c8(const void* x, void* y, int N, int C, int H, int W, int64_t
 // classes of dX pixels as four stride-1 gathers in one launch (classes without taps store zeros).
 // 1 (default): bf16 forward / input-gradient tiles are stored through LDS in row-contiguous 16-byte
 // chunks; 0: straight from the MFMA accumulator layout (A/B switch, ROCKET_CONV_LDS_EPI)
+// BatchNorm-apply prologue of the next conv call on this host thread (see g_pro_ss): the gathered
+// input X (fwd / wgrad) is the BatchNorm's input z and the conv reads relu(z*scale + shift),
+// ss = [2][Cin] f32 (scale, shift; Cin <= 512); rk_conv_dgrad_bn: the ReLU mask from bn_x and ss
+RK_API int rk_conv_set_bn_prologue(const float* ss) {
+  g_pro_ss = ss;
+  return 0;
+}
 RK_API int rk_conv_set_tile_group(int gh) {
   g_tile_group = gh < 1 ? 1 : gh;
   return 0;
@@ -852,6 +1008,8 @@ RK_API int rk_conv_set_cfg(int cfg) {
 RK_API int rk_conv_dgrad_bn(int dt, const void* dy, const void* w, void* dx, int accumulate, int N, int H, int W,
                             int Cin, int Cout, int R, int S, int pad, const void* bn_x, const void* bn_mask,
                             const float* mean, const float* invstd, float* part, hipStream_t s) {
+  const float* pro = take_pro();
+  if (pro && (bn_mask || !aligned16(pro))) return (int)hipErrorInvalidValue;
   if (!dt_ok(dt) || Cout % 64 || Cin % 8 || R * S > 32 || !aligned16(dy) || !aligned16(w) || !aligned16(dx) || !aligned16(bn_x) || !part ||
       !aligned16(mean) || !aligned16(invstd) || !aligned16(part))
     return (int)hipErrorInvalidValue;
@@ -868,6 +1026,7 @@ RK_API int rk_conv_dgrad_bn(int dt, const void* dy, const void* w, void* dx, int
   cg.bnb_mean = mean;
   cg.bnb_invstd = invstd;
   cg.bnb_part = part;
+  cg.bnb_ss = pro;
   return launch_conv<kConvDgrad>(g, cg, dt, s);
 }
 
@@ -921,7 +1080,9 @@ RK_API int rk_conv_dgrad(int dt, const void* dy, const void* w, void* dx, int dx
 RK_API int rk_conv_wgrad(int dt, const void* dy, const void* x, float* dw, int accumulate, float* db, int N, int H,
                          int W, int Cin, int Cout, int R, int S, int stride, int pad, int OH, int OW, int splitk,
                          float* slab, hipStream_t s) {
+  const float* pro = take_pro();
   if (!dt_ok(dt) || Cin % 8 || Cout % 8 || !aligned16(dy) || !aligned16(x)) return (int)hipErrorInvalidValue;
+  if (pro && (Cin > kProMaxC || !aligned16(pro))) return (int)hipErrorInvalidValue;
   const int P = N * OH * OW, Ncol = R * S * Cin;
   MArgs g = margs(dy, Cout, x, 0, dw, F32, Ncol, Cout, Ncol, P);
   g.rowsum = db;
@@ -934,6 +1095,7 @@ RK_API int rk_conv_wgrad(int dt, const void* dy, const void* x, float* dw, int a
   g.k_per_split = kps;
   g.slab = slab;
   ConvGeom cg = geom(N, H, W, Cin, OH, OW, R, S, stride, pad, Cin);
+  cg.pro_ss = pro;
   int rc = launch_conv<kConvWgrad>(g, cg, dt, s);
   if (rc || splitk == 1) return rc;
   launch_mgemm_reduce(slab, splitk, Cout, Ncol, nullptr, dw, F32, Ncol, accumulate, s);

@@ -11,6 +11,8 @@
 #include "rk_common.h"
 #include "rows_common.h"
 
+#include <algorithm>
+
 #include <hip/hip_ext.h>
 
 namespace {
@@ -24,6 +26,7 @@ struct GatherArgs {
   int64_t src_rows[kMaxGather];
   int ntensors;
   uint64_t* trace;  // diagnostics: [blocks][2] start / end stamps (s_memrealtime), or null
+  int pieces[kMaxGather];  // wave work items per row of tensor t (ceil(row_bytes / kPiece))
 };
 
 // grid: x = row blocks (kRowsPerBlock rows each), y = tensor.  One wave copies one row; each lane
@@ -31,6 +34,9 @@ struct GatherArgs {
 // round trip instead of one per 1 KB chunk (a 3 KB LeNet image row: 4 -> 1).
 constexpr int kThreads = 256;
 constexpr int kRowsPerBlock = kThreads / 64;
+// rows longer than this are cut into pieces copied by different waves (a 3x224x224 bf16 image row is
+// 294 KiB: one wave per row left a 128-row ViT batch on 32 CUs, 0.6 TB/s)
+constexpr int64_t kPiece = 16384;
 constexpr int kUnroll = 4;  // the register pin below names 4 values
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -48,16 +54,19 @@ __device__ __forceinline__ void copy_row(const V* __restrict__ src, V* __restric
   }
 }
 
-__device__ __forceinline__ void copy_one(const GatherArgs& a, int t, int64_t s, int64_t r, int lane);
+__device__ __forceinline__ void copy_one(const GatherArgs& a, int t, int64_t s, int64_t r, int lane, int piece);
 
 __global__ void __launch_bounds__(kThreads) gather_rows_kernel(GatherArgs a, const int64_t* __restrict__ idx,
                                                                int64_t nrows) {
   const int t = blockIdx.y;
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  const int64_t item = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);  // (row, piece) of tensor t
+  const int np = a.pieces[t];
+  const int64_t r = item / np;
+  const int piece = (int)(item - r * np);
   uint64_t* tr = a.trace ? a.trace + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 : nullptr;
   if (tr && threadIdx.x == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
-  if (r < nrows) copy_one(a, t, idx[r], r, lane);
+  if (r < nrows) copy_one(a, t, idx[r], r, lane, piece);
   if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -68,12 +77,14 @@ __global__ void __launch_bounds__(256) rows_next_kernel(const int64_t* __restric
   rows_next_block(table, meta, rows, n_cur, bs);
 }
 
-__device__ __forceinline__ void copy_one(const GatherArgs& a, int t, int64_t s, int64_t r, int lane) {
+__device__ __forceinline__ void copy_one(const GatherArgs& a, int t, int64_t s, int64_t r, int lane, int piece) {
   s = s < 0 ? s + a.src_rows[t] : s;
   s = s < 0 ? 0 : (s >= a.src_rows[t] ? a.src_rows[t] - 1 : s);
-  const int64_t rb = a.row_bytes[t];
-  const char* __restrict__ src = a.src[t] + s * rb;
-  char* __restrict__ dst = a.dst[t] + r * rb;
+  const int64_t full = a.row_bytes[t];
+  const int64_t off = (int64_t)piece * kPiece;
+  const int64_t rb = full - off < kPiece || a.pieces[t] == 1 ? full - off : kPiece;  // this piece's bytes
+  const char* __restrict__ src = a.src[t] + s * full + off;
+  char* __restrict__ dst = a.dst[t] + r * full + off;
   if (((rb | (int64_t)a.src[t] | (int64_t)a.dst[t]) & 15) == 0) {
     copy_row((const u32x4*)src, (u32x4*)dst, (int)(rb >> 4), lane);
   } else if (((rb | (int64_t)a.src[t] | (int64_t)a.dst[t]) & 7) == 0) {
@@ -117,7 +128,14 @@ static int gather_launch(int ntensors, const void* const* srcs, void* const* dst
   }
   a.ntensors = ntensors;
   a.trace = g_gather_trace;
-  dim3 grid((unsigned)((nrows + kRowsPerBlock - 1) / kRowsPerBlock), (unsigned)ntensors);
+  int64_t maxp = 1;
+  for (int i = 0; i < ntensors; ++i) {
+    // pieces of whole 16-byte vectors only when the row is vector-aligned (else one wave per row)
+    const bool vec = ((row_bytes[i] | (int64_t)srcs[i] | (int64_t)dsts[i]) & 15) == 0;
+    a.pieces[i] = vec ? (int)((row_bytes[i] + kPiece - 1) / kPiece) : 1;
+    maxp = std::max<int64_t>(maxp, a.pieces[i]);
+  }
+  dim3 grid((unsigned)((nrows * maxp + kRowsPerBlock - 1) / kRowsPerBlock), (unsigned)ntensors);
   if (g_gather_any_order) {
     // AQL barrier bit clear: the gather may start while the previous packet on the stream (the
     // last kernel of the step before) still runs; see rk_gather_rows_any_order

@@ -57,6 +57,7 @@ KERNEL_SIGS = {
     "rk_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_int64, c_int] + [c_void_p] * 9 + [c_float, c_float, c_void_p,
                                                                                             c_void_p, c_void_p]),
     "rk_conv_set_lds_epi": (c_int, [c_int]),
+    "rk_conv_set_bn_prologue": (c_int, [c_void_p]),
     "rk_conv_set_tile_group": (c_int, [c_int]),
     "rk_conv_set_cfg": (c_int, [c_int]),
     "rk_mlp3_set_trace": (None, [c_void_p]),

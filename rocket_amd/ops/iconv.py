@@ -409,3 +409,117 @@ def conv_entry(x: torch.Tensor, conv_a: nn.Conv2d, conv_b: nn.Conv2d | None):
 def conv2d_reference(x, w, stride, pad):
     """fp32 reference of the same op (tests)."""
     return F.conv2d(x.float(), w.float(), stride=stride, padding=pad)
+
+
+# BatchNorm folded into the consuming conv (ROCKET_BN_FOLD, default 1): ``conv(relu(bn(z)))`` with the
+# BatchNorm's ``relu(z*scale + shift)`` formed in the conv's operand staging (conv.hip PRO), so the
+# BatchNorm output and its ReLU mask are never written: forward = statistics finalize + one conv
+# launch, backward = the conv dgrad (ReLU mask recomputed from z in its BatchNorm epilogue) + the
+# BatchNorm input-gradient pass + the conv wgrad (the same prologue on its gathered z).
+BN_FOLD = os.environ.get("ROCKET_BN_FOLD", "1") != "0"
+FOLD_MAX_C = 512  # conv.hip kProMaxC: channels of the prologue's LDS scale / shift table
+FOLD_HITS = 0  # folded (BatchNorm, conv) pairs run (tests)
+
+
+class _BNConvFn(torch.autograd.Function):
+    """``conv(relu(bn(z)))`` as one node (module docstring of :func:`bn_relu_conv`)."""
+
+    @staticmethod
+    def forward(ctx, z, gamma, beta, running_mean, running_var, nbt, momentum: float, eps: float, partials,
+                weight, w16, stride: int, pad: int, bnpart):
+        from rocket_amd.ops import norm as _norm
+
+        lib = _kernels()
+        dev = z.device
+        s = _lib.stream_ptr(dev)
+        zc = _cl(z, w16.dtype)
+        C = zc.shape[1]
+        R = zc.numel() // C
+        stats = torch.empty(4, C, dtype=torch.float32, device=dev)  # mean, invstd, scale, shift
+        ws = torch.empty(int(lib.rk_bn_workspace(R, C)), dtype=torch.float32, device=dev)
+        nctr = int(lib.rk_bn_counters(C))
+        counters = _lib.Workspace.get(dev).counter_array(f"bn{nctr}", nctr)
+        g, b = gamma.detach(), beta.detach()
+        args = (_lib.ptr(g), _lib.ptr(b), stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(),
+                stats[3].data_ptr(), _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(nbt), float(momentum),
+                float(eps), ws.data_ptr(), counters, s)
+        if partials is not None:
+            tp, ntiles, tile_rows = partials
+            _lib.check(lib.rk_bn_finalize(tp.data_ptr(), ntiles, tile_rows, R, C, *args), "rk_bn_finalize")
+        else:
+            _lib.check(lib.rk_bn_stats(_norm._dt(zc), _norm._rows_view(zc).data_ptr(), R, C, *args), "rk_bn_stats")
+        lib.rk_conv_set_bn_prologue(stats[2].data_ptr())  # [scale][shift] rows: the [2][C] table
+        y = _conv_fwd(zc, w16, stride, pad, bnpart)
+        ctx.save_for_backward(zc, w16, stats)
+        ctx.params = (gamma, beta, weight)
+        ctx.geo = _geo(zc, w16, stride, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from rocket_amd.ops.lenet import _finish, _grad_targets
+
+        global FOLD_HITS
+        FOLD_HITS += 1
+        zc, w16, stats = ctx.saved_tensors
+        gamma, beta, weight = ctx.params
+        N, C, H, W, Co, R, S, stride, pad, OH, OW = ctx.geo
+        dev = zc.device
+        s = _lib.stream_ptr(dev)
+        lib = _kernels()
+        dyc = _cl(dy, zc.dtype)
+        rows = N * H * W
+        # dX' = relu-mask(z) * (dY (*) W^T), with the BatchNorm backward's per-tile reductions
+        dxp = torch.empty_like(zc)
+        ntiles = -(-rows // 128)
+        part = torch.empty(ntiles * 2 * C, dtype=torch.float32, device=dev)
+        lib.rk_conv_set_bn_prologue(stats[2].data_ptr())
+        _lib.check(lib.rk_conv_dgrad_bn(_dt(dyc), dyc.data_ptr(), w16.data_ptr(), dxp.data_ptr(), 0, N, H, W, C, Co, R, S,
+                                        pad, zc.data_ptr(), None, stats[0].data_ptr(), stats[1].data_ptr(),
+                                        part.data_ptr(), s), "rk_conv_dgrad_bn(fold)")
+        # dz from dX' and the partials (BatchNorm input gradient; dgamma / dbeta into their grads)
+        bufs, direct = _grad_targets([gamma, beta], dev)
+        dz = torch.empty_like(zc)
+        ws = torch.empty(int(lib.rk_bn_workspace(rows, C)), dtype=torch.float32, device=dev)
+        coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
+        nctr = int(lib.rk_bn_counters(C))
+        counters = _lib.Workspace.get(dev).counter_array(f"bn{nctr}", nctr)
+        _lib.check(lib.rk_bn_bwd_partials(_dt(zc), _dt(dxp), dxp.data_ptr(), zc.data_ptr(), part.data_ptr(), ntiles,
+                                          rows, C, stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(),
+                                          bufs[0].data_ptr(), bufs[1].data_ptr(), dz.data_ptr(), None,
+                                          ws.data_ptr(), coef.data_ptr(), counters, s), "rk_bn_bwd_partials(fold)")
+        gg, gb = _finish([gamma, beta], bufs, direct)
+        # the conv's weight gradient over relu(z*scale + shift), formed by the same prologue
+        dw = None
+        if ctx.needs_input_grad[9]:
+            lib.rk_conv_set_bn_prologue(stats[2].data_ptr())
+            dw = _conv_wgrad(dyc, zc, weight, ctx.geo)
+        return dz, gg, gb, None, None, None, None, None, None, dw, None, None, None, None
+
+
+def fold_ok(bn: nn.Module, conv: nn.Module, z: torch.Tensor) -> bool:
+    """Whether ``conv(bn(z))`` runs as :class:`_BNConvFn`: a training BatchNorm(+ReLU) with
+    affine parameters and running statistics feeding a stride-1 native conv, over <= 512 16-bit
+    channels-last channels."""
+    from rocket_amd.ops.norm import BatchNormAct2d
+
+    return (BN_FOLD and isinstance(bn, BatchNormAct2d) and isinstance(conv, IConv2d) and bn.training and bn.relu
+            and not bn.maxpool and bn.affine and bn.track_running_stats and bn.momentum is not None
+            and z.dim() == 4 and z.dtype in _LOWP and z.dtype == torch.get_autocast_dtype("cuda")
+            and z.is_contiguous(memory_format=torch.channels_last) and z.shape[1] <= FOLD_MAX_C
+            and bn._fused_ok(z, None) and native_ok(conv, z) and conv.stride[0] == 1
+            and conv.out_channels % 64 == 0)
+
+
+def bn_relu_conv(bn: nn.Module, conv: nn.Module, z: torch.Tensor) -> torch.Tensor:
+    """``conv(bn(z))`` for a ReLU BatchNorm feeding a conv: folded into the conv (:class:`_BNConvFn`)
+    when :func:`fold_ok`, else the two modules."""
+    if not fold_ok(bn, conv, z):
+        return conv(bn(z))
+    partials = getattr(z, "_rocket_bn_partials", None)
+    if partials is not None and partials[0].numel() != 2 * partials[1] * z.shape[1]:
+        partials = None
+    w16, part = conv._prep(z)
+    y = _BNConvFn.apply(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                        bn.momentum, bn.eps, partials, conv.weight, w16, conv.stride[0], conv.padding[0], part)
+    return conv._attach(y, part)

@@ -54,8 +54,10 @@ MODE = os.environ.get("ROCKET_VIT_GEMM", "lib")
 #   fc1 forward       z = x W1^T + b1 and h = gelu(z) from ONE launch (no gelu_fwd pass);
 #   fc2 input grad    dz = (dy W2) * gelu'(z) and db1 += colsum(dz) from ONE launch (no GELU-backward
 #                     + column-sum pass; W2 read through a per-step transposed bf16 copy).
-# ROCKET_VIT_X4_MLP=0 keeps them on the MODE's engine with separate GELU kernels.
-X4_MLP = os.environ.get("ROCKET_VIT_X4_MLP", "1") != "0"
+# Opt-in (ROCKET_VIT_X4_MLP=1): the fused launches are correct (tests/kernels/test_xgemm4.py) but the
+# 256x256 core runs these short-K shapes at ~2/3 of hipBLASLt's rate, and the saved GELU passes do not
+# pay for it: ViT-B/16 5,163 img/s fused vs 5,782 separate (profiles/r5_vit_b16_x4_mlp.md).
+X4_MLP = os.environ.get("ROCKET_VIT_X4_MLP", "0") == "1"
 _TILE_WIDE_FWD, _TILE_DEFAULT = 4, 0
 
 

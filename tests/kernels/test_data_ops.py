@@ -20,6 +20,22 @@ def test_gather_rows_multi_tensor():
         assert torch.equal(o, t.index_select(0, idx))
 
 
+def test_gather_rows_long_rows_split_across_waves():
+    """Rows longer than one 16 KiB piece are copied by several waves (ViT/ResNet image rows)."""
+    from rocket_amd.ops.data import gather_rows
+
+    dev = torch.device("cuda", 0)
+    x = torch.randn(64, 3, 224, 224, device=dev, dtype=torch.bfloat16)  # 301,056 B: 18.4 pieces
+    y = torch.randn(64, 5000, device=dev)  # 20,000 B: one full piece + a 3,616 B tail
+    z = torch.randn(64, 8195, device=dev, dtype=torch.bfloat16)  # 16,390 B, not 16-B aligned: one wave
+    lab = torch.randint(0, 1000, (64,), device=dev)
+    idx = torch.randint(-64, 64, (45,), device=dev)
+    outs = [torch.empty((45,) + t.shape[1:], dtype=t.dtype, device=dev) for t in (x, y, z, lab)]
+    gather_rows([x, y, z, lab], idx, outs)
+    for t, o in zip((x, y, z, lab), outs):
+        assert torch.equal(o, t.index_select(0, idx % 64))
+
+
 def test_loss_accum_ring():
     from rocket_amd.ops.data import loss_accum
 

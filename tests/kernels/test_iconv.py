@@ -169,6 +169,9 @@ def test_bn_backward_reduction_in_dgrad_epilogue(monkeypatch, kind):
     state = {k: v.clone() for k, v in net.state_dict().items()}
     x0 = torch.randn(4, cin, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     outs = []
+    import rocket_amd.ops.iconv as ic
+
+    monkeypatch.setattr(ic, "BN_FOLD", False)  # the folded pairs need no link (test_bn_fold_matches_unfused)
     for fuse in (True, False):
         net.load_state_dict(state)
         monkeypatch.setattr(nm, "BWD_FUSE", fuse)
@@ -189,6 +192,60 @@ def test_bn_backward_reduction_in_dgrad_epilogue(monkeypatch, kind):
     assert _rel(dx1, dx2) < 2e-2, _rel(dx1, dx2)
     for a, b in zip(g1, g2):
         assert _rel(a, b) < 2e-2, _rel(a, b)
+
+
+@pytest.mark.parametrize("kind", ["bottleneck", "basic"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_bn_fold_matches_unfused(monkeypatch, kind, dtype):
+    """BatchNorm(+ReLU) folded into the consuming conv (conv.hip BatchNorm-apply prologue on the
+    forward / wgrad operand, ReLU mask recomputed in the dgrad epilogue) equals the separate
+    BatchNorm + conv: outputs, input / parameter gradients and running statistics, through identity
+    and strided blocks (the stride-2 consumers stay unfolded)."""
+    import rocket_amd.ops.iconv as ic
+    from rocket_amd.models.resnet import BasicBlock, Bottleneck
+    from rocket_amd.ops.norm import BatchNormAct2d
+
+    torch.manual_seed(6)
+    if kind == "bottleneck":
+        net = torch.nn.Sequential(BatchNormAct2d(256, relu=True), Bottleneck(256, 64, 1), Bottleneck(256, 128, 2),
+                                  Bottleneck(512, 128, 1))
+        cin, want_hits = 256, 5
+    else:
+        net = torch.nn.Sequential(BatchNormAct2d(64, relu=True), BasicBlock(64, 64, 1), BasicBlock(64, 128, 2),
+                                  BasicBlock(128, 128, 1))
+        cin, want_hits = 64, 3
+    net = net.cuda().to(memory_format=torch.channels_last)
+    for m in net.modules():
+        if isinstance(m, BatchNormAct2d):
+            with torch.no_grad():
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    state = {k: v.clone() for k, v in net.state_dict().items()}
+    x0 = torch.randn(4, cin, 16, 16, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for fold in (True, False):
+        net.load_state_dict(state)
+        monkeypatch.setattr(ic, "BN_FOLD", fold)
+        hits0 = ic.FOLD_HITS
+        net.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=dtype):
+            y = net(x)
+        torch.manual_seed(7)
+        g = torch.randn(y.shape, device="cuda").to(y.dtype).contiguous(memory_format=torch.channels_last)
+        y.backward(g)
+        torch.cuda.synchronize()
+        bufs = {k: v.float().clone() for k, v in net.state_dict().items() if "running" in k}
+        outs.append((y.detach().float(), x.grad.float(), [p.grad.float().clone() for p in net.parameters()], bufs,
+                     ic.FOLD_HITS - hits0))
+    (y1, dx1, g1, b1, hits), (y2, dx2, g2, b2, nohits) = outs
+    assert nohits == 0 and hits == want_hits, hits
+    assert _rel(y1, y2) < 1e-3, _rel(y1, y2)
+    assert _rel(dx1, dx2) < 1e-2, _rel(dx1, dx2)
+    for a, b in zip(g1, g2):
+        assert _rel(a, b) < 1e-2, _rel(a, b)
+    for k in b1:
+        torch.testing.assert_close(b1[k], b2[k], rtol=1e-4, atol=1e-5)
 
 
 @pytest.mark.parametrize("R,stride,pad,H", [(7, 2, 3, 32), (3, 1, 1, 16)])
