@@ -411,12 +411,16 @@ def conv2d_reference(x, w, stride, pad):
     return F.conv2d(x.float(), w.float(), stride=stride, padding=pad)
 
 
-# BatchNorm folded into the consuming conv (ROCKET_BN_FOLD, default 1): ``conv(relu(bn(z)))`` with the
+# BatchNorm folded into the consuming conv (ROCKET_BN_FOLD=1, opt-in): ``conv(relu(bn(z)))`` with the
 # BatchNorm's ``relu(z*scale + shift)`` formed in the conv's operand staging (conv.hip PRO), so the
 # BatchNorm output and its ReLU mask are never written: forward = statistics finalize + one conv
 # launch, backward = the conv dgrad (ReLU mask recomputed from z in its BatchNorm epilogue) + the
 # BatchNorm input-gradient pass + the conv wgrad (the same prologue on its gathered z).
-BN_FOLD = os.environ.get("ROCKET_BN_FOLD", "1") != "0"
+# Measured slower (ResNet-50 10,094 vs 10,609 img/s, ResNet-18 70.2k vs 76.2k; profiles/r5_bn_fold_ab.md):
+# an implicit GEMM re-stages every input element once per tap and per output-column tile (9 x 1-16 times
+# for a 3x3), so the transform costs several times the VALU work of the one bn_apply pass it replaces,
+# while the HBM round trip it saves is cheap at 8 TB/s.
+BN_FOLD = os.environ.get("ROCKET_BN_FOLD", "0") == "1"
 FOLD_MAX_C = 512  # conv.hip kProMaxC: channels of the prologue's LDS scale / shift table
 FOLD_HITS = 0  # folded (BatchNorm, conv) pairs run (tests)
 

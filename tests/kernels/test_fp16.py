@@ -106,6 +106,9 @@ def test_bn_backward_in_dgrad_epilogue_fp16(monkeypatch):
     net = net.cuda().to(memory_format=torch.channels_last)
     state = {k: v.clone() for k, v in net.state_dict().items()}
     x0 = torch.randn(4, 64, 16, 16, device="cuda").to(H16).contiguous(memory_format=torch.channels_last)
+    import rocket_amd.ops.iconv as ic
+
+    monkeypatch.setattr(ic, "BN_FOLD", False)  # folded pairs need no link (test_iconv.py test_bn_fold_matches_unfused)
     outs = []
     for fuse in (True, False):
         net.load_state_dict(state)
