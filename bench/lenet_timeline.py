@@ -153,9 +153,15 @@ class StepTrace:
         if g.shape[0]:  # the NEXT batch's gather (issued one ahead, before this step's launches)
             spans["next_batch_gather"] = {"first_start": us(g[:, 0].min()), "last_end": us(g[:, 1].max()),
                                           "blocks": int(g.shape[0])}
+        # per-wave stamps (us after the block's own phase start, median over blocks, per wave)
+        per_wave = lambda tr, cols, ref: [round(float(v) * 0.01, 2) for v in (tr[:, cols] - tr[:, ref:ref + 1]).median(0).values]  # noqa: E731
+        waves = {"fwd conv1 done (after staging)": per_wave(f, slice(16, 32), 1),
+                 "fwd conv2 done (after the conv1 barrier)": per_wave(f, slice(32, 48), 3),
+                 "bwd dW2 tile done (after scatter)": per_wave(b, slice(16, 26), 8),
+                 "bwd dgrad tiles done (after scatter)": per_wave(b, slice(32, 48), 8)}
         return {"kernel": "captured LeNet step (us from the forward's first block start)", "spans": spans,
                 "fwd_phases": summarize(self.ftr.cpu(), FWD, list(range(9))),
-                "bwd_phases": summarize(self.btr.cpu(), BWD, BWD_MARKS)}
+                "bwd_phases": summarize(self.btr.cpu(), BWD, BWD_MARKS), "waves": waves}
 
 
 if __name__ == "__main__":

@@ -266,14 +266,37 @@ struct ClsFwd {  // classifier operands of the fused forward
   uint64_t* trace;            // optional phase timeline [blocks][kTraceStride]
 };
 
+// The classifier backward's B fragments (fc3 / fc2 / fc1 dgrad), per wave.  The whole-step kernel
+// issues their loads inside the forward, after fc1 (whose fragments are then dead), so their
+// memory latency hides under fc2 / fc3 instead of opening the backward.
+struct ClsBwdFrags {
+  bf16x8 fb3, fb2[3], fb1[2][4];
+};
+__device__ __forceinline__ void load_cls_bwd(const bf16x8* __restrict__ frag, int wave, int lane, ClsBwdFrags& f) {
+  if (wave < 6) f.fb3 = frag[(OFF_B3 + wave) * 64 + lane];
+  if (wave < 8) {
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) f.fb2[ks] = frag[(OFF_B2 + wave * 3 + ks) * 64 + lane];
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = wave + 16 * u;
+    if (t < 25) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) f.fb1[u][ks] = frag[(OFF_B1 + t * 4 + ks) * 64 + lane];
+    }
+  }
+}
+
 template <bool MLP>
 __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ x, const float* __restrict__ w1,
                                          const float* __restrict__ b1, const float* __restrict__ w2,
                                          const float* __restrict__ b2, uint16_t* __restrict__ a1g,
                                          uint8_t* __restrict__ code1, uint16_t* __restrict__ a2g,
-                                         uint8_t* __restrict__ code2, int N, ClsFwd cf, const RowSrc& rs) {
+                                         uint8_t* __restrict__ code2, int N, ClsFwd cf, const RowSrc& rs,
+                                         ClsBwdFrags* pre = nullptr, const bf16x8* bfrag = nullptr) {
   RK_TR(cf.trace, 0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // conv B operands: the fused path loads the prep kernel's fragments first thing (one 16-byte
   // load per k-step, latency hidden behind the image staging); the generic path gathers them
   bf16x8 bw1, bw2[7];
@@ -391,54 +414,54 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
   // independent chains in flight instead of one read -> MFMA -> max -> store chain at a time)
   constexpr int U1 = 4;
   if constexpr (MLP) {
-    // Issue-bound phase (4 waves per SIMD, ~100 instructions per tile when every address is
-    // derived from the tile index): addresses are per-lane constants plus an incrementally
-    // stepped window position.  The parity of pos1(w, q) is (q>>1 ^ q&1), independent of w, and
-    // so is the parity of every tap offset: each lane's choice between the two image copies (the
-    // aligned pair read) is fixed, as are its output slots up to a per-tile stride.
+    // VALU-issue-bound phase (4 waves per SIMD): tiles are laid out so that every per-tile address
+    // step is wave-uniform.  Wave sw owns pool-window columns 4sw .. 4sw+3 of all 14 pool rows (one
+    // tile per row; columns 14, 15 of wave 3 are padding lanes whose outputs are not stored): moving
+    // one pool row down is +2 image rows for every lane, so the 14 tiles' LDS reads and stores are
+    // the lane's base address plus immediate offsets — no per-tile address arithmetic.  (The
+    // 49-tile walk over consecutive windows spent ~15 VALU instructions per tile on window
+    // wrap-around and addresses, half of the phase.)  56 tiles instead of 49; the epilogue is ~14
+    // VALU instructions per tile.
     const int q4 = lo & 3;
     const int par = ((q4 >> 1) ^ q4) & 1;
-    uint32_t pb[4], pm[4];  // per pair: LDS byte base (copy + tap offset), mask on the window position
+    const int wl = 4 * sw + (lo >> 2);  // this lane's A row: window column wl, quadrant q4
+    const int pos0 = (q4 >> 1) * IMGS + 2 * wl + (q4 & 1);  // pool row 0
+    const char* pbq[4];  // per pair: the lane's LDS address in pool row 0
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int kp = koffp[q];
-      const bool ok = kp >= 0;
-      const int xp = par ^ (ok ? (kp & 1) : 0);  // parity of pos + kp
-      const uint16_t* basep = ok ? (xp ? img1 - 1 + kp : img0 + kp) : img0 + IMGZ;
-      pb[q] = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint16_t*)basep;
-      pm[q] = ok ? 0xffffffffu : 0u;
+      // padded taps (k >= K1P) have zero B rows: any finite pair will do (the window's first pair)
+      const int kp = koffp[q] >= 0 ? koffp[q] : 0;
+      const int xp = par ^ (kp & 1);  // parity of pos + kp (pos0's parity is par; rows step by 66)
+      pbq[q] = (const char*)(xp ? img1 - 1 + kp : img0 + kp) + 2 * pos0;
     }
-    // window of tile t: w = 4t + (lo >> 2), stepped by 16 (= one pool row + 2) per WPS tiles
-    int wc = (4 * sw + (lo >> 2)) % Q1, wr = (4 * sw + (lo >> 2)) / Q1;
-    int pos = (2 * wr + (q4 >> 1)) * IMGS + 2 * wc + (q4 & 1);
-    const int ostep = lo < C1 ? 4 * WPS : 0;
-    int o = lo < C1 ? lo * (Q1 * Q1) + 4 * sw + hi : A1N + 4;
-    const int cstep = lo < 8 ? 4 * WPS * 8 : 0;
-    int oc = lo < 8 ? (4 * sw + hi) * 8 + lo : A1CL + 8;
-    uint16_t* const a1cl = sm.a1cl[slot];
-    for (int t0 = sw; t0 < 49; t0 += U1 * WPS) {
+    const int wo = 4 * sw + hi;  // this lane's output window column (C rows 4hi + i: its 4 quadrants)
+    const bool st1 = lo < C1 && wo < Q1, st2 = lo < 8 && wo < Q1;
+    uint16_t* const a1p = a1 + (lo < C1 ? lo : 0) * (Q1 * Q1) + wo;
+    uint8_t* const c1p = c1 + (lo < C1 ? lo : 0) * (Q1 * Q1) + wo;
+    uint16_t* const clp = sm.a1cl[slot] + wo * 8 + (lo < 8 ? lo : 0);
+    const float bias1z = lo < C1 ? bias1 : 0.f;  // channels 6, 7 of the channel-last copy: relu(0) = 0
+#pragma unroll
+    for (int r0 = 0; r0 < Q1; r0 += U1) {
       bf16x8 a[U1];
-      int pu = pos, wcu = wc;
 #pragma unroll
       for (int u = 0; u < U1; ++u) {
-        const int pc = min(pu, (PADI - 1) * IMGS);  // tiles past 48: any in-image position, never stored
-        uint32_t w4[4];
+        if (r0 + u < Q1) {
+          const int ro = (r0 + u) * 2 * IMGS * 2;  // bytes: two image rows per pool row
+          uint32_t w4[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          w4[q] = *(const __attribute__((address_space(3))) uint32_t*)(uintptr_t)(pb[q] + 2u * ((uint32_t)pc & pm[q]));
-        a[u] = __builtin_bit_cast(bf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
-        // step 16 windows: +1 pool row (+66) and +2 columns (+4); wrapping a row: +2 rows, -12 columns
-        wcu += 2;
-        const bool wrap = wcu >= Q1;
-        wcu = wrap ? wcu - Q1 : wcu;
-        pu += wrap ? 2 * 2 * IMGS + 4 - 2 * Q1 : 2 * IMGS + 4;
+          for (int q = 0; q < 4; ++q) w4[q] = *(const uint32_t*)(pbq[q] + ro);
+          a[u] = __builtin_bit_cast(bf16x8, make_uint4(w4[0], w4[1], w4[2], w4[3]));
+        }
       }
       f32x4 acc[U1];
 #pragma unroll
-      for (int u = 0; u < U1; ++u) acc[u] = mfma16(a[u], bw1, f32x4{0.f, 0.f, 0.f, 0.f});
+      for (int u = 0; u < U1; ++u)
+        if (r0 + u < Q1) acc[u] = mfma16(a[u], bw1, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int u = 0; u < U1; ++u) {
-        if (t0 + u * WPS >= 49) break;  // wave-uniform
+        if (r0 + u >= Q1) break;
+        const int r = r0 + u;
+        // max over the window's 4 quadrants; code = first quadrant attaining it (strict > as before)
         float m = acc[u][0];
         int arg = 0;
 #pragma unroll
@@ -447,17 +470,15 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
           m = gt ? acc[u][i] : m;
           arg = gt ? i : arg;
         }
-        m += bias1;
+        m += bias1z;
         const bool on = m > 0.f;
         const uint16_t v = c16(on ? m : 0.f);
-        a1[o + u * ostep] = v;
-        c1[o + u * ostep] = on ? (uint8_t)arg : 0xFF;
-        a1cl[oc + u * cstep] = lo < C1 ? v : (uint16_t)0;
+        if (st1) {
+          a1p[r * Q1] = v;
+          c1p[r * Q1] = on ? (uint8_t)arg : 0xFF;
+        }
+        if (st2) clp[r * Q1 * 8] = v;
       }
-      pos = pu;
-      wc = wcu;
-      o += U1 * ostep;
-      oc += U1 * cstep;
     }
   } else {
     for (int t0 = sw; t0 < 49; t0 += U1 * WPS) {
@@ -494,6 +515,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       }
     }
   }
+  RK_TRW(cf.trace, 16);  // per wave: conv1 tiles done
   if constexpr (MLP) {  // fc1 fragments (bw1 is dead now)
     if (wave < 8) {
 #pragma unroll
@@ -568,6 +590,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       sm.k.c2[slot][o] = on ? (uint8_t)arg : 0xFF;
     }
   }
+  RK_TRW(cf.trace, 32);  // per wave: conv2 tiles done
   if constexpr (MLP) {  // fc2 / fc3 fragments (bw2 is dead now; fc1 hides their latency)
     if (wave < 6) {
 #pragma unroll
@@ -624,6 +647,9 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
         if (col < F2) *(uint2*)(cf.h2T + (int64_t)col * N + n0) = pack4(v[0], v[1], v[2], v[3]);
       }
     }
+    // the backward's classifier fragments, issued once fc2 no longer waits on its own operands
+    // (issued before fc2 they put vmcnt waits into fc2's chain: +0.8 us)
+    if (pre) load_cls_bwd(bfrag, wave, lane, *pre);
     lds_barrier();
     RK_TR(cf.trace, 7);
     if (wave == 0) {  // fc3: 1 n-tile x 3 k-steps -> fp32 logits
@@ -664,21 +690,26 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
 //  phase D  block totals -> one row of a per-block gradient slab (fused path; summed by the
 //           weight-gradient launch) or global f32 atomics (generic path)
 constexpr int DC = 18;             // dConv2 image side: 10 + 2*4 zero ring
-constexpr int DCN = DC * DC * C2;  // 5184, channel-last [y][x][co]; zero pixel at DCN
+constexpr int DCN = DC * DC * C2;  // 5184, channel-last [y][x][co]
+// (Measured round 5: two 8-channel planes with one-pixel-row tiles — conflict-free 256-byte operand
+// reads — made phase B slower, 5.48 -> 5.72 us: the 4 extra tiles cost more than the conflicts.)
 constexpr int DTS = 136;           // row stride of dConv2^T [co][position] (100 used, zero padded; 272 B: rows on distinct LDS slots)
 // fused path: per-block conv-gradient slab row [dW1 150 | db1 6 | dW2 2400 | db2 16] (+pad)
 constexpr int SL_W1 = 0, SL_B1 = SL_W1 + C1 * R1, SL_W2 = SL_B1 + C1, SL_B2 = SL_W2 + C2 * R2;
 constexpr int SLABN = SL_B2 + C2;  // 2572
 constexpr int SLABW = 2576;
 
+constexpr int DX2S = Q1 * Q1 + 4;  // dx2 channel row: the 196 windows + 4 zeros (phase C's last k-step)
+constexpr int PT_N = 8 * 25 + 8;    // posT entries: windows 0 .. 8*24 + 7
 struct BwdSmem {
   // k.imgb: bf16 image in two copies: [0][i] = img[i], [1][i] = img[i + 1], so any pair (x, x+1) is
   // ONE aligned 4-byte read (copy x & 1 at x & ~1) — the dW1 B operand is 4 pair reads per fragment.
   // Zero pair at [0][IMGZ].  k.a1 (+ zero slot at A1N), k.c1 (+ never-matching slot at A1N), k.c2.
   KeepSmem k;
-  float dx2[SPB][A1N + 4];          // dL/d a1 (conv2 input gradient)
+  float dx2[SPB][C1 * DX2S];        // dL/d a1 (conv2 input gradient), channel rows of DX2S (zero tail)
+  uint16_t posT[PT_N];              // phase C: byte offset 2*pos1(w, 0) of pool window w (w >= 196: clamped)
   uint16_t a1o[SPB][A1N + 8];       // a1 shifted by one element (pair reads for the dW2 B operand)
-  uint16_t dc2[SPB][DCN + 16];      // dense channel-last dConv2 with zero ring; zero pixel at DCN
+  uint16_t dc2[SPB][DCN + 16];      // dense channel-last dConv2 with zero ring
                                     // (after phase B: the 16 waves' dW1 partials [16][2][256] f32)
   uint16_t dcT[SPB][C2 * DTS];      // dConv2^T [co][p = 4*window + quadrant] (wgrad2 A operand)
   // fused classifier backward (MLP=true): gradients of the 4 samples as MFMA A rows
@@ -732,9 +763,10 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
                                          const uint8_t* __restrict__ code1g, const uint16_t* __restrict__ da2g,
                                          const uint8_t* __restrict__ code2g, const float* __restrict__ w2,
                                          float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dw2,
-                                         float* __restrict__ db2, int N, int rounds, ClsBwd cb) {
+                                         float* __restrict__ db2, int N, int rounds, ClsBwd cb,
+                                         const ClsBwdFrags* pre = nullptr) {
   RK_TR(cb.trace, 0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hi = lane >> 4, lo = lane & 15;
 
   // conv2-dgrad reduction index ordered k = (kh*5 + kw)*16 + co (co fastest), so a lane's 8
@@ -765,12 +797,18 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
   if (MLP && cb.ce && threadIdx.x == 0) sm.lossp[0] = sm.cecnt[0] = 0.f;
   // fused path: the classifier dgrad B fragments and ReLU masks are loaded now, so the chain below
   // runs on registers and LDS only (each was one global round trip after a barrier)
-  bf16x8 fb3, fb2[3], fb1[2][4];
+  ClsBwdFrags fl;
+  if constexpr (MLP) {
+    if (pre) fl = *pre;
+    else load_cls_bwd(cb.frag, wave, lane, fl);
+  }
+  const bf16x8& fb3 = fl.fb3;
+  const bf16x8 (&fb2)[3] = fl.fb2;
+  const bf16x8 (&fb1)[2][4] = fl.fb1;
   uint2 mk2 = make_uint2(0u, 0u), mk1 = make_uint2(0u, 0u);
   if constexpr (MLP) {
     const int nb = blockIdx.x * rounds * SPB;
     if (wave < 6) {
-      fb3 = cb.frag[(OFF_B3 + wave) * 64 + lane];
       const int col = 16 * wave + lo;
       if (RES) {
         if (hi == 0)
@@ -779,22 +817,12 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       } else if (hi == 0) mk2 = *(const uint2*)(cb.h2T + (int64_t)(col < F2 ? col : 0) * N + nb);
     }
     if (wave < 8) {
-#pragma unroll
-      for (int ks = 0; ks < 3; ++ks) fb2[ks] = cb.frag[(OFF_B2 + wave * 3 + ks) * 64 + lane];
       const int col = 16 * wave + lo;
       if (RES) {
         if (hi == 0)
           mk1 = make_uint2((uint32_t)sm.k.h1[0][col] | ((uint32_t)sm.k.h1[1][col] << 16),
                            (uint32_t)sm.k.h1[2][col] | ((uint32_t)sm.k.h1[3][col] << 16));
       } else if (hi == 0) mk1 = *(const uint2*)(cb.h1T + (int64_t)(col < F1 ? col : 0) * N + nb);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int t = wave + 16 * u;
-      if (t < 25) {
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) fb1[u][ks] = cb.frag[(OFF_B1 + t * 4 + ks) * 64 + lane];
-      }
     }
   }
 
@@ -1035,6 +1063,12 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     }
     lds_barrier();
     RK_TR(cb.trace, 7);
+    if (threadIdx.x < SPB * C1 * 4)  // dx2 zero tails (phase B writes windows < 196 only)
+      sm.dx2[threadIdx.x / (C1 * 4)][(threadIdx.x / 4) % C1 * DX2S + Q1 * Q1 + (threadIdx.x & 3)] = 0.f;
+    if (threadIdx.x >= NTHR - PT_N) {  // phase C's window -> image offset table
+      const int w = threadIdx.x - (NTHR - PT_N);
+      sm.posT[w] = (uint16_t)(2 * pos1(min(w, Q1 * Q1 - 1), 0));
+    }
     for (int i = threadIdx.x; i < SPB * A2N; i += NTHR) {  // scatter the pooled gradients
       const int sl = i / A2N, e = i % A2N, co = e / 25, w = e % 25;
       const int n = nbase + sl, nc = n < N ? n : 0;
@@ -1167,7 +1201,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int p = 16 * t + 4 * hi + i;
-            if (p < Q1 * Q1) sm.dx2[sl][lo * (Q1 * Q1) + p] = acc[i];
+            if (p < Q1 * Q1) sm.dx2[sl][lo * DX2S + p] = acc[i];
           }
         }
       }
@@ -1180,46 +1214,47 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     // column r = 25 of tile u = 1 is the ones column (db1)
     f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     {
-      // B element j of tile u at img offset pa(window) + cst[u][k]: the pair's copy (x & 1) does
-      // not depend on the window (pos1 offsets are even), so it is folded into cst once
-      int cst[2][4], pm[2];
+      // Wave = (sample wave & 3, k-steps ks = wave / 4 + 4j): every per-step index is a lane constant
+      // plus the wave-uniform 8*ks, so a k-step is ~25 VALU instructions (it was ~80 with the window
+      // divisions, validity selects and code compares per lane; phase C was VALU-issue-bound).
+      // A (row co = lo, k = the 4 positions of windows wa = 8ks + 2hi and wa + 1): the pooled gradient
+      // placed at its argmax position by a 64-bit shift (code >= 4: ReLU off -> zero); lanes co >= 6
+      // duplicate channel 0 (their C rows are never stored); windows >= 196 read dx2's zero tail.
+      // B (k, col r = 16u + lo): 4 pair reads at the window's image offset (posT) + a lane constant;
+      // column r = 25 is the ones column (db1: offset 0 -> the ones pair), r > 25 are never stored.
+      int cst[2][4];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int r = 16 * u + lo;
-        const bool tap = r < R1;
-        pm[u] = tap ? 1 : 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          if (tap) {
-            const int x = (k & 1) * IMGS + (r / KS) * IMGS + (r % KS);
-            cst[u][k] = (x & 1) ? (IMGN + 8) + x - 1 : x;  // copy 1 holds img[x] at x - 1
-          } else {
-            cst[u][k] = r == R1 ? IMGN + 2 : IMGZ;  // ones pair (db1) / zero pair
-          }
+          const int x = (k & 1) * IMGS + (min(r, R1 - 1) / KS) * IMGS + (min(r, R1 - 1) % KS);
+          cst[u][k] = 2 * (r == R1 ? IMGN + 2 : ((x & 1) ? (IMGN + 8) + x - 1 : x));  // bytes
         }
       }
-      for (int it = wave; it < SPB * 25; it += NTHR / 64) {
-        const int sl = it / 25, ks = it % 25;
-        const int wa = 8 * ks + 2 * hi, wb = wa + 1;  // this lane's 2 windows (j<4 / j>=4)
-        const bool va = lo < C1 && wa < Q1 * Q1, vb = lo < C1 && wb < Q1 * Q1;
-        const int ia = va ? lo * 196 + wa : A1N, ib = vb ? lo * 196 + wb : A1N;
-        const float da = sm.dx2[sl][va ? ia : 0], dbv = sm.dx2[sl][vb ? ib : 0];
-        const uint32_t ca = sm.k.c1[sl][ia], cb = sm.k.c1[sl][ib];
-        // windows past the grid have an all-zero A; clamp them to a valid window for B
-        const int pa = pos1(min(wa, Q1 * Q1 - 1), 0), pb = pos1(min(wb, Q1 * Q1 - 1), 0);
-        const uint32_t ab = c16(da), bb = c16(dbv);
-        const uint4 aw = make_uint4((ca == 0 ? ab : 0u) | (ca == 1 ? ab << 16 : 0u),
-                                    (ca == 2 ? ab : 0u) | (ca == 3 ? ab << 16 : 0u),
-                                    (cb == 0 ? bb : 0u) | (cb == 1 ? bb << 16 : 0u),
-                                    (cb == 2 ? bb : 0u) | (cb == 3 ? bb << 16 : 0u));
-        const bf16x8 a = __builtin_bit_cast(bf16x8, aw);
-        const uint16_t* ib0 = &sm.k.imgb[sl][0][0];
+      const bool onecol = lo == R1 - 16;  // u = 1 lane of the ones column: no window offset
+      const int sl = wave & (SPB - 1);
+      const int co = lo < C1 ? lo : 0;
+      const float* dxr = &sm.dx2[sl][co * DX2S + 2 * hi];
+      const uint8_t* cr = &sm.k.c1[sl][co * (Q1 * Q1) + 2 * hi];
+      const uint16_t* pt = &sm.posT[2 * hi];
+      const char* ib = (const char*)&sm.k.imgb[sl][0][0];
+      static_assert(NTHR / 64 == 4 * SPB, "4 waves per sample in phase C");
+      for (int ks = wave / SPB; ks < 25; ks += 4) {
+        const int o = 8 * ks;
+        const float da = dxr[o], dbv = dxr[o + 1];
+        const uint32_t ca = cr[o], cb2 = cr[o + 1];
+        const uint32_t pa = pt[o], pb = pt[o + 1];
+        const uint32_t ab = pack16t<kH16>(da, dbv);
+        const uint64_t ea = ca < 4 ? (uint64_t)(ab & 0xffffu) << (16 * ca) : 0ull;
+        const uint64_t eb = cb2 < 4 ? (uint64_t)(ab >> 16) << (16 * cb2) : 0ull;
+        const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4((uint32_t)ea, (uint32_t)(ea >> 32), (uint32_t)eb,
+                                                               (uint32_t)(eb >> 32)));
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const uint4 w = make_uint4(*(const uint32_t*)(ib0 + pa * pm[u] + cst[u][0]),
-                                     *(const uint32_t*)(ib0 + pa * pm[u] + cst[u][1]),
-                                     *(const uint32_t*)(ib0 + pb * pm[u] + cst[u][2]),
-                                     *(const uint32_t*)(ib0 + pb * pm[u] + cst[u][3]));
+          const uint32_t qa = (u == 1 && onecol) ? 0u : pa, qb = (u == 1 && onecol) ? 0u : pb;
+          const uint4 w = make_uint4(*(const uint32_t*)(ib + qa + cst[u][0]), *(const uint32_t*)(ib + qa + cst[u][1]),
+                                     *(const uint32_t*)(ib + qb + cst[u][2]), *(const uint32_t*)(ib + qb + cst[u][3]));
           g1[u] = mfma16(a, __builtin_bit_cast(bf16x8, w), g1[u]);
         }
       }
@@ -1343,14 +1378,18 @@ __global__ void __launch_bounds__(NTHR) lenet_train_kernel(const float* __restri
   __shared__ __attribute__((aligned(16))) TrainSmem sm;
   // a1 / codes stay in LDS (sm.f.k == sm.b.k): no global copies (a regular backward after a missed
   // speculation re-runs rk_lenet_fwd for them, ops/lenet.py)
-  fwd_body<true>(sm.f, x, nullptr, b1, nullptr, b2, nullptr, nullptr, nullptr, nullptr, N, cf, rs);
-  __syncthreads();  // LDS reuse + this block's global stores visible to all its waves
+  ClsBwdFrags pre;
+  fwd_body<true>(sm.f, x, nullptr, b1, nullptr, b2, nullptr, nullptr, nullptr, nullptr, N, cf, rs, &pre, cb.frag);
+  // LDS reuse only: this backward (RES) reads nothing the forward wrote to global memory (logits,
+  // labels, masks and a1 / codes are in LDS), so the forward's stores need not have landed — a
+  // __syncthreads() here would wait for all of them (vmcnt(0))
+  lds_barrier();
   if (rs.rows) {  // the block's targets through the rows (as its own label stores, which it just made)
     cb.row_table = rs.rows;
     cb.row_labels = rs.ysrc;
   }
   bwd_body<true, true>(sm.b, x, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, N, 1,
-                       cb);
+                       cb, &pre);
 }
 
 }  // namespace

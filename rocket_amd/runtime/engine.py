@@ -182,20 +182,24 @@ class EngineScheduler:
     accumulation micro-steps it only advances ``_step_count``.
     """
 
-    #: Opt-in (ROCKET_SCHED_SPECULATE=1), fp16 device-resident scaler only: instead of waiting for
-    #: the step's skip flag (a host sync per step), step the scheduler assuming "not skipped" and
-    #: verify at the next scheduler step; a wrong guess (an inf/NaN step) restores the scheduler and
-    #: the param-group hyperparameters.  The one update issued in between then ran with the
-    #: speculated lr, which accelerate never does (it does not step the scheduler after a skipped
-    #: step), so the default is the exact form: the lr sequence matches accelerate's.
+    #: fp16 device-resident scaler: the step's skip flag is on the device when the scheduler steps.
+    #: Exact form (default): step the scheduler provisionally and keep it undecided only when that
+    #: leaves every param-group hyperparameter unchanged (StepLR / MultiStepLR between milestones,
+    #: warmup plateaus...) — the next update then runs with the same lr whichever way the flag reads,
+    #: so the lr sequence is accelerate's, and the flag is read at the next scheduler step (a
+    #: skipped step rolls the scheduler state back).  A step that would change a hyperparameter
+    #: waits for the flag (a host sync on those steps only).
+    #: Opt-in (ROCKET_SCHED_SPECULATE=1): provisional steps also when the hyperparameters change;
+    #: after a skipped step one update then runs with the next lr, which accelerate never does.
     SPECULATE = os.environ.get("ROCKET_SCHED_SPECULATE", "0") == "1"
 
     def __init__(self, scheduler, optimizers: List[EngineOptimizer], engine: "Engine"):
         self.scheduler = scheduler
         self.optimizers = optimizers
         self.engine = engine
-        self._pending = None  # (flag handles, snapshot) of a speculated step
-        self.mispredicted = 0
+        self._pending = None  # (flag handles, snapshot) of a provisional step
+        self.mispredicted = 0  # provisional steps rolled back (their update was skipped)
+        self.provisional = 0  # steps taken before their skip flag was read
 
     def _groups(self):
         return [g for o in self.optimizers for g in o.optimizer.param_groups]
@@ -227,14 +231,20 @@ class EngineScheduler:
             self.scheduler._step_count += 1
             return
         self._resolve()
-        if self.SPECULATE:
-            lazy = [o for o in self.optimizers if o._skip_lazy and o._lazy_handle is not None]
-            handles = [o._lazy_handle for o in lazy]
-            if lazy and len(lazy) == len(self.optimizers) and not all(FusedGradScaler.handle_ready(h) for h in handles):
-                snap = self._snapshot()
-                self._do_step(*args, **kwargs)
+        lazy = [o for o in self.optimizers if o._skip_lazy and o._lazy_handle is not None]
+        handles = [o._lazy_handle for o in lazy]
+        if lazy and len(lazy) == len(self.optimizers) and not all(FusedGradScaler.handle_ready(h) for h in handles):
+            snap = self._snapshot()
+            self._do_step(*args, **kwargs)
+            if self.SPECULATE or all(
+                    {k: v for k, v in g.items() if k != "params"} == saved for g, saved in zip(self._groups(), snap[1])):
+                self.provisional += 1
                 self._pending = (handles, snap)
                 return
+            # this step moves a hyperparameter: undo it and decide on the flag itself
+            self.scheduler.load_state_dict(snap[0])
+            for g, saved in zip(self._groups(), snap[1]):
+                g.update(saved)
         if any(o.step_was_skipped for o in self.optimizers):
             return
         self._do_step(*args, **kwargs)

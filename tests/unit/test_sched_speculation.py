@@ -1,7 +1,9 @@
 """EngineScheduler under the fp16 device-resident scaler.
 
 Default (exact form): a skipped step never advances the schedule, as in accelerate
-(``accelerate@1.14.0:scheduler.py:54-83``; reference ``rocket/core/scheduler.py:94-113``).
+(``accelerate@1.14.0:scheduler.py:54-83``; reference ``rocket/core/scheduler.py:94-113``); a step
+whose skip flag has not landed is taken provisionally only when it leaves the hyperparameters
+unchanged (then no update can see the difference), else the flag is waited for.
 Opt-in speculation (ROCKET_SCHED_SPECULATE=1, runtime/engine.py EngineScheduler.SPECULATE): the
 scheduler steps when the step's skip flag has not landed yet and a mispredicted (skipped) step is
 rolled back when the flag is read; checkpoints settle the speculation first."""
@@ -129,3 +131,35 @@ def test_checkpoint_settles_a_mispredicted_speculation(tmp_path):
     eo._skip_lazy, eo._lazy_handle = True, _flag(True)
     sch.step()
     assert eo.state_dict()["param_groups"][0]["lr"] == 1.0
+
+
+def test_exact_form_defers_hyperparameter_neutral_steps():
+    """StepLR(step_size=3): steps that do not cross a milestone leave lr unchanged, so the exact form
+    takes them without waiting for the flag; the milestone step waits.  The lr sequence still
+    equals accelerate's, including across skipped steps."""
+    skips = [False, True, False, False, True, False, False, False, True, False]
+
+    def run():
+        p = torch.nn.Parameter(torch.zeros(2))
+        opt = torch.optim.SGD([p], lr=1.0)
+        eo = EngineOptimizer(opt, _Eng())
+        sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=3, gamma=0.5), [eo], _Eng())
+        seen = []
+        for sk in skips:
+            seen.append(opt.param_groups[0]["lr"])
+            eo._skip_lazy, eo._lazy_handle = True, _flag(sk)
+            sch.step()
+        sch.get_last_lr()
+        return seen, opt.param_groups[0]["lr"], sch
+
+    lr, n, want = 1.0, 0, []
+    for sk in skips:
+        want.append(lr)
+        if not sk:
+            n += 1
+            if n % 3 == 0:
+                lr *= 0.5
+    seen, final, sch = run()
+    assert seen == want and final == lr
+    assert sch.provisional >= 5  # the non-milestone steps never waited
+    assert sch.mispredicted >= 1  # and the skipped ones among them were rolled back
