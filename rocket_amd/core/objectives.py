@@ -170,6 +170,16 @@ class Loss(Capsule):
         self._step = state["step"]
 
 
+# ROCKET_OPT_EPILOGUE=0: no fused-producer optimizer epilogue / AMP check fold (read once)
+_OPT_EPILOGUE = os.environ.get("ROCKET_OPT_EPILOGUE", "1") != "0"
+
+
+def _is_fused_scaler(scaler) -> bool:
+    from rocket_amd.runtime.amp import FusedGradScaler
+
+    return isinstance(scaler, FusedGradScaler)
+
+
 class Optimizer(Capsule):
     def __init__(self, optimizer: torch.optim.Optimizer, tag: str = "opt", priority: int = 1000) -> None:
         super().__init__(statefull=False, priority=priority)
@@ -234,15 +244,12 @@ class Optimizer(Capsule):
             # a gradient-sync step and no AMP scaler.  A fused gradient producer (the LeNet weight-
             # gradient launch) then applies the update itself; see _FusedBase.epilogue.
             inner.epilogue_armed = (engine.sync_gradients and engine.num_processes == 1 and engine.scaler is None
-                                    and os.environ.get("ROCKET_OPT_EPILOGUE", "1") != "0")
+                                    and _OPT_EPILOGUE)
             # under the device fp16 scaler the same producer can instead flag non-finite gradients
             # itself (the step's separate check launch is then skipped; see _FusedBase.amp_checked):
             # exact when its gradients are final and local ones are all there is (one replica)
-            from rocket_amd.runtime.amp import FusedGradScaler
-
-            inner.amp_fold_armed = (engine.sync_gradients and engine.num_processes == 1
-                                    and isinstance(engine.scaler, FusedGradScaler)
-                                    and os.environ.get("ROCKET_OPT_EPILOGUE", "1") != "0")
+            inner.amp_fold_armed = (engine.sync_gradients and engine.num_processes == 1 and engine.scaler is not None
+                                    and _OPT_EPILOGUE and _is_fused_scaler(engine.scaler))
             if (inner.epilogue_armed or inner.amp_fold_armed) and not getattr(self, "_epi_tagged", False):
                 for g in inner.param_groups:
                     for p in g["params"]:

@@ -18,6 +18,8 @@ from __future__ import annotations
 
 from typing import List, Optional
 
+import operator
+
 import torch
 
 from rocket_amd.ops import _lib
@@ -39,6 +41,8 @@ class _FusedBase(torch.optim.Optimizer):
         self._hyper_host = None
         self._hyper_list = None
         self._hyper_dev = None
+        self._hyper_get = None
+        self._hyper_raw = None
         self._step_dev = None
         self._device = None
         self._gdtype = 0
@@ -110,8 +114,19 @@ class _FusedBase(torch.optim.Optimizer):
         self._opt_called = True  # what torch's LR schedulers check for "optimizer.step() ran first"
         return True
 
+    #: the param-group entries _hyper_row reads (raw values: an unchanged step is one tuple compare)
+    HYPER_KEYS: tuple = ()
+
     def refresh_hyper(self) -> None:
         """Upload the per-group hyper-parameters if a scheduler/user changed them (cheap when unchanged)."""
+        if self.HYPER_KEYS:
+            get = self._hyper_get
+            if get is None:
+                get = self._hyper_get = operator.itemgetter(*self.HYPER_KEYS)
+            raw = [get(g) for g in self.param_groups]
+            if raw == self._hyper_raw:
+                return  # (never cached while any entry is a tensor: those change in place)
+            self._hyper_raw = None if any(isinstance(v, torch.Tensor) for r in raw for v in r) else raw
         flat = [x for g in self.param_groups for x in self._hyper_row(g)]
         if flat != self._hyper_list:
             self._hyper_list = flat
@@ -318,6 +333,8 @@ class FusedAdamW(_FusedBase):
                         foreach=foreach, capturable=capturable, differentiable=differentiable, fused=fused)
         super().__init__(params, defaults)
 
+    HYPER_KEYS = ("lr", "betas", "eps", "weight_decay", "maximize")
+
     def _hyper_row(self, g):
         lr = float(g["lr"])
         b1, b2 = g["betas"]
@@ -346,6 +363,8 @@ class FusedSGD(_FusedBase):
                         nesterov=nesterov, maximize=maximize, foreach=foreach, differentiable=differentiable,
                         fused=fused)
         super().__init__(params, defaults)
+
+    HYPER_KEYS = ("lr", "momentum", "dampening", "weight_decay", "nesterov", "maximize")
 
     def _hyper_row(self, g):
         return [float(g["lr"]), float(g["momentum"]), float(g["dampening"]), float(g["weight_decay"]),

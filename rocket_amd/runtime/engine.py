@@ -224,7 +224,27 @@ class EngineScheduler:
             total = getattr(self.scheduler, "total_steps", None)
             if total is not None and self.scheduler._step_count > total:
                 continue
-            self.scheduler.step(*args, **kwargs)
+            if args or kwargs or not self._fast_step():
+                self.scheduler.step(*args, **kwargs)
+
+    def _fast_step(self) -> bool:
+        """``StepLR.step()`` between milestones without torch's generic machinery (~4 us of host
+        time per iteration): exactly what it does there — ``_step_count`` and ``last_epoch`` advance,
+        the param groups' lr stay, ``_last_lr`` is re-read.  Only for the exact class with float lrs
+        and off its first call (where torch checks the optimizer-order warnings)."""
+        s = self.scheduler
+        if type(s) is not torch.optim.lr_scheduler.StepLR or s._step_count == 1:
+            return False
+        e = s.last_epoch + 1
+        if e != 0 and e % s.step_size == 0:
+            return False  # a milestone: the lr changes
+        lrs = [g["lr"] for g in s.optimizer.param_groups]
+        if not all(type(v) is float for v in lrs):
+            return False
+        s._step_count += 1
+        s.last_epoch = e
+        s._last_lr = lrs
+        return True
 
     def step(self, *args, **kwargs):
         if not self.engine.sync_gradients:

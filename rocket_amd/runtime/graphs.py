@@ -64,6 +64,7 @@ other input is copied into a static buffer before replay.
 from __future__ import annotations
 
 import collections
+import operator
 import os
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -80,6 +81,9 @@ MAX_VARIANTS = 32
 
 def _use_launch_lists() -> bool:
     return os.environ.get("ROCKET_LAUNCH_LIST", "1") != "0"
+
+
+_VERSION = operator.attrgetter("_version")
 
 
 class _Part:
@@ -229,7 +233,8 @@ class StepGraphs:
         # (e.g. the fused LeNet's optimizer-maintained bf16 fragment table)
         if self._params is None:
             self._params = list(self.mod._module.parameters())
-        return tuple(t() for t in self._toks) + (sum(p._version for p in self._params),)
+        # (map + attrgetter: ~1 us less per step than a generator over the parameters)
+        return tuple([t() for t in self._toks]) + (sum(map(_VERSION, self._params)),)
 
     def _predict_sync(self) -> bool:
         engine = self.mod._accelerator

@@ -91,9 +91,11 @@ def test_optimizer_epilogue_matches_separate_update(tmp_path, monkeypatch):
     """The captured LeNet step applies AdamW inside the weight-gradient launch (optimizer epilogue):
     same update math per element as the multi-tensor launch, so training is bitwise identical to the
     same captured step with the separate optimizer launch — and the device step counter advances."""
-    monkeypatch.setenv("ROCKET_OPT_EPILOGUE", "0")
+    import rocket_amd.core.objectives as objectives
+
+    monkeypatch.setattr(objectives, "_OPT_EPILOGUE", False)  # ROCKET_OPT_EPILOGUE=0
     la, wa, ma = _train(tmp_path / "sep", capture=True, steps=10)
-    monkeypatch.setenv("ROCKET_OPT_EPILOGUE", "1")
+    monkeypatch.setattr(objectives, "_OPT_EPILOGUE", True)
     lb, wb, mb = _train(tmp_path / "epi", capture=True, steps=10)
     assert la == lb
     bad = {k: float((wa[k] - wb[k]).abs().max()) for k in wa if not torch.equal(wa[k], wb[k])}

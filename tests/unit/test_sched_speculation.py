@@ -163,3 +163,24 @@ def test_exact_form_defers_hyperparameter_neutral_steps():
     assert seen == want and final == lr
     assert sch.provisional >= 5  # the non-milestone steps never waited
     assert sch.mispredicted >= 1  # and the skipped ones among them were rolled back
+
+
+def test_steplr_fast_path_matches_torch():
+    """EngineScheduler's StepLR fast path (between milestones) leaves exactly torch's state."""
+    import copy
+
+    def make():
+        p = torch.nn.Parameter(torch.zeros(2))
+        opt = torch.optim.SGD([p], lr=1.0)
+        opt.step()
+        return opt, torch.optim.lr_scheduler.StepLR(opt, step_size=3, gamma=0.5)
+
+    opt_a, ref = make()
+    opt_b, s = make()
+    sch = EngineScheduler(s, [EngineOptimizer(opt_b, _Eng())], _Eng())
+    for _ in range(10):
+        ref.step()
+        sch.step()
+        assert opt_a.param_groups[0]["lr"] == opt_b.param_groups[0]["lr"]
+        assert ref.state_dict() == s.state_dict()
+    assert copy.deepcopy(s.get_last_lr()) == ref.get_last_lr()
