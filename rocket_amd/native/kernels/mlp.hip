@@ -466,6 +466,14 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   // already synchronises (its LDS reduction), so its memory round trip overlaps the gradient loads
   // instead of preceding them; likewise the count partials of a normalising launch
   const float cur = a.epi.on ? a.epi.step[0] : 0.f;
+  // the optimizer step counter's ticket, taken when the block STARTS: the block that arrives last
+  // advances the counter at its end (rk_opt::advance_step takes it at the end, so every block's
+  // tail waited one agent-scope atomic round trip).  Every block has read `cur` long before: the
+  // last block's store comes after its whole tile, microseconds after all tickets (and the loads
+  // issued before them) were taken.
+  unsigned ticket = 0;
+  if (a.epi.on && threadIdx.x == 0)
+    ticket = __hip_atomic_fetch_add(a.epi.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float cpart = 0.f;
   if (a.cnt_parts)
     for (int i = threadIdx.x; i < a.ncnt; i += NT) cpart += a.cnt_parts[i];
@@ -480,7 +488,10 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   } else {
     wgrad_tile<LDSV>(a, red, rsum, ks, sf, stage);
   }
-  if (a.epi.on) rk_opt::advance_step(a.epi.step, a.epi.counter, false, cur);
+  if (a.epi.on && threadIdx.x == 0 && ticket == gridDim.x - 1) {
+    a.epi.step[0] = cur + 1.f;
+    __hip_atomic_store(a.epi.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
 }
 

@@ -3,7 +3,7 @@
 # optimizer / scheduler tests, LeNet driver + long bench (host_issue_ms)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r5p; rm -rf $O; mkdir -p $O
+O=$R/gpurun_out/${RUN:-r5p}; rm -rf $O; mkdir -p $O
 cd $R && export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/gpu/test_graph_capture.py \
   tests/kernels/test_ce_optim.py tests/kernels/test_amp.py tests/gpu/test_launcher_gpu.py tests/examples > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
