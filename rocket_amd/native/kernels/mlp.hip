@@ -331,9 +331,9 @@ struct StepFill {
   rk_opt::AdamStep* s_ks;
   float cpart;   // this thread's share of the count partials (loaded at kernel start)
   float* s_cnt;  // [NW] per-wave count sums
+  rk_opt::AdamHyper hy;  // threads < kEpiGroups: their group's hyperparameters (loaded at kernel start)
   __device__ __forceinline__ void operator()() const {
-    if (a->epi.on && threadIdx.x < kEpiGroups)
-      s_ks[threadIdx.x] = rk_opt::adam_step(a->epi.hyper[threadIdx.x < a->epi.on ? threadIdx.x : 0], cur + 1.f);
+    if (a->epi.on && threadIdx.x < kEpiGroups) s_ks[threadIdx.x] = rk_opt::adam_step(hy, cur + 1.f);
     if (a->cnt_parts) {
       const float c = wave_sum(cpart);
       if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = c;
@@ -477,7 +477,11 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   float cpart = 0.f;
   if (a.cnt_parts)
     for (int i = threadIdx.x; i < a.ncnt; i += NT) cpart += a.cnt_parts[i];
-  const StepFill sf{&a, cur, s_ks, cpart, s_cnt};
+  // the hyperparameters too: read here, their latency hides under the tile's loads (read in sf(),
+  // after the MFMA loop, they were one more memory round trip on every block's tail)
+  rk_opt::AdamHyper hy{};
+  if (a.epi.on && threadIdx.x < kEpiGroups) hy = a.epi.hyper[threadIdx.x < a.epi.on ? threadIdx.x : 0];
+  const StepFill sf{&a, cur, s_ks, cpart, s_cnt, hy};
   const rk_opt::AdamStep* ks = a.epi.on ? s_ks : nullptr;
   if (a.has_rows && (int)blockIdx.x == (int)gridDim.x - 1) {
     // the step's batch cursor (no gradient work; still takes the optimizer step's ticket below)
