@@ -552,24 +552,28 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
   {
     const uint16_t* acl = sm.a1cl[slot];
     const bool two = sw + WPS < 7;  // wave-uniform
-    int pos[2];
-    bool wvalid[2];
+    // A rows of windows past the grid and k-steps of the padded taps (kk >= 25: zero B rows) read
+    // some in-grid pixel instead of the zero pixel: those rows are never stored and those products
+    // are zero, so no per-k-step select — the address is the lane's window base plus a per-k-step
+    // lane constant (the selects and tap divisions were ~8 VALU instructions per MFMA)
+    const uint16_t* wb[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int t = u ? (two ? sw + WPS : sw) : sw;
       const int w = 4 * t + (lo >> 2);
-      wvalid[u] = w < Q2 * Q2;
-      pos[u] = pos2(wvalid[u] ? w : 0, lo & 3);  // conv2 output position = pixel of a1
+      wb[u] = acl + pos2(w < Q2 * Q2 ? w : 0, lo & 3) * 8;  // conv2 output position = pixel of a1
+    }
+    int toff2[7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int kk = 4 * s + hi;
+      toff2[s] = kk < R1 ? ((kk / KS) * Q1 + (kk % KS)) * 8 : 0;
     }
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 7; ++s)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int kk = 4 * s + hi;
-        const int px = (wvalid[u] && kk < R1) ? pos[u] + (kk / KS) * Q1 + (kk % KS) : Q1 * Q1;  // Q1*Q1 -> zero pixel
-        acc[u] = mfma16(*(const bf16x8*)(acl + px * 8), bw2[s], acc[u]);
-      }
+      for (int u = 0; u < 2; ++u) acc[u] = mfma16(*(const bf16x8*)(wb[u] + toff2[s]), bw2[s], acc[u]);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (u == 1 && !two) break;
@@ -908,14 +912,12 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       }
       *(uint2*)(sm.k.c1[sl] + e) = *(const uint2*)(code1g + (int64_t)nc * A1N + e);
     }
-    for (int i = threadIdx.x; i < SPB * (DCN + 16) / 8; i += NTHR) {  // zero dc2 (16-byte stores)
-      const int sl = i / ((DCN + 16) / 8), e = (i % ((DCN + 16) / 8)) * 8;
-      *(uint4*)(sm.dc2[sl] + e) = make_uint4(0, 0, 0, 0);
-    }
-    for (int i = threadIdx.x; i < SPB * C2 * DTS / 8; i += NTHR) {
-      const int sl = i / (C2 * DTS / 8), e = (i % (C2 * DTS / 8)) * 8;
-      *(uint4*)(sm.dcT[sl] + e) = make_uint4(0, 0, 0, 0);
-    }
+    // zero dc2 / dcT (16-byte stores over each array as one flat range: no per-store division)
+    static_assert(sizeof(sm.dc2) % 16 == 0 && sizeof(sm.dcT) % 16 == 0, "whole 16-byte stores");
+    for (int i = threadIdx.x; i < (int)(sizeof(sm.dc2) / 16); i += NTHR)
+      ((uint4*)&sm.dc2[0][0])[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < (int)(sizeof(sm.dcT) / 16); i += NTHR)
+      ((uint4*)&sm.dcT[0][0])[i] = make_uint4(0, 0, 0, 0);
     RK_TR(cb.trace, 2);
     // the classifier chain runs while the conv operands above are still in flight
     if constexpr (MLP) {
@@ -1069,15 +1071,21 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       const int w = threadIdx.x - (NTHR - PT_N);
       sm.posT[w] = (uint16_t)(2 * pos1(min(w, Q1 * Q1 - 1), 0));
     }
-    for (int i = threadIdx.x; i < SPB * A2N; i += NTHR) {  // scatter the pooled gradients
-      const int sl = i / A2N, e = i % A2N, co = e / 25, w = e % 25;
-      const int n = nbase + sl, nc = n < N ? n : 0;
-      const uint16_t g = MLP ? sm.da2[sl][e] : da2g[(int64_t)nc * A2N + e];
-      const uint8_t cd = RES ? sm.k.c2[sl][e] : code2g[(int64_t)nc * A2N + e];
-      if (n < N && cd < 4) {
-        const int rr = 2 * (w / Q2) + (cd >> 1), cc = 2 * (w % Q2) + (cd & 1);
-        sm.dc2[sl][((rr + 4) * DC + cc + 4) * C2 + co] = g;
-        sm.dcT[sl][co * DTS + 4 * w + cd] = g;
+    // scatter the pooled gradients: thread e owns pooled element (co, w) of all SPB samples, so its
+    // index arithmetic (divisions by 25 and 5) is done once, not once per (sample, element)
+    static_assert(A2N <= NTHR, "one pooled element per thread");
+    if (threadIdx.x < A2N) {
+      const int e = threadIdx.x, co = e / 25, w = e % 25;
+      const int d0 = ((2 * (w / Q2) + 4) * DC + 2 * (w % Q2) + 4) * C2 + co, t0 = co * DTS + 4 * w;
+#pragma unroll
+      for (int sl = 0; sl < SPB; ++sl) {
+        const int n = nbase + sl, nc = n < N ? n : 0;
+        const uint16_t g = MLP ? sm.da2[sl][e] : da2g[(int64_t)nc * A2N + e];
+        const uint8_t cd = RES ? sm.k.c2[sl][e] : code2g[(int64_t)nc * A2N + e];
+        if (n < N && cd < 4) {
+          sm.dc2[sl][d0 + ((cd >> 1) * DC + (cd & 1)) * C2] = g;
+          sm.dcT[sl][t0 + cd] = g;
+        }
       }
     }
     if (threadIdx.x < SPB * 8) {
