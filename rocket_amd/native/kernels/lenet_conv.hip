@@ -712,6 +712,7 @@ struct BwdSmem {
   KeepSmem k;
   float dx2[SPB][C1 * DX2S];        // dL/d a1 (conv2 input gradient), channel rows of DX2S (zero tail)
   uint16_t posT[PT_N];              // phase C: byte offset 2*pos1(w, 0) of pool window w (w >= 196: clamped)
+  uint16_t posT2[32];               // phase B (dW2): pos2(w, 0) of conv2 window w (w >= 25: clamped)
   uint16_t a1o[SPB][A1N + 8];       // a1 shifted by one element (pair reads for the dW2 B operand)
   uint16_t dc2[SPB][DCN + 16];      // dense channel-last dConv2 with zero ring
                                     // (after phase B: the 16 waves' dW1 partials [16][2][256] f32)
@@ -912,12 +913,17 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       }
       *(uint2*)(sm.k.c1[sl] + e) = *(const uint2*)(code1g + (int64_t)nc * A1N + e);
     }
-    // zero dc2 / dcT (16-byte stores over each array as one flat range: no per-store division)
+    // zero dc2 / dcT (16-byte stores over each array as one flat range: no per-store division);
+    // with the fused cross-entropy, waves 1.. do it while wave 0 runs the softmax below
     static_assert(sizeof(sm.dc2) % 16 == 0 && sizeof(sm.dcT) % 16 == 0, "whole 16-byte stores");
-    for (int i = threadIdx.x; i < (int)(sizeof(sm.dc2) / 16); i += NTHR)
-      ((uint4*)&sm.dc2[0][0])[i] = make_uint4(0, 0, 0, 0);
-    for (int i = threadIdx.x; i < (int)(sizeof(sm.dcT) / 16); i += NTHR)
-      ((uint4*)&sm.dcT[0][0])[i] = make_uint4(0, 0, 0, 0);
+    {
+      const bool ce_wave0 = MLP && cb.ce;
+      if (!ce_wave0 || wave > 0) {
+        const int t0 = ce_wave0 ? (int)threadIdx.x - 64 : (int)threadIdx.x, nt = ce_wave0 ? NTHR - 64 : NTHR;
+        for (int i = t0; i < (int)(sizeof(sm.dc2) / 16); i += nt) ((uint4*)&sm.dc2[0][0])[i] = make_uint4(0, 0, 0, 0);
+        for (int i = t0; i < (int)(sizeof(sm.dcT) / 16); i += nt) ((uint4*)&sm.dcT[0][0])[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
     RK_TR(cb.trace, 2);
     // the classifier chain runs while the conv operands above are still in flight
     if constexpr (MLP) {
@@ -1070,6 +1076,9 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     if (threadIdx.x >= NTHR - PT_N) {  // phase C's window -> image offset table
       const int w = threadIdx.x - (NTHR - PT_N);
       sm.posT[w] = (uint16_t)(2 * pos1(min(w, Q1 * Q1 - 1), 0));
+    } else if (threadIdx.x >= NTHR - PT_N - 32) {  // phase B's (dW2) window -> a1 offset table
+      const int w = threadIdx.x - (NTHR - PT_N - 32);
+      sm.posT2[w] = (uint16_t)pos2(min(w, Q2 * Q2 - 1), 0);
     }
     // scatter the pooled gradients: thread e owns pooled element (co, w) of all SPB samples, so its
     // index arithmetic (divisions by 25 and 5) is done once, not once per (sample, element)
@@ -1112,20 +1121,28 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       // dW2 tile u = wave: rows co (16), cols r = 16u + lo; K = positions of 4 samples (4 x 4 k-steps)
       const int u = wave;
       const int r = 16 * u + lo;
-      const int cof = r < R2 ? (r / R1) * (Q1 * Q1) + ((r / KS) % KS) * Q1 + (r % KS) : -100000;
       // B element j of k-step ks at a1 offset (j<4 ? pa : pb) + ((j&3)>>1)*Q1 + (j&1): 4 pairs,
-      // each one aligned 4-byte read from a1 (even x) or a1o (odd x), relative to sample 0's a1
+      // each one aligned 4-byte read from a1 (even x) or a1o (odd x), relative to sample 0's a1.
+      // pos2(w, 0) and Q1 are even, so a pair's copy (x & 1) is that of the lane's column offset
+      // alone: x = posT2[w] + a lane constant per (k & 1).  Columns r > 150 are never stored and
+      // windows >= 25 meet zero A values (dcT's zero padding), so they read any in-range pair; the
+      // ones column r = 150 (db2) reads the ones pair whatever the window (multiplier 0).
       constexpr int A1O = (int)(offsetof(BwdSmem, a1o) - offsetof(BwdSmem, k.a1)) / 2;
+      const int rc = r < R2 ? r : R2 - 1;
+      const int cof = (rc / R1) * (Q1 * Q1) + ((rc / KS) % KS) * Q1 + (rc % KS);
+      const int wmul = r == R2 ? 0 : 1;
+      int cst2[2];
+#pragma unroll
+      for (int k1 = 0; k1 < 2; ++k1) {
+        const int c = cof + k1 * Q1;
+        cst2[k1] = r == R2 ? A1N + 2 : ((c & 1) ? A1O + c - 1 : c);
+      }
+      const uint16_t* pt2 = sm.posT2 + 2 * hi;
       int pofs[4][4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int wv = 8 * ks + 2 * hi + (k >> 1);
-          int x = (wv < Q2 * Q2 && cof >= 0) ? pos2(wv, 0) + cof + (k & 1) * Q1 : A1N;
-          if (r == R2) x = A1N + 2;  // ones pair -> db2
-          pofs[ks][k] = (x & 1) ? A1O + x - 1 : x;
-        }
+        for (int k = 0; k < 4; ++k) pofs[ks][k] = (int)pt2[8 * ks + (k >> 1)] * wmul + cst2[k & 1];
       const uint16_t* a1b = &sm.k.a1[0][0];
       // 16 k-steps (4 samples x 4), operands of step i + 1 read before step i's MFMA
       auto ld_a = [&](int i) {  // A[co = lo][p]
