@@ -135,7 +135,7 @@ constexpr int OFF_B2 = OFF_B3 + 6 * 1;     // fc2 dgrad: 8 (120) x 3 (84)
 constexpr int OFF_B1 = OFF_B2 + 8 * 3;     // fc1 dgrad: 25 (400) x 4 (120)
 constexpr int OFF_C1 = OFF_B1 + 25 * 4;    // conv1 fwd B: 1 k-step (25 taps)
 constexpr int OFF_C2 = OFF_C1 + 1;         // conv2 fwd B: 7 k-steps (25 taps x 8 padded channels)
-constexpr int OFF_D2 = OFF_C2 + 7;         // conv2 dgrad B: 13 k-steps (25 taps x 16 channels)
+constexpr int OFF_D2 = OFF_C2 + 7;         // conv2 dgrad weights, plain [tap 25][ci 8][co 16] (400 x 16 B of 13 x 1 KB)
 constexpr int NFRAG = OFF_D2 + 13;         // 282 fragments x 64 lanes x 16 B
 constexpr int A2P = 432;                   // LDS row of pooled conv2 output: data 0..399, zero 400..415, trash 424
 constexpr int A2TRASH = 424;
@@ -156,9 +156,9 @@ __global__ void __launch_bounds__(64) lenet_prep_kernel(const float* __restrict_
       } else if (f < OFF_D2) {  // B[k = (tap kk = 4s + hi, ci = j)][col = co lo]
         const int kk = 4 * (f - OFF_C2) + hi;
         if (kk < R1 && j < C1) x = cw2[(lo * C1 + j) * R1 + kk];
-      } else {  // dgrad B[k = (tap 2s + hi/2, co = 8(hi&1) + j)][col = ci lo]
-        const int kk = 2 * (f - OFF_D2) + (hi >> 1), co = 8 * (hi & 1) + j;
-        if (kk < R1 && lo < C1) x = cw2[(co * C1 + lo) * R1 + kk];
+      } else {  // dgrad weights [kk][ci][co]: 16-byte unit u = (kk, ci, co half), see d2frag
+        const int u = (f - OFF_D2) * 64 + lane, kk = u >> 4, ci = (u >> 1) & 7, co = 8 * (u & 1) + j;
+        if (kk < R1 && ci < C1) x = cw2[(co * C1 + ci) * R1 + kk];
       }
       v[j] = e16(x);
     }
@@ -233,7 +233,23 @@ struct RowSrc {
 // ------------------------------------------------------------------------------ forward
 constexpr int A1CL = Q1 * Q1 * 8;  // channel-last conv1 output: [pixel][8 channels], 6 used
 
-constexpr int K2P = 13;            // conv2-dgrad k-steps: (kh,kw,co) = 400 -> 416
+// conv2 dgrad as an implicit GEMM whose 16 B columns are (d, ci) = (lo >> 3, lo & 7): TWO output
+// pixels (ih, iw0 + d), iw0 even, per A row, so the A rows are the 98 pixel pairs of a sample and the
+// K index runs over a 5 x 6 window (dy, dx) of dConv2 pixels x 16 channels: 480 -> 15 k-steps
+// (with one output pixel per row and 16 columns for 6 channels: 13 tiles x 13 k-steps per sample;
+// this form is 7 x 15, -38% MFMAs and A-operand LDS reads).  B[(dy, dx, co)][(d, ci)] =
+// w2[co][ci][4 - dy][4 + d - dx] (0 where that kw is outside 0..4 or ci >= 6).
+constexpr int K2P = 15;
+constexpr int DGT = 7;              // dgrad row tiles per sample (98 pixel pairs -> 112 rows)
+
+// B fragment element group of conv2-dgrad k-step s, lane l from the plain [kk][ci][co] table (16-byte
+// units): lane (lo, hi) holds k = 32s + 8hi + j -> window position pi = 2s + hi/2 = (dy, dx) =
+// (pi / 6, pi % 6), co = 8(hi & 1) + j; column lo = (d, ci).  Returns -1 for an all-zero fragment.
+__device__ __forceinline__ int d2unit(int s, int l) {
+  const int h = l >> 4, c = l & 15, pi = 2 * s + (h >> 1), dy = pi / 6, dx = pi % 6;
+  const int d = c >> 3, ci = c & 7, kh = 4 - dy, kw = 4 + d - dx;
+  return (kw >= 0 && kw < KS && ci < C1) ? ((kh * KS + kw) * 8 + ci) * 2 + (h & 1) : -1;
+}
 
 // The forward state the backward reuses.  Both phase layouts (FwdSmem, BwdSmem) START with it, so in
 // the whole-step kernel (TrainSmem, a union of the two) the backward finds the staged image, the
@@ -343,7 +359,10 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
     }
     if constexpr (MLP) {
       if (rs.keep)  // the backward's conv2-dgrad fragments (its phase A then waits on no global load)
-        for (int i = threadIdx.x; i < K2P * 64; i += NTHR) sm.k.wfr[i] = cf.frag[OFF_D2 * 64 + i];
+        for (int i = threadIdx.x; i < K2P * 64; i += NTHR) {
+          const int u = d2unit(i >> 6, i & 63);
+          sm.k.wfr[i] = u >= 0 ? cf.frag[OFF_D2 * 64 + u] : bf16x8{};
+        }
     }
     for (int b = st; b < 4 * IMGS + IMG * 5 + 8; b += 64 * WPS) {  // border / zero-slot elements
       int bi;
@@ -686,8 +705,8 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
 //  phase A  stage 4 samples; expand the pooled conv2 gradient into a dense, zero-ringed
 //           dConv2 image [16][18][18] (bf16) through the argmax/ReLU codes
 //  phase B  conv2 dgrad as a GATHER implicit GEMM: dX2[pixel][ci] = sum_{co,kh,kw}
-//           dConv2[co][ih+4-kh][iw+4-kw] . W2[co][ci][kh][kw]  (13 pixel tiles x 13 k-steps per
-//           sample, all 16 waves); every output element is written by exactly one lane
+//           dConv2[co][ih+4-kh][iw+4-kw] . W2[co][ci][kh][kw]  (7 pixel-pair tiles x 15 k-steps per
+//           sample, see K2P, all 16 waves); every output element is written by exactly one lane
 //  phase C  dW2: waves 0..9 one 16-column tile each (issued alongside phase B — it needs no dX2),
 //           reducing over the 4 samples' positions in registers; then dW1 (2 column tiles) on all
 //           16 waves over a share of the 4 x 784 positions
@@ -774,24 +793,24 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hi = lane >> 4, lo = lane & 15;
 
-  // conv2-dgrad reduction index ordered k = (kh*5 + kw)*16 + co (co fastest), so a lane's 8
-  // consecutive k share (kh, kw) and step co by 1: gather offsets are base + j*DC*DC.
-  // B operand B[k][col = ci] = w2[co][ci][kh][kw]: 13 k-steps, lanes lo < 6.
-  // kept in LDS in fragment order (wfr[s*64 + lane]), one ds_read_b128 per k-step
+  // conv2-dgrad B operand (two output pixels per A row, see K2P): 15 k-steps kept in LDS in
+  // fragment order (wfr[s*64 + lane]), one ds_read_b128 per k-step
   if constexpr (RES) {
     // staged by the forward (KeepSmem)
   } else if constexpr (MLP) {
-    for (int i = threadIdx.x; i < K2P * 64; i += NTHR) sm.k.wfr[i] = cb.frag[OFF_D2 * 64 + i];
+    for (int i = threadIdx.x; i < K2P * 64; i += NTHR) {
+      const int u = d2unit(i >> 6, i & 63);
+      sm.k.wfr[i] = u >= 0 ? cb.frag[OFF_D2 * 64 + u] : bf16x8{};
+    }
   } else
   for (int i = threadIdx.x; i < K2P * 64; i += NTHR) {
-    const int s = i >> 6, l = i & 63, h = l >> 4, c = l & 15;
+    const int u = d2unit(i >> 6, i & 63), kk = u >> 4, ci = (u >> 1) & 7;
     bf16x8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int kk = 2 * s + (h >> 1), co = 8 * (h & 1) + j;
-      const bool ok = kk < R1 && c < C1;
-      const float f = w2[ok ? (co * C1 + c) * R1 + kk : 0];
-      v[j] = e16(ok ? f : 0.f);
+      const int co = 8 * (u & 1) + j;
+      const float f = w2[u >= 0 ? (co * C1 + ci) * R1 + kk : 0];
+      v[j] = e16(u >= 0 ? f : 0.f);
     }
     sm.k.wfr[i] = v;
   }
@@ -1111,9 +1130,9 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     lds_barrier();
     RK_TR(cb.trace, 8);
 
-    // ---- phase B: conv2 dgrad (4 samples x 13 pixel tiles) and dW2 (10 column tiles), which
-    // needs only dcT and a1: waves 0..9 take one dW2 tile + two dgrad tiles, waves 10..15 five or
-    // six dgrad tiles each.  Per-lane address offsets are hoisted out of the tile loops (the phase is
+    // ---- phase B: conv2 dgrad (4 samples x 7 pixel-pair tiles) and dW2 (10 column tiles), which
+    // needs only dcT and a1: 38 work items (the dW2 tiles, then the dgrad tiles) dealt round-robin,
+    // item w + 16i to wave w: waves 0..5 a dW2 tile + 2 dgrad tiles, 6..9 a dW2 tile + 1, 10..15 2.  Per-lane address offsets are hoisted out of the tile loops (the phase is
     // VALU-issue-bound, not MFMA- or LDS-bound), and the bias gradients come out of the MFMAs as
     // "ones columns" (B column r = R2 of dW2 / r = R1 of dW1 is all ones -> C = row sums of A).
     f32x4 g2 = {0.f, 0.f, 0.f, 0.f};         // waves 0..9: dW2 tile u = wave (col r = 150: db2)
@@ -1172,10 +1191,8 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     }
     RK_TRW(cb.trace, 16);  // per wave: dW2 tile done
     {
-      constexpr int NDG = SPB * 13, NHEAVY = 32;  // dgrad tiles; [0, 32) -> waves 10..15, rest 2 per wave 0..9
-      const int t_begin = wave >= 10 ? wave - 10 : NHEAVY + wave;
-      const int t_step = wave >= 10 ? 6 : 10;
-      const int t_end = wave >= 10 ? NHEAVY : NDG;
+      constexpr int NDG = SPB * DGT;  // dgrad tiles = work items 10 .. 37
+      const int t_begin = wave >= 10 ? wave - 10 : wave + 6;
       // fused path: this lane's B fragments read from LDS once per wave, not once per tile (the
       // generic multi-round variant keeps re-reading them: registers would spill there)
       bf16x8 wr[MLP ? K2P : 1];
@@ -1183,33 +1200,29 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
 #pragma unroll
         for (int s = 0; s < K2P; ++s) wr[s] = sm.k.wfr[s * 64 + lane];
       }
-      // pixel (ih, iw) reads dConv2 pixel (ih + 4 - kh, iw + 4 - kw), tap kk = 2s + hi/2; the pad
-      // tap kk = 25 has zero weights, so it may read any finite pixel (clamped to tap 24)
-      int toff[K2P];
-#pragma unroll
-      for (int s = 0; s < K2P; ++s) {
-        const int kk = min(2 * s + (hi >> 1), R1 - 1);
-        toff[s] = ((4 - kk / KS) * DC + (4 - kk % KS)) * C2 + 8 * (hi & 1);
-      }
-      for (int tt = t_begin; tt < t_end; tt += t_step) {
-        const int sl = tt / 13, t = tt % 13;
-        const int pix = 16 * t + lo;  // A row of this lane (pixels >= 196: rows discarded below)
-        const bool pv = pix < Q1 * Q1;
-        const int ih = pv ? pix / Q1 : 0, iw = pv ? pix % Q1 : 0;
-        const uint16_t* ab = sm.dc2[sl] + (ih * DC + iw) * C2;
+      // A row = pixel pair (ih, iw0 = 2jx .. +1) reads the (ring) dConv2 pixels (ih + dy, iw0 + dx):
+      // k-step s covers window positions 2s, 2s + 1 = (dy, dx) = (s / 3, 2(s % 3) + hi / 2), channels
+      // 8(hi & 1) ..: the lane part is 8hi elements, the rest an immediate per k-step
+      auto toff = [](int s) { return ((s / 3) * DC + 2 * (s % 3)) * C2; };
+      for (int tt = t_begin; tt < NDG; tt += 16) {
+        const int sl = tt / DGT, t = tt % DGT;
+        const int m = 16 * t + lo;  // A row of this lane (pairs >= 98: rows discarded below)
+        const bool pv = m < Q1 * Q1 / 2;
+        const int ih = pv ? m / (Q1 / 2) : 0, iw0 = pv ? 2 * (m % (Q1 / 2)) : 0;
+        const uint16_t* ab = sm.dc2[sl] + (ih * DC + iw0) * C2 + 8 * hi;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         // A operands in chunks of 4 k-steps, the next chunk's LDS reads issued before this
         // chunk's MFMAs (one read + wait per MFMA would expose the LDS latency every step)
         constexpr int CH = 4, NCH = (K2P + CH - 1) / CH;
         bf16x8 abuf[2][CH];
 #pragma unroll
-        for (int q = 0; q < CH; ++q) abuf[0][q] = *(const bf16x8*)(ab + toff[q]);
+        for (int q = 0; q < CH; ++q) abuf[0][q] = *(const bf16x8*)(ab + toff(q));
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
           if (c + 1 < NCH) {
 #pragma unroll
             for (int q = 0; q < CH; ++q)
-              if ((c + 1) * CH + q < K2P) abuf[(c + 1) & 1][q] = *(const bf16x8*)(ab + toff[(c + 1) * CH + q]);
+              if ((c + 1) * CH + q < K2P) abuf[(c + 1) & 1][q] = *(const bf16x8*)(ab + toff((c + 1) * CH + q));
           }
           __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this chunk's MFMAs
 #pragma unroll
@@ -1221,12 +1234,14 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
             }
           }
         }
-        // C[row = pixel 16t + 4hi + i][col = ci = lo]
-        if (lo < C1) {
+        // C[row = pair 16t + 4hi + i][col = (d, ci) = (lo >> 3, lo & 7)] -> pixel 2 * pair + d
+        // (a pair's two pixels are adjacent in one image row: Q1 is even)
+        if ((lo & 7) < C1) {
+          float* dst = sm.dx2[sl] + (lo & 7) * DX2S + (lo >> 3);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int p = 16 * t + 4 * hi + i;
-            if (p < Q1 * Q1) sm.dx2[sl][lo * DX2S + p] = acc[i];
+            const int mp = 16 * t + 4 * hi + i;
+            if (mp < Q1 * Q1 / 2) dst[2 * mp] = acc[i];
           }
         }
       }

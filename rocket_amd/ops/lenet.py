@@ -197,11 +197,11 @@ def _frag_index_maps():
                     kk = 4 * (f - _OFF_C2) + hi
                     ok = (kk < 25) & (j < 6)
                     elem, key, col = (lo * 6 + j) * 25 + kk, "c2", 0
-                else:
-                    kk = 2 * (f - _OFF_D2) + (hi >> 1)
-                    co = 8 * (hi & 1) + j
-                    ok = (kk < 25) & (lo < 6)
-                    elem, key, col = (co * 6 + lo) * 25 + kk, "c2", 1
+                else:  # plain [kk][ci 8][co 16] dgrad weights, 16-byte unit u = (kk, ci, co half)
+                    u = (f - _OFF_D2) * 64 + lane
+                    kk, ci, co = u >> 4, (u >> 1) & 7, 8 * (u & 1) + j
+                    ok = (kk < 25) & (ci < 6)
+                    elem, key, col = (co * 6 + ci) * 25 + kk, "c2", 1
             else:
                 if f < _OFF_F2:
                     key, tile, ks, bwd = "f1", (f - _OFF_F1) // 13, (f - _OFF_F1) % 13, 0

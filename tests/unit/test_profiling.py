@@ -47,3 +47,53 @@ def test_lenet_fragment_index_maps_cover_every_weight_once():
     for name, m, has_bwd in zip(("fc1", "fc2", "fc3", "conv1", "conv2"), maps, (1, 1, 1, 0, 1)):
         assert (m[:, 0] >= 0).all(), name
         assert ((m[:, 1] >= 0).all() if has_bwd else (m[:, 1] < 0).all()), name
+
+
+def test_lenet_conv2_dgrad_pixel_pair_decomposition():
+    """Host model of the whole-step kernel's conv2 dgrad (lenet_conv.hip K2P / d2unit / phase B):
+    A rows = pixel pairs, K = a 5 x 6 window of ring dConv2 pixels x 16 channels, columns (d, ci),
+    B fragments gathered from the plain [kk][ci][co] table — equals the conv2 input gradient."""
+    import numpy as np
+    import torch
+
+    from rocket_amd.ops.lenet import _OFF_D2, _frag_index_maps
+
+    g = torch.Generator().manual_seed(0)
+    w2 = torch.randn(16, 6, 5, 5, generator=g)
+    dc = torch.randn(1, 16, 10, 10, generator=g)
+    ref = torch.nn.grad.conv2d_input((1, 6, 14, 14), w2, dc)[0]  # [6][14][14]
+    # the fragment table's dgrad section, written through the optimizer's index map
+    table = np.zeros(282 * 64 * 8, dtype=np.float32)
+    m = _frag_index_maps()[4][:, 1]
+    table[m] = w2.numpy().reshape(-1)
+    sect = table[_OFF_D2 * 512:].reshape(-1, 8)  # 16-byte units
+
+    def d2unit(s, lane):
+        h, c = lane >> 4, lane & 15
+        pi = 2 * s + (h >> 1)
+        dy, dx, d, ci = pi // 6, pi % 6, c >> 3, c & 7
+        kh, kw = 4 - dy, 4 + d - dx
+        return ((kh * 5 + kw) * 8 + ci) * 2 + (h & 1) if (0 <= kw < 5 and ci < 6) else -1
+
+    B = np.zeros((15 * 32, 16), dtype=np.float32)  # B[k = 32s + 8hi + j][col lo]
+    for s in range(15):
+        for lane in range(64):
+            u = d2unit(s, lane)
+            if u >= 0:
+                B[32 * s + 8 * (lane >> 4):32 * s + 8 * (lane >> 4) + 8, lane & 15] = sect[u]
+    ring = np.zeros((18, 18, 16), dtype=np.float32)  # channel-last, zero ring of 4
+    ring[4:14, 4:14] = dc[0].permute(1, 2, 0).numpy()
+    flat = ring.reshape(-1)
+    out = np.zeros((6, 196), dtype=np.float32)
+    for mrow in range(98):
+        ih, iw0 = mrow // 7, 2 * (mrow % 7)
+        a = np.zeros(480, dtype=np.float32)
+        for s in range(15):
+            for hi in range(4):
+                base = (ih * 18 + iw0) * 16 + 8 * hi + ((s // 3) * 18 + 2 * (s % 3)) * 16
+                a[32 * s + 8 * hi:32 * s + 8 * hi + 8] = flat[base:base + 8]
+        c = a @ B
+        for lo in range(16):
+            if (lo & 7) < 6:
+                out[lo & 7, 2 * mrow + (lo >> 3)] = c[lo]
+    np.testing.assert_allclose(out.reshape(6, 14, 14), ref.numpy(), rtol=1e-4, atol=1e-4)
