@@ -136,8 +136,9 @@ class StepTrace:
                       "median_end": us(w[:, 2].median()), "last_end": us(w[:, 2].max()), "blocks": int(w.shape[0])},
         }
         wall = self.wtr.cpu().double()
-        groups = {"fc3 tiles": (0, 3), "fc2 tiles": (3, 15), "fc1 tiles": (15, 67), "slab cols": (67, 108),
-                  "loss": (108, 109)}
+        # block ranges of the grouped launch (mlp.hip: 16 x 32 dW tiles, 32-column slab blocks)
+        groups = {"fc3 tiles": (0, 3), "fc2 tiles": (3, 27), "fc1 tiles": (27, 131), "slab cols": (131, 212),
+                  "loss": (212, 213)}
         wg = {}
         for name, (lo, hi) in groups.items():
             g = wall[lo:hi]

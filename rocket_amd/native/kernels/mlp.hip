@@ -320,8 +320,10 @@ __device__ __forceinline__ void flag_nonfinite(float* found, float v) {
 
 
 
-// one slab block: 64 columns x all rows; 8 row groups per block, 8 independent loads per thread
-// in flight, LDS reduce over the groups, one plain RMW per column (sole owner: deterministic)
+// one slab block: SLC = 32 columns x all rows; 16 row groups per block, 16 independent loads per
+// thread in flight, LDS reduce over the groups, one plain RMW per column (sole owner: deterministic).
+// (32 columns, not 64: the LeNet launch then has > 200 workgroups, the slab part 81 of them.)
+constexpr int SLC = 32, SLG = NT / SLC;
 constexpr int kEpiGroups = 4;  // param groups the epilogue precomputes step constants for
 
 // per-group Adam constants of this launch's step, written to LDS before the caller's barrier
@@ -389,17 +391,17 @@ __device__ void loss_fin_block(const LossFin& f, float (*red)[32 * 32], const St
 __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, float (*red)[32 * 32],
                                                   const rk_opt::AdamStep* ks, const StepFill& sf) {
   const SlabArgs& s = a.sl;
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = j * 64 + cl;
+  const int cl = threadIdx.x % SLC, rg = threadIdx.x / SLC;
+  const int c = j * SLC + cl;
   const bool ok = c < s.ncols;
   const float* base = s.slab + (ok ? c : 0);
   // the destination value is read up front (this block is its only writer), and each thread keeps
-  // 32 slab rows in flight at once: the launch is one memory round trip, not four
+  // its slab rows in flight at once: the launch is one memory round trip, not several
   float* dst = nullptr;
   float old = 0.f;
   int di = 0;
   rk_opt::EpiElem ee{};
-  if (threadIdx.x < 64 && ok) {
+  if (threadIdx.x < SLC && ok) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (c >= s.bound[i] && c < s.bound[i + 1] && s.dst[i]) {
@@ -411,25 +413,26 @@ __device__ __forceinline__ void slab_reduce_block(const WgradArgs& a, int j, flo
       if (ks) ee = rk_opt::epi_fetch(a.rsl[di], c - s.bound[di]);
     }
   }
-  constexpr int U = 32;
+  constexpr int U = 16;
   float acc = 0.f;
   int r = rg;
-  for (; r + (U - 1) * NW < s.rows; r += U * NW) {
+  for (; r + (U - 1) * SLG < s.rows; r += U * SLG) {
     float v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = base[(int64_t)(r + u * NW) * s.width];
+    for (int u = 0; u < U; ++u) v[u] = base[(int64_t)(r + u * SLG) * s.width];
 #pragma unroll
     for (int u = 0; u < U; ++u) acc += v[u];
   }
-  for (; r < s.rows; r += NW) acc += base[(int64_t)r * s.width];
-  red[rg][cl] = acc;
+  for (; r < s.rows; r += SLG) acc += base[(int64_t)r * s.width];
+  float* const redf = &red[0][0];
+  redf[rg * SLC + cl] = acc;
   sf();
   __syncthreads();
   if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
   if (dst) {
     float t = 0.f;
 #pragma unroll
-    for (int g = 0; g < NW; ++g) t += red[g][threadIdx.x];
+    for (int g = 0; g < SLG; ++g) t += redf[g * SLC + threadIdx.x];
     t *= sf.gs();
     if (ks) rk_opt::epi_apply(a.rsl[di], ks[a.rsl[di].group], c - s.bound[di], ee, old + t, a.epi.zero_grads);
     else *dst = old + t;
@@ -446,6 +449,12 @@ __device__ __forceinline__ bf16x8 rowfrag(const uint16_t* T, int R, int M, int r
   return __builtin_bit_cast(bf16x8, ok ? v : z);
 }
 
+
+// dW tile: WTN output features (rows of d^T) x 32 input features (rows of x^T).  16, not 32: the
+// LeNet launch's 67 tiles become 131 (> 200 workgroups with the slab blocks), each block's chain of
+// operand latency -> 8-wave LDS reduction -> optimizer epilogue half as long.
+constexpr int WTN = 16, WNI = WTN / 16, WEPT = WTN * 32 / NT;
+static_assert(WEPT >= 1 && WTN * 32 % NT == 0, "tile elements per thread");
 
 template <bool LDSV>
 __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks,
@@ -508,42 +517,45 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     if (i < a.nprob && (int)blockIdx.x >= a.p[i].tile_begin) pi = i;
   const WgradProb P = a.p[pi];
   const int t = blockIdx.x - P.tile_begin;
-  const int n0 = (t / P.tiles_k) * 32, k0 = (t % P.tiles_k) * 32;
+  const int n0 = (t / P.tiles_k) * WTN, k0 = (t % P.tiles_k) * 32;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lo = lane & 15, hi = lane >> 4;
   const int per = ((a.M + NW * 64 - 1) / (NW * 64)) * 64;  // batch range per wave, multiple of 64
   const int mb = wv * per, me = min(a.M, mb + per);
   // this block is the only writer of its dW tile / db rows: read their old values up front so the
   // final accumulate does not wait on a memory round trip
-  float dw_old[32 * 32 / NT];
-  rk_opt::EpiElem ew[32 * 32 / NT], eb{};
+  float dw_old[WEPT];
+  rk_opt::EpiElem ew[WEPT], eb{};
 #pragma unroll
-  for (int q = 0; q < 32 * 32 / NT; ++q) {
+  for (int q = 0; q < WEPT; ++q) {
     const int e = threadIdx.x + q * NT, r = e >> 5, c = e & 31;
     const bool in = n0 + r < P.N && k0 + c < P.K;
     dw_old[q] = in ? P.dw[(int64_t)(n0 + r) * P.K + k0 + c] : 0.f;
     if (ks && in) ew[q] = rk_opt::epi_fetch(a.rdw[pi], (int64_t)(n0 + r) * P.K + k0 + c);
   }
   if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime() + (uint64_t)(dw_old[0] == 12345.f);
-  const bool has_db = k0 == 0 && P.db && threadIdx.x < 32 && n0 + (int)threadIdx.x < P.N;
+  const bool has_db = k0 == 0 && P.db && threadIdx.x < WTN && n0 + (int)threadIdx.x < P.N;
   const float db_old = has_db ? P.db[n0 + threadIdx.x] : 0.f;
   if (ks && has_db) eb = rk_opt::epi_fetch(a.rdb[pi], n0 + threadIdx.x);
-  f32x4 acc[2][2];
+  f32x4 acc[WNI][2];
+  float rs[WNI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WNI; ++i) {
+    rs[i] = 0.f;
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float rs[2] = {0.f, 0.f};
+  }
   if constexpr (LDSV) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    // wave region: [32 d rows][256 B] then [32 x rows][256 B]; row r's 16-B chunk c at c ^ (r & 15)
+    // wave region: [WTN d rows][256 B] then [32 x rows][256 B]; row r's 16-B chunk c at c ^ (r & 15)
     // (the 16 rows a ds_read_b128 lane group reads hit 16 different bank slots); the LDS-DMA image
     // is lane-linear, so the swizzle is applied to each lane's SOURCE chunk
     char* const wst = stage + wv * 16384;
+    constexpr int QD = WTN / 4;  // 1-KiB pieces of d rows
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {  // 16 x 1 KiB: 4 rows x 256 B each
-      const int r = 4 * (q & 7) + (lane >> 4), c = lane & 15;
-      const uint16_t* T = q < 8 ? P.dT : P.xT;
-      const int R = q < 8 ? P.N : P.K, r0 = q < 8 ? n0 : k0;
+    for (int q = 0; q < QD + 8; ++q) {  // 1 KiB each: 4 rows x 256 B
+      const int r = 4 * (q < QD ? q : q - QD) + (lane >> 4), c = lane & 15;
+      const uint16_t* T = q < QD ? P.dT : P.xT;
+      const int R = q < QD ? P.N : P.K, r0 = q < QD ? n0 : k0;
       const int gr = min(r0 + r, R - 1);  // rows past the edge: any valid row (their outputs are not stored)
       const uint16_t* src = T + (int64_t)gr * a.M + mb + 8 * (c ^ (r & 15));
       __builtin_amdgcn_global_load_lds((const void*)src,
@@ -553,15 +565,15 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      bf16x8 af[2], bf[2];
+      bf16x8 af[WNI], bf[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int ra = 16 * i + lo;
-        af[i] = *(const bf16x8*)(wst + ra * 256 + (((4 * s4 + hi) ^ (ra & 15)) * 16));
-        bf[i] = *(const bf16x8*)(wst + 8192 + ra * 256 + (((4 * s4 + hi) ^ (ra & 15)) * 16));
+        if (i < WNI) af[i] = *(const bf16x8*)(wst + ra * 256 + (((4 * s4 + hi) ^ (ra & 15)) * 16));
+        bf[i] = *(const bf16x8*)(wst + WTN * 256 + ra * 256 + (((4 * s4 + hi) ^ (ra & 15)) * 16));
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < WNI; ++i) {
         const bool rin = n0 + 16 * i + lo < P.N;  // clamped rows must not enter the row sums
         const uint4 aw = __builtin_bit_cast(uint4, af[i]);
         const uint32_t awd[4] = {aw.x, aw.y, aw.z, aw.w};
@@ -576,21 +588,21 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
 #endif
   } else
   for (int m = mb; m < me; m += 128) {  // four k-steps per iteration, all loads issued first
-    bf16x8 af[4][2], bf[4][2];
+    bf16x8 af[4][WNI], bf[4][2];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int mk = m + 32 * s + 8 * hi;
       const int mm = mk < me ? mk : a.M;  // a.M -> zero fragment
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        af[s][i] = rowfrag(P.dT, P.N, a.M, n0 + 16 * i + lo, mm);
+        if (i < WNI) af[s][i] = rowfrag(P.dT, P.N, a.M, n0 + 16 * i + lo, mm);
         bf[s][i] = rowfrag(P.xT, P.K, a.M, k0 + 16 * i + lo, mm);
       }
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < WNI; ++i) {
         // (the fragment's elements via its dwords: a per-element __bf16 -> uint16_t bit_cast of
         // the vector's lanes miscompiles under -O3 to element 0 eight times)
         const uint4 aw = __builtin_bit_cast(uint4, af[s][i]);
@@ -606,27 +618,24 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
   if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memrealtime() + (uint64_t)(acc[0][0][0] == 12345.f);
   // reduce the 8 waves' partial tiles in LDS; C element (row 16i + 4hi + r, col 16j + lo)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WNI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wv][(16 * i + 4 * hi + r) * 32 + 16 * j + lo] = acc[i][j][r];
   // row sums of d^T (bias gradient): lanes lo, lo+16, lo+32, lo+48 hold parts of row 16i + lo
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < WNI; ++i) {
     rs[i] += __shfl_xor(rs[i], 16, 64);
     rs[i] += __shfl_xor(rs[i], 32, 64);
-  }
-  if (hi == 0) {
-    rsum[wv][lo] = rs[0];
-    rsum[wv][16 + lo] = rs[1];
+    if (hi == 0) rsum[wv][16 * i + lo] = rs[i];
   }
   sf();
   __syncthreads();
   if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
   const float gsc = sf.gs();
 #pragma unroll
-  for (int q = 0; q < 32 * 32 / NT; ++q) {
+  for (int q = 0; q < WEPT; ++q) {
     const int e = threadIdx.x + q * NT, r = e >> 5, c = e & 31;
     float v = 0.f;
 #pragma unroll
@@ -766,7 +775,7 @@ RK_API int RKL_NAME(rk_mlp3_wgrad_loss)(int nprob, const void* const* dT, const 
     a.p[i].K = Ks[j];
     a.p[i].tiles_k = (Ks[j] + 31) / 32;
     a.p[i].tile_begin = tiles;
-    if (i < nprob) tiles += ((Ns[j] + 31) / 32) * a.p[i].tiles_k;
+    if (i < nprob) tiles += ((Ns[j] + WTN - 1) / WTN) * a.p[i].tiles_k;
   }
   a.tiles = tiles;
   int extra = 0;
@@ -778,7 +787,7 @@ RK_API int RKL_NAME(rk_mlp3_wgrad_loss)(int nprob, const void* const* dT, const 
     a.sl.ncols = slab_bound[4];
     for (int i = 0; i < 4; ++i) a.sl.dst[i] = slab_dst[i];
     for (int i = 0; i < 5; ++i) a.sl.bound[i] = slab_bound[i];
-    extra = (a.sl.ncols + 63) / 64;
+    extra = (a.sl.ncols + SLC - 1) / SLC;
   }
   a.nslab = extra;
   if (loss) {
