@@ -713,16 +713,25 @@ __global__ void __launch_bounds__(NTHR) lenet_conv_fwd(const float* __restrict__
 //  phase D  block totals -> one row of a per-block gradient slab (fused path; summed by the
 //           weight-gradient launch) or global f32 atomics (generic path)
 constexpr int DC = 18;             // dConv2 image side: 10 + 2*4 zero ring
-constexpr int DCN = DC * DC * C2;  // 5184, channel-last [y][x][co]
+// channel-last [y][x][co] with a row pitch of 19 pixels (608 B = 38 16-B slots, 6 mod 16): with the
+// phase-B row order below every ds_read_b128 lane group of the dgrad A operand hits 16 distinct
+// bank slots (18-pixel rows, 4 mod 16: 2.7-way on average, by a model of the b128 lane groups)
+constexpr int DCR = (DC + 1) * C2;  // 304 elements per ring row
+constexpr int DCN = DC * DCR;       // 5472
 // (Measured round 5: two 8-channel planes with one-pixel-row tiles — conflict-free 256-byte operand
 // reads — made phase B slower, 5.48 -> 5.72 us: the 4 extra tiles cost more than the conflicts.)
-constexpr int DTS = 136;           // row stride of dConv2^T [co][position] (100 used, zero padded; 272 B: rows on distinct LDS slots)
+// row stride of dConv2^T [co][position] (100 used, zero padded): 288 B = 18 16-B slots (2 mod 16), so
+// the dW2 A read's b128 lane groups (16 rows at one or two hi) hit 16 distinct slots (272 B: 2-way)
+constexpr int DTS = 144;
 // fused path: per-block conv-gradient slab row [dW1 150 | db1 6 | dW2 2400 | db2 16] (+pad)
 constexpr int SL_W1 = 0, SL_B1 = SL_W1 + C1 * R1, SL_W2 = SL_B1 + C1, SL_B2 = SL_W2 + C2 * R2;
 constexpr int SLABN = SL_B2 + C2;  // 2572
 constexpr int SLABW = 2576;
 
-constexpr int DX2S = Q1 * Q1 + 4;  // dx2 channel row: the 196 windows + 4 zeros (phase C's last k-step)
+// dx2 channel row: the 196 windows + zeros (phase C's last k-step reads up to 199); 202 = 10 mod 32
+// keeps phase B's dx2 stores (rows = 2 image rows apart, channel lanes) and phase C's 8-byte reads
+// conflict-free (200: 2.75-way stores)
+constexpr int DX2S = Q1 * Q1 + 6;
 constexpr int PT_N = 8 * 25 + 8;    // posT entries: windows 0 .. 8*24 + 7
 struct BwdSmem {
   // k.imgb: bf16 image in two copies: [0][i] = img[i], [1][i] = img[i + 1], so any pair (x, x+1) is
@@ -1104,14 +1113,14 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     static_assert(A2N <= NTHR, "one pooled element per thread");
     if (threadIdx.x < A2N) {
       const int e = threadIdx.x, co = e / 25, w = e % 25;
-      const int d0 = ((2 * (w / Q2) + 4) * DC + 2 * (w % Q2) + 4) * C2 + co, t0 = co * DTS + 4 * w;
+      const int d0 = (2 * (w / Q2) + 4) * DCR + (2 * (w % Q2) + 4) * C2 + co, t0 = co * DTS + 4 * w;
 #pragma unroll
       for (int sl = 0; sl < SPB; ++sl) {
         const int n = nbase + sl, nc = n < N ? n : 0;
         const uint16_t g = MLP ? sm.da2[sl][e] : da2g[(int64_t)nc * A2N + e];
         const uint8_t cd = RES ? sm.k.c2[sl][e] : code2g[(int64_t)nc * A2N + e];
         if (n < N && cd < 4) {
-          sm.dc2[sl][d0 + ((cd >> 1) * DC + (cd & 1)) * C2] = g;
+          sm.dc2[sl][d0 + (cd >> 1) * DCR + (cd & 1) * C2] = g;
           sm.dcT[sl][t0 + cd] = g;
         }
       }
@@ -1203,13 +1212,16 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
       // A row = pixel pair (ih, iw0 = 2jx .. +1) reads the (ring) dConv2 pixels (ih + dy, iw0 + dx):
       // k-step s covers window positions 2s, 2s + 1 = (dy, dx) = (s / 3, 2(s % 3) + hi / 2), channels
       // 8(hi & 1) ..: the lane part is 8hi elements, the rest an immediate per k-step
-      auto toff = [](int s) { return ((s / 3) * DC + 2 * (s % 3)) * C2; };
+      auto toff = [](int s) { return (s / 3) * DCR + 2 * (s % 3) * C2; };
+      // Tile t = pair column jx = t (iw0 = 2t); row r -> ih: rows {0-3, 12-15} -> 0..7, rows 4..11 ->
+      // 8..15 (14, 15: pad rows, re-reading 6, 7, never stored).  A b128 lane group is one of those
+      // row classes at one hi: 8 rows at slots 6ih + const mod 16 (distinct even slots for 8
+      // consecutive ih) and 8 rows of the other class at odd ones.
+      auto row_ih = [](int r) { return (r >= 4 && r < 12) ? r + 4 : (r < 4 ? r : r - 8); };
       for (int tt = t_begin; tt < NDG; tt += 16) {
         const int sl = tt / DGT, t = tt % DGT;
-        const int m = 16 * t + lo;  // A row of this lane (pairs >= 98: rows discarded below)
-        const bool pv = m < Q1 * Q1 / 2;
-        const int ih = pv ? m / (Q1 / 2) : 0, iw0 = pv ? 2 * (m % (Q1 / 2)) : 0;
-        const uint16_t* ab = sm.dc2[sl] + (ih * DC + iw0) * C2 + 8 * hi;
+        const int ihr = row_ih(lo), ih = ihr < Q1 ? ihr : ihr - 8;
+        const uint16_t* ab = sm.dc2[sl] + ih * DCR + 2 * t * C2 + 8 * hi;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         // A operands in chunks of 4 k-steps, the next chunk's LDS reads issued before this
         // chunk's MFMAs (one read + wait per MFMA would expose the LDS latency every step)
@@ -1234,14 +1246,13 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
             }
           }
         }
-        // C[row = pair 16t + 4hi + i][col = (d, ci) = (lo >> 3, lo & 7)] -> pixel 2 * pair + d
-        // (a pair's two pixels are adjacent in one image row: Q1 is even)
+        // C[row 4hi + i][col = (d, ci) = (lo >> 3, lo & 7)] -> pixel (ih(row), 2t + d)
         if ((lo & 7) < C1) {
-          float* dst = sm.dx2[sl] + (lo & 7) * DX2S + (lo >> 3);
+          float* dst = sm.dx2[sl] + (lo & 7) * DX2S + (lo >> 3) + 2 * t;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int mp = 16 * t + 4 * hi + i;
-            if (mp < Q1 * Q1 / 2) dst[2 * mp] = acc[i];
+            const int r = row_ih(4 * hi + i);
+            if (r < Q1) dst[r * Q1] = acc[i];
           }
         }
       }

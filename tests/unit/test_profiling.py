@@ -81,19 +81,25 @@ def test_lenet_conv2_dgrad_pixel_pair_decomposition():
             u = d2unit(s, lane)
             if u >= 0:
                 B[32 * s + 8 * (lane >> 4):32 * s + 8 * (lane >> 4) + 8, lane & 15] = sect[u]
-    ring = np.zeros((18, 18, 16), dtype=np.float32)  # channel-last, zero ring of 4
+    ring = np.zeros((18, 19, 16), dtype=np.float32)  # channel-last, zero ring of 4, 19-pixel row pitch
     ring[4:14, 4:14] = dc[0].permute(1, 2, 0).numpy()
     flat = ring.reshape(-1)
-    out = np.zeros((6, 196), dtype=np.float32)
-    for mrow in range(98):
-        ih, iw0 = mrow // 7, 2 * (mrow % 7)
-        a = np.zeros(480, dtype=np.float32)
-        for s in range(15):
-            for hi in range(4):
-                base = (ih * 18 + iw0) * 16 + 8 * hi + ((s // 3) * 18 + 2 * (s % 3)) * 16
-                a[32 * s + 8 * hi:32 * s + 8 * hi + 8] = flat[base:base + 8]
-        c = a @ B
-        for lo in range(16):
-            if (lo & 7) < 6:
-                out[lo & 7, 2 * mrow + (lo >> 3)] = c[lo]
-    np.testing.assert_allclose(out.reshape(6, 14, 14), ref.numpy(), rtol=1e-4, atol=1e-4)
+    out = np.full((6, 14, 14), np.nan, dtype=np.float32)
+
+    def row_ih(r):  # tile row -> image row (14, 15: pad rows)
+        return r + 4 if 4 <= r < 12 else (r if r < 4 else r - 8)
+
+    for t in range(7):  # tile t = pixel pairs (ih, 2t .. 2t + 1)
+        for r in range(16):
+            ih = row_ih(r) if row_ih(r) < 14 else row_ih(r) - 8
+            a = np.zeros(480, dtype=np.float32)
+            for s in range(15):
+                for hi in range(4):
+                    base = ih * 304 + 2 * t * 16 + 8 * hi + (s // 3) * 304 + 2 * (s % 3) * 16
+                    a[32 * s + 8 * hi:32 * s + 8 * hi + 8] = flat[base:base + 8]
+            c = a @ B
+            if row_ih(r) < 14:
+                for lo in range(16):
+                    if (lo & 7) < 6:
+                        out[lo & 7, ih, 2 * t + (lo >> 3)] = c[lo]
+    np.testing.assert_allclose(out, ref.numpy(), rtol=1e-4, atol=1e-4)
