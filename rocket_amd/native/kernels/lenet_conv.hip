@@ -104,8 +104,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 constexpr int SPB = 4;               // samples per block
 constexpr int WPS = 4;               // waves per sample
 constexpr int NTHR = 64 * SPB * WPS; // 1024
-constexpr int IMGS = PADI + 1;       // LDS row stride of the padded image (33: breaks bank aliasing)
-constexpr int IMGN = PADI * IMGS;    // 1056
+// LDS row stride of the padded image, and the distance between its two copies (even / odd pair
+// starts): 35 and IMGN + 16 make conv1's A-operand and the dW1 B-operand pair reads 1.4-way / 1.8-way
+// by a model of the ds_read_b32 lane groups (33 and IMGN + 8: 2.4-way / 2.5-way)
+constexpr int IMGS = PADI + 3;
+constexpr int IMGN = PADI * IMGS;    // 1120
+constexpr int IMGC = IMGN + 16;      // element distance of the two image copies
+constexpr int NBC = IMGS - IMG;      // border columns of an interior row: 0, 1, 30 .. IMGS-1
+constexpr int NBORD = 4 * IMGS + IMG * NBC;  // border elements (rows 0, 1, 30, 31 + interior columns)
 constexpr int IMGZ = IMGN;           // zero slot index in img
 
 // padded-image offset of conv1 output position (window w of the 14x14 pool grid, quadrant q)
@@ -256,7 +262,7 @@ __device__ __forceinline__ int d2unit(int s, int l) {
 // pooled conv1 output a1 and both argmax/ReLU code maps still in LDS: no global round trip (and no
 // global copy of a1 / codes at all, which also shrinks the dirty bytes the kernel boundary writes back).
 struct KeepSmem {
-  uint16_t imgb[SPB][2][IMGN + 8];  // bf16 image, two copies for pair reads (see BwdSmem)
+  uint16_t imgb[SPB][2][IMGC];      // bf16 image, two copies for pair reads (see BwdSmem)
   uint16_t a1[SPB][A1N + 8];        // fwd: zero slot at A1N, trash at A1N+4; bwd: zero / ones pairs there
   uint8_t c1[SPB][A1N + 8];         // bwd: never-matching slot at A1N
   uint8_t c2[SPB][A2P];             // same row pitch as a2: the trash slot A2TRASH must stay inside the row
@@ -273,6 +279,7 @@ struct FwdSmem {
   uint16_t a2[SPB][A2P];  // data 0..399, zero pad 400..415, trash at A2TRASH
   uint16_t zrow[A2P];
 };
+static_assert(offsetof(FwdSmem, a1cl) % 16 == 0 && offsetof(FwdSmem, a2) % 16 == 0, "16-byte operand reads stay aligned");
 
 struct ClsFwd {  // classifier operands of the fused forward
   const bf16x8* frag;
@@ -364,16 +371,16 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
           sm.k.wfr[i] = u >= 0 ? cf.frag[OFF_D2 * 64 + u] : bf16x8{};
         }
     }
-    for (int b = st; b < 4 * IMGS + IMG * 5 + 8; b += 64 * WPS) {  // border / zero-slot elements
+    for (int b = st; b < NBORD + 8; b += 64 * WPS) {  // border / zero-slot elements
       int bi;
       if (b < 4 * IMGS) {  // rows 0, 1, 30, 31
         const int r = b / IMGS;
         bi = (r < 2 ? r : r + IMG) * IMGS + b % IMGS;
-      } else if (b < 4 * IMGS + IMG * 5) {  // columns 0, 1, 30, 31, 32 of rows 2..29
-        const int u = b - 4 * IMGS, c5 = u % 5;
-        bi = (2 + u / 5) * IMGS + (c5 < 2 ? c5 : c5 + IMG);
+      } else if (b < NBORD) {  // columns 0, 1, 30 .. IMGS-1 of rows 2..29
+        const int u = b - 4 * IMGS, c5 = u % NBC;
+        bi = (2 + u / NBC) * IMGS + (c5 < 2 ? c5 : c5 + IMG);
       } else {
-        bi = IMGN + (b - 4 * IMGS - IMG * 5);  // zero slots past the image
+        bi = IMGN + (b - NBORD);  // zero slots past the image
       }
       img0[bi] = 0;
       if (bi > 0) img1[bi - 1] = 0;
@@ -741,8 +748,10 @@ struct BwdSmem {
   float dx2[SPB][C1 * DX2S];        // dL/d a1 (conv2 input gradient), channel rows of DX2S (zero tail)
   uint16_t posT[PT_N];              // phase C: byte offset 2*pos1(w, 0) of pool window w (w >= 196: clamped)
   uint16_t posT2[32];               // phase B (dW2): pos2(w, 0) of conv2 window w (w >= 25: clamped)
+  uint16_t pad_a1o[46];             // places a1o at 46 mod 64 elements from a1 (see static_assert below)
   uint16_t a1o[SPB][A1N + 8];       // a1 shifted by one element (pair reads for the dW2 B operand)
-  uint16_t dc2[SPB][DCN + 16];      // dense channel-last dConv2 with zero ring
+  // (16-byte aligned: the pad before a1o must not shift the b128-read arrays from here on)
+  alignas(16) uint16_t dc2[SPB][DCN + 16];  // dense channel-last dConv2 with zero ring
                                     // (after phase B: the 16 waves' dW1 partials [16][2][256] f32)
   uint16_t dcT[SPB][C2 * DTS];      // dConv2^T [co][p = 4*window + quadrant] (wgrad2 A operand)
   // fused classifier backward (MLP=true): gradients of the 4 samples as MFMA A rows
@@ -759,6 +768,14 @@ struct BwdSmem {
 };
 static_assert(sizeof(((BwdSmem*)nullptr)->dc2) >= (NTHR / 64) * 2 * 256 * sizeof(float),
               "dW1 partials alias dc2");
+// The dW2 B operand reads pairs from a1 (even offsets) and a1o (odd ones) in one ds_read_b32: the
+// distance between the two copies mod 64 elements (32 banks) sets how the two halves of a lane group
+// collide; 46 measured best of all even distances by a model of the b32 lane groups (2.2-way -> 1.7-way).
+static_assert(((offsetof(BwdSmem, a1o) - offsetof(BwdSmem, k.a1)) / 2) % 64 == 46, "a1o bank placement");
+static_assert(offsetof(BwdSmem, dc2) % 16 == 0 && offsetof(BwdSmem, dcT) % 16 == 0 && offsetof(BwdSmem, dyl) % 16 == 0 &&
+              offsetof(BwdSmem, d2l) % 16 == 0 && offsetof(BwdSmem, d1l) % 16 == 0 && offsetof(BwdSmem, da2) % 16 == 0 &&
+              offsetof(BwdSmem, dx2) % 16 == 0 && offsetof(KeepSmem, wfr) % 16 == 0,
+              "16-byte operand reads stay aligned");
 
 struct ClsBwd {
   const bf16x8* frag;
@@ -903,15 +920,15 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
         a1v = *(const uint4*)(a1g + (int64_t)(nbase + sl) * A1N + e);
         c1v = *(const uint2*)(code1g + (int64_t)(nbase + sl) * A1N + e);
       }
-      for (int t = threadIdx.x; t < SPB * 272; t += NTHR) {  // border of the padded image (rows/cols)
-        const int sl = t / 272, b = t % 272;
+      for (int t = threadIdx.x; t < SPB * NBORD; t += NTHR) {  // border of the padded image (rows/cols)
+        const int sl = t / NBORD, b = t % NBORD;
         int bi;
         if (b < 4 * IMGS) {
           const int r = b / IMGS;
           bi = (r < 2 ? r : r + IMG) * IMGS + b % IMGS;
         } else {
-          const int u = b - 4 * IMGS, c5 = u % 5;
-          bi = (2 + u / 5) * IMGS + (c5 < 2 ? c5 : c5 + IMG);
+          const int u = b - 4 * IMGS, c5 = u % NBC;
+          bi = (2 + u / NBC) * IMGS + (c5 < 2 ? c5 : c5 + IMG);
         }
         sm.k.imgb[sl][0][bi] = 0;
         if (bi > 0) sm.k.imgb[sl][1][bi - 1] = 0;
@@ -1280,7 +1297,7 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int x = (k & 1) * IMGS + (min(r, R1 - 1) / KS) * IMGS + (min(r, R1 - 1) % KS);
-          cst[u][k] = 2 * (r == R1 ? IMGN + 2 : ((x & 1) ? (IMGN + 8) + x - 1 : x));  // bytes
+          cst[u][k] = 2 * (r == R1 ? IMGN + 2 : ((x & 1) ? IMGC + x - 1 : x));  // bytes
         }
       }
       const bool onecol = lo == R1 - 16;  // u = 1 lane of the ones column: no window offset
