@@ -37,6 +37,32 @@ constexpr int BN_FU = 4;                     // partial-tile rows in flight per 
 
 template <typename T> struct V8;
 template <> struct V8<uint16_t> {
+  static __device__ __forceinline__ void unpack(const uint4 u, float* v) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = __uint_as_float(w[k] << 16);
+      v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ uint4 pack(const float* v) {
+    uint4 u;
+    uint32_t* w = (uint32_t*)&u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
+    return u;
+  }
+  // streaming forms (nontemporal: the elementwise BatchNorm passes touch each element once)
+  static __device__ __forceinline__ void load_nt(const uint16_t* p, float* v) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 t = __builtin_nontemporal_load((const u32x4*)p);
+    unpack(make_uint4(t.x, t.y, t.z, t.w), v);
+  }
+  static __device__ __forceinline__ void store_nt(uint16_t* p, const float* v) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const uint4 u = pack(v);
+    __builtin_nontemporal_store(u32x4{u.x, u.y, u.z, u.w}, (u32x4*)p);
+  }
   static __device__ __forceinline__ void load(const uint16_t* p, float* v) {
     const uint4 u = *(const uint4*)p;
     const uint32_t w[4] = {u.x, u.y, u.z, u.w};
@@ -80,6 +106,21 @@ template <> struct V8<float> {
   static __device__ __forceinline__ void store(float* p, const float* v) {
     *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
     *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+// elementwise-pass variant (bf16 -> bf16 only; ROCKET_BN_EW, A/B knob): bit 0 = nontemporal loads /
+// stores, bit 1 = 8 rows in flight per thread instead of BN_U
+template <typename T, int EV> struct BnEw {
+  static constexpr bool NT = (EV & 1) && std::is_same<T, uint16_t>::value;
+  static constexpr int U = (EV & 2) ? 8 : BN_U;
+  static __device__ __forceinline__ void load(const T* p, float* v) {
+    if constexpr (NT) V8<uint16_t>::load_nt((const uint16_t*)p, v);
+    else V8<T>::load(p, v);
+  }
+  static __device__ __forceinline__ void store(T* p, const float* v) {
+    if constexpr (NT) V8<uint16_t>::store_nt((uint16_t*)p, v);
+    else V8<T>::store(p, v);
   }
 };
 
@@ -530,7 +571,7 @@ __device__ __forceinline__ const T* at_b(const T* base, uint32_t e) {
   return (const T*)((const char*)base + e * (uint32_t)sizeof(T));
 }
 
-template <typename T, typename TO, bool RES, bool RELU>
+template <typename T, typename TO, bool RES, bool RELU, int EV = 0>
 __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x, const TO* __restrict__ res,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
                                                         TO* __restrict__ y, uint8_t* __restrict__ mask, int64_t R,
@@ -550,16 +591,19 @@ __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x,
   const TO* qb = RES ? res + r0 * C : res;
   TO* yb = y + r0 * C;
   uint8_t* mb = mask ? mask + r0 * (C >> 3) : mask;
-  for (int r = threadIdx.x / CV; r < nr; r += BN_U * RPP) {
-    float v[BN_U][8], q[BN_U][8];
+  using EX = BnEw<T, EV>;
+  using EO = BnEw<TO, EV>;
+  constexpr int U = EX::U;
+  for (int r = threadIdx.x / CV; r < nr; r += U * RPP) {
+    float v[U][8], q[U][8];
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint32_t e = (uint32_t)min(r + u * RPP, nr - 1) * (uint32_t)C + (uint32_t)c;
-      V8<T>::load(at_b(xb, e), v[u]);
-      if constexpr (RES) V8<TO>::load(at_b(qb, e), q[u]);
+      EX::load(at_b(xb, e), v[u]);
+      if constexpr (RES) EO::load(at_b(qb, e), q[u]);
     }
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       unsigned m = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -573,7 +617,7 @@ __global__ void __launch_bounds__(BN_T) bn_apply_kernel(const T* __restrict__ x,
       }
       const int ru = r + u * RPP;
       if (ru < nr) {
-        V8<TO>::store(at_b(yb, (uint32_t)ru * (uint32_t)C + (uint32_t)c), v[u]);
+        EO::store(at_b(yb, (uint32_t)ru * (uint32_t)C + (uint32_t)c), v[u]);
         if (RELU && mb) mb[(uint32_t)ru * (uint32_t)CV + (uint32_t)cv] = (uint8_t)m;
       }
     }
@@ -716,7 +760,7 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_finalize_kernel(BnBwdArgs a, cons
 }
 
 // dx = P*dy' + Q*x + S (per-channel coefficients in registers); dres = dy'
-template <typename T, typename TO>
+template <typename T, typename TO, int EV = 0>
 __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(const TO* __restrict__ dy, const T* __restrict__ x,
                                                             const uint8_t* __restrict__ mask,
                                                             const float* __restrict__ coef, T* __restrict__ dx,
@@ -738,19 +782,22 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(const TO* __restrict
   T* dxb = dx + r0 * C;
   TO* drb = dres ? dres + r0 * C : dres;
   const uint8_t* mkb = mask ? mask + r0 * CV : mask;
-  for (int r = threadIdx.x / CV; r < nr; r += BN_U * RPP) {
-    float g[BN_U][8], xv[BN_U][8];
-    unsigned mb[BN_U];
+  using EX = BnEw<T, EV>;
+  using EO = BnEw<TO, EV>;
+  constexpr int U = EX::U;
+  for (int r = threadIdx.x / CV; r < nr; r += U * RPP) {
+    float g[U][8], xv[U][8];
+    unsigned mb[U];
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint32_t ru = (uint32_t)min(r + u * RPP, nr - 1);
       const uint32_t e = ru * (uint32_t)C + (uint32_t)c;
-      V8<TO>::load(at_b(gb, e), g[u]);
-      V8<T>::load(at_b(xb, e), xv[u]);
+      EO::load(at_b(gb, e), g[u]);
+      EX::load(at_b(xb, e), xv[u]);
       mb[u] = mkb ? mkb[ru * (uint32_t)CV + (uint32_t)cv] : 0xFFu;
     }
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (mkb) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) g[u][k] = ((mb[u] >> k) & 1u) ? g[u][k] : 0.f;
@@ -758,10 +805,10 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(const TO* __restrict
       const int ru = r + u * RPP;
       const bool ok = ru < nr;
       const uint32_t e = (uint32_t)ru * (uint32_t)C + (uint32_t)c;
-      if (ok && drb) V8<TO>::store(at_b(drb, e), g[u]);
+      if (ok && drb) EO::store(at_b(drb, e), g[u]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) xv[u][k] = P[k] * g[u][k] + Q[k] * xv[u][k] + S[k];
-      if (ok) V8<T>::store(at_b(dxb, e), xv[u]);
+      if (ok) EX::store(at_b(dxb, e), xv[u]);
     }
   }
 }
@@ -1266,6 +1313,12 @@ RK_API int rk_bn_finalize(const float* tp, int ntiles, int tile_rows, int64_t R,
 }
 
 // rows per block for the elementwise passes: ~2048 blocks, whole passes of RPP rows
+static int bn_ew_variant() {
+  // default 1 (nontemporal): ResNet-50 10,569-10,579 -> 10,668-10,682 img/s, the fused BN
+  // fwd+bwd probe +10% on the 56x56 / 28x28 residual shapes (profiles/r5_bn_ew_ab.md)
+  static const int v = getenv("ROCKET_BN_EW") ? atoi(getenv("ROCKET_BN_EW")) & 3 : 1;
+  return v;
+}
 static int bn_elem_rows(int64_t R, int C, int* grid) {
   const int rpp = BN_T / (C / 8);
   int64_t per = (R + 2047) / 2048;
@@ -1374,24 +1427,30 @@ RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const fl
   int grid;
   const int rpb = bn_elem_rows(R, C, &grid);
   if (!bn_elem_ok(rpb, C)) return (int)hipErrorInvalidValue;
-#define RK_BA2(T, TO, RES)                                                                                      \
+#define RK_BA2(T, TO, RES, EV)                                                                                 \
   do {                                                                                                          \
     if (relu)                                                                                                   \
-      bn_apply_kernel<T, TO, RES, true><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift, (TO*)y, \
-                                                              (uint8_t*)mask, R, C, rpb);                       \
+      bn_apply_kernel<T, TO, RES, true, EV><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift,    \
+                                                                  (TO*)y, (uint8_t*)mask, R, C, rpb);           \
     else                                                                                                        \
-      bn_apply_kernel<T, TO, RES, false><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift,       \
-                                                               (TO*)y, nullptr, R, C, rpb);                     \
+      bn_apply_kernel<T, TO, RES, false, EV><<<grid, BN_T, 0, s>>>((const T*)x, (const TO*)res, scale, shift,   \
+                                                                   (TO*)y, nullptr, R, C, rpb);                 \
   } while (0)
-#define RK_BA(T, TO)              \
-  do {                            \
-    if (res) RK_BA2(T, TO, true); \
-    else RK_BA2(T, TO, false);    \
+#define RK_BA(T, TO, ...)                                  \
+  do {                                                     \
+    if (res) RK_BA2(T, TO, true, __VA_OPT__(__VA_ARGS__ +) 0);   \
+    else RK_BA2(T, TO, false, __VA_OPT__(__VA_ARGS__ +) 0);      \
   } while (0)
   if (dt == F16 && dto == F16) RK_BA(f16_t, f16_t);
   else if (dt == F16 && dto == F32) RK_BA(f16_t, float);
-  else if (dt == BF16 && dto == BF16) RK_BA(uint16_t, uint16_t);
-  else if (dt == BF16) RK_BA(uint16_t, float);
+  else if (dt == BF16 && dto == BF16) {
+    switch (bn_ew_variant()) {
+      case 1: RK_BA(uint16_t, uint16_t, 1); break;
+      case 2: RK_BA(uint16_t, uint16_t, 2); break;
+      case 3: RK_BA(uint16_t, uint16_t, 3); break;
+      default: RK_BA(uint16_t, uint16_t, 0);
+    }
+  } else if (dt == BF16) RK_BA(uint16_t, float);
   else if (dto == BF16) RK_BA(float, uint16_t);
   else RK_BA(float, float);
 #undef RK_BA
@@ -1412,16 +1471,22 @@ RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void*
   int eg;
   const int erpb = bn_elem_rows(R, C, &eg);
   if (!bn_elem_ok(erpb, C)) return (int)hipErrorInvalidValue;
-#define RK_BB(T, TO)                                                                                               \
+#define RK_BB(T, TO, ...)                                                                                          \
   do {                                                                                                             \
     bn_bwd_reduce_kernel<T, TO><<<grid, BN_T, 0, s>>>(a);                                                          \
-    bn_bwd_apply_kernel<T, TO><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x, (const uint8_t*)mask, coef,      \
-                                                   (T*)dx,                                                         \
-                                                   (TO*)dres, R, C, erpb);                                         \
+    bn_bwd_apply_kernel<T, TO, __VA_OPT__(__VA_ARGS__ +) 0><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x,       \
+                                                   (const uint8_t*)mask, coef, (T*)dx, (TO*)dres, R, C, erpb);      \
   } while (0)
   if (dt == F16 && dto == F16) RK_BB(f16_t, f16_t);
   else if (dt == F16 && dto == F32) RK_BB(f16_t, float);
-  else if (dt == BF16 && dto == BF16) RK_BB(uint16_t, uint16_t);
+  else if (dt == BF16 && dto == BF16) {
+    switch (bn_ew_variant()) {
+      case 1: RK_BB(uint16_t, uint16_t, 1); break;
+      case 2: RK_BB(uint16_t, uint16_t, 2); break;
+      case 3: RK_BB(uint16_t, uint16_t, 3); break;
+      default: RK_BB(uint16_t, uint16_t, 0);
+    }
+  }
   else if (dt == BF16) RK_BB(uint16_t, float);
   else if (dto == BF16) RK_BB(float, uint16_t);
   else RK_BB(float, float);
@@ -1451,12 +1516,19 @@ RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, co
   int eg;
   const int erpb = bn_elem_rows(R, C, &eg);
   if (!bn_elem_ok(erpb, C)) return (int)hipErrorInvalidValue;
-#define RK_BP(T, TO)                                                                                      \
-  bn_bwd_apply_kernel<T, TO><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x, nullptr, coef, (T*)dx, (TO*)dres, R, C, \
-                                                 erpb)
+#define RK_BP(T, TO, ...)                                                                                       \
+  bn_bwd_apply_kernel<T, TO, __VA_OPT__(__VA_ARGS__ +) 0><<<eg, BN_T, 0, s>>>((const TO*)dy, (const T*)x, nullptr, coef, \
+                                                                            (T*)dx, (TO*)dres, R, C, erpb)
   if (dt == F16 && dto == F16) RK_BP(f16_t, f16_t);
   else if (dt == F16 && dto == F32) RK_BP(f16_t, float);
-  else if (dt == BF16 && dto == BF16) RK_BP(uint16_t, uint16_t);
+  else if (dt == BF16 && dto == BF16) {
+    switch (bn_ew_variant()) {
+      case 1: RK_BP(uint16_t, uint16_t, 1); break;
+      case 2: RK_BP(uint16_t, uint16_t, 2); break;
+      case 3: RK_BP(uint16_t, uint16_t, 3); break;
+      default: RK_BP(uint16_t, uint16_t, 0);
+    }
+  }
   else if (dt == BF16) RK_BP(uint16_t, float);
   else if (dto == BF16) RK_BP(float, uint16_t);
   else RK_BP(float, float);
