@@ -61,6 +61,41 @@ __global__ void __launch_bounds__(T) gelu_fwd_kernel(const TI* __restrict__ x, T
   }
 }
 
+// 16-bit in and out (bf16 / fp16, same type), n % 8 == 0: 16-byte accesses, GU chunks of 8 elements
+// per thread with all their loads issued first, and (NT) nontemporal loads / stores — the pass
+// touches each element once and the tensors are far larger than L2 (ViT fc1: 25216 x 3072).
+// (The 4-element form above kept one 8-byte load in flight per thread: 4.3 TB/s on the ViT shape.)
+template <typename E, bool NT>
+__global__ void __launch_bounds__(T) gelu_fwd16_kernel(const E* __restrict__ x, E* __restrict__ y, int64_t n) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int GU = 4;
+  const int64_t stride = (int64_t)gridDim.x * T * 8;
+  for (int64_t i0 = ((int64_t)blockIdx.x * T + threadIdx.x) * 8; i0 < n; i0 += stride * GU) {
+    u32x4 w[GU];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const int64_t i = i0 + u * stride;
+      const u32x4* p = (const u32x4*)(x + (i < n ? i : 0));
+      w[u] = NT ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n) break;
+      float v[8];
+      V4<E>::load((const E*)&w[u], v);
+      V4<E>::load((const E*)&w[u] + 4, v + 4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = gelu_f(v[k]);
+      u32x4 o;
+      V4<E>::store((E*)&o, v);
+      V4<E>::store((E*)&o + 4, v + 4);
+      if (NT) __builtin_nontemporal_store(o, (u32x4*)(y + i));
+      else *(u32x4*)(y + i) = o;
+    }
+  }
+}
+
 template <typename TI, typename TG>
 __global__ void __launch_bounds__(T) gelu_bwd_kernel(const TG* __restrict__ dy, const TI* __restrict__ x,
                                                      TI* __restrict__ dx, int64_t n) {
@@ -146,6 +181,19 @@ int egrid(int64_t n) {
 
 RK_API int rk_gelu_fwd(int dti, int dto, const void* x, void* y, int64_t n, hipStream_t s) {
   if (n % 4 || dti < 0 || dti > 2 || dto < 0 || dto > 2) return (int)hipErrorInvalidValue;
+  // ROCKET_GELU_EW: 0 = the 4-element kernel, 1 = 16-byte chunks, 2 = 16-byte chunks, nontemporal (default)
+  static const int ev = getenv("ROCKET_GELU_EW") ? atoi(getenv("ROCKET_GELU_EW")) : 2;
+  if (ev > 0 && dti == dto && dti != F32 && n % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+    const int g = egrid((n / 8 + 3) / 4);
+    if (dti == BF16) {
+      if (ev == 2) gelu_fwd16_kernel<uint16_t, true><<<g, T, 0, s>>>((const uint16_t*)x, (uint16_t*)y, n);
+      else gelu_fwd16_kernel<uint16_t, false><<<g, T, 0, s>>>((const uint16_t*)x, (uint16_t*)y, n);
+    } else {
+      if (ev == 2) gelu_fwd16_kernel<f16_t, true><<<g, T, 0, s>>>((const f16_t*)x, (f16_t*)y, n);
+      else gelu_fwd16_kernel<f16_t, false><<<g, T, 0, s>>>((const f16_t*)x, (f16_t*)y, n);
+    }
+    return (int)hipGetLastError();
+  }
   const int g = egrid(n / 4);
   RK_ACT_T(dti, TI, RK_ACT_T(dto, TO, gelu_fwd_kernel<TI, TO><<<g, T, 0, s>>>((const TI*)x, (TO*)y, n);););
   return (int)hipGetLastError();

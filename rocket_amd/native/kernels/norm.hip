@@ -424,7 +424,7 @@ __global__ void __launch_bounds__(BN_T) colsum_acc_kernel(const T* __restrict__ 
 // dz = dh * gelu'(z) (bf16 [R][C]) AND out[c] += sum_r dz[r][c]: the transformer MLP's GELU
 // backward fused with fc1's bias gradient, so the [tokens x hidden] gradient is read once instead of
 // twice.  Grid and two-level reduction as colsum_acc_kernel.
-template <typename T>  // uint16_t: bf16, f16_t: fp16
+template <typename T, int EV = 0>  // uint16_t: bf16, f16_t: fp16; EV: see BnEw (bf16 only)
 __global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const T* __restrict__ dh,
                                                                const T* __restrict__ z, T* __restrict__ dz,
                                                                int64_t R, int C, int rpb, float* part,
@@ -448,24 +448,26 @@ __global__ void __launch_bounds__(BN_T) gelu_bwd_colsum_kernel(const T* __restri
   const T* zb = z + base;
   T* dzb = dz + base;
   const int nr = (int)(r1 - r0);
-  for (int r = rg; r < nr; r += BN_U * BN_RG) {
-    float g[BN_U][8], v[BN_U][8];
+  using EX = BnEw<T, EV>;
+  constexpr int U = EX::U;
+  for (int r = rg; r < nr; r += U * BN_RG) {
+    float g[U][8], v[U][8];
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       // byte offset: base (SGPR) + zero-extended 32-bit VGPR offset = the saddr load form
       const uint32_t off = ((uint32_t)min(r + u * BN_RG, nr - 1) * (uint32_t)C + (uint32_t)(cok ? c : 0)) * 2u;
-      V8<T>::load((const T*)((const char*)dhb + off), g[u]);
-      V8<T>::load((const T*)((const char*)zb + off), v[u]);
+      EX::load((const T*)((const char*)dhb + off), g[u]);
+      EX::load((const T*)((const char*)zb + off), v[u]);
     }
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const bool ok = r + u * BN_RG < nr && cok;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         v[u][k] = g[u][k] * gelu_grad(v[u][k]);
         acc[k] += ok ? v[u][k] : 0.f;
       }
-      if (ok) V8<T>::store((T*)((char*)dzb + ((uint32_t)(r + u * BN_RG) * (uint32_t)C + c) * 2u), v[u]);
+      if (ok) EX::store((T*)((char*)dzb + ((uint32_t)(r + u * BN_RG) * (uint32_t)C + c) * 2u), v[u]);
     }
   }
   reduce_rowgroups(acc, lds, s1);
@@ -1409,8 +1411,16 @@ RK_API int rk_gelu_bwd_colsum16(int dt, const void* dh, const void* z, void* dz,
     gelu_bwd_colsum_kernel<f16_t><<<grid, BN_T, 0, s>>>((const f16_t*)dh, (const f16_t*)z, (f16_t*)dz, R, C, rpb, ws,
                                                         counters, out);
   else
-    gelu_bwd_colsum_kernel<uint16_t><<<grid, BN_T, 0, s>>>((const uint16_t*)dh, (const uint16_t*)z, (uint16_t*)dz, R, C,
-                                                           rpb, ws, counters, out);
+  {
+    // ROCKET_GELU_EW (act.hip rk_gelu_fwd): 2 (default) = nontemporal loads / stores here too
+    static const int gev = getenv("ROCKET_GELU_EW") ? atoi(getenv("ROCKET_GELU_EW")) : 2;
+    if (gev == 2)
+      gelu_bwd_colsum_kernel<uint16_t, 1><<<grid, BN_T, 0, s>>>((const uint16_t*)dh, (const uint16_t*)z, (uint16_t*)dz,
+                                                                R, C, rpb, ws, counters, out);
+    else
+      gelu_bwd_colsum_kernel<uint16_t><<<grid, BN_T, 0, s>>>((const uint16_t*)dh, (const uint16_t*)z, (uint16_t*)dz, R, C,
+                                                             rpb, ws, counters, out);
+  }
   return (int)hipGetLastError();
 }
 RK_API int rk_gelu_bwd_colsum(const void* dh, const void* z, void* dz, int64_t R, int C, float* out, float* ws,

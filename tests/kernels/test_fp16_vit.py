@@ -51,6 +51,23 @@ def test_gelu_fp16():
     assert _rel(y, yr) < 2e-3 and _rel(x.grad, xr.grad) < 2e-3
 
 
+@pytest.mark.parametrize("shape", [(1000, 3072), (5, 36), (257, 8)])
+def test_gelu_bf16_vector_paths(shape):
+    """bf16 GELU forward on the 16-byte / nontemporal kernel (n % 8 == 0, grid-stride tails) and the
+    4-element kernel (n % 8 != 0), against fp32 torch."""
+    from rocket_amd.ops.activation import gelu
+
+    x = (torch.randn(*shape, device="cuda") * 3).to(torch.bfloat16).requires_grad_()
+    y = gelu(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    yr = F.gelu(xr)
+    yr.backward(g.float())
+    assert y.dtype == torch.bfloat16
+    assert _rel(y, yr) < 8e-3 and _rel(x.grad, xr.grad) < 8e-3
+
+
 @pytest.mark.parametrize("add", [False, True])
 def test_layernorm_fp16_autocast(add):
     from rocket_amd.ops.norm import FusedLayerNorm
