@@ -72,6 +72,7 @@ struct ConvGeom {
   int ncls;              // strided dgrad: parity classes in the launch
   int zero_nb;           // strided dgrad, 1x1 kernel: only class (0, 0) has taps; its tiles also zero
                          // the three odd-parity neighbours of each of their pixels
+  int st_nt;             // row-chunk tile stores (store_tile_lds) nontemporal (ROCKET_CONV_NT)
   DgCls cls[4];
 };
 
@@ -523,7 +524,12 @@ __device__ __forceinline__ void store_tile_lds(const MArgs& g, const ConvGeom& c
           s2[e] = __builtin_fmaf(rr, (x - mu[e]) * is[e], s2[e]);
         }
       }
-      *(uint4*)dst = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      if (cg.st_nt) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u32x4{pk[0], pk[1], pk[2], pk[3]}, (u32x4*)dst);
+      } else {
+        *(uint4*)dst = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      }
     }
   }
   if constexpr (BNB) {
@@ -872,6 +878,10 @@ ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stri
   cg.bnb_x = nullptr; cg.bnb_mask = nullptr; cg.bnb_mean = nullptr; cg.bnb_invstd = nullptr; cg.bnb_part = nullptr;
   cg.pro_ss = nullptr; cg.bnb_ss = nullptr;
   cg.hoff = cg.woff = pad; cg.dx_h = cg.dx_w = 0; cg.w_s = S; cg.ncls = 0; cg.zero_nb = 0;
+  // the tile's outputs stream to HBM (ResNet activations are far larger than L2) and their next
+  // reader is another launch: nontemporal stores (ROCKET_CONV_NT=0: plain)
+  static const int nt = getenv("ROCKET_CONV_NT") ? atoi(getenv("ROCKET_CONV_NT")) : 1;
+  cg.st_nt = nt;
   cg.inv_gw = 1.f / (float)GW;
   cg.inv_gh = 1.f / (float)GH;
   cg.inv_s = 1.f / (float)S;
