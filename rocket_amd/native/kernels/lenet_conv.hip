@@ -421,7 +421,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
     const int k = 8 * hi + 2 * q;
     koffp[q] = k < K1P ? (k / 6) * IMGS + (k % 6) : -100000;
   }
-  const float bias1 = b1[lo < C1 ? lo : 0];
+  const float bias1 = b1[(lo & 7) < C1 ? (lo & 7) : 0];  // (lo & 7: the fused path's merged tile pairs)
   // every later layer's bias, issued now: its global-load latency hides behind conv1 instead of
   // stalling the conv2 / classifier epilogues (~1 us each after a barrier)
   const float bias2 = b2[lo];
@@ -460,12 +460,18 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       const int xp = par ^ (kp & 1);  // parity of pos + kp (pos0's parity is par; rows step by 66)
       pbq[q] = (const char*)(xp ? img1 - 1 + kp : img0 + kp) + 2 * pos0;
     }
+    // Epilogue on merged tile PAIRS: an MFMA tile's columns are 16 channels of which 6 are real, so
+    // the pool / ReLU / store sequence ran on 6 of 16 lanes.  Rows r and r + 1 are merged into one
+    // register set first — lanes 8..15 take tile r + 1's channels 0..7 by one DPP row shift per
+    // accumulator (row_shr:8 into banks 2-3) — and the sequence then runs once per pair.
     const int wo = 4 * sw + hi;  // this lane's output window column (C rows 4hi + i: its 4 quadrants)
-    const bool st1 = lo < C1 && wo < Q1, st2 = lo < 8 && wo < Q1;
-    uint16_t* const a1p = a1 + (lo < C1 ? lo : 0) * (Q1 * Q1) + wo;
-    uint8_t* const c1p = c1 + (lo < C1 ? lo : 0) * (Q1 * Q1) + wo;
-    uint16_t* const clp = sm.a1cl[slot] + wo * 8 + (lo < 8 ? lo : 0);
-    const float bias1z = lo < C1 ? bias1 : 0.f;  // channels 6, 7 of the channel-last copy: relu(0) = 0
+    const int ch = lo & 7, rb = lo >> 3;  // merged lane: channel ch of pool row r + rb
+    const bool st1 = ch < C1 && wo < Q1, st2 = wo < Q1;
+    uint16_t* const a1p = a1 + (ch < C1 ? ch : 0) * (Q1 * Q1) + wo + rb * Q1;
+    uint8_t* const c1p = c1 + (ch < C1 ? ch : 0) * (Q1 * Q1) + wo + rb * Q1;
+    uint16_t* const clp = sm.a1cl[slot] + (wo + rb * Q1) * 8 + ch;
+    const float bias1z = ch < C1 ? bias1 : 0.f;  // channels 6, 7 of the channel-last copy: relu(0) = 0
+    static_assert(Q1 % 2 == 0 && U1 % 2 == 0, "pool rows in whole pairs");
 #pragma unroll
     for (int r0 = 0; r0 < Q1; r0 += U1) {
       bf16x8 a[U1];
@@ -484,16 +490,23 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
       for (int u = 0; u < U1; ++u)
         if (r0 + u < Q1) acc[u] = mfma16(a[u], bw1, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-      for (int u = 0; u < U1; ++u) {
+      for (int u = 0; u < U1; u += 2) {
         if (r0 + u >= Q1) break;
-        const int r = r0 + u;
+        const int r = r0 + u;  // the pair's first pool row
+        // (whole-vector bit casts: hipcc folds a bit cast of ONE element of a vector to element 0)
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const i32x4 ai = __builtin_bit_cast(i32x4, acc[u]), bi = __builtin_bit_cast(i32x4, acc[u + 1]);
+        i32x4 mi;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mi[i] = __builtin_amdgcn_update_dpp(ai[i], bi[i], 0x118, 0xf, 0xc, false);
+        const f32x4 mg = __builtin_bit_cast(f32x4, mi);
         // max over the window's 4 quadrants; code = first quadrant attaining it (strict > as before)
-        float m = acc[u][0];
+        float m = mg[0];
         int arg = 0;
 #pragma unroll
         for (int i = 1; i < 4; ++i) {
-          const bool gt = acc[u][i] > m;
-          m = gt ? acc[u][i] : m;
+          const bool gt = mg[i] > m;
+          m = gt ? mg[i] : m;
           arg = gt ? i : arg;
         }
         m += bias1z;
