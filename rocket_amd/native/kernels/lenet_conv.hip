@@ -752,16 +752,17 @@ constexpr int SLABW = 2576;
 // keeps phase B's dx2 stores (rows = 2 image rows apart, channel lanes) and phase C's 8-byte reads
 // conflict-free (200: 2.75-way stores)
 constexpr int DX2S = Q1 * Q1 + 6;
-constexpr int PT_N = 8 * 25 + 8;    // posT entries: windows 0 .. 8*24 + 7
+// phase C's ones image: the ones column's B reads at the lane's offsets + the unrolled rows' immediates
+constexpr int PC_ONES = 880;
 struct BwdSmem {
   // k.imgb: bf16 image in two copies: [0][i] = img[i], [1][i] = img[i + 1], so any pair (x, x+1) is
   // ONE aligned 4-byte read (copy x & 1 at x & ~1) — the dW1 B operand is 4 pair reads per fragment.
   // Zero pair at [0][IMGZ].  k.a1 (+ zero slot at A1N), k.c1 (+ never-matching slot at A1N), k.c2.
   KeepSmem k;
   float dx2[SPB][C1 * DX2S];        // dL/d a1 (conv2 input gradient), channel rows of DX2S (zero tail)
-  uint16_t posT[PT_N];              // phase C: byte offset 2*pos1(w, 0) of pool window w (w >= 196: clamped)
+  uint16_t ones[PC_ONES];           // phase C: 16-bit 1.0 everywhere (the db1 "ones column" reads it)
   uint16_t posT2[32];               // phase B (dW2): pos2(w, 0) of conv2 window w (w >= 25: clamped)
-  uint16_t pad_a1o[46];             // places a1o at 46 mod 64 elements from a1 (see static_assert below)
+  uint16_t pad_a1o[78];             // places a1o at 46 mod 64 elements from a1 (see static_assert below)
   uint16_t a1o[SPB][A1N + 8];       // a1 shifted by one element (pair reads for the dW2 B operand)
   // (16-byte aligned: the pad before a1o must not shift the b128-read arrays from here on)
   alignas(16) uint16_t dc2[SPB][DCN + 16];  // dense channel-last dConv2 with zero ring
@@ -1131,13 +1132,11 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     RK_TR(cb.trace, 7);
     if (threadIdx.x < SPB * C1 * 4)  // dx2 zero tails (phase B writes windows < 196 only)
       sm.dx2[threadIdx.x / (C1 * 4)][(threadIdx.x / 4) % C1 * DX2S + Q1 * Q1 + (threadIdx.x & 3)] = 0.f;
-    if (threadIdx.x >= NTHR - PT_N) {  // phase C's window -> image offset table
-      const int w = threadIdx.x - (NTHR - PT_N);
-      sm.posT[w] = (uint16_t)(2 * pos1(min(w, Q1 * Q1 - 1), 0));
-    } else if (threadIdx.x >= NTHR - PT_N - 32) {  // phase B's (dW2) window -> a1 offset table
-      const int w = threadIdx.x - (NTHR - PT_N - 32);
+    if (threadIdx.x >= NTHR - 32) {  // phase B's (dW2) window -> a1 offset table
+      const int w = threadIdx.x - (NTHR - 32);
       sm.posT2[w] = (uint16_t)pos2(min(w, Q2 * Q2 - 1), 0);
     }
+    for (int i = threadIdx.x; i < PC_ONES; i += NTHR) sm.ones[i] = (uint16_t)(kH16 ? 0x3C00 : 0x3F80);
     // scatter the pooled gradients: thread e owns pooled element (co, w) of all SPB samples, so its
     // index arithmetic (divisions by 25 and 5) is done once, not once per (sample, element)
     static_assert(A2N <= NTHR, "one pooled element per thread");
@@ -1291,51 +1290,59 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
     lds_barrier();
     RK_TR(cb.trace, 9);
 
-    // ---- phase C: dW1 on all 16 waves (4 x 25 k-steps over the positions of the 14x14 pool grid);
-    // column r = 25 of tile u = 1 is the ones column (db1)
+    // ---- phase C: dW1 on all 16 waves over the positions of the 14x14 pool grid; column r = 25 of
+    // tile u = 1 is the ones column (db1)
     f32x4 g1[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     {
-      // Wave = (sample wave & 3, k-steps ks = wave / 4 + 4j): every per-step index is a lane constant
-      // plus the wave-uniform 8*ks, so a k-step is ~25 VALU instructions (it was ~80 with the window
-      // divisions, validity selects and code compares per lane; phase C was VALU-issue-bound).
-      // A (row co = lo, k = the 4 positions of windows wa = 8ks + 2hi and wa + 1): the pooled gradient
-      // placed at its argmax position by a 64-bit shift (code >= 4: ReLU off -> zero); lanes co >= 6
-      // duplicate channel 0 (their C rows are never stored); windows >= 196 read dx2's zero tail.
-      // B (k, col r = 16u + lo): 4 pair reads at the window's image offset (posT) + a lane constant;
-      // column r = 25 is the ones column (db1: offset 0 -> the ones pair), r > 25 are never stored.
-      int cst[2][4];
+      // Wave = (sample wave & 3, h0 = wave / 4): k-step j covers pool row r0 + 2j (r0 = h0 >> 1) and
+      // the 8 window columns 8*half + 2hi, +1 of lane group hi (half = h0 & 1; columns 14, 15 are
+      // padding: zero A).  Every address is then a lane constant plus a compile-time offset of the
+      // unrolled row loop — no per-step address arithmetic (the window-major order spent ~45 VALU
+      // instructions per k-step, 12 of them address adds; 28 k-steps instead of 25, the slowest wave
+      // still 7).
+      // A (row co = lo, k = the 4 positions of windows wa, wa + 1): the pooled gradient placed at its
+      // argmax position by a 64-bit shift (code >= 4: ReLU off, or padding -> zero); lanes co >= 6
+      // duplicate channel 0 (their C rows are never stored).
+      // B (k, col r = 16u + lo): 4 pair reads at the windows' image offsets + a column constant; the
+      // ones column r = 25 reads the ones image at the same offsets; r > 25 are never stored.
+      const int sl = wave & (SPB - 1), h0 = wave / SPB, half = h0 & 1, r0 = h0 >> 1;
+      const int c0 = 8 * half + 2 * hi;
+      const bool padl = c0 >= Q1;
+      const int cw = padl ? 0 : c0;  // padding lanes read window column 0 (any finite value; code forced)
+      const uint32_t cpad = padl ? 4u : 0u;
+      const int co = lo < C1 ? lo : 0;
+      const float* dxr = &sm.dx2[sl][co * DX2S + r0 * Q1 + cw];
+      const uint8_t* cr = &sm.k.c1[sl][co * (Q1 * Q1) + r0 * Q1 + cw];
+      const bool onecol = lo == R1 - 16;  // u = 1 lane of the ones column
+      const char* ib = (const char*)&sm.k.imgb[sl][0][0] + 2 * (2 * r0 * IMGS + 2 * cw);  // window (r0, cw)
+      const char* bb[2][4];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int r = 16 * u + lo;
+        const int r = min(16 * u + lo, R1 - 1);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const int x = (k & 1) * IMGS + (min(r, R1 - 1) / KS) * IMGS + (min(r, R1 - 1) % KS);
-          cst[u][k] = 2 * (r == R1 ? IMGN + 2 : ((x & 1) ? IMGC + x - 1 : x));  // bytes
+          const int x = (k & 1) * IMGS + (r / KS) * IMGS + (r % KS);
+          const int cst = 2 * ((x & 1) ? IMGC + x - 1 : x) + (k >> 1) * 4;  // bytes; window wa + 1: +2 pixels
+          bb[u][k] = (u == 1 && onecol) ? (const char*)sm.ones + (k >> 1) * 4 : ib + cst;
         }
       }
-      const bool onecol = lo == R1 - 16;  // u = 1 lane of the ones column: no window offset
-      const int sl = wave & (SPB - 1);
-      const int co = lo < C1 ? lo : 0;
-      const float* dxr = &sm.dx2[sl][co * DX2S + 2 * hi];
-      const uint8_t* cr = &sm.k.c1[sl][co * (Q1 * Q1) + 2 * hi];
-      const uint16_t* pt = &sm.posT[2 * hi];
-      const char* ib = (const char*)&sm.k.imgb[sl][0][0];
       static_assert(NTHR / 64 == 4 * SPB, "4 waves per sample in phase C");
-      for (int ks = wave / SPB; ks < 25; ks += 4) {
-        const int o = 8 * ks;
-        const float da = dxr[o], dbv = dxr[o + 1];
-        const uint32_t ca = cr[o], cb2 = cr[o + 1];
-        const uint32_t pa = pt[o], pb = pt[o + 1];
-        const uint32_t ab = pack16t<kH16>(da, dbv);
+      static_assert(6 * 8 * IMGS + 8 + 4 <= 2 * PC_ONES, "ones image covers the unrolled rows");
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {  // pool rows r0 + 2j
+        const float2 dd = *(const float2*)(dxr + 2 * j * Q1);
+        const uint32_t cc = *(const uint16_t*)(cr + 2 * j * Q1);
+        const uint32_t ca = (cc & 0xffu) | cpad, cb2 = (cc >> 8) | cpad;
+        const uint32_t ab = pack16t<kH16>(dd.x, dd.y);
         const uint64_t ea = ca < 4 ? (uint64_t)(ab & 0xffffu) << (16 * ca) : 0ull;
         const uint64_t eb = cb2 < 4 ? (uint64_t)(ab >> 16) << (16 * cb2) : 0ull;
         const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4((uint32_t)ea, (uint32_t)(ea >> 32), (uint32_t)eb,
                                                                (uint32_t)(eb >> 32)));
+        const int ro = j * 8 * IMGS;  // bytes: two pool rows = four image rows
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const uint32_t qa = (u == 1 && onecol) ? 0u : pa, qb = (u == 1 && onecol) ? 0u : pb;
-          const uint4 w = make_uint4(*(const uint32_t*)(ib + qa + cst[u][0]), *(const uint32_t*)(ib + qa + cst[u][1]),
-                                     *(const uint32_t*)(ib + qb + cst[u][2]), *(const uint32_t*)(ib + qb + cst[u][3]));
+          const uint4 w = make_uint4(*(const uint32_t*)(bb[u][0] + ro), *(const uint32_t*)(bb[u][1] + ro),
+                                     *(const uint32_t*)(bb[u][2] + ro), *(const uint32_t*)(bb[u][3] + ro));
           g1[u] = mfma16(a, __builtin_bit_cast(bf16x8, w), g1[u]);
         }
       }
