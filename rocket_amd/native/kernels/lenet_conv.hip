@@ -993,23 +993,15 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
         if (wave == 0) {
           const int sl = lane >> 4, o = lane & 15;
           const bool valid = ce_t != cb.ignore_index, oc = o < F3;
-          float mx = oc ? ce_x : -INFINITY;
-#pragma unroll
-          for (int k = 1; k < 16; k <<= 1) mx = fmaxf(mx, __shfl_xor(mx, k, 64));
+          // row reductions on the DPP network (each sample's 16 logits are one 16-lane row): the
+          // ds_bpermute shuffles were ten LDS round trips in a row on the step's critical path
+          const float mx = row16_max(oc ? ce_x : -INFINITY);
           const float e = oc ? __expf(ce_x - mx) : 0.f;
-          float se = e, xt = (oc && (int64_t)o == ce_t) ? ce_x : 0.f;
-#pragma unroll
-          for (int k = 1; k < 16; k <<= 1) {
-            se += __shfl_xor(se, k, 64);
-            xt += __shfl_xor(xt, k, 64);
-          }
+          const float se = row16_sum(e), xt = row16_sum((oc && (int64_t)o == ce_t) ? ce_x : 0.f);
           if (oc) sm.dyf[sl][o] = valid ? e / se - ((int64_t)o == ce_t ? 1.f : 0.f) : 0.f;
-          float li = (o == 0 && valid) ? mx + __logf(se) - xt : 0.f;  // lanes 0/16/32/48: a sample's loss
-          float ci = (o == 0 && valid) ? 1.f : 0.f;
-          li += __shfl_xor(li, 16, 64);
-          li += __shfl_xor(li, 32, 64);
-          ci += __shfl_xor(ci, 16, 64);
-          ci += __shfl_xor(ci, 32, 64);
+          // lanes 0/16/32/48: a sample's loss and valid count -> the block's sums (wave-uniform)
+          const float li = rows4_sum((o == 0 && valid) ? mx + __logf(se) - xt : 0.f);
+          const float ci = rows4_sum((o == 0 && valid) ? 1.f : 0.f);
           if (lane == 0) {  // block running sums over rounds (LDS: no live register)
             sm.lossp[0] += li;
             sm.cecnt[0] += ci;

@@ -116,6 +116,35 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
          (__builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 32)) +
           __builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 48)));
 }
+// Reduction over each 16-lane row (DPP butterflies, no LDS): every lane gets its row's sum / max.
+__device__ __forceinline__ float row16_sum(float v) {
+  int t = __builtin_bit_cast(int, v);
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0xb1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]
+  t = __builtin_bit_cast(int, v);
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x4e, 0xf, 0xf, false));  // quad_perm [2,3,0,1]
+  t = __builtin_bit_cast(int, v);
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  t = __builtin_bit_cast(int, v);
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x140, 0xf, 0xf, false));  // row_mirror
+}
+__device__ __forceinline__ float row16_max(float v) {
+  int t = __builtin_bit_cast(int, v);
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0xb1, 0xf, 0xf, false)));
+  t = __builtin_bit_cast(int, v);
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x4e, 0xf, 0xf, false)));
+  t = __builtin_bit_cast(int, v);
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x141, 0xf, 0xf, false)));
+  t = __builtin_bit_cast(int, v);
+  return fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x140, 0xf, 0xf, false)));
+}
+// sum of lanes 0, 16, 32, 48 (one value per 16-lane row), wave-uniform
+__device__ __forceinline__ float rows4_sum(float v) {
+  const int t = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(t, 48)));
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
