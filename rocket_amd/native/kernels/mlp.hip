@@ -337,7 +337,7 @@ struct StepFill {
   __device__ __forceinline__ void operator()() const {
     if (a->epi.on && threadIdx.x < kEpiGroups) s_ks[threadIdx.x] = rk_opt::adam_step(hy, cur + 1.f);
     if (a->cnt_parts) {
-      const float c = wave_sum(cpart);
+      const float c = wave_sum_dpp(cpart);  // (all lanes active; DPP, not six ds_bpermute round trips)
       if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = c;
     }
   }
