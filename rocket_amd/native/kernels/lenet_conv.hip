@@ -295,12 +295,16 @@ struct ClsFwd {  // classifier operands of the fused forward
 struct ClsBwdFrags {
   bf16x8 fb3, fb2[3], fb1[2][4];
 };
-__device__ __forceinline__ void load_cls_bwd(const bf16x8* __restrict__ frag, int wave, int lane, ClsBwdFrags& f) {
+__device__ __forceinline__ void load_cls_bwd23(const bf16x8* __restrict__ frag, int wave, int lane, ClsBwdFrags& f) {
   if (wave < 6) f.fb3 = frag[(OFF_B3 + wave) * 64 + lane];
   if (wave < 8) {
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) f.fb2[ks] = frag[(OFF_B2 + wave * 3 + ks) * 64 + lane];
   }
+}
+// fc1's (100 of the 130 KB per block): issued after fc3, so the 100 KB do not share fc2's phase
+// with its own operand traffic (the vector-memory pipe, ~64 B/clk/CU, set fc2's length)
+__device__ __forceinline__ void load_cls_bwd1(const bf16x8* __restrict__ frag, int wave, int lane, ClsBwdFrags& f) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int t = wave + 16 * u;
@@ -692,7 +696,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
     }
     // the backward's classifier fragments, issued once fc2 no longer waits on its own operands
     // (issued before fc2 they put vmcnt waits into fc2's chain: +0.8 us)
-    if (pre) load_cls_bwd(bfrag, wave, lane, *pre);
+    if (pre) load_cls_bwd23(bfrag, wave, lane, *pre);
     lds_barrier();
     RK_TR(cf.trace, 7);
     if (wave == 0) {  // fc3: 1 n-tile x 3 k-steps -> fp32 logits
@@ -706,6 +710,7 @@ __device__ __forceinline__ void fwd_body(FwdSmem& sm, const float* __restrict__ 
         }
       }
     }
+    if (pre) load_cls_bwd1(bfrag, wave, lane, *pre);
     RK_TR(cf.trace, 8);
   }
 }
@@ -864,7 +869,10 @@ __device__ __forceinline__ void bwd_body(BwdSmem& sm, const float* __restrict__ 
   ClsBwdFrags fl;
   if constexpr (MLP) {
     if (pre) fl = *pre;
-    else load_cls_bwd(cb.frag, wave, lane, fl);
+    else {
+      load_cls_bwd23(cb.frag, wave, lane, fl);
+      load_cls_bwd1(cb.frag, wave, lane, fl);
+    }
   }
   const bf16x8& fb3 = fl.fb3;
   const bf16x8 (&fb2)[3] = fl.fb2;
