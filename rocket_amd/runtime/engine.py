@@ -206,18 +206,36 @@ class EngineScheduler:
 
     def _snapshot(self):
         sd = {k: (list(v) if isinstance(v, list) else v) for k, v in self.scheduler.state_dict().items()}
-        return sd, [{k: v for k, v in g.items() if k != "params"} for g in self._groups()]
+        return "full", sd, [{k: v for k, v in g.items() if k != "params"} for g in self._groups()]
 
     def _resolve(self) -> None:
         p, self._pending = self._pending, None
         if p is None:
             return
-        handles, (sd, groups) = p
+        handles, snap = p
         if any(FusedGradScaler.handle_skipped(h) for h in handles):
             self.mispredicted += 1
+            if snap[0] == "light":  # fast StepLR steps: only these three fields moved
+                s = self.scheduler
+                _, s._step_count, s.last_epoch, s._last_lr = snap
+                return
+            _, sd, groups = snap
             self.scheduler.load_state_dict(sd)
             for g, saved in zip(self._groups(), groups):
                 g.update(saved)
+
+    def _light_ok(self) -> bool:
+        """The next scheduler step(s) of this sync step are all ``_fast_step``s (StepLR between
+        milestones): they move only ``_step_count`` / ``last_epoch`` / ``_last_lr`` and leave every
+        hyperparameter, so the provisional step needs no state_dict snapshot nor group compare."""
+        s = self.scheduler
+        if type(s) is not torch.optim.lr_scheduler.StepLR or s._step_count == 1:
+            return False
+        for i in range(1, self.engine.num_processes + 1):
+            e = s.last_epoch + i
+            if e == 0 or e % s.step_size == 0:
+                return False
+        return all(type(g["lr"]) is float for g in s.optimizer.param_groups)
 
     def _do_step(self, *args, **kwargs) -> None:
         for _ in range(self.engine.num_processes):
@@ -254,16 +272,23 @@ class EngineScheduler:
         lazy = [o for o in self.optimizers if o._skip_lazy and o._lazy_handle is not None]
         handles = [o._lazy_handle for o in lazy]
         if lazy and len(lazy) == len(self.optimizers) and not all(FusedGradScaler.handle_ready(h) for h in handles):
+            if not args and not kwargs and self._light_ok():
+                s = self.scheduler
+                snap = ("light", s._step_count, s.last_epoch, s._last_lr)
+                self._do_step()
+                self.provisional += 1
+                self._pending = (handles, snap)
+                return
             snap = self._snapshot()
             self._do_step(*args, **kwargs)
             if self.SPECULATE or all(
-                    {k: v for k, v in g.items() if k != "params"} == saved for g, saved in zip(self._groups(), snap[1])):
+                    {k: v for k, v in g.items() if k != "params"} == saved for g, saved in zip(self._groups(), snap[2])):
                 self.provisional += 1
                 self._pending = (handles, snap)
                 return
             # this step moves a hyperparameter: undo it and decide on the flag itself
-            self.scheduler.load_state_dict(snap[0])
-            for g, saved in zip(self._groups(), snap[1]):
+            self.scheduler.load_state_dict(snap[1])
+            for g, saved in zip(self._groups(), snap[2]):
                 g.update(saved)
         if any(o.step_was_skipped for o in self.optimizers):
             return

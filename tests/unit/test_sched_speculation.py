@@ -184,3 +184,29 @@ def test_steplr_fast_path_matches_torch():
         assert opt_a.param_groups[0]["lr"] == opt_b.param_groups[0]["lr"]
         assert ref.state_dict() == s.state_dict()
     assert copy.deepcopy(s.get_last_lr()) == ref.get_last_lr()
+
+
+def test_light_provisional_step_rolls_back_exactly():
+    """Between StepLR milestones the provisional step keeps a three-field snapshot (no
+    state_dict); a skipped step restores exactly the state of a scheduler that never took it."""
+    p = torch.nn.Parameter(torch.zeros(2))
+    opt = torch.optim.SGD([p], lr=1.0)
+    eo = EngineOptimizer(opt, _Eng())
+    sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=10, gamma=0.5), [eo], _Eng())
+    ref_opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(2))], lr=1.0)
+    ref = torch.optim.lr_scheduler.StepLR(ref_opt, step_size=10, gamma=0.5)
+    skips = [False, False, True, False, True, True, False, False, False, False, False, False, True, False]
+    for i, sk in enumerate(skips):
+        eo._skip_lazy, eo._lazy_handle = True, _flag(sk)
+        sch.step()
+        if i + 1 < len(skips) and 1 < sch.scheduler._step_count and (sch.scheduler.last_epoch % 10):
+            assert sch._pending is None or sch._pending[1][0] in ("light", "full")
+        if not sk:
+            ref_opt.step()
+            ref.step()
+    sch._resolve()
+    assert sch.scheduler.last_epoch == ref.last_epoch
+    assert sch.scheduler._step_count == ref._step_count
+    assert sch.scheduler.get_last_lr() == ref.get_last_lr()
+    assert opt.param_groups[0]["lr"] == ref_opt.param_groups[0]["lr"]
+    assert sch.provisional > 0
