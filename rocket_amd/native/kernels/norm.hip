@@ -1315,6 +1315,15 @@ RK_API int rk_bn_finalize(const float* tp, int ntiles, int tile_rows, int64_t R,
 }
 
 // rows per block for the elementwise passes: ~2048 blocks, whole passes of RPP rows
+static int bn_ew_variant();
+// the variant for one tensor: nontemporal only for tensors far beyond the Infinity Cache's reuse
+// (ResNet-50's >= 103 MB BatchNorm tensors gain 1-10%; ResNet-18's CIFAR-shape 33 MB ones lose 1.9%
+// with it: the next pass re-reads them from the cache; scripts/r5/gpu_r18.sh)
+static int bn_ew_for(int64_t R, int C) {
+  int v = bn_ew_variant();
+  if (R * (int64_t)C * 2 < ((int64_t)64 << 20)) v &= ~1;
+  return v;
+}
 static int bn_ew_variant() {
   // default 1 (nontemporal): ResNet-50 10,569-10,579 -> 10,668-10,682 img/s, the fused BN
   // fwd+bwd probe +10% on the 56x56 / 28x28 residual shapes (profiles/r5_bn_ew_ab.md)
@@ -1454,7 +1463,7 @@ RK_API int rk_bn_apply(int dt, int dto, const void* x, const void* res, const fl
   if (dt == F16 && dto == F16) RK_BA(f16_t, f16_t);
   else if (dt == F16 && dto == F32) RK_BA(f16_t, float);
   else if (dt == BF16 && dto == BF16) {
-    switch (bn_ew_variant()) {
+    switch (bn_ew_for(R, C)) {
       case 1: RK_BA(uint16_t, uint16_t, 1); break;
       case 2: RK_BA(uint16_t, uint16_t, 2); break;
       case 3: RK_BA(uint16_t, uint16_t, 3); break;
@@ -1490,7 +1499,7 @@ RK_API int rk_bn_bwd(int dt, int dto, const void* dy, const void* x, const void*
   if (dt == F16 && dto == F16) RK_BB(f16_t, f16_t);
   else if (dt == F16 && dto == F32) RK_BB(f16_t, float);
   else if (dt == BF16 && dto == BF16) {
-    switch (bn_ew_variant()) {
+    switch (bn_ew_for(R, C)) {
       case 1: RK_BB(uint16_t, uint16_t, 1); break;
       case 2: RK_BB(uint16_t, uint16_t, 2); break;
       case 3: RK_BB(uint16_t, uint16_t, 3); break;
@@ -1532,7 +1541,7 @@ RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, co
   if (dt == F16 && dto == F16) RK_BP(f16_t, f16_t);
   else if (dt == F16 && dto == F32) RK_BP(f16_t, float);
   else if (dt == BF16 && dto == BF16) {
-    switch (bn_ew_variant()) {
+    switch (bn_ew_for(R, C)) {
       case 1: RK_BP(uint16_t, uint16_t, 1); break;
       case 2: RK_BP(uint16_t, uint16_t, 2); break;
       case 3: RK_BP(uint16_t, uint16_t, 3); break;
