@@ -192,6 +192,11 @@ class EngineScheduler:
     #: Opt-in (ROCKET_SCHED_SPECULATE=1): provisional steps also when the hyperparameters change;
     #: after a skipped step one update then runs with the next lr, which accelerate never does.
     SPECULATE = os.environ.get("ROCKET_SCHED_SPECULATE", "0") == "1"
+    #: ROCKET_SCHED_LIGHT=1: provisional steps between StepLR milestones keep a three-field snapshot
+    #: instead of a state_dict copy.  Off: it cut host time per step but the fp16 LeNet step measured
+    #: slower with it (19.7-19.8 M vs 21.1-21.3 M samples/s, same box, scripts/r5/gpu_fp.sh; the GPU
+    #: step p50 rose 0.043 -> 0.046 ms — the faster host polls the device's skip-flag ring sooner)
+    LIGHT = os.environ.get("ROCKET_SCHED_LIGHT", "0") == "1"
 
     def __init__(self, scheduler, optimizers: List[EngineOptimizer], engine: "Engine"):
         self.scheduler = scheduler
@@ -272,7 +277,7 @@ class EngineScheduler:
         lazy = [o for o in self.optimizers if o._skip_lazy and o._lazy_handle is not None]
         handles = [o._lazy_handle for o in lazy]
         if lazy and len(lazy) == len(self.optimizers) and not all(FusedGradScaler.handle_ready(h) for h in handles):
-            if not args and not kwargs and self._light_ok():
+            if self.LIGHT and not args and not kwargs and self._light_ok():
                 s = self.scheduler
                 snap = ("light", s._step_count, s.last_epoch, s._last_lr)
                 self._do_step()

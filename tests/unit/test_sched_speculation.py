@@ -193,6 +193,7 @@ def test_light_provisional_step_rolls_back_exactly():
     opt = torch.optim.SGD([p], lr=1.0)
     eo = EngineOptimizer(opt, _Eng())
     sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=10, gamma=0.5), [eo], _Eng())
+    sch.LIGHT = True
     ref_opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(2))], lr=1.0)
     ref = torch.optim.lr_scheduler.StepLR(ref_opt, step_size=10, gamma=0.5)
     skips = [False, False, True, False, True, True, False, False, False, False, False, False, True, False]
