@@ -905,6 +905,7 @@ RK_API int rk_attn_set_waves(int fwd, int bwd_q, int bwd_kv) {
 RK_API int rk_attn_fwd16(int hf, const void* q, const void* k, const void* v, int ld, void* out, int ldo, float* lse,
                          int B, int L, int H, float scale, hipStream_t s) {
   if (L < 1 || L > LMAX || B < 1 || H < 1) return (int)hipErrorInvalidValue;
+  if (ldo % 4 != 0 || (uintptr_t)out % 8 != 0) return (int)hipErrorInvalidValue;  // 8-byte O row pieces
   AttnArgs a{};
   a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v;
   a.out = (uint16_t*)out; a.lse = lse; a.ld = ld; a.ldo = ldo; a.L = L; a.H = H; a.scale = scale;
