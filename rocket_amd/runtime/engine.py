@@ -197,12 +197,16 @@ class EngineScheduler:
     #: slower with it (19.7-19.8 M vs 21.1-21.3 M samples/s, same box, scripts/r5/gpu_fp.sh; the GPU
     #: step p50 rose 0.043 -> 0.046 ms — the faster host polls the device's skip-flag ring sooner)
     LIGHT = os.environ.get("ROCKET_SCHED_LIGHT", "0") == "1"
+    #: provisional steps kept undecided at once (exact form): a step does not wait for the previous
+    #: steps' flags, it settles the ones that have landed (the flag ring holds 64 updates).
+    #: ROCKET_SCHED_QUEUE=1: one at a time (every step first waits for the previous step's flag)
+    MAXQ = max(1, min(32, int(os.environ.get("ROCKET_SCHED_QUEUE", "16"))))
 
     def __init__(self, scheduler, optimizers: List[EngineOptimizer], engine: "Engine"):
         self.scheduler = scheduler
         self.optimizers = optimizers
         self.engine = engine
-        self._pending = None  # (flag handles, snapshot) of a provisional step
+        self._queue = []  # [(flag handles, snapshot)] of provisional steps, oldest first
         self.mispredicted = 0  # provisional steps rolled back (their update was skipped)
         self.provisional = 0  # steps taken before their skip flag was read
 
@@ -213,21 +217,44 @@ class EngineScheduler:
         sd = {k: (list(v) if isinstance(v, list) else v) for k, v in self.scheduler.state_dict().items()}
         return "full", sd, [{k: v for k, v in g.items() if k != "params"} for g in self._groups()]
 
-    def _resolve(self) -> None:
-        p, self._pending = self._pending, None
-        if p is None:
+    @property
+    def _pending(self):
+        """The newest provisional step (flag handles, snapshot), or None."""
+        return self._queue[-1] if self._queue else None
+
+    def _restore(self, snap) -> None:
+        if snap[0] == "light":  # fast StepLR steps: only these three fields moved
+            s = self.scheduler
+            _, s._step_count, s.last_epoch, s._last_lr = snap
             return
-        handles, snap = p
-        if any(FusedGradScaler.handle_skipped(h) for h in handles):
-            self.mispredicted += 1
-            if snap[0] == "light":  # fast StepLR steps: only these three fields moved
-                s = self.scheduler
-                _, s._step_count, s.last_epoch, s._last_lr = snap
+        _, sd, groups = snap
+        self.scheduler.load_state_dict(sd)
+        for g, saved in zip(self._groups(), groups):
+            g.update(saved)
+
+    def _resolve(self, wait: bool = True) -> None:
+        """Settle the provisional steps in order: a kept one is dropped from the queue; a skipped one
+        is undone (its snapshot restored) and the later, still undecided ones are taken again from
+        there.  They left every hyperparameter unchanged, and re-taken one epoch earlier they stay
+        inside the same constant stretch of the schedule, so no update sees a different lr.
+        ``wait=False``: stop at the first step whose flag has not landed (no host sync)."""
+        while self._queue:
+            handles, snap = self._queue[0]
+            if not wait and not all(FusedGradScaler.handle_ready(h) for h in handles):
                 return
-            _, sd, groups = snap
-            self.scheduler.load_state_dict(sd)
-            for g, saved in zip(self._groups(), groups):
-                g.update(saved)
+            if not any(FusedGradScaler.handle_skipped(h) for h in handles):
+                self._queue.pop(0)
+                continue
+            self.mispredicted += 1
+            later = self._queue[1:]
+            self._restore(snap)
+            self._queue = []
+            for h2, old in later:
+                light = old[0] == "light"
+                s = self.scheduler
+                self._queue.append((h2, ("light", s._step_count, s.last_epoch, s._last_lr) if light
+                                    else self._snapshot()))
+                self._do_step()
 
     def _light_ok(self) -> bool:
         """The next scheduler step(s) of this sync step are all ``_fast_step``s (StepLR between
@@ -273,7 +300,11 @@ class EngineScheduler:
         if not self.engine.sync_gradients:
             self.scheduler._step_count += 1
             return
-        self._resolve()
+        # exact form: settle the provisional steps whose flags have landed, without waiting for the
+        # rest (a host sync here would drain the device queue every step); speculation / explicit
+        # scheduler arguments keep one undecided step at a time
+        queued = not (self.SPECULATE or args or kwargs)
+        self._resolve(wait=not queued or len(self._queue) >= self.MAXQ)
         lazy = [o for o in self.optimizers if o._skip_lazy and o._lazy_handle is not None]
         handles = [o._lazy_handle for o in lazy]
         if lazy and len(lazy) == len(self.optimizers) and not all(FusedGradScaler.handle_ready(h) for h in handles):
@@ -282,19 +313,19 @@ class EngineScheduler:
                 snap = ("light", s._step_count, s.last_epoch, s._last_lr)
                 self._do_step()
                 self.provisional += 1
-                self._pending = (handles, snap)
+                self._queue.append((handles, snap))
                 return
             snap = self._snapshot()
             self._do_step(*args, **kwargs)
             if self.SPECULATE or all(
                     {k: v for k, v in g.items() if k != "params"} == saved for g, saved in zip(self._groups(), snap[2])):
                 self.provisional += 1
-                self._pending = (handles, snap)
+                self._queue.append((handles, snap))
                 return
-            # this step moves a hyperparameter: undo it and decide on the flag itself
-            self.scheduler.load_state_dict(snap[1])
-            for g, saved in zip(self._groups(), snap[2]):
-                g.update(saved)
+            # this step moves a hyperparameter: undo it, settle every earlier provisional step, then
+            # decide on this step's own flag
+            self._restore(snap)
+            self._resolve()
         if any(o.step_was_skipped for o in self.optimizers):
             return
         self._do_step(*args, **kwargs)
@@ -308,7 +339,7 @@ class EngineScheduler:
         return self.scheduler.state_dict()
 
     def load_state_dict(self, sd):
-        self._pending = None
+        self._queue = []
         self.scheduler.load_state_dict(sd)
 
     def __getattr__(self, name):

@@ -211,3 +211,60 @@ def test_light_provisional_step_rolls_back_exactly():
     assert sch.scheduler.get_last_lr() == ref.get_last_lr()
     assert opt.param_groups[0]["lr"] == ref_opt.param_groups[0]["lr"]
     assert sch.provisional > 0
+
+
+class _LagFlags:
+    """A skip flag that lands ``lag`` scheduler steps after its update (the device running behind
+    the host); reading it before then waits (counted)."""
+
+    clock = [0]
+    waits = [0]
+
+    def __init__(self, skipped: bool, lag: int):
+        self.skipped, self.at = skipped, _LagFlags.clock[0] + lag
+
+    def _entry(self, seq):
+        return self.skipped if _LagFlags.clock[0] >= self.at else None
+
+    def _resolve(self, seq):
+        if _LagFlags.clock[0] < self.at:
+            _LagFlags.waits[0] += 1
+        return self.skipped
+
+
+def test_queued_provisional_steps_with_lagging_flags_match_accelerate():
+    """Exact form with the device several steps behind: provisional steps queue up (no wait per
+    step), flags settle in order as they land, a skipped one is undone and the later ones re-taken;
+    the lr every update runs with and the final scheduler state equal accelerate's, and only the
+    milestone steps wait."""
+    for light in (False, True):
+        skips = [False, True, False, False, True, True, False, False, False, True, False, False, False, True,
+                 False, False, False, False, True, False, False, False, False, False, False]
+        p = torch.nn.Parameter(torch.zeros(2))
+        opt = torch.optim.SGD([p], lr=1.0)
+        eo = EngineOptimizer(opt, _Eng())
+        sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=4, gamma=0.5), [eo], _Eng())
+        sch.LIGHT = light
+        ref_opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(2))], lr=1.0)
+        ref = torch.optim.lr_scheduler.StepLR(ref_opt, step_size=4, gamma=0.5)
+        _LagFlags.clock[0], _LagFlags.waits[0] = 0, 0
+        seen, want = [], []
+        for sk in skips:
+            seen.append(opt.param_groups[0]["lr"])
+            want.append(ref_opt.param_groups[0]["lr"])
+            eo._skip_lazy, eo._lazy_handle = True, (_LagFlags(sk, lag=3), 1)
+            milestone = (sch.scheduler.last_epoch + 1) % 4 == 0  # this step would change the lr
+            w0 = _LagFlags.waits[0]
+            sch.step()
+            assert milestone or _LagFlags.waits[0] == w0  # only a milestone step waits for flags
+            _LagFlags.clock[0] += 1
+            if not sk:
+                ref_opt.step()
+                ref.step()
+            assert len(sch._queue) <= sch.MAXQ
+        sch._resolve()
+        assert seen == want
+        assert sch.scheduler.last_epoch == ref.last_epoch and sch.scheduler._step_count == ref._step_count
+        assert sch.scheduler.get_last_lr() == ref.get_last_lr()
+        assert opt.param_groups[0]["lr"] == ref_opt.param_groups[0]["lr"]
+        assert sch.mispredicted >= 3 and sch.provisional >= 10
