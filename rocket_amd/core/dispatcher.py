@@ -27,7 +27,7 @@ class Dispatcher(Capsule):
         self.guard(capsules)
         # list.sort is stable: equal priorities keep insertion order
         self._capsules = sorted(capsules, key=lambda c: c._priority, reverse=True)
-        self._launch_handlers = None  # (children list, bound launch handlers) — see launch()
+        self._launch_handlers = None  # (children list, bound launch handlers, len) — see launch(); set to None after re-binding a child's launch on the instance
 
     def _fan_out(self, event: Events, attrs: Attributes | None) -> None:
         for capsule in self._capsules:
@@ -54,11 +54,13 @@ class Dispatcher(Capsule):
         # the per-iteration event: the children's bound ``launch`` handlers, resolved once (a child
         # that overrides ``dispatch`` keeps going through it), called in priority order — the same
         # calls as ``_fan_out(Events.LAUNCH)`` without an enum lookup + getattr per child per step
+        # (re-resolved when the child list is replaced or mutated in place: identity + length)
         hs = self._launch_handlers
-        if hs is None or hs[0] is not self._capsules:
-            hs = self._launch_handlers = (self._capsules, [
+        caps = self._capsules
+        if hs is None or hs[0] is not caps or hs[2] != len(caps):
+            hs = self._launch_handlers = (caps, [
                 c.launch if type(c).dispatch is _BASE_DISPATCH else (lambda a, c=c: c.dispatch(Events.LAUNCH, a))
-                for c in self._capsules])
+                for c in caps], len(caps))
         for h in hs[1]:
             h(attrs)
 

@@ -114,12 +114,16 @@ class Looper(Dispatcher):
 
             bar = tqdm(total=self._repeats, desc=f"{_green(self._tag)} epoch={epoch}, grad={self._grad_enabled}")
         last = 0.0
-        # grad mode for the whole loop (the reference enters it per iteration, loop.py:217; the
-        # children see the same mode either way, and it is restored when the loop ends)
-        with torch.set_grad_enabled(self._grad_enabled):
+        # grad mode entered once for the whole loop and re-established after any iteration whose
+        # children switched it outside a context manager: every iteration starts in the mode the
+        # reference enters per iteration (loop.py:217), without a context enter/exit per step
+        g = self._grad_enabled
+        with torch.set_grad_enabled(g):
             for i in range(self._repeats):
                 attrs["batch"] = None
                 Dispatcher.launch(self, attrs)
+                if torch.is_grad_enabled() != g:
+                    torch.set_grad_enabled(g)
                 if attrs["looper"]["terminate"]:
                     break
                 if bar is not None:

@@ -126,7 +126,9 @@ class _FusedBase(torch.optim.Optimizer):
             raw = [get(g) for g in self.param_groups]
             if raw == self._hyper_raw:
                 return  # (never cached while any entry is a tensor: those change in place)
-            self._hyper_raw = None if any(isinstance(v, torch.Tensor) for r in raw for v in r) else raw
+            # tuple entries too (betas=(Tensor, Tensor) is valid torch Adam/AdamW input)
+            self._hyper_raw = None if any(isinstance(x, torch.Tensor) for r in raw for v in r
+                                          for x in (v if isinstance(v, (tuple, list)) else (v,))) else raw
         flat = [x for g in self.param_groups for x in self._hyper_row(g)]
         if flat != self._hyper_list:
             self._hyper_list = flat

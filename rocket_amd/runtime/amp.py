@@ -245,6 +245,17 @@ class FusedGradScaler:
         return h[1] == 0 or h[0]._entry(h[1]) is not None
 
     @staticmethod
+    def handle_seq(h):
+        """The update number a handle names (None for the null handle or a stand-in without one)."""
+        return h[1] if h[1] != 0 and isinstance(h[1], int) else None
+
+    @staticmethod
+    def handle_age(h) -> int:
+        """Updates launched on the handle's scaler since the one it names (the flag ring keeps RING)."""
+        seq = getattr(h[0], "_seq", None)
+        return 0 if h[1] == 0 or not isinstance(seq, int) else seq - h[1]
+
+    @staticmethod
     def handle_skipped(h) -> bool:
         return False if h[1] == 0 else h[0]._resolve(h[1])
 

@@ -37,7 +37,7 @@ from torch import nn
 from rocket_amd.parallel.ddp import DataParallel, unwrap
 from rocket_amd.runtime import comm as _comm
 from rocket_amd.runtime import checkpoint_io
-from rocket_amd.runtime.amp import FusedGradScaler, make_scaler
+from rocket_amd.runtime.amp import RING as _AMP_RING, FusedGradScaler, make_scaler
 from rocket_amd.runtime.host_data import HostLoader, HostTensorDataset
 from rocket_amd.runtime.data import (
     DeviceLoader,
@@ -194,7 +194,7 @@ class EngineScheduler:
     SPECULATE = os.environ.get("ROCKET_SCHED_SPECULATE", "0") == "1"
     #: ROCKET_SCHED_LIGHT=1: provisional steps between StepLR milestones keep a three-field snapshot
     #: instead of a state_dict copy.  Off: it cut host time per step but the fp16 LeNet step measured
-    #: slower with it (19.7-19.8 M vs 21.1-21.3 M samples/s, same box, scripts/r5/gpu_fp.sh; the GPU
+    #: slower with it (19.7-19.8 M vs 21.1-21.3 M samples/s, same box, scripts/archive/r5/gpu_fp.sh; the GPU
     #: step p50 rose 0.043 -> 0.046 ms — the faster host polls the device's skip-flag ring sooner)
     LIGHT = os.environ.get("ROCKET_SCHED_LIGHT", "0") == "1"
     #: provisional steps kept undecided at once (exact form): a step does not wait for the previous
@@ -209,6 +209,7 @@ class EngineScheduler:
         self._queue = []  # [(flag handles, snapshot)] of provisional steps, oldest first
         self.mispredicted = 0  # provisional steps rolled back (their update was skipped)
         self.provisional = 0  # steps taken before their skip flag was read
+        self._seen_seq = {}  # id(scaler) -> its update count at the previous scheduler step
 
     def _groups(self):
         return [g for o in self.optimizers for g in o.optimizer.param_groups]
@@ -255,6 +256,27 @@ class EngineScheduler:
                 self._queue.append((h2, ("light", s._step_count, s.last_epoch, s._last_lr) if light
                                     else self._snapshot()))
                 self._do_step()
+
+    def _cadence(self, handles) -> int:
+        """Scaler updates since the previous scheduler step (the largest over the handles' scalers);
+        remembers the current counts for the next call."""
+        seen = self._seen_seq
+        cadence = 0
+        for h in handles:
+            seq = FusedGradScaler.handle_seq(h)
+            if seq is None:
+                continue
+            cadence = max(cadence, seq - seen.get(id(h[0]), 0))  # first step: updates since the start
+            seen[id(h[0])] = seq
+        return cadence
+
+    def _ages_out(self, cadence: int) -> bool:
+        """Whether the oldest provisional step's flag would be overwritten in the scaler's flag ring
+        (``amp.RING`` updates) before the next scheduler step: then it is settled now."""
+        if not self._queue:
+            return False
+        age = max((FusedGradScaler.handle_age(h) for h in self._queue[0][0]), default=0)
+        return age + cadence + len(self.optimizers) >= _AMP_RING
 
     def _light_ok(self) -> bool:
         """The next scheduler step(s) of this sync step are all ``_fast_step``s (StepLR between
@@ -304,10 +326,16 @@ class EngineScheduler:
         # rest (a host sync here would drain the device queue every step); speculation / explicit
         # scheduler arguments keep one undecided step at a time
         queued = not (self.SPECULATE or args or kwargs)
-        self._resolve(wait=not queued or len(self._queue) >= self.MAXQ)
         lazy = [o for o in self.optimizers if o._skip_lazy and o._lazy_handle is not None]
         handles = [o._lazy_handle for o in lazy]
-        if lazy and len(lazy) == len(self.optimizers) and not all(FusedGradScaler.handle_ready(h) for h in handles):
+        cadence = self._cadence(handles)
+        self._resolve(wait=not queued or len(self._queue) >= self.MAXQ or self._ages_out(cadence))
+        # a flag must still be in the scaler's ring when the NEXT scheduler step reads it: at a slow
+        # cadence (a scheduler stepped once per epoch, several optimizers on one scaler) the step
+        # waits for its own flag instead of queueing (one host sync per scheduler step)
+        slow = 2 * cadence + len(self.optimizers) >= _AMP_RING
+        if lazy and len(lazy) == len(self.optimizers) and not slow and \
+                not all(FusedGradScaler.handle_ready(h) for h in handles):
             if self.LIGHT and not args and not kwargs and self._light_ok():
                 s = self.scheduler
                 snap = ("light", s._step_count, s.last_epoch, s._last_lr)

@@ -180,6 +180,7 @@ class StepGraphs:
         self._params = None  # parameter list for the version token (fixed once graphs exist)
         self._dev = None
         self._bcache: dict = {}  # id(batch) -> (batch, tensors, signature, persistent key) of ring slots
+        self._bcache_ring = None  # id of the ring (mark_ring sets) those entries belong to
         self.launch_lists = 0  # captured parts replayed as native launch lists
         self.launch_list_reason = None  # why a part kept hipGraphLaunch replay (first such part)
 
@@ -258,7 +259,14 @@ class StepGraphs:
                 return False
             bsig = _signature(batch)
             pkey = tuple(t.data_ptr() if getattr(t, "_rocket_persistent", False) else 0 for t in tens)
-            if type(batch) is tuple and all(pkey) and len(self._bcache) < 64:
+            if type(batch) is tuple and all(pkey):
+                # entries pin their ring's buffers: a batch from another ring (a recreated loader, a
+                # resumed with_skip loader, another batch size) drops the old ring's entries
+                ring = getattr(tens[0], "_rocket_ring", None)
+                rid = id(ring[0]) if ring is not None else None
+                if rid != self._bcache_ring or len(self._bcache) >= 64:
+                    self._bcache.clear()
+                    self._bcache_ring = rid
                 self._bcache[id(batch)] = (batch, tens, bsig, pkey)
         sync = self._predict_sync()
         sig = (sync, bsig)

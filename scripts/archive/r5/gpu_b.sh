@@ -18,7 +18,7 @@ pmc() {  # name counters cmd...
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc $c -d $O/$n -o run -- "$@" > $O/$n.log 2>&1
 }
 for p in A B C D; do pmc l$p "${!p}" python3 $R/bench.py --steps 30 --warmup 10 || { echo "lenet pmc $p failed"; tail -5 $O/l$p.log; exit 1; }; done
-cd $R && python3 bench/summarize_pmc.py $O/lA $O/lB $O/lC $O/lD --steps 10 --marker mlp3_wgrad_kernel --title "LeNet bs1024 captured step (launch-list replay), PMC, round 5" > gpurun_out/r5_pmc_lenet.md
+cd $R && python3 bench/summarize_pmc.py $O/lA $O/lB $O/lC $O/lD --steps 10 --marker mlp3_wgrad_kernel --title "LeNet bs1024 captured step (launch-list replay), PMC, round 5" > gpurun_out/r5_pmc_lenet_progression.md
 cd /tmp
 for p in A B C D; do pmc r$p "${!p}" python3 $R/bench.py --model resnet50 --steps 3 --warmup 2 || { echo "resnet pmc $p failed"; tail -5 $O/r$p.log; exit 1; }; done
 cd $R && python3 bench/summarize_pmc.py $O/rA $O/rB $O/rC $O/rD --steps 2 --marker sgd_mt_kernel --top 25 --title "ResNet-50 bs256 bf16 captured step, PMC, round 5" > gpurun_out/r5_pmc_resnet50.md
@@ -35,4 +35,4 @@ python3 bench/summarize_trace.py $f --steps 5 --title "ViT-B/16 bs128 fp16 step 
 f=$(find $O/r50 -name "*kernel_trace.csv" | head -1)
 python3 bench/summarize_trace.py $f --steps 5 --marker sgd_mt_kernel --title "ResNet-50 bs256 bf16 step (round 5, HEAD), rocprofv3 kernel trace" > gpurun_out/r5_resnet50_kernels.md
 rm -rf $O/vf16 $O/r50
-head -16 gpurun_out/r5_pmc_lenet.md gpurun_out/r5_pmc_vit_b16.md
+head -16 gpurun_out/r5_pmc_lenet_progression.md gpurun_out/r5_pmc_vit_b16.md

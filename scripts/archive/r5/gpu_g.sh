@@ -20,6 +20,6 @@ D="WRITE_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"
 for p in A B C D; do
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc ${!p} -d $O/l$p -o run -- python3 $R/bench.py --steps 30 --warmup 10 > $O/l$p.log 2>&1 || { echo "lenet pmc $p failed"; tail -5 $O/l$p.log; exit 1; }
 done
-cd $R && python3 bench/summarize_pmc.py $O/lA $O/lB $O/lC $O/lD --steps 10 --marker mlp3_wgrad_kernel --title "LeNet bs1024 captured step (launch-list replay), PMC, round 5 (KeepSmem forward state, LDS-DMA wgrad)" > gpurun_out/r5_pmc_lenet_v2.md
+cd $R && python3 bench/summarize_pmc.py $O/lA $O/lB $O/lC $O/lD --steps 10 --marker mlp3_wgrad_kernel --title "LeNet bs1024 captured step (launch-list replay), PMC, round 5 (KeepSmem forward state, LDS-DMA wgrad)" > gpurun_out/r5_pmc_lenet_progression.md
 rm -rf $O/lA $O/lB $O/lC $O/lD
-cat gpurun_out/r5_pmc_lenet_v2.md
+cat gpurun_out/r5_pmc_lenet_progression.md

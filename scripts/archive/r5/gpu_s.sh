@@ -12,7 +12,7 @@ for p in A B; do
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc ${!p} -d $O/w$p -o run -- python3 $R/bench.py --steps 30 --warmup 10 > $O/w$p.log 2>&1 || { echo "pmc $p failed"; tail -5 $O/w$p.log; exit 1; }
 done
 cd $R
-python3 bench/summarize_pmc.py $O/sA $O/sB --steps 10 --marker mlp3_wgrad_kernel --title "LeNet, forward and backward as separate launches (ROCKET_LENET_SPEC=0), PMC" > gpurun_out/r5_pmc_lenet_split.md || true
-python3 bench/summarize_pmc.py $O/wA $O/wB --steps 10 --marker mlp3_wgrad_kernel --title "LeNet whole-step (default), PMC at HEAD" > gpurun_out/r5_pmc_lenet_v3.md || true
+python3 bench/summarize_pmc.py $O/sA $O/sB --steps 10 --marker mlp3_wgrad_kernel --title "LeNet, forward and backward as separate launches (ROCKET_LENET_SPEC=0), PMC" > gpurun_out/r5_pmc_lenet_progression.md || true
+python3 bench/summarize_pmc.py $O/wA $O/wB --steps 10 --marker mlp3_wgrad_kernel --title "LeNet whole-step (default), PMC at HEAD" > gpurun_out/r5_pmc_lenet_progression.md || true
 rm -rf $O/sA $O/sB $O/wA $O/wB
-cat gpurun_out/r5_pmc_lenet_split.md gpurun_out/r5_pmc_lenet_v3.md
+cat gpurun_out/r5_pmc_lenet_progression.md gpurun_out/r5_pmc_lenet_progression.md

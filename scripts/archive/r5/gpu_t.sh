@@ -3,7 +3,7 @@
 # and the split (ROCKET_LENET_SPEC=0) launches at HEAD
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-RUN=${RUN:-r5t} bash $R/scripts/r5/gpu_h.sh || exit 1
+RUN=${RUN:-r5t} bash $R/scripts/archive/r5/gpu_h.sh || exit 1
 O=$R/gpurun_out/${RUN:-r5t}
 cd /tmp && export TMPDIR=/tmp
 B="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE"

@@ -268,3 +268,84 @@ def test_queued_provisional_steps_with_lagging_flags_match_accelerate():
         assert sch.scheduler.get_last_lr() == ref.get_last_lr()
         assert opt.param_groups[0]["lr"] == ref_opt.param_groups[0]["lr"]
         assert sch.mispredicted >= 3 and sch.provisional >= 10
+
+
+class _RingScaler:
+    """FusedGradScaler's flag ring (runtime/amp.py): update ``seq``'s flag is readable from the time the
+    device publishes it until RING later updates have overwritten its slot; ``_resolve`` waits for the
+    device and, for an overwritten slot, falls back to the LATEST update's flag (the real fallback)."""
+
+    def __init__(self):
+        from rocket_amd.runtime.amp import RING
+
+        self.ring = RING
+        self._seq = 0  # updates launched
+        self.published = 0  # updates the device has finished
+        self.flags = {}
+        self.syncs = 0
+
+    def launch(self, skipped: bool):
+        self._seq += 1
+        self.flags[self._seq] = skipped
+        self.published = self._seq - 1  # the device runs one update behind the host
+
+    def _entry(self, seq):
+        if seq > self.published or self.published - seq >= self.ring:
+            return None
+        return self.flags[seq]
+
+    def _resolve(self, seq):
+        f = self._entry(seq)
+        if f is not None:
+            return f
+        self.syncs += 1
+        self.published = self._seq
+        f = self._entry(seq)
+        return f if f is not None else self.flags[self._seq]
+
+
+def test_per_epoch_scheduler_never_reads_an_overwritten_flag():
+    """a scheduler stepped once per epoch (100 updates per step) must not queue provisional
+    steps whose flags leave the 64-update ring before they are read: the lr sequence equals
+    accelerate's although every epoch's LAST update (the one the scheduler step follows) alternates
+    between kept and skipped."""
+    p = torch.nn.Parameter(torch.zeros(2))
+    opt = torch.optim.SGD([p], lr=1.0)
+    eo = EngineOptimizer(opt, _Eng())
+    sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=3, gamma=0.5), [eo], _Eng())
+    ref_opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(2))], lr=1.0)
+    ref = torch.optim.lr_scheduler.StepLR(ref_opt, step_size=3, gamma=0.5)
+    sc = _RingScaler()
+    last_skipped = [False, True, False, False, True, False, True, True, False, False, False, True]
+    for epoch, sk in enumerate(last_skipped):
+        for i in range(100):
+            sc.launch(sk if i == 99 else False)
+        eo._skip_lazy, eo._lazy_handle = True, (sc, sc._seq)
+        sch.step()
+        if not sk:
+            ref.step()
+        assert opt.param_groups[0]["lr"] == ref_opt.param_groups[0]["lr"], epoch
+        assert len(sch._queue) <= 1
+    sch._resolve()
+    assert sch.scheduler.last_epoch == ref.last_epoch and sch.scheduler.get_last_lr() == ref.get_last_lr()
+
+
+def test_fast_cadence_settles_a_step_before_its_flag_ages_out():
+    """Per-iteration cadence with the device far behind: a queued step whose flag would be overwritten
+    before the next scheduler step is settled (waited for) instead of left to the stale fallback."""
+    p = torch.nn.Parameter(torch.zeros(2))
+    opt = torch.optim.SGD([p], lr=1.0)
+    eo = EngineOptimizer(opt, _Eng())
+    sch = EngineScheduler(torch.optim.lr_scheduler.StepLR(opt, step_size=1000, gamma=0.5), [eo], _Eng())
+    sch.MAXQ = 32
+    sc = _RingScaler()
+    for it in range(200):
+        for _ in range(3):  # three updates per scheduler step (e.g. three optimizers' worth)
+            sc.launch(False)
+        sc.published = max(0, sc._seq - 60)  # the device lags 60 updates: flags land late
+        eo._skip_lazy, eo._lazy_handle = True, (sc, sc._seq)
+        sch.step()
+        for h, _ in sch._queue:
+            assert sc._seq - h[0][1] < sc.ring  # every queued flag is still in the ring
+    sch._resolve()
+    assert sch.scheduler.last_epoch == 200 and sch.mispredicted == 0
