@@ -250,7 +250,13 @@ class Optimizer(Capsule):
             # exact when its gradients are final and local ones are all there is (one replica)
             inner.amp_fold_armed = (engine.sync_gradients and engine.num_processes == 1 and engine.scaler is not None
                                     and _OPT_EPILOGUE and _is_fused_scaler(engine.scaler))
-            if (inner.epilogue_armed or inner.amp_fold_armed) and not getattr(self, "_epi_tagged", False):
+            # W > 1 on the P2P transport: the gradient all-reduce can apply the update in its write-
+            # back instead (DataParallel._reduce_with_update); exact under the same conditions with
+            # the REDUCED gradients as the final ones
+            inner.reduce_epilogue_armed = (engine.sync_gradients and engine.num_processes > 1 and engine.scaler is None
+                                           and _OPT_EPILOGUE)
+            if (inner.epilogue_armed or inner.amp_fold_armed or inner.reduce_epilogue_armed) and \
+                    not getattr(self, "_epi_tagged", False):
                 for g in inner.param_groups:
                     for p in g["params"]:
                         p._rocket_optimizer = inner
@@ -277,6 +283,8 @@ class Optimizer(Capsule):
             inner.epilogue_armed = False
         if getattr(inner, "amp_fold_armed", False):
             inner.amp_fold_armed = False
+        if getattr(inner, "reduce_epilogue_armed", False):
+            inner.reduce_epilogue_armed = False
         scaler = self._accelerator.scaler
         if scaler is not None and self._accelerator.sync_gradients:
             # the skipped-step flag of the replayed update: copied behind it, read only if asked

@@ -29,6 +29,7 @@
 // included, exactly as for an fp16 overflow.  The host reads the error word (a plain host load) on
 // every launch and replay and raises.  The kernel never waits on anything but peer flags.
 #include "rk_common.h"
+#include "optim_common.h"
 
 #include <cstring>
 #include <new>
@@ -61,9 +62,16 @@ __device__ __forceinline__ unsigned load_flag(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Write-back of the plain all-reduce: the averaged gradient goes back in place.
+struct StoreSum {
+  __device__ __forceinline__ void vec(float* data, int64_t j, f32x4 s) const { *(f32x4*)(data + j) = s; }
+  __device__ __forceinline__ void one(float* data, int64_t j, float s) const { data[j] = s; }
+};
+
 // One region b (kChunk floats): stage, signal, wait, reduce.  False when a peer timed out.
-template <int W>
-__device__ __forceinline__ bool p2p_region(const P2PArgs& a, int b, unsigned& s_ep, int& s_timeout) {
+template <int W, class Out = StoreSum>
+__device__ __forceinline__ bool p2p_region(const P2PArgs& a, int b, unsigned& s_ep, int& s_timeout,
+                                           const Out& out = Out{}) {
   const int t = threadIdx.x;
   if (t == 0) {
     s_ep = a.epoch[b] + 1;
@@ -135,7 +143,7 @@ __device__ __forceinline__ bool p2p_region(const P2PArgs& a, int b, unsigned& s_
       f32x4 s = v[u][0];
 #pragma unroll
       for (int r = 1; r < W; ++r) s += v[u][r];
-      *(f32x4*)(a.data + base + (int64_t)(u * kThreads + t) * kVec) = s * a.scale;
+      out.vec(a.data, base + (int64_t)(u * kThreads + t) * kVec, s * a.scale);
     }
   } else {
     for (int64_t j = base + t; j < a.n && j < base + kChunk; j += kThreads) {
@@ -145,7 +153,7 @@ __device__ __forceinline__ bool p2p_region(const P2PArgs& a, int b, unsigned& s_
       float s = v[0];
 #pragma unroll
       for (int r = 1; r < W; ++r) s += v[r];
-      a.data[j] = s * a.scale;
+      out.one(a.data, j, s * a.scale);
     }
   }
   if (t == 0) a.epoch[b] = ep;
@@ -162,6 +170,82 @@ __global__ void __launch_bounds__(kThreads) p2p_allreduce_kernel(P2PArgs a, int 
   __shared__ int s_timeout;
   for (int b = blockIdx.x; b < nregions; b += gridDim.x)
     if (!p2p_region<W>(a, b, s_ep, s_timeout)) return;
+}
+
+// ---------------------------------------------------------------------------------------------
+// All-reduce + AdamW update in one launch (the data-parallel LeNet step at W > 1: backward ->
+// THIS -> next step, instead of backward -> all-reduce -> optimizer).  The reduced gradient of a
+// parameter element is never stored as such: its block applies the update right away (p, m, v,
+// bf16/fp16 shadow, gradient cleared or stored), exactly the arithmetic of the multi-tensor update
+// (rk_opt::adam_update).  Elements of the flat buffer that belong to no segment (16-byte padding,
+// the loss side channel) get the plain average.  Armed by the host only when that is exact: a
+// gradient-sync step, no AMP scaler, an Adam-family optimizer whose every active parameter lies in
+// P2P buckets.  A peer timeout: the timed-out block leaves its elements un-updated and raises the
+// fault guard's found flag, the host raises on the error word (the step is not usable anyway).
+constexpr int kMaxSeg = 32;
+struct P2PUpd {
+  const int64_t* segs;  // [nseg][10]: rk_opt::TensorRec (8 x int64), flat start, 0
+  const rk_opt::AdamHyper* hyper;
+  float* step;
+  unsigned* counter;
+  float* amp;  // AmpSlot block whose found flag skips the update (the fault guard), may be null
+  int nseg, ngroups, zero_grads, advance;
+};
+
+struct UpdOut {
+  const rk_opt::TensorRec* rec;
+  const int64_t* start;
+  const rk_opt::AdamStep* ks;
+  int nseg, zero_grads;
+  float gs;
+  bool skip;
+  __device__ __forceinline__ void one(float* data, int64_t j, float s) const {
+    int q = -1;
+    for (int i = 0; i < nseg; ++i)
+      if (j >= start[i] && j < start[i] + rec[i].n) q = i;
+    if (q < 0 || skip) {  // padding / side channel; a skipped step clears (or keeps) the gradient
+      data[j] = (q >= 0 && zero_grads) ? 0.f : s;
+      return;
+    }
+    const rk_opt::TensorRec& tr = rec[q];
+    const int64_t e = j - start[q];
+    rk_opt::epi_apply(tr, ks[tr.group], e, rk_opt::epi_fetch(tr, e), s * gs, zero_grads);
+  }
+  __device__ __forceinline__ void vec(float* data, int64_t j, f32x4 s) const {
+#pragma unroll
+    for (int k = 0; k < kVec; ++k) one(data, j + k, s[k]);
+  }
+};
+
+template <int W>
+__global__ void __launch_bounds__(kThreads) p2p_allreduce_upd_kernel(P2PArgs a, int nregions, P2PUpd u) {
+  __shared__ unsigned s_ep;
+  __shared__ int s_timeout;
+  __shared__ rk_opt::TensorRec s_rec[kMaxSeg];
+  __shared__ int64_t s_start[kMaxSeg];
+  __shared__ rk_opt::AdamStep s_ks[4];
+  __shared__ float s_cur, s_gs;
+  __shared__ int s_skip;
+  const int t = threadIdx.x;
+  for (int i = t; i < u.nseg * 10; i += kThreads) {
+    const int q = i / 10, f = i % 10;
+    if (f < 8) ((int64_t*)&s_rec[q])[f] = u.segs[i];
+    else if (f == 8) s_start[q] = u.segs[i];
+  }
+  if (t == 0) {
+    s_cur = u.step[0];
+    s_skip = u.amp != nullptr && u.amp[rk_opt::kAmpFound] != 0.f;
+    s_gs = u.amp ? u.amp[rk_opt::kAmpInv] : 1.f;
+  }
+  __syncthreads();
+  if (t < u.ngroups) s_ks[t] = rk_opt::adam_step(u.hyper[t], s_cur + 1.f);
+  __syncthreads();
+  const UpdOut out{s_rec, s_start, s_ks, u.nseg, u.zero_grads, s_gs, s_skip != 0};
+  for (int b = blockIdx.x; b < nregions; b += gridDim.x)
+    if (!p2p_region<W>(a, b, s_ep, s_timeout, out)) break;
+  // every block takes its ticket (a timed-out one too): the last one advances the step counter and
+  // consumes the guard's found flag, as the optimizer launch this one replaces would
+  if (u.advance) rk_opt::advance_step(u.step, u.counter, s_skip != 0, s_cur, u.amp);
 }
 
 struct P2PCtx {
@@ -263,13 +347,8 @@ RK_API int rk_p2p_open(void* ctx, const void* all) {
   return 0;
 }
 
-// data[0:n] <- scale * sum over ranks (in place, stream-ordered, graph-capturable).  16-byte
-// aligned data; n <= cap.
-RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipStream_t s) {
-  auto* c = (P2PCtx*)ctx;
-  if (n <= 0) return 0;
+static int p2p_args(P2PCtx* c, float* data, int64_t n, float scale, P2PArgs& a) {
   if (n > c->cap || ((uintptr_t)data & 15)) return (int)hipErrorInvalidValue;
-  P2PArgs a{};
   for (int r = 0; r < c->world; ++r) {
     if (!c->peer_stage[r]) return (int)hipErrorNotInitialized;
     a.stage[r] = c->peer_stage[r];
@@ -290,6 +369,16 @@ RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipS
   a.timeout_ticks = (uint64_t)(c->timeout_s * (double)kTicksPerSecond);
   a.rank = c->rank;
   a.world = c->world;
+  return 0;
+}
+
+// data[0:n] <- scale * sum over ranks (in place, stream-ordered, graph-capturable).  16-byte
+// aligned data; n <= cap.
+RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipStream_t s) {
+  auto* c = (P2PCtx*)ctx;
+  if (n <= 0) return 0;
+  P2PArgs a{};
+  if (int rc = p2p_args(c, data, n, scale, a)) return rc;
   const int regions = (int)((n + kChunk - 1) / kChunk);
   const int blocks = regions < kMaxGrid ? regions : kMaxGrid;
   switch (c->world) {
@@ -301,6 +390,36 @@ RK_API int rk_p2p_allreduce(void* ctx, float* data, int64_t n, float scale, hipS
     case 6: p2p_allreduce_kernel<6><<<blocks, kThreads, 0, s>>>(a, regions); break;
     case 7: p2p_allreduce_kernel<7><<<blocks, kThreads, 0, s>>>(a, regions); break;
     default: p2p_allreduce_kernel<8><<<blocks, kThreads, 0, s>>>(a, regions); break;
+  }
+  return (int)hipGetLastError();
+}
+
+// The same all-reduce with the Adam/AdamW update applied in its write-back (P2PUpd above).
+// segs: device int64 [nseg][10] (TensorRec, flat start into data, 0), nseg <= 32, segments disjoint
+// and inside [0, n); hyper: AdamHyper[ngroups] (ngroups <= 4); step / counter: the optimizer's
+// device step and ticket counter; amp: its AmpSlot block or null; advance: this launch advances
+// the step (the optimizer's last bucket).
+RK_API int rk_p2p_allreduce_adam(void* ctx, float* data, int64_t n, float scale, const int64_t* segs, int nseg,
+                                 const void* hyper, int ngroups, float* step, unsigned* counter, float* amp,
+                                 int zero_grads, int advance, hipStream_t s) {
+  auto* c = (P2PCtx*)ctx;
+  if (n <= 0) return 0;
+  if (nseg < 0 || nseg > kMaxSeg || (nseg && !segs) || ngroups < 1 || ngroups > 4 || !hyper || !step || !counter)
+    return (int)hipErrorInvalidValue;
+  P2PArgs a{};
+  if (int rc = p2p_args(c, data, n, scale, a)) return rc;
+  P2PUpd u{segs, (const rk_opt::AdamHyper*)hyper, step, counter, amp, nseg, ngroups, zero_grads, advance};
+  const int regions = (int)((n + kChunk - 1) / kChunk);
+  const int blocks = regions < kMaxGrid ? regions : kMaxGrid;
+  switch (c->world) {
+    case 1: p2p_allreduce_upd_kernel<1><<<blocks, kThreads, 0, s>>>(a, regions, u); break;
+    case 2: p2p_allreduce_upd_kernel<2><<<blocks, kThreads, 0, s>>>(a, regions, u); break;
+    case 3: p2p_allreduce_upd_kernel<3><<<blocks, kThreads, 0, s>>>(a, regions, u); break;
+    case 4: p2p_allreduce_upd_kernel<4><<<blocks, kThreads, 0, s>>>(a, regions, u); break;
+    case 5: p2p_allreduce_upd_kernel<5><<<blocks, kThreads, 0, s>>>(a, regions, u); break;
+    case 6: p2p_allreduce_upd_kernel<6><<<blocks, kThreads, 0, s>>>(a, regions, u); break;
+    case 7: p2p_allreduce_upd_kernel<7><<<blocks, kThreads, 0, s>>>(a, regions, u); break;
+    default: p2p_allreduce_upd_kernel<8><<<blocks, kThreads, 0, s>>>(a, regions, u); break;
   }
   return (int)hipGetLastError();
 }

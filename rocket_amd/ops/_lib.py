@@ -144,6 +144,8 @@ KERNEL_SIGS = {
     "rk_p2p_create": (c_int, [c_int, c_int, c_int64, c_void_p, c_void_p]),
     "rk_p2p_open": (c_int, [c_void_p, c_void_p]),
     "rk_p2p_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
+    "rk_p2p_allreduce_adam": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_int, c_void_p, c_int,
+                                      c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "rk_p2p_error": (c_int, [c_void_p]),
     "rk_p2p_set_timeout": (c_int, [c_void_p, ctypes.c_double]),
     "rk_p2p_set_skip": (c_int, [c_void_p, c_void_p, c_void_p]),

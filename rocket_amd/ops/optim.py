@@ -298,6 +298,52 @@ class _FusedBase(torch.optim.Optimizer):
         active = self._active()
         return len(active) == len(params) and {id(p) for _, p in active} == {id(p) for p in params}
 
+    # The same fusion one stage later, for data parallelism: the P2P all-reduce of the gradient
+    # buckets applies the update in its write-back (parallel/p2p.py ``all_reduce_adam_``).  Armed by
+    # the Optimizer capsule on a gradient-sync step of a W > 1 run without an AMP scaler.
+    reduce_epilogue_armed = False
+
+    def reduce_plan(self, flat: torch.Tensor, params) -> Optional[tuple]:
+        """``(segments, ngroups, hyper_ptr, step_ptr, counter_ptr, amp_ptr)`` for a P2P reduce of
+        ``flat`` whose ``params`` (their ``.grad`` are views into ``flat``) are updated in its
+        write-back; None when that is not exact or not supported.  ``segments``: device int64
+        [n, 10] (tensor record, element offset in ``flat``, 0), cached per (flat, table version)."""
+        if not (self.reduce_epilogue_armed and self.KIND == 0 and self._tables is not None and self._gdtype == 0):
+            return None
+        if len(self.param_groups) > 4 or self.amp is not None or self._torch_amp is not None:
+            return None
+        key = (flat.data_ptr(), flat.numel(), self.version, tuple(id(p) for p in params))
+        cache = getattr(self, "_reduce_plans", None)
+        if cache is None:
+            cache = self._reduce_plans = {}
+        hit = cache.get(key)
+        if hit is not None:
+            return hit
+        gidx = {id(p): gi for gi, p in self._active()}
+        base = flat.data_ptr()
+        rows = []
+        for p in params:
+            if id(p) not in gidx or p.grad is None:
+                return None
+            off, rem = divmod(p.grad.data_ptr() - base, 4)
+            if rem or off < 0 or off + p.numel() > flat.numel() or not _same_layout(p.grad, p):
+                return None
+            st = self.state[p]
+            s = [st[k].data_ptr() for k in self.STATE_KEYS]
+            rows.append([p.data_ptr(), p.grad.data_ptr(), s[0], s[1], p.numel(), gidx[id(p)], *self._shadow_ptrs(p),
+                         off, 0])
+        if not rows or len(rows) > 32:
+            return None
+        segs = torch.tensor(rows, dtype=torch.int64).to(self._device)
+        dev = self._device
+        amp = self.guard
+        plan = (segs, len(self.param_groups), self._hyper_dev.data_ptr(), self._step_dev.data_ptr(),
+                _lib.Workspace.get(dev).counter(f"optim_{id(self)}"), _lib.ptr(amp))
+        if len(cache) > 8:
+            cache.clear()
+        cache[key] = plan
+        return plan
+
     def epilogue(self, params) -> Optional[tuple]:
         """``(ngroups, hyper_ptr, step_ptr, counter_ptr, records)`` when ``params`` are exactly this
         optimizer's active parameters and the epilogue is armed; ``records[i]`` is the 8-int64 tensor

@@ -147,6 +147,7 @@ class DataParallel(nn.Module):
         self._reduces = 0
         self._debug = os.environ.get("ROCKET_DEBUG_SYNC", "0") == "1"
         self._launched: List[int] = []
+        self.fused_updates = 0  # captured sync steps whose P2P reduce applied the optimizer update
         # small models: one-shot xGMI all-reduce kernel (graph-capturable) instead of RCCL
         self._p2p = self._make_p2p()
         # native transport: per-bucket all-reduce on a side stream, one join before the optimizer
@@ -346,12 +347,50 @@ class DataParallel(nn.Module):
     def reduce_now(self) -> None:
         """Average every bucket (incl. the side channel) across ranks; stream-ordered, no host wait."""
         self._launched = []
+        if self._p2p is not None and self._reduce_with_update():
+            return
         works = [self._launch(b) for b in self.buckets]
         if self._native is not None:
             self._native.join()
         for w in works:
             if w is not None:
                 w.wait()
+
+    def _reduce_with_update(self) -> bool:
+        """P2P transport, captured sync step: when ONE fused Adam-family optimizer owns exactly the
+        bucketed parameters and has armed its reduce epilogue (``Optimizer.graph_prepare``: sync
+        step, W > 1, no AMP scaler), each bucket's all-reduce applies the update in its write-back
+        and the optimizer's own launch is skipped (``epilogue_done``): the data-parallel LeNet step
+        is then backward -> reduce+update, one launch fewer than reduce -> update."""
+        fused = self.prepare_reduce()
+        if fused is None:
+            return False
+        opt, plans = fused
+        last = len(self.buckets) - 1
+        for i, (b, plan) in enumerate(zip(self.buckets, plans)):
+            if self._debug:
+                self._debug_check_launch(b)
+            self._p2p.all_reduce_adam_(b.flat, 1.0 / self.comm.world, plan, advance=i == last)
+        opt.epilogue_done = True
+        opt.reduce_epilogue_armed = False
+        self.fused_updates += 1
+        return True
+
+    def prepare_reduce(self):
+        """``(optimizer, per-bucket plans)`` of the reduce-with-update path, or None.  The plans
+        (device segment tables) are built on first use and cached by the optimizer: the graph
+        executor calls this before capturing a step, so no table is uploaded inside a capture."""
+        opt = None
+        for b in self.buckets:
+            for p in b.params:
+                o = getattr(p, "_rocket_optimizer", None)
+                if o is None or not getattr(o, "reduce_epilogue_armed", False) or (opt is not None and o is not opt):
+                    return None
+                opt = o
+        if opt is None or {id(p) for _, p in opt._active()} != {id(p) for b in self.buckets for p in b.params}:
+            return None
+        plans = [opt.reduce_plan(b.flat, b.params) for b in self.buckets]
+        return None if any(pl is None for pl in plans) else (opt, plans)
 
     def side_slot(self, n: int = 1) -> torch.Tensor:
         """``n`` fp32 slots that are averaged together with the gradients on every sync step."""

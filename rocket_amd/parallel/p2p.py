@@ -146,6 +146,20 @@ class P2PAllReduce:
         self.launches += 1
         self.check()  # a plain load of a host-mapped word: reports a timeout of any earlier launch
 
+    def all_reduce_adam_(self, flat: torch.Tensor, scale: float, plan: tuple, advance: bool = True,
+                         zero_grads: bool = True) -> None:
+        """``all_reduce_`` whose write-back applies the Adam/AdamW update of the parameters whose
+        gradients live in ``flat`` (``plan`` = :meth:`rocket_amd.ops.optim._FusedBase.reduce_plan`);
+        ``advance``: this launch advances the optimizer's step counter (its last bucket)."""
+        if flat.dtype != torch.float32 or not flat.is_contiguous() or flat.numel() > self.cap:
+            raise ValueError("p2p all-reduce takes a contiguous fp32 buffer within the capacity")
+        segs, ngroups, hyper, step, counter, amp = plan
+        _lib.check(_lib.kernels().rk_p2p_allreduce_adam(
+            self._ctx, flat.data_ptr(), flat.numel(), float(scale), segs.data_ptr(), segs.shape[0], hyper, ngroups,
+            step, counter, amp, int(zero_grads), int(advance), _lib.stream_ptr(flat.device)), "rk_p2p_allreduce_adam")
+        self.launches += 1
+        self.check()
+
     def check(self) -> None:
         """Raise if a launch ever timed out waiting for a peer.  Its timed-out blocks left their
         gradients un-reduced, and raised the fault guard's found flag, so the optimizer launch of

@@ -477,6 +477,8 @@ class StepGraphs:
         v.host_sync_buffers = v.sync and rep is not None and rep.broadcast_buffers and not overlap
         if v.host_sync_buffers:
             rep.sync_buffers()
+        if inline:
+            rep.prepare_reduce()  # device tables of a reduce-with-update step: uploaded before capture
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
         cap = Attributes(attrs)

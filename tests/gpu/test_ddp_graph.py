@@ -12,7 +12,11 @@ rehearses the multi-GPU code paths on the single-GPU box, one per ``DataParallel
   branches run alongside the rest of backward (the structure the native RCCL reducer captures on
   real multi-GPU nodes), with the rank-0 BatchNorm buffer broadcast captured in the forward —
 
-plus side-channel loss averaging in all of them, for LeNet and a BatchNorm ResNet-18.
+plus side-channel loss averaging in all of them, for LeNet and a BatchNorm ResNet-18; and the
+overlap capture failing on ONE rank (``overlap_fail``: rank 1's first overlapped capture raises after
+it has claimed the pending batch and set the fused optimizer's step flags): both ranks must drop to
+split mode together, with the side effects of the discarded capture undone (runtime/graphs.py
+``_capture``), and train exactly like the eager run.
 """
 
 import json
@@ -33,7 +37,26 @@ def _free_port():
 
 
 _ENV = {"split": dict(ROCKET_P2P="0"), "inline": dict(ROCKET_P2P="force"),
-        "overlap": dict(ROCKET_P2P="0", ROCKET_DP_COMM="p2p")}
+        "overlap": dict(ROCKET_P2P="0", ROCKET_DP_COMM="p2p"),
+        "overlap_fail": dict(ROCKET_P2P="0", ROCKET_DP_COMM="p2p")}
+
+
+def _inject_capture_failure(rank, injected):
+    """Rank 1's first overlapped capture runs to the end (every side effect of a capture happens) and
+    then raises, as a rank-local capture error would."""
+    from rocket_amd.runtime import graphs as G
+
+    orig = G.StepGraphs._capture_inner
+
+    def capture_inner(self, attrs, tens, pend):
+        v = orig(self, attrs, tens, pend)
+        rep = self._replica()
+        if rank == 1 and not injected and rep is not None and rep.capture_mode == "overlap" and v.sync:
+            injected.append(1)
+            raise RuntimeError("injected overlapped-capture failure")
+        return v
+
+    G.StepGraphs._capture_inner = capture_inner
 
 
 def _worker(rank, world, port, out_dir, mode, model):
@@ -53,8 +76,17 @@ def _worker(rank, world, port, out_dir, mode, model):
             if attrs.looper.state.loss is not None:
                 self.losses.append(attrs.looper.state.loss)
 
+    injected = []
+    if mode == "overlap_fail":
+        _inject_capture_failure(rank, injected)
     res = {}
-    for capture in (False, True):
+    from rocket_amd.core import objectives as _obj
+
+    variants = [(False, True), (True, True)]
+    if mode == "inline":
+        variants.append((True, False))  # captured, the all-reduce NOT fused with the AdamW update
+    for capture, fuse in variants:
+        _obj._OPT_EPILOGUE = fuse
         dev = torch.device("cuda", 0)
         g = torch.Generator(device=dev).manual_seed(3)
         bs = 128 if model == "lenet" else 32
@@ -81,7 +113,9 @@ def _worker(rank, world, port, out_dir, mode, model):
             destroy_process_group_after_launch=False,
         ).launch()
         torch.cuda.synchronize()
-        res[str(capture)] = dict(
+        rep = mod._module
+        res[str(capture) if fuse else "unfused"] = dict(
+            fused=getattr(rep, "fused_updates", 0),
             losses=[float(v) for v in rec.losses],
             w=float(sum(p.detach().double().sum() for p in net.parameters())),
             bufs=float(sum(b.detach().double().sum() for b in net.buffers())),
@@ -89,6 +123,7 @@ def _worker(rank, world, port, out_dir, mode, model):
             parts=(mod._graphs.parts if mod._graphs is not None else 0),
             mode=getattr(mod._module, "capture_mode", None),
             reason=(mod._graphs.disabled_reason if mod._graphs is not None else None),
+            injected=len(injected),
         )
     with open(os.path.join(out_dir, f"r{rank}.json"), "w") as fh:
         json.dump(res, fh)
@@ -99,7 +134,8 @@ def _worker(rank, world, port, out_dir, mode, model):
 
 
 @pytest.mark.parametrize("mode,model", [("split", "lenet"), ("inline", "lenet"), ("overlap", "lenet"),
-                                        ("split", "resnet18"), ("overlap", "resnet18")])
+                                        ("split", "resnet18"), ("overlap", "resnet18"),
+                                        ("overlap_fail", "lenet")])
 def test_ddp_graph_two_ranks(tmp_path, mode, model):
     port = _free_port()
     mp.start_processes(_worker, args=(2, port, str(tmp_path), mode, model), nprocs=2, start_method="spawn",
@@ -111,7 +147,12 @@ def test_ddp_graph_two_ranks(tmp_path, mode, model):
     for rank in range(2):
         e, g = r[rank]["False"], r[rank]["True"]
         assert g["replays"] > 0 and g["reason"] == "released", g
-        assert g["mode"] == mode and g["parts"] == (2 if mode == "split" else 1), g
+        if mode == "overlap_fail":
+            # both ranks dropped to split mode together; only rank 1 failed its capture
+            assert g["mode"] == "split" and g["parts"] == 2, g
+            assert g["injected"] == (1 if rank == 1 else 0), g
+        else:
+            assert g["mode"] == mode and g["parts"] == (2 if mode == "split" else 1), g
         assert len(e["losses"]) == len(g["losses"]) > 0
         for a, b in zip(e["losses"], g["losses"]):
             assert abs(a - b) <= tol_l * max(1.0, abs(a)), (e["losses"], g["losses"])
@@ -123,6 +164,13 @@ def test_ddp_graph_two_ranks(tmp_path, mode, model):
     # reported loss is the cross-rank mean
     assert abs(r[0]["True"]["w"] - r[1]["True"]["w"]) < 1e-6 * max(1.0, abs(r[0]["True"]["w"]))
     assert r[0]["True"]["losses"] == pytest.approx(r[1]["True"]["losses"], rel=1e-6)
+    if mode == "inline":
+        # the P2P reduce applied the AdamW update in its write-back on every captured sync step,
+        # and that equals all-reduce -> optimizer launch bit for bit (same sums, same update math)
+        for rank in range(2):
+            g, u = r[rank]["True"], r[rank]["unfused"]
+            assert g["fused"] > 0 and u["fused"] == 0, (g, u)
+            assert g["w"] == u["w"] and g["losses"] == u["losses"], (g, u)
     if model != "lenet":
         # BatchNorm statistics are rank 0's at the start of every synchronised forward (torch DDP's
         # broadcast_buffers semantics), then each rank folds in its own batch: after the last step
