@@ -48,6 +48,9 @@ from rocket_amd.ops.mgemm import mgemm, pick_split
 #                  256x256 / 256x128 tiles, buffer-load LDS-DMA ring; forward + bias, K-major-weight
 #                  dgrad, split-K wgrad with the bias gradient from the same launch); the only route
 #                  with fp16 operands (the GELU runs as its own streaming kernel)
+#   x5             forward and input gradient on the persistent 256x256 kernel of
+#                  native/kernels/xgemm5.hip (bias inside the MFMAs; the input gradient reads a per-step
+#                  transposed bf16 weight copy), weight gradients as in lib
 MODE = os.environ.get("ROCKET_VIT_GEMM", "lib")
 # The transformer MLP's two GEMMs whose neighbours are streaming GELU passes run on the native 256x256
 # kernel (native/kernels/xgemm4.hip) with the GELU fused into their epilogues, beside any MODE:
@@ -92,12 +95,34 @@ def _x_split(M: int, N: int, K: int) -> int:
     return best[1]
 
 
+def _x5_shape(N: int, K: int) -> bool:
+    """Output width / reduction depth rk_xgemm5 takes (N % 128, K % 64, K >= 320)."""
+    return N % 128 == 0 and K % 64 == 0 and K >= 320
+
+
+def _x5(a: torch.Tensor, b: torch.Tensor, bias, M: int, N: int, K: int) -> torch.Tensor:
+    """C = a b^T (+ bias) on rk_xgemm5: a [M, K], b [N, K] bf16, C bf16."""
+    c = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    _lib.check(_lib.kernels().rk_xgemm5(a.data_ptr(), K, b.data_ptr(), K, c.data_ptr(), N, _lib.dtype_code(c),
+                                        _lib.ptr(bias), M, N, K, _lib.stream_ptr(a.device)), "rk_xgemm5")
+    return c
+
+
+def _transposed16(w16: torch.Tensor) -> torch.Tensor:
+    """w16^T as a dense 16-bit copy (one launch): the input-gradient GEMM's K-contiguous B operand."""
+    N, K = w16.shape
+    wt = torch.empty(K, N, dtype=w16.dtype, device=w16.device)
+    _lib.check(_lib.kernels().rk_transpose16(w16.data_ptr(), N, K, wt.data_ptr(), _lib.stream_ptr(w16.device)),
+               "rk_transpose16")
+    return wt
+
+
 def _lib_fwd(K: int) -> bool:
-    return MODE in ("lib", "libw", "libd") or (MODE == "hybrid" and K < 2048)
+    return MODE in ("lib", "libw", "libd", "x5") or (MODE == "hybrid" and K < 2048)
 
 
 def _lib_dgrad(N_in: int) -> bool:
-    return MODE in ("lib", "libw") or (MODE == "hybrid" and N_in > 2048)
+    return MODE in ("lib", "libw", "x5") or (MODE == "hybrid" and N_in > 2048)
 
 
 def _ok(x: torch.Tensor, N: int, K: int) -> bool:
@@ -125,6 +150,8 @@ def _linear_fwd(x2: torch.Tensor, w16: torch.Tensor, bias: torch.Tensor, b16: to
         y = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
         mgemm(x2, w16, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, tile=_x_tile(M, N, x2.dtype))
         return y
+    if MODE == "x5" and x2.dtype == torch.bfloat16 and _x5_shape(N, K):
+        return _x5(x2, w16, bias, M, N, K)
     if _lib_fwd(K):
         return torch.addmm(b16, x2, w16.t())
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
@@ -142,6 +169,8 @@ def _linear_dgrad(dy2: torch.Tensor, w16: torch.Tensor, gelu_of: torch.Tensor | 
         dx = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
         mgemm(dy2, w16, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, b_kmaj=True, tile=_x_tile(M, K, dy2.dtype))
         return dx
+    if MODE == "x5" and dy2.dtype == torch.bfloat16 and _x5_shape(K, N) and gelu_of is None:
+        return _x5(dy2, _transposed16(w16), None, M, K, N)
     if _lib_dgrad(K):
         assert gelu_of is None
         return dy2 @ w16
@@ -157,7 +186,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
     engine provides them (returns None for those), else returned as new tensors."""
     M, N = dy.shape
     K = x.shape[1]
-    if MODE in ("lib", "libd"):
+    if MODE in ("lib", "libd", "x5"):
         return lib_param_grads(dy, x, weight, bias, need_w, need_b)
     direct = (not need_w or _direct(weight)) and (not need_b or _direct(bias))
     if direct:
@@ -361,7 +390,7 @@ class _MMlpFn(torch.autograd.Function):
             # gelu'(z) and fc1's bias gradient in fc2's input-gradient GEMM epilogue
             dz, db1 = _x4_dgrad_gelu(dy2, w2_16, z, b1 if need_b1 else None)
             need_b1 = False
-        elif MODE == "lib" and need_b1:
+        elif MODE in ("lib", "x5") and need_b1:
             # GELU backward and fc1's bias gradient in one pass over the [tokens, hidden] gradient
             dz, db1 = _gelu_bwd_bias(_linear_dgrad(dy2, w2_16), z, b1)
             need_b1 = False
@@ -391,7 +420,7 @@ def _native(module: nn.Linear, x: torch.Tensor) -> bool:
     dt = _cdtype()
     # fp16: the library routes (hipBLASLt fp16 GEMMs beside the fp16 attention / LayerNorm / GELU
     # kernels) and the xgemm route; the mgemm routes are bf16-only
-    return (x.is_cuda and native_route() and (dt == torch.bfloat16 or (dt == torch.float16 and MODE in ("x", "lib")))
+    return (x.is_cuda and native_route() and (dt == torch.bfloat16 or (dt == torch.float16 and MODE in ("x", "lib", "x5")))
             and module.weight.dtype == torch.float32 and module.weight.is_contiguous()
             and _ok(x, module.out_features, module.in_features))
 
