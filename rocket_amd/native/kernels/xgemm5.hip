@@ -194,11 +194,13 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   const uint32_t c_lo = (uint32_t)(uintptr_t)g.C, c_hi = (uint32_t)((uintptr_t)g.C >> 32);
   const i32x4_t crs = {(int)c_lo, (int)(c_hi & 0xffff), (int)cb, 0x00020000};
 #define X5_STV(q, v)                                                                              \
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3"                               \
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 1"                   \
                :                                                                                   \
                : "v"(v), "v"(c_vb[(q) >> 3]), "s"(crs), "i"((((q) >> 1) & 3) * 64 + ((q) & 1) * 32) \
                : "memory")
 #define X5_ST(q) X5_STV(q, cst[(q) - X5_NIM])
+  // (s_nop 1 ends the store: a dwordx4 store reads its data registers a cycle late, and hipcc,
+  // which does not model the asm, may overwrite them with the very next VALU instruction)
 
   // 16 MFMAs of one k16 step on (Fa, Fb), the 8 reads of the next step interleaved (one per two
   // MFMAs); D' = B-fragment x A-fragment: lane holds column m = l32, rows n in its 16 registers
@@ -228,12 +230,15 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     step(FIRSTc, bc<true>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
     if constexpr (SB >= 0) { X5_ST(SB); X5_ST(SB + 1); }
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
     step(bc<false>{}, bc<true>{}, A1, B1, A0, B0, ra(st, 2), rb(st, 2));
     if constexpr (SB >= 0) X5_ST(SB + 2);
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
     step(bc<false>{}, bc<true>{}, A0, B0, A1, B1, ra(st, 3), rb(st, 3));
     if constexpr (SB >= 0) X5_ST(SB + 3);
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
     // boundary: k-tile q + 1 landed (the only VMEM ops after its DMA: this k-tile's stores)
     if (q + 1 < S) {
       if constexpr (SB >= 0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -245,12 +250,14 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     const int st1 = (q + 1) & 1;
     step(bc<false>{}, bc<!LAST>{}, A1, B1, A0, B0, ra(st1, 0), rb(st1, 0));
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
   };
   // the next k-tile's step-0 fragments, read after an epilogue (not held through the packing)
   auto rd0 = [&](int q) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) rd(A0, B0, ra(q & 1, 0), rb(q & 1, 0), k);
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
   };
 
   // bias as a rank-2 update inside the MFMAs: the tile's first 16 MFMAs multiply a fragment holding
@@ -285,6 +292,7 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     asm volatile("ds_read_b32 %0, %1 offset:384" : "=v"(b[3]) : "v"(ba));
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
     const uint32_t one2 = h == 0 ? 0x3F803F80u : 0u;  // bf16 (1, 1)
     const bf16x8 ones = __builtin_bit_cast(bf16x8, w4_t{one2, 0u, 0u, 0u});
     bf16x8 bfr[4];
@@ -294,6 +302,9 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
       const uint32_t wv = h == 0 ? pack2<BF16>(hi, b[j] - hi) : 0u;
       bfr[j] = __builtin_bit_cast(bf16x8, w4_t{wv, 0u, 0u, 0u});
     }
+    // VALU-written MFMA operands: the wait states hipcc does not insert before an asm MFMA
+    asm volatile("s_nop 1" ::"v"(bfr[0]), "v"(bfr[1]), "v"(bfr[2]), "v"(bfr[3]), "v"(ones));
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -331,7 +342,7 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     ktile(bc<false>{}, ic<-1>{}, bc<true>{}, q++);  // U >= 5 (host check)
     // epilogue: pack this tile (accumulators + bias -> 16-bit, lane halves swapped so each store
     // covers 16 B); row blocks 0-1 go out at once, 2-3 under the next tile's first k-tiles
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs' results
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs' results (16-pass XDL)
     int tm, tn;
     grouped_tile(pos + ti * G, tiles_m, tiles_n, 4, tm, tn);
     const int c_m0 = tm * X5_BM + 128 * wm;

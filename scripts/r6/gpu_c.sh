@@ -1,0 +1,8 @@
+#!/bin/bash
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r6c; rm -rf $O; mkdir -p $O
+cd $R && export TMPDIR=/tmp
+timeout -k 10 200 python bench/x5_diag.py > $O/diag.log 2>&1 || { tail -20 $O/diag.log; exit 1; }
+cut -c1-600 $O/diag.log
+bash scripts/r6/gpu_b.sh
