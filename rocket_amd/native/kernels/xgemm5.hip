@@ -116,30 +116,44 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   };
   if (my > 0) iss_tile(0);
   // one descriptor per operand and k-tile (rows past M / N read as zeros: the VGPR offset is
-  // range-checked); the row part of each instruction's offset is added at the instruction to an
-  // opaque copy of the lane part, so the 16 sums are not hoisted into 16 live registers
-  auto dma_op = [&](const char* base, int64_t bytes, int64_t ld2, char* lds, const uint32_t(&voff)[2]) {
+  // range-checked).  dma_begin(q) forms them for k-tile q (a k-tile past the stream gets an empty
+  // descriptor: its 16 instructions still issue, so every vmcnt count stays static, and only write
+  // zeros into a stage nobody reads any more); dma_one(k) issues instruction k (0-7 A, 8-15 B),
+  // its row offset added at the instruction to an opaque copy of the lane part (no 16 hoisted sums).
+  __amdgpu_buffer_rsrc_t d_ra, d_rb;
+  char* d_st = smem;
+  auto dma_begin = [&](int q) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const int n = (int)(bytes < 0 ? 0 : (bytes > 0x7fffffff ? 0x7fffffff : bytes));
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, n, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < X5_NI; ++i) {
-      const int row0 = 64 * w + 8 * i;
-      uint32_t vo = voff[i & 1];
-      asm volatile("" : "+v"(vo));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + row0 * X5_ROWB), 16, vo + (uint32_t)(row0 * ld2),
-                                               0, 0, 0);
-    }
-#endif
-  };
-  auto dma_next = [&](int q) {  // k-tile q of the stream into stage q & 1
-    char* st = smem + (q & 1) * X5_STAGE;
-    dma_op(ia + iss_k * X5_ROWB, ia_n - iss_k * X5_ROWB, g.lda * 2, st, va);
-    dma_op(ib + iss_k * X5_ROWB, ib_n - iss_k * X5_ROWB, g.ldb * 2, st + X5_OPB, vb);
-    if (++iss_k == U) {
+    const bool real = q < S;
+    d_st = smem + (q & 1) * X5_STAGE;
+    auto clampn = [](int64_t b) { return (int)(b < 0 ? 0 : (b > 0x7fffffff ? 0x7fffffff : b)); };
+    const char* pa = real ? ia + iss_k * X5_ROWB : (const char*)g.A;
+    const char* pb = real ? ib + iss_k * X5_ROWB : (const char*)g.B;
+    d_ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pa), (short)0, real ? clampn(ia_n - iss_k * X5_ROWB) : 0,
+                                             0x00020000);
+    d_rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pb), (short)0, real ? clampn(ib_n - iss_k * X5_ROWB) : 0,
+                                             0x00020000);
+    if (real && ++iss_k == U) {
       iss_k = 0;
       if (++iss_i < my) iss_tile(iss_i);
     }
+#endif
+  };
+  auto dma_one = [&](int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int op = k >> 3, i = k & 7;
+    const int row0 = 64 * w + 8 * i;
+    uint32_t vo = op ? vb[i & 1] : va[i & 1];
+    asm volatile("" : "+v"(vo));
+    vo += (uint32_t)(row0 * (op ? g.ldb : g.lda) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? d_rb : d_ra, (lds_void*)(d_st + op * X5_OPB + row0 * X5_ROWB), 16,
+                                             vo, 0, 0, 0);
+#endif
+  };
+  auto dma_next = [&](int q) {  // a whole k-tile at once (prologue)
+    dma_begin(q);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dma_one(k);
   };
 
   // ---- fragment reads: 32x32x16 operand of rows r0 .. r0+31 at k16 step s: lane reads row
@@ -166,16 +180,18 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     return v + (uint32_t)(st * X5_STAGE) + bdelta;
   };
 #define X5_RD(dst, a, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(a), "i"(off))
+  // read k of a step's batch, in the order the next step's MFMAs (i-major) first need them:
+  // B0 A0 B1 B2 B3 A1 A2 A3 (so counted lgkmcnt waits let a step start on the early fragments)
   auto rd = [&](bf16x8 (&Fa)[4], bf16x8 (&Fb)[4], uint32_t a, uint32_t b, int k) {
     switch (k) {  // immediate offsets must be literals
-      case 0: X5_RD(Fa[0], a, 0); break;
-      case 1: X5_RD(Fb[0], b, 0); break;
-      case 2: X5_RD(Fa[1], a, 4096); break;
-      case 3: X5_RD(Fb[1], b, 4096); break;
-      case 4: X5_RD(Fa[2], a, 8192); break;
-      case 5: X5_RD(Fb[2], b, 8192); break;
-      case 6: X5_RD(Fa[3], a, 12288); break;
-      default: X5_RD(Fb[3], b, 12288); break;
+      case 0: X5_RD(Fb[0], b, 0); break;
+      case 1: X5_RD(Fa[0], a, 0); break;
+      case 2: X5_RD(Fb[1], b, 4096); break;
+      case 3: X5_RD(Fb[2], b, 8192); break;
+      case 4: X5_RD(Fb[3], b, 12288); break;
+      case 5: X5_RD(Fa[1], a, 4096); break;
+      case 6: X5_RD(Fa[2], a, 8192); break;
+      default: X5_RD(Fa[3], a, 12288); break;
     }
   };
 
@@ -204,16 +220,28 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
 
   // 16 MFMAs of one k16 step on (Fa, Fb), the 8 reads of the next step interleaved (one per two
   // MFMAs); D' = B-fragment x A-fragment: lane holds column m = l32, rows n in its 16 registers
-  auto step = [&](auto FIRSTc, auto RDc, const bf16x8 (&Fa)[4], const bf16x8 (&Fb)[4], bf16x8 (&Na)[4],
+  // DM: one DMA instruction of the k-tile begun by dma_begin after every MFMA (the library's spread
+  // schedule: the 16 instructions never queue ahead of a fragment read as one burst)
+  auto step = [&](auto FIRSTc, auto RDc, auto DMc, const bf16x8 (&Fa)[4], const bf16x8 (&Fb)[4], bf16x8 (&Na)[4],
                   bf16x8 (&Nb)[4], uint32_t a, uint32_t b) {
-    constexpr bool FIRST = decltype(FIRSTc)::value, RD = decltype(RDc)::value;
+    constexpr bool FIRST = decltype(FIRSTc)::value, RD = decltype(RDc)::value, DM = decltype(DMc)::value;
+    // counted waits on the previous step's batch (issued one per two MFMAs of that step, in rd()'s
+    // order): MFMAs 0-3 need reads 0-4, MFMA 4 read 5, MFMA 8 read 6, MFMA 12 read 7; this step's
+    // own reads (after MFMAs 1, 3, 5, ...) are younger and in the count when RD
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        if (j == 0) {
+          if (i == 0) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+          else if (i == 1) { if constexpr (RD) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory"); else asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory"); }
+          else if (i == 2) { if constexpr (RD) asm volatile("s_waitcnt lgkmcnt(5)" ::: "memory"); else asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory"); }
+          else { if constexpr (RD) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+        }
         if constexpr (FIRST) mfma32_0(acc[i][j], Fb[j], Fa[i]);
         else mfma32(acc[i][j], Fb[j], Fa[i]);
         if constexpr (RD) if (j & 1) rd(Na, Nb, a, b, 2 * i + (j >> 1));
+        if constexpr (DM) dma_one(4 * i + j);
       }
   };
   constexpr int kWaitLgkm0 = 0xC07F;
@@ -227,16 +255,13 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     constexpr int SB = decltype(SBc)::value;
     constexpr bool LAST = decltype(LASTc)::value;  // the tile's last k-tile: step 3 reads nothing
     const int st = q & 1;
-    step(FIRSTc, bc<true>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
+    step(FIRSTc, bc<true>{}, bc<false>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
     if constexpr (SB >= 0) { X5_ST(SB); X5_ST(SB + 1); }
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-    __builtin_amdgcn_sched_barrier(0);
-    step(bc<false>{}, bc<true>{}, A1, B1, A0, B0, ra(st, 2), rb(st, 2));
+    step(bc<false>{}, bc<true>{}, bc<false>{}, A1, B1, A0, B0, ra(st, 2), rb(st, 2));
     if constexpr (SB >= 0) X5_ST(SB + 2);
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-    __builtin_amdgcn_sched_barrier(0);
-    step(bc<false>{}, bc<true>{}, A0, B0, A1, B1, ra(st, 3), rb(st, 3));
+    step(bc<false>{}, bc<true>{}, bc<false>{}, A0, B0, A1, B1, ra(st, 3), rb(st, 3));
     if constexpr (SB >= 0) X5_ST(SB + 3);
+    // every wave's reads of this stage are done before the barrier that frees it for the DMA
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
     // boundary: k-tile q + 1 landed (the only VMEM ops after its DMA: this k-tile's stores)
@@ -246,11 +271,9 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (q + 2 < S) dma_next(q + 2);
+    dma_begin(q + 2);  // issued spread over step 3 (past the stream: an empty descriptor)
     const int st1 = (q + 1) & 1;
-    step(bc<false>{}, bc<!LAST>{}, A1, B1, A0, B0, ra(st1, 0), rb(st1, 0));
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-    __builtin_amdgcn_sched_barrier(0);
+    step(bc<false>{}, bc<!LAST>{}, bc<true>{}, A1, B1, A0, B0, ra(st1, 0), rb(st1, 0));
   };
   // the next k-tile's step-0 fragments, read after an epilogue (not held through the packing)
   auto rd0 = [&](int q) {
@@ -396,6 +419,8 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   // the last tile's stores (for a block with no tile: dropped, the offsets are past the records)
 #pragma unroll
   for (int k = X5_NIM; k < X5_NST; ++k) X5_ST(k);
+  // every LDS-DMA (the empty ones past the stream included) lands before the block's LDS is freed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #undef X5_ST
 #undef X5_RD
 }
