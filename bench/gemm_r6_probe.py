@@ -67,7 +67,15 @@ def main():
             err = ((y.float() - rf).abs().max() / rf.abs().max()).item()
             rec[f"{tag}_rel_err"] = round(err, 5) if err == err else "nan"
         flop = 2.0 * m * n * k
-        engines = {"lib": lambda: torch.addmm(b16, x, w.t()), "x5": x5(True), "x5_nobias": x5(False), "x4": x4}
+        def shaped(sh):
+            def f():
+                lib.rk_xgemm5_set_shape(sh)
+                x5(True)()
+                lib.rk_xgemm5_set_shape(0)
+            return f
+
+        engines = {"lib": lambda: torch.addmm(b16, x, w.t()), "x5": x5(True), "x5_nobias": x5(False), "x4": x4,
+                   "x5_256x256": shaped(1), "x5_128x256": shaped(2), "x5_256x128": shaped(3)}
         times = {t: [] for t in engines}
         for _ in range(a.rounds):
             for tag, fn in engines.items():

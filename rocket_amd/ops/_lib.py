@@ -44,6 +44,7 @@ KERNEL_SIGS = {
                          c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "rk_xgemm_set_dbg": (c_int, [c_int]),
     "rk_xgemm4_set_dbg": (c_int, [c_int]),
+    "rk_xgemm5_set_shape": (c_int, [c_int]),
     "rk_xgemm5": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_int, c_int, c_int,
                           c_void_p]),
     "rk_xgemm4_set_trace": (c_int, [c_void_p]),

@@ -31,10 +31,18 @@ def _run(a, b, c, bias, M, N, K, ldc=None):
     return rc
 
 
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "256x256", "128x256", "256x128"])
+def x5_shape(request):
+    lib = _lib().kernels()
+    lib.rk_xgemm5_set_shape(request.param)
+    yield request.param
+    lib.rk_xgemm5_set_shape(0)
+
+
 @pytest.mark.parametrize("M,N,K", [(300, 256, 320), (777, 384, 448), (2056, 768, 768), (25216, 2304, 768),
-                                   (4100, 3072, 768), (1999, 768, 3072)])
+                                   (4100, 3072, 768), (1999, 768, 3072), (25216, 768, 768)])
 @pytest.mark.parametrize("with_bias", [True, False])
-def test_xgemm5_fwd(M, N, K, with_bias):
+def test_xgemm5_fwd(M, N, K, with_bias, x5_shape):
     torch.manual_seed(M + N + K)
     a, b = _r(M, K), _r(N, K)
     bias = torch.randn(N, device="cuda") if with_bias else None
@@ -48,7 +56,7 @@ def test_xgemm5_fwd(M, N, K, with_bias):
     assert _rel(c, ref) < 5e-3, _rel(c, ref)
 
 
-def test_xgemm5_fp16_out_and_wide_ldc():
+def test_xgemm5_fp16_out_and_wide_ldc(x5_shape):
     torch.manual_seed(5)
     M, N, K, ldc = 1030, 512, 640, 520
     a, b = _r(M, K), _r(N, K)
@@ -61,7 +69,7 @@ def test_xgemm5_fp16_out_and_wide_ldc():
     assert torch.isnan(c[:, N:]).all()  # the columns past N are never written
 
 
-def test_xgemm5_bias_exact_to_2e16():
+def test_xgemm5_bias_exact_to_2e16(x5_shape):
     """A zero product isolates the bias path: C = bf16(b_hi + b_lo) must equal bf16(b)."""
     M, N, K = 512, 256, 320
     a = torch.zeros(M, K, dtype=torch.bfloat16, device="cuda")
