@@ -70,7 +70,8 @@ def test_xgemm5_fp16_out_and_wide_ldc(x5_shape):
 
 
 def test_xgemm5_bias_exact_to_2e16(x5_shape):
-    """A zero product isolates the bias path: C = bf16(b_hi + b_lo) must equal bf16(b)."""
+    """A zero product isolates the bias path: C = bf16(b_hi + b_lo) with b_hi + b_lo within 2^-16 of
+    b, so C is bf16(b) except where b sits that close to a rounding midpoint (then one ulp off)."""
     M, N, K = 512, 256, 320
     a = torch.zeros(M, K, dtype=torch.bfloat16, device="cuda")
     b = _r(N, K)
@@ -78,7 +79,9 @@ def test_xgemm5_bias_exact_to_2e16(x5_shape):
     c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     assert _run(a, b, c, bias, M, N, K) == 0
     torch.cuda.synchronize()
-    assert torch.equal(c, bias.to(torch.bfloat16).expand(M, N))
+    want = bias.to(torch.bfloat16).expand(M, N)
+    assert (c == want).float().mean().item() > 0.99
+    assert ((c.float() - bias).abs() <= bias.abs() * 2.0 ** -8).all()
 
 
 def test_xgemm5_rejects_unsupported_shapes():
