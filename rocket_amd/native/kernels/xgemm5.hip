@@ -128,6 +128,7 @@ struct X5Args {
   const float* bias;
   int64_t lda, ldb, ldc;
   int M, N, K, c_dt;
+  int dbg;  // ablation (timing only, results wrong): bit 0 no in-loop DMA, 1 no barrier, 2 no in-loop fragment reads, 3 no lgkm waits
 };
 
 template <int CDT, bool HASB, int FM, int FN>
@@ -286,14 +287,14 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
       constexpr int m = decltype(Mc)::value;
       constexpr int i = m / FN, j = m % FN;
       constexpr int wt = SC::wait_before(m, RD);
-      if constexpr (wt >= 0) wait_lgkm<wt>();
+      if constexpr (wt >= 0) if (!(g.dbg & 8)) wait_lgkm<wt>();
       if constexpr (FIRST) mfma32_0(acc[i][j], Fb[j], Fa[i]);
       else mfma32(acc[i][j], Fb[j], Fa[i]);
-      if constexpr (RD && SC::read_after(m) >= 0) rd(Na, Nb, a, b, ic<SC::read_after(m)>{});
+      if constexpr (RD && SC::read_after(m) >= 0) if (!(g.dbg & 4)) rd(Na, Nb, a, b, ic<SC::read_after(m)>{});
       if constexpr (DM) {  // DMA instructions d with d * Q / NDMA == m
 #pragma unroll
         for (int d = 0; d < NDMA; ++d)
-          if (d * SC::Q / NDMA == m) dma_one(d);
+          if (d * SC::Q / NDMA == m && !(g.dbg & 1)) dma_one(d);
       }
     };
     sfor<SC::Q>(one);
@@ -330,7 +331,7 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    __builtin_amdgcn_s_barrier();
+    if (!(g.dbg & 2)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     dma_begin(q + 2);  // issued spread over step 3 (past the stream: an empty descriptor)
     const int st1 = (q + 1) & 1;
@@ -488,12 +489,14 @@ int x5_launch(int fm, int fn, int grid, const X5Args& g, hipStream_t s) {
 }
 
 int g_x5_shape = 0;  // diagnostics: force a tile shape (0 auto, 1 256x256, 2 128x256, 3 256x128)
+int g_x5_dbg = 0;    // diagnostics: X5Args::dbg of later launches
 
 }  // namespace
 
-// Diagnostics: force the tile shape of later rk_xgemm5 calls (0 = automatic).
+// Diagnostics: force the tile shape of later rk_xgemm5 calls (0 = automatic); ablation bits.
 RK_API int rk_xgemm5_set_shape(int s) {
-  g_x5_shape = s;
+  g_x5_shape = s & 0xff;
+  g_x5_dbg = s >> 8;
   return 0;
 }
 
@@ -533,7 +536,7 @@ RK_API int rk_xgemm5(const void* a, int64_t lda, const void* b, int64_t ldb, voi
     if (cost(256, 128) < best - 1e-9) { fm = 4; fn = 2; }
   }
   const int grid = std::min(tiles(64 * fm, 64 * fn), ncu);
-  X5Args g{(const uint16_t*)a, (const uint16_t*)b, c, bias, lda, ldb, ldc, M, N, K, c_dt};
+  X5Args g{(const uint16_t*)a, (const uint16_t*)b, c, bias, lda, ldb, ldc, M, N, K, c_dt, g_x5_dbg};
   if (c_dt == F16) return bias ? x5_launch<F16, true>(fm, fn, grid, g, s) : x5_launch<F16, false>(fm, fn, grid, g, s);
   return bias ? x5_launch<BF16, true>(fm, fn, grid, g, s) : x5_launch<BF16, false>(fm, fn, grid, g, s);
 }
