@@ -41,8 +41,9 @@ using namespace rk;
 
 namespace {
 
-constexpr int X5_BK = 64, X5_NT = 256;
-constexpr int X5_ROWB = X5_BK * 2;  // 128-byte image rows
+constexpr int X5_BK = 32, X5_NT = 256;  // a "unit": 32-deep k-slice, two k16 steps
+constexpr int X5_ROWB = X5_BK * 2;      // 64-byte image rows
+constexpr int X5_NS = 4;                // LDS ring: 4 units (3 in flight)
 
 template <int I>
 using ic = std::integral_constant<int, I>;
@@ -128,7 +129,7 @@ struct X5Args {
   const float* bias;
   int64_t lda, ldb, ldc;
   int M, N, K, c_dt;
-  int dbg;  // ablation (timing only, results wrong): bit 0 no in-loop DMA, 1 no barrier, 2 no in-loop fragment reads, 3 no lgkm waits
+  int dbg;  // unused (the round-6 ablation bits are gone: runtime branches inside the MFMA code made the allocator spill)
 };
 
 template <int CDT, bool HASB, int FM, int FN>
@@ -136,50 +137,48 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   constexpr int BM = 64 * FM, BN = 64 * FN;          // block tile
   constexpr int OPA = BM * X5_ROWB, OPB = BN * X5_ROWB;  // operand images per stage
   constexpr int STAGE = OPA + OPB;
-  constexpr int NIA = 2 * FM, NIB = 2 * FN;           // DMA instructions per wave per operand
+  constexpr int NIA = FM, NIB = FN;                   // DMA instructions per wave per operand and unit
   constexpr int NDMA = NIA + NIB;
   constexpr int NST = 2 * FM * FN;                    // 16-byte stores per wave per tile
   constexpr int NIM = NST / 2;                        // issued at the epilogue (rows i < FM / 2)
-  constexpr int NPK = NST - NIM;                      // kept packed, issued in the next tile's quad
-  constexpr int SPK = NPK / 4;                        // per k-tile of that quad
+  constexpr int NPK = NST - NIM;                      // kept packed, issued in the next tile's first 4 units
+  constexpr int SPK = NPK / 4;                        // per unit of those
   using SC = X5Sched<FM, FN>;
   // 2-stage ring + one 1-KiB bias row per wave (one __shared__ object: see the guide's trap 4(a))
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * 1024];
+  __shared__ __attribute__((aligned(1024))) char smem[X5_NS * STAGE + 4 * 1024];
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const int total = tiles_m * tiles_n;
   const int G = gridDim.x;
   const int pos = xcd_remap(blockIdx.x, G);
   const int my = pos < total ? (total - pos + G - 1) / G : 0;
   const int U = g.K / X5_BK;
-  const int S = my * U;  // k-tiles in this block's stream
+  const int S = my * U;  // units in this block's stream
   const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = w >> 1, wn = w & 1;
 
-  // ---- DMA (xgemm4's lane pattern): lane l of a 1-KiB piece lands at image row l/8, slot l%8
-  uint32_t va[2], vb[2];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int row = 8 * p + (lane >> 3);
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
-    va[p] = (uint32_t)((lane >> 3) * g.lda * 2 + c * 16);
-    vb[p] = (uint32_t)((lane >> 3) * g.ldb * 2 + c * 16);
-  }
+  // ---- DMA: lane l of a 1-KiB piece (16 rows x 64 B) lands at image row l/4, slot l%4, i.e. holds
+  // source chunk (l%4) ^ rswz(row); pieces start at 16-row boundaries, so rswz(row) depends on the
+  // lane only: one per-lane offset per operand
+  const int drow = lane >> 2;
+  const uint32_t va = (uint32_t)(drow * g.lda * 2 + (((lane & 3) ^ rswz<32>(drow)) * 16));
+  const uint32_t vb = (uint32_t)(drow * g.ldb * 2 + (((lane & 3) ^ rswz<32>(drow)) * 16));
   // issue cursor: tile of the next DMA and its k-tile
   int iss_i = 0, iss_k = 0;
   const char *ia = nullptr, *ib = nullptr;
-  int64_t ia_n = 0, ib_n = 0;
+  int ia_n = 0, ib_n = 0;  // bytes from the tile's first row to the operand's end (clamped to 2^31 - 1)
   auto iss_tile = [&](int i) {
     int tm, tn;
     grouped_tile(pos + i * G, tiles_m, tiles_n, 4, tm, tn);
     ia = (const char*)g.A + (int64_t)tm * BM * g.lda * 2;
     ib = (const char*)g.B + (int64_t)tn * BN * g.ldb * 2;
-    ia_n = ((int64_t)g.M - tm * BM) * g.lda * 2;
-    ib_n = ((int64_t)g.N - tn * BN) * g.ldb * 2;
+    const int64_t an = ((int64_t)g.M - tm * BM) * g.lda * 2, bn = ((int64_t)g.N - tn * BN) * g.ldb * 2;
+    ia_n = (int)(an > 0x7fffffff ? 0x7fffffff : an);
+    ib_n = (int)(bn > 0x7fffffff ? 0x7fffffff : bn);
   };
   if (my > 0) iss_tile(0);
-  // one descriptor per operand and k-tile (rows past M / N read as zeros: the VGPR offset is
-  // range-checked).  dma_begin(q) forms them for k-tile q (a k-tile past the stream gets an empty
+  // one descriptor per operand and unit (rows past M / N read as zeros: the VGPR offset is
+  // range-checked).  dma_begin(q) forms them for unit q (a unit past the stream gets an empty
   // descriptor: its instructions still issue, so every vmcnt count stays static, and only write
   // zeros into a stage nobody reads any more); dma_one(k) issues instruction k (A first, then B),
   // its row offset added at the instruction to an opaque copy of the lane part (no hoisted sums).
@@ -188,14 +187,12 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   auto dma_begin = [&](int q) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const bool real = q < S;
-    d_st = smem + (q & 1) * STAGE;
-    auto clampn = [](int64_t b) { return (int)(b < 0 ? 0 : (b > 0x7fffffff ? 0x7fffffff : b)); };
+    d_st = smem + (q & (X5_NS - 1)) * STAGE;
     const char* pa = real ? ia + iss_k * X5_ROWB : (const char*)g.A;
     const char* pb = real ? ib + iss_k * X5_ROWB : (const char*)g.B;
-    d_ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pa), (short)0, real ? clampn(ia_n - iss_k * X5_ROWB) : 0,
-                                             0x00020000);
-    d_rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pb), (short)0, real ? clampn(ib_n - iss_k * X5_ROWB) : 0,
-                                             0x00020000);
+    const int na = real ? max(ia_n - iss_k * X5_ROWB, 0) : 0, nb = real ? max(ib_n - iss_k * X5_ROWB, 0) : 0;
+    d_ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pa), (short)0, na, 0x00020000);
+    d_rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pb), (short)0, nb, 0x00020000);
     if (real && ++iss_k == U) {
       iss_k = 0;
       if (++iss_i < my) iss_tile(iss_i);
@@ -206,33 +203,34 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const bool opb = k >= NIA;
     const int i = opb ? k - NIA : k;
-    const int row0 = (opb ? 16 * FN : 16 * FM) * w + 8 * i;  // wave w stages a quarter of each image
-    uint32_t vo = opb ? vb[i & 1] : va[i & 1];
+    const int row0 = (opb ? 16 * FN : 16 * FM) * w + 16 * i;  // wave w stages a quarter of each image
+    uint32_t vo = opb ? vb : va;
     asm volatile("" : "+v"(vo));
     vo += (uint32_t)(row0 * (opb ? g.ldb : g.lda) * 2);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(opb ? d_rb : d_ra, (lds_void*)(d_st + (opb ? OPA : 0) + row0 * X5_ROWB),
                                              16, vo, 0, 0, 0);
 #endif
   };
-  auto dma_next = [&](int q) {  // a whole k-tile at once (prologue)
+  auto dma_next = [&](int q) {  // a whole unit at once (prologue)
     dma_begin(q);
 #pragma unroll
     for (int k = 0; k < NDMA; ++k) dma_one(k);
   };
 
-  // ---- fragment reads: 32x32x16 operand of rows r0 .. r0+31 at k16 step s: lane reads row
-  // r0 + l32, chunk 2s + h (slot ^ ((l32 >> 1) & 7)); fragment i = +i * 4096 (32 rows) immediate
+  // ---- fragment reads: 32x32x16 operand of rows r0 .. r0+31 at k16 step s (0, 1) of a unit: lane
+  // reads row r0 + l32, chunk 2s + h at slot chunk ^ rswz(row) (64-B rows: four rows share a bank
+  // row, rswz spreads rows 4 apart over the four slots: conflict-free); fragment i = +i * 2048
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const lds_void*)smem;
-  const int fsw = (l32 >> 1) & 7;
-  // per-lane part of step s's address (A image, stage 0); B and stage 1 differ by wave-uniform
-  // amounts added per step (4 VGPRs instead of 16)
-  uint32_t la[4];
+  const int fsw = rswz<32>(l32);
+  // per-lane part of step s's address (A image, stage 0); B and the other stages differ by
+  // wave-uniform amounts added per step
+  uint32_t la[2];
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+  for (int s = 0; s < 2; ++s)
     la[s] = lds0 + wm * 32 * FM * X5_ROWB + (uint32_t)(l32 * X5_ROWB + (((2 * s + h) ^ fsw) * 16));
   const uint32_t bdelta = (uint32_t)(OPA + (wn * 32 * FN - wm * 32 * FM) * X5_ROWB);
   // (the base goes through an empty asm so the sums are formed at each use, not hoisted out of
-  // the loop into 16 live registers)
+  // the loop into live registers)
   auto ra = [&](int st, int s) {
     uint32_t v = la[s];
     asm volatile("" : "+v"(v));
@@ -249,8 +247,8 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     constexpr int k = decltype(Kc)::value;
     if constexpr (k == 0) X5_RD(Fb[0], b, 0);
     else if constexpr (k == 1) X5_RD(Fa[0], a, 0);
-    else if constexpr (k <= FN) X5_RD(Fb[k - 1], b, (k - 1) * 4096);
-    else X5_RD(Fa[k - FN], a, (k - FN) * 4096);
+    else if constexpr (k <= FN) X5_RD(Fb[k - 1], b, (k - 1) * 2048);
+    else X5_RD(Fa[k - FN], a, (k - FN) * 2048);
   };
 
   f32x16 acc[FM][FN];
@@ -282,64 +280,60 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   // the next step (RD) and, in step 3 (DM), the k-tile's DMA instructions interleaved
   auto step = [&](auto FIRSTc, auto RDc, auto DMc, const bf16x8 (&Fa)[FM], const bf16x8 (&Fb)[FN],
                   bf16x8 (&Na)[FM], bf16x8 (&Nb)[FN], uint32_t a, uint32_t b) {
-    constexpr bool FIRST = decltype(FIRSTc)::value, RD = decltype(RDc)::value, DM = decltype(DMc)::value;
+    constexpr bool FIRST = decltype(FIRSTc)::value, RD = decltype(RDc)::value;
+    constexpr int DM = decltype(DMc)::value;  // 0 none, 1 / 2: the first / second half of a unit's DMA
     auto one = [&](auto Mc) {
       constexpr int m = decltype(Mc)::value;
       constexpr int i = m / FN, j = m % FN;
       constexpr int wt = SC::wait_before(m, RD);
-      if constexpr (wt >= 0) if (!(g.dbg & 8)) wait_lgkm<wt>();
+      if constexpr (wt >= 0) wait_lgkm<wt>();
       if constexpr (FIRST) mfma32_0(acc[i][j], Fb[j], Fa[i]);
       else mfma32(acc[i][j], Fb[j], Fa[i]);
-      if constexpr (RD && SC::read_after(m) >= 0) if (!(g.dbg & 4)) rd(Na, Nb, a, b, ic<SC::read_after(m)>{});
-      if constexpr (DM) {  // DMA instructions d with d * Q / NDMA == m
+      if constexpr (RD && SC::read_after(m) >= 0) rd(Na, Nb, a, b, ic<SC::read_after(m)>{});
+      if constexpr (DM > 0) {  // the half's DMA instructions d with d * Q / NH == m
+        constexpr int NH = NDMA / 2;
 #pragma unroll
-        for (int d = 0; d < NDMA; ++d)
-          if (d * SC::Q / NDMA == m && !(g.dbg & 1)) dma_one(d);
+        for (int d = 0; d < NH; ++d)
+          if (d * SC::Q / NH == m) dma_one(d + (DM - 1) * NH);
       }
     };
     sfor<SC::Q>(one);
   };
   constexpr int kWaitLgkm0 = 0xC07F;
 
-  // one k-tile q.  FIRST: the tile's first k-tile (its MFMAs start the accumulators with C = 0).
-  // SB >= 0: the k-tile issues the previous tile's stores SB .. SB + SPK - 1 over steps 0..2 (static
-  // indices: a peeled quad of k-tiles issues them all, after which the packed tile is dead, so it
-  // is never live across the k-loop).  Step 3's reads always go out (past the stream's end they
-  // re-read a stage nobody uses): no branch around MFMA code.
-  auto ktile = [&](auto FIRSTc, auto SBc, auto LASTc, int q) {
+  // one unit q (two k16 steps).  FIRST: the tile's first unit (its MFMAs start the accumulators with
+  // C = 0).  SB >= 0: the unit issues the previous tile's stores SB .. SB + SPK - 1 (static indices: a
+  // peeled quad of units issues them all, after which the packed tile is dead, so it is never live
+  // across the k-loop).  LAST: the tile's last unit, whose step 1 reads nothing.
+  //   step 0: MFMAs || reads of step 1 (this stage) || second half of unit q + 3's DMA
+  //   lgkmcnt(0) (this stage fully read) + vmcnt (unit q + 1 landed) + ONE barrier
+  //   step 1: MFMAs || reads of step 0 of unit q + 1 || first half of unit q + 4's DMA, into this
+  //           unit's stage (freed by the barrier)
+  // A unit's DMA is issued over two steps of two different units and has two more units to land.
+  auto unit = [&](auto FIRSTc, auto SBc, auto LASTc, int q) {
     constexpr int SB = decltype(SBc)::value;
-    constexpr bool LAST = decltype(LASTc)::value;  // the tile's last k-tile: step 3 reads nothing
-    const int st = q & 1;
-    step(FIRSTc, bc<true>{}, bc<false>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
+    constexpr bool LAST = decltype(LASTc)::value;
+    const int st = q & (X5_NS - 1);
+    step(FIRSTc, bc<true>{}, ic<2>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
     if constexpr (SB >= 0) {
-      X5_ST(SB);
-      if constexpr (SPK > 2) X5_ST(SB + 1);
+#pragma unroll
+      for (int k = 0; k < SPK; ++k) X5_ST(SB + k);
     }
-    step(bc<false>{}, bc<true>{}, bc<false>{}, A1, B1, A0, B0, ra(st, 2), rb(st, 2));
-    if constexpr (SB >= 0) X5_ST(SB + (SPK > 2 ? 2 : 1));
-    step(bc<false>{}, bc<true>{}, bc<false>{}, A0, B0, A1, B1, ra(st, 3), rb(st, 3));
-    if constexpr (SB >= 0 && SPK > 2) X5_ST(SB + 3);
-    // every wave's reads of this stage are done before the barrier that frees it for the DMA
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
-    // boundary: k-tile q + 1 landed (the only VMEM ops after its DMA: this k-tile's stores)
-    if (q + 1 < S) {
-      if constexpr (SB >= 0) {
-        if constexpr (SPK == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    if (!(g.dbg & 2)) __builtin_amdgcn_s_barrier();
+    // unit q + 1 landed: after its last DMA instruction came units q + 2 and q + 3 (2 NDMA
+    // instructions; stores in between only make this wait longer)
+    if constexpr (NDMA == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    dma_begin(q + 2);  // issued spread over step 3 (past the stream: an empty descriptor)
-    const int st1 = (q + 1) & 1;
-    step(bc<false>{}, bc<!LAST>{}, bc<true>{}, A1, B1, A0, B0, ra(st1, 0), rb(st1, 0));
+    dma_begin(q + 4);  // past the stream: an empty descriptor
+    const int st1 = (q + 1) & (X5_NS - 1);
+    step(bc<false>{}, bc<!LAST>{}, ic<1>{}, A1, B1, A0, B0, ra(st1, 0), rb(st1, 0));
   };
   // the next k-tile's step-0 fragments, read after an epilogue (not held through the packing)
   auto rd0 = [&](int q) {
-    const uint32_t a = ra(q & 1, 0), b = rb(q & 1, 0);
+    const uint32_t a = ra(q & (X5_NS - 1), 0), b = rb(q & (X5_NS - 1), 0);
     sfor<SC::R>([&](auto Kc) { rd(A0, B0, a, b, Kc); });
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
@@ -348,7 +342,7 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   // bias: each wave DMAs the tile's bias row (up to 256 floats) into its own 1-KiB LDS slot a tile
   // ahead (one VMEM instruction in the in-order stream: landed by the second k-tile's boundary
   // wait) and reads its lane's FN values from there (inline asm: no compiler-inserted vmcnt waits)
-  const uint32_t bslot = lds0 + 2 * STAGE + w * 1024;
+  const uint32_t bslot = lds0 + X5_NS * STAGE + w * 1024;
   auto load_bias = [&](int ti) {
     if constexpr (HASB) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -358,7 +352,7 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
         const int left = (g.N - tn * BN) * 4;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(g.bias + tn * BN), (short)0, left, 0x00020000);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(smem + 2 * STAGE + w * 1024), 16,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(smem + X5_NS * STAGE + w * 1024), 16,
                                                  (uint32_t)(lane * 16), 0, 0, 0);
       }
 #endif
@@ -395,36 +389,36 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   };
 
   if (S > 0) {
-    load_bias(0);  // before both DMAs: landed once k-tile 0 has
+    load_bias(0);  // before the DMAs: landed once unit 0 has
     dma_next(0);
-    if (S > 1) {
-      dma_next(1);
-      if constexpr (NDMA == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    dma_next(1);
+    dma_next(2);
+    dma_begin(3);  // unit 3's first half now, its second half in unit 0's step 0 (steady state)
+#pragma unroll
+    for (int k = 0; k < NDMA / 2; ++k) dma_one(k);
+    if constexpr (NDMA == 8) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     rd0(0);
   }
 
-  // U >= 5 (host check): the first four k-tiles of every tile carry the previous tile's stores
+  // U >= 10 (host check): the first four units of every tile carry the previous tile's stores
   int q = 0;
   for (int ti = 0; ti < my; ++ti) {
     if (ti > 0) rd0(q);
     if constexpr (HASB) {
       bias_mfmas();
       load_bias(ti + 1);
-      ktile(bc<false>{}, ic<NIM>{}, bc<false>{}, q++);
+      unit(bc<false>{}, ic<NIM>{}, bc<false>{}, q++);
     } else {
-      ktile(bc<true>{}, ic<NIM>{}, bc<false>{}, q++);
+      unit(bc<true>{}, ic<NIM>{}, bc<false>{}, q++);
     }
-    ktile(bc<false>{}, ic<NIM + SPK>{}, bc<false>{}, q++);
-    ktile(bc<false>{}, ic<NIM + 2 * SPK>{}, bc<false>{}, q++);
-    ktile(bc<false>{}, ic<NIM + 3 * SPK>{}, bc<false>{}, q++);
-    for (int kt = 4; kt < U - 1; ++kt) ktile(bc<false>{}, ic<-1>{}, bc<false>{}, q++);
-    ktile(bc<false>{}, ic<-1>{}, bc<true>{}, q++);
+    unit(bc<false>{}, ic<NIM + SPK>{}, bc<false>{}, q++);
+    unit(bc<false>{}, ic<NIM + 2 * SPK>{}, bc<false>{}, q++);
+    unit(bc<false>{}, ic<NIM + 3 * SPK>{}, bc<false>{}, q++);
+    for (int kt = 4; kt < U - 1; ++kt) unit(bc<false>{}, ic<-1>{}, bc<false>{}, q++);
+    unit(bc<false>{}, ic<-1>{}, bc<true>{}, q++);
     // epilogue: pack this tile (accumulators -> 16-bit, lane halves swapped so each store covers
     // 16 B); the first half of the rows goes out at once, the rest under the next tile's quad
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs' results (16-pass XDL)
@@ -507,7 +501,7 @@ RK_API int rk_xgemm5_set_shape(int s) {
 RK_API int rk_xgemm5(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int c_dt,
                      const float* bias, int M, int N, int K, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
-  if (K < 5 * X5_BK || K % X5_BK || N % 128 || ldc % 8 || c_dt == F32 || ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16 ||
+  if (K < 320 || K % 64 || N % 128 || ldc % 8 || c_dt == F32 || ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16 ||
       (lda * 2) % 16 || (ldb * 2) % 16)
     return (int)hipErrorInvalidValue;
   if ((int64_t)256 * lda * 2 >= (1ll << 31) || (int64_t)256 * ldb * 2 >= (1ll << 31) ||
