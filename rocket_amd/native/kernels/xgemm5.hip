@@ -421,7 +421,12 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     unit(bc<false>{}, ic<-1>{}, bc<true>{}, q++);
     // epilogue: pack this tile (accumulators -> 16-bit, lane halves swapped so each store covers
     // 16 B); the first half of the rows goes out at once, the rest under the next tile's quad
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last MFMAs' results (16-pass XDL)
+    // the last MFMAs' results (16-pass XDL) before any accumulator read.  The sched_barrier keeps
+    // hipcc from hoisting an accumulator read above the nops (or above the last MFMAs, which it
+    // does not know write late: fragment (0, 0), done 7 MFMAs early, was read too soon otherwise)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     int tm, tn;
     grouped_tile(pos + ti * G, tiles_m, tiles_n, 4, tm, tn);
     const int c_m0 = tm * BM + 32 * FM * wm;
