@@ -25,7 +25,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops.activation import attention_qkv
-from rocket_amd.ops.linear import LibLinear, PatchEmbed
+from rocket_amd.ops.linear import PatchEmbed
 from rocket_amd.ops.mlinear import MLinear, MMlp
 from rocket_amd.ops.norm import FusedLayerNorm
 
@@ -90,7 +90,7 @@ class VisionTransformer(nn.Module):
         self.pos_embed = nn.Parameter(torch.zeros(1, n + 1, dim))
         self.blocks = nn.ModuleList([Block(dim, heads, mlp_ratio) for _ in range(depth)])
         self.norm = FusedLayerNorm(dim, eps=1e-6)
-        self.head = LibLinear(dim, num_classes)  # nn.Linear; column-sum bias gradient on the GPU
+        self.head = MLinear(dim, num_classes)  # nn.Linear; the ViT GEMM route (ROCKET_VIT_GEMM) runs it too
         nn.init.trunc_normal_(self.pos_embed, std=0.02)
         nn.init.trunc_normal_(self.cls_token, std=0.02)
         for m in self.modules():

@@ -379,7 +379,13 @@ class _PatchEmbedFn(torch.autograd.Function):
                                                   B, C, H, W, k, _lib.stream_ptr(x.device)), "rk_patchify")
         else:
             p = x.to(w16.dtype).reshape(B, C, gh, k, gw, k).permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * k * k)
-        y = torch.addmm(b16, p, w16.reshape(w16.shape[0], -1).t())
+        from rocket_amd.ops import mlinear as _ml
+
+        w2d = w16.reshape(w16.shape[0], -1)
+        if _ml.MODE == "x5" and p.dtype == torch.bfloat16 and _ml._x5_shape(w2d.shape[0], w2d.shape[1]):
+            y = _ml._x5(p, w2d, bias, p.shape[0], w2d.shape[0], w2d.shape[1])  # bias inside the MFMAs
+        else:
+            y = torch.addmm(b16, p, w2d.t())
         ctx.save_for_backward(p)
         ctx.params = (weight, bias)
         return y.view(B, gh * gw, -1)
@@ -394,7 +400,12 @@ class _PatchEmbedFn(torch.autograd.Function):
             dy2 = dy2.to(p.dtype)
         dy2 = dy2.contiguous()
         w2 = _FlatParam(weight)
-        dw, db = lib_param_grads(dy2, p, w2, bias, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        from rocket_amd.ops import mlinear as _ml
+
+        if _ml.MODE == "x5" and dy2.dtype == torch.bfloat16:  # native split-K wgrad + bias grad
+            dw, db = _ml._wgrad(dy2, p, w2, bias, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        else:
+            dw, db = lib_param_grads(dy2, p, w2, bias, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return None, (dw.view_as(weight) if dw is not None else None), db, None, None, None
 
 

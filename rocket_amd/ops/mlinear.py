@@ -48,9 +48,11 @@ from rocket_amd.ops.mgemm import mgemm, pick_split
 #                  256x256 / 256x128 tiles, buffer-load LDS-DMA ring; forward + bias, K-major-weight
 #                  dgrad, split-K wgrad with the bias gradient from the same launch); the only route
 #                  with fp16 operands (the GELU runs as its own streaming kernel)
-#   x5             forward and input gradient on the persistent 256x256 kernel of
-#                  native/kernels/xgemm5.hip (bias inside the MFMAs; the input gradient reads a per-step
-#                  transposed bf16 weight copy), weight gradients as in lib
+#   x5             forward and input gradient on the persistent kernel of native/kernels/xgemm5.hip
+#                  (bias inside the MFMAs; the input gradient reads a per-step transposed bf16 weight
+#                  copy), products it does not take (N % 128, K < 320: the classifier head) on mgemm;
+#                  weight gradients on mgemm (split-K over the tokens, bias gradient from the same
+#                  launch) - no library GEMM anywhere
 MODE = os.environ.get("ROCKET_VIT_GEMM", "lib")
 # The transformer MLP's two GEMMs whose neighbours are streaming GELU passes run on the native 256x256
 # kernel (native/kernels/xgemm4.hip) with the GELU fused into their epilogues, beside any MODE:
@@ -118,11 +120,11 @@ def _transposed16(w16: torch.Tensor) -> torch.Tensor:
 
 
 def _lib_fwd(K: int) -> bool:
-    return MODE in ("lib", "libw", "libd", "x5") or (MODE == "hybrid" and K < 2048)
+    return MODE in ("lib", "libw", "libd") or (MODE == "hybrid" and K < 2048)
 
 
 def _lib_dgrad(N_in: int) -> bool:
-    return MODE in ("lib", "libw", "x5") or (MODE == "hybrid" and N_in > 2048)
+    return MODE in ("lib", "libw") or (MODE == "hybrid" and N_in > 2048)
 
 
 def _ok(x: torch.Tensor, N: int, K: int) -> bool:
@@ -186,7 +188,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
     engine provides them (returns None for those), else returned as new tensors."""
     M, N = dy.shape
     K = x.shape[1]
-    if MODE in ("lib", "libd", "x5"):
+    if MODE in ("lib", "libd"):
         return lib_param_grads(dy, x, weight, bias, need_w, need_b)
     direct = (not need_w or _direct(weight)) and (not need_b or _direct(bias))
     if direct:
