@@ -60,7 +60,7 @@ def main():
                                      stream), "rk_xgemm4")
 
         rec = {"case": name, "M": m, "N": n, "K": k}
-        for tag, fn, rf in (("x5", x5(True), ref), ("x5_nobias", x5(False), ref - bias), ("x4", x4, ref)):
+        for tag, fn, rf in (("x5", x5(True), ref), ("x5_nobias", x5(False), ref - bias)):
             y.fill_(float("nan"))
             fn()
             torch.cuda.synchronize()
@@ -74,8 +74,9 @@ def main():
                 lib.rk_xgemm5_set_shape(0)
             return f
 
-        engines = {"lib": lambda: torch.addmm(b16, x, w.t()), "x5": x5(True), "x5_nobias": x5(False), "x4": x4,
-                   "x5_256x256": shaped(1), "x5_128x256": shaped(2), "x5_256x128": shaped(3)}
+        engines = {"lib": lambda: torch.addmm(b16, x, w.t()), "x5": x5(True), "x5_nobias": x5(False),
+                   "x5_256x256": shaped(1), "x5_128x256": shaped(2), "x5_256x128": shaped(3),
+                   "w8_256x256": shaped(4), "w8_128x256": shaped(5), "w8_256x128": shaped(6)}
         times = {t: [] for t in engines}
         for _ in range(a.rounds):
             for tag, fn in engines.items():

@@ -9,9 +9,13 @@
 // * persistent: one block per CU walks its tiles pos, pos + G, ... (XCD-aware remap + grouped
 //   order); the LDS-DMA k-tile stream runs ACROSS tiles, so the next tile's first two k-tiles are
 //   already landing while the current one finishes (no per-tile prologue);
-// * 32x32x16 MFMAs, 4 waves (2 x 2), each wave FM x FN fragments of 32 x 32 (all its accumulators in
-//   the accumulator registers: 256 at 4 x 4).  One k16 step needs only FM + FN fragments (4 VGPRs
-//   each); two fragment sets leave room for the finished tile PACKED to 16-bit in VGPRs;
+// * 32x32x16 MFMAs, WM x WN waves, each FM x FN fragments of 32 x 32 (accumulators in the
+//   accumulator registers).  Two layouts per tile size: 4 waves (2 x 2, one per SIMD, 4 x 4
+//   fragments at 256 x 256) and 8 waves (two per SIMD, 4 x 2 fragments at 256 x 256).  A wave's
+//   vector-memory instructions stall its own issue for tens of cycles each (the LDS-DMA pieces: with
+//   them removed the 4-wave loop ran 27% faster, and register-path loads cost the same); with two
+//   waves per SIMD the partner's MFMAs fill those gaps.  One k16 step needs FM + FN fragments (4
+//   VGPRs each); two fragment sets leave room for the finished tile PACKED to 16-bit in VGPRs;
 // * epilogue = pack only (accumulators -> 16-bit, lane halves swapped with permlane32 so every store
 //   is 16 B per lane, T21).  The first half of the wave's rows is stored at once; the second half
 //   stays packed and is stored over the next tile's first four k-tiles, as inline-asm buffer
@@ -24,14 +28,14 @@
 //   256-wide tiles would leave the last round of CUs mostly idle (ViT's N = 768 products: 297
 //   tiles on 256 CUs).
 //
-// Per k-tile (64 deep, 2-stage LDS ring, image as xgemm4: [rows][64] bf16 per operand, 16-byte chunk
-// c of row r at c ^ ((r >> 1) & 7)):
-//   step s = 0, 1, 2: FM FN MFMAs on fragment set s & 1  ||  the FM + FN reads of step s + 1 into the
-//                     other set, ordered by first use, with counted lgkmcnt waits (+ the previous
-//                     tile's pending stores in the first four k-tiles);
-//   boundary        : lgkmcnt(0); vmcnt(#stores since) = k-tile q + 1 landed; ONE barrier;
-//   step 3          : MFMAs || reads of step 0 of k-tile q + 1  ||  the DMA of k-tile q + 2 into this
-//                     k-tile's stage, one instruction between MFMAs (never a burst).
+// Per unit (32 deep; 4-stage LDS ring; image [rows][32] bf16 per operand, 16-byte chunk c of row r
+// at c ^ rswz(r)); a unit's DMA is split in two parts issued in two different units' steps:
+//   step 0   : FM FN MFMAs on fragment set 0  ||  the FM + FN reads of step 1 (front-loaded, ordered
+//              by first use, counted lgkmcnt waits)  ||  second part of unit q + 3's DMA
+//              (+ the previous tile's pending stores in the first four units);
+//   boundary : lgkmcnt(0); vmcnt(2 NDMA) = unit q + 1 landed; ONE barrier;
+//   step 1   : MFMAs on set 1  ||  reads of step 0 of unit q + 1  ||  first part of unit q + 4's DMA
+//              into this unit's stage (freed by the barrier).
 // vmcnt counts rely on vector-memory ops completing in issue order (DMA loads and stores alike).
 #include "mgemm_core.h"
 
@@ -41,9 +45,15 @@ using namespace rk;
 
 namespace {
 
-constexpr int X5_BK = 32, X5_NT = 256;  // a "unit": 32-deep k-slice, two k16 steps
-constexpr int X5_ROWB = X5_BK * 2;      // 64-byte image rows
-constexpr int X5_NS = 4;                // LDS ring: 4 units (3 in flight)
+constexpr int X5_BK = 64;     // a "unit": 64-deep k-slice, four k16 steps
+constexpr int X5_ROWB = X5_BK * 2;  // 128-byte image rows: every DMA piece reads whole cache lines
+constexpr int X5_NS = 2;            // LDS ring: 2 units
+#ifndef X5_DS
+#define X5_DS 2  // steps carrying a unit's DMA: the previous unit's last step + this many - 1 of its own
+#endif
+// 16-byte chunk c of image row r sits at slot c ^ swz8(r): a ds_read_b128 lane group (16 rows
+// distinct mod 16, one chunk) then covers all 16 slots of the 256-byte bank row (conflict-free)
+__device__ __forceinline__ int swz8(int r) { return (r >> 1) & 7; }
 
 template <int I>
 using ic = std::integral_constant<int, I>;
@@ -92,8 +102,10 @@ struct X5Sched {
   // read index of the fragment an MFMA needs
   static constexpr int rb(int j) { return j == 0 ? 0 : j + 1; }
   static constexpr int ra(int i) { return i == 0 ? 1 : FN + i; }
-  // the MFMA after which read k goes out (reads spread evenly over the step)
-  static constexpr int after(int k) { return (k + 1) * Q / R - 1; }
+  // the MFMA after which read k goes out: front-loaded, one read per MFMA (the reads land in the
+  // other fragment set, free since the previous step; the batch is complete long before the unit's
+  // lgkmcnt(0) + barrier, so the MFMA pipe does not drain there)
+  static constexpr int after(int k) { return k; }
   // which read (or -1) goes out right after MFMA m
   static constexpr int read_after(int m) {
     for (int k = 0; k < R; ++k)
@@ -132,20 +144,27 @@ struct X5Args {
   int dbg;  // unused (the round-6 ablation bits are gone: runtime branches inside the MFMA code made the allocator spill)
 };
 
-template <int CDT, bool HASB, int FM, int FN>
-__global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
-  constexpr int BM = 64 * FM, BN = 64 * FN;          // block tile
+template <int CDT, bool HASB, int FM, int FN, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN, 1) xgemm5_kernel(X5Args g) {
+  constexpr int NW = WM * WN;                               // waves: WM x WN, each FM x FN fragments
+  constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;      // block tile
   constexpr int OPA = BM * X5_ROWB, OPB = BN * X5_ROWB;  // operand images per stage
   constexpr int STAGE = OPA + OPB;
-  constexpr int NIA = FM, NIB = FN;                   // DMA instructions per wave per operand and unit
+  constexpr int FR = 32 * X5_ROWB;                        // one 32-row fragment block of an image
+  constexpr int NIA = BM / (8 * NW), NIB = BN / (8 * NW);  // DMA pieces (8 rows x 128 B) per wave per operand
+  static_assert(NIA * 8 * NW == BM && NIB * 8 * NW == BN && NIA % 2 == 0 && NIB % 2 == 0,
+                "a unit's images split evenly over the waves, an even number of pieces each");
   constexpr int NDMA = NIA + NIB;
+  constexpr int DS = X5_DS;
+  static_assert(DS >= 1 && DS <= 3, "a unit's DMA must leave a step to land in");
   constexpr int NST = 2 * FM * FN;                    // 16-byte stores per wave per tile
   constexpr int NIM = NST / 2;                        // issued at the epilogue (rows i < FM / 2)
   constexpr int NPK = NST - NIM;                      // kept packed, issued in the next tile's first 4 units
   constexpr int SPK = NPK / 4;                        // per unit of those
+  static_assert(SPK * 4 == NPK, "stores split over four units");
   using SC = X5Sched<FM, FN>;
   // 2-stage ring + one 1-KiB bias row per wave (one __shared__ object: see the guide's trap 4(a))
-  __shared__ __attribute__((aligned(1024))) char smem[X5_NS * STAGE + 4 * 1024];
+  __shared__ __attribute__((aligned(1024))) char smem[X5_NS * STAGE + NW * 1024];
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const int total = tiles_m * tiles_n;
   const int G = gridDim.x;
@@ -155,15 +174,17 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   const int S = my * U;  // units in this block's stream
   const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WN, wn = w % WN;
 
-  // ---- DMA: lane l of a 1-KiB piece (16 rows x 64 B) lands at image row l/4, slot l%4, i.e. holds
-  // source chunk (l%4) ^ rswz(row); pieces start at 16-row boundaries, so rswz(row) depends on the
-  // lane only: one per-lane offset per operand
-  const int drow = lane >> 2;
-  const uint32_t va = (uint32_t)(drow * g.lda * 2 + (((lane & 3) ^ rswz<32>(drow)) * 16));
-  const uint32_t vb = (uint32_t)(drow * g.ldb * 2 + (((lane & 3) ^ rswz<32>(drow)) * 16));
-  // issue cursor: tile of the next DMA and its k-tile
+  // ---- DMA: lane l of a 1-KiB piece (8 rows x 128 B) lands at image row l/8, slot l%8, i.e. holds
+  // source chunk (l%8) ^ swz8(row).  Pieces start at 8-row boundaries: swz8 of the row depends on the
+  // lane and on the piece's parity (row0 % 16 = 0 or 8; every wave's first piece is at a multiple
+  // of 16 rows): two per-lane offsets per operand
+  const int drow = lane >> 3;
+  const uint32_t c0 = (uint32_t)(((lane & 7) ^ swz8(drow)) * 16), c8 = (uint32_t)(((lane & 7) ^ swz8(drow + 8)) * 16);
+  const uint32_t va0 = (uint32_t)(drow * g.lda * 2) + c0, va8 = (uint32_t)(drow * g.lda * 2) + c8;
+  const uint32_t vb0 = (uint32_t)(drow * g.ldb * 2) + c0, vb8 = (uint32_t)(drow * g.ldb * 2) + c8;
+  // issue cursor: tile of the next DMA and its unit
   int iss_i = 0, iss_k = 0;
   const char *ia = nullptr, *ib = nullptr;
   int ia_n = 0, ib_n = 0;  // bytes from the tile's first row to the operand's end (clamped to 2^31 - 1)
@@ -180,19 +201,25 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
   // one descriptor per operand and unit (rows past M / N read as zeros: the VGPR offset is
   // range-checked).  dma_begin(q) forms them for unit q (a unit past the stream gets an empty
   // descriptor: its instructions still issue, so every vmcnt count stays static, and only write
-  // zeros into a stage nobody reads any more); dma_one(k) issues instruction k (A first, then B),
-  // its row offset added at the instruction to an opaque copy of the lane part (no hoisted sums).
-  __amdgpu_buffer_rsrc_t d_ra, d_rb;
+  // zeros into a stage nobody reads any more); dma_one(k) issues piece k (A first, then B), its
+  // row offset added at the instruction to an opaque copy of the lane part (no hoisted sums).
+  // (the descriptors are formed at each instruction from plain scalars: rsrc-typed variables
+  // carried across the tile-advance branch became a per-thread alloca that hipcc moved into LDS)
+  const char *d_pa = (const char*)g.A, *d_pb = (const char*)g.B;
+  int d_na = 0, d_nb = 0;
   char* d_st = smem;
   auto dma_begin = [&](int q) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const bool real = q < S;
     d_st = smem + (q & (X5_NS - 1)) * STAGE;
-    const char* pa = real ? ia + iss_k * X5_ROWB : (const char*)g.A;
-    const char* pb = real ? ib + iss_k * X5_ROWB : (const char*)g.B;
-    const int na = real ? max(ia_n - iss_k * X5_ROWB, 0) : 0, nb = real ? max(ib_n - iss_k * X5_ROWB, 0) : 0;
-    d_ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pa), (short)0, na, 0x00020000);
-    d_rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pb), (short)0, nb, 0x00020000);
+    const int koff = iss_k * X5_ROWB;
+    const char* pa = real ? ia + koff : (const char*)g.A;
+    const char* pb = real ? ib + koff : (const char*)g.B;
+    const int na = real ? max(ia_n - koff, 0) : 0, nb = real ? max(ib_n - koff, 0) : 0;
+    d_pa = pa;
+    d_pb = pb;
+    d_na = na;
+    d_nb = nb;
     if (real && ++iss_k == U) {
       iss_k = 0;
       if (++iss_i < my) iss_tile(iss_i);
@@ -203,30 +230,48 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const bool opb = k >= NIA;
     const int i = opb ? k - NIA : k;
-    const int row0 = (opb ? 16 * FN : 16 * FM) * w + 16 * i;  // wave w stages a quarter of each image
-    uint32_t vo = opb ? vb : va;
+    const int row0 = (opb ? 8 * NIB : 8 * NIA) * w + 8 * i;  // wave w stages 1/NW of each image
+    // (branches on the compile-time operand, not a ?: of captured lvalues: a select of two
+    // variables' addresses keeps them in memory, and hipcc moved that memory into LDS)
+    uint32_t vo;
+    const char* pp;
+    int nn;
+    int64_t ld;
+    if (opb) {
+      vo = (i & 1) ? vb8 : vb0;
+      pp = d_pb;
+      nn = d_nb;
+      ld = g.ldb;
+    } else {
+      vo = (i & 1) ? va8 : va0;
+      pp = d_pa;
+      nn = d_na;
+      ld = g.lda;
+    }
     asm volatile("" : "+v"(vo));
-    vo += (uint32_t)(row0 * (opb ? g.ldb : g.lda) * 2);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(opb ? d_rb : d_ra, (lds_void*)(d_st + (opb ? OPA : 0) + row0 * X5_ROWB),
+    vo += (uint32_t)(row0 * ld * 2);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pp), (short)0, nn, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(d_st + (opb ? OPA : 0) + row0 * X5_ROWB),
                                              16, vo, 0, 0, 0);
 #endif
   };
-  auto dma_next = [&](int q) {  // a whole unit at once (prologue)
-    dma_begin(q);
+  // DMA group gi of a unit (DS groups): pieces [gi NDMA / DS, (gi + 1) NDMA / DS)
+  auto dma_group = [&](auto Gc) {
+    constexpr int gi = decltype(Gc)::value;
 #pragma unroll
-    for (int k = 0; k < NDMA; ++k) dma_one(k);
+    for (int k = gi * NDMA / DS; k < (gi + 1) * NDMA / DS; ++k) dma_one(k);
   };
 
-  // ---- fragment reads: 32x32x16 operand of rows r0 .. r0+31 at k16 step s (0, 1) of a unit: lane
-  // reads row r0 + l32, chunk 2s + h at slot chunk ^ rswz(row) (64-B rows: four rows share a bank
-  // row, rswz spreads rows 4 apart over the four slots: conflict-free); fragment i = +i * 2048
+  // ---- fragment reads: 32x32x16 operand of rows r0 .. r0+31 at k16 step s (0..3) of a unit: lane
+  // reads row r0 + l32, chunk 2s + h at slot chunk ^ swz8(row); fragment i = +i * FR (32 rows: the
+  // swizzle of row r0 + l32 is that of l32)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const lds_void*)smem;
-  const int fsw = rswz<32>(l32);
-  // per-lane part of step s's address (A image, stage 0); B and the other stages differ by
+  const int fsw = swz8(l32);
+  // per-lane part of step s's address (A image, stage 0); B and the other stage differ by
   // wave-uniform amounts added per step
-  uint32_t la[2];
+  uint32_t la[4];
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < 4; ++s)
     la[s] = lds0 + wm * 32 * FM * X5_ROWB + (uint32_t)(l32 * X5_ROWB + (((2 * s + h) ^ fsw) * 16));
   const uint32_t bdelta = (uint32_t)(OPA + (wn * 32 * FN - wm * 32 * FM) * X5_ROWB);
   // (the base goes through an empty asm so the sums are formed at each use, not hoisted out of
@@ -247,8 +292,8 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     constexpr int k = decltype(Kc)::value;
     if constexpr (k == 0) X5_RD(Fb[0], b, 0);
     else if constexpr (k == 1) X5_RD(Fa[0], a, 0);
-    else if constexpr (k <= FN) X5_RD(Fb[k - 1], b, (k - 1) * 2048);
-    else X5_RD(Fa[k - FN], a, (k - FN) * 2048);
+    else if constexpr (k <= FN) X5_RD(Fb[k - 1], b, (k - 1) * FR);
+    else X5_RD(Fa[k - FN], a, (k - FN) * FR);
   };
 
   f32x16 acc[FM][FN];
@@ -277,11 +322,11 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
 #define X5_ST(q) X5_STV(q, cst[(q) - NIM])
 
   // Q MFMAs of one k16 step on (Fa, Fb) with the counted waits on the previous batch, the reads of
-  // the next step (RD) and, in step 3 (DM), the k-tile's DMA instructions interleaved
-  auto step = [&](auto FIRSTc, auto RDc, auto DMc, const bf16x8 (&Fa)[FM], const bf16x8 (&Fb)[FN],
+  // the next step (RD) and DMA group DG (-1: none) interleaved
+  auto step = [&](auto FIRSTc, auto RDc, auto DGc, const bf16x8 (&Fa)[FM], const bf16x8 (&Fb)[FN],
                   bf16x8 (&Na)[FM], bf16x8 (&Nb)[FN], uint32_t a, uint32_t b) {
     constexpr bool FIRST = decltype(FIRSTc)::value, RD = decltype(RDc)::value;
-    constexpr int DM = decltype(DMc)::value;  // 0 none, 1 / 2: the first / second half of a unit's DMA
+    constexpr int DG = decltype(DGc)::value;
     auto one = [&](auto Mc) {
       constexpr int m = decltype(Mc)::value;
       constexpr int i = m / FN, j = m % FN;
@@ -290,46 +335,45 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
       if constexpr (FIRST) mfma32_0(acc[i][j], Fb[j], Fa[i]);
       else mfma32(acc[i][j], Fb[j], Fa[i]);
       if constexpr (RD && SC::read_after(m) >= 0) rd(Na, Nb, a, b, ic<SC::read_after(m)>{});
-      if constexpr (DM > 0) {  // the half's DMA instructions d with d * Q / NH == m
-        constexpr int NH = NDMA / 2;
+      if constexpr (DG >= 0) {  // the group's pieces d with d * Q / NG == m
+        constexpr int k0 = DG * NDMA / DS, NG = (DG + 1) * NDMA / DS - k0;
 #pragma unroll
-        for (int d = 0; d < NH; ++d)
-          if (d * SC::Q / NH == m) dma_one(d + (DM - 1) * NH);
+        for (int d = 0; d < NG; ++d)
+          if (d * SC::Q / NG == m) dma_one(k0 + d);
       }
     };
     sfor<SC::Q>(one);
   };
   constexpr int kWaitLgkm0 = 0xC07F;
 
-  // one unit q (two k16 steps).  FIRST: the tile's first unit (its MFMAs start the accumulators with
+  // one unit q (four k16 steps).  FIRST: the tile's first unit (its MFMAs start the accumulators with
   // C = 0).  SB >= 0: the unit issues the previous tile's stores SB .. SB + SPK - 1 (static indices: a
   // peeled quad of units issues them all, after which the packed tile is dead, so it is never live
-  // across the k-loop).  LAST: the tile's last unit, whose step 1 reads nothing.
-  //   step 0: MFMAs || reads of step 1 (this stage) || second half of unit q + 3's DMA
-  //   lgkmcnt(0) (this stage fully read) + vmcnt (unit q + 1 landed) + ONE barrier
-  //   step 1: MFMAs || reads of step 0 of unit q + 1 || first half of unit q + 4's DMA, into this
-  //           unit's stage (freed by the barrier)
-  // A unit's DMA is issued over two steps of two different units and has two more units to land.
+  // across the k-loop).  LAST: the tile's last unit, whose step 3 reads nothing.
+  //   steps 0-2: MFMAs || reads of the next step (this stage) || DMA groups 1 .. DS-1 of unit q + 1
+  //   lgkmcnt(0) (this stage fully read) + vmcnt(0) (unit q + 1 landed: nothing younger is a DMA)
+  //   + ONE barrier
+  //   step 3   : MFMAs || reads of step 0 of unit q + 1 || DMA group 0 of unit q + 2 into this
+  //              unit's stage (freed by the barrier) || the previous tile's stores
   auto unit = [&](auto FIRSTc, auto SBc, auto LASTc, int q) {
     constexpr int SB = decltype(SBc)::value;
     constexpr bool LAST = decltype(LASTc)::value;
     const int st = q & (X5_NS - 1);
-    step(FIRSTc, bc<true>{}, ic<2>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
+    step(FIRSTc, bc<true>{}, ic<(DS > 1 ? 1 : -1)>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
+    step(bc<false>{}, bc<true>{}, ic<(DS > 2 ? 2 : -1)>{}, A1, B1, A0, B0, ra(st, 2), rb(st, 2));
+    step(bc<false>{}, bc<true>{}, ic<-1>{}, A0, B0, A1, B1, ra(st, 3), rb(st, 3));
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    dma_begin(q + 2);  // past the stream: an empty descriptor
     if constexpr (SB >= 0) {
 #pragma unroll
       for (int k = 0; k < SPK; ++k) X5_ST(SB + k);
     }
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-    __builtin_amdgcn_sched_barrier(0);
-    // unit q + 1 landed: after its last DMA instruction came units q + 2 and q + 3 (2 NDMA
-    // instructions; stores in between only make this wait longer)
-    if constexpr (NDMA == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    dma_begin(q + 4);  // past the stream: an empty descriptor
     const int st1 = (q + 1) & (X5_NS - 1);
-    step(bc<false>{}, bc<!LAST>{}, ic<1>{}, A1, B1, A0, B0, ra(st1, 0), rb(st1, 0));
+    step(bc<false>{}, bc<!LAST>{}, ic<0>{}, A1, B1, A0, B0, ra(st1, 0), rb(st1, 0));
   };
   // the next k-tile's step-0 fragments, read after an epilogue (not held through the packing)
   auto rd0 = [&](int q) {
@@ -362,6 +406,7 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
     typedef __attribute__((ext_vector_type(4))) unsigned int w4_t;
     float b[FN];
     const uint32_t ba = bslot + (uint32_t)((wn * 32 * FN + l32) * 4);
+    static_assert(FN == 2 || FN == 4, "bias reads");
     asm volatile("ds_read_b32 %0, %1 offset:0" : "=v"(b[0]) : "v"(ba));
     asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(b[1]) : "v"(ba));
     if constexpr (FN == 4) {
@@ -390,20 +435,18 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
 
   if (S > 0) {
     load_bias(0);  // before the DMAs: landed once unit 0 has
-    dma_next(0);
-    dma_next(1);
-    dma_next(2);
-    dma_begin(3);  // unit 3's first half now, its second half in unit 0's step 0 (steady state)
+    dma_begin(0);
 #pragma unroll
-    for (int k = 0; k < NDMA / 2; ++k) dma_one(k);
-    if constexpr (NDMA == 8) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    for (int k = 0; k < NDMA; ++k) dma_one(k);
+    dma_begin(1);  // unit 1's group 0 now (steady state: issued in unit 0's predecessor's last step)
+    dma_group(ic<0>{});
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NDMA / DS) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     rd0(0);
   }
 
-  // U >= 10 (host check): the first four units of every tile carry the previous tile's stores
+  // U >= 5 (host check): the first four units of every tile carry the previous tile's stores
   int q = 0;
   for (int ti = 0; ti < my; ++ti) {
     if (ti > 0) rd0(q);
@@ -479,23 +522,31 @@ __global__ void __launch_bounds__(X5_NT, 1) xgemm5_kernel(X5Args g) {
 }
 
 template <int CDT, bool HASB>
-int x5_launch(int fm, int fn, int grid, const X5Args& g, hipStream_t s) {
-  if (fm == 4 && fn == 4) xgemm5_kernel<CDT, HASB, 4, 4><<<grid, X5_NT, 0, s>>>(g);
-  else if (fm == 2 && fn == 4) xgemm5_kernel<CDT, HASB, 2, 4><<<grid, X5_NT, 0, s>>>(g);
-  else if (fm == 4 && fn == 2) xgemm5_kernel<CDT, HASB, 4, 2><<<grid, X5_NT, 0, s>>>(g);
-  else return (int)hipErrorInvalidValue;
+int x5_launch(int shape, int grid, const X5Args& g, hipStream_t s) {
+  switch (shape) {
+    case 1: xgemm5_kernel<CDT, HASB, 4, 4, 2, 2><<<grid, 256, 0, s>>>(g); break;
+    case 2: xgemm5_kernel<CDT, HASB, 2, 4, 2, 2><<<grid, 256, 0, s>>>(g); break;
+    case 3: xgemm5_kernel<CDT, HASB, 4, 2, 2, 2><<<grid, 256, 0, s>>>(g); break;
+    case 4: xgemm5_kernel<CDT, HASB, 4, 2, 2, 4><<<grid, 512, 0, s>>>(g); break;
+    case 5: xgemm5_kernel<CDT, HASB, 2, 2, 2, 4><<<grid, 512, 0, s>>>(g); break;
+    case 6: xgemm5_kernel<CDT, HASB, 2, 2, 4, 2><<<grid, 512, 0, s>>>(g); break;
+    default: return (int)hipErrorInvalidValue;
+  }
   return (int)hipGetLastError();
 }
 
-int g_x5_shape = 0;  // diagnostics: force a tile shape (0 auto, 1 256x256, 2 128x256, 3 256x128)
-int g_x5_dbg = 0;    // diagnostics: X5Args::dbg of later launches
+// tile shapes: 1 / 2 / 3 = 256x256 / 128x256 / 256x128 on 4 waves (one per SIMD), 4 / 5 / 6 the same
+// tiles on 8 waves (two per SIMD: one wave's vector-memory issue stalls hide under its partner's MFMAs)
+int g_x5_shape = 0;   // diagnostics: force a tile shape (0 automatic)
+int g_x5_family = 4;  // automatic choice among shapes family .. family + 2
 
 }  // namespace
 
-// Diagnostics: force the tile shape of later rk_xgemm5 calls (0 = automatic); ablation bits.
+// Diagnostics: force the tile shape of later rk_xgemm5 calls (0 = automatic; 1..6, see g_x5_shape);
+// s >= 16: the automatic choice uses family s - 16 (1: 4-wave tiles, 4: 8-wave tiles).
 RK_API int rk_xgemm5_set_shape(int s) {
-  g_x5_shape = s & 0xff;
-  g_x5_dbg = s >> 8;
+  if (s >= 16) g_x5_family = (s - 16) == 1 ? 1 : 4;
+  else g_x5_shape = s;
   return 0;
 }
 
@@ -526,16 +577,17 @@ RK_API int rk_xgemm5(const void* a, int64_t lda, const void* b, int64_t ldb, voi
     const double per = (double)bm * bn / 65536.0 * (bm * bn == 65536 ? 1.0 : 1.15);
     return ((t + ncu - 1) / ncu) * per;
   };
-  int fm = 4, fn = 4;
-  if (g_x5_shape == 2) fm = 2;
-  else if (g_x5_shape == 3) fn = 2;
-  else if (g_x5_shape == 0) {
+  int shape = g_x5_shape, bm = 256, bn = 256;
+  if (shape == 0) {
     double best = cost(256, 256);
-    if (cost(128, 256) < best - 1e-9) { best = cost(128, 256); fm = 2; }
-    if (cost(256, 128) < best - 1e-9) { fm = 4; fn = 2; }
+    shape = g_x5_family;
+    if (cost(128, 256) < best - 1e-9) { best = cost(128, 256); shape = g_x5_family + 1; }
+    if (cost(256, 128) < best - 1e-9) shape = g_x5_family + 2;
   }
-  const int grid = std::min(tiles(64 * fm, 64 * fn), ncu);
-  X5Args g{(const uint16_t*)a, (const uint16_t*)b, c, bias, lda, ldb, ldc, M, N, K, c_dt, g_x5_dbg};
-  if (c_dt == F16) return bias ? x5_launch<F16, true>(fm, fn, grid, g, s) : x5_launch<F16, false>(fm, fn, grid, g, s);
-  return bias ? x5_launch<BF16, true>(fm, fn, grid, g, s) : x5_launch<BF16, false>(fm, fn, grid, g, s);
+  if (shape == 2 || shape == 5) bm = 128;
+  if (shape == 3 || shape == 6) bn = 128;
+  const int grid = std::min(tiles(bm, bn), ncu);
+  X5Args g{(const uint16_t*)a, (const uint16_t*)b, c, bias, lda, ldb, ldc, M, N, K, c_dt, 0};
+  if (c_dt == F16) return bias ? x5_launch<F16, true>(shape, grid, g, s) : x5_launch<F16, false>(shape, grid, g, s);
+  return bias ? x5_launch<BF16, true>(shape, grid, g, s) : x5_launch<BF16, false>(shape, grid, g, s);
 }

@@ -31,7 +31,8 @@ def _run(a, b, c, bias, M, N, K, ldc=None):
     return rc
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "256x256", "128x256", "256x128"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6],
+                ids=["auto", "256x256", "128x256", "256x128", "w8-256x256", "w8-128x256", "w8-256x128"])
 def x5_shape(request):
     lib = _lib().kernels()
     lib.rk_xgemm5_set_shape(request.param)
