@@ -1,6 +1,6 @@
 """Run one GEMM engine on one shape a few times (PMC passes: rocprofv3 --pmc over this program).
 
-    python bench/x5_one.py qkv x5 [reps]       engines: x5, x4, lib
+    python bench/x5_one.py qkv x5 [reps]       engines: x5, x5:<shape code>, x4, lib
 """
 import os
 import sys
@@ -20,6 +20,9 @@ w = (torch.rand(n, k, device=dev) * 2 - 1).to(torch.bfloat16)
 bias = torch.randn(n, device=dev)
 y = torch.empty(m, n, dtype=torch.bfloat16, device=dev)
 lib = _lib.kernels()
+if eng.startswith("x5:"):  # x5:<rk_xgemm5_set_shape code>
+    lib.rk_xgemm5_set_shape(int(eng[3:]))
+    eng = "x5"
 for _ in range(reps):
     if eng == "x5":
         lib.rk_xgemm5(x.data_ptr(), k, w.data_ptr(), k, y.data_ptr(), n, 1, bias.data_ptr(), m, n, k, _lib.stream_ptr(dev))

@@ -144,24 +144,29 @@ struct X5Args {
   int dbg;  // unused (the round-6 ablation bits are gone: runtime branches inside the MFMA code made the allocator spill)
 };
 
+// 128x128 tiles (68 KiB of LDS) run two blocks per CU: one block's DMA issue and fill/drain
+// overlap the other's MFMAs
+template <int FM, int FN, int WM, int WN>
+constexpr int x5_blocks_per_cu() { return FM * FN * WM * WN <= 16 ? 2 : 1; }
+
 template <int CDT, bool HASB, int FM, int FN, int WM, int WN>
-__global__ void __launch_bounds__(64 * WM * WN, 1) xgemm5_kernel(X5Args g) {
+__global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN>())) xgemm5_kernel(X5Args g) {
   constexpr int NW = WM * WN;                               // waves: WM x WN, each FM x FN fragments
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;      // block tile
   constexpr int OPA = BM * X5_ROWB, OPB = BN * X5_ROWB;  // operand images per stage
   constexpr int STAGE = OPA + OPB;
   constexpr int FR = 32 * X5_ROWB;                        // one 32-row fragment block of an image
   constexpr int NIA = BM / (8 * NW), NIB = BN / (8 * NW);  // DMA pieces (8 rows x 128 B) per wave per operand
-  static_assert(NIA * 8 * NW == BM && NIB * 8 * NW == BN && NIA % 2 == 0 && NIB % 2 == 0,
-                "a unit's images split evenly over the waves, an even number of pieces each");
+  static_assert(NIA * 8 * NW == BM && NIB * 8 * NW == BN, "a unit's images split evenly over the waves");
   constexpr int NDMA = NIA + NIB;
   constexpr int DS = X5_DS;
   static_assert(DS >= 1 && DS <= 3, "a unit's DMA must leave a step to land in");
   constexpr int NST = 2 * FM * FN;                    // 16-byte stores per wave per tile
   constexpr int NIM = NST / 2;                        // issued at the epilogue (rows i < FM / 2)
-  constexpr int NPK = NST - NIM;                      // kept packed, issued in the next tile's first 4 units
-  constexpr int SPK = NPK / 4;                        // per unit of those
-  static_assert(SPK * 4 == NPK, "stores split over four units");
+  constexpr int NPK = NST - NIM;                      // kept packed, issued in the next tile's first NSU units
+  constexpr int NSU = NPK % 4 == 0 ? 4 : 5;           // (U >= NSU + 1: host check)
+  constexpr int SPK = NPK / NSU;                      // per unit of those
+  static_assert(SPK * NSU == NPK, "stores split over four or five units");
   using SC = X5Sched<FM, FN>;
   // 2-stage ring + one 1-KiB bias row per wave (one __shared__ object: see the guide's trap 4(a))
   __shared__ __attribute__((aligned(1024))) char smem[X5_NS * STAGE + NW * 1024];
@@ -237,13 +242,15 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm5_kernel(X5Args g) {
     const char* pp;
     int nn;
     int64_t ld;
+    // parity of the piece's first 8-row group (wave-uniform; compile-time for even NIA / NIB)
+    const bool par = (((opb ? NIB : NIA) * w + i) & 1) != 0;
     if (opb) {
-      vo = (i & 1) ? vb8 : vb0;
+      vo = par ? vb8 : vb0;
       pp = d_pb;
       nn = d_nb;
       ld = g.ldb;
     } else {
-      vo = (i & 1) ? va8 : va0;
+      vo = par ? va8 : va0;
       pp = d_pa;
       nn = d_na;
       ld = g.lda;
@@ -314,10 +321,18 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm5_kernel(X5Args g) {
   const i32x4_t crs = {(int)c_lo, (int)(c_hi & 0xffff), (int)cb, 0x00020000};
   // (s_nop 1 ends each store: a dwordx4 store reads its data registers a cycle late, and hipcc,
   // which does not model the asm, may overwrite them with the very next VALU instruction)
+  // (tiles narrower than a multiple of 128 columns, e.g. 160, can end past N: a 32-column block
+  // whose first column is at or past N gets the dropped offset; c_nl = N - the wave's first column)
+  int c_nl = 0;
+  auto st_off = [&](int q) -> uint32_t {
+    const uint32_t o = c_vb[q / (2 * FN)];
+    if constexpr (BN % 128 == 0) return o;
+    else return 32 * ((q >> 1) % FN) < c_nl ? o : 0x7ffff000u;
+  };
 #define X5_STV(q, v)                                                                              \
   asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 1"                   \
                :                                                                                   \
-               : "v"(v), "v"(c_vb[(q) / (2 * FN)]), "s"(crs), "i"((((q) >> 1) % FN) * 64 + ((q) & 1) * 32) \
+               : "v"(v), "v"(st_off(q)), "s"(crs), "i"((((q) >> 1) % FN) * 64 + ((q) & 1) * 32) \
                : "memory")
 #define X5_ST(q) X5_STV(q, cst[(q) - NIM])
 
@@ -406,13 +421,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm5_kernel(X5Args g) {
     typedef __attribute__((ext_vector_type(4))) unsigned int w4_t;
     float b[FN];
     const uint32_t ba = bslot + (uint32_t)((wn * 32 * FN + l32) * 4);
-    static_assert(FN == 2 || FN == 4, "bias reads");
+    static_assert(FN >= 2 && FN <= 5, "bias reads");
     asm volatile("ds_read_b32 %0, %1 offset:0" : "=v"(b[0]) : "v"(ba));
     asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(b[1]) : "v"(ba));
-    if constexpr (FN == 4) {
-      asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(b[2]) : "v"(ba));
-      asm volatile("ds_read_b32 %0, %1 offset:384" : "=v"(b[3]) : "v"(ba));
-    }
+    if constexpr (FN > 2) asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(b[2 % FN]) : "v"(ba));
+    if constexpr (FN > 3) asm volatile("ds_read_b32 %0, %1 offset:384" : "=v"(b[3 % FN]) : "v"(ba));
+    if constexpr (FN > 4) asm volatile("ds_read_b32 %0, %1 offset:512" : "=v"(b[4 % FN]) : "v"(ba));
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t one2 = h == 0 ? 0x3F803F80u : 0u;  // bf16 (1, 1)
@@ -446,7 +460,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm5_kernel(X5Args g) {
     rd0(0);
   }
 
-  // U >= 5 (host check): the first four units of every tile carry the previous tile's stores
+  // U >= NSU + 1 (host check): the first NSU units of every tile carry the previous tile's stores
   int q = 0;
   for (int ti = 0; ti < my; ++ti) {
     if (ti > 0) rd0(q);
@@ -460,7 +474,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm5_kernel(X5Args g) {
     unit(bc<false>{}, ic<NIM + SPK>{}, bc<false>{}, q++);
     unit(bc<false>{}, ic<NIM + 2 * SPK>{}, bc<false>{}, q++);
     unit(bc<false>{}, ic<NIM + 3 * SPK>{}, bc<false>{}, q++);
-    for (int kt = 4; kt < U - 1; ++kt) unit(bc<false>{}, ic<-1>{}, bc<false>{}, q++);
+    if constexpr (NSU == 5) unit(bc<false>{}, ic<NIM + 4 * SPK>{}, bc<false>{}, q++);
+    for (int kt = NSU; kt < U - 1; ++kt) unit(bc<false>{}, ic<-1>{}, bc<false>{}, q++);
     unit(bc<false>{}, ic<-1>{}, bc<true>{}, q++);
     // epilogue: pack this tile (accumulators -> 16-bit, lane halves swapped so each store covers
     // 16 B); the first half of the rows goes out at once, the rest under the next tile's quad
@@ -480,6 +495,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) xgemm5_kernel(X5Args g) {
       const uint32_t blk = (uint32_t)(32 * (int)g.ldc * 2);
 #pragma unroll
       for (int i = 0; i < FM; ++i) c_vb[i] = in ? o0 + i * blk : 0x7ffff000u;
+      c_nl = g.N - c_n0;
     }
     auto pack_row = [&](auto Ic) {  // fragments (i, 0 .. FN-1)
       constexpr int i = decltype(Ic)::value;
@@ -530,22 +546,33 @@ int x5_launch(int shape, int grid, const X5Args& g, hipStream_t s) {
     case 4: xgemm5_kernel<CDT, HASB, 4, 2, 2, 4><<<grid, 512, 0, s>>>(g); break;
     case 5: xgemm5_kernel<CDT, HASB, 2, 2, 2, 4><<<grid, 512, 0, s>>>(g); break;
     case 6: xgemm5_kernel<CDT, HASB, 2, 2, 4, 2><<<grid, 512, 0, s>>>(g); break;
+    case 7: xgemm5_kernel<CDT, HASB, 2, 2, 2, 2><<<grid, 256, 0, s>>>(g); break;
+    case 8: xgemm5_kernel<CDT, HASB, 2, 5, 4, 1><<<grid, 256, 0, s>>>(g); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
 }
 
 // tile shapes: 1 / 2 / 3 = 256x256 / 128x256 / 256x128 on 4 waves (one per SIMD), 4 / 5 / 6 the same
-// tiles on 8 waves (two per SIMD: one wave's vector-memory issue stalls hide under its partner's MFMAs)
+// tiles on 8 waves (two per SIMD), 7 = 128x128 on 4 waves, 8 = 256x160 on 4 waves (4 x 1, 64 x 160 per
+// wave: N = 768 in 5 column tiles, 495 tiles on 256 CUs = two nearly full rounds)
 int g_x5_shape = 0;   // diagnostics: force a tile shape (0 automatic)
+int g_x5_split = 0;   // diagnostics: force the row split with this tail shape (0 automatic)
 int g_x5_family = 4;  // automatic choice among shapes family .. family + 2
+
+void x5_dims(int shape, int& bm, int& bn) {
+  bm = (shape == 2 || shape == 5 || shape == 7) ? 128 : 256;
+  bn = shape == 8 ? 160 : (shape == 3 || shape == 6 || shape == 7) ? 128 : 256;
+}
 
 }  // namespace
 
-// Diagnostics: force the tile shape of later rk_xgemm5 calls (0 = automatic; 1..6, see g_x5_shape);
-// s >= 16: the automatic choice uses family s - 16 (1: 4-wave tiles, 4: 8-wave tiles).
+// Diagnostics: force the tile shape of later rk_xgemm5 calls (0 = automatic; 1..7, see g_x5_shape);
+// 16 / 17: the automatic choice uses 4-wave / 8-wave tiles; 32 + t: force the row split with tail
+// shape t (32: automatic).
 RK_API int rk_xgemm5_set_shape(int s) {
-  if (s >= 16) g_x5_family = (s - 16) == 1 ? 1 : 4;
+  if (s >= 32) g_x5_split = s - 32;
+  else if (s >= 16) g_x5_family = s == 16 ? 1 : 4;
   else g_x5_shape = s;
   return 0;
 }
@@ -570,24 +597,50 @@ RK_API int rk_xgemm5(const void* a, int64_t lda, const void* b, int64_t ldb, voi
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
   }
-  auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  // CU rounds x tile size, half-size tiles priced 1.15x per element (their per-wave tile reads more)
-  auto cost = [&](int bm, int bn) {
-    const int t = tiles(bm, bn);
-    const double per = (double)bm * bn / 65536.0 * (bm * bn == 65536 ? 1.0 : 1.15);
-    return ((t + ncu - 1) / ncu) * per;
+  // CU rounds x tile area, smaller tiles priced higher per element (their per-wave tiles read more
+  // per MFMA): the single-launch cost of a shape over `rows` rows
+  auto price = [](int bm, int bn) {
+    return bm * bn == 65536 ? 1.0 : bm * bn == 40960 ? 1.08 : bm * bn == 32768 ? 1.15 : 1.4;
   };
-  int shape = g_x5_shape, bm = 256, bn = 256;
-  if (shape == 0) {
-    double best = cost(256, 256);
-    shape = g_x5_family;
-    if (cost(128, 256) < best - 1e-9) { best = cost(128, 256); shape = g_x5_family + 1; }
-    if (cost(256, 128) < best - 1e-9) shape = g_x5_family + 2;
+  auto cost = [&](int shape, int rows) {
+    int bm, bn;
+    x5_dims(shape, bm, bn);
+    const int t = ((rows + bm - 1) / bm) * ((N + bn - 1) / bn), slots = shape == 7 ? 2 * ncu : ncu;
+    return ((t + slots - 1) / slots) * (double)bm * bn / 65536.0 * price(bm, bn) * (shape == 7 ? 2.0 : 1.0);
+  };
+  // Plan: one launch, or (when the 256x256 tiles leave the last CU round part-empty, e.g. ViT's
+  // N = 768 products: 297 tiles on 256 CUs) the rows of the full rounds on 256x256 tiles and the
+  // remaining rows on a smaller tile as a second launch.
+  int s1 = g_x5_shape == 8 && K < 384 ? 1 : g_x5_shape, s2 = 0, rows1 = M;
+  if (s1 == 0) {
+    s1 = g_x5_family;
+    double best = cost(s1, M);
+    for (int t = g_x5_family + 1; t <= g_x5_family + 2; ++t)
+      if (cost(t, M) < best - 1e-9) { best = cost(t, M); s1 = t; }
+    if (K >= 384 && cost(8, M) < best - 1e-9) { best = cost(8, M); s1 = 8; }  // 256x160 needs U >= 6
+    const int tn = (N + 255) / 256, full = ((M + 255) / 256) * tn;
+    int r = full / ncu, r1 = (r * ncu / tn) * 256;
+    if (g_x5_split > 0 && r1 <= 0) r1 = (M / 2) / 256 * 256;  // diagnostics on small problems
+    if (r1 > 0 && r1 < M) {
+      const int cand[4] = {g_x5_family + 1, g_x5_family + 2, 7, 0};
+      for (int ci = 0; cand[ci]; ++ci) {
+        const int t = g_x5_split > 0 ? g_x5_split : cand[ci];
+        const double c = (double)(((r1 / 256) * tn + ncu - 1) / ncu) + cost(t, M - r1) + 0.2;  // a launch's fill + drain
+        if (g_x5_split > 0 || c < best - 1e-9) { best = c; s1 = g_x5_family; s2 = t; rows1 = r1; }
+        if (g_x5_split > 0) break;
+      }
+    }
   }
-  if (shape == 2 || shape == 5) bm = 128;
-  if (shape == 3 || shape == 6) bn = 128;
-  const int grid = std::min(tiles(bm, bn), ncu);
-  X5Args g{(const uint16_t*)a, (const uint16_t*)b, c, bias, lda, ldb, ldc, M, N, K, c_dt, 0};
-  if (c_dt == F16) return bias ? x5_launch<F16, true>(shape, grid, g, s) : x5_launch<F16, false>(shape, grid, g, s);
-  return bias ? x5_launch<BF16, true>(shape, grid, g, s) : x5_launch<BF16, false>(shape, grid, g, s);
+  auto launch = [&](int shape, int r0, int rows) {
+    int bm, bn;
+    x5_dims(shape, bm, bn);
+    const int grid = std::min(((rows + bm - 1) / bm) * ((N + bn - 1) / bn), shape == 7 ? 2 * ncu : ncu);
+    X5Args g{(const uint16_t*)a + (int64_t)r0 * lda, (const uint16_t*)b, (char*)c + (int64_t)r0 * ldc * 2, bias,
+             lda, ldb, ldc, rows, N, K, c_dt, 0};
+    if (c_dt == F16) return bias ? x5_launch<F16, true>(shape, grid, g, s) : x5_launch<F16, false>(shape, grid, g, s);
+    return bias ? x5_launch<BF16, true>(shape, grid, g, s) : x5_launch<BF16, false>(shape, grid, g, s);
+  };
+  int rc = launch(s1, 0, rows1);
+  if (rc == 0 && s2 > 0) rc = launch(s2, rows1, M - rows1);
+  return rc;
 }

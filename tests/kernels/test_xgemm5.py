@@ -31,13 +31,18 @@ def _run(a, b, c, bias, M, N, K, ldc=None):
     return rc
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6],
-                ids=["auto", "256x256", "128x256", "256x128", "w8-256x256", "w8-128x256", "w8-256x128"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8, 32 + 7, 32 + 5],
+                ids=["auto", "256x256", "128x256", "256x128", "w8-256x256", "w8-128x256", "w8-256x128", "128x128",
+                     "256x160",
+                     "split-128x128", "split-w8-128x256"])
 def x5_shape(request):
+    """Tile shape of rk_xgemm5 (codes of rk_xgemm5_set_shape): every single-launch shape, and the
+    two-launch row split (256x256 rows + a smaller-tile tail) forced onto each problem."""
     lib = _lib().kernels()
     lib.rk_xgemm5_set_shape(request.param)
     yield request.param
     lib.rk_xgemm5_set_shape(0)
+    lib.rk_xgemm5_set_shape(32)
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 256, 320), (777, 384, 448), (2056, 768, 768), (25216, 2304, 768),
