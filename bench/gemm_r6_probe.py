@@ -74,9 +74,15 @@ def main():
                 lib.rk_xgemm5_set_shape(0)
             return f
 
+        def fam(f):
+            def g():
+                lib.rk_xgemm5_set_shape(16 + f)
+                x5(True)()
+                lib.rk_xgemm5_set_shape(16 + 2)
+            return g
+
         engines = {"lib": lambda: torch.addmm(b16, x, w.t()), "x5": x5(True), "x5_nobias": x5(False),
-                   "x5_256x256": shaped(1), "x5_128x256": shaped(2), "x5_256x128": shaped(3),
-                   "w8_256x256": shaped(4), "w8_128x256": shaped(5), "w8_256x128": shaped(6)}
+                   "f0": fam(0), "f1": fam(1), "s1": shaped(1), "s8": shaped(8), "s9": shaped(9), "s10": shaped(10)}
         times = {t: [] for t in engines}
         for _ in range(a.rounds):
             for tag, fn in engines.items():

@@ -68,6 +68,12 @@ __device__ __forceinline__ void mfma32(f32x16& c, const bf16x8& a, const bf16x8&
 __device__ __forceinline__ void mfma32_0(f32x16& c, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
 }
+__device__ __forceinline__ void mfma32(f32x4& c, const bf16x8& a, const bf16x8& b) {  // 16x16x32
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma32_0(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+}
 // f(ic<0>{}), f(ic<1>{}), ... f(ic<N-1>{}): compile-time indices for unrolled bodies
 template <class F, int... I>
 __device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
@@ -130,7 +136,8 @@ struct X5Sched {
     if (rd)
       for (int k = 0; k < R; ++k)
         if (after(k) < m) ++fresh;
-    return (R - 1 - need(m)) + fresh;
+    const int w = (R - 1 - need(m)) + fresh;
+    return w > 15 ? 15 : w;  // lgkmcnt is 4 bits: waiting for more than needed stays correct
   }
 };
 
@@ -149,25 +156,34 @@ struct X5Args {
 template <int FM, int FN, int WM, int WN>
 constexpr int x5_blocks_per_cu() { return FM * FN * WM * WN <= 16 ? 2 : 1; }
 
-template <int CDT, bool HASB, int FM, int FN, int WM, int WN>
+// MF: the MFMA shape, 32 (v_mfma_f32_32x32x16_bf16, four k16 steps per unit) or 16
+// (v_mfma_f32_16x16x32_bf16, two k32 steps per unit; the same FLOP per cycle, and the chip holds a
+// higher clock on it).  FM x FN count 32 x 32 blocks either way (a 32-block = 2 x 2 16-blocks).
+template <int CDT, bool HASB, int FM, int FN, int WM, int WN, int MF = 32>
 __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN>())) xgemm5_kernel(X5Args g) {
+  static_assert(MF == 32 || MF == 16, "MFMA shape");
+  constexpr int SUB = MF == 16 ? 2 : 1;        // MFMA blocks per 32-row (column) block
+  constexpr int AM = FM * SUB, AN = FN * SUB;  // MFMA blocks per wave
+  constexpr int NSTEP = MF == 16 ? 2 : 4;      // MFMA k-steps per 64-deep unit
+  constexpr int NCV = MF == 16 ? 2 * FM : FM;  // per-lane store row offsets
+  using accT = std::conditional_t<MF == 16, f32x4, f32x16>;
   constexpr int NW = WM * WN;                               // waves: WM x WN, each FM x FN fragments
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;      // block tile
   constexpr int OPA = BM * X5_ROWB, OPB = BN * X5_ROWB;  // operand images per stage
   constexpr int STAGE = OPA + OPB;
-  constexpr int FR = 32 * X5_ROWB;                        // one 32-row fragment block of an image
+  constexpr int FR = MF * X5_ROWB;                        // one MF-row fragment block of an image
   constexpr int NIA = BM / (8 * NW), NIB = BN / (8 * NW);  // DMA pieces (8 rows x 128 B) per wave per operand
   static_assert(NIA * 8 * NW == BM && NIB * 8 * NW == BN, "a unit's images split evenly over the waves");
   constexpr int NDMA = NIA + NIB;
-  constexpr int DS = X5_DS;
-  static_assert(DS >= 1 && DS <= 3, "a unit's DMA must leave a step to land in");
+  constexpr int DS = MF == 16 ? 1 : X5_DS;  // (two steps per unit: all of it after the barrier)
+  static_assert(DS >= 1 && DS <= NSTEP - 1, "a unit's DMA must leave a step to land in");
   constexpr int NST = 2 * FM * FN;                    // 16-byte stores per wave per tile
   constexpr int NIM = NST / 2;                        // issued at the epilogue (rows i < FM / 2)
   constexpr int NPK = NST - NIM;                      // kept packed, issued in the next tile's first NSU units
   constexpr int NSU = NPK % 4 == 0 ? 4 : 5;           // (U >= NSU + 1: host check)
   constexpr int SPK = NPK / NSU;                      // per unit of those
   static_assert(SPK * NSU == NPK, "stores split over four or five units");
-  using SC = X5Sched<FM, FN>;
+  using SC = X5Sched<AM, AN>;
   // 2-stage ring + one 1-KiB bias row per wave (one __shared__ object: see the guide's trap 4(a))
   __shared__ __attribute__((aligned(1024))) char smem[X5_NS * STAGE + NW * 1024];
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
@@ -273,13 +289,18 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
   // reads row r0 + l32, chunk 2s + h at slot chunk ^ swz8(row); fragment i = +i * FR (32 rows: the
   // swizzle of row r0 + l32 is that of l32)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const lds_void*)smem;
-  const int fsw = swz8(l32);
+  // (16x16x32: lane reads row r0 + lane % 16, chunk 4 s + lane / 16 — a lane group's 16 rows are
+  // still distinct mod 16: conflict-free under the same swizzle)
+  const int frow = MF == 16 ? (lane & 15) : l32;
+  const int fsw = swz8(frow);
   // per-lane part of step s's address (A image, stage 0); B and the other stage differ by
   // wave-uniform amounts added per step
-  uint32_t la[4];
+  uint32_t la[NSTEP];
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
-    la[s] = lds0 + wm * 32 * FM * X5_ROWB + (uint32_t)(l32 * X5_ROWB + (((2 * s + h) ^ fsw) * 16));
+  for (int s = 0; s < NSTEP; ++s) {
+    const int ch = MF == 16 ? 4 * s + (lane >> 4) : 2 * s + h;
+    la[s] = lds0 + wm * 32 * FM * X5_ROWB + (uint32_t)(frow * X5_ROWB + ((ch ^ fsw) * 16));
+  }
   const uint32_t bdelta = (uint32_t)(OPA + (wn * 32 * FN - wm * 32 * FM) * X5_ROWB);
   // (the base goes through an empty asm so the sums are formed at each use, not hoisted out of
   // the loop into live registers)
@@ -295,16 +316,16 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
   };
 #define X5_RD(dst, a, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(a), "i"(off))
   // read k of a step's batch: B0 A0 B1 .. B(FN-1) A1 .. A(FM-1) (X5Sched)
-  auto rd = [&](bf16x8 (&Fa)[FM], bf16x8 (&Fb)[FN], uint32_t a, uint32_t b, auto Kc) {
+  auto rd = [&](bf16x8 (&Fa)[AM], bf16x8 (&Fb)[AN], uint32_t a, uint32_t b, auto Kc) {
     constexpr int k = decltype(Kc)::value;
     if constexpr (k == 0) X5_RD(Fb[0], b, 0);
     else if constexpr (k == 1) X5_RD(Fa[0], a, 0);
-    else if constexpr (k <= FN) X5_RD(Fb[k - 1], b, (k - 1) * FR);
-    else X5_RD(Fa[k - FN], a, (k - FN) * FR);
+    else if constexpr (k <= AN) X5_RD(Fb[k - 1], b, (k - 1) * FR);
+    else X5_RD(Fa[k - AN], a, (k - AN) * FR);
   };
 
-  f32x16 acc[FM][FN];
-  bf16x8 A0[FM], B0[FN], A1[FM], B1[FN];
+  accT acc[AM][AN];
+  bf16x8 A0[AM], B0[AN], A1[AM], B1[AN];
 
   // ---- the packed previous tile and its stores: lane (l32, h) of store q = 2 (FN i + j) + p
   // writes C[c_m0 + 32 i + l32][c_n0 + 32 j + 16 p + 8 h .. + 8]: per-lane offset c_vb[i] (rows past
@@ -313,9 +334,11 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
   u32x4 cst[NPK];  // stores NIM .. NST - 1
   // before the first tile the offsets point past the records, so the first tile's (unconditional)
   // store slots are dropped by the hardware
-  uint32_t c_vb[FM];
+  // (16x16 blocks: store q = 2 (FN i + j) + i2 writes rows 32 i + 16 i2 + lane % 16; lane group
+  // g = lane / 16 holds columns 32 j + 16 (g & 1) + 8 (g >> 1) .. + 8 after the permlane16 swap)
+  uint32_t c_vb[NCV];
 #pragma unroll
-  for (int i = 0; i < FM; ++i) c_vb[i] = 0x7ffff000u;
+  for (int i = 0; i < NCV; ++i) c_vb[i] = 0x7ffff000u;
   const int64_t cb = (int64_t)g.M * g.ldc * 2;  // < 2^31 (host check)
   const uint32_t c_lo = (uint32_t)(uintptr_t)g.C, c_hi = (uint32_t)((uintptr_t)g.C >> 32);
   const i32x4_t crs = {(int)c_lo, (int)(c_hi & 0xffff), (int)cb, 0x00020000};
@@ -325,26 +348,26 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
   // whose first column is at or past N gets the dropped offset; c_nl = N - the wave's first column)
   int c_nl = 0;
   auto st_off = [&](int q) -> uint32_t {
-    const uint32_t o = c_vb[q / (2 * FN)];
+    const uint32_t o = MF == 16 ? c_vb[(q / (2 * FN)) * 2 + (q & 1)] : c_vb[q / (2 * FN)];
     if constexpr (BN % 128 == 0) return o;
     else return 32 * ((q >> 1) % FN) < c_nl ? o : 0x7ffff000u;
   };
 #define X5_STV(q, v)                                                                              \
   asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 1"                   \
                :                                                                                   \
-               : "v"(v), "v"(st_off(q)), "s"(crs), "i"((((q) >> 1) % FN) * 64 + ((q) & 1) * 32) \
+               : "v"(v), "v"(st_off(q)), "s"(crs), "i"((((q) >> 1) % FN) * 64 + (MF == 16 ? 0 : ((q) & 1) * 32)) \
                : "memory")
 #define X5_ST(q) X5_STV(q, cst[(q) - NIM])
 
   // Q MFMAs of one k16 step on (Fa, Fb) with the counted waits on the previous batch, the reads of
   // the next step (RD) and DMA group DG (-1: none) interleaved
-  auto step = [&](auto FIRSTc, auto RDc, auto DGc, const bf16x8 (&Fa)[FM], const bf16x8 (&Fb)[FN],
-                  bf16x8 (&Na)[FM], bf16x8 (&Nb)[FN], uint32_t a, uint32_t b) {
+  auto step = [&](auto FIRSTc, auto RDc, auto DGc, const bf16x8 (&Fa)[AM], const bf16x8 (&Fb)[AN],
+                  bf16x8 (&Na)[AM], bf16x8 (&Nb)[AN], uint32_t a, uint32_t b) {
     constexpr bool FIRST = decltype(FIRSTc)::value, RD = decltype(RDc)::value;
     constexpr int DG = decltype(DGc)::value;
     auto one = [&](auto Mc) {
       constexpr int m = decltype(Mc)::value;
-      constexpr int i = m / FN, j = m % FN;
+      constexpr int i = m / AN, j = m % AN;
       constexpr int wt = SC::wait_before(m, RD);
       if constexpr (wt >= 0) wait_lgkm<wt>();
       if constexpr (FIRST) mfma32_0(acc[i][j], Fb[j], Fa[i]);
@@ -374,9 +397,13 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
     constexpr int SB = decltype(SBc)::value;
     constexpr bool LAST = decltype(LASTc)::value;
     const int st = q & (X5_NS - 1);
-    step(FIRSTc, bc<true>{}, ic<(DS > 1 ? 1 : -1)>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
-    step(bc<false>{}, bc<true>{}, ic<(DS > 2 ? 2 : -1)>{}, A1, B1, A0, B0, ra(st, 2), rb(st, 2));
-    step(bc<false>{}, bc<true>{}, ic<-1>{}, A0, B0, A1, B1, ra(st, 3), rb(st, 3));
+    if constexpr (NSTEP == 4) {
+      step(FIRSTc, bc<true>{}, ic<(DS > 1 ? 1 : -1)>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
+      step(bc<false>{}, bc<true>{}, ic<(DS > 2 ? 2 : -1)>{}, A1, B1, A0, B0, ra(st, 2), rb(st, 2));
+      step(bc<false>{}, bc<true>{}, ic<-1>{}, A0, B0, A1, B1, ra(st, 3), rb(st, 3));
+    } else {
+      step(FIRSTc, bc<true>{}, ic<-1>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
+    }
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -419,32 +446,33 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
   };
   auto bias_mfmas = [&]() {
     typedef __attribute__((ext_vector_type(4))) unsigned int w4_t;
-    float b[FN];
-    const uint32_t ba = bslot + (uint32_t)((wn * 32 * FN + l32) * 4);
-    static_assert(FN >= 2 && FN <= 5, "bias reads");
-    asm volatile("ds_read_b32 %0, %1 offset:0" : "=v"(b[0]) : "v"(ba));
-    asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(b[1]) : "v"(ba));
-    if constexpr (FN > 2) asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(b[2 % FN]) : "v"(ba));
-    if constexpr (FN > 3) asm volatile("ds_read_b32 %0, %1 offset:384" : "=v"(b[3 % FN]) : "v"(ba));
-    if constexpr (FN > 4) asm volatile("ds_read_b32 %0, %1 offset:512" : "=v"(b[4 % FN]) : "v"(ba));
+    float b[AN];  // column wn 32 FN + MF j + lane % MF of the tile
+    const uint32_t ba = bslot + (uint32_t)((wn * 32 * FN + (lane & (MF - 1))) * 4);
+    static_assert(AN >= 2 && AN <= 10, "bias reads");
+#define X5_BR(j) \
+  if constexpr ((j) < AN) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(b[(j) % AN]) : "v"(ba), "i"((j) * MF * 4))
+    X5_BR(0); X5_BR(1); X5_BR(2); X5_BR(3); X5_BR(4); X5_BR(5); X5_BR(6); X5_BR(7); X5_BR(8); X5_BR(9);
+#undef X5_BR
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
-    const uint32_t one2 = h == 0 ? 0x3F803F80u : 0u;  // bf16 (1, 1)
+    // the lanes holding k = 0 .. 7 of the operands: lanes 0-31 (32x32x16), 0-15 (16x16x32)
+    const bool k0 = MF == 16 ? lane < 16 : h == 0;
+    const uint32_t one2 = k0 ? 0x3F803F80u : 0u;  // bf16 (1, 1)
     const bf16x8 ones = __builtin_bit_cast(bf16x8, w4_t{one2, 0u, 0u, 0u});
-    bf16x8 bfr[FN];
+    bf16x8 bfr[AN];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
+    for (int j = 0; j < AN; ++j) {
       const float hi = bf2f(f2bf(b[j]));
-      const uint32_t wv = h == 0 ? pack2<BF16>(hi, b[j] - hi) : 0u;
+      const uint32_t wv = k0 ? pack2<BF16>(hi, b[j] - hi) : 0u;
       bfr[j] = __builtin_bit_cast(bf16x8, w4_t{wv, 0u, 0u, 0u});
     }
     // VALU-written MFMA operands: the wait states hipcc does not insert before an asm MFMA
-    asm volatile("s_nop 1" ::"v"(bfr[0]), "v"(bfr[FN - 1]), "v"(ones));
+    asm volatile("s_nop 1" ::"v"(bfr[0]), "v"(bfr[AN - 1]), "v"(ones));
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < AM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) mfma32_0(acc[i][j], bfr[j], ones);
+      for (int j = 0; j < AN; ++j) mfma32_0(acc[i][j], bfr[j], ones);
   };
 
   if (S > 0) {
@@ -491,39 +519,64 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
     const int c_n0 = __builtin_amdgcn_readfirstlane(tn * BN + 32 * FN * wn);
     {  // 32-bit offsets (the host checks (M + BM) * ldc * 2 < 2^31); a select, not a branch
       const bool in = c_n0 < g.N;
-      const uint32_t o0 = (uint32_t)(((c_m0 + l32) * (int)g.ldc + c_n0 + 8 * h) * 2);
-      const uint32_t blk = (uint32_t)(32 * (int)g.ldc * 2);
+      if constexpr (MF == 16) {
+        const int gq = lane >> 4;
+        const uint32_t o0 =
+            (uint32_t)(((c_m0 + (lane & 15)) * (int)g.ldc + c_n0 + 16 * (gq & 1) + 8 * (gq >> 1)) * 2);
+        const uint32_t blk = (uint32_t)(16 * (int)g.ldc * 2);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) c_vb[i] = in ? o0 + i * blk : 0x7ffff000u;
+        for (int i = 0; i < NCV; ++i) c_vb[i] = in ? o0 + i * blk : 0x7ffff000u;
+      } else {
+        const uint32_t o0 = (uint32_t)(((c_m0 + l32) * (int)g.ldc + c_n0 + 8 * h) * 2);
+        const uint32_t blk = (uint32_t)(32 * (int)g.ldc * 2);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) c_vb[i] = in ? o0 + i * blk : 0x7ffff000u;
+      }
       c_nl = g.N - c_n0;
     }
-    auto pack_row = [&](auto Ic) {  // fragments (i, 0 .. FN-1)
+    // store q = 2 (FN i + j) + p of the 16-byte vector v: straight out (first half of the rows,
+    // L2 absorbs it) or kept packed for the next tile's first units
+    auto put = [&](auto Qc, const u32x4& v) {
+      constexpr int qq = decltype(Qc)::value;
+      if constexpr (qq < NIM) X5_STV(qq, v);
+      else cst[qq - NIM] = v;
+    };
+    auto pack_row = [&](auto Ic) {  // 32-row block i, fragments (i, 0 .. FN-1)
       constexpr int i = decltype(Ic)::value;
+      sfor<FN>([&](auto Jc) {
+        constexpr int j = decltype(Jc)::value;
+        if constexpr (MF == 32) {
+          uint32_t pk[4][2];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        uint32_t pk[4][2];
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          pk[gq][0] = pack2<CDT>(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
-          pk[gq][1] = pack2<CDT>(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
-        }
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          // groups 2p (vdst) and 2p+1 (src): lanes 0-31 end with columns 16p + 0..7, lanes 32-63
-          // with 16p + 8..15 (T21)
-          auto r0 = __builtin_amdgcn_permlane32_swap(pk[2 * p][0], pk[2 * p + 1][0], false, false);
-          auto r1 = __builtin_amdgcn_permlane32_swap(pk[2 * p][1], pk[2 * p + 1][1], false, false);
-          const u32x4 v = u32x4{r0[0], r1[0], r0[1], r1[1]};
-          if constexpr (i < FM / 2) {
-            X5_STV(2 * (FN * i + j) + p, v);  // first half of the rows: straight out (L2 absorbs it)
-          } else {
-            cst[2 * (FN * i + j) + p - NIM] = v;
+          for (int gq = 0; gq < 4; ++gq) {
+            pk[gq][0] = pack2<CDT>(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
+            pk[gq][1] = pack2<CDT>(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
           }
+          sfor<2>([&](auto Pc) {
+            constexpr int p = decltype(Pc)::value;
+            // groups 2p (vdst) and 2p+1 (src): lanes 0-31 end with columns 16p + 0..7, lanes 32-63
+            // with 16p + 8..15 (T21)
+            auto r0 = __builtin_amdgcn_permlane32_swap(pk[2 * p][0], pk[2 * p + 1][0], false, false);
+            auto r1 = __builtin_amdgcn_permlane32_swap(pk[2 * p][1], pk[2 * p + 1][1], false, false);
+            put(ic<2 * (FN * i + j) + p>{}, u32x4{r0[0], r1[0], r0[1], r1[1]});
+          });
+        } else {
+          sfor<2>([&](auto I2c) {
+            constexpr int i2 = decltype(I2c)::value;
+            // 16-blocks X = (2i + i2, 2j) and Y = (.., 2j + 1): lane group g holds columns 4g .. 4g+3
+            // of each; the permlane16 swap (odd groups' vdst <-> even groups' src) leaves X's 0..7
+            // in group 0, Y's 0..7 in group 1, X's 8..15 in group 2, Y's 8..15 in group 3
+            const accT& X = acc[2 * i + i2][2 * j];
+            const accT& Y = acc[2 * i + i2][2 * j + 1];
+            auto r0 = __builtin_amdgcn_permlane16_swap(pack2<CDT>(X[0], X[1]), pack2<CDT>(Y[0], Y[1]), false, false);
+            auto r1 = __builtin_amdgcn_permlane16_swap(pack2<CDT>(X[2], X[3]), pack2<CDT>(Y[2], Y[3]), false, false);
+            put(ic<2 * (FN * i + j) + i2>{}, u32x4{r0[0], r1[0], r0[1], r1[1]});
+          });
         }
         // one fragment at a time: the accumulator reads of the next one are not hoisted (their
         // temporaries would need the registers the packed tile occupies)
         __builtin_amdgcn_sched_barrier(0);
-      }
+      });
     };
     sfor<FM>(pack_row);
   }
@@ -548,6 +601,10 @@ int x5_launch(int shape, int grid, const X5Args& g, hipStream_t s) {
     case 6: xgemm5_kernel<CDT, HASB, 2, 2, 4, 2><<<grid, 512, 0, s>>>(g); break;
     case 7: xgemm5_kernel<CDT, HASB, 2, 2, 2, 2><<<grid, 256, 0, s>>>(g); break;
     case 8: xgemm5_kernel<CDT, HASB, 2, 5, 4, 1><<<grid, 256, 0, s>>>(g); break;
+    case 9: xgemm5_kernel<CDT, HASB, 4, 4, 2, 2, 16><<<grid, 256, 0, s>>>(g); break;
+    case 10: xgemm5_kernel<CDT, HASB, 2, 5, 4, 1, 16><<<grid, 256, 0, s>>>(g); break;
+    case 11: xgemm5_kernel<CDT, HASB, 2, 4, 2, 2, 16><<<grid, 256, 0, s>>>(g); break;
+    case 12: xgemm5_kernel<CDT, HASB, 4, 2, 2, 2, 16><<<grid, 256, 0, s>>>(g); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -558,21 +615,23 @@ int x5_launch(int shape, int grid, const X5Args& g, hipStream_t s) {
 // wave: N = 768 in 5 column tiles, 495 tiles on 256 CUs = two nearly full rounds)
 int g_x5_shape = 0;   // diagnostics: force a tile shape (0 automatic)
 int g_x5_split = 0;   // diagnostics: force the row split with this tail shape (0 automatic)
-int g_x5_family = 4;  // automatic choice among shapes family .. family + 2
+// automatic choice: family f's shapes {256x256, 128x256, 256x128, 256x160}
+constexpr int kX5Fam[3][4] = {{1, 2, 3, 8}, {4, 5, 6, 8}, {9, 11, 12, 10}};
+int g_x5_family = 2;
 
 void x5_dims(int shape, int& bm, int& bn) {
-  bm = (shape == 2 || shape == 5 || shape == 7) ? 128 : 256;
-  bn = shape == 8 ? 160 : (shape == 3 || shape == 6 || shape == 7) ? 128 : 256;
+  bm = (shape == 2 || shape == 5 || shape == 7 || shape == 11) ? 128 : 256;
+  bn = (shape == 8 || shape == 10) ? 160 : (shape == 3 || shape == 6 || shape == 7 || shape == 12) ? 128 : 256;
 }
 
 }  // namespace
 
 // Diagnostics: force the tile shape of later rk_xgemm5 calls (0 = automatic; 1..7, see g_x5_shape);
-// 16 / 17: the automatic choice uses 4-wave / 8-wave tiles; 32 + t: force the row split with tail
-// shape t (32: automatic).
+// 16 + f: the automatic choice uses family f (0: 4-wave 32x32x16 tiles, 1: 8-wave, 2: 4-wave
+// 16x16x32); 32 + t: force the row split with tail shape t (32: automatic).
 RK_API int rk_xgemm5_set_shape(int s) {
   if (s >= 32) g_x5_split = s - 32;
-  else if (s >= 16) g_x5_family = s == 16 ? 1 : 4;
+  else if (s >= 16) g_x5_family = (s - 16) % 3;
   else g_x5_shape = s;
   return 0;
 }
@@ -611,22 +670,23 @@ RK_API int rk_xgemm5(const void* a, int64_t lda, const void* b, int64_t ldb, voi
   // Plan: one launch, or (when the 256x256 tiles leave the last CU round part-empty, e.g. ViT's
   // N = 768 products: 297 tiles on 256 CUs) the rows of the full rounds on 256x256 tiles and the
   // remaining rows on a smaller tile as a second launch.
-  int s1 = g_x5_shape == 8 && K < 384 ? 1 : g_x5_shape, s2 = 0, rows1 = M;
+  int s1 = (g_x5_shape == 8 || g_x5_shape == 10) && K < 384 ? 1 : g_x5_shape, s2 = 0, rows1 = M;
   if (s1 == 0) {
-    s1 = g_x5_family;
+    const int* fam = kX5Fam[g_x5_family];
+    s1 = fam[0];
     double best = cost(s1, M);
-    for (int t = g_x5_family + 1; t <= g_x5_family + 2; ++t)
-      if (cost(t, M) < best - 1e-9) { best = cost(t, M); s1 = t; }
-    if (K >= 384 && cost(8, M) < best - 1e-9) { best = cost(8, M); s1 = 8; }  // 256x160 needs U >= 6
+    for (int t = 1; t <= 2; ++t)
+      if (cost(fam[t], M) < best - 1e-9) { best = cost(fam[t], M); s1 = fam[t]; }
+    if (K >= 384 && cost(fam[3], M) < best - 1e-9) { best = cost(fam[3], M); s1 = fam[3]; }  // 256x160: U >= 6
     const int tn = (N + 255) / 256, full = ((M + 255) / 256) * tn;
     int r = full / ncu, r1 = (r * ncu / tn) * 256;
     if (g_x5_split > 0 && r1 <= 0) r1 = (M / 2) / 256 * 256;  // diagnostics on small problems
     if (r1 > 0 && r1 < M) {
-      const int cand[4] = {g_x5_family + 1, g_x5_family + 2, 7, 0};
+      const int cand[4] = {fam[1], fam[2], 7, 0};
       for (int ci = 0; cand[ci]; ++ci) {
         const int t = g_x5_split > 0 ? g_x5_split : cand[ci];
         const double c = (double)(((r1 / 256) * tn + ncu - 1) / ncu) + cost(t, M - r1) + 0.2;  // a launch's fill + drain
-        if (g_x5_split > 0 || c < best - 1e-9) { best = c; s1 = g_x5_family; s2 = t; rows1 = r1; }
+        if (g_x5_split > 0 || c < best - 1e-9) { best = c; s1 = fam[0]; s2 = t; rows1 = r1; }
         if (g_x5_split > 0) break;
       }
     }

@@ -12,5 +12,5 @@ timeout -k 10 300 python bench/gemm_r6_probe.py --out $O/probe.jsonl --shapes ${
 python3 - <<'PY'
 import json,os
 for l in open(os.environ.get('GRAFT_REPO_ROOT','.')+'/gpurun_out/r6d/probe.jsonl'):
-    r=json.loads(l); print(r['case'], 'lib', r['lib']['tflops'], 'x5', r['x5']['tflops'], r['x5_rel_err'], 'w4', r['x5_256x256']['tflops'], r['x5_128x256']['tflops'], r['x5_256x128']['tflops'], 'w8', r['w8_256x256']['tflops'], r['w8_128x256']['tflops'], r['w8_256x128']['tflops'])
+    r=json.loads(l); print(r['case'], 'lib', r['lib']['tflops'], 'x5', r['x5']['tflops'], r['x5_rel_err'], 'f0', r['f0']['tflops'], 'f1', r['f1']['tflops'], 's1', r['s1']['tflops'], 's8', r['s8']['tflops'], 's9', r['s9']['tflops'], 's10', r['s10']['tflops'])
 PY

@@ -31,9 +31,9 @@ def _run(a, b, c, bias, M, N, K, ldc=None):
     return rc
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8, 32 + 7, 32 + 5],
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 32 + 7, 32 + 5],
                 ids=["auto", "256x256", "128x256", "256x128", "w8-256x256", "w8-128x256", "w8-256x128", "128x128",
-                     "256x160",
+                     "256x160", "m16-256x256", "m16-256x160", "m16-128x256", "m16-256x128",
                      "split-128x128", "split-w8-128x256"])
 def x5_shape(request):
     """Tile shape of rk_xgemm5 (codes of rk_xgemm5_set_shape): every single-launch shape, and the
