@@ -47,7 +47,6 @@ namespace {
 
 constexpr int X5_BK = 64;     // a "unit": 64-deep k-slice, four k16 steps
 constexpr int X5_ROWB = X5_BK * 2;  // 128-byte image rows: every DMA piece reads whole cache lines
-constexpr int X5_NS = 2;            // LDS ring: 2 units
 #ifndef X5_DS
 #define X5_DS 2  // steps carrying a unit's DMA: the previous unit's last step + this many - 1 of its own
 #endif
@@ -184,8 +183,11 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
   constexpr int SPK = NPK / NSU;                      // per unit of those
   static_assert(SPK * NSU == NPK, "stores split over four or five units");
   using SC = X5Sched<AM, AN>;
-  // 2-stage ring + one 1-KiB bias row per wave (one __shared__ object: see the guide's trap 4(a))
-  __shared__ __attribute__((aligned(1024))) char smem[X5_NS * STAGE + NW * 1024];
+  // NS-stage ring + one 1-KiB bias row per wave (one __shared__ object: see the guide's trap 4(a))
+  // LDS ring of NS units: 3 where they fit beside the bias rows (a third unit in flight hides the
+  // HBM latency of operands that are not cache-resident, e.g. ViT's fc2 input), else 2
+  constexpr int NS = (x5_blocks_per_cu<FM, FN, WM, WN>() == 1 && 3 * STAGE + NW * 1024 <= 163840) ? 3 : 2;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE + NW * 1024];
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const int total = tiles_m * tiles_n;
   const int G = gridDim.x;
@@ -232,7 +234,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
   auto dma_begin = [&](int q) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const bool real = q < S;
-    d_st = smem + (q & (X5_NS - 1)) * STAGE;
+    d_st = smem + (q % NS) * STAGE;
     const int koff = iss_k * X5_ROWB;
     const char* pa = real ? ia + koff : (const char*)g.A;
     const char* pb = real ? ib + koff : (const char*)g.B;
@@ -391,12 +393,12 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
   //   steps 0-2: MFMAs || reads of the next step (this stage) || DMA groups 1 .. DS-1 of unit q + 1
   //   lgkmcnt(0) (this stage fully read) + vmcnt(0) (unit q + 1 landed: nothing younger is a DMA)
   //   + ONE barrier
-  //   step 3   : MFMAs || reads of step 0 of unit q + 1 || DMA group 0 of unit q + 2 into this
+  //   step 3   : MFMAs || reads of step 0 of unit q + 1 || DMA group 0 of unit q + NS into this
   //              unit's stage (freed by the barrier) || the previous tile's stores
   auto unit = [&](auto FIRSTc, auto SBc, auto LASTc, int q) {
     constexpr int SB = decltype(SBc)::value;
     constexpr bool LAST = decltype(LASTc)::value;
-    const int st = q & (X5_NS - 1);
+    const int st = q % NS;
     if constexpr (NSTEP == 4) {
       step(FIRSTc, bc<true>{}, ic<(DS > 1 ? 1 : -1)>{}, A0, B0, A1, B1, ra(st, 1), rb(st, 1));
       step(bc<false>{}, bc<true>{}, ic<(DS > 2 ? 2 : -1)>{}, A1, B1, A0, B0, ra(st, 2), rb(st, 2));
@@ -406,20 +408,21 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
     }
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // unit q + 1 landed: the only DMA younger than it is unit q + 2's (NS = 3)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NS - 2) * NDMA) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    dma_begin(q + 2);  // past the stream: an empty descriptor
+    dma_begin(q + NS);  // past the stream: an empty descriptor
     if constexpr (SB >= 0) {
 #pragma unroll
       for (int k = 0; k < SPK; ++k) X5_ST(SB + k);
     }
-    const int st1 = (q + 1) & (X5_NS - 1);
+    const int st1 = (q + 1) % NS;
     step(bc<false>{}, bc<!LAST>{}, ic<0>{}, A1, B1, A0, B0, ra(st1, 0), rb(st1, 0));
   };
   // the next k-tile's step-0 fragments, read after an epilogue (not held through the packing)
   auto rd0 = [&](int q) {
-    const uint32_t a = ra(q & (X5_NS - 1), 0), b = rb(q & (X5_NS - 1), 0);
+    const uint32_t a = ra(q % NS, 0), b = rb(q % NS, 0);
     sfor<SC::R>([&](auto Kc) { rd(A0, B0, a, b, Kc); });
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
@@ -428,7 +431,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
   // bias: each wave DMAs the tile's bias row (up to 256 floats) into its own 1-KiB LDS slot a tile
   // ahead (one VMEM instruction in the in-order stream: landed by the second k-tile's boundary
   // wait) and reads its lane's FN values from there (inline asm: no compiler-inserted vmcnt waits)
-  const uint32_t bslot = lds0 + X5_NS * STAGE + w * 1024;
+  const uint32_t bslot = lds0 + NS * STAGE + w * 1024;
   auto load_bias = [&](int ti) {
     if constexpr (HASB) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -438,7 +441,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
         const int left = (g.N - tn * BN) * 4;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(g.bias + tn * BN), (short)0, left, 0x00020000);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(smem + X5_NS * STAGE + w * 1024), 16,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(smem + NS * STAGE + w * 1024), 16,
                                                  (uint32_t)(lane * 16), 0, 0, 0);
       }
 #endif
@@ -477,12 +480,14 @@ __global__ void __launch_bounds__(64 * WM * WN, (x5_blocks_per_cu<FM, FN, WM, WN
 
   if (S > 0) {
     load_bias(0);  // before the DMAs: landed once unit 0 has
-    dma_begin(0);
+    for (int u = 0; u < NS - 1; ++u) {
+      dma_begin(u);
 #pragma unroll
-    for (int k = 0; k < NDMA; ++k) dma_one(k);
-    dma_begin(1);  // unit 1's group 0 now (steady state: issued in unit 0's predecessor's last step)
+      for (int k = 0; k < NDMA; ++k) dma_one(k);
+    }
+    dma_begin(NS - 1);  // its group 0 now (steady state: issued in unit 0's predecessor's last step)
     dma_group(ic<0>{});
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NDMA / DS) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NS - 2) * NDMA + NDMA / DS) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     rd0(0);
