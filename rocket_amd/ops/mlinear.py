@@ -33,7 +33,7 @@ from rocket_amd.ops.linear import native_route, _bf16_copy, _direct, _lowp_copy,
 from rocket_amd.ops.mgemm import mgemm, pick_split
 
 # Which engine runs each product.  ROCKET_VIT_GEMM:
-#   lib (default)  every product on the library GEMM (hipBLASLt with the shipped TunableOp table:
+#   lib            every product on the library GEMM (hipBLASLt with the shipped TunableOp table:
 #                  tuned 256-wide tiles, K-split strided-batched wgrad) - the fastest routing
 #                  measured in-model on 1x MI355X: ViT-B/16 5,058 img/s vs 4,629 hybrid and 4,290
 #                  native (profiles/r2_vit_gemm_routing.md);
@@ -53,7 +53,12 @@ from rocket_amd.ops.mgemm import mgemm, pick_split
 #                  copy), products it does not take (N % 128, K < 320: the classifier head) on mgemm;
 #                  weight gradients on mgemm (split-K over the tokens, bias gradient from the same
 #                  launch) - no library GEMM anywhere
-MODE = os.environ.get("ROCKET_VIT_GEMM", "lib")
+#   mixed (default) x5 for the products where it beat the library IN-MODEL (ViT-B/16, 1x MI355X,
+#                  profiles/r6_vit_gemm_inmodel.md): the forward and input gradient with >= 2048 output
+#                  features (256x256 tiles: qkv / fc1 forward, fc2 input gradient); the library for the
+#                  768-wide outputs and the weight gradients
+MODE = os.environ.get("ROCKET_VIT_GEMM", "mixed")
+_X5_WIDE = 2048  # mixed: output width from which the forward / input gradient runs on xgemm5
 # The transformer MLP's two GEMMs whose neighbours are streaming GELU passes run on the native 256x256
 # kernel (native/kernels/xgemm4.hip) with the GELU fused into their epilogues, beside any MODE:
 #   fc1 forward       z = x W1^T + b1 and h = gelu(z) from ONE launch (no gelu_fwd pass);
@@ -120,11 +125,15 @@ def _transposed16(w16: torch.Tensor) -> torch.Tensor:
 
 
 def _lib_fwd(K: int) -> bool:
-    return MODE in ("lib", "libw", "libd") or (MODE == "hybrid" and K < 2048)
+    return MODE in ("lib", "libw", "libd", "mixed") or (MODE == "hybrid" and K < 2048)
 
 
 def _lib_dgrad(N_in: int) -> bool:
-    return MODE in ("lib", "libw") or (MODE == "hybrid" and N_in > 2048)
+    return MODE in ("lib", "libw", "mixed") or (MODE == "hybrid" and N_in > 2048)
+
+
+def _x5_fwd(N: int, K: int, dtype: torch.dtype) -> bool:
+    return dtype == torch.bfloat16 and _x5_shape(N, K) and (MODE == "x5" or (MODE == "mixed" and N >= _X5_WIDE))
 
 
 def _ok(x: torch.Tensor, N: int, K: int) -> bool:
@@ -152,7 +161,7 @@ def _linear_fwd(x2: torch.Tensor, w16: torch.Tensor, bias: torch.Tensor, b16: to
         y = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
         mgemm(x2, w16, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, tile=_x_tile(M, N, x2.dtype))
         return y
-    if MODE == "x5" and x2.dtype == torch.bfloat16 and _x5_shape(N, K):
+    if _x5_fwd(N, K, x2.dtype):
         return _x5(x2, w16, bias, M, N, K)
     if _lib_fwd(K):
         return torch.addmm(b16, x2, w16.t())
@@ -171,7 +180,7 @@ def _linear_dgrad(dy2: torch.Tensor, w16: torch.Tensor, gelu_of: torch.Tensor | 
         dx = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
         mgemm(dy2, w16, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, b_kmaj=True, tile=_x_tile(M, K, dy2.dtype))
         return dx
-    if MODE == "x5" and dy2.dtype == torch.bfloat16 and _x5_shape(K, N) and gelu_of is None:
+    if gelu_of is None and _x5_fwd(K, N, dy2.dtype):
         return _x5(dy2, _transposed16(w16), None, M, K, N)
     if _lib_dgrad(K):
         assert gelu_of is None
@@ -188,7 +197,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
     engine provides them (returns None for those), else returned as new tensors."""
     M, N = dy.shape
     K = x.shape[1]
-    if MODE in ("lib", "libd"):
+    if MODE in ("lib", "libd", "mixed"):
         return lib_param_grads(dy, x, weight, bias, need_w, need_b)
     direct = (not need_w or _direct(weight)) and (not need_b or _direct(bias))
     if direct:
@@ -392,7 +401,7 @@ class _MMlpFn(torch.autograd.Function):
             # gelu'(z) and fc1's bias gradient in fc2's input-gradient GEMM epilogue
             dz, db1 = _x4_dgrad_gelu(dy2, w2_16, z, b1 if need_b1 else None)
             need_b1 = False
-        elif MODE in ("lib", "x5") and need_b1:
+        elif MODE in ("lib", "x5", "mixed") and need_b1:
             # GELU backward and fc1's bias gradient in one pass over the [tokens, hidden] gradient
             dz, db1 = _gelu_bwd_bias(_linear_dgrad(dy2, w2_16), z, b1)
             need_b1 = False
@@ -422,7 +431,7 @@ def _native(module: nn.Linear, x: torch.Tensor) -> bool:
     dt = _cdtype()
     # fp16: the library routes (hipBLASLt fp16 GEMMs beside the fp16 attention / LayerNorm / GELU
     # kernels) and the xgemm route; the mgemm routes are bf16-only
-    return (x.is_cuda and native_route() and (dt == torch.bfloat16 or (dt == torch.float16 and MODE in ("x", "lib", "x5")))
+    return (x.is_cuda and native_route() and (dt == torch.bfloat16 or (dt == torch.float16 and MODE in ("x", "lib", "x5", "mixed")))
             and module.weight.dtype == torch.float32 and module.weight.is_contiguous()
             and _ok(x, module.out_features, module.in_features))
 
