@@ -371,8 +371,9 @@ class DataParallel(nn.Module):
             if self._debug:
                 self._debug_check_launch(b)
             self._p2p.all_reduce_adam_(b.flat, 1.0 / self.comm.world, plan, advance=i == last)
+        # (the arming stays: one prepare can precede several captures — the loader ring's slots are
+        # captured together — and every one of them takes this path; graph_host disarms)
         opt.epilogue_done = True
-        opt.reduce_epilogue_armed = False
         self.fused_updates += 1
         return True
 

@@ -171,6 +171,7 @@ class StepGraphs:
         self.disabled_reason = None
         self.replays = 0
         self.captures = 0
+        self.sync_captures = 0  # captures of gradient-sync steps
         self._token = None
         self._checked = False
         self._rep = False  # resolved lazily (the module is wrapped during setup)
@@ -453,10 +454,10 @@ class StepGraphs:
         opts = [getattr(o, "optimizer", o) for o in getattr(self.mod._accelerator, "_optimizers", [])]
         flags = [(o, {f: getattr(o, f) for f in self._OPT_FLAGS if hasattr(o, f)}) for o in opts]
         return ((pend.done, pend.advanced) if pend is not None else None, flags, self.captures, self.parts,
-                self.launch_lists)
+                self.launch_lists, self.sync_captures)
 
     def _restore_side_effects(self, pend, side) -> None:
-        pstate, flags, self.captures, self.parts, self.launch_lists = side
+        pstate, flags, self.captures, self.parts, self.launch_lists, self.sync_captures = side
         if pend is not None:
             pend.done, pend.advanced = pstate
         for o, vals in flags:
@@ -516,6 +517,7 @@ class StepGraphs:
         # by a captured cursor-mode launch): every replay gathers the batch of its iteration
         v.rows_in_graph = pend is not None and pend.done
         self.captures += 1
+        self.sync_captures += int(v.sync)
         self.parts = max(self.parts, len(v.graphs))
         logger.info(f"captured HIP graph(s) for sync={v.sync} ({len(v.graphs)} part(s), mode={mode})")
         return v

@@ -120,6 +120,7 @@ def _worker(rank, world, port, out_dir, mode, model):
             w=float(sum(p.detach().double().sum() for p in net.parameters())),
             bufs=float(sum(b.detach().double().sum() for b in net.buffers())),
             replays=(mod._graphs.replays if mod._graphs is not None else 0),
+            sync_captures=(mod._graphs.sync_captures if mod._graphs is not None else 0),
             parts=(mod._graphs.parts if mod._graphs is not None else 0),
             mode=getattr(mod._module, "capture_mode", None),
             reason=(mod._graphs.disabled_reason if mod._graphs is not None else None),
@@ -169,7 +170,8 @@ def test_ddp_graph_two_ranks(tmp_path, mode, model):
         # and that equals all-reduce -> optimizer launch bit for bit (same sums, same update math)
         for rank in range(2):
             g, u = r[rank]["True"], r[rank]["unfused"]
-            assert g["fused"] > 0 and u["fused"] == 0, (g, u)
+            # every captured sync step (each loader-ring slot is its own capture) takes the fused path
+            assert g["fused"] > 0 and g["fused"] == g["sync_captures"] and u["fused"] == 0, (g, u)
             assert g["w"] == u["w"] and g["losses"] == u["losses"], (g, u)
     if model != "lenet":
         # BatchNorm statistics are rank 0's at the start of every synchronised forward (torch DDP's
