@@ -116,6 +116,10 @@ class Loss(Capsule):
     def graph_device(self, attrs: Attributes) -> None:
         engine = self._accelerator
         sync_here = engine.sync_gradients and not attrs.graph_split
+        # a data-parallel sync step whose all-reduce can also move the reduced accumulator into the
+        # ring (inline P2P): no bookkeeping launch of our own after the reduce
+        fold = attrs.get("fold_loss") if (engine.sync_gradients and attrs.get("graph_split")) else None
+        self._folded = bool(fold is not None and fold(self._acc, self._ring, self._slot))
         fused = getattr(self._objective, "loss_and_grad", None)
         scaler = engine.scaler
         dev_scale = getattr(scaler, "scale_tensor", None) if scaler is not None else None
@@ -140,7 +144,8 @@ class Loss(Capsule):
             engine.backward(loss)
 
     def graph_device_synced(self, attrs: Attributes) -> None:
-        if self._accelerator.sync_gradients and attrs.graph_split:
+        folded, self._folded = getattr(self, "_folded", False), False
+        if self._accelerator.sync_gradients and attrs.graph_split and not folded:
             _data_ops.loss_accum(self._zero, self._acc, self._ring, self._slot, 0.0, True)
 
     def graph_host(self, attrs: Attributes) -> None:

@@ -56,7 +56,21 @@ struct P2PArgs {
   uint64_t timeout_ticks;
   float scale;
   int rank, world;
+  // loss-ring fold (rk_p2p_set_loss_ring; lring null = none): element lidx of data is the step's
+  // loss accumulator (the side channel); its reduced value goes to lring[*lslot] (the slot advances,
+  // mod lsize) and the element is cleared -- the Loss capsule's separate bookkeeping launch
+  float* lring;
+  int64_t* lslot;
+  int64_t lidx;
+  int lsize;
 };
+
+__device__ __forceinline__ void loss_fold(const P2PArgs& a, float v) {
+  const int64_t k = a.lslot[0];
+  a.lring[k] = v;
+  a.lslot[0] = (k + 1) % a.lsize;
+  a.data[a.lidx] = 0.f;
+}
 
 __device__ __forceinline__ unsigned load_flag(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -143,7 +157,17 @@ __device__ __forceinline__ bool p2p_region(const P2PArgs& a, int b, unsigned& s_
       f32x4 s = v[u][0];
 #pragma unroll
       for (int r = 1; r < W; ++r) s += v[u][r];
-      out.vec(a.data, base + (int64_t)(u * kThreads + t) * kVec, s * a.scale);
+      const int64_t j = base + (int64_t)(u * kThreads + t) * kVec;
+      if (a.lring != nullptr && (uint64_t)(a.lidx - j) < (uint64_t)kVec) {  // the loss slot's vector
+        s *= a.scale;
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+          if (j + k == a.lidx) loss_fold(a, s[k]);
+          else out.one(a.data, j + k, s[k]);
+        }
+      } else {
+        out.vec(a.data, j, s * a.scale);
+      }
     }
   } else {
     for (int64_t j = base + t; j < a.n && j < base + kChunk; j += kThreads) {
@@ -153,7 +177,8 @@ __device__ __forceinline__ bool p2p_region(const P2PArgs& a, int b, unsigned& s_
       float s = v[0];
 #pragma unroll
       for (int r = 1; r < W; ++r) s += v[r];
-      out.one(a.data, j, s * a.scale);
+      if (a.lring != nullptr && j == a.lidx) loss_fold(a, s * a.scale);
+      else out.one(a.data, j, s * a.scale);
     }
   }
   if (t == 0) a.epoch[b] = ep;
@@ -262,6 +287,11 @@ struct P2PCtx {
   float* peer_stage[kMaxPeers] = {};
   unsigned* peer_flags[kMaxPeers] = {};
   bool mapped[kMaxPeers] = {};
+  // the next launch's loss-ring fold (rk_p2p_set_loss_ring), consumed by it
+  float* lf_ring = nullptr;
+  int64_t* lf_slot = nullptr;
+  int64_t lf_idx = -1;
+  int lf_size = 0;
 };
 
 constexpr int kHandleBytes = (int)sizeof(hipIpcMemHandle_t);
@@ -369,6 +399,14 @@ static int p2p_args(P2PCtx* c, float* data, int64_t n, float scale, P2PArgs& a) 
   a.timeout_ticks = (uint64_t)(c->timeout_s * (double)kTicksPerSecond);
   a.rank = c->rank;
   a.world = c->world;
+  if (c->lf_ring && c->lf_idx >= 0 && c->lf_idx < n) {
+    a.lring = c->lf_ring;
+    a.lslot = c->lf_slot;
+    a.lidx = c->lf_idx;
+    a.lsize = c->lf_size;
+  }
+  c->lf_ring = nullptr;  // one launch only
+  c->lf_idx = -1;
   return 0;
 }
 
@@ -422,6 +460,19 @@ RK_API int rk_p2p_allreduce_adam(void* ctx, float* data, int64_t n, float scale,
     default: p2p_allreduce_upd_kernel<8><<<blocks, kThreads, 0, s>>>(a, regions, u); break;
   }
   return (int)hipGetLastError();
+}
+
+// The NEXT all-reduce launch on this context also folds the loss bookkeeping in: element idx of
+// its buffer (the loss side channel) is averaged as usual, stored to ring[*slot], *slot advances
+// mod size, and the element is cleared.  ring / slot: device fp32 [size] / int64 [1].
+RK_API int rk_p2p_set_loss_ring(void* ctx, float* ring, int64_t* slot, int size, int64_t idx) {
+  if (!ctx || !ring || !slot || size < 1 || idx < 0) return (int)hipErrorInvalidValue;
+  auto* c = (P2PCtx*)ctx;
+  c->lf_ring = ring;
+  c->lf_slot = slot;
+  c->lf_size = size;
+  c->lf_idx = idx;
+  return 0;
 }
 
 // Peer-poll timeout of later launches (seconds; default 30).  The creation self-test uses a short one.

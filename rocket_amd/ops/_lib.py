@@ -152,6 +152,7 @@ KERNEL_SIGS = {
     "rk_p2p_error": (c_int, [c_void_p]),
     "rk_p2p_set_timeout": (c_int, [c_void_p, ctypes.c_double]),
     "rk_p2p_set_skip": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "rk_p2p_set_loss_ring": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64]),
     "rk_p2p_clear_error": (c_int, [c_void_p]),
     "rk_p2p_error_ptr": (c_void_p, [c_void_p]),
     "rk_p2p_destroy": (c_int, [c_void_p]),

@@ -148,6 +148,8 @@ class DataParallel(nn.Module):
         self._debug = os.environ.get("ROCKET_DEBUG_SYNC", "0") == "1"
         self._launched: List[int] = []
         self.fused_updates = 0  # captured sync steps whose P2P reduce applied the optimizer update
+        self._loss_fold = None  # (bucket, element, ring, slot) of the next inline P2P reduce (fold_loss_ring)
+        self.loss_folds = 0  # captured steps whose P2P reduce did the loss-ring bookkeeping
         # small models: one-shot xGMI all-reduce kernel (graph-capturable) instead of RCCL
         self._p2p = self._make_p2p()
         # native transport: per-bucket all-reduce on a side stream, one join before the optimizer
@@ -344,12 +346,41 @@ class DataParallel(nn.Module):
         finally:
             self._deferred = old
 
+    def fold_loss_ring(self, acc: torch.Tensor, ring: torch.Tensor, slot: torch.Tensor) -> bool:
+        """Inline P2P steps: the next :meth:`reduce_now` moves the reduced loss accumulator ``acc`` (a
+        side-slot view of a bucket) into ``ring[slot]``, advances ``slot`` and clears ``acc`` inside
+        the all-reduce launch (``rk_p2p_set_loss_ring``).  True when taken: the caller then skips its
+        own bookkeeping launch."""
+        if self._p2p is None or self.capture_mode != "inline" or acc.numel() != 1:
+            return False
+        p = acc.data_ptr()
+        for i, b in enumerate(self.buckets):
+            f = b.flat
+            lo = f.data_ptr()
+            if lo <= p < lo + f.numel() * f.element_size():
+                self._loss_fold = (i, (p - lo) // f.element_size(), ring, slot)
+                return True
+        return False
+
+    def _fold_for(self, i: int) -> None:
+        if self._loss_fold is not None and self._loss_fold[0] == i:
+            _, idx, ring, slot = self._loss_fold
+            self._p2p.set_loss_ring(ring, slot, idx)
+            self.loss_folds += 1
+
     def reduce_now(self) -> None:
         """Average every bucket (incl. the side channel) across ranks; stream-ordered, no host wait."""
         self._launched = []
-        if self._p2p is not None and self._reduce_with_update():
-            return
-        works = [self._launch(b) for b in self.buckets]
+        try:
+            if self._p2p is not None and self._reduce_with_update():
+                return
+            works = []
+            for i, b in enumerate(self.buckets):
+                if self._p2p is not None:
+                    self._fold_for(i)
+                works.append(self._launch(b))
+        finally:
+            self._loss_fold = None
         if self._native is not None:
             self._native.join()
         for w in works:
@@ -370,6 +401,7 @@ class DataParallel(nn.Module):
         for i, (b, plan) in enumerate(zip(self.buckets, plans)):
             if self._debug:
                 self._debug_check_launch(b)
+            self._fold_for(i)
             self._p2p.all_reduce_adam_(b.flat, 1.0 / self.comm.world, plan, advance=i == last)
         # (the arming stays: one prepare can precede several captures — the loader ring's slots are
         # captured together — and every one of them takes this path; graph_host disarms)

@@ -146,6 +146,13 @@ class P2PAllReduce:
         self.launches += 1
         self.check()  # a plain load of a host-mapped word: reports a timeout of any earlier launch
 
+    def set_loss_ring(self, ring: torch.Tensor, slot: torch.Tensor, idx: int) -> None:
+        """The NEXT launch also does the Loss capsule's ring bookkeeping for element ``idx`` of its
+        buffer (the loss side channel): ``ring[slot] = reduced value; slot = (slot + 1) % len(ring);
+        element = 0`` (``rk_p2p_set_loss_ring``) — one launch per data-parallel step fewer."""
+        _lib.check(_lib.kernels().rk_p2p_set_loss_ring(self._ctx, ring.data_ptr(), slot.data_ptr(), ring.numel(),
+                                                       int(idx)), "rk_p2p_set_loss_ring")
+
     def all_reduce_adam_(self, flat: torch.Tensor, scale: float, plan: tuple, advance: bool = True,
                          zero_grads: bool = True) -> None:
         """``all_reduce_`` whose write-back applies the Adam/AdamW update of the parameters whose

@@ -478,6 +478,8 @@ class StepGraphs:
         v.host_sync_buffers = v.sync and rep is not None and rep.broadcast_buffers and not overlap
         if v.host_sync_buffers:
             rep.sync_buffers()
+        if rep is not None and getattr(rep, "_loss_fold", None) is not None:
+            rep._loss_fold = None  # a fold registered by an abandoned capture
         if inline:
             rep.prepare_reduce()  # device tables of a reduce-with-update step: uploaded before capture
         if self.pool is None:
@@ -486,6 +488,8 @@ class StepGraphs:
         cap.batch = _rebuild(attrs.batch, iter(v.static_in))
         cap.capturing = True
         cap.graph_split = v.sync and rep is not None  # a cross-rank reduce separates device / device_synced
+        # inline P2P step: the loss capsule may hand its ring bookkeeping to the reduce launch
+        cap.fold_loss = rep.fold_loss_ring if (inline and hasattr(rep, "fold_loss_ring")) else None
         torch.cuda.synchronize()
         ga = torch.cuda.CUDAGraph(keep_graph=True)
         # thread_local: the RCCL watchdog thread keeps polling its events while we capture

@@ -116,6 +116,7 @@ def _worker(rank, world, port, out_dir, mode, model):
         rep = mod._module
         res[str(capture) if fuse else "unfused"] = dict(
             fused=getattr(rep, "fused_updates", 0),
+            loss_folds=getattr(rep, "loss_folds", 0),
             losses=[float(v) for v in rec.losses],
             w=float(sum(p.detach().double().sum() for p in net.parameters())),
             bufs=float(sum(b.detach().double().sum() for b in net.buffers())),
@@ -172,6 +173,8 @@ def test_ddp_graph_two_ranks(tmp_path, mode, model):
             g, u = r[rank]["True"], r[rank]["unfused"]
             # every captured sync step (each loader-ring slot is its own capture) takes the fused path
             assert g["fused"] > 0 and g["fused"] == g["sync_captures"] and u["fused"] == 0, (g, u)
+            # ... and its all-reduce also did the loss-ring bookkeeping (no separate launch), fused or not
+            assert g["loss_folds"] == g["sync_captures"] and u["loss_folds"] == u["sync_captures"] > 0, (g, u)
             assert g["w"] == u["w"] and g["losses"] == u["losses"], (g, u)
     if model != "lenet":
         # BatchNorm statistics are rank 0's at the start of every synchronised forward (torch DDP's
