@@ -23,7 +23,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from rocket_amd.ops.iconv import IConv2d, bn_relu_conv, conv_entry, stem_ok
-from rocket_amd.ops.linear import LibLinear, native_route
+from rocket_amd.ops.linear import native_route
+from rocket_amd.ops.mlinear import MLinear
 from rocket_amd.ops.norm import BatchNormAct2d
 from rocket_amd.ops.pool import global_avg_pool
 
@@ -103,10 +104,10 @@ class ResNet(nn.Module):
                 cin = width * block.expansion
             stages.append(nn.Sequential(*blocks))
         self.layer1, self.layer2, self.layer3, self.layer4 = stages
-        # nn.Linear on the library GEMM with an optimizer-kept 16-bit weight copy and a column-sum bias
-        # gradient straight into the fp32 grad (ops/linear.py LibLinear; plain nn.Linear when the
-        # class count is not a multiple of 8 or the fused kernels are off)
-        self.fc = LibLinear(cin, num_classes)
+        # nn.Linear on the native MFMA GEMM (ops/mlinear.py MLinear: the small-product route of the
+        # default GEMM routing; plain nn.Linear when the class count is not a multiple of 8 or the
+        # fused kernels are off)
+        self.fc = MLinear(cin, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")

@@ -55,10 +55,16 @@ from rocket_amd.ops.mgemm import mgemm, pick_split
 #                  launch) - no library GEMM anywhere
 #   mixed (default) x5 for the products where it beat the library IN-MODEL (ViT-B/16, 1x MI355X,
 #                  profiles/r6_vit_gemm_inmodel.md): the forward and input gradient with >= 2048 output
-#                  features (256x256 tiles: qkv / fc1 forward, fc2 input gradient); the library for the
-#                  768-wide outputs and the weight gradients
+#                  features (256x256 tiles: qkv / fc1 forward, fc2 input gradient) and mgemm for the
+#                  small products (classifier heads, <= 2^30 MACs); the library for the 768-wide outputs
+#                  and the weight gradients
 MODE = os.environ.get("ROCKET_VIT_GEMM", "mixed")
 _X5_WIDE = 2048  # mixed: output width from which the forward / input gradient runs on xgemm5
+_SMALL = 1 << 30  # mixed: products of at most this many MACs (classifier heads) run on mgemm
+
+
+def _small(M: int, N: int, K: int) -> bool:
+    return MODE == "mixed" and M * N * K <= _SMALL
 # The transformer MLP's two GEMMs whose neighbours are streaming GELU passes run on the native 256x256
 # kernel (native/kernels/xgemm4.hip) with the GELU fused into their epilogues, beside any MODE:
 #   fc1 forward       z = x W1^T + b1 and h = gelu(z) from ONE launch (no gelu_fwd pass);
@@ -163,7 +169,7 @@ def _linear_fwd(x2: torch.Tensor, w16: torch.Tensor, bias: torch.Tensor, b16: to
         return y
     if _x5_fwd(N, K, x2.dtype):
         return _x5(x2, w16, bias, M, N, K)
-    if _lib_fwd(K):
+    if _lib_fwd(K) and not _small(M, N, K):
         return torch.addmm(b16, x2, w16.t())
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
     mgemm(x2, w16, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, tile=_fwd_tile(N))
@@ -182,7 +188,7 @@ def _linear_dgrad(dy2: torch.Tensor, w16: torch.Tensor, gelu_of: torch.Tensor | 
         return dx
     if gelu_of is None and _x5_fwd(K, N, dy2.dtype):
         return _x5(dy2, _transposed16(w16), None, M, K, N)
-    if _lib_dgrad(K):
+    if _lib_dgrad(K) and not _small(M, N, K):
         assert gelu_of is None
         return dy2 @ w16
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy2.device)
@@ -197,7 +203,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
     engine provides them (returns None for those), else returned as new tensors."""
     M, N = dy.shape
     K = x.shape[1]
-    if MODE in ("lib", "libd", "mixed"):
+    if MODE in ("lib", "libd") or (MODE == "mixed" and not _small(M, N, K)):
         return lib_param_grads(dy, x, weight, bias, need_w, need_b)
     direct = (not need_w or _direct(weight)) and (not need_b or _direct(bias))
     if direct:

@@ -376,3 +376,32 @@ def test_mgemm_pingpong_epilogue():
     pre = torch.empty_like(c)
     mgemm(a, b, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, epi="gelu", c_pre=pre, tile=10)
     assert _rel(pre, z) < 5e-3 and _rel(c, F.gelu(z)) < 5e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(128, 1000, 768), (256, 1000, 2048)])
+def test_mlinear_small_head_native(M, N, K, monkeypatch):
+    """The default route's small products (classifier heads) run on mgemm: forward, input and
+    parameter gradients against fp32 torch on bf16-rounded operands."""
+    from rocket_amd.ops import mlinear
+
+    monkeypatch.setattr(mlinear, "MODE", "mixed")
+    assert mlinear._small(M, N, K)
+    torch.manual_seed(0)
+    m = mlinear.MLinear(K, N).cuda()
+    x = (torch.randn(M, K, device="cuda") * 0.5).requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    g = torch.randn_like(y.float())
+    y.float().backward(g)
+    xr = x.detach().bfloat16().float().requires_grad_()
+    wr = m.weight.detach().bfloat16().float().requires_grad_()
+    br = m.bias.detach().float().requires_grad_()
+    yr = xr @ wr.t() + br
+    yr.backward(g)
+    scale = yr.abs().max().item()
+    assert (y.float() - yr).abs().max().item() <= 2e-2 * scale
+    assert (x.grad - xr.grad).abs().max().item() <= 2e-2 * xr.grad.abs().max().item()
+    assert (m.weight.grad - wr.grad).abs().max().item() <= 2e-2 * wr.grad.abs().max().item()
+    assert (m.bias.grad - br.grad).abs().max().item() <= 2e-2 * br.grad.abs().max().item()
+
