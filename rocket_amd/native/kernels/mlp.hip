@@ -288,6 +288,7 @@ struct LossFin {
   int sync;
 };
 struct WgradArgs {
+  int late_ticket;  // LDS-staged dW tile blocks take the optimizer-step ticket after their operand wait
   uint64_t* trace;  // optional phase stamps [blocks][8] (s_memrealtime): start, reduced, end, tile: old values in, main loop done
   float gscale;     // every produced gradient is scaled by this (the upstream gradient factor)
   // normalisation by a count the backward left unapplied (the fused LeNet cross-entropy's mean,
@@ -458,7 +459,7 @@ static_assert(WEPT >= 1 && WTN * 32 % NT == 0, "tile elements per thread");
 
 template <bool LDSV>
 __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks,
-                           const StepFill& sf, char* stage);
+                           const StepFill& sf, char* stage, unsigned* ticket);
 
 // LDSV: the tiles' operands arrive by LDS-DMA in whole 256-B row segments (16 KiB per wave: its 32 rows
 // of d^T and x^T over its 128 batch elements) and the MFMA fragments are read back from LDS, instead of
@@ -480,8 +481,11 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
   // tail waited one agent-scope atomic round trip).  Every block has read `cur` long before: the
   // last block's store comes after its whole tile, microseconds after all tickets (and the loads
   // issued before them) were taken.
+  // (an LDS-staged dW tile block takes it later, right after its operands landed: taken here, the
+  // atomic's round trip on the one contended counter sat inside that block's operand wait)
   unsigned ticket = 0;
-  if (a.epi.on && threadIdx.x == 0)
+  const bool late_ticket = LDSV && a.late_ticket && !(a.has_rows && (int)blockIdx.x == (int)gridDim.x - 1) && (int)blockIdx.x < a.tiles;
+  if (a.epi.on && threadIdx.x == 0 && !late_ticket)
     ticket = __hip_atomic_fetch_add(a.epi.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float cpart = 0.f;
   if (a.cnt_parts)
@@ -499,7 +503,7 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
     if ((int)blockIdx.x - a.tiles < a.nslab) slab_reduce_block(a, blockIdx.x - a.tiles, red, ks, sf);
     else loss_fin_block(a.lf, red, sf);
   } else {
-    wgrad_tile<LDSV>(a, red, rsum, ks, sf, stage);
+    wgrad_tile<LDSV>(a, red, rsum, ks, sf, stage, late_ticket ? &ticket : nullptr);
   }
   if (a.epi.on && threadIdx.x == 0 && ticket == gridDim.x - 1) {
     a.epi.step[0] = cur + 1.f;
@@ -510,7 +514,7 @@ __global__ void __launch_bounds__(NT) mlp3_wgrad_kernel(WgradArgs a) {
 
 template <bool LDSV>
 __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rsum)[32], const rk_opt::AdamStep* ks,
-                           const StepFill& sf, char* stage) {
+                           const StepFill& sf, char* stage, unsigned* ticket) {
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < 3; ++i)
@@ -563,6 +567,10 @@ __device__ void wgrad_tile(const WgradArgs& a, float (*red)[32 * 32], float (*rs
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("" ::: "memory");
+    // the optimizer step's ticket (see the kernel): its round trip overlaps the MFMAs and the
+    // reduction; the value is needed only at the block's end
+    if (ticket && a.epi.on && threadIdx.x == 0)
+      *ticket = __hip_atomic_fetch_add(a.epi.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       bf16x8 af[WNI], bf[2];
@@ -755,6 +763,8 @@ RK_API int RKL_NAME(rk_mlp3_wgrad_loss)(int nprob, const void* const* dT, const 
   if (nprob < 1 || nprob > 3 || (M & 7)) return (int)hipErrorInvalidValue;
   WgradArgs a{};
   a.trace = g_wgrad_trace;
+  static const int late_env = getenv("ROCKET_WGRAD_LATE_TICKET") ? atoi(getenv("ROCKET_WGRAD_LATE_TICKET")) : 1;
+  a.late_ticket = late_env;
   a.gscale = gscale;
   a.amp_found = amp_found;
   if (norm_by_count) {  // count partials follow the loss partials: partials[nparts .. 2 nparts)

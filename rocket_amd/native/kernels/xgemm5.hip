@@ -4,38 +4,41 @@
 // Why this kernel: the one-wave-per-SIMD 256x256 tile (xgemm4.hip) runs its K = 768 main loop at
 // ~20 us per tile but then spends ~8 us storing the tile, with every CU storing at once (32 MiB in
 // one burst, HBM-write bound), plus a 2 us pipeline fill per tile and wave quantisation
-// (profiles/r5_x4_trace.md).  Here:
+// (profiles/r5_x4_trace.md).  Here (measurements: profiles/r6_vit_gemm_inmodel.md):
 //
-// * persistent: one block per CU walks its tiles pos, pos + G, ... (XCD-aware remap + grouped
-//   order); the LDS-DMA k-tile stream runs ACROSS tiles, so the next tile's first two k-tiles are
-//   already landing while the current one finishes (no per-tile prologue);
-// * 32x32x16 MFMAs, WM x WN waves, each FM x FN fragments of 32 x 32 (accumulators in the
-//   accumulator registers).  Two layouts per tile size: 4 waves (2 x 2, one per SIMD, 4 x 4
-//   fragments at 256 x 256) and 8 waves (two per SIMD, 4 x 2 fragments at 256 x 256).  A wave's
-//   vector-memory instructions stall its own issue for tens of cycles each (the LDS-DMA pieces: with
-//   them removed the 4-wave loop ran 27% faster, and register-path loads cost the same); with two
-//   waves per SIMD the partner's MFMAs fill those gaps.  One k16 step needs FM + FN fragments (4
-//   VGPRs each); two fragment sets leave room for the finished tile PACKED to 16-bit in VGPRs;
-// * epilogue = pack only (accumulators -> 16-bit, lane halves swapped with permlane32 so every store
-//   is 16 B per lane, T21).  The first half of the wave's rows is stored at once; the second half
-//   stays packed and is stored over the next tile's first four k-tiles, as inline-asm buffer
-//   stores (out-of-range lanes point past the descriptor's record count, so every store instruction
-//   issues and the vmcnt counts below stay static);
+// * persistent: one block per CU (two for 128 x 128 tiles) walks its tiles pos, pos + G, ...
+//   (XCD-aware remap + grouped order); the LDS-DMA unit stream runs ACROSS tiles, so the next
+//   tile's first units are already landing while the current one finishes (no per-tile prologue);
+// * a "unit" is a 64-deep k-slice of both operand panels, staged by LDS-DMA in WHOLE CACHE LINES:
+//   each 1-KiB piece is 8 rows x 128 B (the round-6 start used 16 rows x 64 B, half lines: the
+//   ablations put 27% of the loop on those loads, and 128-B pieces took it back); 16-byte chunk c
+//   of image row r sits at c ^ swz8(r) (swizzle applied to the source address, the LDS image is
+//   lane-linear), so every ds_read_b128 fragment read is conflict-free;
+// * an NS-unit LDS ring (3 where it fits in 160 KiB with the bias rows, else 2) with counted
+//   vmcnt waits and ONE barrier per unit; a unit's DMA is issued after that barrier into the stage
+//   it freed, spread over the step's MFMAs;
+// * MFMA shape MF: 32x32x16 (four k16 steps per unit) or 16x16x32 (two k32 steps: same FLOP per
+//   cycle, the chip holds a higher clock on it); WM x WN waves of FM x FN 32 x 32 blocks each
+//   (accumulators in AGPRs), fragment reads front-loaded into the other register set with
+//   lgkmcnt waits counted per MFMA (X5Sched);
+// * epilogue = pack only (accumulators -> 16-bit; permlane32 / permlane16 swaps so every store is
+//   16 B per lane, T21).  The first half of the wave's rows is stored at once; the second half stays
+//   packed and is stored over the next tile's first units, as inline-asm buffer stores
+//   (out-of-range lanes point past the descriptor's record count, so every store instruction issues
+//   and the vmcnt counts stay static; 160-wide tiles also mask 32-column blocks past N);
 // * bias as a rank-2 update INSIDE the MFMAs: the tile's first MFMAs multiply a fragment holding
 //   (hi, lo) = (bf16(b), bf16(b - hi)) at k = 0, 1 by a fragment of ones (b to 2^-16 relative, in
 //   f32 before any product; no epilogue work and no per-column loads there);
-// * tile shape per problem (host): 256 x 256 (FM = FN = 4), or 128 x 256 / 256 x 128 where the
-//   256-wide tiles would leave the last round of CUs mostly idle (ViT's N = 768 products: 297
-//   tiles on 256 CUs).
+// * tile shape per problem (host): 256 x 256, 128 x 256, 256 x 128, 128 x 128 or 256 x 160 (ViT's
+//   N = 768 in five column tiles: 495 tiles on 256 CUs instead of 297), by CU rounds, or a
+//   two-launch row split (full rounds of 256 x 256 tiles, the remaining rows on a smaller tile).
 //
-// Per unit (32 deep; 4-stage LDS ring; image [rows][32] bf16 per operand, 16-byte chunk c of row r
-// at c ^ rswz(r)); a unit's DMA is split in two parts issued in two different units' steps:
-//   step 0   : FM FN MFMAs on fragment set 0  ||  the FM + FN reads of step 1 (front-loaded, ordered
-//              by first use, counted lgkmcnt waits)  ||  second part of unit q + 3's DMA
-//              (+ the previous tile's pending stores in the first four units);
-//   boundary : lgkmcnt(0); vmcnt(2 NDMA) = unit q + 1 landed; ONE barrier;
-//   step 1   : MFMAs on set 1  ||  reads of step 0 of unit q + 1  ||  first part of unit q + 4's DMA
-//              into this unit's stage (freed by the barrier).
+// Per unit q (stage q % NS):
+//   steps 0 .. NSTEP-2 : MFMAs on one fragment set || the next step's reads into the other set ||
+//                        the remaining DMA groups of unit q + 1 (32x32x16 only)
+//   boundary           : lgkmcnt(0) (this stage fully read); vmcnt = unit q + 1 landed; ONE barrier
+//   last step          : MFMAs || reads of unit q + 1's first step || DMA group 0 of unit q + NS into
+//                        this unit's stage || the previous tile's pending stores
 // vmcnt counts rely on vector-memory ops completing in issue order (DMA loads and stores alike).
 #include "mgemm_core.h"
 
@@ -147,7 +150,6 @@ struct X5Args {
   const float* bias;
   int64_t lda, ldb, ldc;
   int M, N, K, c_dt;
-  int dbg;  // unused (the round-6 ablation bits are gone: runtime branches inside the MFMA code made the allocator spill)
 };
 
 // 128x128 tiles (68 KiB of LDS) run two blocks per CU: one block's DMA issue and fill/drain
@@ -701,7 +703,7 @@ RK_API int rk_xgemm5(const void* a, int64_t lda, const void* b, int64_t ldb, voi
     x5_dims(shape, bm, bn);
     const int grid = std::min(((rows + bm - 1) / bm) * ((N + bn - 1) / bn), shape == 7 ? 2 * ncu : ncu);
     X5Args g{(const uint16_t*)a + (int64_t)r0 * lda, (const uint16_t*)b, (char*)c + (int64_t)r0 * ldc * 2, bias,
-             lda, ldb, ldc, rows, N, K, c_dt, 0};
+             lda, ldb, ldc, rows, N, K, c_dt};
     if (c_dt == F16) return bias ? x5_launch<F16, true>(shape, grid, g, s) : x5_launch<F16, false>(shape, grid, g, s);
     return bias ? x5_launch<BF16, true>(shape, grid, g, s) : x5_launch<BF16, false>(shape, grid, g, s);
   };
