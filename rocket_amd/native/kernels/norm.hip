@@ -1049,13 +1049,20 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const TO* __restrict__ dy,
   // consecutive lanes: whole bank rows), then each thread sums the 4 waves' values of its columns
   // (per-wave images instead of LDS atomics into one: the atomics' per-block cost measured higher
   // than the 4x LDS footprint, bench/ln_probe.py)
+  // k-major image: column 4q + k at k (C / 4) + q, so a wave's 4-byte stores cover consecutive
+  // words (the 16-byte stores of the natural order measured 60% SQ_LDS_BANK_CONFLICT); the block
+  // partial keeps that order and colsum_kernel maps it back (perm_q = C / 4)
+  const int cq = C / 4;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const int c = (j * 64 + lane) * 4;
-    if (c < C) {
-      *(float4*)&sm[(w * NP) * C + c] = make_float4(ag[j][0], ag[j][1], ag[j][2], ag[j][3]);
-      *(float4*)&sm[(w * NP + 1) * C + c] = make_float4(ab[j][0], ab[j][1], ab[j][2], ab[j][3]);
-      if (NP == 3) *(float4*)&sm[(w * NP + 2) * C + c] = make_float4(ar[j][0], ar[j][1], ar[j][2], ar[j][3]);
+    const int q = j * 64 + lane;
+    if (4 * q < C) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sm[(w * NP) * C + k * cq + q] = ag[j][k];
+        sm[(w * NP + 1) * C + k * cq + q] = ab[j][k];
+        if (NP == 3) sm[(w * NP + 2) * C + k * cq + q] = ar[j][k];
+      }
     }
   }
   __syncthreads();
@@ -1657,7 +1664,7 @@ RK_API int rk_ln_bwd(int dt, int dto, const void* dy, const void* x, const float
 #undef RK_LBN
 #undef RK_LB
   if (dgamma || dbeta || dres_sum)
-    colsum_kernel<<<(np * C + 63) / 64, CS_T, 0, s>>>(ws, grid, np * C, dgamma, dbeta, C, dres_sum, 0, dres_acc);
+    colsum_kernel<<<(np * C + 63) / 64, CS_T, 0, s>>>(ws, grid, np * C, dgamma, dbeta, C, dres_sum, C / 4, dres_acc);
   (void)counter;
   return (int)hipGetLastError();
 }
