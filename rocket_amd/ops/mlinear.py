@@ -63,8 +63,9 @@ _X5_WIDE = 2048  # mixed: output width from which the forward / input gradient r
 _SMALL = 1 << 30  # mixed: products of at most this many MACs (classifier heads) run on mgemm
 
 
-def _small(M: int, N: int, K: int) -> bool:
-    return MODE == "mixed" and M * N * K <= _SMALL
+def _small(M: int, N: int, K: int, dtype: torch.dtype) -> bool:
+    """mixed: a small bf16 product (classifier head) for mgemm (bf16 operands only)."""
+    return MODE == "mixed" and dtype == torch.bfloat16 and M * N * K <= _SMALL
 # The transformer MLP's two GEMMs whose neighbours are streaming GELU passes run on the native 256x256
 # kernel (native/kernels/xgemm4.hip) with the GELU fused into their epilogues, beside any MODE:
 #   fc1 forward       z = x W1^T + b1 and h = gelu(z) from ONE launch (no gelu_fwd pass);
@@ -169,7 +170,7 @@ def _linear_fwd(x2: torch.Tensor, w16: torch.Tensor, bias: torch.Tensor, b16: to
         return y
     if _x5_fwd(N, K, x2.dtype):
         return _x5(x2, w16, bias, M, N, K)
-    if _lib_fwd(K) and not _small(M, N, K):
+    if _lib_fwd(K) and not _small(M, N, K, x2.dtype):
         return torch.addmm(b16, x2, w16.t())
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
     mgemm(x2, w16, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias, tile=_fwd_tile(N))
@@ -188,7 +189,7 @@ def _linear_dgrad(dy2: torch.Tensor, w16: torch.Tensor, gelu_of: torch.Tensor | 
         return dx
     if gelu_of is None and _x5_fwd(K, N, dy2.dtype):
         return _x5(dy2, _transposed16(w16), None, M, K, N)
-    if _lib_dgrad(K) and not _small(M, N, K):
+    if _lib_dgrad(K) and not _small(M, N, K, dy2.dtype):
         assert gelu_of is None
         return dy2 @ w16
     dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy2.device)
@@ -203,7 +204,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, bias: torch.
     engine provides them (returns None for those), else returned as new tensors."""
     M, N = dy.shape
     K = x.shape[1]
-    if MODE in ("lib", "libd") or (MODE == "mixed" and not _small(M, N, K)):
+    if MODE in ("lib", "libd") or (MODE == "mixed" and not _small(M, N, K, dy.dtype)):
         return lib_param_grads(dy, x, weight, bias, need_w, need_b)
     direct = (not need_w or _direct(weight)) and (not need_b or _direct(bias))
     if direct:
@@ -437,7 +438,7 @@ def _native(module: nn.Linear, x: torch.Tensor) -> bool:
     dt = _cdtype()
     # fp16: the library routes (hipBLASLt fp16 GEMMs beside the fp16 attention / LayerNorm / GELU
     # kernels) and the xgemm route; the mgemm routes are bf16-only
-    return (x.is_cuda and native_route() and (dt == torch.bfloat16 or (dt == torch.float16 and MODE in ("x", "lib", "x5", "mixed")))
+    return (x.is_cuda and native_route() and (dt == torch.bfloat16 or (dt == torch.float16 and MODE in ("x", "lib", "mixed")))
             and module.weight.dtype == torch.float32 and module.weight.is_contiguous()
             and _ok(x, module.out_features, module.in_features))
 
