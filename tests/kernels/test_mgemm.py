@@ -386,7 +386,7 @@ def test_mlinear_small_head_native(M, N, K, monkeypatch):
     from rocket_amd.ops import mlinear
 
     monkeypatch.setattr(mlinear, "MODE", "mixed")
-    assert mlinear._small(M, N, K)
+    assert mlinear._small(M, N, K, torch.bfloat16)
     torch.manual_seed(0)
     m = mlinear.MLinear(K, N).cuda()
     x = (torch.randn(M, K, device="cuda") * 0.5).requires_grad_()
