@@ -74,6 +74,11 @@ struct ConvGeom {
                          // the three odd-parity neighbours of each of their pixels
   int st_nt;             // row-chunk tile stores (store_tile_lds) nontemporal (ROCKET_CONV_NT)
   DgCls cls[4];
+  // tail-reduce job (rk_conv_defer_reduce): the split-K combine of a preceding weight gradient, run
+  // by tr_blocks extra blocks appended to this launch (mgemm_core.h reduce_slabs; dW[tr_M][tr_N] f32)
+  const float* tr_slab;
+  float* tr_c;
+  int tr_splitk, tr_M, tr_N, tr_acc, tr_blocks, tr_g4;
 };
 
 // (n, gh, gw) of grid pixel m (exact for m < 2^24 after the correction steps)
@@ -610,7 +615,19 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) conv_kernel(M
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE_BYTES];
   __shared__ __attribute__((aligned(16))) float pro_tab[PL ? 2 * kProMaxC : 4];  // [scale C][shift C]
 
-  int lin = xcd_remap(blockIdx.x, gridDim.x);
+  if (cg0.tr_blocks) {  // appended blocks: the deferred split-K combine (independent of the tiles)
+    const int nmain = (int)gridDim.x - cg0.tr_blocks;
+    if ((int)blockIdx.x >= nmain) {
+      if (cg0.tr_g4)
+        reduce_slabs<4>(cg0.tr_slab, cg0.tr_splitk, cg0.tr_M, cg0.tr_N, nullptr, cg0.tr_c, F32, cg0.tr_N, cg0.tr_acc,
+                        (int)blockIdx.x - nmain, cg0.tr_blocks, 64 * NW);
+      else
+        reduce_slabs<1>(cg0.tr_slab, cg0.tr_splitk, cg0.tr_M, cg0.tr_N, nullptr, cg0.tr_c, F32, cg0.tr_N, cg0.tr_acc,
+                        (int)blockIdx.x - nmain, cg0.tr_blocks, 64 * NW);
+      return;
+    }
+  }
+  int lin = xcd_remap(blockIdx.x, (int)gridDim.x - cg0.tr_blocks);
   ConvGeom cg = cg0;
   int r0y = 0, r0x = 0;
   ClsRow crow = {};
@@ -829,20 +846,53 @@ int conv_tiles(const MArgs& g, const ConvGeom& cg, int bm, int bn) {
 
 int g_conv_cfg = 0;  // rk_conv_set_cfg: k-tile pipeline of the bf16 kernels
 
+// The deferred split-K combine of the last rk_conv_wgrad (rk_conv_defer_reduce(1)): the next conv
+// launch on the same stream runs it in appended blocks (the stride-1 dgrad of the same backward:
+// iconv.py issues the wgrad first), rk_conv_flush_reduce launches it on its own otherwise.  One
+// launch and its ~5 us floor fewer per ResNet conv backward, the combine overlapping the dgrad's
+// last wave.  Host-side state, one pending job (the backward issues its launches in order).
+struct TailJob {
+  const float* slab = nullptr;
+  float* c = nullptr;
+  int splitk = 0, M = 0, N = 0, acc = 0;
+  hipStream_t s = nullptr;
+  bool pending = false;
+};
+TailJob g_tail;
+int g_defer_reduce = 0;
+int64_t g_tail_attached = 0, g_tail_flushed = 0;  // rk_conv_tail_counts (tests)
+
+void attach_tail(ConvGeom& cg, hipStream_t s, int nt) {
+  cg.tr_blocks = 0;
+  if (!g_tail.pending || g_tail.s != s) return;
+  const int64_t nq = (int64_t)g_tail.M * g_tail.N / 4;
+  const int G = g_tail.splitk >= 8 ? 4 : 1;
+  cg.tr_slab = g_tail.slab; cg.tr_c = g_tail.c; cg.tr_splitk = g_tail.splitk;
+  cg.tr_M = g_tail.M; cg.tr_N = g_tail.N; cg.tr_acc = g_tail.acc; cg.tr_g4 = G == 4;
+  cg.tr_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((nq * G + nt - 1) / nt, 1024));
+  g_tail.pending = false;
+  ++g_tail_attached;
+}
+
 template <int MODE, bool H, int BK, int NS, int OCC, int WN128 = 4, bool PRO = false>
-int launch_conv_p(const MArgs& g, const ConvGeom& cg, hipStream_t s) {
+int launch_conv_p(const MArgs& g, const ConvGeom& cg_in, hipStream_t s) {
   // (the forward's wave row slice is 64 pixels in every variant: the BatchNorm partials rely on it)
   // 64-wide GEMM side (Cout / Cin = 64 layers): a 64-wide tile with 4 waves instead of half an
   // empty 128-wide one; everything else 128 x 128 with 8 waves
+  ConvGeom cg = cg_in;
   if (MODE != kConvWgrad && g.N <= 64) {
     const int tiles = conv_tiles<MODE>(g, cg, 128, 64);
-    conv_kernel<MODE, 128, 64, 2, 2, H, BK, NS, OCC, PRO><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+    attach_tail(cg, s, 256);
+    conv_kernel<MODE, 128, 64, 2, 2, H, BK, NS, OCC, PRO><<<tiles * g.splitk + cg.tr_blocks, 256, 0, s>>>(g, cg);
   } else if (MODE == kConvWgrad && g.M <= 64) {
     const int tiles = ((g.M + 63) / 64) * ((g.N + 127) / 128);
-    conv_kernel<MODE, 64, 128, 2, 2, H, BK, NS, OCC, PRO><<<tiles * g.splitk, 256, 0, s>>>(g, cg);
+    attach_tail(cg, s, 256);
+    conv_kernel<MODE, 64, 128, 2, 2, H, BK, NS, OCC, PRO><<<tiles * g.splitk + cg.tr_blocks, 256, 0, s>>>(g, cg);
   } else {
     const int tiles = conv_tiles<MODE>(g, cg, 128, 128);
-    conv_kernel<MODE, 128, 128, 2, WN128, H, BK, NS, OCC, PRO><<<tiles * g.splitk, 128 * WN128, 0, s>>>(g, cg);
+    attach_tail(cg, s, 128 * WN128);
+    conv_kernel<MODE, 128, 128, 2, WN128, H, BK, NS, OCC, PRO>
+        <<<tiles * g.splitk + cg.tr_blocks, 128 * WN128, 0, s>>>(g, cg);
   }
   return (int)hipGetLastError();
 }
@@ -878,6 +928,8 @@ ConvGeom geom(int N, int H, int W, int C, int GH, int GW, int R, int S, int stri
   cg.bnb_x = nullptr; cg.bnb_mask = nullptr; cg.bnb_mean = nullptr; cg.bnb_invstd = nullptr; cg.bnb_part = nullptr;
   cg.pro_ss = nullptr; cg.bnb_ss = nullptr;
   cg.hoff = cg.woff = pad; cg.dx_h = cg.dx_w = 0; cg.w_s = S; cg.ncls = 0; cg.zero_nb = 0;
+  cg.tr_slab = nullptr; cg.tr_c = nullptr;
+  cg.tr_splitk = cg.tr_M = cg.tr_N = cg.tr_acc = cg.tr_blocks = cg.tr_g4 = 0;
   // the tile's outputs stream to HBM (ResNet activations are far larger than L2) and their next
   // reader is another launch: nontemporal stores (ROCKET_CONV_NT=0: plain)
   static const int nt = getenv("ROCKET_CONV_NT") ? atoi(getenv("ROCKET_CONV_NT")) : 1;
@@ -1108,6 +1160,35 @@ RK_API int rk_conv_wgrad(int dt, const void* dy, const void* x, float* dw, int a
   cg.pro_ss = pro;
   int rc = launch_conv<kConvWgrad>(g, cg, dt, s);
   if (rc || splitk == 1) return rc;
+  if (g_defer_reduce) {  // the next conv launch on this stream (or rk_conv_flush_reduce) combines
+    g_tail.slab = slab; g_tail.c = dw; g_tail.splitk = splitk; g_tail.M = Cout; g_tail.N = Ncol;
+    g_tail.acc = accumulate; g_tail.s = s; g_tail.pending = true;
+    return 0;
+  }
   launch_mgemm_reduce(slab, splitk, Cout, Ncol, nullptr, dw, F32, Ncol, accumulate, s);
+  return (int)hipGetLastError();
+}
+
+// 1: the next rk_conv_wgrad leaves its split-K combine to the following conv launch (TailJob)
+RK_API int rk_conv_defer_reduce(int on) {
+  g_defer_reduce = on;
+  return 0;
+}
+
+// deferred combines run by a conv launch's appended blocks / flushed on their own, since load
+RK_API int rk_conv_tail_counts(int64_t* out) {
+  out[0] = g_tail_attached;
+  out[1] = g_tail_flushed;
+  return 0;
+}
+
+// launch a still-pending deferred combine on its own (no-op when a conv launch took it)
+RK_API int rk_conv_flush_reduce(hipStream_t s) {
+  if (!g_tail.pending) return 0;
+  g_tail.pending = false;
+  ++g_tail_flushed;
+  launch_mgemm_reduce(g_tail.slab, g_tail.splitk, g_tail.M, g_tail.N, nullptr, g_tail.c, F32, g_tail.N, g_tail.acc,
+                      g_tail.s);
+  (void)s;
   return (int)hipGetLastError();
 }

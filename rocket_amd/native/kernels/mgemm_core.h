@@ -251,14 +251,16 @@ __device__ __forceinline__ void store_tile(const MArgs& g, f32x4 (&acc)[FM][FN],
 // one output float4, lane g summing the slabs s = g, g + G, ... (four loads in flight), combined by
 // xor-shuffles: small outputs with many splits (ResNet wgrads: 9k float4 x 32 splits) get G-fold more
 // loads in flight instead of a long serial slab loop per thread.  Fixed order: deterministic.
+// block `bid` of `nb` blocks (`nt` threads each) of the combine: mgemm_reduce's body, also run by
+// extra blocks appended to a later launch (conv.hip: the tail-reduce job of a stride-1 dgrad)
 template <int G>
-__global__ void __launch_bounds__(256) mgemm_reduce(const float* __restrict__ slab, int splitk, int M, int N,
-                                                    const float* __restrict__ bias, void* c, int c_dt, int64_t ldc,
-                                                    int accumulate) {
+__device__ __forceinline__ void reduce_slabs(const float* __restrict__ slab, int splitk, int M, int N,
+                                             const float* __restrict__ bias, void* c, int c_dt, int64_t ldc,
+                                             int accumulate, int bid, int nb, int nt) {
   const int64_t nq = (int64_t)M * N / 4;
   const int64_t plane = (int64_t)M * N;
   const int g = (int)(threadIdx.x % G);
-  for (int64_t q = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G; q < nq; q += (int64_t)gridDim.x * (256 / G)) {
+  for (int64_t q = ((int64_t)bid * nt + threadIdx.x) / G; q < nq; q += (int64_t)nb * (nt / G)) {
     const int64_t e = q * 4;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     int s = g;
@@ -307,6 +309,13 @@ __global__ void __launch_bounds__(256) mgemm_reduce(const float* __restrict__ sl
       *(float4*)o = v;
     }
   }
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) mgemm_reduce(const float* __restrict__ slab, int splitk, int M, int N,
+                                                    const float* __restrict__ bias, void* c, int c_dt, int64_t ldc,
+                                                    int accumulate) {
+  reduce_slabs<G>(slab, splitk, M, N, bias, c, c_dt, ldc, accumulate, blockIdx.x, gridDim.x, 256);
 }
 
 // launch the split-K combine: 4 lanes per output float4 once there are >= 8 slabs

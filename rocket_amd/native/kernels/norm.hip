@@ -1300,6 +1300,24 @@ RK_API int rk_bn_stats(int dt, const void* x, int64_t R, int C, const float* gam
   return (int)hipGetLastError();
 }
 
+// Tiles per block of the finalize launches (whole passes of BN_RG, at most rb_max row blocks: the
+// workspace rk_bn_workspace(R, C) sized).  The partials are small (ResNet-18 CIFAR: <= 2048 tiles x
+// 2 x C floats), so the launch is latency-bound: at most BN_GS row blocks per column while each
+// thread keeps <= 4 passes of BN_FU tiles makes the ticket tree one level deep (one store / ticket /
+// re-read round trip instead of two).  ROCKET_BN_FIN_ONE=0: as many row blocks as the workspace allows.
+static int bn_final_per(int ntiles, int rb_max) {
+  static const int one = [] {
+    const char* e = getenv("ROCKET_BN_FIN_ONE");
+    return e ? atoi(e) : 1;
+  }();
+  int per = (ntiles + rb_max - 1) / rb_max;
+  if (one) {
+    const int p1 = (ntiles + BN_GS - 1) / BN_GS;
+    if (p1 <= 4 * BN_FU * BN_RG) per = max(per, p1);
+  }
+  return (per + BN_RG - 1) / BN_RG * BN_RG;
+}
+
 // Same outputs as rk_bn_stats, from the per-row-tile partials tp ([ntiles][2][C]: tile mean, M2) of
 // an R-row activation cut into tiles of tile_rows rows.  ws / counters as for rk_bn_stats(R, C).
 RK_API int rk_bn_finalize(const float* tp, int ntiles, int tile_rows, int64_t R, int C, const float* gamma,
@@ -1312,8 +1330,7 @@ RK_API int rk_bn_finalize(const float* tp, int ntiles, int tile_rows, int64_t R,
   // tiles per block: whole passes of BN_RG, at most the row blocks rk_bn_workspace(R, C) sized for
   int rpb_rows;
   const int rb_max = bn_grid_rows(R, C, &rpb_rows);
-  int per = (ntiles + rb_max - 1) / rb_max;
-  per = (per + BN_RG - 1) / BN_RG * BN_RG;
+  const int per = bn_final_per(ntiles, rb_max);
   a.rpb = per;
   const int rb = (ntiles + per - 1) / per;
   dim3 grid((C + BN_CT - 1) / BN_CT, rb);
@@ -1534,8 +1551,7 @@ RK_API int rk_bn_bwd_partials(int dt, int dto, const void* dy, const void* x, co
   BnBwdArgs a{dy, x, nullptr, R, C, 0, mean, invstd, ws, counters, dgamma, dbeta, scale, coef};
   int rpb_rows;
   const int rb_max = bn_grid_rows(R, C, &rpb_rows);  // the workspace rk_bn_workspace(R, C) sized
-  int per = (ntiles + rb_max - 1) / rb_max;
-  per = (per + BN_RG - 1) / BN_RG * BN_RG;
+  const int per = bn_final_per(ntiles, rb_max);
   a.rpb = per;
   dim3 grid((C + BN_CT - 1) / BN_CT, (ntiles + per - 1) / per);
   bn_bwd_finalize_kernel<<<grid, BN_T, 0, s>>>(a, tp, ntiles);

@@ -68,6 +68,9 @@ KERNEL_SIGS = {
     "rk_bn_bwd_partials": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_int] + [c_void_p] * 11),
     "rk_conv_dgrad": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_int] * 11 + [c_void_p]),
     "rk_conv_wgrad": (c_int, [c_int] + [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p, c_void_p]),
+    "rk_conv_defer_reduce": (c_int, [c_int]),
+    "rk_conv_flush_reduce": (c_int, [c_void_p]),
+    "rk_conv_tail_counts": (c_int, [c_void_p]),
     "rk_conv_pool_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 7 + [c_void_p]),
     "rk_conv_pool_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
     "rk_conv_pool_dgrad": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int] + [c_int] * 7 + [c_void_p]),

@@ -37,6 +37,8 @@ from rocket_amd.ops.mgemm import _slab
 MODE = os.environ.get("ROCKET_CONV", "native")
 # strided (stride-2) input gradients: native parity-class launch or the library
 SDGRAD = os.environ.get("ROCKET_CONV_SDGRAD", "native")
+# wgrad split-K combine in the following dgrad launch (conv.hip TailJob); 0: its own launch
+DEFER_REDUCE = os.environ.get("ROCKET_CONV_DEFER_REDUCE", "1") != "0"
 # residual-block entries (first conv + shortcut) as one autograd node: ROCKET_CONV_ENTRY=0 disables
 ENTRY = os.environ.get("ROCKET_CONV_ENTRY", "1") != "0"
 N_SLOTS = 512  # resident 128x128 conv blocks (2 per CU)
@@ -176,9 +178,14 @@ def _conv_dgrad(dyc: torch.Tensor, w16: torch.Tensor, geo, dx: torch.Tensor | No
     return g if dx is None else dx.add_(g)
 
 
-def _conv_wgrad(dyc: torch.Tensor, xc: torch.Tensor, weight: torch.Tensor, geo):
+def _conv_wgrad(dyc: torch.Tensor, xc: torch.Tensor, weight: torch.Tensor, geo, defer: bool = False):
     """Weight gradient, accumulated straight into a persistent ``weight.grad`` when the engine
-    provides one (returns None then), else returned."""
+    provides one (returns None then), else returned.
+
+    ``defer``: the split-K combine is left to the next conv launch on the stream (conv.hip TailJob:
+    appended blocks of the dgrad the caller issues next) and a finisher is returned instead — call
+    it right after that dgrad: it launches the combine if no conv launch took it, then marks the
+    gradient ready (DP bucket hooks) and returns what the plain call would."""
     N, C, H, W, Co, R, S, stride, pad, OH, OW = geo
     direct = _direct(weight) and weight.grad.is_contiguous(memory_format=torch.channels_last)
     target = weight.grad if direct else torch.empty(weight.shape, dtype=torch.float32, device=dyc.device,
@@ -186,13 +193,28 @@ def _conv_wgrad(dyc: torch.Tensor, xc: torch.Tensor, weight: torch.Tensor, geo):
     P, ncol = N * OH * OW, R * S * C
     split = _wgrad_split(Co, ncol, P)
     slab = _slab(dyc.device, split * Co * ncol) if split > 1 else None
-    _lib.check(_lib.kernels().rk_conv_wgrad(_dt(xc), dyc.data_ptr(), xc.data_ptr(), target.data_ptr(), int(direct), None, N, H,
-                                            W, C, Co, R, S, stride, pad, OH, OW, split, _lib.ptr(slab),
-                                            _lib.stream_ptr(dyc.device)), "rk_conv_wgrad")
-    if direct:
-        grad_ready(weight)
-        return None
-    return target
+    lib = _lib.kernels()
+    stream = _lib.stream_ptr(dyc.device)
+    defer = defer and split > 1
+    if defer:
+        lib.rk_conv_defer_reduce(1)
+    try:
+        _lib.check(lib.rk_conv_wgrad(_dt(xc), dyc.data_ptr(), xc.data_ptr(), target.data_ptr(), int(direct), None, N, H,
+                                     W, C, Co, R, S, stride, pad, OH, OW, split, _lib.ptr(slab), stream), "rk_conv_wgrad")
+    finally:
+        if defer:
+            lib.rk_conv_defer_reduce(0)
+
+    def finish():
+        if defer:
+            _lib.check(lib.rk_conv_flush_reduce(stream), "rk_conv_flush_reduce")
+        if direct:
+            grad_ready(weight)
+            return None
+        return target
+
+    return finish if defer else finish()
+
 
 
 class _IConvFn(torch.autograd.Function):
@@ -210,8 +232,11 @@ class _IConvFn(torch.autograd.Function):
     def backward(ctx, dy):
         xc, w16 = ctx.saved_tensors
         dyc = _cl(dy, xc.dtype)
-        dx = _conv_dgrad(dyc, w16, ctx.geo, None, ctx.bn) if ctx.needs_input_grad[0] else None
-        dw = _conv_wgrad(dyc, xc, ctx.weight, ctx.geo) if ctx.needs_input_grad[1] else None
+        need = ctx.needs_input_grad
+        # the wgrad first: its split-K combine rides in the dgrad's launch (DEFER_REDUCE)
+        fin = _conv_wgrad(dyc, xc, ctx.weight, ctx.geo, defer=DEFER_REDUCE and need[0]) if need[1] else None
+        dx = _conv_dgrad(dyc, w16, ctx.geo, None, ctx.bn) if need[0] else None
+        dw = fin() if callable(fin) else fin
         ctx.bn = None
         return dx, dw, None, None, None, None, None
 
@@ -244,16 +269,32 @@ class _EntryFn(torch.autograd.Function):
         dx = None
         gac = _cl(ga, xc.dtype) if ga is not None else None
         gbc = _cl(gb, xc.dtype) if gb is not None else None
+        # each wgrad just before the dgrad of the same conv: its split-K combine rides in that
+        # dgrad's launch (DEFER_REDUCE); the finisher runs before the next wgrad is issued
+        wa_do = need[1] and gac is not None
+        wb_do = wb is not None and need[6] and gbc is not None
+        dwa = dwb = None
         if need[0]:
             if gbc is not None:
                 # shortcut first: downsample dgrad into a fresh dx / the identity's gradient as dx
-                dx = _conv_dgrad(gbc, wb16, geo_b, None) if wb is not None else gbc
+                if wb is not None:
+                    fin = _conv_wgrad(gbc, xc, wb, geo_b, defer=DEFER_REDUCE) if wb_do else None
+                    dx = _conv_dgrad(gbc, wb16, geo_b, None)
+                    dwb = fin() if callable(fin) else fin
+                    wb_do = False
+                else:
+                    dx = gbc
             if gac is not None:
+                fin = _conv_wgrad(gac, xc, wa, geo_a, defer=DEFER_REDUCE) if wa_do else None
                 dx = _conv_dgrad(gac, wa16, geo_a, dx, ctx.bn)
+                dwa = fin() if callable(fin) else fin
+                wa_do = False
             if dx is None:
                 dx = torch.zeros_like(xc)
-        dwa = _conv_wgrad(gac, xc, wa, geo_a) if need[1] and gac is not None else None
-        dwb = _conv_wgrad(gbc, xc, wb, geo_b) if wb is not None and need[6] and gbc is not None else None
+        if wa_do:
+            dwa = _conv_wgrad(gac, xc, wa, geo_a)
+        if wb_do:
+            dwb = _conv_wgrad(gbc, xc, wb, geo_b)
         ctx.bn = None
         return dx, dwa, None, None, None, None, dwb, None, None, None, None, None
 

@@ -55,12 +55,17 @@ def _clone_params(ps):
     return [torch.nn.Parameter(p.detach().clone()) for p in ps]
 
 
-@pytest.mark.parametrize("kind", ["adamw", "adam", "sgd", "sgd_nesterov"])
+@pytest.mark.parametrize("kind", ["adamw", "adam", "sgd", "sgd_nesterov", "sgd_big", "sgd_nomom_big", "adamw_big"])
 def test_fused_optimizer_matches_torch(kind):
+    """Small (LeNet-sized: 1024-element chunks) and big (> 2M parameters: 4096-element chunks, the
+    vectorised full-chunk path plus the scalar tail) parameter sets against torch.optim."""
     from rocket_amd.ops.optim import FusedAdam, FusedAdamW, FusedSGD
 
     torch.manual_seed(0)
     shapes = [(6, 1, 5, 5), (6,), (16, 6, 5, 5), (16,), (120, 400), (120,), (84, 120), (84,), (10, 84), (10,), (5000,)]
+    if kind.endswith("_big"):
+        shapes = shapes + [(1500, 1501), (512, 2048), (77,)]
+        kind = kind[:-4]
     base = [torch.randn(s, device="cuda") for s in shapes]
     a, b = _clone_params(base), _clone_params(base)
     if kind == "adamw":
@@ -72,6 +77,9 @@ def test_fused_optimizer_matches_torch(kind):
     elif kind == "sgd":
         oa = FusedSGD(a, lr=0.1, momentum=0.9, weight_decay=1e-4)
         ob = torch.optim.SGD(b, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    elif kind == "sgd_nomom":
+        oa = FusedSGD(a, lr=0.1, weight_decay=1e-4)
+        ob = torch.optim.SGD(b, lr=0.1, weight_decay=1e-4)
     else:
         oa = FusedSGD(a, lr=0.1, momentum=0.9, nesterov=True)
         ob = torch.optim.SGD(b, lr=0.1, momentum=0.9, nesterov=True)

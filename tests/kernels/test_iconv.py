@@ -142,6 +142,57 @@ def test_block_entry_matches_separate(monkeypatch, kind, cin, width, stride):
         assert _rel(a, b) < 1e-2
 
 
+def _tail_counts():
+    import ctypes
+
+    from rocket_amd.ops import _lib
+
+    out = (ctypes.c_int64 * 2)()
+    _lib.kernels().rk_conv_tail_counts(ctypes.cast(out, ctypes.c_void_p))
+    return out[0], out[1]
+
+
+@pytest.mark.parametrize("kind", ["bottleneck", "basic"])
+def test_wgrad_combine_in_dgrad_launch(monkeypatch, kind):
+    """The weight gradients' split-K combine run by blocks appended to the following dgrad launch
+    (conv.hip TailJob, iconv DEFER_REDUCE) gives bit-identical gradients to its own mgemm_reduce
+    launch (same per-element summation order), through plain convs and block entries with identity
+    and strided shortcuts; every deferred combine is taken by a dgrad launch or flushed."""
+    import rocket_amd.ops.iconv as ic
+    from rocket_amd.models.resnet import BasicBlock, Bottleneck
+    from rocket_amd.ops.norm import BatchNormAct2d
+
+    torch.manual_seed(6)
+    if kind == "bottleneck":
+        net = torch.nn.Sequential(BatchNormAct2d(256, relu=True), Bottleneck(256, 64, 1), Bottleneck(256, 128, 2))
+        cin = 256
+    else:
+        net = torch.nn.Sequential(BatchNormAct2d(64, relu=True), BasicBlock(64, 64, 1), BasicBlock(64, 128, 2))
+        cin = 64
+    net = net.cuda().to(memory_format=torch.channels_last)
+    x0 = torch.randn(32, cin, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for defer in (True, False):
+        monkeypatch.setattr(ic, "DEFER_REDUCE", defer)
+        net.zero_grad(set_to_none=True)
+        c0 = _tail_counts()
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = net(x)
+        torch.manual_seed(7)
+        g = torch.randn(y.shape, device="cuda").to(y.dtype).contiguous(memory_format=torch.channels_last)
+        y.backward(g)
+        torch.cuda.synchronize()
+        c1 = _tail_counts()
+        outs.append((x.grad.float(), [p.grad.float().clone() for p in net.parameters()],
+                     (c1[0] - c0[0], c1[1] - c0[1])))
+    (dx1, g1, (att, fl)), (dx2, g2, (att0, fl0)) = outs
+    assert att >= 2 and att0 == 0 and fl0 == 0, (att, fl, att0, fl0)
+    assert torch.equal(dx1, dx2)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("kind", ["bottleneck", "basic"])
 def test_bn_backward_reduction_in_dgrad_epilogue(monkeypatch, kind):
     """BatchNorm backward reductions done by the consuming stride-1 conv's dgrad epilogue
