@@ -1,0 +1,208 @@
+// Classifier heads whose class count is not a multiple of 8 (CIFAR-10's 10 classes, CIFAR-100's 100
+// beyond the MFMA routes' N % 8 rule): y = x W^T + b with fp32 W / b / y and a 16-bit or fp32 x,
+// and the whole backward (dx, dW, db) in ONE launch.
+//
+// These products are tiny (ResNet-18 CIFAR: 256 x 10 x 512 = 1.3 MFLOP): the library route costs
+// a dozen launches around three GEMMs (weight / bias casts to bf16, the fp32 casts of the logits
+// and of both gradients, autograd's accumulation adds, a bias column sum), each at the ~5 us floor
+// of a kernel boundary.  Here: one forward launch, one backward launch, fp32 logits handed to the
+// cross-entropy directly (no cast), gradients accumulated into the persistent fp32 grads.
+//
+// Forward: one block per row m, threads over k (coalesced x and W rows, every load of a round in
+// flight), 16 class accumulators per pass, butterfly + LDS reductions.  Backward: blocks [0, KB)
+// form dW / db — a block owns 64 k-columns (one per lane), its 16 waves split the rows, LDS
+// combines them in a fixed order (deterministic); the remaining blocks form dx, one element per
+// thread.  Both are latency-bound launches: the loads are issued in rounds, not row by row.
+#include "rk_common.h"
+
+using namespace rk;
+
+namespace {
+
+constexpr int HT = 256;      // forward: threads per block (one block per row)
+constexpr int HW = HT / 64;  // forward: waves per block
+constexpr int BT = 1024;     // backward: threads per block
+constexpr int BW = BT / 64;  // backward: waves per block
+constexpr int HNC = 16;      // classes per accumulator pass
+constexpr int HNMAX = 128;   // largest class count served
+constexpr int SR = 256;      // backward: dy rows staged in LDS per pass
+
+template <int DT>
+__device__ __forceinline__ float ldx(const void* p, int64_t i) {
+  if constexpr (DT == F32) return ((const float*)p)[i];
+  else if constexpr (DT == F16) return h2f(((const uint16_t*)p)[i]);
+  else return bf2f(((const uint16_t*)p)[i]);
+}
+template <int DT>
+__device__ __forceinline__ void stx(void* p, int64_t i, float v) {
+  if constexpr (DT == F32) ((float*)p)[i] = v;
+  else if constexpr (DT == F16) ((uint16_t*)p)[i] = f2h(v);
+  else ((uint16_t*)p)[i] = f2bf(v);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// one block per row: each thread 4 k's per round (all x / W loads of the round in flight), the
+// block's partial dot products reduced by butterflies then across the 4 waves in LDS (fixed order)
+template <int DT>
+__global__ void __launch_bounds__(HT) head_fwd_kernel(const void* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ b, float* __restrict__ y, int M,
+                                                      int N, int K) {
+  __shared__ float red[HW][HNC];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int m = blockIdx.x;
+  for (int n0 = 0; n0 < N; n0 += HNC) {
+    float acc[HNC];
+#pragma unroll
+    for (int j = 0; j < HNC; ++j) acc[j] = 0.f;
+    for (int k0 = 0; k0 < K; k0 += 4 * HT) {
+      float xv[4], wr[4][HNC];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * HT + (int)threadIdx.x;
+        xv[u] = k < K ? ldx<DT>(x, (int64_t)m * K + k) : 0.f;
+#pragma unroll
+        for (int j = 0; j < HNC; ++j) wr[u][j] = (k < K && n0 + j < N) ? w[(int64_t)(n0 + j) * K + k] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < HNC; ++j) acc[j] += xv[u] * wr[u][j];
+    }
+#pragma unroll
+    for (int j = 0; j < HNC; ++j) {
+      const float v = wave_sum(acc[j]);
+      if (lane == 0) red[wv][j] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < HNC && n0 + (int)threadIdx.x < N) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < HW; ++q) v += red[q][threadIdx.x];
+      y[(int64_t)m * N + n0 + threadIdx.x] = v + (b ? b[n0 + threadIdx.x] : 0.f);
+    }
+    __syncthreads();
+  }
+}
+
+// blocks [0, kb): dW / db over 64 k-columns (one per lane), the 16 waves splitting each staged
+// chunk of SR rows (16 rows per wave, all their x loads in flight; dy read from LDS as broadcasts),
+// then an LDS reduction over the waves in a fixed order; the rest: dx, one element per thread
+template <int DT>
+__global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ dy, const void* __restrict__ x,
+                                                      const float* __restrict__ w, void* __restrict__ dx,
+                                                      float* __restrict__ dw, float* __restrict__ db, int acc_w,
+                                                      int acc_b, int M, int N, int K, int kb) {
+  __shared__ float sdy[SR][HNC];
+  __shared__ float red[BW][HNC][64 + 1];
+  __shared__ float redb[BW][HNC];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if ((int)blockIdx.x < kb) {  // dW[n][k] = sum_m dy[m][n] x[m][k]; db[n] = sum_m dy[m][n] (block 0)
+    const int k = blockIdx.x * 64 + lane;
+    const bool kok = k < K;
+    for (int n0 = 0; n0 < N; n0 += HNC) {
+      float acc[HNC], accb[HNC];
+#pragma unroll
+      for (int j = 0; j < HNC; ++j) acc[j] = accb[j] = 0.f;
+      for (int mc = 0; mc < M; mc += SR) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < SR * HNC; i += BT) {
+          const int r = i / HNC, j = i % HNC;
+          sdy[r][j] = (mc + r < M && n0 + j < N) ? dy[(int64_t)(mc + r) * N + n0 + j] : 0.f;
+        }
+        __syncthreads();
+        float xv[SR / BW];
+#pragma unroll
+        for (int t = 0; t < SR / BW; ++t) {
+          const int m = mc + wv + BW * t;
+          xv[t] = (kok && m < M) ? ldx<DT>(x, (int64_t)m * K + k) : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < SR / BW; ++t)
+#pragma unroll
+          for (int j = 0; j < HNC; ++j) {
+            const float g = sdy[wv + BW * t][j];
+            acc[j] += g * xv[t];
+            accb[j] += g;
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < HNC; ++j) red[wv][j][lane] = acc[j];
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < HNC; ++j) redb[wv][j] = accb[j];
+      }
+      __syncthreads();
+      {  // wave wv finishes class wv (16 waves, 16 classes): the waves' partials summed in wave order
+        const int j = wv;
+        float sum = 0.f;
+#pragma unroll
+        for (int q = 0; q < BW; ++q) sum += red[q][j][lane];
+        if (kok && n0 + j < N) {
+          float* o = dw + (int64_t)(n0 + j) * K + k;
+          *o = acc_w ? *o + sum : sum;
+        }
+      }
+      if (db != nullptr && blockIdx.x == 0 && threadIdx.x < HNC && n0 + (int)threadIdx.x < N) {
+        float sum = 0.f;
+#pragma unroll
+        for (int q = 0; q < BW; ++q) sum += redb[q][threadIdx.x];
+        float* o = db + n0 + threadIdx.x;
+        *o = acc_b ? *o + sum : sum;
+      }
+    }
+    return;
+  }
+  if (dx == nullptr) return;
+  // dx[m][k] = sum_n dy[m][n] W[n][k]: each chunk's 16 dy / W loads in flight together
+  const int64_t e = (int64_t)(blockIdx.x - kb) * BT + threadIdx.x;
+  if (e >= (int64_t)M * K) return;
+  const int m = (int)(e / K), k = (int)(e % K);
+  const float* d = dy + (int64_t)m * N;
+  float s = 0.f;
+  for (int n0 = 0; n0 < N; n0 += HNC) {
+    float dv[HNC], wr[HNC];
+#pragma unroll
+    for (int j = 0; j < HNC; ++j) {
+      dv[j] = n0 + j < N ? d[n0 + j] : 0.f;
+      wr[j] = n0 + j < N ? w[(int64_t)(n0 + j) * K + k] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < HNC; ++j) s += dv[j] * wr[j];
+  }
+  stx<DT>(dx, e, s);
+}
+
+}  // namespace
+
+// y[M][N] f32 = x[M][K] (dt) W[N][K]^T (f32) + b[N] (f32, may be null); N <= 128
+RK_API int rk_head_fwd(int dt, const void* x, const float* w, const float* b, float* y, int M, int N, int K,
+                       hipStream_t s) {
+  if (M <= 0 || N <= 0 || N > HNMAX || K <= 0 || (int64_t)M * K >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  const int grid = M;
+  if (dt == BF16) head_fwd_kernel<BF16><<<grid, HT, 0, s>>>(x, w, b, y, M, N, K);
+  else if (dt == F16) head_fwd_kernel<F16><<<grid, HT, 0, s>>>(x, w, b, y, M, N, K);
+  else if (dt == F32) head_fwd_kernel<F32><<<grid, HT, 0, s>>>(x, w, b, y, M, N, K);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// One launch: dx[M][K] (dt, may be null) = dy W; dW[N][K] f32 (+)= dy^T x (may be null);
+// db[N] f32 (+)= column sums of dy (may be null).  dy: f32 [M][N].
+RK_API int rk_head_bwd(int dt, const float* dy, const void* x, const float* w, void* dx, float* dw, float* db,
+                       int acc_w, int acc_b, int M, int N, int K, hipStream_t s) {
+  if (M <= 0 || N <= 0 || N > HNMAX || K <= 0 || (int64_t)M * K >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (db != nullptr && dw == nullptr) return (int)hipErrorInvalidValue;  // db rides on the dW blocks
+  const int kb = dw != nullptr ? (K + 63) / 64 : 0;
+  const int xb = dx != nullptr ? (int)(((int64_t)M * K + BT - 1) / BT) : 0;
+  if (kb + xb == 0) return 0;
+  if (dt == BF16) head_bwd_kernel<BF16><<<kb + xb, BT, 0, s>>>(dy, x, w, dx, dw, db, acc_w, acc_b, M, N, K, kb);
+  else if (dt == F16) head_bwd_kernel<F16><<<kb + xb, BT, 0, s>>>(dy, x, w, dx, dw, db, acc_w, acc_b, M, N, K, kb);
+  else if (dt == F32) head_bwd_kernel<F32><<<kb + xb, BT, 0, s>>>(dy, x, w, dx, dw, db, acc_w, acc_b, M, N, K, kb);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}

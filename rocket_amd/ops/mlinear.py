@@ -443,10 +443,73 @@ def _native(module: nn.Linear, x: torch.Tensor) -> bool:
             and _ok(x, module.out_features, module.in_features))
 
 
+# classifier heads whose class count is not a multiple of 8 (head.hip): one forward, one backward
+# launch, fp32 logits.  ROCKET_HEAD=0: nn.Linear (the library route under autocast)
+HEAD = os.environ.get("ROCKET_HEAD", "1") != "0"
+_HEAD_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def _head_ok(module: nn.Linear, x: torch.Tensor) -> bool:
+    N, K = module.out_features, module.in_features
+    return (HEAD and x.is_cuda and native_route() and N % 8 != 0 and N <= 128 and x.dtype in _HEAD_DT
+            and x.shape[-1] == K and x.numel() < (1 << 31) and module.weight.dtype == torch.float32
+            and module.weight.is_contiguous() and (module.bias is None or module.bias.dtype == torch.float32)
+            and _lib.available())
+
+
+class _HeadFn(torch.autograd.Function):
+    """y = x W^T + b (fp32 logits) and its backward in one launch each (head.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        N, K = weight.shape
+        x2 = x.reshape(-1, K)
+        x2 = x2 if x2.is_contiguous() else x2.contiguous()
+        M = x2.shape[0]
+        y = torch.empty(M, N, dtype=torch.float32, device=x.device)
+        _lib.check(_lib.kernels().rk_head_fwd(_HEAD_DT[x2.dtype], x2.data_ptr(), weight.data_ptr(), _lib.ptr(bias),
+                                              y.data_ptr(), M, N, K, _lib.stream_ptr(x.device)), "rk_head_fwd")
+        ctx.save_for_backward(x2, weight)
+        ctx.bias = bias
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        bias = ctx.bias
+        N, K = weight.shape
+        M = x2.shape[0]
+        dy2 = dy.reshape(M, N)
+        if dy2.dtype != torch.float32 or not dy2.is_contiguous():
+            dy2 = dy2.float().contiguous()
+        need_x, need_w, need_b = ctx.needs_input_grad
+        need_b = need_b and bias is not None
+        dev = x2.device
+        dx = torch.empty_like(x2) if need_x else None
+        direct_w = need_w and _direct(weight) and weight.grad.is_contiguous()
+        direct_b = need_b and _direct(bias)
+        dw = weight.grad if direct_w else (torch.empty(N, K, dtype=torch.float32, device=dev)
+                                           if (need_w or need_b) else None)  # db rides on the dW blocks
+        db = (bias.grad if direct_b else torch.empty(N, dtype=torch.float32, device=dev)) if need_b else None
+        _lib.check(_lib.kernels().rk_head_bwd(_HEAD_DT[x2.dtype], dy2.data_ptr(), x2.data_ptr(), weight.data_ptr(),
+                                              _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(db), int(direct_w), int(direct_b),
+                                              M, N, K, _lib.stream_ptr(dev)), "rk_head_bwd")
+        if direct_w:
+            grad_ready(weight)
+        if direct_b:
+            grad_ready(bias)
+        return (dx.view(ctx.xshape) if need_x else None, dw if need_w and not direct_w else None,
+                db if need_b and not direct_b else None)
+
+
 class MLinear(nn.Linear):
-    """``nn.Linear`` on the native MFMA GEMM under bf16 autocast (module docstring)."""
+    """``nn.Linear`` on the native MFMA GEMM under bf16 autocast (module docstring); class counts
+    that are not a multiple of 8 on the head kernels (:class:`_HeadFn`, fp32 logits)."""
 
     def forward(self, x):
+        if _head_ok(self, x):
+            return _HeadFn.apply(x, self.weight, self.bias)
         if _native(self, x) and self.bias is not None:
             dt = _cdtype()
             w16 = _lowp_copy(self, "_w16", self.weight, dt)

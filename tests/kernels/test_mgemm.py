@@ -405,3 +405,35 @@ def test_mlinear_small_head_native(M, N, K, monkeypatch):
     assert (m.weight.grad - wr.grad).abs().max().item() <= 2e-2 * wr.grad.abs().max().item()
     assert (m.bias.grad - br.grad).abs().max().item() <= 2e-2 * br.grad.abs().max().item()
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,dtype", [(256, 10, 512, torch.bfloat16), (100, 100, 768, torch.bfloat16),
+                                         (37, 10, 2048, torch.float16), (64, 3, 96, torch.float32)])
+def test_head_kernels_vs_fp32(M, N, K, dtype):
+    """Class counts off the MFMA routes' N % 8 rule run on head.hip (one forward, one backward
+    launch, fp32 logits): forward, input / weight / bias gradients against fp32 torch on the same
+    (16-bit) input."""
+    from rocket_amd.ops import mlinear
+
+    torch.manual_seed(1)
+    m = mlinear.MLinear(K, N).cuda()
+    x = (torch.randn(M, K, device="cuda") * 0.5).to(dtype).requires_grad_()
+    ctx = torch.autocast("cuda", dtype=torch.bfloat16) if dtype != torch.float16 else \
+        torch.autocast("cuda", dtype=torch.float16)
+    with ctx:
+        assert mlinear._head_ok(m, x)
+        y = m(x)
+    assert y.dtype == torch.float32 and y.shape == (M, N)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    wr = m.weight.detach().clone().requires_grad_()
+    br = m.bias.detach().clone().requires_grad_()
+    yr = xr @ wr.t() + br
+    yr.backward(g)
+    assert (y - yr).abs().max().item() <= 1e-4 * yr.abs().max().item() + 1e-5
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert (x.grad.float() - xr.grad).abs().max().item() <= tol * xr.grad.abs().max().item()
+    assert (m.weight.grad - wr.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item()
+    assert (m.bias.grad - br.grad).abs().max().item() <= 1e-4 * br.grad.abs().max().item()
