@@ -10,7 +10,7 @@
 //
 // Forward: one block per row m, threads over k (coalesced x and W rows, every load of a round in
 // flight), 16 class accumulators per pass, butterfly + LDS reductions.  Backward: blocks [0, KB)
-// form dW / db — a block owns 64 k-columns (one per lane), its 16 waves split the rows, LDS
+// form dW / db — a block owns 64 k-columns (one per lane), its 4 waves split the rows, LDS
 // combines them in a fixed order (deterministic); the remaining blocks form dx, one element per
 // thread.  Both are latency-bound launches: the loads are issued in rounds, not row by row.
 #include "rk_common.h"
@@ -21,11 +21,13 @@ namespace {
 
 constexpr int HT = 256;      // forward: threads per block (one block per row)
 constexpr int HW = HT / 64;  // forward: waves per block
-constexpr int BT = 1024;     // backward: threads per block
+// backward: small blocks (4 waves, ~21 KB LDS), so a block always fits next to co-resident
+// persistent kernels (the spinning P2P all-reduce blocks of DP ranks sharing a GPU)
+constexpr int BT = 256;      // backward: threads per block
 constexpr int BW = BT / 64;  // backward: waves per block
 constexpr int HNC = 16;      // classes per accumulator pass
 constexpr int HNMAX = 128;   // largest class count served
-constexpr int SR = 256;      // backward: dy rows staged in LDS per pass
+constexpr int SR = 64;       // backward: dy rows staged in LDS per pass (16 per wave)
 
 template <int DT>
 __device__ __forceinline__ float ldx(const void* p, int64_t i) {
@@ -89,7 +91,7 @@ __global__ void __launch_bounds__(HT) head_fwd_kernel(const void* __restrict__ x
   }
 }
 
-// blocks [0, kb): dW / db over 64 k-columns (one per lane), the 16 waves splitting each staged
+// blocks [0, kb): dW / db over 64 k-columns (one per lane), the 4 waves splitting each staged
 // chunk of SR rows (16 rows per wave, all their x loads in flight; dy read from LDS as broadcasts),
 // then an LDS reduction over the waves in a fixed order; the rest: dx, one element per thread
 template <int DT>
@@ -137,8 +139,7 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
         for (int j = 0; j < HNC; ++j) redb[wv][j] = accb[j];
       }
       __syncthreads();
-      {  // wave wv finishes class wv (16 waves, 16 classes): the waves' partials summed in wave order
-        const int j = wv;
+      for (int j = wv; j < HNC; j += BW) {  // wave wv finishes classes wv, wv + 4, ...: partials in wave order
         float sum = 0.f;
 #pragma unroll
         for (int q = 0; q < BW; ++q) sum += red[q][j][lane];

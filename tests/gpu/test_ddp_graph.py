@@ -60,6 +60,10 @@ def _inject_capture_failure(rank, injected):
 
 
 def _worker(rank, world, port, out_dir, mode, model):
+    if os.environ.get("ROCKET_TEST_HANG_DUMP"):  # debugging: dump the worker's stacks and exit on a hang
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["ROCKET_TEST_HANG_DUMP"]), exit=True)
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROCKET_DIST_BACKEND="gloo", **_ENV[mode])
     import rocket_amd as rocket
