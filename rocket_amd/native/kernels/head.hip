@@ -27,7 +27,7 @@ constexpr int BT = 256;      // backward: threads per block
 constexpr int BW = BT / 64;  // backward: waves per block
 constexpr int HNC = 16;      // classes per accumulator pass
 constexpr int HNMAX = 128;   // largest class count served
-constexpr int SR = 64;       // backward: dy rows staged in LDS per pass (16 per wave)
+constexpr int SR = 64;       // backward: dy rows staged in LDS per pass (16 per wave, their x loads in one round)
 
 template <int DT>
 __device__ __forceinline__ float ldx(const void* p, int64_t i) {
@@ -99,9 +99,13 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ w, void* __restrict__ dx,
                                                       float* __restrict__ dw, float* __restrict__ db, int acc_w,
                                                       int acc_b, int M, int N, int K, int kb) {
-  __shared__ float sdy[SR][HNC];
-  __shared__ float red[BW][HNC][64 + 1];
+  // the staged dy rows and the cross-wave partials share one LDS region (~17 KB in all: the block
+  // must fit next to whatever else is resident, see BT)
+  __shared__ float lds_u[BW * HNC * (64 + 1)];
   __shared__ float redb[BW][HNC];
+  float (*sdy)[HNC] = reinterpret_cast<float (*)[HNC]>(lds_u);
+  float (*red)[HNC][64 + 1] = reinterpret_cast<float (*)[HNC][64 + 1]>(lds_u);
+  static_assert(SR * HNC <= BW * HNC * (64 + 1), "staged rows fit the shared region");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if ((int)blockIdx.x < kb) {  // dW[n][k] = sum_m dy[m][n] x[m][k]; db[n] = sum_m dy[m][n] (block 0)
     const int k = blockIdx.x * 64 + lane;
@@ -112,8 +116,9 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
       for (int j = 0; j < HNC; ++j) acc[j] = accb[j] = 0.f;
       for (int mc = 0; mc < M; mc += SR) {
         __syncthreads();
-        for (int i = threadIdx.x; i < SR * HNC; i += BT) {
-          const int r = i / HNC, j = i % HNC;
+#pragma unroll
+        for (int t = 0; t < SR * HNC / BT; ++t) {
+          const int i = (int)threadIdx.x + t * BT, r = i / HNC, j = i % HNC;
           sdy[r][j] = (mc + r < M && n0 + j < N) ? dy[(int64_t)(mc + r) * N + n0 + j] : 0.f;
         }
         __syncthreads();
@@ -132,6 +137,7 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
             accb[j] += g;
           }
       }
+      __syncthreads();  // the last stage's sdy reads are done before red overwrites the region
 #pragma unroll
       for (int j = 0; j < HNC; ++j) red[wv][j][lane] = acc[j];
       if (lane == 0) {

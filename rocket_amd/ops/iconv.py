@@ -310,6 +310,23 @@ def _stem_weight(weight: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return w8
 
 
+def _stem_weight_into(weight: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """:func:`_stem_weight` into a buffer kept on the parameter: its zero padding is written once,
+    each step only copies the live taps (one launch instead of a fill and a copy).  A buffer first
+    needed inside a graph capture is not kept (its memory would belong to the capture's pool)."""
+    co, ci, R, S = weight.shape
+    kp = -(-(R * S * 8) // 64) * 64
+    buf = getattr(weight, "_rocket_w8", None)
+    if buf is None or buf.dtype != dtype or buf.device != weight.device or buf.shape != (co, kp):
+        if torch.cuda.is_current_stream_capturing():
+            return _stem_weight(weight, dtype)
+        buf = torch.zeros(co, kp, dtype=dtype, device=weight.device)
+        weight._rocket_w8 = buf
+    with torch.no_grad():
+        buf[:, : R * S * 8].view(co, R, S, 8)[..., :ci].copy_(weight.detach().permute(0, 2, 3, 1))
+    return buf
+
+
 class _StemFn(torch.autograd.Function):
     """Stem conv (Cin <= 8) on the native kernels; the input (the image) takes no gradient."""
 
@@ -329,7 +346,7 @@ class _StemFn(torch.autograd.Function):
             sn, sc, sh, sw = xc.stride()
         x8 = torch.empty((N, H, W, 8), dtype=cdt, device=dev)
         _lib.check(lib.rk_pad_c8(xc.data_ptr(), x8.data_ptr(), N, C, H, W, sn, sc, sw, s), "rk_pad_c8")
-        w8 = _stem_weight(weight, cdt)
+        w8 = _stem_weight_into(weight, cdt)
         y = torch.empty((N, co, OH, OW), dtype=cdt, device=dev, memory_format=torch.channels_last)
         _lib.check(lib.rk_conv_fwd_c8(_dt(x8), x8.data_ptr(), w8.data_ptr(), y.data_ptr(), N, H, W, co, R, S, stride, pad, OH,
                                       OW, _lib.ptr(bnpart), s), "rk_conv_fwd_c8")
