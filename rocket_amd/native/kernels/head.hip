@@ -91,53 +91,58 @@ __global__ void __launch_bounds__(HT) head_fwd_kernel(const void* __restrict__ x
   }
 }
 
-// blocks [0, kb): dW / db over 64 k-columns (one per lane), the 4 waves splitting each staged
-// chunk of SR rows (16 rows per wave, all their x loads in flight; dy read from LDS as broadcasts),
-// then an LDS reduction over the waves in a fixed order; the rest: dx, one element per thread
+// blocks [0, kb * mb): dW / db partials of 64 k-columns (one per lane) over one chunk of SR rows
+// (16 rows per wave, all their x loads in flight; dy staged in LDS, read as broadcasts), the 4
+// waves' sums combined in LDS in wave order and stored as the chunk's partial; the last chunk block
+// of a column group (ticket, no waiting) sums the mb partials in chunk order (deterministic) into
+// dW / db.  The rest of the grid: dx, one element per thread.
 template <int DT>
 __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ dy, const void* __restrict__ x,
                                                       const float* __restrict__ w, void* __restrict__ dx,
                                                       float* __restrict__ dw, float* __restrict__ db, int acc_w,
-                                                      int acc_b, int M, int N, int K, int kb) {
+                                                      int acc_b, int M, int N, int K, int kb, int mb,
+                                                      float* __restrict__ part, unsigned* __restrict__ cnt) {
   // the staged dy rows and the cross-wave partials share one LDS region (~17 KB in all: the block
   // must fit next to whatever else is resident, see BT)
   __shared__ float lds_u[BW * HNC * (64 + 1)];
   __shared__ float redb[BW][HNC];
+  __shared__ int last;
   float (*sdy)[HNC] = reinterpret_cast<float (*)[HNC]>(lds_u);
   float (*red)[HNC][64 + 1] = reinterpret_cast<float (*)[HNC][64 + 1]>(lds_u);
   static_assert(SR * HNC <= BW * HNC * (64 + 1), "staged rows fit the shared region");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if ((int)blockIdx.x < kb) {  // dW[n][k] = sum_m dy[m][n] x[m][k]; db[n] = sum_m dy[m][n] (block 0)
-    const int k = blockIdx.x * 64 + lane;
+  if ((int)blockIdx.x < kb * mb) {  // partial dW[n][k] = sum_m dy[m][n] x[m][k] over rows [mc, mc + SR)
+    const int kbi = (int)blockIdx.x % kb, mbi = (int)blockIdx.x / kb;
+    const int k = kbi * 64 + lane, mc = mbi * SR;
     const bool kok = k < K;
+    float* pw = part + (int64_t)mbi * N * K;          // [mb][N][K]
+    float* pb = part + (int64_t)mb * N * K + mbi * N;  // [mb][N]
     for (int n0 = 0; n0 < N; n0 += HNC) {
       float acc[HNC], accb[HNC];
+      __syncthreads();  // the previous class chunk's reads of the shared region are done
+#pragma unroll
+      for (int t = 0; t < SR * HNC / BT; ++t) {
+        const int i = (int)threadIdx.x + t * BT, r = i / HNC, j = i % HNC;
+        sdy[r][j] = (mc + r < M && n0 + j < N) ? dy[(int64_t)(mc + r) * N + n0 + j] : 0.f;
+      }
+      __syncthreads();
+      float xv[SR / BW];
+#pragma unroll
+      for (int t = 0; t < SR / BW; ++t) {
+        const int m = mc + wv + BW * t;
+        xv[t] = (kok && m < M) ? ldx<DT>(x, (int64_t)m * K + k) : 0.f;
+      }
 #pragma unroll
       for (int j = 0; j < HNC; ++j) acc[j] = accb[j] = 0.f;
-      for (int mc = 0; mc < M; mc += SR) {
-        __syncthreads();
 #pragma unroll
-        for (int t = 0; t < SR * HNC / BT; ++t) {
-          const int i = (int)threadIdx.x + t * BT, r = i / HNC, j = i % HNC;
-          sdy[r][j] = (mc + r < M && n0 + j < N) ? dy[(int64_t)(mc + r) * N + n0 + j] : 0.f;
+      for (int t = 0; t < SR / BW; ++t)
+#pragma unroll
+        for (int j = 0; j < HNC; ++j) {
+          const float g = sdy[wv + BW * t][j];
+          acc[j] += g * xv[t];
+          accb[j] += g;
         }
-        __syncthreads();
-        float xv[SR / BW];
-#pragma unroll
-        for (int t = 0; t < SR / BW; ++t) {
-          const int m = mc + wv + BW * t;
-          xv[t] = (kok && m < M) ? ldx<DT>(x, (int64_t)m * K + k) : 0.f;
-        }
-#pragma unroll
-        for (int t = 0; t < SR / BW; ++t)
-#pragma unroll
-          for (int j = 0; j < HNC; ++j) {
-            const float g = sdy[wv + BW * t][j];
-            acc[j] += g * xv[t];
-            accb[j] += g;
-          }
-      }
-      __syncthreads();  // the last stage's sdy reads are done before red overwrites the region
+      __syncthreads();  // the sdy reads are done before red overwrites the region
 #pragma unroll
       for (int j = 0; j < HNC; ++j) red[wv][j][lane] = acc[j];
       if (lane == 0) {
@@ -145,20 +150,42 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
         for (int j = 0; j < HNC; ++j) redb[wv][j] = accb[j];
       }
       __syncthreads();
-      for (int j = wv; j < HNC; j += BW) {  // wave wv finishes classes wv, wv + 4, ...: partials in wave order
+      for (int j = wv; j < HNC; j += BW) {  // wave wv: classes wv, wv + 4, ...; partials in wave order
         float sum = 0.f;
 #pragma unroll
         for (int q = 0; q < BW; ++q) sum += red[q][j][lane];
-        if (kok && n0 + j < N) {
-          float* o = dw + (int64_t)(n0 + j) * K + k;
-          *o = acc_w ? *o + sum : sum;
-        }
+        if (kok && n0 + j < N) st_sc1(pw + (int64_t)(n0 + j) * K + k, sum);
       }
-      if (db != nullptr && blockIdx.x == 0 && threadIdx.x < HNC && n0 + (int)threadIdx.x < N) {
+      if (kbi == 0 && threadIdx.x < HNC && n0 + (int)threadIdx.x < N) {
         float sum = 0.f;
 #pragma unroll
         for (int q = 0; q < BW; ++q) sum += redb[q][threadIdx.x];
-        float* o = db + n0 + threadIdx.x;
+        st_sc1(pb + n0 + threadIdx.x, sum);
+      }
+    }
+    // ticket (rk_common.h protocol: partials stored / read with sc1, every wave's stores drained
+    // before lane 0's ticket): the last of the column group's mb chunk blocks combines and resets
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(cnt + kbi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = t == (unsigned)(mb - 1);
+    }
+    __syncthreads();
+    if (!last) return;
+    reset_counter(cnt + kbi);
+    for (int j = wv; j < N; j += BW) {
+      if (!kok) break;
+      float sum = 0.f;
+      for (int q = 0; q < mb; ++q) sum += ld_sc1(part + ((int64_t)q * N + j) * K + k);
+      float* o = dw + (int64_t)j * K + k;
+      *o = acc_w ? *o + sum : sum;
+    }
+    if (db != nullptr && kbi == 0) {
+      for (int j = threadIdx.x; j < N; j += BT) {
+        float sum = 0.f;
+        for (int q = 0; q < mb; ++q) sum += ld_sc1(part + (int64_t)mb * N * K + q * N + j);
+        float* o = db + j;
         *o = acc_b ? *o + sum : sum;
       }
     }
@@ -166,7 +193,7 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
   }
   if (dx == nullptr) return;
   // dx[m][k] = sum_n dy[m][n] W[n][k]: each chunk's 16 dy / W loads in flight together
-  const int64_t e = (int64_t)(blockIdx.x - kb) * BT + threadIdx.x;
+  const int64_t e = (int64_t)(blockIdx.x - kb * mb) * BT + threadIdx.x;
   if (e >= (int64_t)M * K) return;
   const int m = (int)(e / K), k = (int)(e % K);
   const float* d = dy + (int64_t)m * N;
@@ -199,17 +226,30 @@ RK_API int rk_head_fwd(int dt, const void* x, const float* w, const float* b, fl
 }
 
 // One launch: dx[M][K] (dt, may be null) = dy W; dW[N][K] f32 (+)= dy^T x (may be null);
-// db[N] f32 (+)= column sums of dy (may be null).  dy: f32 [M][N].
+// db[N] f32 (+)= column sums of dy (may be null).  dy: f32 [M][N].  part: f32 scratch of
+// rk_head_bwd_scratch(M, N, K) floats; cnt: ceil(K / 64) zeroed counters (left zeroed).
+RK_API int64_t rk_head_bwd_scratch(int M, int N, int K) {
+  const int64_t mb = (M + SR - 1) / SR;
+  return mb * N * (int64_t)K + mb * N;
+}
+
 RK_API int rk_head_bwd(int dt, const float* dy, const void* x, const float* w, void* dx, float* dw, float* db,
-                       int acc_w, int acc_b, int M, int N, int K, hipStream_t s) {
+                       int acc_w, int acc_b, int M, int N, int K, float* part, unsigned* cnt, hipStream_t s) {
   if (M <= 0 || N <= 0 || N > HNMAX || K <= 0 || (int64_t)M * K >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   if (db != nullptr && dw == nullptr) return (int)hipErrorInvalidValue;  // db rides on the dW blocks
+  if (dw != nullptr && (part == nullptr || cnt == nullptr)) return (int)hipErrorInvalidValue;
   const int kb = dw != nullptr ? (K + 63) / 64 : 0;
+  const int mb = (M + SR - 1) / SR;
+  if ((int64_t)kb * mb >= ((int64_t)1 << 30)) return (int)hipErrorInvalidValue;
   const int xb = dx != nullptr ? (int)(((int64_t)M * K + BT - 1) / BT) : 0;
-  if (kb + xb == 0) return 0;
-  if (dt == BF16) head_bwd_kernel<BF16><<<kb + xb, BT, 0, s>>>(dy, x, w, dx, dw, db, acc_w, acc_b, M, N, K, kb);
-  else if (dt == F16) head_bwd_kernel<F16><<<kb + xb, BT, 0, s>>>(dy, x, w, dx, dw, db, acc_w, acc_b, M, N, K, kb);
-  else if (dt == F32) head_bwd_kernel<F32><<<kb + xb, BT, 0, s>>>(dy, x, w, dx, dw, db, acc_w, acc_b, M, N, K, kb);
+  const int wb = kb * mb;
+  if (wb + xb == 0) return 0;
+#define RK_HB(D) head_bwd_kernel<D><<<wb + xb, BT, 0, s>>>(dy, x, w, dx, dw, db, acc_w, acc_b, M, N, K, wb ? kb : 1, \
+                                                         wb ? mb : 0, part, cnt)
+  if (dt == BF16) RK_HB(BF16);
+  else if (dt == F16) RK_HB(F16);
+  else if (dt == F32) RK_HB(F32);
   else return (int)hipErrorInvalidValue;
+#undef RK_HB
   return (int)hipGetLastError();
 }

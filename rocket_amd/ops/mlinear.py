@@ -492,9 +492,15 @@ class _HeadFn(torch.autograd.Function):
         dw = weight.grad if direct_w else (torch.empty(N, K, dtype=torch.float32, device=dev)
                                            if (need_w or need_b) else None)  # db rides on the dW blocks
         db = (bias.grad if direct_b else torch.empty(N, dtype=torch.float32, device=dev)) if need_b else None
-        _lib.check(_lib.kernels().rk_head_bwd(_HEAD_DT[x2.dtype], dy2.data_ptr(), x2.data_ptr(), weight.data_ptr(),
-                                              _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(db), int(direct_w), int(direct_b),
-                                              M, N, K, _lib.stream_ptr(dev)), "rk_head_bwd")
+        lib = _lib.kernels()
+        part = cnt = None
+        if dw is not None:  # dW partials per 64-row chunk + the chunk-combine tickets (left zeroed)
+            part = torch.empty(int(lib.rk_head_bwd_scratch(M, N, K)), dtype=torch.float32, device=dev)
+            kb = -(-K // 64)
+            cnt = _lib.Workspace.get(dev).counter_array(f"head{kb}", kb)
+        _lib.check(lib.rk_head_bwd(_HEAD_DT[x2.dtype], dy2.data_ptr(), x2.data_ptr(), weight.data_ptr(),
+                                   _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(db), int(direct_w), int(direct_b),
+                                   M, N, K, _lib.ptr(part), cnt, _lib.stream_ptr(dev)), "rk_head_bwd")
         if direct_w:
             grad_ready(weight)
         if direct_b:

@@ -409,7 +409,8 @@ def test_mlinear_small_head_native(M, N, K, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K,dtype", [(256, 10, 512, torch.bfloat16), (100, 100, 768, torch.bfloat16),
-                                         (37, 10, 2048, torch.float16), (64, 3, 96, torch.float32)])
+                                         (37, 10, 2048, torch.float16), (64, 3, 96, torch.float32),
+                                         (1000, 10, 520, torch.bfloat16)])
 def test_head_kernels_vs_fp32(M, N, K, dtype):
     """Class counts off the MFMA routes' N % 8 rule run on head.hip (one forward, one backward
     launch, fp32 logits): forward, input / weight / bias gradients against fp32 torch on the same
