@@ -16,6 +16,8 @@ Architecture per He et al. (basic/bottleneck blocks, stride on the 3×3 conv as 
 
 from __future__ import annotations
 
+import os
+
 from typing import List, Type
 
 import torch
@@ -24,9 +26,12 @@ from torch import nn
 
 from rocket_amd.ops.iconv import IConv2d, bn_relu_conv, conv_entry, stem_ok
 from rocket_amd.ops.linear import native_route
-from rocket_amd.ops.mlinear import MLinear
+from rocket_amd.ops.mlinear import MLinear, pooled_head, pooled_head_ok
 from rocket_amd.ops.norm import BatchNormAct2d
 from rocket_amd.ops.pool import global_avg_pool
+
+# global average pool fused into the classifier head's launches when the head runs on head.hip
+POOLED_HEAD = os.environ.get("ROCKET_POOLED_HEAD", "1") != "0"
 
 
 def _conv(cin, cout, k, stride=1):
@@ -127,6 +132,8 @@ class ResNet(nn.Module):
             x = x.contiguous(memory_format=torch.channels_last)
         x = self.stem(x)  # ImageNet stem: the max-pool is inside its BatchNormAct2d
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        if native_route() and POOLED_HEAD and pooled_head_ok(self.fc, x):
+            return pooled_head(self.fc, x)  # the pool inside the head's two launches (head.hip)
         if native_route():
             x = global_avg_pool(x)  # one pooling launch, one broadcast launch in the backward
         else:

@@ -49,14 +49,18 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // one block per row: each thread 4 k's per round (all x / W loads of the round in flight), the
-// block's partial dot products reduced by butterflies then across the 4 waves in LDS (fixed order)
+// block's partial dot products reduced by butterflies then across the 4 waves in LDS (fixed order).
+// hw > 1: x is the channels-last activation [M][hw][K] and the row is its global average pool
+// (fp32 sum, rounded to the activation dtype like rk_gap_fwd's output), also stored to xpool
+// [M][K] for the backward.
 template <int DT>
 __global__ void __launch_bounds__(HT) head_fwd_kernel(const void* __restrict__ x, const float* __restrict__ w,
                                                       const float* __restrict__ b, float* __restrict__ y, int M,
-                                                      int N, int K) {
+                                                      int N, int K, int hw, void* __restrict__ xpool) {
   __shared__ float red[HW][HNC];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int m = blockIdx.x;
+  const float inv_hw = 1.f / (float)hw;
   for (int n0 = 0; n0 < N; n0 += HNC) {
     float acc[HNC];
 #pragma unroll
@@ -66,7 +70,18 @@ __global__ void __launch_bounds__(HT) head_fwd_kernel(const void* __restrict__ x
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int k = k0 + u * HT + (int)threadIdx.x;
-        xv[u] = k < K ? ldx<DT>(x, (int64_t)m * K + k) : 0.f;
+        if (hw == 1) {
+          xv[u] = k < K ? ldx<DT>(x, (int64_t)m * K + k) : 0.f;
+        } else {
+          float sum = 0.f;
+#pragma unroll 8
+          for (int p = 0; p < hw; ++p) sum += k < K ? ldx<DT>(x, ((int64_t)m * hw + p) * K + k) : 0.f;
+          xv[u] = 0.f;
+          if (k < K) {
+            stx<DT>(xpool, (int64_t)m * K + k, sum * inv_hw);  // the pooled row, as rk_gap_fwd stores it
+            xv[u] = ldx<DT>(xpool, (int64_t)m * K + k);         // (rounded: the value the head consumes)
+          }
+        }
 #pragma unroll
         for (int j = 0; j < HNC; ++j) wr[u][j] = (k < K && n0 + j < N) ? w[(int64_t)(n0 + j) * K + k] : 0.f;
       }
@@ -101,7 +116,7 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ w, void* __restrict__ dx,
                                                       float* __restrict__ dw, float* __restrict__ db, int acc_w,
                                                       int acc_b, int M, int N, int K, int kb, int mb,
-                                                      float* __restrict__ part, unsigned* __restrict__ cnt) {
+                                                      float* __restrict__ part, unsigned* __restrict__ cnt, int hw) {
   // the staged dy rows and the cross-wave partials share one LDS region (~17 KB in all: the block
   // must fit next to whatever else is resident, see BT)
   __shared__ float lds_u[BW * HNC * (64 + 1)];
@@ -208,19 +223,30 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
 #pragma unroll
     for (int j = 0; j < HNC; ++j) s += dv[j] * wr[j];
   }
-  stx<DT>(dx, e, s);
+  if (hw == 1) {
+    stx<DT>(dx, e, s);
+    return;
+  }
+  // pooled head: the input gradient of the average pool, dy / hw broadcast over the row's pixels of
+  // the channels-last activation (the pooled gradient rounded first, as rk_gap_bwd reads it)
+  stx<DT>(dx, ((int64_t)m * hw) * K + k, s);
+  const float g = ldx<DT>(dx, ((int64_t)m * hw) * K + k) * (1.f / (float)hw);
+  for (int p = 0; p < hw; ++p) stx<DT>(dx, ((int64_t)m * hw + p) * K + k, g);
 }
 
 }  // namespace
 
 // y[M][N] f32 = x[M][K] (dt) W[N][K]^T (f32) + b[N] (f32, may be null); N <= 128
-RK_API int rk_head_fwd(int dt, const void* x, const float* w, const float* b, float* y, int M, int N, int K,
-                       hipStream_t s) {
-  if (M <= 0 || N <= 0 || N > HNMAX || K <= 0 || (int64_t)M * K >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+// hw > 1: x is a channels-last activation [M][hw][K] pooled first (its pooled rows -> xpool [M][K]).
+RK_API int rk_head_fwd(int dt, const void* x, const float* w, const float* b, float* y, int M, int N, int K, int hw,
+                       void* xpool, hipStream_t s) {
+  if (M <= 0 || N <= 0 || N > HNMAX || K <= 0 || hw <= 0 || (int64_t)M * hw * K >= ((int64_t)1 << 31))
+    return (int)hipErrorInvalidValue;
+  if (hw > 1 && xpool == nullptr) return (int)hipErrorInvalidValue;
   const int grid = M;
-  if (dt == BF16) head_fwd_kernel<BF16><<<grid, HT, 0, s>>>(x, w, b, y, M, N, K);
-  else if (dt == F16) head_fwd_kernel<F16><<<grid, HT, 0, s>>>(x, w, b, y, M, N, K);
-  else if (dt == F32) head_fwd_kernel<F32><<<grid, HT, 0, s>>>(x, w, b, y, M, N, K);
+  if (dt == BF16) head_fwd_kernel<BF16><<<grid, HT, 0, s>>>(x, w, b, y, M, N, K, hw, xpool);
+  else if (dt == F16) head_fwd_kernel<F16><<<grid, HT, 0, s>>>(x, w, b, y, M, N, K, hw, xpool);
+  else if (dt == F32) head_fwd_kernel<F32><<<grid, HT, 0, s>>>(x, w, b, y, M, N, K, hw, xpool);
   else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
@@ -233,9 +259,12 @@ RK_API int64_t rk_head_bwd_scratch(int M, int N, int K) {
   return mb * N * (int64_t)K + mb * N;
 }
 
+// hw > 1: x is the pooled input [M][K] (rk_head_fwd's xpool) and dx the channels-last activation
+// gradient [M][hw][K] (the pool's backward in the same launch).
 RK_API int rk_head_bwd(int dt, const float* dy, const void* x, const float* w, void* dx, float* dw, float* db,
-                       int acc_w, int acc_b, int M, int N, int K, float* part, unsigned* cnt, hipStream_t s) {
-  if (M <= 0 || N <= 0 || N > HNMAX || K <= 0 || (int64_t)M * K >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+                       int acc_w, int acc_b, int M, int N, int K, float* part, unsigned* cnt, int hw, hipStream_t s) {
+  if (M <= 0 || N <= 0 || N > HNMAX || K <= 0 || hw <= 0 || (int64_t)M * hw * K >= ((int64_t)1 << 31))
+    return (int)hipErrorInvalidValue;
   if (db != nullptr && dw == nullptr) return (int)hipErrorInvalidValue;  // db rides on the dW blocks
   if (dw != nullptr && (part == nullptr || cnt == nullptr)) return (int)hipErrorInvalidValue;
   const int kb = dw != nullptr ? (K + 63) / 64 : 0;
@@ -245,7 +274,7 @@ RK_API int rk_head_bwd(int dt, const float* dy, const void* x, const float* w, v
   const int wb = kb * mb;
   if (wb + xb == 0) return 0;
 #define RK_HB(D) head_bwd_kernel<D><<<wb + xb, BT, 0, s>>>(dy, x, w, dx, dw, db, acc_w, acc_b, M, N, K, wb ? kb : 1, \
-                                                         wb ? mb : 0, part, cnt)
+                                                         wb ? mb : 0, part, cnt, hw)
   if (dt == BF16) RK_HB(BF16);
   else if (dt == F16) RK_HB(F16);
   else if (dt == F32) RK_HB(F32);

@@ -71,8 +71,9 @@ KERNEL_SIGS = {
     "rk_conv_defer_reduce": (c_int, [c_int]),
     "rk_conv_flush_reduce": (c_int, [c_void_p]),
     "rk_conv_tail_counts": (c_int, [c_void_p]),
-    "rk_head_fwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
-    "rk_head_bwd": (c_int, [c_int] + [c_void_p] * 6 + [c_int] * 5 + [c_void_p] * 3),
+    "rk_head_fwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                            c_void_p]),
+    "rk_head_bwd": (c_int, [c_int] + [c_void_p] * 6 + [c_int] * 5 + [c_void_p] * 2 + [c_int, c_void_p]),
     "rk_head_bwd_scratch": (c_int64, [c_int, c_int, c_int]),
     "rk_conv_pool_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 7 + [c_void_p]),
     "rk_conv_pool_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),

@@ -468,10 +468,12 @@ class _HeadFn(torch.autograd.Function):
         M = x2.shape[0]
         y = torch.empty(M, N, dtype=torch.float32, device=x.device)
         _lib.check(_lib.kernels().rk_head_fwd(_HEAD_DT[x2.dtype], x2.data_ptr(), weight.data_ptr(), _lib.ptr(bias),
-                                              y.data_ptr(), M, N, K, _lib.stream_ptr(x.device)), "rk_head_fwd")
+                                              y.data_ptr(), M, N, K, 1, None, _lib.stream_ptr(x.device)),
+                   "rk_head_fwd")
         ctx.save_for_backward(x2, weight)
         ctx.bias = bias
         ctx.xshape = x.shape
+        ctx.hw = 1
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
@@ -486,7 +488,12 @@ class _HeadFn(torch.autograd.Function):
         need_x, need_w, need_b = ctx.needs_input_grad
         need_b = need_b and bias is not None
         dev = x2.device
-        dx = torch.empty_like(x2) if need_x else None
+        hw = ctx.hw
+        if need_x:
+            dx = torch.empty_like(x2) if hw == 1 else torch.empty(ctx.xshape, dtype=x2.dtype, device=x2.device,
+                                                                   memory_format=torch.channels_last)
+        else:
+            dx = None
         direct_w = need_w and _direct(weight) and weight.grad.is_contiguous()
         direct_b = need_b and _direct(bias)
         dw = weight.grad if direct_w else (torch.empty(N, K, dtype=torch.float32, device=dev)
@@ -500,13 +507,46 @@ class _HeadFn(torch.autograd.Function):
             cnt = _lib.Workspace.get(dev).counter_array(f"head{kb}", kb)
         _lib.check(lib.rk_head_bwd(_HEAD_DT[x2.dtype], dy2.data_ptr(), x2.data_ptr(), weight.data_ptr(),
                                    _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(db), int(direct_w), int(direct_b),
-                                   M, N, K, _lib.ptr(part), cnt, _lib.stream_ptr(dev)), "rk_head_bwd")
+                                   M, N, K, _lib.ptr(part), cnt, hw, _lib.stream_ptr(dev)), "rk_head_bwd")
         if direct_w:
             grad_ready(weight)
         if direct_b:
             grad_ready(bias)
-        return (dx.view(ctx.xshape) if need_x else None, dw if need_w and not direct_w else None,
+        return (dx.view(ctx.xshape) if need_x and hw == 1 else dx, dw if need_w and not direct_w else None,
                 db if need_b and not direct_b else None)
+
+
+class _PooledHeadFn(_HeadFn):
+    """``head(global_avg_pool(x))`` for a channels-last ``[N, C, H, W]`` activation: the pool runs
+    inside the head's forward launch (pooled rows kept for the weight gradient) and its backward
+    (the ``dy / HW`` broadcast) inside the head's backward launch — two launches fewer than
+    ``ops.pool.global_avg_pool`` + :class:`_HeadFn`, same rounding."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        N, C, H, W = x.shape
+        Nc, K = weight.shape
+        xpool = torch.empty(N, C, dtype=x.dtype, device=x.device)
+        y = torch.empty(N, Nc, dtype=torch.float32, device=x.device)
+        _lib.check(_lib.kernels().rk_head_fwd(_HEAD_DT[x.dtype], x.data_ptr(), weight.data_ptr(), _lib.ptr(bias),
+                                              y.data_ptr(), N, Nc, K, H * W, xpool.data_ptr(),
+                                              _lib.stream_ptr(x.device)), "rk_head_fwd(pooled)")
+        ctx.save_for_backward(xpool, weight)
+        ctx.bias = bias
+        ctx.xshape = x.shape
+        ctx.hw = H * W
+        return y
+
+
+def pooled_head_ok(module: nn.Module, x: torch.Tensor) -> bool:
+    """Whether ``module(global_avg_pool(x))`` can run as :class:`_PooledHeadFn`."""
+    return (isinstance(module, MLinear) and x.dim() == 4 and x.shape[1] == module.in_features
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[2] * x.shape[3] > 1
+            and _head_ok(module, x.new_empty(0, module.in_features)))
+
+
+def pooled_head(module: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    return _PooledHeadFn.apply(x, module.weight, module.bias)
 
 
 class MLinear(nn.Linear):

@@ -438,3 +438,32 @@ def test_head_kernels_vs_fp32(M, N, K, dtype):
     assert (x.grad.float() - xr.grad).abs().max().item() <= tol * xr.grad.abs().max().item()
     assert (m.weight.grad - wr.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item()
     assert (m.bias.grad - br.grad).abs().max().item() <= 1e-4 * br.grad.abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_pooled_head_matches_pool_then_head(dtype):
+    """The global average pool fused into the head's launches (_PooledHeadFn) gives the outputs and
+    gradients of ops.pool.global_avg_pool followed by the head kernels (same rounding points)."""
+    from rocket_amd.ops import mlinear
+    from rocket_amd.ops.pool import global_avg_pool
+
+    torch.manual_seed(2)
+    m = mlinear.MLinear(512, 10).cuda()
+    x0 = torch.randn(64, 512, 4, 4, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for fused in (True, False):
+        m.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=dtype):
+            assert mlinear.pooled_head_ok(m, x)
+            y = mlinear.pooled_head(m, x) if fused else m(global_avg_pool(x))
+        torch.manual_seed(3)
+        g = torch.randn_like(y)
+        y.backward(g)
+        outs.append((y.detach(), x.grad.float(), m.weight.grad.clone(), m.bias.grad.clone()))
+    (y1, dx1, w1, b1), (y2, dx2, w2, b2) = outs
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
+    assert torch.allclose(y1, y2, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(dx1, dx2, rtol=1e-2, atol=1e-6)
+    assert torch.allclose(w1, w2, rtol=1e-4, atol=1e-6) and torch.allclose(b1, b2, rtol=1e-5, atol=1e-6)
