@@ -42,6 +42,13 @@ __device__ __forceinline__ void stx(void* p, int64_t i, float v) {
   else ((uint16_t*)p)[i] = f2bf(v);
 }
 
+template <int DT>
+__device__ __forceinline__ float rnd(float v) {  // the value a DT store then load would give
+  if constexpr (DT == F32) return v;
+  else if constexpr (DT == F16) return h2f(f2h(v));
+  else return bf2f(f2bf(v));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -74,13 +81,18 @@ __global__ void __launch_bounds__(HT) head_fwd_kernel(const void* __restrict__ x
           xv[u] = k < K ? ldx<DT>(x, (int64_t)m * K + k) : 0.f;
         } else {
           float sum = 0.f;
+          if (hw <= 16) {  // ResNet's 4x4 / 7x7-class heads: every pixel load of the round in flight
+            float pv[16];
+#pragma unroll
+            for (int p = 0; p < 16; ++p) pv[p] = (p < hw && k < K) ? ldx<DT>(x, ((int64_t)m * hw + p) * K + k) : 0.f;
+#pragma unroll
+            for (int p = 0; p < 16; ++p) sum += pv[p];
+          } else {
 #pragma unroll 8
-          for (int p = 0; p < hw; ++p) sum += k < K ? ldx<DT>(x, ((int64_t)m * hw + p) * K + k) : 0.f;
-          xv[u] = 0.f;
-          if (k < K) {
-            stx<DT>(xpool, (int64_t)m * K + k, sum * inv_hw);  // the pooled row, as rk_gap_fwd stores it
-            xv[u] = ldx<DT>(xpool, (int64_t)m * K + k);         // (rounded: the value the head consumes)
+            for (int p = 0; p < hw; ++p) sum += k < K ? ldx<DT>(x, ((int64_t)m * hw + p) * K + k) : 0.f;
           }
+          xv[u] = rnd<DT>(sum * inv_hw);  // the pooled row as rk_gap_fwd stores it: the value the head consumes
+          if (k < K) stx<DT>(xpool, (int64_t)m * K + k, xv[u]);
         }
 #pragma unroll
         for (int j = 0; j < HNC; ++j) wr[u][j] = (k < K && n0 + j < N) ? w[(int64_t)(n0 + j) * K + k] : 0.f;
@@ -229,8 +241,7 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
   }
   // pooled head: the input gradient of the average pool, dy / hw broadcast over the row's pixels of
   // the channels-last activation (the pooled gradient rounded first, as rk_gap_bwd reads it)
-  stx<DT>(dx, ((int64_t)m * hw) * K + k, s);
-  const float g = ldx<DT>(dx, ((int64_t)m * hw) * K + k) * (1.f / (float)hw);
+  const float g = rnd<DT>(s) * (1.f / (float)hw);
   for (int p = 0; p < hw; ++p) stx<DT>(dx, ((int64_t)m * hw + p) * K + k, g);
 }
 
