@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(BT) head_bwd_kernel(const float* __restrict__ 
       }
 #pragma unroll
       for (int j = 0; j < HNC; ++j) acc[j] = accb[j] = 0.f;
-#pragma unroll
+#pragma unroll 2
       for (int t = 0; t < SR / BW; ++t)
 #pragma unroll
         for (int j = 0; j < HNC; ++j) {
